@@ -1,0 +1,161 @@
+"""TEST INFRASTRUCTURE -- ctypes binding of the C oracle (oracle/liborc.so).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline may import
+this module; the product (dqn-marl_amd/) never does. See evac_oracle.h.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liborc.so")
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        _lib = C.CDLL(LIB_PATH)
+        _lib.orc_mt_next.restype = C.c_uint32
+        _lib.orc_mt_random.restype = C.c_double
+        _lib.orc_mt_randbelow.restype = C.c_uint32
+        _lib.orc_pairwise_sum.restype = C.c_double
+        _lib.orc_pairwise_sum.argtypes = [C.c_void_p, C.c_long]
+        _lib.orc_run_batch.restype = C.c_long
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+class OrcLayout(C.Structure):
+    _fields_ = [("L", C.c_int), ("W", C.c_int), ("P", C.c_int), ("R", C.c_int), ("t_max", C.c_int),
+                ("floor", C.c_void_p), ("valid", C.c_void_p), ("exitm", C.c_void_p),
+                ("barrier", C.c_void_p), ("danger_p", C.c_void_p), ("danger_o", C.c_void_p),
+                ("ox0", C.c_int), ("oy0", C.c_int), ("OX", C.c_int), ("OY", C.c_int),
+                ("exit_x", C.c_int), ("exit_y", C.c_int), ("rx_lo", C.c_int), ("rx_hi", C.c_int),
+                ("reset_view_x", C.c_int), ("reset_view_y", C.c_int), ("reset_robots", C.c_int),
+                ("robot_init", C.c_void_p), ("repel_k", C.c_double), ("repel_range", C.c_double),
+                ("evac_reward", C.c_double), ("death_penalty", C.c_double),
+                ("death_acc_penalty", C.c_double), ("alive_bonus", C.c_double)]
+
+
+class OrcEnv(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ["pos", "health", "acc", "flags", "rmap", "thmap", "robots",
+                                         "view", "scal", "time", "py_mt", "np_mt"]]
+
+
+REWARD_DEFAULTS = dict(evac_reward=50.0, death_penalty=200.0, death_acc_penalty=0.5, alive_bonus=1.0)
+
+
+class Layout:
+    """Oracle view of one layout: tables + geometry (all arrays kept alive here)."""
+
+    def __init__(self, *, L, W, P, R, floor, valid, exit_mask, barrier, danger_p, danger_o,
+                 obs_origin, exit, robot_range, reset_view, reset_robots, robot_init,
+                 repel_k=-20.0, repel_range=5.0, **reward):
+        rw = dict(REWARD_DEFAULTS, **reward)
+        self.arrs = dict(
+            floor=np.ascontiguousarray(floor, np.float64), valid=np.ascontiguousarray(valid, np.uint8),
+            exitm=np.ascontiguousarray(exit_mask, np.uint8), barrier=np.ascontiguousarray(barrier, np.uint8),
+            danger_p=np.ascontiguousarray(danger_p, np.float64),
+            danger_o=np.ascontiguousarray(danger_o, np.float64),
+            robot_init=np.ascontiguousarray(np.asarray(robot_init, np.int32).reshape(-1, 2)))
+        self.L, self.W, self.P, self.R = int(L), int(W), int(P), int(R)
+        self.GX, self.GY = self.L + 2, self.W + 2
+        dpo = self.arrs["danger_o"]
+        self.c = OrcLayout(L=self.L, W=self.W, P=self.P, R=self.R, t_max=dpo.shape[0] - 1,
+                           ox0=int(obs_origin[0]), oy0=int(obs_origin[1]), OX=dpo.shape[1], OY=dpo.shape[2],
+                           exit_x=int(exit[0]), exit_y=int(exit[1]), rx_lo=int(robot_range[0]),
+                           rx_hi=int(robot_range[1]), reset_view_x=int(reset_view[0]),
+                           reset_view_y=int(reset_view[1]), reset_robots=int(bool(reset_robots)),
+                           repel_k=repel_k, repel_range=repel_range, **rw)
+        for k, a in self.arrs.items():
+            setattr(self.c, k, a.ctypes.data)
+        assert self.arrs["danger_p"].shape[0] == dpo.shape[0]
+
+    @classmethod
+    def from_tables(cls, tables, P, **kw):
+        s = tables.spec
+        return cls(L=s.L, W=s.W, P=P, R=s.R, floor=tables.floor, valid=tables.valid,
+                   exit_mask=tables.exit_mask, barrier=tables.barrier, danger_p=tables.danger_p,
+                   danger_o=tables.danger_o, obs_origin=tables.obs_origin, exit=s.exit,
+                   robot_range=s.robot_range, reset_view=s.reset_view, reset_robots=s.reset_robots,
+                   robot_init=s.robot_init, **kw)
+
+
+class Env:
+    """One oracle env instance: state arrays + the two MT19937 streams."""
+
+    def __init__(self, layout: Layout, thmap=True):
+        self.lay = layout
+        P, R, G = layout.P, layout.R, layout.GX * layout.GY
+        self.pos = np.zeros((P, 2), np.int32)
+        self.health = np.zeros(P, np.float64)
+        self.acc = np.zeros(P, np.float64)
+        self.flags = np.zeros(P, np.uint8)
+        self.rmap = np.zeros((layout.GX, layout.GY), np.uint8)
+        self.thmap = np.zeros((layout.GX, layout.GY), np.int32) if thmap else None
+        self.robots = np.array(layout.arrs["robot_init"], np.int32).copy()
+        self.view = np.array([layout.c.reset_view_x, layout.c.reset_view_y], np.int32)
+        self.scal = np.zeros(4, np.int32)
+        self.time = np.zeros(1, np.float64)
+        self.py_mt = np.zeros(625, np.uint32)
+        self.np_mt = np.zeros(625, np.uint32)
+        self.c = OrcEnv(**{k: _p(getattr(self, k)) for k in
+                           ["pos", "health", "acc", "flags", "rmap", "thmap", "robots", "view", "scal",
+                            "time", "py_mt", "np_mt"]})
+
+    @property
+    def fire_step(self):
+        return int(self.scal[0])
+
+    def seed(self, seed):
+        lib().orc_seed_py(C.c_uint32(seed), _p(self.py_mt))
+        lib().orc_seed_np(C.c_uint32(seed), _p(self.np_mt))
+
+    def reset(self):
+        obs = np.zeros((self.lay.R, 11, 11, 6), np.float64)
+        lib().orc_env_reset(C.byref(self.lay.c), C.byref(self.c), _p(obs))
+        return obs
+
+    def step(self, actions):
+        a = np.ascontiguousarray(np.asarray(actions, np.int32).reshape(self.lay.R))
+        obs = np.zeros((self.lay.R, 11, 11, 6), np.float64)
+        r = np.zeros(1, np.float64)
+        d = np.zeros(1, np.int32)
+        lib().orc_env_step(C.byref(self.lay.c), C.byref(self.c), _p(a), _p(r), _p(d), _p(obs))
+        return obs, float(r[0]), bool(d[0])
+
+    def state(self):
+        return dict(pos=self.pos.copy(), health=self.health.copy(), acc=self.acc.copy(),
+                    flags=self.flags.copy(), rmap=self.rmap.copy(),
+                    thmap=None if self.thmap is None else self.thmap.copy(),
+                    robots=self.robots.copy(), view=self.view.copy(), scal=self.scal.copy(),
+                    time=float(self.time[0]), py_mt=self.py_mt.copy(), np_mt=self.np_mt.copy())
+
+
+def run_batch(layout: Layout, envs, steps, actions, nthreads=0):
+    """CPU baseline: step all envs `steps` times (OpenMP over envs); returns env-steps."""
+    arr = (OrcEnv * len(envs))(*[e.c for e in envs])
+    a = np.ascontiguousarray(actions, np.int32)
+    assert a.size == steps * len(envs) * layout.R
+    rs = np.zeros(len(envs), np.float64)
+    n = lib().orc_run_batch(C.byref(layout.c), arr, C.c_int(len(envs)), C.c_int(steps), _p(a), _p(rs),
+                            C.c_int(nthreads))
+    return int(n), rs
+
+
+def pairwise_sum(a):
+    a = np.ascontiguousarray(a, np.float64)
+    return lib().orc_pairwise_sum(_p(a), len(a))
