@@ -1,0 +1,72 @@
+"""ctypes binding of libevacx.so (include/evacx.h).
+
+The library is built in-tree by ``make -C dqn-marl_amd/csrc`` (or
+``__graft_entry__.build()``). There is no fallback: if it is missing or a call
+fails, an ``EvacxError`` is raised.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libevacx.so")
+
+
+class EvacxError(RuntimeError):
+    pass
+
+
+class evx_layout(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ["L", "W", "P", "R", "t_max", "ox0", "oy0", "OX", "OY", "exit_x",
+                                        "exit_y", "rx_lo", "rx_hi", "reset_view_x", "reset_view_y",
+                                        "reset_robots", "flags", "repel_d2", "pad0"]] + \
+               [(n, C.c_double) for n in ["repel_k", "repel_range", "evac_reward", "death_penalty",
+                                         "death_acc_penalty", "alive_bonus"]] + \
+               [(n, C.c_void_p) for n in ["floor", "cellinfo", "valid_bits", "danger_p", "danger_o",
+                                         "danger_o32", "robot_init"]]
+
+
+class evx_state(C.Structure):
+    _fields_ = [("E", C.c_int32)] + [(n, C.c_void_p) for n in
+                                     ["pk", "health", "acc", "rmap", "thmap", "robots", "view", "scal",
+                                      "py_mt", "np_mt"]]
+
+
+class evx_step_out(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ["reward", "done", "counts", "obs", "err"]]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise EvacxError(f"{LIB_PATH} not built: run `make -C dqn-marl_amd/csrc` (or __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        L.evx_last_error.restype = C.c_char_p
+        L.evx_step_lds_bytes.restype = C.c_int64
+        for name in ["evx_env_step", "evx_env_reset", "evx_obs_expand_f32", "evx_obs_expand_f64",
+                     "evx_seed_host"]:
+            getattr(L, name).restype = C.c_int
+        L.evx_env_step.argtypes = [C.POINTER(evx_layout), C.POINTER(evx_state), C.c_void_p,
+                                   C.POINTER(evx_step_out), C.c_void_p]
+        L.evx_env_reset.argtypes = [C.POINTER(evx_layout), C.POINTER(evx_state), C.c_void_p, C.c_void_p,
+                                    C.c_void_p, C.c_void_p]
+        L.evx_obs_expand_f32.argtypes = [C.POINTER(evx_layout), C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p]
+        L.evx_obs_expand_f64.argtypes = [C.POINTER(evx_layout), C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p]
+        L.evx_seed_host.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        raise EvacxError(f"{what} failed ({rc}): {lib().evx_last_error().decode()}")
+
+
+# every C symbol include/evacx.h declares (checked by tests/test_abi.py)
+EXPORTS = ["evx_env_step", "evx_env_reset", "evx_obs_expand_f32", "evx_obs_expand_f64", "evx_seed_host",
+           "evx_step_lds_bytes", "evx_last_error"]

@@ -1,0 +1,212 @@
+"""Device-resident vectorised evacuation environments (host driver of libevacx).
+
+``DeviceLayout`` uploads the static tables of one layout (evacx.layout) to HBM
+once; ``VecEnv`` holds E env instances as one structure-of-arrays state in HBM
+and steps all of them with one kernel launch (include/evacx.h). Nothing here
+computes the environment: it allocates, packs and launches.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from .layout import LayoutSpec, LayoutTables, build_tables
+
+REWARD_DEFAULTS = dict(evac_reward=50.0, death_penalty=200.0, death_acc_penalty=0.5, alive_bonus=1.0)
+OBS_WORDS = 8  # sizeof(evx_obs) / 4
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def pack_xy(x, y) -> np.ndarray:
+    x = np.asarray(x, np.int64) & 0xFFFF
+    y = np.asarray(y, np.int64) & 0xFFFF
+    return (x | (y << 16)).astype(np.uint32).view(np.int32)
+
+
+def unpack_xy(v) -> np.ndarray:
+    u = np.asarray(v).view(np.uint32).astype(np.int64)
+    x = (u & 0xFFFF).astype(np.int16).astype(np.int32)
+    y = (u >> 16).astype(np.int16).astype(np.int32)
+    return np.stack([x, y], -1)
+
+
+def repel_threshold(repel_range: float) -> int:
+    """Smallest integer n with sqrt(n) >= repel_range (so dist < range <=> d2 < n)."""
+    if not repel_range > 0:
+        return 0
+    n = max(0, int(math.ceil(repel_range * repel_range)) - 2)
+    while math.sqrt(n) < repel_range:
+        n += 1
+    return n
+
+
+class DeviceLayout:
+    """Static tables of one layout in HBM + the evx_layout descriptor."""
+
+    def __init__(self, tables: LayoutTables, P: int, device="cuda", repel_k=-20.0, repel_range=5.0,
+                 **reward):
+        spec = tables.spec
+        self.spec, self.tables, self.P, self.R = spec, tables, int(P), spec.R
+        self.device = torch.device(device)
+        self.GX, self.GY = spec.L + 2, spec.W + 2
+        self.G = self.GX * self.GY
+        self.RW = (self.G + 31) // 32
+        d = self.device
+        cell = (tables.valid.astype(np.uint8) | (tables.exit_mask.astype(np.uint8) << 1)
+                | (tables.barrier.astype(np.uint8) << 2)).reshape(-1)
+        vb = np.zeros(self.RW * 32, np.uint8)
+        vb[:self.G] = tables.valid.reshape(-1)
+        bits = np.packbits(vb.reshape(-1, 32)[:, ::-1], axis=1).view(">u4").astype(np.uint32).reshape(-1)
+        self.t = dict(
+            floor=torch.from_numpy(np.ascontiguousarray(tables.floor.reshape(-1))).to(d),
+            cellinfo=torch.from_numpy(cell).to(d),
+            valid_bits=torch.from_numpy(bits.view(np.int32)).to(d),
+            danger_p=torch.from_numpy(np.ascontiguousarray(tables.danger_p.reshape(-1))).to(d),
+            danger_o=torch.from_numpy(np.ascontiguousarray(tables.danger_o.reshape(-1))).to(d),
+            robot_init=torch.from_numpy(np.asarray(spec.robot_init, np.int32).reshape(-1)).to(d),
+        )
+        self.t["danger_o32"] = self.t["danger_o"].to(torch.float32)
+        T = tables.danger_p.shape[0] - 1
+        OX, OY = tables.danger_o.shape[1:]
+        self.c = _lib.evx_layout(
+            L=spec.L, W=spec.W, P=self.P, R=self.R, t_max=T, ox0=tables.obs_origin[0], oy0=tables.obs_origin[1],
+            OX=OX, OY=OY, exit_x=spec.exit[0], exit_y=spec.exit[1], rx_lo=spec.robot_range[0],
+            rx_hi=spec.robot_range[1], reset_view_x=spec.reset_view[0], reset_view_y=spec.reset_view[1],
+            reset_robots=int(bool(spec.reset_robots)), flags=0)
+        for k, v in self.t.items():
+            setattr(self.c, k, v.data_ptr())
+        self.set_params(repel_k=repel_k, repel_range=repel_range, **dict(REWARD_DEFAULTS, **reward))
+
+    def set_params(self, **kw):
+        """Runtime-mutable coefficients (the reference's class attributes)."""
+        for k, v in kw.items():
+            if k == "repel_range":
+                self.c.repel_range = float(v)
+                self.c.repel_d2 = repel_threshold(float(v))
+            else:
+                setattr(self.c, k, float(v))
+
+    @classmethod
+    def from_spec(cls, spec: LayoutSpec, P: int, device="cuda", **kw):
+        return cls(build_tables(spec), P, device, **kw)
+
+
+class VecEnv:
+    """E env instances of one layout, state resident in HBM (SoA, env-major)."""
+
+    def __init__(self, layout: DeviceLayout, E: int, thmap: bool = False):
+        self.lay = layout
+        self.E = int(E)
+        P, R, d = layout.P, layout.R, layout.device
+        i32 = dict(dtype=torch.int32, device=d)
+        f64 = dict(dtype=torch.float64, device=d)
+        self.pk = torch.zeros(E * P, **i32)
+        self.health = torch.zeros(E * P, **f64)
+        self.acc = torch.zeros(E * P, **f64)
+        self.rmap = torch.zeros(E * layout.RW, **i32)
+        self.thmap = torch.zeros(E * layout.G, **i32) if thmap else None
+        spec = layout.spec
+        ri = pack_xy([p[0] for p in spec.robot_init], [p[1] for p in spec.robot_init])
+        self.robots = torch.from_numpy(np.tile(ri, E)).to(d)
+        v0 = pack_xy(*spec.reset_view)
+        self.view = torch.full((E,), int(v0), **i32)
+        self.scal = torch.zeros(E * 4, **i32)
+        self.py_mt = torch.zeros(E * 625, **i32)
+        self.np_mt = torch.zeros(E * 625, **i32)
+        # outputs
+        self.reward = torch.zeros(E, **f64)
+        self.done = torch.zeros(E, dtype=torch.uint8, device=d)
+        self.counts = torch.zeros(E * 2, **i32)
+        self.obs = torch.zeros(E * R * OBS_WORDS, **i32)
+        self.err = torch.zeros(1, **i32)
+        self.c = _lib.evx_state(E=E, pk=_ptr(self.pk), health=_ptr(self.health), acc=_ptr(self.acc),
+                                rmap=_ptr(self.rmap), thmap=_ptr(self.thmap), robots=_ptr(self.robots),
+                                view=_ptr(self.view), scal=_ptr(self.scal), py_mt=_ptr(self.py_mt),
+                                np_mt=_ptr(self.np_mt))
+        self.out = _lib.evx_step_out(reward=_ptr(self.reward), done=_ptr(self.done), counts=_ptr(self.counts),
+                                     obs=_ptr(self.obs), err=_ptr(self.err))
+
+    # -------------------------------------------------------------- seeding
+    def seed(self, seeds: Sequence[int]):
+        """random.seed(s) / numpy.random.seed(s) per env (host MT19937 init)."""
+        s = np.ascontiguousarray(np.asarray(seeds, np.int64) % (1 << 32), np.uint32)
+        assert s.shape == (self.E,)
+        py = np.zeros((self.E, 625), np.uint32)
+        nps = np.zeros((self.E, 625), np.uint32)
+        _lib.check(_lib.lib().evx_seed_host(s.ctypes.data, self.E, py.ctypes.data, nps.ctypes.data), "seed")
+        self.set_rng(py, nps)
+
+    def set_rng(self, py_states: np.ndarray, np_states: np.ndarray, env_ids=None):
+        py = torch.from_numpy(np.ascontiguousarray(py_states, np.uint32).view(np.int32).reshape(-1, 625))
+        nps = torch.from_numpy(np.ascontiguousarray(np_states, np.uint32).view(np.int32).reshape(-1, 625))
+        if env_ids is None:
+            self.py_mt.copy_(py.reshape(-1))
+            self.np_mt.copy_(nps.reshape(-1))
+        else:
+            self.py_mt.view(self.E, 625)[env_ids] = py.to(self.py_mt.device)
+            self.np_mt.view(self.E, 625)[env_ids] = nps.to(self.np_mt.device)
+
+    def get_rng(self):
+        return (self.py_mt.view(self.E, 625).cpu().numpy().view(np.uint32),
+                self.np_mt.view(self.E, 625).cpu().numpy().view(np.uint32))
+
+    # ---------------------------------------------------------------- steps
+    def reset(self, mask: Optional[torch.Tensor] = None):
+        m = None if mask is None else mask.to(torch.uint8).contiguous()
+        _lib.check(_lib.lib().evx_env_reset(C.byref(self.lay.c), C.byref(self.c), _ptr(m), _ptr(self.obs),
+                                            _ptr(self.err), _stream()), "evx_env_reset")
+
+    def step(self, actions: torch.Tensor):
+        a = actions.to(torch.int32).contiguous()
+        assert a.numel() == self.E * self.lay.R
+        _lib.check(_lib.lib().evx_env_step(C.byref(self.lay.c), C.byref(self.c), a.data_ptr(), C.byref(self.out),
+                                           _stream()), "evx_env_step")
+
+    def expand_obs(self, dtype=torch.float32, obs: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Reference-layout observation tensor [E, R, 11, 11, 6]."""
+        ob = self.obs if obs is None else obs
+        n = ob.numel() // OBS_WORDS
+        out = torch.empty((n, 11, 11, 6), dtype=dtype, device=ob.device)
+        fn = _lib.lib().evx_obs_expand_f32 if dtype == torch.float32 else _lib.lib().evx_obs_expand_f64
+        assert dtype in (torch.float32, torch.float64)
+        _lib.check(fn(C.byref(self.lay.c), ob.data_ptr(), n, out.data_ptr(), _stream()), "evx_obs_expand")
+        return out.view(-1, self.lay.R, 11, 11, 6)
+
+    def check_err(self):
+        v = int(self.err.item())
+        if v:
+            raise _lib.EvacxError(f"device error word {v}")
+
+    # ----------------------------------------------------- host inspection
+    def host_state(self, e: int) -> dict:
+        """One env's state in the oracle's representation (tests / drop-in)."""
+        lay = self.lay
+        P, R = lay.P, lay.R
+        pk = self.pk.view(self.E, P)[e].cpu().numpy().view(np.uint32)
+        pos = np.stack([pk & 0xFFF, (pk >> 12) & 0xFFF], -1).astype(np.int32)
+        flags = ((pk >> 24) & 3).astype(np.uint8)
+        bits = self.rmap.view(self.E, lay.RW)[e].cpu().numpy().view(np.uint32)
+        rm = ((bits[:, None] >> np.arange(32, dtype=np.uint32)[None, :]) & 1).astype(np.uint8).reshape(-1)
+        out = dict(pos=pos, flags=flags,
+                   health=self.health.view(self.E, P)[e].cpu().numpy(),
+                   acc=self.acc.view(self.E, P)[e].cpu().numpy(),
+                   rmap=rm[:lay.G].reshape(lay.GX, lay.GY),
+                   robots=unpack_xy(self.robots.view(self.E, R)[e].cpu().numpy()),
+                   view=unpack_xy(self.view[e:e + 1].cpu().numpy())[0],
+                   scal=self.scal.view(self.E, 4)[e].cpu().numpy(),
+                   py_mt=self.py_mt.view(self.E, 625)[e].cpu().numpy().view(np.uint32),
+                   np_mt=self.np_mt.view(self.E, 625)[e].cpu().numpy().view(np.uint32))
+        out["thmap"] = None if self.thmap is None else self.thmap.view(self.E, lay.GX, lay.GY)[e].cpu().numpy()
+        return out

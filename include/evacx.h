@@ -1,0 +1,117 @@
+/* evacx -- C-ABI of the MI355X-native evacuation CA + DQN hot path (libevacx.so).
+ *
+ * The reference (LX-530/DQN-MARL, Louvre_Evacuation/) has no FFI: its boundary
+ * is the duck-typed Python API its runners call. Each entry point below names
+ * the reference function it replaces (paths relative to
+ * /root/reference/Louvre_Evacuation/); the Python mirror in
+ * dqn-marl_amd/Louvre_Evacuation binds them through ctypes.
+ *
+ * Conventions
+ *  - every call returns 0 or a negative errno-like code; evx_last_error() has text;
+ *  - every buffer is caller-owned DEVICE memory unless the name says _host;
+ *  - no hidden allocations, no internal threads, no host syncs; `stream` is a
+ *    hipStream_t passed as void* (0 = the null stream);
+ *  - plain pointers and sizes only (no torch types).
+ */
+#ifndef EVACX_H
+#define EVACX_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EVX_MT_WORDS 625 /* 624 MT19937 words + index, CPython/numpy layout */
+#define EVX_OBS_CELLS 121
+#define EVX_OBS_CH 6
+
+/* Static, read-only description of one layout (device tables built on the host
+ * by evacx/layout.py: Map.__init__ + Init_Potential envs/map.py:38-148,
+ * ProgressiveFireModel envs/fire_model.py:4-199). */
+typedef struct {
+    int32_t L, W;             /* interior; padded grid (L+2)x(W+2), cell = x*(W+2)+y */
+    int32_t P, R;             /* people per env, robots per env */
+    int32_t t_max;            /* fire max_steps (tables hold t = 0..t_max) */
+    int32_t ox0, oy0, OX, OY; /* danger_o window origin / size */
+    int32_t exit_x, exit_y;   /* EvacuationEnv.exit_location */
+    int32_t rx_lo, rx_hi;     /* Map.robot_range (envs/map.py:75) */
+    int32_t reset_view_x, reset_view_y; /* Map.robot_position set by reset (envs/evacuation_env.py:64) */
+    int32_t reset_robots;     /* 1 = EvacuationEnvMulti.reset re-places robots */
+    int32_t flags;            /* EVX_LAYOUT_* */
+    int32_t repel_d2;         /* smallest integer n with sqrt(n) >= repel_range (host-computed) */
+    int32_t pad0;
+    double repel_k, repel_range;  /* People.ROBOT_REPEL_K / _RANGE (envs/people.py:94-95) */
+    double evac_reward, death_penalty, death_acc_penalty, alive_bonus; /* envs/evacuation_env.py:16-19 */
+    const double *floor;      /* [G] floor field */
+    const uint8_t *cellinfo;  /* [G] bit0 valid, bit1 exit (checkSavefy), bit2 barrier_list */
+    const uint32_t *valid_bits; /* [ceil(G/32)] bit0 of cellinfo as a bitmap */
+    const double *danger_p;   /* [(t_max+1)*G] danger at person positions (x+.5,y+.5) */
+    const double *danger_o;   /* [(t_max+1)*OX*OY] danger at integer obs coordinates */
+    const float *danger_o32;  /* same, float32 (network input path) */
+    const int32_t *robot_init;/* [R*2] robot positions after a multi-robot reset */
+} evx_layout;
+
+/* Structure-of-arrays state of E env instances (env-major). */
+typedef struct {
+    int32_t E;
+    uint32_t *pk;      /* [E*P] person: x | y<<12 | safe<<24 | dead<<25 */
+    double *health;    /* [E*P] Person.health */
+    double *acc;       /* [E*P] Person.move_accumulator */
+    uint32_t *rmap;    /* [E*ceil(G/32)] People.rmap as a bitmap */
+    int32_t *thmap;    /* [E*G] People.thmap, or NULL (diagnostic heat map) */
+    uint32_t *robots;  /* [E*R] Map.robot_positions: (uint16)x | (uint16)y<<16 */
+    uint32_t *view;    /* [E]   Map.robot_position (same packing) */
+    int32_t *scal;     /* [E*4] fire_step, current_step, prev_evacuated, prev_dead */
+    uint32_t *py_mt;   /* [E*625] CPython `random` MT19937 state per env */
+    uint32_t *np_mt;   /* [E*625] legacy numpy.random MT19937 state per env */
+} evx_state;
+
+/* Compact per-robot observation (32 B). Expands to the reference's 11x11x6
+ * _get_state tensor (envs/evacuation_env.py:84-120) given the layout. */
+typedef struct {
+    uint32_t occ[4];   /* bit c (c = i*11+j): People.rmap at (cx+i-5, cy+j-5) if valid */
+    int32_t cx, cy;    /* window centre */
+    int32_t fire_step; /* env fire model step the obs was taken at */
+    int32_t pad;
+} evx_obs;
+
+/* Per-step outputs. */
+typedef struct {
+    double *reward;    /* [E] EvacuationEnv._calculate_reward (envs/evacuation_env.py:174-288) */
+    uint8_t *done;     /* [E] */
+    int32_t *counts;   /* [E*2] evacuated, dead after the step (may be NULL) */
+    evx_obs *obs;      /* [E*R] observation after the step */
+    int32_t *err;      /* [1] sticky device error word (may be NULL) */
+} evx_step_out;
+
+/* Replaces EvacuationEnv.step / EvacuationEnvMulti.step (envs/evacuation_env.py:122-172,
+ * envs/evacuation_env_multi.py:55-89): robot moves (Map.move_robot envs/map.py:160-201),
+ * People.run (envs/people.py:196-314), fire update, reward, counters, observation.
+ * actions: [E*R] int32; values outside 0..4 are ignored as in the reference. */
+int evx_env_step(const evx_layout *lay, const evx_state *st, const int32_t *actions,
+                 const evx_step_out *out, void *stream);
+
+/* Replaces EvacuationEnv.reset / EvacuationEnvMulti.reset (envs/evacuation_env.py:61-82,
+ * envs/evacuation_env_multi.py:31-42) incl. People placement (envs/people.py:183-194).
+ * mask: [E] uint8 (NULL = all envs); obs receives the reset observation of masked envs. */
+int evx_env_reset(const evx_layout *lay, const evx_state *st, const uint8_t *mask, evx_obs *obs,
+                  int32_t *err, void *stream);
+
+/* Expands n compact observations to the reference tensor layout [n][11][11][6]. */
+int evx_obs_expand_f32(const evx_layout *lay, const evx_obs *obs, int64_t n, float *out, void *stream);
+int evx_obs_expand_f64(const evx_layout *lay, const evx_obs *obs, int64_t n, double *out, void *stream);
+
+/* Host helper: MT19937 states for integer seeds as random.seed(s) (init_by_array)
+ * and numpy.random.seed(s) (init_genrand) produce them. Host pointers. */
+int evx_seed_host(const uint32_t *seeds_host, int32_t n, uint32_t *py_mt_host, uint32_t *np_mt_host);
+
+/* Bytes of dynamic LDS the step kernel needs for a layout (diagnostics). */
+int64_t evx_step_lds_bytes(const evx_layout *lay);
+
+const char *evx_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

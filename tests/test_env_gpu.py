@@ -1,0 +1,163 @@
+"""GPU parity of the HIP env path (libevacx.so) against the reference and the oracle.
+
+* golden replays: the reference's own trajectories (tests/golden, captured by
+  tools/capture_golden.py) re-run on the GPU from the recorded MT19937 states,
+  bit-exact on every state field, observation, reward and done flag;
+* oracle parity at scale: E independent envs per layout (36x30 P150 R1,
+  64x64 P569 R8, 128x128 P2276 R16), seeds 1234+env, random actions,
+  auto-reset, bit-exact against oracle/evac_oracle.c on every step.
+"""
+import numpy as np
+import pytest
+import torch
+
+from golden_util import FIELDS, digest, load, traj_spec
+
+pytestmark = pytest.mark.gpu
+
+
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def fixture_tables(traj):
+    from evacx.layout import LayoutTables
+    lname, P, spec = traj_spec(traj)
+    t = load(lname)
+    return LayoutTables(spec=spec, floor=t["floor"], valid=t["valid"], exit_mask=t["exit_mask"],
+                        barrier=t["barrier"], danger_p=t["danger_p"], danger_o=t["danger_o"],
+                        obs_origin=tuple(int(v) for v in t["obs_origin"])), P
+
+
+def gpu_state_fields(env, e, obs64):
+    st = env.host_state(e)
+    return dict(pos=st["pos"], health=st["health"], acc=st["acc"], flags=st["flags"], rmap=st["rmap"],
+                thmap=st["thmap"], robots=st["robots"], view=st["view"], obs=obs64[e]), st
+
+
+@pytest.mark.parametrize("traj", ["cfg1_single_traj", "cfg1_multi_traj", "g64_multi_traj", "g128_multi_traj"])
+def test_gpu_replays_reference_trajectory(traj):
+    _need_gpu()
+    from evacx.env import DeviceLayout, VecEnv
+    tables, P = fixture_tables(traj)
+    tr = load(traj)
+    E = 3  # identical copies: envs must not interfere
+    lay = DeviceLayout(tables, P)
+    env = VecEnv(lay, E, thmap=True)
+    R = lay.R
+    first = True
+    for k in range(len(tr["reward"])):
+        if tr["is_reset"][k]:
+            if first:
+                env.set_rng(np.tile(tr["rng_py"][k], (E, 1)), np.tile(tr["rng_np"][k], (E, 1)))
+                first = False
+            env.reset()
+        else:
+            a = torch.from_numpy(np.tile(tr["actions"][k].astype(np.int32), E)).cuda()
+            env.step(a)
+        obs64 = env.expand_obs(torch.float64).cpu().numpy()
+        torch.cuda.synchronize()
+        for e in range(E):
+            f, st = gpu_state_fields(env, e, obs64)
+            if k + 1 < len(tr["reward"]):
+                assert np.array_equal(st["py_mt"], tr["rng_py"][k + 1]), (k, e, "py stream")
+                assert np.array_equal(st["np_mt"], tr["rng_np"][k + 1]), (k, e, "np stream")
+            for name in FIELDS:
+                assert np.array_equal(digest(name, f[name]), tr["dig_" + name][k]), (k, e, name)
+            assert int(st["scal"][0]) == tr["fire_step"][k]
+            assert int(st["scal"][1]) == tr["cur_step"][k]
+            if not tr["is_reset"][k]:
+                assert env.reward[e].item() == tr["reward"][k], (k, e)
+                assert bool(env.done[e].item()) == bool(tr["done"][k]), (k, e)
+    env.check_err()
+    py, nps = env.get_rng()
+    assert np.array_equal(py[0], tr["rng_py_final"]) and np.array_equal(nps[0], tr["rng_np_final"])
+
+
+def _oracle_pair(spec, P, E, steps, seed0=1234, act_seed=7, thmap=True, check_every=1):
+    """Run E envs on the GPU and in the oracle with identical seeds/actions."""
+    from evacx.env import DeviceLayout, VecEnv
+    from evacx.layout import build_tables
+    from oracle import oracle as orc
+    tables = build_tables(spec)
+    lay = DeviceLayout(tables, P)
+    env = VecEnv(lay, E, thmap=thmap)
+    R = spec.R
+    env.seed([seed0 + i for i in range(E)])
+    olay = orc.Layout.from_tables(tables, P)
+    oenvs = [orc.Env(olay, thmap=thmap) for _ in range(E)]
+    for i, oe in enumerate(oenvs):
+        oe.seed(seed0 + i)
+    env.reset()
+    oobs = [oe.reset() for oe in oenvs]
+    rng = np.random.RandomState(act_seed)
+    n_resets = 0
+    for s in range(steps + 1):
+        if s > 0:
+            acts = rng.randint(0, 5, size=(E, R)).astype(np.int32)
+            acts[rng.rand(E, R) < 0.02] = 7  # invalid actions are ignored by the reference
+            env.step(torch.from_numpy(acts.reshape(-1)).cuda())
+            res = [oe.step(acts[i]) for i, oe in enumerate(oenvs)]
+            oobs = [r[0] for r in res]
+            rew = env.reward.cpu().numpy()
+            done = env.done.cpu().numpy().astype(bool)
+            for i in range(E):
+                assert rew[i] == res[i][1], (s, i, rew[i], res[i][1])
+                assert done[i] == res[i][2], (s, i)
+        if s % check_every == 0 or s == steps:
+            obs64 = env.expand_obs(torch.float64).cpu().numpy()
+            obs32 = env.expand_obs(torch.float32).cpu().numpy()
+            for i in range(E):
+                f, st = gpu_state_fields(env, i, obs64)
+                ost = oenvs[i].state()
+                for name in ["pos", "health", "acc", "flags", "rmap", "robots", "view"]:
+                    assert np.array_equal(f[name], ost[name]), (s, i, name)
+                if thmap:
+                    assert np.array_equal(f["thmap"], ost["thmap"]), (s, i, "thmap")
+                assert np.array_equal(st["scal"], ost["scal"]), (s, i, "scal")
+                assert np.array_equal(st["py_mt"], ost["py_mt"]), (s, i, "py_mt")
+                assert np.array_equal(st["np_mt"], ost["np_mt"]), (s, i, "np_mt")
+                assert np.array_equal(obs64[i], oobs[i]), (s, i, "obs")
+                assert np.array_equal(obs32[i], oobs[i].astype(np.float32)), (s, i, "obs32")
+        if s > 0:
+            d = env.done.clone()
+            if d.any():
+                n_resets += int(d.sum())
+                env.reset(mask=d)
+                for i in np.nonzero(d.cpu().numpy())[0]:
+                    oobs[i] = oenvs[i].reset()
+    env.check_err()
+    return n_resets
+
+
+def test_gpu_vs_oracle_cfg1_many_envs_with_resets():
+    _need_gpu()
+    from evacx.layout import reference_single
+    n = _oracle_pair(reference_single(), 150, E=48, steps=260, check_every=13)
+    assert n > 48  # every env went through several episodes (fire saturated)
+
+
+def test_gpu_vs_oracle_multi_cfg1():
+    _need_gpu()
+    from evacx.layout import reference_multi
+    _oracle_pair(reference_multi(), 150, E=16, steps=120, check_every=7)
+
+
+def test_gpu_vs_oracle_synthetic_64():
+    _need_gpu()
+    from evacx.layout import synthetic
+    _oracle_pair(synthetic(64, 64, 8), 569, E=12, steps=60, check_every=6)
+
+
+def test_gpu_vs_oracle_synthetic_128_r16():
+    _need_gpu()
+    from evacx.layout import synthetic
+    _oracle_pair(synthetic(128, 128, 16), 2276, E=6, steps=40, check_every=5)
+
+
+def test_gpu_vs_oracle_dense_conflicts():
+    """Many people on a small grid: heavy move conflicts, duplicates, big shuffles."""
+    _need_gpu()
+    from evacx.layout import synthetic
+    _oracle_pair(synthetic(24, 20, 4), 380, E=16, steps=50, check_every=1)
