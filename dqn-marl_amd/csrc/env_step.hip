@@ -1,10 +1,13 @@
 // MI355X (gfx950) evacuation cellular automaton: env reset / step / observation.
 //
-// One 256-thread workgroup owns one env instance for a whole step. Person state
-// (packed cell+flags, health f64, acc f64) lives in registers, K persons per
-// thread (person p = tid + k*256, so every global access is coalesced). The
-// occupancy grid is an LDS bitmap, the move-conflict table an LDS array of
-// 16-bit entries, and the two MT19937 streams LDS rings (evx_device.h).
+// One 512-thread workgroup (8 waves) owns one env instance for a whole step.
+// Persons are processed in rows of 512 (person p = row*512 + tid, so global
+// accesses are coalesced) by runtime loops (a small instruction footprint: the
+// kernel is latency-bound and must not thrash the instruction cache).
+// Per-person packed cell+flags, planned direction and first-planner index live
+// in LDS; health/acc stream from HBM once per step. The occupancy grid is an
+// LDS bitmap, the move-conflict table an LDS array of 16-bit entries, and the
+// two MT19937 streams LDS rings (evx_device.h).
 //
 // The step is the reference's EvacuationEnv.step (envs/evacuation_env.py:122-172)
 // and EvacuationEnvMulti.step (envs/evacuation_env_multi.py:55-89), evaluated
@@ -30,20 +33,21 @@
 
 namespace evx {
 
-constexpr int RING_PY = 4096;  // >= 256 persons x 8 candidates x 2 words
-constexpr int RING_NP = 1024;  // >= 256 persons x 2 words, >= 851
+constexpr int RING = 2048;          // MT ring (words), >= 1078
+constexpr int RMASK = RING - 1;
+constexpr int WIN = RING - MT_GEN - 16;  // words per consumption window
 constexpr int GRP_CAP = 256;
-constexpr uint32_t NIL = 0xffffffffu;
-constexpr int SHUF_CHUNK = 2048;
-
-// MoveTO (envs/map.py:11-19)
-__constant__ int c_dx[8] = {1, 0, -1, 0, 1, -1, -1, 1};
-__constant__ int c_dy[8] = {0, -1, 0, 1, -1, -1, 1, 1};
+constexpr int PW_CAP = 256;         // pairwise-sum leaves
+constexpr uint32_t NIL16 = 0xffffu;
+constexpr int SHUF_CHUNK = 1024;
+constexpr uint32_t NODIR = 0xffu;
 
 struct Geo {
     int L, W, GY, G, RW, P, R;
 };
 
+__device__ __forceinline__ int move_dx(int d) { return (int)((0x8246u >> (2 * d)) & 3u) - 1; }  // MoveTO x
+__device__ __forceinline__ int move_dy(int d) { return (int)((0xA091u >> (2 * d)) & 3u) - 1; }  // MoveTO y
 __device__ __forceinline__ int pk_x(uint32_t v) { return v & 0xfff; }
 __device__ __forceinline__ int pk_y(uint32_t v) { return (v >> 12) & 0xfff; }
 __device__ __forceinline__ bool pk_safe(uint32_t v) { return (v >> 24) & 1; }
@@ -86,7 +90,7 @@ __device__ __forceinline__ double person_speed(double h) {
     return 1.0 * (0.3 + 0.7 * (h / 100.0));
 }
 
-// Build the compact observation of one robot with one wave (bits by ballot).
+// Compact observation of one robot built by one wave (bits by ballot).
 __device__ __forceinline__ void write_obs(const Geo& g, const uint32_t* validb, const uint32_t* rmapb, int cx,
                                           int cy, int fs, evx_obs* dst) {
     const int lane = threadIdx.x & 63;
@@ -111,15 +115,14 @@ __device__ __forceinline__ void write_obs(const Geo& g, const uint32_t* validb, 
 }
 
 // Store the MT state after consuming up to raw index `head` (CPython index semantics).
-__device__ __forceinline__ void mt_store(uint32_t* ring, int mask, int& front, int head, uint32_t* gst) {
+__device__ __forceinline__ void mt_store(uint32_t* ring, int& front, int head, uint32_t* gst) {
     if (head <= MT_N) {
-        // no twist happened: words unchanged, only the index moves
-        if (threadIdx.x == 0) gst[MT_N] = (uint32_t)head;
+        if (threadIdx.x == 0) gst[MT_N] = (uint32_t)head;  // no twist: words unchanged
         return;
     }
     const int b = MT_N * ((head - 1) / MT_N);
-    mt_ensure(ring, mask, front, b + MT_N);
-    for (int i = threadIdx.x; i < MT_N; i += NT) gst[i] = ring[(b + i) & mask];
+    mt_ensure(ring, RMASK, front, b + MT_N);
+    for (int i = threadIdx.x; i < MT_N; i += NT) gst[i] = ring[(b + i) & RMASK];
     if (threadIdx.x == 0) gst[MT_N] = (uint32_t)(head - b);
 }
 
@@ -128,31 +131,39 @@ __device__ __forceinline__ void mt_load(uint32_t* ring, const uint32_t* gst, int
     head = (int)gst[MT_N];
 }
 
-struct StepLds {
-    // word offsets into dynamic LDS
-    int regionA, claim, pyring, npring, rmapb, validb, lhead, lnext, confl, grp, robots, wsum, dsum, ctrl, total;
-    int regionA_words;
+struct StepLds {  // word offsets into dynamic LDS
+    int region, pyring, npring, claim, distbuf, hbuf, pwsum;
+    int pk, dir, pf, lhead, lnext, confl, rmapb, validb, grp, robots, wsum, dsum, ctrl, total;
 };
 
 __host__ __device__ inline StepLds step_lds(int G, int P, int R) {
     StepLds s;
     const int RW = (G + 31) / 32;
     const int CW = (G + 1) / 2;
-    int a = CW + RING_PY + RING_NP;
-    if (a < 4 * P) a = 4 * P;
+    // region: rows -> [py ring][np ring]; claims..execute -> [py ring][claim];
+    //         reward -> [distbuf P doubles][hbuf P doubles][leaf sums]
+    int a = RING + (CW > RING ? CW : RING);
+    const int P4 = (2 * P + 3) & ~3;  // 16-B aligned double arrays
+    const int b = 2 * P4 + 2 * PW_CAP;
+    if (a < b) a = b;
     a = (a + 3) & ~3;
     int o = 0;
-    s.regionA = o;
-    s.claim = o;
-    s.pyring = o + CW;
-    s.npring = o + CW + RING_PY;
-    s.regionA_words = a;
+    s.region = o;
+    s.pyring = o;
+    s.npring = o + RING;
+    s.claim = o + RING;
+    s.distbuf = o;
+    s.hbuf = o + P4;
+    s.pwsum = o + 2 * P4;
     o += a;
-    s.rmapb = o; o += RW;
-    s.validb = o; o += RW;
-    s.lhead = o; o += P;
+    s.pk = o; o += P;
+    s.dir = o; o += (P + 3) / 4;
+    s.pf = o; o += (P + 1) / 2;
+    s.lhead = o; o += (P + 1) / 2;
     s.lnext = o; o += (P + 1) / 2;
     s.confl = o; o += (P + 31) / 32;
+    s.rmapb = o; o += RW;
+    s.validb = o; o += RW;
     s.grp = o; o += GRP_CAP;
     s.robots = o; o += R;
     o = (o + 1) & ~1;
@@ -164,41 +175,60 @@ __host__ __device__ inline StepLds step_lds(int G, int P, int R) {
     return s;
 }
 
-template <int K>
-__global__ __launch_bounds__(NT) void env_step_kernel(evx_layout lay, evx_state st, const int32_t* __restrict__ actions,
-                                                      evx_step_out out) {
+// Diagnostic phase stamps (evx_step_out.stamps; off when NULL).
+#define EVX_STAMP(i)                                                                                   \
+    do {                                                                                               \
+        if (out.stamps && threadIdx.x == 0)                                                            \
+            out.stamps[(size_t)blockIdx.x * 16 + (i)] = (int64_t)__builtin_amdgcn_s_memtime();         \
+    } while (0)
+#define EVX_COUNT(i, v)                                                                                \
+    do {                                                                                               \
+        if (out.stamps && threadIdx.x == 0) out.stamps[(size_t)blockIdx.x * 16 + (i)] = (v);           \
+    } while (0)
+
+__global__ __launch_bounds__(NT, 4) void env_step_kernel(evx_layout lay, evx_state st,
+                                                         const int32_t* __restrict__ actions, evx_step_out out) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const int e = blockIdx.x;
     const int tid = threadIdx.x;
+    EVX_STAMP(0);
     Geo g;
     g.L = lay.L; g.W = lay.W; g.GY = lay.W + 2; g.G = (lay.L + 2) * (lay.W + 2);
     g.RW = (g.G + 31) / 32; g.P = lay.P; g.R = lay.R;
     const int P = g.P, R = g.R;
+    const int NROW = (P + NT - 1) / NT;
     const StepLds S = step_lds(g.G, P, R);
-    uint32_t* claim = smem + S.claim;
     uint32_t* pyring = smem + S.pyring;
     uint32_t* npring = smem + S.npring;
-    uint32_t* rmapb = smem + S.rmapb;
-    uint32_t* validb = smem + S.validb;
-    uint32_t* lhead = smem + S.lhead;
+    uint32_t* claim = smem + S.claim;
+    uint32_t* pkL = smem + S.pk;
+    uint8_t* dirL = reinterpret_cast<uint8_t*>(smem + S.dir);
+    uint16_t* pfL = reinterpret_cast<uint16_t*>(smem + S.pf);
+    uint32_t* lhead = smem + S.lhead;  // 16-bit entries
     uint16_t* lnext = reinterpret_cast<uint16_t*>(smem + S.lnext);
     uint32_t* confl = smem + S.confl;
+    uint32_t* rmapb = smem + S.rmapb;
+    uint32_t* validb = smem + S.validb;
     int* grp = reinterpret_cast<int*>(smem + S.grp);
     uint32_t* robots = smem + S.robots;
     int* wsum = reinterpret_cast<int*>(smem + S.wsum);
     double* dsum = reinterpret_cast<double*>(smem + S.dsum);
     int* ctrl = reinterpret_cast<int*>(smem + S.ctrl);
-    double* distbuf = reinterpret_cast<double*>(smem + S.regionA);
-    double* hbuf = distbuf + P;
+    double* distbuf = reinterpret_cast<double*>(smem + S.distbuf);
+    double* hbuf = reinterpret_cast<double*>(smem + S.hbuf);
+    double* pwsum = reinterpret_cast<double*>(smem + S.pwsum);
+
+    uint32_t* pk_g = st.pk + (size_t)e * P;
+    double* h_g = st.health + (size_t)e * P;
+    double* a_g = st.acc + (size_t)e * P;
 
     // ---------------------------------------------------------------- load
-    const int CW = (g.G + 1) / 2;
     for (int i = tid; i < g.RW; i += NT) {
         rmapb[i] = st.rmap[(size_t)e * g.RW + i];
         validb[i] = lay.valid_bits[i];
     }
-    for (int i = tid; i < CW; i += NT) claim[i] = 0xffffffffu;
-    for (int i = tid; i < P; i += NT) lhead[i] = NIL;
+    for (int p = tid; p < P; p += NT) pkL[p] = pk_g[p];
+    for (int i = tid; i < (P + 1) / 2; i += NT) lhead[i] = 0xffffffffu;
     for (int i = tid; i < (P + 31) / 32; i += NT) confl[i] = 0;
     int py_head, np_head;
     mt_load(pyring, st.py_mt + (size_t)e * EVX_MT_WORDS, py_head);
@@ -218,8 +248,9 @@ __global__ __launch_bounds__(NT) void env_step_kernel(evx_layout lay, evx_state 
             else if (a == 1) ny = y - 1;
             else if (a == 2) nx = x - 1;
             else if (a == 3) ny = y + 1;
+            const int c = nx * g.GY + ny;
             if (lay.rx_lo <= nx && nx <= lay.rx_hi && 0 <= ny && ny <= g.W && nx >= 1 && nx <= g.L && ny >= 1 &&
-                ny <= g.W && ((lay.valid_bits[(nx * g.GY + ny) >> 5] >> ((nx * g.GY + ny) & 31)) & 1u))
+                ny <= g.W && ((lay.valid_bits[c >> 5] >> (c & 31)) & 1u))
                 rp = rp_pack(nx, ny);
         }
         robots[tid] = rp;
@@ -228,134 +259,148 @@ __global__ __launch_bounds__(NT) void env_step_kernel(evx_layout lay, evx_state 
     }
     __syncthreads();
     if (ctrl[0]) view = robots[0];  // robot_position refreshed only after a valid action
-    __syncthreads();
+    EVX_STAMP(1);
 
-    // ------------------------------------------------ per-person registers
-    uint32_t pk[K];
-    double hh[K], ac[K];
-    int tg[K], pfv[K];
-    bool act0[K];
-    const uint32_t* pk_g = st.pk + (size_t)e * P;
-    const double* h_g = st.health + (size_t)e * P;
-    const double* a_g = st.acc + (size_t)e * P;
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-        const int p = tid + k * NT;
-        pk[k] = (p < P) ? pk_g[p] : (3u << 24);
-        act0[k] = (p < P) && !((pk[k] >> 24) & 3u);
-        // health of every non-dead person feeds the reward's sum (safe ones included)
-        hh[k] = ((p < P) && !((pk[k] >> 25) & 1u)) ? h_g[p] : 0.0;
-        ac[k] = act0[k] ? a_g[p] : 0.0;
-        tg[k] = -1;
-        pfv[k] = -1;
-    }
+    // --------------------- People.run phases 1+2 (health, accumulate, plan)
     const double* dpt = lay.danger_p + (size_t)fs * g.G;
-
-    // ------------------------------- People.run phases 1+2, row by row
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-        const int p = tid + k * NT;
+    for (int row = 0; row < NROW; row++) {
+        const int p = row * NT + tid;
+        const bool inr = p < P;
+        uint32_t v = inr ? pkL[p] : (3u << 24);
+        const bool act = !((v >> 24) & 3u);
+        double hh = 0.0, ac = 0.0, dg = 0.0;
+        const int x = pk_x(v), y = pk_y(v);
+        if (act) {
+            hh = h_g[p];
+            ac = a_g[p];
+            dg = dpt[x * g.GY + y];
+        }
         // phase 1: Person.update_state -> update_health (numpy stream)
-        double dg = 0.0;
-        if (act0[k]) dg = dpt[pk_x(pk[k]) * g.GY + pk_y(pk[k])];
-        const bool need = act0[k] && dg > 0;
+        const bool need = act && dg > 0;
         int tot;
-        int off = block_exscan(need ? 2 : 0, wsum, tot);
-        mt_ensure(npring, RING_NP - 1, np_front, np_head + tot);
-        bool alive = act0[k];
-        if (need) {
-            const double u = mt_double(npring, RING_NP - 1, np_head + off);
-            if (update_health(hh[k], dg, u)) {
-                pk[k] |= (2u << 24);
-                alive = false;
+        const int off = block_exscan(need ? 2 : 0, wsum, tot);
+        bool alive = act;
+        for (int lo = 0; lo < tot; lo += WIN) {  // windowed: rows may need more words than the ring
+            mt_ensure(npring, RMASK, np_front, np_head + min(tot, lo + WIN));
+            if (need && off >= lo && off < lo + WIN) {
+                const double u = mt_double(npring, RMASK, np_head + off);
+                if (update_health(hh, dg, u)) {
+                    v |= (2u << 24);
+                    alive = false;
+                }
             }
         }
         np_head += tot;
-        // phase 2: accumulate, plan with find_best_direction (Python stream)
+        // phase 2: accumulate; plan with find_best_direction (Python stream)
         bool planner = false;
         if (alive) {
-            ac[k] += person_speed(hh[k]) * 0.5;
-            if (ac[k] >= 1.0) {
-                ac[k] -= 1.0;
+            ac += person_speed(hh) * 0.5;
+            if (ac >= 1.0) {
+                ac -= 1.0;
                 planner = true;
             }
         }
         int cand = 0, ncand = 0;
-        const int x = pk_x(pk[k]), y = pk_y(pk[k]);
         if (planner) {
-#pragma unroll
             for (int d = 0; d < 8; d++) {
-                const int nx = x + c_dx[d], ny = y + c_dy[d];
+                const int nx = x + move_dx(d), ny = y + move_dy(d);
                 if (check_valid(g, validb, nx, ny) && !bit_get(rmapb, nx * g.GY + ny)) {
                     cand |= 1 << d;
                     ncand++;
                 }
             }
         }
-        off = block_exscan(2 * ncand, wsum, tot);
-        mt_ensure(pyring, RING_PY - 1, py_front, py_head + tot);
-        if (planner && ncand) {
-            const double fxy = lay.floor[x * g.GY + y];
-            int best = -1;
-            double maxs = -INFINITY;
-            int idx = py_head + off;
-            for (int d = 0; d < 8; d++) {
-                if (!((cand >> d) & 1)) continue;
-                const int nx = x + c_dx[d], ny = y + c_dy[d];
-                const double delta_p = fxy - lay.floor[nx * g.GY + ny];
-                int md2 = 0x7fffffff;
-                for (int r = 0; r < R; r++) {
-                    const uint32_t rp = robots[r];
-                    const int dx = nx - rp_x(rp), dy = ny - rp_y(rp);
-                    const int d2 = dx * dx + dy * dy;
-                    md2 = d2 < md2 ? d2 : md2;
-                }
-                double effect = 0.0;
-                if (md2 < lay.repel_d2) effect = lay.repel_k / (sqrt((double)md2) + 0.1);
-                const double u = -0.1 + (0.1 - -0.1) * mt_double(pyring, RING_PY - 1, idx);
-                idx += 2;
-                const double score = delta_p * 5.0 + effect + u;
-                if (score > maxs) {
-                    maxs = score;
-                    best = d;
+        int tot2;
+        const int off2 = block_exscan(2 * ncand, wsum, tot2);
+        uint32_t best = NODIR;
+        for (int lo = 0; lo < tot2; lo += WIN) {
+            mt_ensure(pyring, RMASK, py_front, py_head + min(tot2, lo + WIN) + 16);
+            if (ncand && off2 >= lo && off2 < lo + WIN) {
+                const double fxy = lay.floor[x * g.GY + y];
+                double maxs = -INFINITY;
+                int idx = py_head + off2;
+                for (int d = 0; d < 8; d++) {
+                    if (!((cand >> d) & 1)) continue;
+                    const int nx = x + move_dx(d), ny = y + move_dy(d);
+                    const double delta_p = fxy - lay.floor[nx * g.GY + ny];
+                    int md2 = 0x7fffffff;
+                    for (int r = 0; r < R; r++) {
+                        const uint32_t rp = robots[r];
+                        const int dx = nx - rp_x(rp), dy = ny - rp_y(rp);
+                        const int d2 = dx * dx + dy * dy;
+                        md2 = d2 < md2 ? d2 : md2;
+                    }
+                    double effect = 0.0;
+                    if (md2 < lay.repel_d2) effect = lay.repel_k / (sqrt((double)md2) + 0.1);
+                    const double u = -0.1 + (0.1 - -0.1) * mt_double(pyring, RMASK, idx);
+                    idx += 2;
+                    const double score = delta_p * 5.0 + effect + u;
+                    if (score > maxs) {
+                        maxs = score;
+                        best = (uint32_t)d;
+                    }
                 }
             }
-            if (best >= 0) tg[k] = (x + c_dx[best]) * g.GY + (y + c_dy[best]);
         }
-        py_head += tot;
-        (void)p;
+        py_head += tot2;
+        if (inr) {
+            dirL[p] = (uint8_t)best;
+            if (act) {
+                pkL[p] = v;
+                h_g[p] = hh;
+                a_g[p] = ac;
+            }
+        }
     }
+    // the numpy stream is finished for this step: its ring becomes the claim table
+    mt_store(npring, np_front, np_head, st.np_mt + (size_t)e * EVX_MT_WORDS);
+    EVX_COUNT(13, np_head);
+    __syncthreads();
+    EVX_STAMP(2);
 
     // ------------------------------------ targets: first planner per cell
-#pragma unroll
-    for (int k = 0; k < K; k++)
-        if (tg[k] >= 0) lds_min16(claim, tg[k], (uint32_t)(tid + k * NT));
+    const int CW = (g.G + 1) / 2;
+    for (int i = tid; i < CW; i += NT) claim[i] = 0xffffffffu;
     __syncthreads();
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-        if (tg[k] >= 0) {
-            const int p = tid + k * NT;
-            const int pf = (int)lds_read16(claim, tg[k]);
-            pfv[k] = pf;
-            if (pf != p) {
+    for (int p = tid; p < P; p += NT) {
+        const uint32_t d = dirL[p];
+        if (d != NODIR) {
+            const uint32_t v = pkL[p];
+            lds_min16(claim, (pk_x(v) + move_dx(d)) * g.GY + pk_y(v) + move_dy(d), (uint32_t)p);
+        }
+    }
+    __syncthreads();
+    for (int p = tid; p < P; p += NT) {
+        const uint32_t d = dirL[p];
+        if (d != NODIR) {
+            const uint32_t v = pkL[p];
+            const int t = (pk_x(v) + move_dx(d)) * g.GY + pk_y(v) + move_dy(d);
+            const uint32_t pf = lds_read16(claim, t);
+            pfL[p] = (uint16_t)pf;
+            if (pf != (uint32_t)p) {
                 atomicOr(&confl[pf >> 5], 1u << (pf & 31));
-                const uint32_t old = atomicExch(&lhead[pf], (uint32_t)p);
-                lnext[p] = (uint16_t)(old & 0xffffu);
+                lnext[p] = (uint16_t)lds_exch16(lhead, (int)pf, (uint32_t)p);
             }
         }
     }
     __syncthreads();
-#pragma unroll
-    for (int k = 0; k < K; k++)
-        if (tg[k] >= 0 && pfv[k] == tid + k * NT) lds_set16_ffff(claim, tg[k]);
+    for (int p = tid; p < P; p += NT) {
+        const uint32_t d = dirL[p];
+        if (d != NODIR && pfL[p] == (uint32_t)p) {
+            const uint32_t v = pkL[p];
+            lds_set16_ffff(claim, (pk_x(v) + move_dx(d)) * g.GY + pk_y(v) + move_dy(d));
+        }
+    }
+    EVX_STAMP(3);
 
     // ------------------------- random.shuffle of contested targets (lane 0)
     if (tid == 0) {
-        ctrl[0] = 0;                 // word index into confl
-        ctrl[1] = (int)confl[0];     // remaining bits of that word
+        ctrl[0] = 0;              // word index into confl
+        ctrl[1] = (int)confl[0];  // remaining bits of that word
         ctrl[2] = py_head;
-        ctrl[3] = 0;                 // done
-        ctrl[4] = 0;                 // error
+        ctrl[3] = 0;              // done
+        ctrl[4] = 0;              // error
+        ctrl[5] = 0;              // groups
     }
     __syncthreads();
     {
@@ -363,13 +408,13 @@ __global__ __launch_bounds__(NT) void env_step_kernel(evx_layout lay, evx_state 
         int last_head = -1;
         while (true) {
             const int h0 = ctrl[2];
-            mt_ensure(pyring, RING_PY - 1, py_front, h0 + SHUF_CHUNK);
+            mt_ensure(pyring, RMASK, py_front, h0 + SHUF_CHUNK);
             __syncthreads();
             if (tid == 0) {
                 int wi = ctrl[0];
                 uint32_t m = (uint32_t)ctrl[1];
                 int head = ctrl[2];
-                int done = 0;
+                int done = 0, ngrp = ctrl[5];
                 const int avail = py_front;
                 while (true) {
                     while (m == 0) {
@@ -384,7 +429,7 @@ __global__ __launch_bounds__(NT) void env_step_kernel(evx_layout lay, evx_state 
                     const int pf = wi * 32 + (__ffs(m) - 1);
                     int n = 0;
                     grp[n++] = pf;
-                    for (uint32_t q = lhead[pf]; q != NIL && (q & 0xffffu) != 0xffffu; q = lnext[q]) {
+                    for (uint32_t q = lds_read16(lhead, pf); q != NIL16; q = lnext[q]) {
                         if (n >= GRP_CAP) {
                             ctrl[4] = 1;
                             break;
@@ -392,26 +437,26 @@ __global__ __launch_bounds__(NT) void env_step_kernel(evx_layout lay, evx_state 
                         grp[n++] = (int)q;
                     }
                     for (int a = 2; a < n; a++) {  // movers in person order
-                        const int v = grp[a];
+                        const int vv = grp[a];
                         int b = a - 1;
-                        while (b >= 1 && grp[b] > v) {
+                        while (b >= 1 && grp[b] > vv) {
                             grp[b + 1] = grp[b];
                             b--;
                         }
-                        grp[b + 1] = v;
+                        grp[b + 1] = vv;
                     }
                     const int hsave = head;
                     bool ok = true;
                     for (int i = n - 1; i >= 1 && ok; i--) {  // Lib/random.py shuffle
                         const uint32_t bound = (uint32_t)(i + 1);
                         const int kb = bit_length(bound);
-                        uint32_t r;
+                        uint32_t r = 0;
                         while (true) {
                             if (head >= avail) {
                                 ok = false;
                                 break;
                             }
-                            r = mt_word(pyring, RING_PY - 1, head++) >> (32 - kb);
+                            r = mt_word(pyring, RMASK, head++) >> (32 - kb);
                             if (r < bound) break;
                         }
                         if (ok) {
@@ -424,13 +469,17 @@ __global__ __launch_bounds__(NT) void env_step_kernel(evx_layout lay, evx_state 
                         head = hsave;
                         break;
                     }
-                    lhead[pf] = (uint32_t)grp[0];  // winner
+                    // winner replaces the list head (read only for contested targets below)
+                    lhead[pf >> 1] = (lhead[pf >> 1] & ~(0xffffu << ((pf & 1) * 16))) |
+                                     ((uint32_t)grp[0] << ((pf & 1) * 16));
+                    ngrp++;
                     m &= m - 1;
                 }
                 ctrl[0] = wi;
                 ctrl[1] = (int)m;
                 ctrl[2] = head;
                 ctrl[3] = done;
+                ctrl[5] = ngrp;
             }
             __syncthreads();
             if (ctrl[3]) break;
@@ -442,57 +491,56 @@ __global__ __launch_bounds__(NT) void env_step_kernel(evx_layout lay, evx_state 
         }
         py_head = ctrl[2];
         if (ctrl[4] && out.err && tid == 0) atomicOr(out.err, ctrl[4]);
+        EVX_COUNT(14, ctrl[5]);
     }
+    mt_store(pyring, py_front, py_head, st.py_mt + (size_t)e * EVX_MT_WORDS);
+    EVX_COUNT(12, py_head);
     __syncthreads();
+    EVX_STAMP(4);
 
     // --------------------------------------------- execute_move, in order
     // event code: min over 0xffff - (first_planner<<2 | sub<<1 | value)
-    uint32_t code_old[K], code_new[K];
-    int oldc[K];
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-        code_old[k] = code_new[k] = 0;
-        oldc[k] = -1;
-        if (tg[k] >= 0) {
-            const int p = tid + k * NT;
-            const int pf = pfv[k];
-            const bool contested = (confl[pf >> 5] >> (pf & 31)) & 1u;
-            const int w = contested ? (int)lhead[pf] : pf;
-            const int cell_old = pk_x(pk[k]) * g.GY + pk_y(pk[k]);
-            if (w == p) {
-                const bool ex = (lay.cellinfo[tg[k]] >> 1) & 1u;
-                code_old[k] = 0xffffu - (((uint32_t)pf << 2) | 0u);
-                code_new[k] = 0xffffu - (((uint32_t)pf << 2) | 2u | (ex ? 0u : 1u));
-                oldc[k] = cell_old;
-                lds_min16(claim, cell_old, code_old[k]);
-                lds_min16(claim, tg[k], code_new[k]);
-                const int nx = tg[k] / g.GY, ny = tg[k] % g.GY;
-                pk[k] = (uint32_t)nx | ((uint32_t)ny << 12) | (ex ? (1u << 24) : 0u);
-                if (st.thmap) atomicAdd(&st.thmap[(size_t)e * g.G + tg[k]], 1);
-            } else {
-                if (st.thmap) atomicAdd(&st.thmap[(size_t)e * g.G + cell_old], 1);
-            }
+    for (int p = tid; p < P; p += NT) {
+        const uint32_t d = dirL[p];
+        if (d == NODIR) continue;
+        const uint32_t v = pkL[p];
+        const int pf = pfL[p];
+        const bool contested = (confl[pf >> 5] >> (pf & 31)) & 1u;
+        const int w = contested ? (int)lds_read16(lhead, pf) : pf;
+        const int cold = pk_x(v) * g.GY + pk_y(v);
+        if (w == p) {
+            const int t = cold + move_dx(d) * g.GY + move_dy(d);
+            const bool ex = (lay.cellinfo[t] >> 1) & 1u;
+            lds_min16(claim, cold, 0xffffu - ((uint32_t)pf << 2));
+            lds_min16(claim, t, 0xffffu - (((uint32_t)pf << 2) | 2u | (ex ? 0u : 1u)));
+            if (st.thmap) atomicAdd(&st.thmap[(size_t)e * g.G + t], 1);
+        } else {
+            dirL[p] = (uint8_t)(0x80u | d);  // lost the conflict: stays
+            if (st.thmap) atomicAdd(&st.thmap[(size_t)e * g.G + cold], 1);
         }
     }
     __syncthreads();
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-        if (oldc[k] >= 0) {
-            if (lds_read16(claim, oldc[k]) == code_old[k])
-                atomicAnd(&rmapb[oldc[k] >> 5], ~(1u << (oldc[k] & 31)));
-            if (lds_read16(claim, tg[k]) == code_new[k]) {
-                if (code_new[k] & 1u)  // value 0 (safe): code = ffff - (..|2|0) -> low bit 1
-                    atomicAnd(&rmapb[tg[k] >> 5], ~(1u << (tg[k] & 31)));
-                else
-                    atomicOr(&rmapb[tg[k] >> 5], 1u << (tg[k] & 31));
-            }
+    for (int p = tid; p < P; p += NT) {
+        const uint32_t d = dirL[p];
+        if (d & 0x80u) continue;  // no plan, or lost
+        const uint32_t v = pkL[p];
+        const int pf = pfL[p];
+        const int cold = pk_x(v) * g.GY + pk_y(v);
+        const int t = cold + move_dx(d) * g.GY + move_dy(d);
+        const bool ex = (lay.cellinfo[t] >> 1) & 1u;
+        const uint32_t code_new = 0xffffu - (((uint32_t)pf << 2) | 2u | (ex ? 0u : 1u));
+        if (lds_read16(claim, cold) == 0xffffu - ((uint32_t)pf << 2))
+            atomicAnd(&rmapb[cold >> 5], ~(1u << (cold & 31)));
+        if (lds_read16(claim, t) == code_new) {
+            if (ex) atomicAnd(&rmapb[t >> 5], ~(1u << (t & 31)));
+            else atomicOr(&rmapb[t >> 5], 1u << (t & 31));
         }
+        pkL[p] = (uint32_t)(pk_x(v) + move_dx(d)) | ((uint32_t)(pk_y(v) + move_dy(d)) << 12) |
+                 (ex ? (1u << 24) : 0u);
     }
-    // MT states go out now: the reward scratch below reuses the ring memory
-    mt_store(pyring, RING_PY - 1, py_front, py_head, st.py_mt + (size_t)e * EVX_MT_WORDS);
-    mt_store(npring, RING_NP - 1, np_front, np_head, st.np_mt + (size_t)e * EVX_MT_WORDS);
     __syncthreads();
     for (int i = tid; i < g.RW; i += NT) st.rmap[(size_t)e * g.RW + i] = rmapb[i];
+    EVX_STAMP(5);
 
     // ---------------------------------- fire update (both fire models)
     const int fs1 = fs < lay.t_max ? fs + 1 : fs;
@@ -502,15 +550,16 @@ __global__ __launch_bounds__(NT) void env_step_kernel(evx_layout lay, evx_state 
     int evac_t = 0, dead_t = 0;
     double gq_t = 0.0;
     int nrem = 0;
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-        const int p = tid + k * NT;
+    for (int row = 0; row < NROW; row++) {
+        const int p = row * NT + tid;
         const bool inr = p < P;
-        const bool sf = inr && pk_safe(pk[k]), dd = inr && pk_dead(pk[k]);
+        const uint32_t v = inr ? pkL[p] : (3u << 24);
+        const bool sf = inr && pk_safe(v), dd = inr && pk_dead(v);
         evac_t += sf;
         dead_t += dd;
+        const double hv = (inr && !dd) ? h_g[p] : 0.0;
         const bool rem = inr && !sf && !dd;
-        const int x2 = 2 * pk_x(pk[k]) + 1, y2 = 2 * pk_y(pk[k]) + 1;
+        const long long x2 = 2 * pk_x(v) + 1, y2 = 2 * pk_y(v) + 1;
         const long long dxr = x2 - 2LL * vx, dyr = y2 - 2LL * vy;
         const long long n4 = dxr * dxr + dyr * dyr;  // (2*distance)^2, exact
         if (rem && n4 <= 100) {
@@ -519,29 +568,69 @@ __global__ __launch_bounds__(NT) void env_step_kernel(evx_layout lay, evx_state 
             if (ne > 1600) gq_t += 2.0;
             else if (ne > 400) gq_t += 1.5;
             else gq_t += 1.0;
-            if (hh[k] < 80) gq_t += 1.0;
+            if (hv < 80) gq_t += 1.0;
         }
         int tot;
         const int off = block_exscan(rem ? 1 : 0, wsum, tot);
         if (rem) distbuf[nrem + off] = 0.5 * sqrt((double)n4);
         nrem += tot;
-        if (inr) hbuf[p] = dd ? -1.0 : hh[k];
+        if (inr) hbuf[p] = hv;  // dead -> +0.0, which leaves the sequential sum unchanged
     }
     const int evac = block_sum(evac_t, wsum);
     const int dead = block_sum(dead_t, wsum);
-    const double gq = block_sum_d(gq_t, dsum);
-    // order-sensitive f64 sums: Python sum (sequential) and numpy pairwise mean
+    const double gq = block_sum_d(gq_t, dsum);  // multiples of 0.5: exact in any order
+    EVX_STAMP(6);
+    // Order-sensitive f64 sums. Python sum over not-dead healths (sequential,
+    // wave 0 lane 0) runs beside numpy's pairwise mean (leaves on wave 1).
     if (tid == 0) {
         double total = 0.0;
-        for (int p = 0; p < P; p++) {
-            const double v = hbuf[p];
-            if (v >= 0.0) total += v;
+        const double2* h2 = reinterpret_cast<const double2*>(hbuf);
+        int p = 0;
+        for (; p + 8 <= P; p += 8) {
+            const double2 a = h2[p / 2], b = h2[p / 2 + 1], c = h2[p / 2 + 2], d = h2[p / 2 + 3];
+            total += a.x; total += a.y; total += b.x; total += b.y;
+            total += c.x; total += c.y; total += d.x; total += d.y;
         }
+        for (; p < P; p++) total += hbuf[p];
         dsum[2 * NWAVE] = total;
-    } else if (tid == 64) {
-        dsum[2 * NWAVE + 1] = nrem > 0 ? np_pairwise_sum(distbuf, nrem) / (double)nrem : 0.0;
+    } else if (tid >= 64 && tid < 128 && nrem > 0) {
+        int lo[4], ll[4];
+        const int lane = tid - 64;
+        int nleaf = 0;
+        {
+            int so[32], sl[32];
+            int sp = 1;
+            so[0] = 0; sl[0] = nrem;
+            while (sp > 0) {
+                sp--;
+                const int o = so[sp], l = sl[sp];
+                if (l <= 128) {
+                    if ((nleaf & 63) == lane && (nleaf >> 6) < 4) {
+                        lo[nleaf >> 6] = o;
+                        ll[nleaf >> 6] = l;
+                    }
+                    nleaf++;
+                } else {
+                    int n2 = l / 2;
+                    n2 -= n2 % 8;
+                    so[sp] = o + n2; sl[sp] = l - n2; sp++;
+                    so[sp] = o; sl[sp] = n2; sp++;
+                }
+            }
+        }
+        for (int j = 0; j < 4; j++) {
+            const int li = j * 64 + lane;
+            if (li < nleaf && li < PW_CAP) pwsum[li] = np_pairwise_leaf(distbuf + lo[j], ll[j]);
+        }
+        if (lane == 0) ctrl[6] = nleaf;
     }
     __syncthreads();
+    if (tid == 64) {
+        if (nrem > 0 && ctrl[6] <= PW_CAP) dsum[2 * NWAVE + 1] = np_pairwise_combine(nrem, pwsum) / (double)nrem;
+        else if (nrem > 0) dsum[2 * NWAVE + 1] = 0.0, (out.err ? atomicOr(out.err, 8) : 0);
+    }
+    __syncthreads();
+    EVX_STAMP(7);
     if (tid == 0) {
         const int remaining = P - evac - dead;
         double reward = 0.0;
@@ -599,20 +688,8 @@ __global__ __launch_bounds__(NT) void env_step_kernel(evx_layout lay, evx_state 
             write_obs(g, validb, rmapb, rp_x(c), rp_y(c), fs1, out.obs + (size_t)e * R + r);
         }
     }
-
-    // ---------------------------------------------------- store state
-    uint32_t* pk_o = st.pk + (size_t)e * P;
-    double* h_o = st.health + (size_t)e * P;
-    double* a_o = st.acc + (size_t)e * P;
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-        const int p = tid + k * NT;
-        if (act0[k]) {
-            pk_o[p] = pk[k];
-            h_o[p] = hh[k];
-            a_o[p] = ac[k];
-        }
-    }
+    for (int p = tid; p < P; p += NT) pk_g[p] = pkL[p];
+    EVX_STAMP(8);
 }
 
 // ------------------------------------------------------------------ reset
@@ -623,7 +700,7 @@ __host__ __device__ inline ResetLds reset_lds(int G, int P) {
     ResetLds s;
     const int RW = (G + 31) / 32;
     int o = 0;
-    s.pyring = o; o += RING_PY;
+    s.pyring = o; o += RING;
     s.validb = o; o += RW;
     s.rmapb = o; o += RW;
     s.pos = o; o += P;
@@ -668,7 +745,7 @@ __global__ __launch_bounds__(NT) void env_reset_kernel(evx_layout lay, evx_state
     int last = -1;
     while (true) {
         const int h0 = ctrl[1];
-        mt_ensure(pyring, RING_PY - 1, py_front, h0 + SHUF_CHUNK);
+        mt_ensure(pyring, RMASK, py_front, h0 + SHUF_CHUNK);
         __syncthreads();
         if (tid == 0) {
             int i = ctrl[0], head = ctrl[1];
@@ -681,13 +758,13 @@ __global__ __launch_bounds__(NT) void env_reset_kernel(evx_layout lay, evx_state
                     uint32_t r;
                     do {
                         if (head >= avail) { ok = false; break; }
-                        r = mt_word(pyring, RING_PY - 1, head++) >> (32 - kx);
+                        r = mt_word(pyring, RMASK, head++) >> (32 - kx);
                     } while (r >= nx);
                     if (!ok) break;
                     x = 1 + (int)r;
                     do {
                         if (head >= avail) { ok = false; break; }
-                        r = mt_word(pyring, RING_PY - 1, head++) >> (32 - ky);
+                        r = mt_word(pyring, RMASK, head++) >> (32 - ky);
                     } while (r >= ny);
                     if (!ok) break;
                     y = 1 + (int)r;
@@ -758,7 +835,7 @@ __global__ __launch_bounds__(NT) void env_reset_kernel(evx_layout lay, evx_state
             write_obs(g, validb, rmapb, rp_x(c), rp_y(c), fs, obs + (size_t)e * R + r);
         }
     }
-    mt_store(pyring, RING_PY - 1, py_front, py_head, st.py_mt + (size_t)e * EVX_MT_WORDS);
+    mt_store(pyring, py_front, py_head, st.py_mt + (size_t)e * EVX_MT_WORDS);
 }
 
 // ---------------------------------------------------- observation expand
@@ -819,19 +896,6 @@ int check_layout(const evx_layout* l) {
     if (!l->floor || !l->cellinfo || !l->valid_bits || !l->danger_p || !l->danger_o) return fail(-22, "missing table");
     return 0;
 }
-template <int K>
-int launch_step(const evx_layout* l, const evx_state* s, const int32_t* a, const evx_step_out* o, hipStream_t st,
-                size_t lds) {
-    auto kern = evx::env_step_kernel<K>;
-    static bool attr_set = false;
-    if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attr_set = true;
-    }
-    hipLaunchKernelGGL(kern, dim3(s->E), dim3(evx::NT), lds, st, *l, *s, a, *o);
-    hipError_t e = hipGetLastError();
-    return e == hipSuccess ? 0 : hip_fail(e, "env_step launch");
-}
 }  // namespace
 
 extern "C" {
@@ -852,15 +916,15 @@ int evx_env_step(const evx_layout* l, const evx_state* s, const int32_t* actions
     const int G = (l->L + 2) * (l->W + 2);
     const size_t lds = (size_t)evx::step_lds(G, l->P, l->R).total * 4;
     if (lds > 160 * 1024) return fail(-7, "layout needs more than 160 KiB of LDS");
-    const int K = (l->P + evx::NT - 1) / evx::NT;
-    hipStream_t st = (hipStream_t)stream;
-    if (K <= 1) return launch_step<1>(l, s, actions, o, st, lds);
-    if (K <= 2) return launch_step<2>(l, s, actions, o, st, lds);
-    if (K <= 4) return launch_step<4>(l, s, actions, o, st, lds);
-    if (K <= 9) return launch_step<9>(l, s, actions, o, st, lds);
-    if (K <= 16) return launch_step<16>(l, s, actions, o, st, lds);
-    if (K <= 36) return launch_step<36>(l, s, actions, o, st, lds);
-    return fail(-22, "P too large");
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)evx::env_step_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        attr_set = true;
+    }
+    hipLaunchKernelGGL(evx::env_step_kernel, dim3(s->E), dim3(evx::NT), lds, (hipStream_t)stream, *l, *s, actions, *o);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : hip_fail(e, "env_step launch");
 }
 
 int evx_env_reset(const evx_layout* l, const evx_state* s, const uint8_t* mask, evx_obs* obs, int32_t* err,
@@ -875,7 +939,8 @@ int evx_env_reset(const evx_layout* l, const evx_state* s, const uint8_t* mask, 
     if (lds > 160 * 1024) return fail(-7, "layout needs more than 160 KiB of LDS");
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)evx::env_reset_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)evx::env_reset_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
         attr_set = true;
     }
     hipLaunchKernelGGL(evx::env_reset_kernel, dim3(s->E), dim3(evx::NT), lds, (hipStream_t)stream, *l, *s, mask, obs,
@@ -920,11 +985,10 @@ int evx_seed_host(const uint32_t* seeds, int32_t n, uint32_t* py, uint32_t* np_)
         if (py) {
             uint32_t* mt = py + (size_t)s * 625;
             init_genrand(mt, 19650218u);
-            int i = 1, j = 0;
+            int i = 1;
             for (int k = 624; k; k--) {
-                mt[i] = (mt[i] ^ ((mt[i - 1] ^ (mt[i - 1] >> 30)) * 1664525u)) + seeds[s] + (uint32_t)j;
+                mt[i] = (mt[i] ^ ((mt[i - 1] ^ (mt[i - 1] >> 30)) * 1664525u)) + seeds[s];  // j == 0
                 i++;
-                j = 0;
                 if (i >= 624) {
                     mt[0] = mt[623];
                     i = 1;

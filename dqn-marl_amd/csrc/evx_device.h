@@ -3,19 +3,22 @@
 // MT19937 "ring": the reference consumes two Mersenne-Twister streams per env
 // (CPython `random`, legacy `numpy.random`). MT19937's raw state sequence obeys
 //     x[n] = x[n-227] ^ twist(x[n-624], x[n-623]),   n >= 624
-// so a workgroup keeps a window of that sequence in LDS and extends it 227 words
-// per barrier phase (all 227 are independent). Output j of the stream is
-// temper(x[pos + j]); consumers read words at prefix-sum offsets in parallel.
+// so a workgroup keeps a window of that sequence in LDS and extends it by up to
+// 454 words per barrier phase (227 threads x 2: the second word of a thread
+// depends only on its own first word and on words older than the phase).
+// Output j of the stream is temper(x[pos + j]); consumers read words at
+// prefix-sum offsets in parallel.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace evx {
 
-constexpr int NT = 256;          // threads per env workgroup (4 waves)
+constexpr int NT = 512;          // threads per env workgroup (8 waves)
 constexpr int NWAVE = NT / 64;
 constexpr int MT_N = 624;
 constexpr int MT_LAG = 227;      // 624 - 397
+constexpr int MT_GEN = 2 * MT_LAG;
 
 __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
     y ^= (y >> 11);
@@ -25,20 +28,26 @@ __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
     return y;
 }
 
-// Extend the raw sequence in `ring` (RING words, power of two) until front >= upto.
+__device__ __forceinline__ uint32_t mt_twist1(uint32_t lag, uint32_t a, uint32_t b) {
+    const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+    return lag ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+}
+
+// Extend the raw sequence in `ring` (power-of-two size >= 1078) until front >= upto.
 // Cooperative: every thread of the block calls with the same (front, upto).
-// Generates exactly what is needed (no over-generation) so that a window of
-// RING words stays readable behind the new front.
+// Generates exactly what is needed, so [upto - RING, upto) stays readable.
 __device__ __forceinline__ void mt_ensure(uint32_t* ring, int mask, int& front, int upto) {
     while (front < upto) {
-        const int cnt = min(MT_LAG, upto - front);
+        const int cnt = min(MT_GEN, upto - front);
         const int t = threadIdx.x;
-        if (t < cnt) {
+        if (t < MT_LAG && t < cnt) {
             const int n = front + t;
-            const uint32_t a = ring[(n - 624) & mask], b = ring[(n - 623) & mask];
-            const uint32_t c = ring[(n - MT_LAG) & mask];
-            const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
-            ring[n & mask] = c ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+            const uint32_t v0 = mt_twist1(ring[(n - MT_LAG) & mask], ring[(n - 624) & mask], ring[(n - 623) & mask]);
+            ring[n & mask] = v0;
+            if (t + MT_LAG < cnt) {
+                const int n2 = n + MT_LAG;
+                ring[n2 & mask] = mt_twist1(v0, ring[(n2 - 624) & mask], ring[(n2 - 623) & mask]);
+            }
         }
         __syncthreads();
         front += cnt;
@@ -57,7 +66,6 @@ __device__ __forceinline__ double mt_double(const uint32_t* ring, int mask, int 
 
 __device__ __forceinline__ int bit_length(uint32_t n) { return n ? 32 - __clz(n) : 0; }
 
-// Wave-level inclusive scan of an int (wave64, shfl_up).
 __device__ __forceinline__ int wave_incl_scan(int v) {
     const int lane = threadIdx.x & 63;
 #pragma unroll
@@ -80,10 +88,9 @@ __device__ __forceinline__ double wave_sum_d(double v) {
     return v;
 }
 
-// Exclusive scan, in PERSON order, of one value per person of "row" k
-// (persons k*NT .. k*NT+NT-1, owned one per thread). `wsum` is an LDS scratch of
-// NWAVE ints. Returns this thread's exclusive offset within the row; `row_total`
-// receives the row sum (uniform). Contains two barriers.
+// Exclusive scan in PERSON order over one row of NT persons (one per thread).
+// `wsum`: LDS scratch of NWAVE ints. Returns the thread's exclusive offset;
+// `row_total` receives the row sum (uniform). Two barriers.
 __device__ __forceinline__ int block_exscan(int v, int* wsum, int& row_total) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int incl = wave_incl_scan(v);
@@ -123,7 +130,7 @@ __device__ __forceinline__ double block_sum_d(double v, double* wsum) {
     return tot;
 }
 
-// 16-bit table entries packed two per 32-bit LDS word; atomic min via CAS.
+// 16-bit LDS table entries packed two per 32-bit word.
 __device__ __forceinline__ void lds_min16(uint32_t* tab, int idx, uint32_t v) {
     uint32_t* w = tab + (idx >> 1);
     const int sh = (idx & 1) * 16;
@@ -138,6 +145,18 @@ __device__ __forceinline__ void lds_min16(uint32_t* tab, int idx, uint32_t v) {
     }
 }
 
+__device__ __forceinline__ uint32_t lds_exch16(uint32_t* tab, int idx, uint32_t v) {
+    uint32_t* w = tab + (idx >> 1);
+    const int sh = (idx & 1) * 16;
+    uint32_t old = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (true) {
+        const uint32_t nv = (old & ~(0xffffu << sh)) | (v << sh);
+        const uint32_t prev = atomicCAS(w, old, nv);
+        if (prev == old) return (old >> sh) & 0xffffu;
+        old = prev;
+    }
+}
+
 __device__ __forceinline__ uint32_t lds_read16(const uint32_t* tab, int idx) {
     return (tab[idx >> 1] >> ((idx & 1) * 16)) & 0xffffu;
 }
@@ -146,58 +165,80 @@ __device__ __forceinline__ void lds_set16_ffff(uint32_t* tab, int idx) {
     atomicOr(tab + (idx >> 1), 0xffffu << ((idx & 1) * 16));
 }
 
-// numpy DOUBLE_pairwise_sum (PW_BLOCKSIZE 128), single lane, iterative.
+// numpy DOUBLE_pairwise_sum leaf (n <= 128), 8 accumulators, aligned double2 loads.
 __device__ inline double np_pairwise_leaf(const double* a, int n) {
     if (n < 8) {
         double res = 0.;
         for (int i = 0; i < n; i++) res += a[i];
         return res;
     }
-    double r0 = a[0], r1 = a[1], r2 = a[2], r3 = a[3], r4 = a[4], r5 = a[5], r6 = a[6], r7 = a[7];
+    const double2* a2 = reinterpret_cast<const double2*>(a);
+    double2 q0 = a2[0], q1 = a2[1], q2 = a2[2], q3 = a2[3];
+    double r0 = q0.x, r1 = q0.y, r2 = q1.x, r3 = q1.y, r4 = q2.x, r5 = q2.y, r6 = q3.x, r7 = q3.y;
     int i;
     for (i = 8; i < n - (n % 8); i += 8) {
-        r0 += a[i]; r1 += a[i + 1]; r2 += a[i + 2]; r3 += a[i + 3];
-        r4 += a[i + 4]; r5 += a[i + 5]; r6 += a[i + 6]; r7 += a[i + 7];
+        q0 = a2[i / 2]; q1 = a2[i / 2 + 1]; q2 = a2[i / 2 + 2]; q3 = a2[i / 2 + 3];
+        r0 += q0.x; r1 += q0.y; r2 += q1.x; r3 += q1.y;
+        r4 += q2.x; r5 += q2.y; r6 += q3.x; r7 += q3.y;
     }
     double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
     for (; i < n; i++) res += a[i];
     return res;
 }
 
-__device__ inline double np_pairwise_sum(const double* a, int n) {
-    // explicit post-order traversal of numpy's split tree
-    int off[24], len[24];
-    double left[24];
-    char stage[24];
-    int sp = 0;
-    off[0] = 0; len[0] = n; stage[0] = 0;
+// Leaves of numpy's pairwise split tree for n elements, left to right.
+// Returns the number of leaves (<= cap) written to off/len.
+__device__ inline int np_pairwise_leaves(int n, int* off, int* len, int cap) {
+    int so[32], sl[32];
+    int sp = 0, nl = 0;
+    so[0] = 0; sl[0] = n; sp = 1;
+    while (sp > 0) {
+        sp--;
+        const int o = so[sp], l = sl[sp];
+        if (l <= 128) {
+            if (nl < cap) { off[nl] = o; len[nl] = l; }
+            nl++;
+        } else {
+            int n2 = l / 2;
+            n2 -= n2 % 8;
+            so[sp] = o + n2; sl[sp] = l - n2; sp++;  // right pushed first -> left popped first
+            so[sp] = o; sl[sp] = n2; sp++;
+        }
+    }
+    return nl;
+}
+
+// Combine leaf sums in numpy's tree order (single lane).
+__device__ inline double np_pairwise_combine(int n, const double* leafsum) {
+    int ol[32], st[32];
+    double left[32];
+    int sp = 0, li = 0;
+    ol[0] = n; st[0] = 0;
     double ret = 0.0;
     while (true) {
-        if (len[sp] <= 128) {
-            ret = np_pairwise_leaf(a + off[sp], len[sp]);
+        if (ol[sp] <= 128) {
+            ret = leafsum[li++];
             while (true) {
                 if (sp == 0) return ret;
                 sp--;
-                if (stage[sp] == 1) {
+                if (st[sp] == 1) {
                     left[sp] = ret;
-                    stage[sp] = 2;
-                    int n2 = len[sp] / 2;
+                    st[sp] = 2;
+                    int n2 = ol[sp] / 2;
                     n2 -= n2 % 8;
-                    off[sp + 1] = off[sp] + n2;
-                    len[sp + 1] = len[sp] - n2;
-                    stage[sp + 1] = 0;
+                    ol[sp + 1] = ol[sp] - n2;
+                    st[sp + 1] = 0;
                     sp++;
                     break;
                 }
                 ret = left[sp] + ret;
             }
         } else {
-            stage[sp] = 1;
-            int n2 = len[sp] / 2;
+            st[sp] = 1;
+            int n2 = ol[sp] / 2;
             n2 -= n2 % 8;
-            off[sp + 1] = off[sp];
-            len[sp + 1] = n2;
-            stage[sp + 1] = 0;
+            ol[sp + 1] = n2;
+            st[sp + 1] = 0;
             sp++;
         }
     }

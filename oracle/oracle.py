@@ -137,6 +137,22 @@ class Env:
         lib().orc_env_step(C.byref(self.lay.c), C.byref(self.c), _p(a), _p(r), _p(d), _p(obs))
         return obs, float(r[0]), bool(d[0])
 
+    def load_state(self, st):
+        """Adopt a state dict (as produced by state() or evacx VecEnv.host_state())."""
+        self.pos[:] = st["pos"]
+        self.health[:] = st["health"]
+        self.acc[:] = st["acc"]
+        self.flags[:] = st["flags"]
+        self.rmap[:] = st["rmap"]
+        if self.thmap is not None and st.get("thmap") is not None:
+            self.thmap[:] = st["thmap"]
+        self.robots[:] = st["robots"]
+        self.view[:] = st["view"]
+        self.scal[:] = st["scal"]
+        self.time[0] = 0.5 * float(st["scal"][1])
+        self.py_mt[:] = st["py_mt"]
+        self.np_mt[:] = st["np_mt"]
+
     def state(self):
         return dict(pos=self.pos.copy(), health=self.health.copy(), acc=self.acc.copy(),
                     flags=self.flags.copy(), rmap=self.rmap.copy(),

@@ -1,0 +1,50 @@
+#!/usr/bin/env python3
+"""Diagnostic: per-phase cycle shares of env_step_kernel from in-kernel s_memtime
+stamps (evx_step_out.stamps). Shares only -- never quote this run's wall time."""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "dqn-marl_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from evacx.env import DeviceLayout, VecEnv, _ptr  # noqa: E402
+from evacx.layout import build_tables, synthetic  # noqa: E402
+
+NAMES = ["load", "regs", "rows(health+plan)", "claims", "shuffle", "execute", "mt_store+rmap", "reward-par",
+         "reward-seq", "obs", "store"]
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--envs", type=int, default=4096)
+ap.add_argument("--grid", type=int, default=128)
+ap.add_argument("--people", type=int, default=2276)
+ap.add_argument("--robots", type=int, default=16)
+ap.add_argument("--warmup", type=int, default=200)
+args = ap.parse_args()
+E, R = args.envs, args.robots
+spec = synthetic(args.grid, args.grid, R)
+lay = DeviceLayout(build_tables(spec), args.people)
+env = VecEnv(lay, E)
+env.seed([1234 + i for i in range(E)])
+env.reset()
+acts = torch.randint(0, 5, (args.warmup + 3, E * R), device="cuda", dtype=torch.int32)
+for i in range(args.warmup):
+    env.step(acts[i])
+    env.reset(mask=env.done)
+stamps = torch.zeros(E * 16, dtype=torch.int64, device="cuda")
+env.out.stamps = _ptr(stamps)
+for i in range(3):
+    env.step(acts[args.warmup + i])
+torch.cuda.synchronize()
+s = stamps.view(E, 16).cpu().numpy()
+d = np.diff(s[:, :11], axis=1)
+tot = s[:, 10] - s[:, 0]
+print(f"envs={E} median total cycles/env-step={np.median(tot):.0f} (wave-lifetime, one env)")
+for i, n in enumerate(NAMES[:10]):
+    print(f"  {n:20s} median {np.median(d[:, i]):9.0f}  mean {d[:, i].mean():9.0f}  share {d[:, i].sum() / tot.sum():6.1%}")
+print("py words/step median", np.median(s[:, 12]), " np words/step median", np.median(s[:, 13]))
+cnt = env.counts.view(E, 2).cpu().numpy()
+print("evacuated median", np.median(cnt[:, 0]), "dead median", np.median(cnt[:, 1]))
