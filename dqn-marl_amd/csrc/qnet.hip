@@ -1,0 +1,516 @@
+// MI355X (gfx950) DQN learner kernels: the Q-network contractions on MFMA and the
+// HBM-bound learner ops around them.
+//
+// Reference: Louvre_Evacuation/agents/dqn_agent.py
+//   DQNNetwork (:15-61)        -> evx_gemm (Linear / im2col-conv layers), evx_im2col/col2im
+//   DQNAgent.act (:101-124)    -> evx_act (argmax + epsilon-greedy)
+//   DQNAgent.learn (:126-168)  -> evx_td_loss (gather, max, TD target, MSE, dQ),
+//                                 evx_gemm backward, evx_colsum (bias grads),
+//                                 evx_sumsq + evx_clip_adam (clip_grad_norm_ + Adam)
+//   DQNAgent.memory (:88-99)   -> evx_replay_push / evx_replay_sample
+// GEMMs take fp32 operands in HBM and compute either exact f32 (v_mfma_f32_32x32x2_f32:
+// a k-ordered fmaf chain, used where parity with torch fp32 matters) or bf16 inputs
+// with f32 accumulation (v_mfma_f32_32x32x16_bf16, the throughput path).
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "evacx.h"
+
+namespace evxq {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int BM = 64, BN = 64, BK = 32;
+
+// ----------------------------------------------------------------- Philox4x32-10
+struct u4 {
+    uint32_t x, y, z, w;
+};
+__device__ __forceinline__ u4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+        const uint32_t h0 = (uint32_t)(p0 >> 32), l0 = (uint32_t)p0, h1 = (uint32_t)(p1 >> 32), l1 = (uint32_t)p1;
+        c0 = h1 ^ c1 ^ k0;
+        c1 = l1;
+        c2 = h0 ^ c3 ^ k1;
+        c3 = l0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return {c0, c1, c2, c3};
+}
+__device__ __forceinline__ float u01(uint32_t v) { return (float)(v >> 8) * (1.0f / 16777216.0f); }
+
+// ------------------------------------------------------------------------ GEMM
+template <typename T>
+__device__ __forceinline__ T to_in(float v);
+template <>
+__device__ __forceinline__ float to_in<float>(float v) { return v; }
+template <>
+__device__ __forceinline__ __bf16 to_in<__bf16>(float v) { return (__bf16)v; }
+
+template <typename TIn>
+__global__ __launch_bounds__(256) void gemm_kernel(evx_gemm_desc g) {
+    constexpr int PADK = sizeof(TIn) == 4 ? 1 : 8;
+    __shared__ __attribute__((aligned(16))) TIn As[BM][BK + PADK];
+    __shared__ __attribute__((aligned(16))) TIn Bs[BN][BK + PADK];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = w >> 1, wn = w & 1;
+    const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; r++) acc[r] = 0.f;
+    const bool a_kc = g.sak == 1, b_nc = g.sbn == 1;
+    for (int k0 = 0; k0 < g.K; k0 += BK) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int idx = tid + 256 * i;
+            int mm, kk;
+            if (a_kc) { mm = idx >> 5; kk = idx & 31; } else { kk = idx >> 6; mm = idx & 63; }
+            const int gm = m0 + mm, gk = k0 + kk;
+            const float v = (gm < g.M && gk < g.K) ? g.A[(int64_t)gm * g.sam + (int64_t)gk * g.sak] : 0.f;
+            As[mm][kk] = to_in<TIn>(v);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int idx = tid + 256 * i;
+            int nn, kk;
+            if (b_nc) { kk = idx >> 6; nn = idx & 63; } else { nn = idx >> 5; kk = idx & 31; }
+            const int gn = n0 + nn, gk = k0 + kk;
+            const float v = (gn < g.N && gk < g.K) ? g.B[(int64_t)gk * g.sbk + (int64_t)gn * g.sbn] : 0.f;
+            Bs[nn][kk] = to_in<TIn>(v);
+        }
+        __syncthreads();
+        const int ar = wm * 32 + (lane & 31), br = wn * 32 + (lane & 31), h = lane >> 5;
+        if constexpr (sizeof(TIn) == 4) {
+#pragma unroll
+            for (int kk = 0; kk < BK / 2; kk++)
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(As[ar][2 * kk + h], Bs[br][2 * kk + h], acc, 0, 0, 0);
+        } else {
+#pragma unroll
+            for (int s = 0; s < BK / 16; s++) {
+                const bf16x8 a = *reinterpret_cast<const bf16x8*>(&As[ar][16 * s + 8 * h]);
+                const bf16x8 b = *reinterpret_cast<const bf16x8*>(&Bs[br][16 * s + 8 * h]);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+            }
+        }
+        __syncthreads();
+    }
+    // epilogue: C/D map of the 32x32 MFMA (col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5))
+    const int gn = n0 + wn * 32 + (lane & 31);
+    if (gn >= g.N) return;
+    const float bias = g.bias ? g.bias[gn] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+        const int gm = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (gm >= g.M) continue;
+        float v = g.alpha * acc[r] + bias;
+        if (g.flags & EVX_GEMM_RELU) v = v > 0.f ? v : 0.f;
+        if (g.mask) v = g.mask[(int64_t)gm * g.ldm + gn] ? v * g.mask_scale : 0.f;
+        if (g.gate) v = g.gate[(int64_t)gm * g.ldg + gn] > 0.f ? v : 0.f;
+        float* cp = g.C + (int64_t)gm * g.ldc + gn;
+        if (g.flags & EVX_GEMM_ACCUM) v += *cp;
+        *cp = v;
+    }
+}
+
+// ------------------------------------------------------------- column sums
+// out[n] (+)= sum_m X[m*ld + n], deterministic: fixed-order partials then a fixed-order total.
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ X, int64_t ld, int M, int N,
+                                                     float* __restrict__ part, int chunks) {
+    const int n = blockIdx.x * 256 + threadIdx.x;
+    const int c = blockIdx.y;
+    if (n >= N) return;
+    const int rows = (M + chunks - 1) / chunks;
+    const int r0 = c * rows, r1 = min(M, r0 + rows);
+    float s = 0.f;
+    for (int m = r0; m < r1; m++) s += X[(int64_t)m * ld + n];
+    part[(int64_t)c * N + n] = s;
+}
+__global__ __launch_bounds__(256) void colsum_finish(const float* __restrict__ part, int N, int chunks,
+                                                     float* __restrict__ out, int accum) {
+    const int n = blockIdx.x * 256 + threadIdx.x;
+    if (n >= N) return;
+    float s = 0.f;
+    for (int c = 0; c < chunks; c++) s += part[(int64_t)c * N + n];
+    out[n] = accum ? out[n] + s : s;
+}
+
+// --------------------------------------------------------------- TD loss
+// DQNAgent.learn (agents/dqn_agent.py:143-151): q = Q(s).gather(a); y = r + gamma *
+// max Q_tgt(s') * ~done; loss = mean((q - y)^2); dQ[i, a_i] = 2 (q - y) / B.
+__global__ __launch_bounds__(256) void td_loss_kernel(const float* __restrict__ Q, const float* __restrict__ Qt,
+                                                      int A, const int32_t* __restrict__ act,
+                                                      const float* __restrict__ rew, const uint8_t* __restrict__ done,
+                                                      float gamma, int B, float* __restrict__ dQ,
+                                                      float* __restrict__ loss_out) {
+    __shared__ float red[256];
+    float part = 0.f;
+    for (int i = threadIdx.x; i < B; i += 256) {
+        float mx = Qt[(int64_t)i * A];
+        for (int j = 1; j < A; j++) mx = fmaxf(mx, Qt[(int64_t)i * A + j]);
+        const float y = rew[i] + gamma * mx * (done[i] ? 0.f : 1.f);
+        const int a = act[i];
+        const float q = Q[(int64_t)i * A + a];
+        const float d = q - y;
+        part += d * d;
+        for (int j = 0; j < A; j++) dQ[(int64_t)i * A + j] = (j == a) ? 2.f * d / (float)B : 0.f;
+    }
+    red[threadIdx.x] = part;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) loss_out[0] = red[0] / (float)B;
+}
+
+// ------------------------------------------------- clip_grad_norm_ + Adam
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g, int64_t n, float* __restrict__ part) {
+    __shared__ float red[256];
+    float s = 0.f;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) s += g[i] * g[i];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int k = 128; k > 0; k >>= 1) {
+        if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+__global__ __launch_bounds__(256) void sumsq_finish(const float* __restrict__ part, int nparts, float* __restrict__ norm) {
+    __shared__ float red[256];
+    float s = 0.f;
+    for (int i = threadIdx.x; i < nparts; i += 256) s += part[i];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int k = 128; k > 0; k >>= 1) {
+        if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) norm[0] = sqrtf(red[0]);
+}
+
+// torch.nn.utils.clip_grad_norm_ (coef = max_norm / (norm + 1e-6), clamped <= 1) fused
+// with torch.optim.Adam's update (exp_avg.lerp_, exp_avg_sq.mul_.addcmul_, addcdiv_).
+__global__ __launch_bounds__(256) void clip_adam_kernel(float* __restrict__ p, float* __restrict__ g,
+                                                        float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                                        const float* __restrict__ norm, float max_norm, float lr,
+                                                        float beta1, float beta2, float eps, float step_size,
+                                                        float bc2_sqrt, float weight_decay) {
+    float coef = 1.f;
+    if (norm && max_norm > 0.f) {
+        coef = max_norm / (norm[0] + 1e-6f);
+        coef = coef < 1.f ? coef : 1.f;
+    }
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        float gi = g[i] * coef;
+        if (weight_decay != 0.f) gi += weight_decay * p[i];
+        const float mi = m[i] + (gi - m[i]) * (1.f - beta1);
+        const float vi = v[i] * beta2 + (1.f - beta2) * gi * gi;
+        m[i] = mi;
+        v[i] = vi;
+        const float denom = sqrtf(vi) / bc2_sqrt + eps;
+        p[i] = p[i] - step_size * (mi / denom);
+        g[i] = gi;
+    }
+}
+
+// ------------------------------------------------------------- dropout mask
+// keep with probability 1-p (torch.nn.Dropout semantics; mask values 0/1)
+__global__ __launch_bounds__(256) void dropout_mask_kernel(uint8_t* __restrict__ mask, int64_t n, float p,
+                                                           uint64_t seed, uint64_t offset) {
+    const int64_t i4 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+    if (i4 >= n) return;
+    const uint64_t c = (uint64_t)i4 / 4 + offset;
+    const u4 r = philox((uint32_t)c, (uint32_t)(c >> 32), 0x5eedu, 0u, (uint32_t)seed, (uint32_t)(seed >> 32));
+    const uint32_t rr[4] = {r.x, r.y, r.z, r.w};
+    for (int j = 0; j < 4 && i4 + j < n; j++) mask[i4 + j] = u01(rr[j]) >= p ? 1 : 0;
+}
+
+// ------------------------------------------------------------------- act
+// DQNAgent.act (agents/dqn_agent.py:101-124): with probability epsilon a uniform
+// random action, else argmax_a Q (first maximum, as np.argmax).
+__global__ __launch_bounds__(256) void act_kernel(const float* __restrict__ Q, int n, int A, float epsilon,
+                                                  uint64_t seed, uint64_t offset, int32_t* __restrict__ actions) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    int best = 0;
+    float bv = Q[(int64_t)i * A];
+    for (int j = 1; j < A; j++) {
+        const float q = Q[(int64_t)i * A + j];
+        if (q > bv) {
+            bv = q;
+            best = j;
+        }
+    }
+    if (epsilon > 0.f) {
+        const uint64_t c = (uint64_t)i + offset;
+        const u4 r = philox((uint32_t)c, (uint32_t)(c >> 32), 0xac7u, 0u, (uint32_t)seed, (uint32_t)(seed >> 32));
+        if (u01(r.x) <= epsilon) best = (int)((uint64_t)r.y * (uint64_t)A >> 32);
+    }
+    actions[i] = best;
+}
+
+// ---------------------------------------------------------------- replay
+// Uniform replay ring (DQNAgent.memory, agents/dqn_agent.py:88-99) with compact
+// observations; per-agent transitions share the env's team reward/done.
+__global__ __launch_bounds__(256) void replay_push_kernel(evx_replay rp, const evx_obs* __restrict__ s,
+                                                          const evx_obs* __restrict__ s2, const int32_t* __restrict__ a,
+                                                          const double* __restrict__ r_env,
+                                                          const uint8_t* __restrict__ done_env, int n, int agents_per_env,
+                                                          int64_t pos) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int64_t slot = (pos + i) % rp.capacity;
+    const int e = i / agents_per_env;
+    rp.s[slot] = s[i];
+    rp.s2[slot] = s2[i];
+    rp.a[slot] = a[i];
+    rp.r[slot] = (float)r_env[e];
+    rp.done[slot] = done_env[e];
+}
+
+__global__ __launch_bounds__(256) void replay_sample_kernel(evx_replay rp, int64_t size, int B, uint64_t seed,
+                                                            uint64_t offset, evx_obs* __restrict__ s,
+                                                            evx_obs* __restrict__ s2, int32_t* __restrict__ a,
+                                                            float* __restrict__ r, uint8_t* __restrict__ done,
+                                                            int64_t* __restrict__ idx_out) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= B) return;
+    const uint64_t c = (uint64_t)i + offset;
+    const u4 q = philox((uint32_t)c, (uint32_t)(c >> 32), 0x5a3b1eu, 0u, (uint32_t)seed, (uint32_t)(seed >> 32));
+    const uint64_t r64 = ((uint64_t)q.x << 32) | q.y;
+    const int64_t j = (int64_t)(r64 % (uint64_t)size);
+    s[i] = rp.s[j];
+    s2[i] = rp.s2[j];
+    a[i] = rp.a[j];
+    r[i] = rp.r[j];
+    done[i] = rp.done[j];
+    if (idx_out) idx_out[i] = j;
+}
+
+__global__ __launch_bounds__(256) void gather_rows_kernel(const evx_obs* __restrict__ src,
+                                                          const int64_t* __restrict__ idx, int n,
+                                                          evx_obs* __restrict__ dst) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) dst[i] = src[idx[i]];
+}
+
+// ------------------------------------------------------------ conv helpers
+// DQNNetwork conv layers (agents/dqn_agent.py:22-24,48-50): 3x3, padding 1, on
+// 11x11 maps, as im2col + GEMM. x: [B][C][11][11] (NCHW); cols: [B*121][C*9]
+// with k = c*9 + ky*3 + kx (the order of a Conv2d weight [Cout][C][3][3]).
+__global__ __launch_bounds__(256) void im2col_kernel(const float* __restrict__ x, int B, int C, int nhwc,
+                                                     float* __restrict__ cols) {
+    const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t total = (int64_t)B * 121 * C * 9;
+    if (gid >= total) return;
+    const int K = C * 9;
+    const int64_t row = gid / K;
+    const int k = (int)(gid - row * K);
+    const int b = (int)(row / 121), pix = (int)(row - (int64_t)b * 121);
+    const int y = pix / 11, xx = pix - y * 11;
+    const int c = k / 9, r = k - c * 9, ky = r / 3, kx = r - ky * 3;
+    const int iy = y + ky - 1, ix = xx + kx - 1;
+    float v = 0.f;
+    if (iy >= 0 && iy < 11 && ix >= 0 && ix < 11) {
+        // nhwc: input given as the reference's (B, 11, 11, C) observation tensor (permute folded here)
+        v = nhwc ? x[(((int64_t)b * 11 + iy) * 11 + ix) * C + c] : x[(((int64_t)b * C + c) * 11 + iy) * 11 + ix];
+    }
+    cols[gid] = v;
+}
+
+// dx[b][c][iy][ix] = sum over (pixel, tap) mapping to it of dcols (fixed order, no atomics)
+__global__ __launch_bounds__(256) void col2im_kernel(const float* __restrict__ dcols, int B, int C,
+                                                     float* __restrict__ dx) {
+    const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t total = (int64_t)B * C * 121;
+    if (gid >= total) return;
+    const int b = (int)(gid / (C * 121));
+    const int rem = (int)(gid - (int64_t)b * C * 121);
+    const int c = rem / 121, pix = rem - c * 121, iy = pix / 11, ix = pix - iy * 11;
+    const int K = C * 9;
+    float s = 0.f;
+    for (int ky = 0; ky < 3; ky++)
+        for (int kx = 0; kx < 3; kx++) {
+            const int y = iy - ky + 1, xx = ix - kx + 1;
+            if (y < 0 || y >= 11 || xx < 0 || xx >= 11) continue;
+            s += dcols[((int64_t)b * 121 + y * 11 + xx) * K + c * 9 + ky * 3 + kx];
+        }
+    dx[gid] = s;
+}
+
+// [B*121][C] (GEMM output, pixel-major) <-> [B][C][121] (NCHW)
+__global__ __launch_bounds__(256) void pix2nchw_kernel(const float* __restrict__ src, int B, int C, int to_nchw,
+                                                       float* __restrict__ dst) {
+    const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t total = (int64_t)B * C * 121;
+    if (gid >= total) return;
+    const int b = (int)(gid / (C * 121));
+    const int rem = (int)(gid - (int64_t)b * C * 121);
+    const int c = rem / 121, pix = rem - c * 121;
+    const int64_t pm = ((int64_t)b * 121 + pix) * C + c;
+    if (to_nchw) dst[gid] = src[pm];
+    else dst[pm] = src[gid];
+}
+
+// dy[i] = y[i] > 0 ? dy[i] : 0 (ReLU backward for outputs that do not come out of a GEMM)
+__global__ __launch_bounds__(256) void relu_grad_kernel(float* __restrict__ dy, const float* __restrict__ y,
+                                                        int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n && !(y[i] > 0.f)) dy[i] = 0.f;
+}
+
+}  // namespace evxq
+
+// ===================================================================== C-ABI
+namespace {
+thread_local char q_err[256] = "";
+int qfail(int code, const char* msg) {
+    snprintf(q_err, sizeof(q_err), "%s", msg);
+    return code;
+}
+int qlaunch(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) return 0;
+    snprintf(q_err, sizeof(q_err), "%s: %s", what, hipGetErrorString(e));
+    return -5;
+}
+unsigned nblk(int64_t n) { return (unsigned)((n + 255) / 256); }
+}  // namespace
+
+extern "C" {
+
+const char* evx_q_last_error(void) { return q_err; }
+
+int evx_gemm(const evx_gemm_desc* g, void* stream) {
+    if (!g || !g->A || !g->B || !g->C) return qfail(-22, "gemm: NULL operand");
+    if (g->M <= 0 || g->N <= 0 || g->K <= 0) return 0;
+    dim3 grid((unsigned)((g->N + evxq::BN - 1) / evxq::BN), (unsigned)((g->M + evxq::BM - 1) / evxq::BM));
+    if (grid.y > 65535u) return qfail(-22, "gemm: M too large for one launch");
+    if (g->precision == EVX_PREC_BF16)
+        hipLaunchKernelGGL(evxq::gemm_kernel<__bf16>, grid, dim3(256), 0, (hipStream_t)stream, *g);
+    else
+        hipLaunchKernelGGL(evxq::gemm_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, *g);
+    return qlaunch("gemm");
+}
+
+int evx_colsum(const float* X, int64_t ld, int32_t M, int32_t N, float* out, int32_t accum, float* scratch,
+               int32_t scratch_elems, void* stream) {
+    if (M <= 0 || N <= 0) return 0;
+    int chunks = (M + 255) / 256;
+    if ((int64_t)chunks * N > scratch_elems) chunks = scratch_elems / N;
+    if (chunks < 1) return qfail(-22, "colsum: scratch too small");
+    hipLaunchKernelGGL(evxq::colsum_kernel, dim3(nblk(N), chunks), dim3(256), 0, (hipStream_t)stream, X, ld, M, N,
+                       scratch, chunks);
+    hipLaunchKernelGGL(evxq::colsum_finish, dim3(nblk(N)), dim3(256), 0, (hipStream_t)stream, scratch, N, chunks, out,
+                       accum);
+    return qlaunch("colsum");
+}
+
+int evx_td_loss(const float* Q, const float* Qt, int32_t A, const int32_t* act, const float* rew, const uint8_t* done,
+                float gamma, int32_t B, float* dQ, float* loss, void* stream) {
+    if (B <= 0) return 0;
+    hipLaunchKernelGGL(evxq::td_loss_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, Q, Qt, A, act, rew, done,
+                       gamma, B, dQ, loss);
+    return qlaunch("td_loss");
+}
+
+int evx_sumsq_norm(const float* g, int64_t n, float* scratch, int32_t scratch_elems, float* norm, void* stream) {
+    int parts = (int)((n + 4095) / 4096);
+    if (parts > scratch_elems) parts = scratch_elems;
+    if (parts > 2048) parts = 2048;
+    if (parts < 1) parts = 1;
+    hipLaunchKernelGGL(evxq::sumsq_kernel, dim3(parts), dim3(256), 0, (hipStream_t)stream, g, n, scratch);
+    hipLaunchKernelGGL(evxq::sumsq_finish, dim3(1), dim3(256), 0, (hipStream_t)stream, scratch, parts, norm);
+    return qlaunch("sumsq");
+}
+
+int evx_clip_adam(float* p, float* g, float* m, float* v, int64_t n, const float* norm, float max_norm,
+                  const evx_adam* h, void* stream) {
+    if (!h) return qfail(-22, "adam: NULL hyper-parameters");
+    if (n <= 0) return 0;
+    const double bc1 = 1.0 - pow((double)h->beta1, (double)h->step);
+    const double bc2 = 1.0 - pow((double)h->beta2, (double)h->step);
+    const float step_size = (float)(h->lr / bc1);
+    const float bc2_sqrt = (float)sqrt(bc2);
+    unsigned blocks = nblk(n);
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(evxq::clip_adam_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, norm,
+                       max_norm, h->lr, h->beta1, h->beta2, h->eps, step_size, bc2_sqrt, h->weight_decay);
+    return qlaunch("clip_adam");
+}
+
+int evx_dropout_mask(uint8_t* mask, int64_t n, float p, uint64_t seed, uint64_t offset, void* stream) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(evxq::dropout_mask_kernel, dim3(nblk((n + 3) / 4)), dim3(256), 0, (hipStream_t)stream, mask, n,
+                       p, seed, offset);
+    return qlaunch("dropout_mask");
+}
+
+int evx_act(const float* Q, int32_t n, int32_t A, float epsilon, uint64_t seed, uint64_t offset, int32_t* actions,
+            void* stream) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(evxq::act_kernel, dim3(nblk(n)), dim3(256), 0, (hipStream_t)stream, Q, n, A, epsilon, seed,
+                       offset, actions);
+    return qlaunch("act");
+}
+
+int evx_replay_push(const evx_replay* rp, const evx_obs* s, const evx_obs* s2, const int32_t* a, const double* r_env,
+                    const uint8_t* done_env, int32_t n, int32_t agents_per_env, int64_t pos, void* stream) {
+    if (!rp || rp->capacity <= 0) return qfail(-22, "replay: bad ring");
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(evxq::replay_push_kernel, dim3(nblk(n)), dim3(256), 0, (hipStream_t)stream, *rp, s, s2, a,
+                       r_env, done_env, n, agents_per_env, pos);
+    return qlaunch("replay_push");
+}
+
+int evx_replay_sample(const evx_replay* rp, int64_t size, int32_t B, uint64_t seed, uint64_t offset, evx_obs* s,
+                      evx_obs* s2, int32_t* a, float* r, uint8_t* done, int64_t* idx_out, void* stream) {
+    if (!rp || size <= 0) return qfail(-22, "replay: empty");
+    if (B <= 0) return 0;
+    hipLaunchKernelGGL(evxq::replay_sample_kernel, dim3(nblk(B)), dim3(256), 0, (hipStream_t)stream, *rp, size, B,
+                       seed, offset, s, s2, a, r, done, idx_out);
+    return qlaunch("replay_sample");
+}
+
+int evx_gather_obs(const evx_obs* src, const int64_t* idx, int32_t n, evx_obs* dst, void* stream) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(evxq::gather_rows_kernel, dim3(nblk(n)), dim3(256), 0, (hipStream_t)stream, src, idx, n, dst);
+    return qlaunch("gather_obs");
+}
+
+int evx_im2col3x3(const float* x, int32_t B, int32_t C, int32_t nhwc, float* cols, void* stream) {
+    const int64_t total = (int64_t)B * 121 * C * 9;
+    if (total <= 0) return 0;
+    hipLaunchKernelGGL(evxq::im2col_kernel, dim3(nblk(total)), dim3(256), 0, (hipStream_t)stream, x, B, C, nhwc, cols);
+    return qlaunch("im2col");
+}
+
+int evx_col2im3x3(const float* dcols, int32_t B, int32_t C, float* dx, void* stream) {
+    const int64_t total = (int64_t)B * C * 121;
+    if (total <= 0) return 0;
+    hipLaunchKernelGGL(evxq::col2im_kernel, dim3(nblk(total)), dim3(256), 0, (hipStream_t)stream, dcols, B, C, dx);
+    return qlaunch("col2im");
+}
+
+int evx_relu_grad(float* dy, const float* y, int64_t n, void* stream) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(evxq::relu_grad_kernel, dim3(nblk(n)), dim3(256), 0, (hipStream_t)stream, dy, y, n);
+    return qlaunch("relu_grad");
+}
+
+int evx_pix_nchw(const float* src, int32_t B, int32_t C, int32_t to_nchw, float* dst, void* stream) {
+    const int64_t total = (int64_t)B * C * 121;
+    if (total <= 0) return 0;
+    hipLaunchKernelGGL(evxq::pix2nchw_kernel, dim3(nblk(total)), dim3(256), 0, (hipStream_t)stream, src, B, C, to_nchw,
+                       dst);
+    return qlaunch("pix_nchw");
+}
+
+}  // extern "C"

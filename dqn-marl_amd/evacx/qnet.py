@@ -1,0 +1,344 @@
+"""Device Q-networks and the DQN learner step (host driver of libevacx's learner kernels).
+
+Reference: Louvre_Evacuation/agents/dqn_agent.py
+  * DQNNetwork (:15-61): conv 6->32->64->128 (3x3, pad 1) on the 11x11x6 patch,
+    fc 15488->512 (+ReLU, Dropout 0.2) ->256 (+ReLU) ->5.     -> ``ConvQNet``
+  * the build-defined MLP variant for the vectorised configs:
+    726->512 (+ReLU, Dropout) ->256 (+ReLU) ->5.              -> ``MLPQNet``
+  * DQNAgent.learn (:126-168): Q(s).gather(a), r + gamma max Q_tgt(s') ~done, MSE,
+    backward, clip_grad_norm_(1.0), Adam.                      -> ``Learner.learn``
+
+Parameters, gradients and Adam moments each live in ONE flat fp32 buffer (the
+reference's state_dict order), so clip+Adam is one fused kernel and a multi-GPU
+gradient all-reduce is one collective. Every contraction runs in evx_gemm
+(MFMA); torch only allocates.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from collections import OrderedDict
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+from . import _lib
+from .env import _stream
+
+PREC = {"f32": 0, "bf16": 1}
+RELU, ACCUM = 1, 2
+DROPOUT_P = 0.2
+
+
+class evx_gemm_desc(C.Structure):
+    _fields_ = [("M", C.c_int32), ("N", C.c_int32), ("K", C.c_int32), ("precision", C.c_int32),
+                ("flags", C.c_int32), ("alpha", C.c_float),
+                ("A", C.c_void_p), ("sam", C.c_int64), ("sak", C.c_int64),
+                ("B", C.c_void_p), ("sbk", C.c_int64), ("sbn", C.c_int64),
+                ("C", C.c_void_p), ("ldc", C.c_int64), ("bias", C.c_void_p),
+                ("mask", C.c_void_p), ("ldm", C.c_int64), ("mask_scale", C.c_float),
+                ("gate", C.c_void_p), ("ldg", C.c_int64)]
+
+
+class evx_adam(C.Structure):
+    _fields_ = [("lr", C.c_float), ("beta1", C.c_float), ("beta2", C.c_float), ("eps", C.c_float),
+                ("weight_decay", C.c_float), ("step", C.c_int64)]
+
+
+_q_inited = False
+
+
+def qlib():
+    global _q_inited
+    L = _lib.lib()
+    if not _q_inited:
+        L.evx_q_last_error.restype = C.c_char_p
+        L.evx_gemm.argtypes = [C.POINTER(evx_gemm_desc), C.c_void_p]
+        L.evx_colsum.argtypes = [C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p,
+                                 C.c_int32, C.c_void_p]
+        L.evx_td_loss.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_float,
+                                  C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.evx_sumsq_norm.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
+        L.evx_clip_adam.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p,
+                                    C.c_float, C.POINTER(evx_adam), C.c_void_p]
+        L.evx_dropout_mask.argtypes = [C.c_void_p, C.c_int64, C.c_float, C.c_uint64, C.c_uint64, C.c_void_p]
+        L.evx_act.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_float, C.c_uint64, C.c_uint64, C.c_void_p,
+                              C.c_void_p]
+        L.evx_im2col3x3.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]
+        L.evx_col2im3x3.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]
+        L.evx_pix_nchw.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]
+        L.evx_relu_grad.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]
+        _q_inited = True
+    return L
+
+
+def qcheck(rc, what):
+    if rc != 0:
+        raise _lib.EvacxError(f"{what} failed ({rc}): {qlib().evx_q_last_error().decode()}")
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def gemm(M, N, K, A, sam, sak, B, sbk, sbn, Cm, ldc, precision="f32", bias=None, relu=False, mask=None,
+         ldm=0, mask_scale=1.0, gate=None, ldg=0, accumulate=False, alpha=1.0):
+    d = evx_gemm_desc(M=M, N=N, K=K, precision=PREC[precision], flags=(RELU if relu else 0) | (ACCUM if accumulate else 0),
+                      alpha=alpha, A=_p(A), sam=sam, sak=sak, B=_p(B), sbk=sbk, sbn=sbn, C=_p(Cm), ldc=ldc,
+                      bias=_p(bias), mask=_p(mask), ldm=ldm, mask_scale=mask_scale, gate=_p(gate), ldg=ldg)
+    qcheck(qlib().evx_gemm(C.byref(d), _stream()), "evx_gemm")
+
+
+def colsum(X, M, N, out, scratch):
+    qcheck(qlib().evx_colsum(_p(X), N, M, N, _p(out), 0, _p(scratch), scratch.numel(), _stream()), "evx_colsum")
+
+
+# ----------------------------------------------------------------------------
+# parameter layout
+# ----------------------------------------------------------------------------
+def layer_specs(kind: str, hidden: int = 512, actions: int = 5, in_dim: int = 726) -> List[Tuple]:
+    """(name, type, fan_in, fan_out[, conv channels]) in the reference state_dict order."""
+    if kind == "conv":
+        return [("conv1", "conv", 6, 32), ("conv2", "conv", 32, 64), ("conv3", "conv", 64, 128),
+                ("fc1", "fc", 11 * 11 * 128, hidden), ("fc2", "fc", hidden, hidden // 2),
+                ("fc3", "fc", hidden // 2, actions)]
+    if kind == "mlp":
+        return [("fc1", "fc", in_dim, hidden), ("fc2", "fc", hidden, hidden // 2),
+                ("fc3", "fc", hidden // 2, actions)]
+    raise ValueError(kind)
+
+
+def param_shapes(specs) -> "OrderedDict[str, Tuple[int, ...]]":
+    out = OrderedDict()
+    for name, typ, fi, fo in specs:
+        out[name + ".weight"] = (fo, fi, 3, 3) if typ == "conv" else (fo, fi)
+        out[name + ".bias"] = (fo,)
+    return out
+
+
+class FlatParams:
+    """All tensors of one network in one flat fp32 device buffer (state_dict order)."""
+
+    def __init__(self, shapes, device, data: Optional[torch.Tensor] = None):
+        self.shapes = shapes
+        self.numel = sum(int(torch.Size(s).numel()) for s in shapes.values())
+        self.flat = torch.zeros(self.numel, dtype=torch.float32, device=device) if data is None else data
+        self.views: Dict[str, torch.Tensor] = OrderedDict()
+        o = 0
+        for k, s in shapes.items():
+            n = int(torch.Size(s).numel())
+            self.views[k] = self.flat[o:o + n].view(s)
+            o += n
+
+    def __getitem__(self, k):
+        return self.views[k]
+
+    def state_dict(self):
+        return OrderedDict((k, v.detach().clone()) for k, v in self.views.items())
+
+    def load_state_dict(self, sd):
+        for k, v in self.views.items():
+            v.copy_(sd[k].to(v.device, torch.float32).view(v.shape))
+
+    def init_like_torch(self, seed: int):
+        """nn.Conv2d / nn.Linear default init (kaiming_uniform a=sqrt(5) -> U(+-1/sqrt(fan_in)))."""
+        g = torch.Generator().manual_seed(seed)
+        for k, v in self.views.items():
+            w_name = k[:-5] + ".weight" if k.endswith(".bias") else k
+            ws = self.shapes[w_name]
+            fan_in = ws[1] * (ws[2] * ws[3] if len(ws) == 4 else 1)
+            bound = 1.0 / (fan_in ** 0.5)
+            v.copy_((torch.rand(v.shape, generator=g) * 2 - 1) * bound)
+
+
+# ----------------------------------------------------------------------------
+# networks
+# ----------------------------------------------------------------------------
+class _Workspace:
+    def __init__(self):
+        self.bufs: Dict[Tuple, torch.Tensor] = {}
+
+    def get(self, name, shape, dtype, device):
+        key = (name, tuple(shape), dtype)
+        t = self.bufs.get(key)
+        if t is None:
+            t = torch.empty(shape, dtype=dtype, device=device)
+            self.bufs[key] = t
+        return t
+
+
+class QNet:
+    """Forward/backward of the reference DQNNetwork (or the MLP variant) on evx_gemm."""
+
+    def __init__(self, kind: str, params: FlatParams, precision="f32", hidden=512, actions=5):
+        self.kind, self.P, self.prec = kind, params, precision
+        self.hidden, self.actions = hidden, actions
+        self.device = params.flat.device
+        self.ws = _Workspace()
+        self.saved = None
+
+    # ------------------------------------------------------------ fc stack
+    def _fc_forward(self, X, B, K0, mask, tag):
+        P, ws, dev, H, A = self.P, self.ws, self.device, self.hidden, self.actions
+        H1 = ws.get(tag + "h1", (B, H), torch.float32, dev)
+        gemm(B, H, K0, X, K0, 1, P["fc1.weight"], 1, K0, H1, H, self.prec, bias=P["fc1.bias"], relu=True,
+             mask=mask, ldm=H, mask_scale=1.0 / (1.0 - DROPOUT_P))
+        H2 = ws.get(tag + "h2", (B, H // 2), torch.float32, dev)
+        gemm(B, H // 2, H, H1, H, 1, P["fc2.weight"], 1, H, H2, H // 2, self.prec, bias=P["fc2.bias"], relu=True)
+        Q = ws.get(tag + "q", (B, A), torch.float32, dev)
+        gemm(B, A, H // 2, H2, H // 2, 1, P["fc3.weight"], 1, H // 2, Q, A, self.prec, bias=P["fc3.bias"])
+        return H1, H2, Q
+
+    def forward(self, x: torch.Tensor, mask: Optional[torch.Tensor], save=True, tag="") -> torch.Tensor:
+        """x: [B, 11, 11, 6] (or [B, 726]) fp32; mask: [B, hidden] uint8 dropout keep-mask or None (eval)."""
+        B = x.shape[0]
+        x = x.reshape(B, -1).contiguous()
+        if self.kind == "mlp":
+            H1, H2, Q = self._fc_forward(x, B, x.shape[1], mask, tag)
+            if save:
+                self.saved = dict(B=B, x=x, H1=H1, H2=H2, mask=mask)
+            return Q
+        ws, dev, P = self.ws, self.device, self.P
+        L = qlib()
+        Mp = B * 121
+        ins, cols, ys = [x], [], []
+        cur, C_in = x, 6
+        for li, (cname, cout) in enumerate([("conv1", 32), ("conv2", 64), ("conv3", 128)]):
+            K9 = C_in * 9
+            col = ws.get(tag + f"col{li}", (Mp, K9), torch.float32, dev)
+            qcheck(L.evx_im2col3x3(_p(cur), B, C_in, 1, _p(col), _stream()), "im2col")
+            Y = ws.get(tag + f"y{li}", (Mp, cout), torch.float32, dev)
+            gemm(Mp, cout, K9, col, K9, 1, P[cname + ".weight"], 1, K9, Y, cout, self.prec, bias=P[cname + ".bias"],
+                 relu=True)
+            cols.append(col)
+            ys.append(Y)
+            cur, C_in = Y, cout
+        F = ws.get(tag + "flat", (B, 128 * 121), torch.float32, dev)
+        qcheck(L.evx_pix_nchw(_p(cur), B, 128, 1, _p(F), _stream()), "pix_nchw")  # torch reshape of NCHW
+        H1, H2, Q = self._fc_forward(F, B, 128 * 121, mask, tag)
+        if save:
+            self.saved = dict(B=B, x=F, H1=H1, H2=H2, mask=mask, cols=cols, ys=ys)
+        return Q
+
+    def backward(self, dQ: torch.Tensor, grads: FlatParams):
+        """Writes d loss / d params into `grads` (overwrites) for the saved forward."""
+        s = self.saved
+        assert s is not None, "forward(save=True) first"
+        B, X, H1, H2, mask = s["B"], s["x"], s["H1"], s["H2"], s["mask"]
+        P, ws, dev, H, A, pr = self.P, self.ws, self.device, self.hidden, self.actions, self.prec
+        K0 = X.shape[1]
+        scratch = ws.get("colsum", (max(1, (max(B * 121, B) + 255) // 256) * max(H, 128),), torch.float32, dev)
+        # fc3
+        gemm(A, H // 2, B, dQ, 1, A, H2, H // 2, 1, grads["fc3.weight"], H // 2, pr)
+        colsum(dQ, B, A, grads["fc3.bias"], scratch)
+        dZ2 = ws.get("dz2", (B, H // 2), torch.float32, dev)
+        gemm(B, H // 2, A, dQ, A, 1, P["fc3.weight"], H // 2, 1, dZ2, H // 2, pr, gate=H2, ldg=H // 2)
+        # fc2
+        gemm(H // 2, H, B, dZ2, 1, H // 2, H1, H, 1, grads["fc2.weight"], H, pr)
+        colsum(dZ2, B, H // 2, grads["fc2.bias"], scratch)
+        dZ1 = ws.get("dz1", (B, H), torch.float32, dev)
+        gemm(B, H, H // 2, dZ2, H // 2, 1, P["fc2.weight"], H, 1, dZ1, H, pr, mask=mask, ldm=H,
+             mask_scale=1.0 / (1.0 - DROPOUT_P), gate=H1, ldg=H)
+        # fc1
+        gemm(H, K0, B, dZ1, 1, H, X, K0, 1, grads["fc1.weight"], K0, pr)
+        colsum(dZ1, B, H, grads["fc1.bias"], scratch)
+        if self.kind == "mlp":
+            return
+        L = qlib()
+        dF = ws.get("dflat", (B, K0), torch.float32, dev)
+        gemm(B, K0, H, dZ1, H, 1, P["fc1.weight"], K0, 1, dF, K0, pr, gate=X, ldg=K0)  # gate: relu(conv3) > 0
+        Mp = B * 121
+        dY = ws.get("dy2", (Mp, 128), torch.float32, dev)
+        qcheck(L.evx_pix_nchw(_p(dF), B, 128, 0, _p(dY), _stream()), "pix_nchw")
+        cols, ys = s["cols"], s["ys"]
+        for li, (cname, cin, cout) in reversed(list(enumerate([("conv1", 6, 32), ("conv2", 32, 64),
+                                                                ("conv3", 64, 128)]))):
+            K9 = cin * 9
+            gemm(cout, K9, Mp, dY, 1, cout, cols[li], K9, 1, grads[cname + ".weight"], K9, pr)
+            colsum(dY, Mp, cout, grads[cname + ".bias"], scratch)
+            if li == 0:
+                break
+            dcol = ws.get(f"dcol{li}", (Mp, K9), torch.float32, dev)
+            gemm(Mp, K9, cout, dY, cout, 1, P[cname + ".weight"], K9, 1, dcol, K9, pr)
+            dx = ws.get(f"dx{li}", (B, cin * 121), torch.float32, dev)
+            qcheck(L.evx_col2im3x3(_p(dcol), B, cin, _p(dx), _stream()), "col2im")
+            dYp = ws.get(f"dyp{li}", (Mp, cin), torch.float32, dev)
+            qcheck(L.evx_pix_nchw(_p(dx), B, cin, 0, _p(dYp), _stream()), "pix_nchw")
+            qcheck(L.evx_relu_grad(_p(dYp), _p(ys[li - 1]), dYp.numel(), _stream()), "relu_grad")
+            dY = dYp
+
+
+class Learner:
+    """Online + target networks, fused clip+Adam, TD loss: DQNAgent.learn on the device."""
+
+    def __init__(self, kind="mlp", device="cuda", lr=1e-4, gamma=0.99, max_norm=1.0, precision="f32",
+                 hidden=512, actions=5, seed=0, betas=(0.9, 0.999), eps=1e-8):
+        self.kind, self.device = kind, torch.device(device)
+        self.shapes = param_shapes(layer_specs(kind, hidden, actions))
+        self.online = FlatParams(self.shapes, self.device)
+        self.online.init_like_torch(seed)
+        self.target = FlatParams(self.shapes, self.device)
+        self.target.flat.copy_(self.online.flat)
+        self.grads = FlatParams(self.shapes, self.device)
+        self.m = torch.zeros_like(self.online.flat)
+        self.v = torch.zeros_like(self.online.flat)
+        self.adam_step = 0
+        self.lr, self.gamma, self.max_norm, self.betas, self.eps = lr, gamma, max_norm, betas, eps
+        self.hidden, self.actions, self.precision = hidden, actions, precision
+        self.net = QNet(kind, self.online, precision, hidden, actions)
+        self.tnet = QNet(kind, self.target, precision, hidden, actions)
+        self.norm = torch.zeros(1, dtype=torch.float32, device=self.device)
+        self.loss = torch.zeros(1, dtype=torch.float32, device=self.device)
+        self.scratch = torch.zeros(2048, dtype=torch.float32, device=self.device)
+        self.seed = seed
+        self.rng_offset = 0
+        self.grad_hook = None  # e.g. an all-reduce over the flat grad buffer
+
+    # ------------------------------------------------------------ dropout
+    def dropout_mask(self, B, tag="m"):
+        m = self.net.ws.get("mask_" + tag, (B, self.hidden), torch.uint8, self.device)
+        qcheck(qlib().evx_dropout_mask(_p(m), m.numel(), DROPOUT_P, self.seed, self.rng_offset, _stream()),
+               "dropout_mask")
+        self.rng_offset += (m.numel() + 3) // 4
+        return m
+
+    def q_values(self, x, train=True, mask=None, target=False):
+        B = x.shape[0]
+        if mask is None and train:
+            mask = self.dropout_mask(B, "act")
+        net = self.tnet if target else self.net
+        return net.forward(x, mask if train else None, save=False, tag="act_")
+
+    def learn(self, s, a, r, done, s2, mask_online=None, mask_target=None):
+        """One DQNAgent.learn step on device tensors; returns the loss tensor (no host sync)."""
+        B = s.shape[0]
+        if mask_online is None:
+            mask_online = self.dropout_mask(B, "on")
+        if mask_target is None:
+            mask_target = self.dropout_mask(B, "tg")
+        Q = self.net.forward(s, mask_online, save=True)
+        Qt = self.tnet.forward(s2, mask_target, save=False, tag="t_")
+        dQ = self.net.ws.get("dq", (B, self.actions), torch.float32, self.device)
+        L = qlib()
+        qcheck(L.evx_td_loss(_p(Q), _p(Qt), self.actions, _p(a), _p(r), _p(done), self.gamma, B, _p(dQ),
+                             _p(self.loss), _stream()), "td_loss")
+        self.net.backward(dQ, self.grads)
+        if self.grad_hook is not None:
+            self.grad_hook(self.grads.flat)
+        self.step_optimizer()
+        return self.loss
+
+    def step_optimizer(self):
+        L = qlib()
+        n = self.online.numel
+        qcheck(L.evx_sumsq_norm(_p(self.grads.flat), n, _p(self.scratch), self.scratch.numel(), _p(self.norm),
+                                _stream()), "sumsq")
+        self.adam_step += 1
+        h = evx_adam(lr=self.lr, beta1=self.betas[0], beta2=self.betas[1], eps=self.eps, weight_decay=0.0,
+                     step=self.adam_step)
+        qcheck(L.evx_clip_adam(_p(self.online.flat), _p(self.grads.flat), _p(self.m), _p(self.v), n,
+                               _p(self.norm) if self.max_norm else None, float(self.max_norm or 0.0), C.byref(h),
+                               _stream()), "clip_adam")
+
+    def sync_target(self):
+        """DQNAgent.update_target_network (agents/dqn_agent.py:170-172)."""
+        self.target.flat.copy_(self.online.flat)

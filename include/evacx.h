@@ -112,6 +112,77 @@ int64_t evx_step_lds_bytes(const evx_layout *lay);
 
 const char *evx_last_error(void);
 
+/* ------------------------------------------------------------------ learner
+ * DQNNetwork / DQNAgent (agents/dqn_agent.py:15-191) as device primitives. */
+
+#define EVX_PREC_F32 0   /* exact f32 MFMA (v_mfma_f32_32x32x2_f32), parity path */
+#define EVX_PREC_BF16 1  /* bf16 inputs, f32 accumulate (v_mfma_f32_32x32x16_bf16) */
+#define EVX_GEMM_RELU 1
+#define EVX_GEMM_ACCUM 2
+
+/* C[m][n] = epi(alpha * sum_k A(m,k) B(k,n) + bias[n]) with A(m,k) = A[m*sam + k*sak],
+ * B(k,n) = B[k*sbk + n*sbn], C[m*ldc + n]; epilogue order: bias, ReLU, dropout mask
+ * (mask[m*ldm+n] ? v*mask_scale : 0), ReLU-backward gate (gate[m*ldg+n] > 0 ? v : 0),
+ * accumulate. Covers nn.Linear forward (A x W^T), its dX (dY W) and dW (dY^T X). */
+typedef struct {
+    int32_t M, N, K;
+    int32_t precision;         /* EVX_PREC_* */
+    int32_t flags;             /* EVX_GEMM_* */
+    float alpha;
+    const float *A; int64_t sam, sak;
+    const float *B; int64_t sbk, sbn;
+    float *C; int64_t ldc;
+    const float *bias;         /* [N] or NULL */
+    const uint8_t *mask; int64_t ldm; float mask_scale;  /* or NULL */
+    const float *gate; int64_t ldg;                        /* or NULL */
+} evx_gemm_desc;
+
+typedef struct {
+    float lr, beta1, beta2, eps, weight_decay;
+    int64_t step;  /* 1-based step count after increment (torch.optim.Adam state['step']) */
+} evx_adam;
+
+/* Uniform replay ring of compact observations (DQNAgent.memory, agents/dqn_agent.py:88-99). */
+typedef struct {
+    int64_t capacity;
+    evx_obs *s, *s2;
+    int32_t *a;
+    float *r;
+    uint8_t *done;
+} evx_replay;
+
+int evx_gemm(const evx_gemm_desc *g, void *stream);
+/* out[n] (+)= sum_m X[m*ld+n] (bias gradients), fixed summation order */
+int evx_colsum(const float *X, int64_t ld, int32_t M, int32_t N, float *out, int32_t accum, float *scratch,
+               int32_t scratch_elems, void *stream);
+/* DQNAgent.learn TD step (agents/dqn_agent.py:143-151): loss = mean((Q[a] - (r + gamma*max Qt * !done))^2),
+ * dQ = d loss / d Q. Q, Qt: [B][A]. */
+int evx_td_loss(const float *Q, const float *Qt, int32_t A, const int32_t *act, const float *rew,
+                const uint8_t *done, float gamma, int32_t B, float *dQ, float *loss, void *stream);
+/* ||g||_2 into norm[0] (clip_grad_norm_'s total norm) */
+int evx_sumsq_norm(const float *g, int64_t n, float *scratch, int32_t scratch_elems, float *norm, void *stream);
+/* g *= min(1, max_norm/(norm+1e-6)) (skipped if norm NULL) then one torch.optim.Adam step */
+int evx_clip_adam(float *p, float *g, float *m, float *v, int64_t n, const float *norm, float max_norm,
+                  const evx_adam *h, void *stream);
+/* nn.Dropout keep-mask (1 with probability 1-p), counter-based Philox4x32-10 */
+int evx_dropout_mask(uint8_t *mask, int64_t n, float p, uint64_t seed, uint64_t offset, void *stream);
+/* DQNAgent.act (agents/dqn_agent.py:101-124): epsilon-greedy over argmax_a Q[i][a] */
+int evx_act(const float *Q, int32_t n, int32_t A, float epsilon, uint64_t seed, uint64_t offset,
+            int32_t *actions, void *stream);
+int evx_replay_push(const evx_replay *rp, const evx_obs *s, const evx_obs *s2, const int32_t *a,
+                    const double *r_env, const uint8_t *done_env, int32_t n, int32_t agents_per_env, int64_t pos,
+                    void *stream);
+/* random.sample replacement for the vectorised learner: B uniform indices < size */
+int evx_replay_sample(const evx_replay *rp, int64_t size, int32_t B, uint64_t seed, uint64_t offset, evx_obs *s,
+                      evx_obs *s2, int32_t *a, float *r, uint8_t *done, int64_t *idx_out, void *stream);
+int evx_gather_obs(const evx_obs *src, const int64_t *idx, int32_t n, evx_obs *dst, void *stream);
+/* DQNNetwork conv layers (agents/dqn_agent.py:22-24) as im2col + GEMM on 11x11 maps */
+int evx_im2col3x3(const float *x, int32_t B, int32_t C, int32_t nhwc, float *cols, void *stream);
+int evx_col2im3x3(const float *dcols, int32_t B, int32_t C, float *dx, void *stream);
+int evx_pix_nchw(const float *src, int32_t B, int32_t C, int32_t to_nchw, float *dst, void *stream);
+int evx_relu_grad(float *dy, const float *y, int64_t n, void *stream);
+const char *evx_q_last_error(void);
+
 #ifdef __cplusplus
 }
 #endif

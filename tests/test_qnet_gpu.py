@@ -1,0 +1,133 @@
+"""GPU numerics of the learner kernels (evx_gemm / td_loss / clip+Adam / conv helpers)
+against a plain PyTorch fp32 reference of the same network with the same dropout masks.
+
+Tolerances: exact-f32 MFMA path rtol 2e-4 / atol 2e-5 (summation order differs from
+torch's); bf16 MFMA path rtol 3e-2 on Q-values (bf16 inputs, f32 accumulation)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def torch_forward(kind, sd, x, mask):
+    """agents/dqn_agent.py:35-61 with an injected dropout keep-mask."""
+    B = x.shape[0]
+    if kind == "conv":
+        h = x.permute(0, 3, 1, 2).contiguous()
+        h = F.relu(F.conv2d(h, sd["conv1.weight"], sd["conv1.bias"], padding=1))
+        h = F.relu(F.conv2d(h, sd["conv2.weight"], sd["conv2.bias"], padding=1))
+        h = F.relu(F.conv2d(h, sd["conv3.weight"], sd["conv3.bias"], padding=1))
+        h = h.reshape(B, -1)
+    else:
+        h = x.reshape(B, -1)
+    h = F.relu(F.linear(h, sd["fc1.weight"], sd["fc1.bias"]))
+    if mask is not None:
+        h = h * mask.float() / 0.8
+    h = F.relu(F.linear(h, sd["fc2.weight"], sd["fc2.bias"]))
+    return F.linear(h, sd["fc3.weight"], sd["fc3.bias"])
+
+
+def make_batch(B, seed):
+    g = torch.Generator().manual_seed(seed)
+    x = (torch.rand(B, 11, 11, 6, generator=g) < 0.3).float()
+    x[..., 2] = torch.rand(B, 11, 11, generator=g) * 0.8
+    x2 = (torch.rand(B, 11, 11, 6, generator=g) < 0.3).float()
+    a = torch.randint(0, 5, (B,), generator=g, dtype=torch.int32)
+    r = torch.randn(B, generator=g) * 50
+    d = (torch.rand(B, generator=g) < 0.1).to(torch.uint8)
+    m1 = (torch.rand(B, 512, generator=g) >= 0.2).to(torch.uint8)
+    m2 = (torch.rand(B, 512, generator=g) >= 0.2).to(torch.uint8)
+    return x, x2, a, r, d, m1, m2
+
+
+@pytest.mark.parametrize("kind", ["mlp", "conv"])
+def test_forward_f32_matches_torch(kind):
+    _need_gpu()
+    from evacx.qnet import Learner
+    lr = Learner(kind=kind, precision="f32", seed=3)
+    x, _, _, _, _, m1, _ = make_batch(37, 0)
+    q = lr.net.forward(x.cuda(), m1.cuda(), save=False).cpu()
+    sd = {k: v.cpu() for k, v in lr.online.state_dict().items()}
+    ref = torch_forward(kind, sd, x, m1)
+    torch.testing.assert_close(q, ref, rtol=2e-4, atol=2e-5)
+
+
+def test_forward_bf16_close_to_torch():
+    _need_gpu()
+    from evacx.qnet import Learner
+    lr = Learner(kind="mlp", precision="bf16", seed=4)
+    x, _, _, _, _, m1, _ = make_batch(300, 1)
+    q = lr.net.forward(x.cuda(), m1.cuda(), save=False).cpu()
+    ref = torch_forward("mlp", {k: v.cpu() for k, v in lr.online.state_dict().items()}, x, m1)
+    err = (q - ref).abs().max() / ref.abs().max()
+    assert err < 3e-2, err
+
+
+@pytest.mark.parametrize("kind", ["mlp", "conv"])
+def test_learn_steps_match_torch_adam(kind):
+    """3 learn steps: loss, clipped grads and params vs torch (MSE, clip_grad_norm_(1.0), Adam 1e-4)."""
+    _need_gpu()
+    from evacx.qnet import Learner
+    B = 32
+    lr = Learner(kind=kind, precision="f32", seed=5, lr=1e-3)
+    sd0 = {k: v.cpu().clone() for k, v in lr.online.state_dict().items()}
+    params = {k: torch.nn.Parameter(v.clone()) for k, v in sd0.items()}
+    tgt = {k: v.clone() for k, v in sd0.items()}
+    opt = torch.optim.Adam(params.values(), lr=1e-3)
+    for it in range(3):
+        if it > 0:  # each step is compared from the same state (params + Adam moments)
+            lr.online.load_state_dict({k: p.detach() for k, p in params.items()})
+            for key, buf in (("exp_avg", lr.m), ("exp_avg_sq", lr.v)):
+                buf.copy_(torch.cat([opt.state[p][key].reshape(-1) for p in params.values()]).cuda())
+        x, x2, a, r, d, m1, m2 = make_batch(B, 10 + it)
+        loss = lr.learn(x.cuda(), a.cuda(), r.float().cuda(), d.cuda(), x2.cuda(), m1.cuda(), m2.cuda())
+        q = torch_forward(kind, params, x, m1).gather(1, a.long().unsqueeze(1))
+        with torch.no_grad():
+            nq = torch_forward(kind, tgt, x2, m2).max(1)[0]
+            y = r.float() + 0.99 * nq * (~d.bool())
+        ref_loss = F.mse_loss(q.squeeze(), y)
+        opt.zero_grad()
+        ref_loss.backward()
+        gnorm = torch.nn.utils.clip_grad_norm_(params.values(), 1.0)
+        grads_ref = {k: p.grad.clone() for k, p in params.items()}
+        opt.step()
+        assert abs(loss.item() - ref_loss.item()) <= 2e-4 * abs(ref_loss.item()) + 1e-5
+        assert abs(lr.norm.item() - gnorm.item()) <= 2e-4 * gnorm.item() + 1e-6
+        for k in params:
+            torch.testing.assert_close(lr.grads[k].cpu(), grads_ref[k], rtol=2e-3, atol=2e-6)
+            # Adam divides by sqrt(v): for near-zero gradients a last-bit grad difference moves
+            # that element's update by a visible fraction of lr. Bar: at most 1e-4 of the
+            # elements beyond 1e-5 (1% of a step, lr = 1e-3), none beyond one full step.
+            diff = (lr.online[k].cpu() - params[k].detach()).abs()
+            assert (diff > 1e-5).float().mean().item() <= 1e-4, (k, diff.max().item())
+            assert diff.max().item() <= 1e-3, (k, diff.max().item())
+
+
+def test_act_argmax_and_epsilon():
+    _need_gpu()
+    from evacx import qnet
+    Q = torch.tensor([[0, 1, 3, 3, 2], [5, 5, 5, 5, 5], [-1, -2, -3, -4, -0.5]], dtype=torch.float32).cuda()
+    out = torch.zeros(3, dtype=torch.int32, device="cuda")
+    qnet.qcheck(qnet.qlib().evx_act(Q.data_ptr(), 3, 5, 0.0, 1, 0, out.data_ptr(), qnet._stream()), "act")
+    assert out.cpu().tolist() == [2, 0, 4]  # first maximum, as np.argmax
+    Qb = torch.zeros(100000, 5, device="cuda")
+    Qb[:, 3] = 1
+    ob = torch.zeros(100000, dtype=torch.int32, device="cuda")
+    qnet.qcheck(qnet.qlib().evx_act(Qb.data_ptr(), 100000, 5, 0.25, 7, 0, ob.data_ptr(), qnet._stream()), "act")
+    frac = (ob != 3).float().mean().item()
+    assert abs(frac - 0.25 * 0.8) < 0.01  # random action is 3 one time in five
+
+
+def test_dropout_mask_rate():
+    _need_gpu()
+    from evacx import qnet
+    m = torch.zeros(1 << 20, dtype=torch.uint8, device="cuda")
+    qnet.qcheck(qnet.qlib().evx_dropout_mask(m.data_ptr(), m.numel(), 0.2, 11, 0, qnet._stream()), "mask")
+    assert abs(m.float().mean().item() - 0.8) < 0.003
