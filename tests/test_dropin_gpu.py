@@ -1,0 +1,152 @@
+"""The drop-in Python API (dqn-marl_amd/Louvre_Evacuation) on the GPU: the reference's
+own trajectories reproduced through EvacuationEnv / EvacuationEnvMulti, including
+what they leave in the global `random` / `numpy.random` streams; DQNAgent
+checkpoints in the reference's format; the training loop end to end."""
+import os
+import random
+
+import numpy as np
+import pytest
+import torch
+import yaml
+
+from golden_util import FIELDS, digest, load, traj_spec
+
+pytestmark = pytest.mark.gpu
+
+
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _install_fixture_layout(traj):
+    from evacx.env import DeviceLayout
+    from evacx.layout import LayoutTables
+    from Louvre_Evacuation.envs import evacuation_env as ee
+    lname, P, spec = traj_spec(traj)
+    t = load(lname)
+    tables = LayoutTables(spec=spec, floor=t["floor"], valid=t["valid"], exit_mask=t["exit_mask"],
+                          barrier=t["barrier"], danger_p=t["danger_p"], danger_o=t["danger_o"],
+                          obs_origin=tuple(int(v) for v in t["obs_origin"]))
+    key = (spec.L, spec.W, tuple(spec.exit), tuple(map(tuple, spec.robot_init)), spec.reset_robots,
+           tuple(spec.reset_view), P)
+    ee._LAYOUTS[key] = DeviceLayout(tables, P)
+
+
+def _set_global_rng(py_words, np_words):
+    random.setstate((3, tuple(int(x) for x in py_words), None))
+    np.random.set_state(("MT19937", np.asarray(np_words[:624], np.uint32), int(np_words[624]), 0, 0.0))
+
+
+def _global_rng():
+    py = np.array(random.getstate()[1], dtype=np.uint64).astype(np.uint32)
+    st = np.random.get_state()
+    return py, np.concatenate([np.asarray(st[1], np.uint32), np.array([st[2]], np.uint32)])
+
+
+@pytest.mark.parametrize("traj", ["cfg1_single_traj", "cfg1_multi_traj"])
+def test_dropin_env_reproduces_reference(traj):
+    _need_gpu()
+    from Louvre_Evacuation.envs.evacuation_env import EvacuationEnv
+    from Louvre_Evacuation.envs.evacuation_env_multi import EvacuationEnvMulti
+    _install_fixture_layout(traj)
+    tr = load(traj)
+    multi = traj == "cfg1_multi_traj"
+    env = (EvacuationEnvMulti if multi else EvacuationEnv)()
+    for k in range(len(tr["reward"])):
+        if tr["is_reset"][k]:
+            _set_global_rng(tr["rng_py"][k], tr["rng_np"][k])
+            obs = env.reset()
+            r, d = 0.0, False
+        else:
+            a = [int(v) for v in tr["actions"][k]]
+            obs, r, d, info = env.step(a if multi else a[0])
+            assert r == tr["reward"][k] and d == bool(tr["done"][k]), k
+            assert info["current_step"] == tr["cur_step"][k]
+        py, nps = _global_rng()
+        if k + 1 < len(tr["reward"]):
+            assert np.array_equal(py, tr["rng_py"][k + 1]) and np.array_equal(nps, tr["rng_np"][k + 1]), k
+        ob = np.stack(obs) if multi else obs[None]
+        assert np.array_equal(digest("obs", ob), tr["dig_obs"][k]), k
+        h = env._host
+        assert np.array_equal(digest("health", h["health"]), tr["dig_health"][k]), k
+        assert np.array_equal(digest("pos", h["pos"]), tr["dig_pos"][k]), k
+        assert np.array_equal(np.array(env.map.robot_positions, np.int32), tr["snap_robots"][k]), k
+        assert env.map.robot_position == list(tr["snap_view"][k])
+        pos = np.array([p.pos for p in env.people.list])
+        assert np.array_equal(pos, tr["snap_pos"][k] + 0.5)
+    m = env.get_performance_metrics()
+    assert m["total_steps"] == tr["cur_step"][-1]
+
+
+def test_dropin_reward_coefficients_are_runtime_mutable():
+    _need_gpu()
+    from Louvre_Evacuation.envs.evacuation_env import EvacuationEnv
+    random.seed(3)
+    np.random.seed(3)
+    env = EvacuationEnv()
+    r1, alive = [], []
+    for _ in range(3):
+        r1.append(env.step(4)[1])
+        alive.append(150 - int(((env._host["flags"] >> 1) & 1).sum()))
+    random.seed(3)
+    np.random.seed(3)
+    env2 = EvacuationEnv()  # identical trajectory: the reward does not feed back into the dynamics
+    old = EvacuationEnv.ALIVE_BONUS
+    try:
+        EvacuationEnv.ALIVE_BONUS = 0.0  # overnight_experiments.py:69-70 mutates the class attribute
+        r2 = [env2.step(4)[1] for _ in range(3)]
+    finally:
+        EvacuationEnv.ALIVE_BONUS = old
+    for a, b, n in zip(r1, r2, alive):
+        assert abs((a - b) - n) < 1e-9
+
+
+def test_dropin_agent_act_learn_checkpoint(tmp_path):
+    _need_gpu()
+    from Louvre_Evacuation.agents.dqn_agent import DQNAgent
+    cfg = yaml.safe_load(open(os.path.join(os.path.dirname(__file__), "..", "dqn-marl_amd", "configs",
+                                           "dqn.yaml")))["agent"]
+    ag = DQNAgent((11, 11, 6), 5, torch.device("cuda"), cfg)
+    keys = list(ag.q_network.state_dict().keys())
+    assert keys == ["conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias", "conv3.weight", "conv3.bias",
+                    "fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias", "fc3.weight", "fc3.bias"]
+    assert sum(p.numel() for p in ag.q_network.parameters()) == 8157093
+    rng = np.random.RandomState(0)
+    for _ in range(40):
+        s = rng.rand(11, 11, 6)
+        a = ag.act(s, training=True)
+        assert 0 <= int(a) < 5
+        ag.remember(s, a, float(rng.randn()), rng.rand(11, 11, 6), bool(rng.rand() < 0.1))
+    losses = [ag.learn() for _ in range(3)]
+    assert all(np.isfinite(l) for l in losses) and ag.steps == 3
+    p = str(tmp_path / "m.pth")
+    ag.save(p)
+    ck = torch.load(p, weights_only=True)
+    assert set(ck) == {"q_network", "target_network", "optimizer", "epsilon", "steps"}
+    assert len(ck["optimizer"]["state"]) == 12 and float(ck["optimizer"]["state"][0]["step"]) == 3
+    ag2 = DQNAgent((11, 11, 6), 5, torch.device("cuda"), cfg)
+    ag2.load(p)
+    for k, v in ag.q_network.state_dict().items():
+        assert torch.equal(v.cpu(), ag2.q_network.state_dict()[k].cpu())
+    assert ag2.steps == 3 and ag2.epsilon == ag.epsilon
+    # a torch.optim.Adam state dict loads into the device optimizer and back
+    opt = torch.optim.Adam([torch.nn.Parameter(v.clone().cpu()) for v in ag.q_network.state_dict().values()])
+    ag2.optimizer.load_state_dict(opt.state_dict())
+    assert ag2._learner.adam_step == 0
+
+
+def test_train_dqn_loop_runs(tmp_path):
+    _need_gpu()
+    from Louvre_Evacuation.runners import train_dqn
+    base = yaml.safe_load(open(os.path.join(os.path.dirname(__file__), "..", "dqn-marl_amd", "configs", "dqn.yaml")))
+    base["episodes"] = 2
+    base["save_path"] = str(tmp_path / "res")
+    cfgp = tmp_path / "cfg.yaml"
+    cfgp.write_text(yaml.safe_dump(base))
+    agent, tracker = train_dqn.train_dqn(config_path=str(cfgp))
+    assert len(tracker.episode_rewards) == 2
+    assert os.path.exists(tmp_path / "res" / "dqn_model.pth")
+    assert os.path.exists(tmp_path / "res" / "reward_logs" / "episode_data.csv")
+    assert agent.steps > 0
