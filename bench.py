@@ -1,12 +1,18 @@
 #!/usr/bin/env python3
-"""Benchmark of the evacuation hot path on MI355X (contract: see README/DESIGN.md).
+"""Benchmark of the evacuation RL hot path on MI355X.
 
-Default workload (BASELINE.json metric, cfg3 per-GPU share): 128x128 synthetic
-layout, 2276 people and 16 robots per env, 4096 envs per GPU, uniform random
-actions, auto-reset, weak scaling over GPUs (env ids are global, seeds
-1234 + global env id). One "step" = one vectorised env.step over all envs
-(env mode) or env.step + act forward + replay push + one learn step (train mode).
+Workload (BASELINE.json metric; configs[2], per-GPU share): synthetic 128x128
+layout, 2276 people and 16 robots per env, 4096 envs per GPU (weak scaling;
+env ids global, seeds 1234 + global env id), uniform-init MLP Q-net (bf16 MFMA),
+batch 4096, replay 2^20 transitions per GPU, gradient all-reduce over RCCL when
+world > 1. One timed "step" = one full vectorised training step:
+act (Q forward for E*R robots + epsilon-greedy) -> env.step (all E envs) ->
+replay push (E*R transitions) -> one learn step (sample, online+target forward,
+TD loss, backward, [all-reduce], clip+Adam) -> auto-reset.
 
+value = env-steps/s of the whole job (E * n_gpus * steps / time); the JSON line
+also carries agent-transitions/s (x R), the env-only rate, the roofline of the
+dominant kernel (env_step_kernel, HBM-bound) and the CPU oracle baseline.
 Prints ONE JSON line on rank 0.
 """
 import argparse
@@ -23,7 +29,8 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 METRIC = "env steps/sec + agent-transitions/sec (whole node), 128x128 grid, 1/2/4/8 GPU"
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
+BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (spec)
 
 
 def bytes_per_env_step(P, R, G):
@@ -35,20 +42,29 @@ def bytes_per_env_step(P, R, G):
     return 40 * P + 8 * RW + 2 * 2 * 2500 + R * 44 + 48
 
 
+def qnet_flops(n_act, B, hidden=512, in_dim=726, actions=5):
+    """Dense MLP FLOPs: act forward over n_act rows + learn (online fwd, target fwd, backward dW+dX)."""
+    fwd = 2 * (in_dim * hidden + hidden * (hidden // 2) + (hidden // 2) * actions)
+    bwd = 2 * fwd - 2 * in_dim * hidden  # no dX for the input layer
+    return n_act * fwd + B * (2 * fwd + bwd)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=300)
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
     ap.add_argument("--grid", type=int, default=128)
     ap.add_argument("--people", type=int, default=2276)
     ap.add_argument("--robots", type=int, default=16)
-    ap.add_argument("--mode", choices=["env"], default="env")
-    ap.add_argument("--cpu-envs", type=int, default=512)
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--precision", choices=["bf16", "f32"], default="bf16")
+    ap.add_argument("--mode", choices=["train", "env"], default="train")
+    ap.add_argument("--env-steps", type=int, default=100, help="extra env-only timed steps (0 = skip)")
+    ap.add_argument("--cpu-envs", type=int, default=2048)
     ap.add_argument("--cpu-steps", type=int, default=100)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--profile-kernel-events", action="store_true", default=True)
     return ap.parse_args()
 
 
@@ -63,65 +79,93 @@ def main():
         import torch.distributed as dist  # noqa: F811
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    from evacx.env import DeviceLayout, VecEnv
+    from evacx.env import DeviceLayout
     from evacx.layout import build_tables, synthetic
+    from evacx.trainer import VecTrainer, make_allreduce_hook
 
     L = W = args.grid
     P, R, E = args.people, args.robots, args.envs
     spec = synthetic(L, W, R)
     tables = build_tables(spec)
     lay = DeviceLayout(tables, P)
-    env = VecEnv(lay, E)
-    env.seed([1234 + rank * E + i for i in range(E)])
-    env.reset()
+    hook = make_allreduce_hook(dist, world) if dist is not None else None
+    tr = VecTrainer(lay, E, env_offset=rank * E, precision=args.precision, batch=args.batch, grad_hook=hook)
+    env = tr.env
 
-    gen = torch.Generator(device="cuda")
-    gen.manual_seed(1234 + rank)
-    nact = args.warmup + args.steps
-    actions = torch.randint(0, 5, (nact, E * R), generator=gen, device="cuda", dtype=torch.int32)
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
 
-    def step(i):
-        env.step(actions[i])
-        env.reset(mask=env.done)
+    def max_over_ranks(x):
+        if dist is None:
+            return x
+        t = torch.tensor([x], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
 
-    for i in range(args.warmup):
-        step(i)
-    torch.cuda.synchronize()
+    # ------------------------------------------------------------ warmup
+    for _ in range(args.warmup):
+        if args.mode == "train":
+            tr.step()
+        else:
+            env.step(torch.randint(0, 5, (E * R,), device="cuda", dtype=torch.int32))
+            env.reset(mask=env.done)
+    barrier()
 
-    # per-launch kernel time of the dominant kernel (env_step) on its own stream
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
+    # the CPU baseline continues from exactly this state (same envs, same episode phase)
+    cpu_snap = None
+    if rank == 0 and not args.no_cpu:
+        cpu_snap = [env.host_state(i) for i in range(min(args.cpu_envs, E))]
+
+    # ------------------------------------------------------- timed steps
+    ev_env = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    ev_learn = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    rand_actions = torch.randint(0, 5, (args.steps, E * R), device="cuda", dtype=torch.int32)
+    barrier()
     t0 = time.perf_counter()
     for s in range(args.steps):
-        a, b = ev[s]
-        a.record()
-        env.step(actions[args.warmup + s])
-        b.record()
-        env.reset(mask=env.done)
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
+        if args.mode == "train":
+            tr.act()
+            tr.obs_prev.copy_(env.obs)
+            ev_env[s][0].record()
+            env.step(tr.actions)
+            ev_env[s][1].record()
+            tr.replay.push(tr.obs_prev, env.obs, tr.actions, env.reward, env.done, tr.n_agents, R)
+            ev_learn[s][0].record()
+            tr.learn()
+            ev_learn[s][1].record()
+            env.reset(mask=env.done)
+            tr.t += 1
+        else:
+            ev_env[s][0].record()
+            env.step(rand_actions[s])
+            ev_env[s][1].record()
+            env.reset(mask=env.done)
+    barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0)
     env.check_err()
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    if dist is not None:
-        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_env]))
+    learn_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_learn])) if args.mode == "train" else None
+    loss = float(tr.last_loss.item()) if tr.last_loss is not None else None
 
-    env_steps = E * world * args.steps
-    value = env_steps / elapsed
+    # --------------------------------------------- env-only rate (extra)
+    env_only = None
+    if args.env_steps > 0 and args.mode == "train":
+        acts = torch.randint(0, 5, (args.env_steps, E * R), device="cuda", dtype=torch.int32)
+        barrier()
+        t1 = time.perf_counter()
+        for s in range(args.env_steps):
+            env.step(acts[s])
+            env.reset(mask=env.done)
+        barrier()
+        env_only = E * world * args.env_steps / max_over_ranks(time.perf_counter() - t1)
+
+    value = E * world * args.steps / elapsed
     G = (L + 2) * (W + 2)
     bpe = bytes_per_env_step(P, R, G)
     achieved = bpe * E / (kern_ms * 1e-3) / 1e9
-
-    cpu = None
-    if rank == 0 and not args.no_cpu:
-        cpu = cpu_baseline(env, tables, P, args, actions)
-
+    cpu = cpu_baseline(cpu_snap, env.lay.R, tables, P, args) if cpu_snap is not None else None
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -135,50 +179,65 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f64",
+            "dtype": "f64" if args.mode == "env" else f"f64 env + {args.precision} Q-net",
             "data": "synthetic",
-            "config": {"workload": f"cfg3 per-GPU share: {L}x{W} synthetic layout, {P} people, {R} robots, "
-                                   f"{E} envs/GPU, uniform random actions, auto-reset (env.step + reset)",
-                       "envs_per_gpu": E, "grid": f"{L}x{W}", "people": P, "robots": R, "mode": args.mode,
-                       "parallelism": f"envs sharded over {world} GPU(s), no collective in env mode"},
+            "config": {
+                "workload": (f"cfg3 per-GPU share: {L}x{W} synthetic layout, {P} people, {R} robots, {E} envs/GPU; "
+                             + ("full training step: act + env.step + replay push + learn (B="
+                                f"{args.batch}) + auto-reset" if args.mode == "train"
+                                else "env.step + auto-reset, uniform random actions")),
+                "envs_per_gpu": E, "grid": f"{L}x{W}", "people": P, "robots": R, "mode": args.mode,
+                "batch": args.batch, "qnet": "MLP 726-512-256-5",
+                "parallelism": f"data-parallel over {world} GPU(s): envs sharded, grad all-reduce (RCCL) per learn",
+            },
+            "env_only_steps_per_s": env_only,
+            "env_step_kernel_ms": kern_ms,
+            "learn_ms": learn_ms,
+            "last_loss": loss,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "env_step_kernel", "kernel_ms": kern_ms, "bytes_per_env_step": bpe},
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "env_step_kernel",
+                         "kernel_ms": kern_ms, "bytes_per_env_step": bpe, "env_steps_per_launch": E},
             "cpu_baseline": cpu,
         }
+        if learn_ms is not None:
+            fl = qnet_flops(0, args.batch)
+            line["roofline_learn"] = {"bound": "mfma", "achieved": fl / (learn_ms * 1e-3) / 1e12,
+                                      "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                      "frac": fl / (learn_ms * 1e-3) / 1e12 / BF16_PEAK_TFLOPS}
         print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()
 
 
-def cpu_baseline(env, tables, P, args, actions):
-    """Oracle (C restatement, OpenMP over envs) on the host cores, continuing from the
-    GPU's warmed-up state of the first cpu_envs envs with the same actions."""
+def cpu_baseline(snap, R, tables, P, args):
+    """Oracle (C restatement, OpenMP over envs) on the host cores, started from the GPU
+    state of the first cpu_envs envs at the beginning of the timed region (same episode
+    phase), stepped with uniform random actions."""
     try:
         from oracle import oracle as orc
     except Exception as e:  # oracle not built: report, never fall back
         return {"error": f"oracle unavailable: {e}"}
-    n = min(args.cpu_envs, env.E)
+    n = len(snap)
     olay = orc.Layout.from_tables(tables, P)
     envs = []
-    for i in range(n):
+    for st in snap:
         oe = orc.Env(olay, thmap=False)
-        oe.load_state(env.host_state(i))
+        oe.load_state(st)
         envs.append(oe)
     try:
         cores = len(os.sched_getaffinity(0))
     except AttributeError:
         cores = os.cpu_count() or 1
     cores = max(1, min(cores, 16))
-    R = env.lay.R
     steps = args.cpu_steps
-    acts = torch.randint(0, 5, (steps, n * R), dtype=torch.int32).numpy()
+    acts = np.random.RandomState(0).randint(0, 5, size=(steps, n * R)).astype(np.int32)
     t0 = time.perf_counter()
     done_steps, _ = orc.run_batch(olay, envs, steps, acts, nthreads=cores)
     dt = time.perf_counter() - t0
     return {"value": done_steps / dt, "unit": "env-steps/s", "cores": cores, "kind": "port",
-            "sample": f"{n} envs x {steps} steps of the same workload from the GPU's warmed-up state, "
-                      f"OpenMP {cores} threads, {dt:.2f}s wall"}
+            "sample": f"{n} envs x {steps} env.steps of the same workload from the GPU's warmed-up state "
+                      f"(env.step only, no learner), OpenMP {cores} threads, {dt:.2f}s wall, "
+                      f"{dt * cores:.1f} core-s"}
 
 
 if __name__ == "__main__":

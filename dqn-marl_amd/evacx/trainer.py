@@ -1,0 +1,143 @@
+"""Vectorised multi-agent DQN training loop, fully device-resident.
+
+One ``step()`` = for all E envs x R robots of this rank:
+  act      -- expand the compact observations, Q-forward (dropout active, as the
+              reference's act never leaves train mode), epsilon-greedy (evx_act)
+  env.step -- evx_env_step (the CA, bit-exact with the reference's step)
+  push     -- E*R transitions into the replay ring (team reward/done per env)
+  learn    -- sample B, online + target forwards, TD loss, backward, optional
+              gradient all-reduce (RCCL over xGMI when world > 1), clip + Adam
+  reset    -- auto-reset finished envs (reference reset semantics)
+
+Reference: runners/train_double_dqn.py:43-69 (independent robots, shared team
+reward) generalised to R robots and E envs; DQNAgent.act/remember/learn
+(agents/dqn_agent.py:97-168). No host syncs inside ``step()``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import torch
+
+from . import _lib
+from .env import OBS_WORDS, DeviceLayout, VecEnv, _stream
+from .qnet import Learner, qcheck, qlib
+
+
+class evx_replay(C.Structure):
+    _fields_ = [("capacity", C.c_int64), ("s", C.c_void_p), ("s2", C.c_void_p), ("a", C.c_void_p),
+                ("r", C.c_void_p), ("done", C.c_void_p)]
+
+
+class Replay:
+    """Uniform replay ring of compact observations in HBM."""
+
+    def __init__(self, capacity: int, device):
+        self.capacity = int(capacity)
+        i32 = dict(dtype=torch.int32, device=device)
+        self.s = torch.zeros(self.capacity * OBS_WORDS, **i32)
+        self.s2 = torch.zeros(self.capacity * OBS_WORDS, **i32)
+        self.a = torch.zeros(self.capacity, **i32)
+        self.r = torch.zeros(self.capacity, dtype=torch.float32, device=device)
+        self.done = torch.zeros(self.capacity, dtype=torch.uint8, device=device)
+        self.c = evx_replay(capacity=self.capacity, s=self.s.data_ptr(), s2=self.s2.data_ptr(), a=self.a.data_ptr(),
+                            r=self.r.data_ptr(), done=self.done.data_ptr())
+        self.pos = 0
+        self.size = 0
+
+    def push(self, s, s2, a, r_env, done_env, n, agents_per_env):
+        L = _lib.lib()
+        L.evx_replay_push.argtypes = [C.POINTER(evx_replay), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                      C.c_void_p, C.c_int32, C.c_int32, C.c_int64, C.c_void_p]
+        qcheck(L.evx_replay_push(C.byref(self.c), s.data_ptr(), s2.data_ptr(), a.data_ptr(), r_env.data_ptr(),
+                                 done_env.data_ptr(), n, agents_per_env, self.pos, _stream()), "replay_push")
+        self.pos = (self.pos + n) % self.capacity
+        self.size = min(self.capacity, self.size + n)
+
+    def sample(self, B, seed, offset, out):
+        L = _lib.lib()
+        L.evx_replay_sample.argtypes = [C.POINTER(evx_replay), C.c_int64, C.c_int32, C.c_uint64, C.c_uint64,
+                                        C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                        C.c_void_p]
+        qcheck(L.evx_replay_sample(C.byref(self.c), self.size, B, seed, offset, out["s"].data_ptr(),
+                                   out["s2"].data_ptr(), out["a"].data_ptr(), out["r"].data_ptr(),
+                                   out["done"].data_ptr(), None, _stream()), "replay_sample")
+
+
+class VecTrainer:
+    def __init__(self, layout: DeviceLayout, E: int, seed_base: int = 1234, env_offset: int = 0,
+                 kind: str = "mlp", precision: str = "bf16", batch: int = 4096, replay_capacity: int = 1 << 20,
+                 lr: float = 1e-4, gamma: float = 0.99, epsilon: float = 1.0, epsilon_min: float = 0.02,
+                 epsilon_decay: float = 0.9995, target_every: int = 1000, learner_seed: int = 0,
+                 grad_hook=None, learn_every: int = 1):
+        self.lay, self.E, self.R = layout, E, layout.R
+        self.device = layout.device
+        self.env = VecEnv(layout, E)
+        self.env.seed([seed_base + env_offset + i for i in range(E)])
+        self.env.reset()
+        self.learner = Learner(kind=kind, device=self.device, lr=lr, gamma=gamma, precision=precision,
+                               seed=learner_seed)
+        self.learner.grad_hook = grad_hook
+        self.replay = Replay(replay_capacity, self.device)
+        self.batch = batch
+        self.epsilon, self.epsilon_min, self.epsilon_decay = epsilon, epsilon_min, epsilon_decay
+        self.target_every, self.learn_every = target_every, learn_every
+        n = E * self.R
+        self.n_agents = n
+        self.obs_prev = torch.zeros(n * OBS_WORDS, dtype=torch.int32, device=self.device)
+        self.actions = torch.zeros(n, dtype=torch.int32, device=self.device)
+        self.samp = dict(s=torch.zeros(batch * OBS_WORDS, dtype=torch.int32, device=self.device),
+                         s2=torch.zeros(batch * OBS_WORDS, dtype=torch.int32, device=self.device),
+                         a=torch.zeros(batch, dtype=torch.int32, device=self.device),
+                         r=torch.zeros(batch, dtype=torch.float32, device=self.device),
+                         done=torch.zeros(batch, dtype=torch.uint8, device=self.device))
+        self.seed = learner_seed * 7919 + env_offset + 17
+        self.t = 0
+        self.learn_steps = 0
+        self.last_loss: Optional[torch.Tensor] = None
+
+    def act(self):
+        x = self.env.expand_obs(torch.float32)  # [E, R, 11, 11, 6]
+        Q = self.learner.q_values(x.view(self.n_agents, 11, 11, 6), train=True)
+        qcheck(qlib().evx_act(Q.data_ptr(), self.n_agents, self.learner.actions, float(self.epsilon), self.seed,
+                              self.t * self.n_agents, self.actions.data_ptr(), _stream()), "act")
+        return self.actions
+
+    def learn(self):
+        if self.replay.size < self.batch:
+            return None
+        self.replay.sample(self.batch, self.seed + 1, self.learn_steps * self.batch, self.samp)
+        s = self.env.expand_obs(torch.float32, self.samp["s"]).view(self.batch, 11, 11, 6)
+        s2 = self.env.expand_obs(torch.float32, self.samp["s2"]).view(self.batch, 11, 11, 6)
+        loss = self.learner.learn(s, self.samp["a"], self.samp["r"], self.samp["done"], s2)
+        self.learn_steps += 1
+        if self.epsilon > self.epsilon_min:  # DQNAgent.learn epsilon schedule (agents/dqn_agent.py:163-164)
+            self.epsilon *= self.epsilon_decay
+        if self.learn_steps % self.target_every == 0:
+            self.learner.sync_target()
+        return loss
+
+    def step(self):
+        self.act()
+        self.obs_prev.copy_(self.env.obs)
+        self.env.step(self.actions)
+        self.replay.push(self.obs_prev, self.env.obs, self.actions, self.env.reward, self.env.done,
+                         self.n_agents, self.R)
+        if self.t % self.learn_every == 0:
+            self.last_loss = self.learn()
+        self.env.reset(mask=self.env.done)
+        self.t += 1
+
+
+def make_allreduce_hook(dist, world: int):
+    """Average the flat gradient buffer over ranks (one collective per learn step)."""
+    backend = dist.get_backend()
+
+    def hook(flat):
+        if backend == "nccl":
+            dist.all_reduce(flat, op=dist.ReduceOp.AVG)
+        else:
+            dist.all_reduce(flat, op=dist.ReduceOp.SUM)
+            flat.div_(world)
+    return hook
