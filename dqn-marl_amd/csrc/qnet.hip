@@ -118,6 +118,130 @@ __global__ __launch_bounds__(256) void gemm_kernel(evx_gemm_desc g) {
     }
 }
 
+// ------------------------------------------------------------- GEMM, big tiles
+// 128x128x32 block tile, 4 waves as 2x2, each wave 64x64 = 2x2 MFMA 32x32 tiles (64 f32
+// accumulators per lane). The next K-tile is fetched into registers while the current
+// one is multiplied (register double buffering, one barrier pair per K-step). gridDim.z
+// splits K: partial sums are atomically added into a zeroed C (used for dW = dY^T X,
+// whose M x N grid alone cannot fill 256 CUs); epilogue ops require gridDim.z == 1.
+constexpr int TB = 128;
+template <typename TIn>
+__global__ __launch_bounds__(256) void gemm128_kernel(evx_gemm_desc g, int ksplit_len) {
+    constexpr int PADK = sizeof(TIn) == 4 ? 1 : 8;
+    __shared__ __attribute__((aligned(16))) TIn As[TB][BK + PADK];
+    __shared__ __attribute__((aligned(16))) TIn Bs[TB][BK + PADK];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = w >> 1, wn = w & 1;
+    const int m0 = blockIdx.y * TB, n0 = blockIdx.x * TB;
+    const int kb = blockIdx.z * ksplit_len, ke = min(g.K, kb + ksplit_len);
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int j = 0; j < 2; j++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc[i][j][r] = 0.f;
+    const bool a_kc = g.sak == 1, b_nc = g.sbn == 1;
+    float ra[16], rb[16];
+    auto fetch = [&](int k0) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const int idx = tid + 256 * i;
+            int mm, kk;
+            if (a_kc) { mm = idx >> 5; kk = idx & 31; } else { kk = idx >> 7; mm = idx & 127; }
+            const int gm = m0 + mm, gk = k0 + kk;
+            ra[i] = (gm < g.M && gk < ke) ? g.A[(int64_t)gm * g.sam + (int64_t)gk * g.sak] : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const int idx = tid + 256 * i;
+            int nn, kk;
+            if (b_nc) { kk = idx >> 7; nn = idx & 127; } else { nn = idx >> 5; kk = idx & 31; }
+            const int gn = n0 + nn, gk = k0 + kk;
+            rb[i] = (gn < g.N && gk < ke) ? g.B[(int64_t)gk * g.sbk + (int64_t)gn * g.sbn] : 0.f;
+        }
+    };
+    auto stash = [&]() {
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const int idx = tid + 256 * i;
+            int mm, kk;
+            if (a_kc) { mm = idx >> 5; kk = idx & 31; } else { kk = idx >> 7; mm = idx & 127; }
+            As[mm][kk] = to_in<TIn>(ra[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const int idx = tid + 256 * i;
+            int nn, kk;
+            if (b_nc) { kk = idx >> 7; nn = idx & 127; } else { nn = idx >> 5; kk = idx & 31; }
+            Bs[nn][kk] = to_in<TIn>(rb[i]);
+        }
+    };
+    if (kb < ke) fetch(kb);
+    for (int k0 = kb; k0 < ke; k0 += BK) {
+        stash();
+        __syncthreads();
+        if (k0 + BK < ke) fetch(k0 + BK);  // in flight during the MFMAs below
+        const int h = lane >> 5;
+#pragma unroll
+        for (int mi = 0; mi < 2; mi++) {
+            const int ar = wm * 64 + mi * 32 + (lane & 31);
+#pragma unroll
+            for (int ni = 0; ni < 2; ni++) {
+                const int br = wn * 64 + ni * 32 + (lane & 31);
+                if constexpr (sizeof(TIn) == 4) {
+#pragma unroll
+                    for (int kk = 0; kk < BK / 2; kk++)
+                        acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(As[ar][2 * kk + h], Bs[br][2 * kk + h],
+                                                                          acc[mi][ni], 0, 0, 0);
+                } else {
+#pragma unroll
+                    for (int s = 0; s < BK / 16; s++) {
+                        const bf16x8 a = *reinterpret_cast<const bf16x8*>(&As[ar][16 * s + 8 * h]);
+                        const bf16x8 b = *reinterpret_cast<const bf16x8*>(&Bs[br][16 * s + 8 * h]);
+                        acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[mi][ni], 0, 0, 0);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+    const bool split = gridDim.z > 1;
+#pragma unroll
+    for (int ni = 0; ni < 2; ni++) {
+        const int gn = n0 + wn * 64 + ni * 32 + (lane & 31);
+        if (gn >= g.N) continue;
+        const float bias = g.bias ? g.bias[gn] : 0.f;
+#pragma unroll
+        for (int mi = 0; mi < 2; mi++) {
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int gm = m0 + wm * 64 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                if (gm >= g.M) continue;
+                float* cp = g.C + (int64_t)gm * g.ldc + gn;
+                if (split) {
+                    atomicAdd(cp, g.alpha * acc[mi][ni][r]);
+                    continue;
+                }
+                float v = g.alpha * acc[mi][ni][r] + bias;
+                if (g.flags & EVX_GEMM_RELU) v = v > 0.f ? v : 0.f;
+                if (g.mask) v = g.mask[(int64_t)gm * g.ldm + gn] ? v * g.mask_scale : 0.f;
+                if (g.gate) v = g.gate[(int64_t)gm * g.ldg + gn] > 0.f ? v : 0.f;
+                if (g.flags & EVX_GEMM_ACCUM) v += *cp;
+                *cp = v;
+            }
+        }
+    }
+}
+
+// zero an f32 matrix C[M][ldc] (split-K target)
+__global__ __launch_bounds__(256) void zero_rows_kernel(float* __restrict__ C, int M, int N, int64_t ldc) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)M * N) return;
+    const int64_t m = i / N, n = i - m * N;
+    C[m * ldc + n] = 0.f;
+}
+
 // ------------------------------------------------------------- column sums
 // out[n] (+)= sum_m X[m*ld + n], deterministic: fixed-order partials then a fixed-order total.
 __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ X, int64_t ld, int M, int N,
@@ -391,12 +515,28 @@ const char* evx_q_last_error(void) { return q_err; }
 int evx_gemm(const evx_gemm_desc* g, void* stream) {
     if (!g || !g->A || !g->B || !g->C) return qfail(-22, "gemm: NULL operand");
     if (g->M <= 0 || g->N <= 0 || g->K <= 0) return 0;
-    dim3 grid((unsigned)((g->N + evxq::BN - 1) / evxq::BN), (unsigned)((g->M + evxq::BM - 1) / evxq::BM));
+    const int TB = evxq::TB;
+    const int tiles = ((g->M + TB - 1) / TB) * ((g->N + TB - 1) / TB);
+    const bool epi = g->bias || g->mask || g->gate || (g->flags & EVX_GEMM_RELU);
+    int S = 1;
+    // split K only on the bf16 path (f32 atomics reorder the sum; the f32 path stays deterministic)
+    if (!epi && g->precision == EVX_PREC_BF16 && tiles < 256 && g->K >= 512) {
+        S = (512 + tiles - 1) / tiles;
+        if (S > g->K / 256) S = g->K / 256;
+        if (S < 1) S = 1;
+    }
+    int klen = (g->K + S - 1) / S;
+    klen = (klen + evxq::BK - 1) / evxq::BK * evxq::BK;
+    S = (g->K + klen - 1) / klen;
+    dim3 grid((unsigned)((g->N + TB - 1) / TB), (unsigned)((g->M + TB - 1) / TB), (unsigned)S);
     if (grid.y > 65535u) return qfail(-22, "gemm: M too large for one launch");
+    if (S > 1 && !(g->flags & EVX_GEMM_ACCUM))
+        hipLaunchKernelGGL(evxq::zero_rows_kernel, dim3(nblk((int64_t)g->M * g->N)), dim3(256), 0,
+                           (hipStream_t)stream, g->C, g->M, g->N, g->ldc);
     if (g->precision == EVX_PREC_BF16)
-        hipLaunchKernelGGL(evxq::gemm_kernel<__bf16>, grid, dim3(256), 0, (hipStream_t)stream, *g);
+        hipLaunchKernelGGL(evxq::gemm128_kernel<__bf16>, grid, dim3(256), 0, (hipStream_t)stream, *g, klen);
     else
-        hipLaunchKernelGGL(evxq::gemm_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, *g);
+        hipLaunchKernelGGL(evxq::gemm128_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, *g, klen);
     return qlaunch("gemm");
 }
 
