@@ -1,13 +1,14 @@
 // MI355X (gfx950) evacuation cellular automaton: env reset / step / observation.
 //
-// One 512-thread workgroup (8 waves) owns one env instance for a whole step.
-// Persons are processed in rows of 512 (person p = row*512 + tid, so global
-// accesses are coalesced) by runtime loops (a small instruction footprint: the
-// kernel is latency-bound and must not thrash the instruction cache).
-// Per-person packed cell+flags, planned direction and first-planner index live
-// in LDS; health/acc stream from HBM once per step. The occupancy grid is an
-// LDS bitmap, the move-conflict table an LDS array of 16-bit entries, and the
-// two MT19937 streams LDS rings (evx_device.h).
+// Step: ONE WAVE (64 lanes, one workgroup) owns one env instance for a whole
+// step, so there is no workgroup barrier on the path: scans are ballots and
+// mbcnt, broadcasts are readlane/shuffles. Persons stream in rows of 64
+// (person p = row*64 + lane, coalesced); the next row's person words, health,
+// accumulator, danger, neighbour-validity mask and the 9 floor-field values
+// around each person are prefetched one row ahead, so a row's work is ALU + LDS
+// only. LDS per env (~22 KB at 130x130): occupancy bitmap, targeted /
+// contested / vacated bitmaps, the two MT19937 rings; everything
+// person-indexed stays in HBM.
 //
 // The step is the reference's EvacuationEnv.step (envs/evacuation_env.py:122-172)
 // and EvacuationEnvMulti.step (envs/evacuation_env_multi.py:55-89), evaluated
@@ -16,12 +17,18 @@
 //     parallel planners read exactly the words the sequential reference loop
 //     consumes (numpy stream: People.update_health envs/people.py:61-88;
 //     Python stream: People.find_best_direction envs/people.py:255-297);
-//   * move_plan's dict insertion order == the order of each target's FIRST
-//     planner, found by an LDS atomic-min per target cell;
-//   * random.shuffle runs only for contested targets, in that order, on lane 0;
+//   * a target cell is CONTESTED when a second planner sets its bit in the
+//     targeted bitmap. Only contested planners enter the conflict machinery:
+//     sorted by (target, person) they form move_plan's groups; each group's
+//     first planner is its dict insertion position (envs/people.py:284-297), so
+//     the groups sorted by first planner are shuffled (random.shuffle) on lane 0
+//     in exactly the reference's order;
 //   * execute_move's last-writer-wins on People.rmap (envs/people.py:299-314)
-//     becomes an atomic-max of (first-planner, sub-step) per touched cell.
-// f64 arithmetic is compiled with -ffp-contract=off (no FMA) to match CPython.
+//     only matters on cells that are both vacated and entered by winners; those
+//     few events are resolved by max (first planner, sub-step) in an LDS list.
+// The reward's order-sensitive sums are evaluated in the reference's order:
+// numpy's pairwise mean over streamed leaves, CPython's sequential health sum
+// on lane 0. f64 arithmetic is compiled with -ffp-contract=off (no FMA).
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -33,14 +40,23 @@
 
 namespace evx {
 
-constexpr int RING = 2048;          // MT ring (words), >= 1078
+constexpr int RING = 2048;          // MT ring of the reset kernel (words), >= 1078
 constexpr int RMASK = RING - 1;
-constexpr int WIN = RING - MT_GEN - 16;  // words per consumption window
-constexpr int GRP_CAP = 256;
-constexpr int PW_CAP = 256;         // pairwise-sum leaves
-constexpr uint32_t NIL16 = 0xffffu;
 constexpr int SHUF_CHUNK = 1024;
 constexpr uint32_t NODIR = 0xffu;
+
+// step kernel (one wave per env)
+constexpr int WR = 1024;             // MT ring words per stream (>= 624 + 227)
+constexpr int WRM = WR - 1;
+constexpr int WWIN = WR - 64 - 16;   // scoring words made readable per ensure
+constexpr int SHUF_WORDS = 384;      // words per lane-0 shuffle round (keeps mt_store_w's window valid)
+constexpr int CL_CAP = 1024;         // contested movers sorted in LDS (more: global scratch)
+constexpr int GH_CAP = 512;          // contested targets (groups) in LDS
+constexpr int EV_CAP = 256;          // order-sensitive occupancy events
+constexpr int LEAF_CAP = 256;        // numpy pairwise leaves (n <= 16383 needs <= 128)
+constexpr int GRP_MAX = 128;         // movers of one contested target
+constexpr int GBITS = 13;            // group index bits in a sorted group head
+constexpr uint32_t DONEPK = 3u << 24;
 
 struct Geo {
     int L, W, GY, G, RW, P, R;
@@ -90,6 +106,12 @@ __device__ __forceinline__ double person_speed(double h) {
     return 1.0 * (0.3 + 0.7 * (h / 100.0));
 }
 
+// Check_Valid, or (validb == nullptr) only its interior range test.
+__device__ __forceinline__ bool in_map(const Geo& g, const uint32_t* validb, int x, int y) {
+    if (validb) return check_valid(g, validb, x, y);
+    return x >= 1 && x <= g.L && y >= 1 && y <= g.W;
+}
+
 // Compact observation of one robot built by one wave (bits by ballot).
 __device__ __forceinline__ void write_obs(const Geo& g, const uint32_t* validb, const uint32_t* rmapb, int cx,
                                           int cy, int fs, evx_obs* dst) {
@@ -98,12 +120,12 @@ __device__ __forceinline__ void write_obs(const Geo& g, const uint32_t* validb, 
     {
         const int c = lane, i = c / 11, j = c % 11;
         const int mx = cx + i - 5, my = cy + j - 5;
-        if (check_valid(g, validb, mx, my)) b0 = bit_get(rmapb, mx * g.GY + my);
+        if (in_map(g, validb, mx, my)) b0 = bit_get(rmapb, mx * g.GY + my);
     }
     {
         const int c = lane + 64, i = c / 11, j = c % 11;
         const int mx = cx + i - 5, my = cy + j - 5;
-        if (c < 121 && check_valid(g, validb, mx, my)) b1 = bit_get(rmapb, mx * g.GY + my);
+        if (c < 121 && in_map(g, validb, mx, my)) b1 = bit_get(rmapb, mx * g.GY + my);
     }
     const unsigned long long m0 = __ballot(b0), m1 = __ballot(b1);
     if (lane == 0) {
@@ -131,116 +153,291 @@ __device__ __forceinline__ void mt_load(uint32_t* ring, const uint32_t* gst, int
     head = (int)gst[MT_N];
 }
 
-struct StepLds {  // word offsets into dynamic LDS
-    int region, pyring, npring, claim, distbuf, hbuf, pwsum;
-    int pk, dir, pf, lhead, lnext, confl, rmapb, validb, grp, robots, wsum, dsum, ctrl, total;
+// ===================================================== step: one wave per env
+// Ordering inside one wave: LDS instructions of a wave execute in issue order,
+// so lane-to-lane LDS hand-offs only need the compiler not to reorder them.
+__device__ __forceinline__ void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront"); }
+
+__device__ __forceinline__ int lanes_below(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Extend the raw MT sequence in a WR-word ring until front >= upto. A batch of
+// up to 227 words depends only on older words (x[n-227], x[n-624], x[n-623]).
+__device__ __forceinline__ void mt_ensure_w(uint32_t* ring, int& front, int upto) {
+    const int lane = threadIdx.x;
+    while (front < upto) {
+        const int cnt = min(MT_LAG, upto - front);
+        for (int t = lane; t < cnt; t += 64) {
+            const int n = front + t;
+            ring[n & WRM] = mt_twist1(ring[(n - MT_LAG) & WRM], ring[(n - 624) & WRM], ring[(n - 623) & WRM]);
+        }
+        front += cnt;
+        wave_fence();
+    }
+}
+
+// Store the state after consuming up to raw index `head` (CPython index
+// semantics). Needs front <= head + 400 so [b, b+624) is still in the ring.
+__device__ __forceinline__ void mt_store_w(uint32_t* ring, int& front, int head, uint32_t* gst) {
+    const int lane = threadIdx.x;
+    if (head <= MT_N) {
+        if (lane == 0) gst[MT_N] = (uint32_t)head;  // no twist: words unchanged
+        return;
+    }
+    const int b = MT_N * ((head - 1) / MT_N);
+    mt_ensure_w(ring, front, b + MT_N);
+    for (int i = lane; i < MT_N; i += 64) gst[i] = ring[(b + i) & WRM];
+    if (lane == 0) gst[MT_N] = (uint32_t)(head - b);
+}
+
+__device__ __forceinline__ void mt_load_w(uint32_t* ring, const uint32_t* gst, int& head) {
+    for (int i = threadIdx.x; i < MT_N; i += 64) ring[i] = gst[i];
+    head = (int)gst[MT_N];
+    wave_fence();
+}
+
+// Ascending bitonic sort of a[0..n), n a power of two, by one wave.
+template <typename T>
+__device__ __forceinline__ void wave_sort(T* a, int n) {
+    const int lane = threadIdx.x;
+    for (int k = 2; k <= n; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int q = lane; q < (n >> 1); q += 64) {
+                const int i = ((q & ~(j - 1)) << 1) | (q & (j - 1));
+                const int l = i | j;
+                const uint32_t x = a[i], y = a[l];
+                if ((x > y) == ((i & k) == 0)) {
+                    a[i] = y;
+                    a[l] = x;
+                }
+            }
+            __syncthreads();  // one wave: waits for its own LDS / memory traffic
+        }
+}
+
+__host__ __device__ __forceinline__ int pow2_ceil(int n) {
+    int m = 1;
+    while (m < n) m <<= 1;
+    return m;
+}
+
+// Contested targets of move_plan (envs/people.py:284-297): L[0..n) holds
+// (target << pb | person) of every planner whose target has >= 2 planners.
+// Sort -> groups (one per target, movers in person order); group heads sorted
+// by first planner = dict insertion order; lane 0 runs Lib/random.py shuffle
+// per group on the Python stream and marks the losers.
+__device__ __forceinline__ int doff_of(uint32_t d, int GY) { return move_dx((int)d) * GY + move_dy((int)d); }
+
+template <typename T>
+__device__ __forceinline__ void contested_groups(T* Lp, T* heads, T* gstart, int n, int pb, uint32_t* pyring, int& py_front,
+                                 int& py_head, uint32_t* lost, uint32_t* grp, int& err) {
+    const int lane = threadIdx.x;
+    const uint32_t pmask = (1u << pb) - 1u;
+    const int n2 = pow2_ceil(n);
+    for (int i = n + lane; i < n2; i += 64) Lp[i] = 0xffffffffu;
+    __syncthreads();
+    wave_sort(Lp, n2);
+    int ngrp = 0;
+    for (int i0 = 0; i0 < n; i0 += 64) {
+        const int i = i0 + lane;
+        bool st = false;
+        uint32_t key = 0;
+        if (i < n) {
+            key = Lp[i];
+            st = (i == 0) || ((Lp[i - 1] >> pb) != (key >> pb));
+        }
+        const unsigned long long m = __ballot(st);
+        if (st) {
+            const int gi = ngrp + lanes_below(m);
+            gstart[gi] = (uint32_t)i;
+            heads[gi] = ((key & pmask) << GBITS) | (uint32_t)gi;
+        }
+        ngrp += __popcll(m);
+    }
+    if (lane == 0) gstart[ngrp] = (uint32_t)n;
+    const int h2 = pow2_ceil(ngrp);
+    for (int i = ngrp + lane; i < h2; i += 64) heads[i] = 0xffffffffu;
+    __syncthreads();
+    wave_sort(heads, h2);
+    int k = 0;
+    while (k < ngrp) {
+        mt_ensure_w(pyring, py_front, py_head + SHUF_WORDS);
+        __syncthreads();
+        int nk = k, nh = py_head, bad = 0;
+        if (lane == 0) {
+            const int avail = py_front;
+            while (nk < ngrp) {
+                const int gi = (int)(heads[nk] & ((1u << GBITS) - 1u));
+                const int s = (int)gstart[gi], cnt = (int)gstart[gi + 1] - s;
+                if (cnt > GRP_MAX) {  // > 128 movers on one target: not representable, flagged
+                    bad |= 1;
+                    nk++;
+                    continue;
+                }
+                for (int j = 0; j < cnt; j++) grp[j] = Lp[s + j] & pmask;
+                int head = nh;
+                bool ok = true;
+                for (int i = cnt - 1; i >= 1 && ok; i--) {  // random.shuffle: _randbelow(i + 1)
+                    const uint32_t bound = (uint32_t)(i + 1);
+                    const int kb = bit_length(bound);
+                    uint32_t r;
+                    do {
+                        if (head >= avail) {
+                            ok = false;
+                            break;
+                        }
+                        r = mt_word(pyring, WRM, head++) >> (32 - kb);
+                    } while (r >= bound);
+                    if (ok) {
+                        const uint32_t t = grp[i];
+                        grp[i] = grp[r];
+                        grp[r] = t;
+                    }
+                }
+                if (!ok) break;  // out of words: retry this group next round
+                nh = head;
+                for (int j = 1; j < cnt; j++) lost[grp[j] >> 5] |= 1u << (grp[j] & 31);
+                nk++;
+            }
+        }
+        nk = __shfl(nk, 0);
+        nh = __shfl(nh, 0);
+        err |= __shfl(bad, 0);
+        __syncthreads();
+        if (nk == k) {  // a group needs more than SHUF_WORDS words (practically impossible)
+            err |= 2;
+            break;
+        }
+        k = nk;
+        py_head = nh;
+    }
+}
+
+// First planner of contested target t (the group's smallest person index).
+__device__ __forceinline__ int find_pf(const uint32_t* Lp, int n, int t, int pb) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if ((int)(Lp[mid] >> pb) < t) lo = mid + 1;
+        else hi = mid;
+    }
+    return (int)(Lp[lo] & ((1u << pb) - 1u));
+}
+
+struct WaveLds {  // word offsets into dynamic LDS
+    int pyring, npring, aux, rmapb, tbits, cbits, obits, lost, robots, misc, total;
 };
 
-__host__ __device__ inline StepLds step_lds(int G, int P, int R) {
-    StepLds s;
+__host__ __device__ inline WaveLds wave_lds(int G, int P, int R) {
+    WaveLds s;
     const int RW = (G + 31) / 32;
-    const int CW = (G + 1) / 2;
-    // region: rows -> [py ring][np ring]; claims..execute -> [py ring][claim];
-    //         reward -> [distbuf P doubles][hbuf P doubles][leaf sums]
-    int a = RING + (CW > RING ? CW : RING);
-    const int P4 = (2 * P + 3) & ~3;  // 16-B aligned double arrays
-    const int b = 2 * P4 + 2 * PW_CAP;
-    if (a < b) a = b;
-    a = (a + 3) & ~3;
     int o = 0;
-    s.region = o;
-    s.pyring = o;
-    s.npring = o + RING;
-    s.claim = o + RING;
-    s.distbuf = o;
-    s.hbuf = o + P4;
-    s.pwsum = o + 2 * P4;
-    o += a;
-    s.pk = o; o += P;
-    s.dir = o; o += (P + 3) / 4;
-    s.pf = o; o += (P + 1) / 2;
-    s.lhead = o; o += (P + 1) / 2;
-    s.lnext = o; o += (P + 1) / 2;
-    s.confl = o; o += (P + 31) / 32;
+    s.pyring = o; o += WR;                 // reward phase: leaf sums | leaf buffer
+    s.npring = o; o += WR;                 // after the rows: contested list (CL_CAP)
+    s.aux = o; o += 2 * GH_CAP + 16;       // group heads | group starts; events; leaf table
     s.rmapb = o; o += RW;
-    s.validb = o; o += RW;
-    s.grp = o; o += GRP_CAP;
+    s.tbits = o; o += RW;
+    s.cbits = o; o += RW;
+    s.obits = o; o += RW;                  // near-robot cells while planning, vacated cells after
+    s.lost = o; o += (P + 31) / 32;
     s.robots = o; o += R;
     o = (o + 1) & ~1;
-    s.wsum = o; o += NWAVE;
-    o = (o + 1) & ~1;
-    s.dsum = o; o += 2 * NWAVE + 8;
-    s.ctrl = o; o += 16;
+    s.misc = o; o += GRP_MAX + 16;         // shuffle group; event counter; pairwise stacks
     s.total = (o + 3) & ~3;
     return s;
 }
 
-// Diagnostic phase stamps (evx_step_out.stamps; off when NULL).
+// per env: move plan [P] uint2 | not-dead list [P] uint2 | spill: contested list,
+// group heads, group starts (each a power of two >= P)
+__host__ __device__ inline int64_t wave_scratch_words(int P) {
+    const int n2 = pow2_ceil(P < 64 ? 64 : P);
+    return ((int64_t)4 * P + 3 * (int64_t)n2 + 2 + 1) & ~(int64_t)1;
+}
+
+__device__ __forceinline__ int pb_bits(int P) { return P > 1 ? bit_length((uint32_t)(P - 1)) : 1; }
+
+// Diagnostic phase stamps (evx_step_out.stamps; off when NULL): slots 0-8 shader
+// clock, 9/10 constant-rate clock at start/end, 11-14 counters.
 #define EVX_STAMP(i)                                                                                   \
     do {                                                                                               \
         if (out.stamps && threadIdx.x == 0)                                                            \
             out.stamps[(size_t)blockIdx.x * 16 + (i)] = (int64_t)__builtin_amdgcn_s_memtime();         \
+    } while (0)
+#define EVX_RSTAMP(i)                                                                                  \
+    do {                                                                                               \
+        if (out.stamps && threadIdx.x == 0)                                                            \
+            out.stamps[(size_t)blockIdx.x * 16 + (i)] = (int64_t)__builtin_amdgcn_s_memrealtime();     \
     } while (0)
 #define EVX_COUNT(i, v)                                                                                \
     do {                                                                                               \
         if (out.stamps && threadIdx.x == 0) out.stamps[(size_t)blockIdx.x * 16 + (i)] = (v);           \
     } while (0)
 
-__global__ __launch_bounds__(NT, 4) void env_step_kernel(evx_layout lay, evx_state st,
-                                                         const int32_t* __restrict__ actions, evx_step_out out) {
+__device__ __forceinline__ double readlane_d(double v, int k) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), k);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), k);
+    return __hiloint2double(hi, lo);
+}
+
+__global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state st, const int32_t* __restrict__ actions,
+                                                      evx_step_out out) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const int e = blockIdx.x;
-    const int tid = threadIdx.x;
+    const int lane = threadIdx.x;
+    EVX_RSTAMP(9);
     EVX_STAMP(0);
     Geo g;
     g.L = lay.L; g.W = lay.W; g.GY = lay.W + 2; g.G = (lay.L + 2) * (lay.W + 2);
     g.RW = (g.G + 31) / 32; g.P = lay.P; g.R = lay.R;
-    const int P = g.P, R = g.R;
-    const int NROW = (P + NT - 1) / NT;
-    const StepLds S = step_lds(g.G, P, R);
+    const int P = g.P, R = g.R, GY = g.GY;
+    const int NR = (P + 63) >> 6;
+    const int pb = pb_bits(P);
+    const WaveLds S = wave_lds(g.G, P, R);
     uint32_t* pyring = smem + S.pyring;
     uint32_t* npring = smem + S.npring;
-    uint32_t* claim = smem + S.claim;
-    uint32_t* pkL = smem + S.pk;
-    uint8_t* dirL = reinterpret_cast<uint8_t*>(smem + S.dir);
-    uint16_t* pfL = reinterpret_cast<uint16_t*>(smem + S.pf);
-    uint32_t* lhead = smem + S.lhead;  // 16-bit entries
-    uint16_t* lnext = reinterpret_cast<uint16_t*>(smem + S.lnext);
-    uint32_t* confl = smem + S.confl;
+    uint32_t* aux = smem + S.aux;
     uint32_t* rmapb = smem + S.rmapb;
-    uint32_t* validb = smem + S.validb;
-    int* grp = reinterpret_cast<int*>(smem + S.grp);
+    uint32_t* tbits = smem + S.tbits;
+    uint32_t* cbits = smem + S.cbits;
+    uint32_t* obits = smem + S.obits;
+    uint32_t* lost = smem + S.lost;
     uint32_t* robots = smem + S.robots;
-    int* wsum = reinterpret_cast<int*>(smem + S.wsum);
-    double* dsum = reinterpret_cast<double*>(smem + S.dsum);
-    int* ctrl = reinterpret_cast<int*>(smem + S.ctrl);
-    double* distbuf = reinterpret_cast<double*>(smem + S.distbuf);
-    double* hbuf = reinterpret_cast<double*>(smem + S.hbuf);
-    double* pwsum = reinterpret_cast<double*>(smem + S.pwsum);
+    uint32_t* misc = smem + S.misc;
+    const uint32_t* __restrict__ validg = lay.valid_bits;
 
     uint32_t* pk_g = st.pk + (size_t)e * P;
     double* h_g = st.health + (size_t)e * P;
     double* a_g = st.acc + (size_t)e * P;
+    const int64_t SW = wave_scratch_words(P);
+    uint32_t* scr = st.scratch + (size_t)e * SW;
+    uint2* plan = reinterpret_cast<uint2*>(scr);           // (person, cell | dir << 24) of every mover
+    uint2* ndl = reinterpret_cast<uint2*>(scr + 2 * P);    // (person, person word) of the not-dead
+    const int n2P = pow2_ceil(P < 64 ? 64 : P);
+    uint32_t* Lg = scr + 4 * P;                             // spill: contested list
+    uint32_t* Hg = Lg + n2P;                                // spill: group heads
+    uint32_t* Sg = Hg + n2P;                                // spill: group starts
 
     // ---------------------------------------------------------------- load
-    for (int i = tid; i < g.RW; i += NT) {
-        rmapb[i] = st.rmap[(size_t)e * g.RW + i];
-        validb[i] = lay.valid_bits[i];
-    }
-    for (int p = tid; p < P; p += NT) pkL[p] = pk_g[p];
-    for (int i = tid; i < (P + 1) / 2; i += NT) lhead[i] = 0xffffffffu;
-    for (int i = tid; i < (P + 31) / 32; i += NT) confl[i] = 0;
-    int py_head, np_head;
-    mt_load(pyring, st.py_mt + (size_t)e * EVX_MT_WORDS, py_head);
-    mt_load(npring, st.np_mt + (size_t)e * EVX_MT_WORDS, np_head);
-    int py_front = MT_N, np_front = MT_N;
     const int* scal_g = st.scal + (size_t)e * 4;
     const int fs = scal_g[0], cur_step = scal_g[1], prev_evac = scal_g[2], prev_dead = scal_g[3];
     uint32_t view = st.view[e];
+    for (int i = lane; i < g.RW; i += 64) {
+        rmapb[i] = st.rmap[(size_t)e * g.RW + i];
+        tbits[i] = 0;
+        cbits[i] = 0;
+        obits[i] = 0;
+    }
+    for (int i = lane; i < (P + 31) / 32; i += 64) lost[i] = 0;
+    int py_head, np_head;
+    mt_load_w(pyring, st.py_mt + (size_t)e * EVX_MT_WORDS, py_head);
+    mt_load_w(npring, st.np_mt + (size_t)e * EVX_MT_WORDS, np_head);
+    int py_front = MT_N, np_front = MT_N;
     // Map.move_robot for every robot (envs/map.py:160-201); robots never interact.
-    if (tid < R) {
-        uint32_t rp = st.robots[(size_t)e * R + tid];
-        const int a = actions[(size_t)e * R + tid];
+    bool valid_a0 = false;
+    for (int r = lane; r < R; r += 64) {
+        uint32_t rp = st.robots[(size_t)e * R + r];
+        const int a = actions[(size_t)e * R + r];
         if (a >= 0 && a <= 4) {
             const int x = rp_x(rp), y = rp_y(rp);
             int nx = x, ny = y;
@@ -248,50 +445,227 @@ __global__ __launch_bounds__(NT, 4) void env_step_kernel(evx_layout lay, evx_sta
             else if (a == 1) ny = y - 1;
             else if (a == 2) nx = x - 1;
             else if (a == 3) ny = y + 1;
-            const int c = nx * g.GY + ny;
+            const int c = nx * GY + ny;
             if (lay.rx_lo <= nx && nx <= lay.rx_hi && 0 <= ny && ny <= g.W && nx >= 1 && nx <= g.L && ny >= 1 &&
-                ny <= g.W && ((lay.valid_bits[c >> 5] >> (c & 31)) & 1u))
+                ny <= g.W && ((validg[c >> 5] >> (c & 31)) & 1u))
                 rp = rp_pack(nx, ny);
         }
-        robots[tid] = rp;
-        st.robots[(size_t)e * R + tid] = rp;
-        if (tid == 0) ctrl[0] = (a >= 0 && a <= 4) ? 1 : 0;
+        robots[r] = rp;
+        st.robots[(size_t)e * R + r] = rp;
+        if (r == 0) valid_a0 = (a >= 0 && a <= 4);
     }
-    __syncthreads();
-    if (ctrl[0]) view = robots[0];  // robot_position refreshed only after a valid action
-    EVX_STAMP(1);
-
-    // --------------------- People.run phases 1+2 (health, accumulate, plan)
-    const double* dpt = lay.danger_p + (size_t)fs * g.G;
-    for (int row = 0; row < NROW; row++) {
-        const int p = row * NT + tid;
-        const bool inr = p < P;
-        uint32_t v = inr ? pkL[p] : (3u << 24);
-        const bool act = !((v >> 24) & 3u);
-        double hh = 0.0, ac = 0.0, dg = 0.0;
-        const int x = pk_x(v), y = pk_y(v);
-        if (act) {
-            hh = h_g[p];
-            ac = a_g[p];
-            dg = dpt[x * g.GY + y];
+    // the not-dead persons in person order (sum(... if not p.dead) and the movers
+    // never look at anyone else)
+    int nnd = 0, n_safe = 0;
+    for (int r0 = 0; r0 < NR; r0 += 12) {  // 12 rows of loads in flight
+        uint32_t vv[12];
+#pragma unroll
+        for (int j = 0; j < 12; j++) {
+            const int p = (r0 + j) * 64 + lane;
+            vv[j] = 2u << 24;
+            if (p < P) vv[j] = pk_g[p];
         }
-        // phase 1: Person.update_state -> update_health (numpy stream)
-        const bool need = act && dg > 0;
-        int tot;
-        const int off = block_exscan(need ? 2 : 0, wsum, tot);
-        bool alive = act;
-        for (int lo = 0; lo < tot; lo += WIN) {  // windowed: rows may need more words than the ring
-            mt_ensure(npring, RMASK, np_front, np_head + min(tot, lo + WIN));
-            if (need && off >= lo && off < lo + WIN) {
-                const double u = mt_double(npring, RMASK, np_head + off);
-                if (update_health(hh, dg, u)) {
-                    v |= (2u << 24);
-                    alive = false;
+#pragma unroll
+        for (int j = 0; j < 12; j++) {
+            const int p = (r0 + j) * 64 + lane;
+            const bool nd = !pk_dead(vv[j]);
+            const unsigned long long m = __ballot(nd);
+            if (nd) ndl[nnd + lanes_below(m)] = make_uint2((uint32_t)p, vv[j]);
+            nnd += __popcll(m);
+            n_safe += __popcll(__ballot(nd && pk_safe(vv[j])));
+        }
+    }
+    wave_fence();
+    if (__shfl((int)valid_a0, 0)) view = robots[0];  // robot_position refreshed only after a valid action
+    // cells within repel range of some robot (d^2 < repel_d2): the only place the
+    // per-robot distance loop can change a score (People.find_best_direction)
+    const int rd2 = lay.repel_d2;
+    if (rd2 > 0) {
+        int rr = 0;
+        while ((rr + 1) * (rr + 1) < rd2) rr++;
+        const int side = 2 * rr + 1, win = side * side;
+        const float inv_side = 1.0f / (float)side;
+        for (int r = 0; r < R; r++) {
+            const uint32_t rp = robots[r];
+            for (int c = lane; c < win; c += 64) {
+                const int q = (int)(((float)c + 0.5f) * inv_side);  // c / side, exact for c < 2^20
+                const int dx = q - rr, dy = c - q * side - rr;
+                const int x = rp_x(rp) + dx, y = rp_y(rp) + dy;
+                if (dx * dx + dy * dy < rd2 && x >= 0 && x <= g.L + 1 && y >= 0 && y <= g.W + 1) {
+                    const int cc = x * GY + y;
+                    atomicOr(&obits[cc >> 5], 1u << (cc & 31));
                 }
             }
         }
-        np_head += tot;
-        // phase 2: accumulate; plan with find_best_direction (Python stream)
+    }
+    __syncthreads();  // not-dead list and LDS tables complete
+    EVX_STAMP(1);
+
+    // --------------------- People.run phases 1+2 (health, accumulate, plan)
+    const double* __restrict__ dpt = lay.danger_p + (size_t)fs * g.G;
+    const double* __restrict__ flo = lay.floor;
+    const uint8_t* __restrict__ nbv = lay.nbr_valid;
+    int doff[8];
+#pragma unroll
+    for (int d = 0; d < 8; d++) doff[d] = move_dx(d) * GY + move_dy(d);
+
+    // one-row-ahead prefetch of what a row reads from HBM
+    const uint2 NOONE = make_uint2(0u, DONEPK);
+    uint2 eN = NOONE, eNN = NOONE;
+    if (lane < nnd) eN = ndl[lane];
+    if (64 + lane < nnd) eNN = ndl[64 + lane];
+    double hN = 0.0, aN = 0.0, dN = 0.0;
+    uint32_t nvN = 0;
+    if (lane < nnd) {
+        hN = h_g[eN.x];
+        if (!((eN.y >> 24) & 3u)) {
+            const int c = pk_x(eN.y) * GY + pk_y(eN.y);
+            aN = a_g[eN.x];
+            dN = dpt[c];
+            nvN = nbv[c];
+        }
+    }
+    const int NRD = (nnd + 63) >> 6;
+    int nplan = 0, n_died = 0;
+    bool any_cont = false;
+    double total = 0.0;  // CPython sum(p.health for p in self.people.list if not p.dead): sequential
+    double* hc = reinterpret_cast<double*>(aux + 384);  // one row of not-dead healths (lane 0 sums them)
+    // Planners wait in an LDS queue and are scored 64 at a time (scoring is the
+    // heavy part and only a few persons per row plan).
+    uint32_t* qa = aux;        // person | candidate mask << 16
+    uint32_t* qb = aux + 128;  // x | y << 12
+    int* qc = reinterpret_cast<int*>(aux + 256);  // first Python-stream word
+    int qn = 0;
+    auto score_batch = [&](int n) {  // People.find_best_direction for queue entries [0, n)
+        const bool has = lane < n;
+        uint32_t ea = 0, eb = 0;
+        int off = 0;
+        if (has) {
+            ea = qa[lane];
+            eb = qb[lane];
+            off = qc[lane];
+        }
+        const int p = (int)(ea & 0xffffu);
+        const uint32_t cand = ea >> 16;
+        const int x = pk_x(eb), y = pk_y(eb), cold = x * GY + y;
+        double f0 = 0.0, f[8];
+#pragma unroll
+        for (int d = 0; d < 8; d++) f[d] = 0.0;
+        if (has) {
+            f0 = flo[cold];
+#pragma unroll
+            for (int d = 0; d < 8; d++)
+                if ((cand >> d) & 1u) f[d] = flo[cold + doff[d]];
+        }
+        const int first = __builtin_amdgcn_readfirstlane(off);
+        const int end = __builtin_amdgcn_readlane(off + 2 * __popc(cand), n - 1);
+        uint32_t best = NODIR;
+        for (int lo = first; lo < end; lo += WWIN) {  // windowed: a batch may need more words than the ring
+            mt_ensure_w(pyring, py_front, min(end, lo + WWIN + 16));
+            if (has && off >= lo && off < lo + WWIN) {
+                double maxs = -INFINITY;
+                int idx = off;
+#pragma unroll
+                for (int d = 0; d < 8; d++) {
+                    if ((cand >> d) & 1u) {
+                        const int nc = cold + doff[d];
+                        const double delta_p = f0 - f[d];
+                        double effect = 0.0;
+                        if (bit_get(obits, nc)) {
+                            const int nx = x + move_dx(d), ny = y + move_dy(d);
+                            int md2 = 0x7fffffff;
+                            for (int r = 0; r < R; r++) {
+                                const uint32_t rp = robots[r];
+                                const int dx = nx - rp_x(rp), dy = ny - rp_y(rp);
+                                const int d2 = dx * dx + dy * dy;
+                                md2 = d2 < md2 ? d2 : md2;
+                            }
+                            if (md2 < rd2) effect = lay.repel_k / (sqrt((double)md2) + 0.1);
+                        }
+                        const double u = -0.1 + (0.1 - -0.1) * mt_double(pyring, WRM, idx);
+                        idx += 2;
+                        const double score = delta_p * 5.0 + effect + u;
+                        if (score > maxs) {
+                            maxs = score;
+                            best = (uint32_t)d;
+                        }
+                    }
+                }
+            }
+        }
+        const bool mover = best != NODIR;
+        const unsigned long long mm = __ballot(mover);
+        if (mover) {
+            const int t = cold + doff_of(best, GY);
+            const uint32_t bit = 1u << (t & 31);
+            const uint32_t old = atomicOr(&tbits[t >> 5], bit);
+            if (old & bit) {
+                atomicOr(&cbits[t >> 5], bit);
+                any_cont = true;
+            }
+            plan[nplan + lanes_below(mm)] = make_uint2((uint32_t)p, (uint32_t)cold | (best << 24));
+        }
+        nplan += __popcll(mm);
+    };
+    for (int row = 0; row < NRD; row++) {
+        const int i = row * 64 + lane;
+        const bool inr = i < nnd;
+        const int p = (int)eN.x;
+        const uint32_t v = eN.y;
+        double hh = hN, ac = aN;
+        const double dg = dN;
+        const uint32_t nv = nvN;
+        // issue the next row's loads
+        eN = eNN;
+        if (i + 64 < nnd) {
+            hN = h_g[eN.x];
+            if (!((eN.y >> 24) & 3u)) {
+                const int c = pk_x(eN.y) * GY + pk_y(eN.y);
+                aN = a_g[eN.x];
+                dN = dpt[c];
+                nvN = nbv[c];
+            }
+        }
+        eNN = NOONE;
+        if (i + 128 < nnd) eNN = ndl[i + 128];
+
+        const bool act = inr && !((v >> 24) & 3u);
+        const int x = pk_x(v), y = pk_y(v), cold = x * GY + y;
+        // phase 1: Person.update_state -> update_health (numpy stream)
+        const bool need = act && dg > 0;
+        const unsigned long long nm = __ballot(need);
+        const int tot = 2 * __popcll(nm);
+        bool alive = act, died = false;
+        if (tot) {
+            mt_ensure_w(npring, np_front, np_head + tot);
+            if (need) {
+                const double u = mt_double(npring, WRM, np_head + 2 * lanes_below(nm));
+                if (update_health(hh, dg, u)) {
+                    died = true;
+                    alive = false;
+                }
+            }
+            np_head += tot;
+        }
+        n_died += __popcll(__ballot(died));
+        {  // health total over the still-not-dead, in person order (lane 0)
+            const unsigned long long hm = __ballot(inr && !died);
+            if (inr && !died) hc[lanes_below(hm)] = hh;
+            wave_fence();
+            if (lane == 0) {
+                const int nh = __popcll(hm);
+                const double2* h2 = reinterpret_cast<const double2*>(hc);
+                int k = 0;
+                for (; k + 8 <= nh; k += 8) {
+                    const double2 a0 = h2[k / 2], a1 = h2[k / 2 + 1], a2 = h2[k / 2 + 2], a3 = h2[k / 2 + 3];
+                    total += a0.x; total += a0.y; total += a1.x; total += a1.y;
+                    total += a2.x; total += a2.y; total += a3.x; total += a3.y;
+                }
+                for (; k < nh; k++) total += hc[k];
+            }
+            wave_fence();
+        }
+        // phase 2: accumulate; candidates of find_best_direction
         bool planner = false;
         if (alive) {
             ac += person_speed(hh) * 0.5;
@@ -300,265 +674,237 @@ __global__ __launch_bounds__(NT, 4) void env_step_kernel(evx_layout lay, evx_sta
                 planner = true;
             }
         }
-        int cand = 0, ncand = 0;
+        uint32_t cand = 0;
         if (planner) {
-            for (int d = 0; d < 8; d++) {
-                const int nx = x + move_dx(d), ny = y + move_dy(d);
-                if (check_valid(g, validb, nx, ny) && !bit_get(rmapb, nx * g.GY + ny)) {
-                    cand |= 1 << d;
-                    ncand++;
-                }
-            }
+            uint32_t occ = 0;
+#pragma unroll
+            for (int d = 0; d < 8; d++) occ |= (uint32_t)bit_get(rmapb, cold + doff[d]) << d;
+            cand = nv & ~occ;
         }
-        int tot2;
-        const int off2 = block_exscan(2 * ncand, wsum, tot2);
-        uint32_t best = NODIR;
-        for (int lo = 0; lo < tot2; lo += WIN) {
-            mt_ensure(pyring, RMASK, py_front, py_head + min(tot2, lo + WIN) + 16);
-            if (ncand && off2 >= lo && off2 < lo + WIN) {
-                const double fxy = lay.floor[x * g.GY + y];
-                double maxs = -INFINITY;
-                int idx = py_head + off2;
-                for (int d = 0; d < 8; d++) {
-                    if (!((cand >> d) & 1)) continue;
-                    const int nx = x + move_dx(d), ny = y + move_dy(d);
-                    const double delta_p = fxy - lay.floor[nx * g.GY + ny];
-                    int md2 = 0x7fffffff;
-                    for (int r = 0; r < R; r++) {
-                        const uint32_t rp = robots[r];
-                        const int dx = nx - rp_x(rp), dy = ny - rp_y(rp);
-                        const int d2 = dx * dx + dy * dy;
-                        md2 = d2 < md2 ? d2 : md2;
-                    }
-                    double effect = 0.0;
-                    if (md2 < lay.repel_d2) effect = lay.repel_k / (sqrt((double)md2) + 0.1);
-                    const double u = -0.1 + (0.1 - -0.1) * mt_double(pyring, RMASK, idx);
-                    idx += 2;
-                    const double score = delta_p * 5.0 + effect + u;
-                    if (score > maxs) {
-                        maxs = score;
-                        best = (uint32_t)d;
-                    }
-                }
-            }
+        // queue the planners with >= 1 candidate; their Python-stream words are
+        // assigned here, in person order (exclusive prefix of 2*|cand| by bit-sliced ballots)
+        const int ncand = __popc(cand);
+        int off2 = 0, tot2 = 0;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            const unsigned long long m = __ballot((ncand >> b) & 1);
+            off2 += lanes_below(m) << (b + 1);
+            tot2 += __popcll(m) << (b + 1);
+        }
+        const unsigned long long qm = __ballot(cand != 0);
+        if (cand) {
+            const int k = qn + lanes_below(qm);
+            qa[k] = (uint32_t)p | (cand << 16);
+            qb[k] = (uint32_t)x | ((uint32_t)y << 12);
+            qc[k] = py_head + off2;
         }
         py_head += tot2;
-        if (inr) {
-            dirL[p] = (uint8_t)best;
-            if (act) {
-                pkL[p] = v;
-                h_g[p] = hh;
-                a_g[p] = ac;
+        qn += __popcll(qm);
+        if (need) h_g[p] = hh;
+        if (alive) a_g[p] = ac;
+        if (died) pk_g[p] = v | (2u << 24);
+        if (qn >= 64) {
+            wave_fence();
+            score_batch(64);
+            const int rest = qn - 64;  // move entries [64, qn) to the front
+            uint32_t ta = 0, tb = 0;
+            int tc = 0;
+            if (lane < rest) {
+                ta = qa[64 + lane];
+                tb = qb[64 + lane];
+                tc = qc[64 + lane];
             }
+            wave_fence();
+            if (lane < rest) {
+                qa[lane] = ta;
+                qb[lane] = tb;
+                qc[lane] = tc;
+            }
+            qn = rest;
+            wave_fence();
         }
     }
-    // the numpy stream is finished for this step: its ring becomes the claim table
-    mt_store(npring, np_front, np_head, st.np_mt + (size_t)e * EVX_MT_WORDS);
+    if (qn > 0) {
+        wave_fence();
+        score_batch(qn);
+    }
+    // the numpy stream is finished for this step
+    mt_store_w(npring, np_front, np_head, st.np_mt + (size_t)e * EVX_MT_WORDS);
     EVX_COUNT(13, np_head);
-    __syncthreads();
+    EVX_COUNT(11, nplan);
+    any_cont = __ballot(any_cont) != 0;
+    __syncthreads();  // plan[] and the person writes are visible to every lane
     EVX_STAMP(2);
 
-    // ------------------------------------ targets: first planner per cell
-    const int CW = (g.G + 1) / 2;
-    for (int i = tid; i < CW; i += NT) claim[i] = 0xffffffffu;
-    __syncthreads();
-    for (int p = tid; p < P; p += NT) {
-        const uint32_t d = dirL[p];
-        if (d != NODIR) {
-            const uint32_t v = pkL[p];
-            lds_min16(claim, (pk_x(v) + move_dx(d)) * g.GY + pk_y(v) + move_dy(d), (uint32_t)p);
-        }
-    }
-    __syncthreads();
-    for (int p = tid; p < P; p += NT) {
-        const uint32_t d = dirL[p];
-        if (d != NODIR) {
-            const uint32_t v = pkL[p];
-            const int t = (pk_x(v) + move_dx(d)) * g.GY + pk_y(v) + move_dy(d);
-            const uint32_t pf = lds_read16(claim, t);
-            pfL[p] = (uint16_t)pf;
-            if (pf != (uint32_t)p) {
-                atomicOr(&confl[pf >> 5], 1u << (pf & 31));
-                lnext[p] = (uint16_t)lds_exch16(lhead, (int)pf, (uint32_t)p);
+    // ------------------------- contested targets: groups, shuffle, losers
+    int err = 0;
+    int ncont = 0;
+    uint32_t* Lp = npring;  // the numpy ring is free now
+    if (any_cont) {
+        for (int i0 = 0; i0 < nplan; i0 += 64) {
+            const int i = i0 + lane;
+            bool c = false;
+            uint32_t key = 0;
+            if (i < nplan) {
+                const uint2 en = plan[i];
+                const int t = (int)(en.y & 0xffffffu) + doff_of(en.y >> 24, GY);
+                c = bit_get(cbits, t);
+                key = ((uint32_t)t << pb) | en.x;
             }
+            const unsigned long long m = __ballot(c);
+            const int pos = ncont + lanes_below(m);
+            if (c && pos < CL_CAP) Lp[pos] = key;
+            ncont += __popcll(m);
+        }
+        if (ncont <= CL_CAP) {
+            contested_groups(Lp, aux, aux + GH_CAP, ncont, pb, pyring, py_front, py_head, lost, misc, err);
+        } else {  // rare: sort in this env's global scratch
+            Lp = Lg;
+            int k = 0;
+            for (int i0 = 0; i0 < nplan; i0 += 64) {
+                const int i = i0 + lane;
+                bool c = false;
+                uint32_t key = 0;
+                if (i < nplan) {
+                    const uint2 en = plan[i];
+                    const int t = (int)(en.y & 0xffffffu) + doff_of(en.y >> 24, GY);
+                    c = bit_get(cbits, t);
+                    key = ((uint32_t)t << pb) | en.x;
+                }
+                const unsigned long long m = __ballot(c);
+                if (c) Lg[k + lanes_below(m)] = key;
+                k += __popcll(m);
+            }
+            __syncthreads();
+            contested_groups(Lg, Hg, Sg, ncont, pb, pyring, py_front, py_head, lost, misc, err);
         }
     }
+    EVX_COUNT(14, ncont);
+    mt_store_w(pyring, py_front, py_head, st.py_mt + (size_t)e * EVX_MT_WORDS);
+    EVX_COUNT(12, py_head);
+    // near-robot bits are done: obits becomes "vacated by a winner"
+    for (int i = lane; i < g.RW; i += 64) obits[i] = 0;
     __syncthreads();
-    for (int p = tid; p < P; p += NT) {
-        const uint32_t d = dirL[p];
-        if (d != NODIR && pfL[p] == (uint32_t)p) {
-            const uint32_t v = pkL[p];
-            lds_set16_ffff(claim, (pk_x(v) + move_dx(d)) * g.GY + pk_y(v) + move_dy(d));
-        }
-    }
     EVX_STAMP(3);
 
-    // ------------------------- random.shuffle of contested targets (lane 0)
-    if (tid == 0) {
-        ctrl[0] = 0;              // word index into confl
-        ctrl[1] = (int)confl[0];  // remaining bits of that word
-        ctrl[2] = py_head;
-        ctrl[3] = 0;              // done
-        ctrl[4] = 0;              // error
-        ctrl[5] = 0;              // groups
+    // --------------------------------------------- execute_move, in order
+    for (int i0 = 0; i0 < nplan; i0 += 64) {
+        const int i = i0 + lane;
+        if (i < nplan) {
+            const uint2 en = plan[i];
+            const int cold = (int)(en.y & 0xffffffu);
+            const int t = cold + doff_of(en.y >> 24, GY);
+            const bool win = !bit_get(cbits, t) || !bit_get(lost, (int)en.x);
+            if (win) atomicOr(&obits[cold >> 5], 1u << (cold & 31));
+            if (st.thmap) atomicAdd(&st.thmap[(size_t)e * g.G + (win ? t : cold)], 1);
+        }
+    }
+    if (lane == 0) misc[0] = 0;
+    __syncthreads();
+    uint32_t* ev = aux;  // (cell, key) pairs; groups are done
+    int n_evac_new = 0;
+    for (int i0 = 0; i0 < nplan; i0 += 64) {
+        const int i = i0 + lane;
+        bool exw = false;
+        if (i < nplan) {
+            const uint2 en = plan[i];
+            const int p = (int)en.x;
+            const int cold = (int)(en.y & 0xffffffu);
+            const int dd = (int)(en.y >> 24);
+            const int t = cold + doff_of((uint32_t)dd, GY);
+            const bool cont = bit_get(cbits, t);
+            if (!cont || !bit_get(lost, p)) {
+                const bool ex = (lay.cellinfo[t] >> 1) & 1u;
+                exw = ex;
+                const bool ev_old = bit_get(tbits, cold), ev_new = bit_get(obits, t);
+                int pf = p;
+                if ((ev_old || ev_new) && cont) pf = find_pf(Lp, ncont, t, pb);
+                if (ev_old) {
+                    const int s = atomicAdd((int*)&misc[0], 1);
+                    if (s < EV_CAP) {
+                        ev[2 * s] = (uint32_t)cold;
+                        ev[2 * s + 1] = ((uint32_t)pf << 2) | 0u;  // sub-step 0: leave, value 0
+                    }
+                } else {
+                    atomicAnd(&rmapb[cold >> 5], ~(1u << (cold & 31)));
+                }
+                if (ev_new) {
+                    const int s = atomicAdd((int*)&misc[0], 1);
+                    if (s < EV_CAP) {
+                        ev[2 * s] = (uint32_t)t;
+                        ev[2 * s + 1] = ((uint32_t)pf << 2) | 2u | (ex ? 0u : 1u);
+                    }
+                } else if (ex) {
+                    atomicAnd(&rmapb[t >> 5], ~(1u << (t & 31)));
+                } else {
+                    atomicOr(&rmapb[t >> 5], 1u << (t & 31));
+                }
+                const int ox = cold / GY, oy = cold - ox * GY;
+                pk_g[p] = (uint32_t)(ox + move_dx(dd)) | ((uint32_t)(oy + move_dy(dd)) << 12) | (ex ? (1u << 24) : 0u);
+            }
+        }
+        n_evac_new += __popcll(__ballot(exw));
     }
     __syncthreads();
     {
-        const int NCW = (P + 31) / 32;
-        int last_head = -1;
-        while (true) {
-            const int h0 = ctrl[2];
-            mt_ensure(pyring, RMASK, py_front, h0 + SHUF_CHUNK);
-            __syncthreads();
-            if (tid == 0) {
-                int wi = ctrl[0];
-                uint32_t m = (uint32_t)ctrl[1];
-                int head = ctrl[2];
-                int done = 0, ngrp = ctrl[5];
-                const int avail = py_front;
-                while (true) {
-                    while (m == 0) {
-                        wi++;
-                        if (wi >= NCW) break;
-                        m = confl[wi];
-                    }
-                    if (wi >= NCW) {
-                        done = 1;
-                        break;
-                    }
-                    const int pf = wi * 32 + (__ffs(m) - 1);
-                    int n = 0;
-                    grp[n++] = pf;
-                    for (uint32_t q = lds_read16(lhead, pf); q != NIL16; q = lnext[q]) {
-                        if (n >= GRP_CAP) {
-                            ctrl[4] = 1;
-                            break;
-                        }
-                        grp[n++] = (int)q;
-                    }
-                    for (int a = 2; a < n; a++) {  // movers in person order
-                        const int vv = grp[a];
-                        int b = a - 1;
-                        while (b >= 1 && grp[b] > vv) {
-                            grp[b + 1] = grp[b];
-                            b--;
-                        }
-                        grp[b + 1] = vv;
-                    }
-                    const int hsave = head;
-                    bool ok = true;
-                    for (int i = n - 1; i >= 1 && ok; i--) {  // Lib/random.py shuffle
-                        const uint32_t bound = (uint32_t)(i + 1);
-                        const int kb = bit_length(bound);
-                        uint32_t r = 0;
-                        while (true) {
-                            if (head >= avail) {
-                                ok = false;
-                                break;
-                            }
-                            r = mt_word(pyring, RMASK, head++) >> (32 - kb);
-                            if (r < bound) break;
-                        }
-                        if (ok) {
-                            const int t = grp[i];
-                            grp[i] = grp[r];
-                            grp[r] = t;
-                        }
-                    }
-                    if (!ok) {
-                        head = hsave;
-                        break;
-                    }
-                    // winner replaces the list head (read only for contested targets below)
-                    lhead[pf >> 1] = (lhead[pf >> 1] & ~(0xffffu << ((pf & 1) * 16))) |
-                                     ((uint32_t)grp[0] << ((pf & 1) * 16));
-                    ngrp++;
-                    m &= m - 1;
-                }
-                ctrl[0] = wi;
-                ctrl[1] = (int)m;
-                ctrl[2] = head;
-                ctrl[3] = done;
-                ctrl[5] = ngrp;
+        const int nev = (int)misc[0];
+        if (nev > EV_CAP) err |= 16;
+        const int ne = min(nev, EV_CAP);
+        for (int i = lane; i < ne; i += 64) {  // last writer = largest (first planner, sub-step)
+            const uint32_t c = ev[2 * i], kv = ev[2 * i + 1];
+            bool top = true;
+            for (int j = 0; j < ne; j++)
+                if (ev[2 * j] == c && ev[2 * j + 1] > kv) top = false;
+            if (top) {
+                if (kv & 1u) atomicOr(&rmapb[c >> 5], 1u << (c & 31));
+                else atomicAnd(&rmapb[c >> 5], ~(1u << (c & 31)));
             }
-            __syncthreads();
-            if (ctrl[3]) break;
-            if (ctrl[2] == last_head) {  // no progress: cannot happen with sane streams
-                if (tid == 0) ctrl[4] = 2;
-                break;
-            }
-            last_head = ctrl[2];
         }
-        py_head = ctrl[2];
-        if (ctrl[4] && out.err && tid == 0) atomicOr(out.err, ctrl[4]);
-        EVX_COUNT(14, ctrl[5]);
     }
-    mt_store(pyring, py_front, py_head, st.py_mt + (size_t)e * EVX_MT_WORDS);
-    EVX_COUNT(12, py_head);
     __syncthreads();
+    for (int i = lane; i < g.RW; i += 64) st.rmap[(size_t)e * g.RW + i] = rmapb[i];
     EVX_STAMP(4);
-
-    // --------------------------------------------- execute_move, in order
-    // event code: min over 0xffff - (first_planner<<2 | sub<<1 | value)
-    for (int p = tid; p < P; p += NT) {
-        const uint32_t d = dirL[p];
-        if (d == NODIR) continue;
-        const uint32_t v = pkL[p];
-        const int pf = pfL[p];
-        const bool contested = (confl[pf >> 5] >> (pf & 31)) & 1u;
-        const int w = contested ? (int)lds_read16(lhead, pf) : pf;
-        const int cold = pk_x(v) * g.GY + pk_y(v);
-        if (w == p) {
-            const int t = cold + move_dx(d) * g.GY + move_dy(d);
-            const bool ex = (lay.cellinfo[t] >> 1) & 1u;
-            lds_min16(claim, cold, 0xffffu - ((uint32_t)pf << 2));
-            lds_min16(claim, t, 0xffffu - (((uint32_t)pf << 2) | 2u | (ex ? 0u : 1u)));
-            if (st.thmap) atomicAdd(&st.thmap[(size_t)e * g.G + t], 1);
-        } else {
-            dirL[p] = (uint8_t)(0x80u | d);  // lost the conflict: stays
-            if (st.thmap) atomicAdd(&st.thmap[(size_t)e * g.G + cold], 1);
-        }
-    }
-    __syncthreads();
-    for (int p = tid; p < P; p += NT) {
-        const uint32_t d = dirL[p];
-        if (d & 0x80u) continue;  // no plan, or lost
-        const uint32_t v = pkL[p];
-        const int pf = pfL[p];
-        const int cold = pk_x(v) * g.GY + pk_y(v);
-        const int t = cold + move_dx(d) * g.GY + move_dy(d);
-        const bool ex = (lay.cellinfo[t] >> 1) & 1u;
-        const uint32_t code_new = 0xffffu - (((uint32_t)pf << 2) | 2u | (ex ? 0u : 1u));
-        if (lds_read16(claim, cold) == 0xffffu - ((uint32_t)pf << 2))
-            atomicAnd(&rmapb[cold >> 5], ~(1u << (cold & 31)));
-        if (lds_read16(claim, t) == code_new) {
-            if (ex) atomicAnd(&rmapb[t >> 5], ~(1u << (t & 31)));
-            else atomicOr(&rmapb[t >> 5], 1u << (t & 31));
-        }
-        pkL[p] = (uint32_t)(pk_x(v) + move_dx(d)) | ((uint32_t)(pk_y(v) + move_dy(d)) << 12) |
-                 (ex ? (1u << 24) : 0u);
-    }
-    __syncthreads();
-    for (int i = tid; i < g.RW; i += NT) st.rmap[(size_t)e * g.RW + i] = rmapb[i];
-    EVX_STAMP(5);
 
     // ---------------------------------- fire update (both fire models)
     const int fs1 = fs < lay.t_max ? fs + 1 : fs;
 
     // ------------------------------------ _calculate_reward + counters
+    const int evac = n_safe + n_evac_new, dead = (P - nnd) + n_died;
+    const int nrem = P - evac - dead;
+    int* ltab = reinterpret_cast<int*>(aux);  // leaf offsets | lengths
+    double* leafsum = reinterpret_cast<double*>(pyring);
+    double* lb = leafsum + LEAF_CAP;          // current leaf's elements (<= 128 + 64)
+    int nleaf = 0;
+    if (lane == 0 && nrem > 0)
+        nleaf = np_pairwise_leaves(nrem, ltab, ltab + LEAF_CAP, LEAF_CAP, reinterpret_cast<int*>(misc));
+    nleaf = __shfl(nleaf, 0);
+    if (nleaf > LEAF_CAP) {
+        err |= 8;
+        nleaf = 0;
+    }
+    wave_fence();
     const int vx = rp_x(view), vy = rp_y(view);
-    int evac_t = 0, dead_t = 0;
     double gq_t = 0.0;
-    int nrem = 0;
-    for (int row = 0; row < NROW; row++) {
-        const int p = row * NT + tid;
-        const bool inr = p < P;
-        const uint32_t v = inr ? pkL[p] : (3u << 24);
-        const bool sf = inr && pk_safe(v), dd = inr && pk_dead(v);
-        evac_t += sf;
-        dead_t += dd;
-        const double hv = (inr && !dd) ? h_g[p] : 0.0;
-        const bool rem = inr && !sf && !dd;
+    int q = 0, lb_base = 0, cur = 0;
+    // remaining persons = the not-dead list minus this step's deaths and evacuations
+    uint32_t iNN = 0u, wN = DONEPK;
+    double hvN = 0.0;
+    if (lane < nnd) {
+        const uint32_t iN = ndl[lane].x;
+        wN = pk_g[iN];
+        hvN = h_g[iN];
+    }
+    if (64 + lane < nnd) iNN = ndl[64 + lane].x;
+    for (int row = 0; row < NRD; row++) {
+        const int i = row * 64 + lane;
+        const uint32_t v = wN;
+        const double hv = hvN;
+        if (i + 64 < nnd) {
+            wN = pk_g[iNN];
+            hvN = h_g[iNN];
+        }
+        if (i + 128 < nnd) iNN = ndl[i + 128].x;
+        const bool rem = i < nnd && !pk_safe(v) && !pk_dead(v);
         const long long x2 = 2 * pk_x(v) + 1, y2 = 2 * pk_y(v) + 1;
         const long long dxr = x2 - 2LL * vx, dyr = y2 - 2LL * vy;
         const long long n4 = dxr * dxr + dyr * dyr;  // (2*distance)^2, exact
@@ -570,74 +916,62 @@ __global__ __launch_bounds__(NT, 4) void env_step_kernel(evx_layout lay, evx_sta
             else gq_t += 1.0;
             if (hv < 80) gq_t += 1.0;
         }
-        int tot;
-        const int off = block_exscan(rem ? 1 : 0, wsum, tot);
-        if (rem) distbuf[nrem + off] = 0.5 * sqrt((double)n4);
-        nrem += tot;
-        if (inr) hbuf[p] = hv;  // dead -> +0.0, which leaves the sequential sum unchanged
-    }
-    const int evac = block_sum(evac_t, wsum);
-    const int dead = block_sum(dead_t, wsum);
-    const double gq = block_sum_d(gq_t, dsum);  // multiples of 0.5: exact in any order
-    EVX_STAMP(6);
-    // Order-sensitive f64 sums. Python sum over not-dead healths (sequential,
-    // wave 0 lane 0) runs beside numpy's pairwise mean (leaves on wave 1).
-    if (tid == 0) {
-        double total = 0.0;
-        const double2* h2 = reinterpret_cast<const double2*>(hbuf);
-        int p = 0;
-        for (; p + 8 <= P; p += 8) {
-            const double2 a = h2[p / 2], b = h2[p / 2 + 1], c = h2[p / 2 + 2], d = h2[p / 2 + 3];
-            total += a.x; total += a.y; total += b.x; total += b.y;
-            total += c.x; total += c.y; total += d.x; total += d.y;
-        }
-        for (; p < P; p++) total += hbuf[p];
-        dsum[2 * NWAVE] = total;
-    } else if (tid >= 64 && tid < 128 && nrem > 0) {
-        int lo[4], ll[4];
-        const int lane = tid - 64;
-        int nleaf = 0;
-        {
-            int so[32], sl[32];
-            int sp = 1;
-            so[0] = 0; sl[0] = nrem;
-            while (sp > 0) {
-                sp--;
-                const int o = so[sp], l = sl[sp];
-                if (l <= 128) {
-                    if ((nleaf & 63) == lane && (nleaf >> 6) < 4) {
-                        lo[nleaf >> 6] = o;
-                        ll[nleaf >> 6] = l;
-                    }
-                    nleaf++;
-                } else {
-                    int n2 = l / 2;
-                    n2 -= n2 % 8;
-                    so[sp] = o + n2; sl[sp] = l - n2; sp++;
-                    so[sp] = o; sl[sp] = n2; sp++;
-                }
+        const unsigned long long rm = __ballot(rem);
+        if (rem) lb[q + lanes_below(rm) - lb_base] = 0.5 * sqrt((double)n4);
+        q += __popcll(rm);
+        wave_fence();
+        // numpy pairwise leaves that are now complete
+        while (cur < nleaf && q >= ltab[cur] + ltab[LEAF_CAP + cur]) {
+            const int len = ltab[LEAF_CAP + cur], o = ltab[cur] - lb_base;
+            const int len8 = len - (len % 8);
+            double r = 0.0;
+            if (len >= 8 && lane < 8) {
+                r = lb[o + lane];
+                for (int k = 8 + lane; k < len8; k += 8) r += lb[o + k];
             }
+            if (len >= 8) {
+                const double r0 = readlane_d(r, 0), r1 = readlane_d(r, 1), r2 = readlane_d(r, 2),
+                             r3 = readlane_d(r, 3), r4 = readlane_d(r, 4), r5 = readlane_d(r, 5),
+                             r6 = readlane_d(r, 6), r7 = readlane_d(r, 7);
+                r = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+            }
+            if (lane == 0) {
+                int k = len8;
+                if (len < 8) {
+                    r = 0.0;
+                    k = 0;
+                }
+                for (; k < len; k++) r += lb[o + k];
+                leafsum[cur] = r;
+            }
+            cur++;
         }
-        for (int j = 0; j < 4; j++) {
-            const int li = j * 64 + lane;
-            if (li < nleaf && li < PW_CAP) pwsum[li] = np_pairwise_leaf(distbuf + lo[j], ll[j]);
+        const int nb = cur < nleaf ? ltab[cur] : q;
+        if (nb > lb_base) {  // drop consumed elements: keep [nb, q) at the buffer start
+            const int keep = q - nb, sh = nb - lb_base;
+            double t0 = 0.0, t1 = 0.0, t2 = 0.0;
+            if (lane < keep) t0 = lb[sh + lane];
+            if (lane + 64 < keep) t1 = lb[sh + lane + 64];
+            if (lane + 128 < keep) t2 = lb[sh + lane + 128];
+            wave_fence();
+            if (lane < keep) lb[lane] = t0;
+            if (lane + 64 < keep) lb[lane + 64] = t1;
+            if (lane + 128 < keep) lb[lane + 128] = t2;
+            lb_base = nb;
         }
-        if (lane == 0) ctrl[6] = nleaf;
+        wave_fence();
     }
-    __syncthreads();
-    if (tid == 64) {
-        if (nrem > 0 && ctrl[6] <= PW_CAP) dsum[2 * NWAVE + 1] = np_pairwise_combine(nrem, pwsum) / (double)nrem;
-        else if (nrem > 0) dsum[2 * NWAVE + 1] = 0.0, (out.err ? atomicOr(out.err, 8) : 0);
-    }
-    __syncthreads();
-    EVX_STAMP(7);
-    if (tid == 0) {
-        const int remaining = P - evac - dead;
+    const double gq = wave_sum_d(gq_t);  // multiples of 0.5: exact in any order
+    EVX_STAMP(5);
+    if (lane == 0) {
+        const int remaining = nrem;
         double reward = 0.0;
         reward += (evac - prev_evac) * lay.evac_reward;
         reward += gq;
-        if (remaining > 0) {
-            const double avg = dsum[2 * NWAVE + 1];
+        if (remaining > 0 && nleaf > 0) {
+            const double avg = np_pairwise_combine(nrem, leafsum, reinterpret_cast<int*>(misc),
+                                                   reinterpret_cast<double*>(misc + 64)) /
+                               (double)nrem;
             const double dr = 2.0 - fabs(avg - 8.0) * 0.2;
             reward += dr > 0 ? dr : 0.0;
         }
@@ -647,7 +981,6 @@ __global__ __launch_bounds__(NT, 4) void env_step_kernel(evx_layout lay, evx_sta
         } else {
             reward -= 0.02;
         }
-        const double total = dsum[2 * NWAVE];
         if (P - dead > 0) {
             const double avg_h = total / (double)(P - dead);
             reward += (avg_h - 90) * 0.05;
@@ -678,18 +1011,18 @@ __global__ __launch_bounds__(NT, 4) void env_step_kernel(evx_layout lay, evx_sta
         sg[2] = evac;
         sg[3] = dead;
         st.view[e] = view;
+        if (err && out.err) atomicOr(out.err, err);
     }
 
     // ------------------------------------------------- observations
-    {
-        const int w = tid >> 6;
-        for (int r = w; r < R; r += NWAVE) {
-            const uint32_t c = (r == 0) ? view : robots[r];
-            write_obs(g, validb, rmapb, rp_x(c), rp_y(c), fs1, out.obs + (size_t)e * R + r);
-        }
+    // People.rmap is only ever set on valid cells, so Check_Valid reduces to the
+    // interior range test here (no table reads).
+    for (int r = 0; r < R; r++) {
+        const uint32_t c = (r == 0) ? view : robots[r];
+        write_obs(g, nullptr, rmapb, rp_x(c), rp_y(c), fs1, out.obs + (size_t)e * R + r);
     }
-    for (int p = tid; p < P; p += NT) pk_g[p] = pkL[p];
     EVX_STAMP(8);
+    EVX_RSTAMP(10);
 }
 
 // ------------------------------------------------------------------ reset
@@ -905,16 +1238,29 @@ const char* evx_last_error(void) { return g_err; }
 int64_t evx_step_lds_bytes(const evx_layout* l) {
     if (check_layout(l)) return -1;
     const int G = (l->L + 2) * (l->W + 2);
-    return (int64_t)evx::step_lds(G, l->P, l->R).total * 4;
+    return (int64_t)evx::wave_lds(G, l->P, l->R).total * 4;
+}
+
+int64_t evx_step_scratch_words(const evx_layout* l) {
+    if (check_layout(l)) return -1;
+    return evx::wave_scratch_words(l->P);
 }
 
 int evx_env_step(const evx_layout* l, const evx_state* s, const int32_t* actions, const evx_step_out* o, void* stream) {
     int rc = check_layout(l);
     if (rc) return rc;
     if (!s || !o || !actions || !o->reward || !o->done || !o->obs) return fail(-22, "NULL argument");
+    if (!s->scratch) return fail(-22, "state scratch is NULL (evx_step_scratch_words per env)");
+    if (!l->nbr_valid) return fail(-22, "missing table nbr_valid");
     if (s->E <= 0) return 0;
     const int G = (l->L + 2) * (l->W + 2);
-    const size_t lds = (size_t)evx::step_lds(G, l->P, l->R).total * 4;
+    {  // contested-list keys are (target << bits(P-1)) | person in 32 bits
+        int pb = 1, gb = 1;
+        while ((1 << pb) < l->P) pb++;
+        while ((1LL << gb) < (long long)G) gb++;
+        if (pb + gb > 32) return fail(-22, "grid cells x people too large for 32-bit move keys");
+    }
+    const size_t lds = (size_t)evx::wave_lds(G, l->P, l->R).total * 4;
     if (lds > 160 * 1024) return fail(-7, "layout needs more than 160 KiB of LDS");
     static bool attr_set = false;
     if (!attr_set) {
@@ -922,7 +1268,7 @@ int evx_env_step(const evx_layout* l, const evx_state* s, const int32_t* actions
                                   160 * 1024);
         attr_set = true;
     }
-    hipLaunchKernelGGL(evx::env_step_kernel, dim3(s->E), dim3(evx::NT), lds, (hipStream_t)stream, *l, *s, actions, *o);
+    hipLaunchKernelGGL(evx::env_step_kernel, dim3(s->E), dim3(64), lds, (hipStream_t)stream, *l, *s, actions, *o);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : hip_fail(e, "env_step launch");
 }

@@ -88,115 +88,24 @@ __device__ __forceinline__ double wave_sum_d(double v) {
     return v;
 }
 
-// Exclusive scan in PERSON order over one row of NT persons (one per thread).
-// `wsum`: LDS scratch of NWAVE ints. Returns the thread's exclusive offset;
-// `row_total` receives the row sum (uniform). Two barriers.
-__device__ __forceinline__ int block_exscan(int v, int* wsum, int& row_total) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int incl = wave_incl_scan(v);
-    if (lane == 63) wsum[w] = incl;
-    __syncthreads();
-    int before = 0, tot = 0;
-#pragma unroll
-    for (int i = 0; i < NWAVE; i++) {
-        const int s = wsum[i];
-        before += (i < w) ? s : 0;
-        tot += s;
-    }
-    __syncthreads();
-    row_total = tot;
-    return before + incl - v;
-}
-
-__device__ __forceinline__ int block_sum(int v, int* wsum) {
-    const int s = wave_sum(v);
-    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = s;
-    __syncthreads();
-    int tot = 0;
-#pragma unroll
-    for (int i = 0; i < NWAVE; i++) tot += wsum[i];
-    __syncthreads();
-    return tot;
-}
-
-__device__ __forceinline__ double block_sum_d(double v, double* wsum) {
-    const double s = wave_sum_d(v);
-    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = s;
-    __syncthreads();
-    double tot = 0;
-#pragma unroll
-    for (int i = 0; i < NWAVE; i++) tot += wsum[i];
-    __syncthreads();
-    return tot;
-}
-
-// 16-bit LDS table entries packed two per 32-bit word.
-__device__ __forceinline__ void lds_min16(uint32_t* tab, int idx, uint32_t v) {
-    uint32_t* w = tab + (idx >> 1);
-    const int sh = (idx & 1) * 16;
-    uint32_t old = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    while (true) {
-        const uint32_t cur = (old >> sh) & 0xffffu;
-        if (cur <= v) return;
-        const uint32_t nv = (old & ~(0xffffu << sh)) | (v << sh);
-        const uint32_t prev = atomicCAS(w, old, nv);
-        if (prev == old) return;
-        old = prev;
-    }
-}
-
-__device__ __forceinline__ uint32_t lds_exch16(uint32_t* tab, int idx, uint32_t v) {
-    uint32_t* w = tab + (idx >> 1);
-    const int sh = (idx & 1) * 16;
-    uint32_t old = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    while (true) {
-        const uint32_t nv = (old & ~(0xffffu << sh)) | (v << sh);
-        const uint32_t prev = atomicCAS(w, old, nv);
-        if (prev == old) return (old >> sh) & 0xffffu;
-        old = prev;
-    }
-}
-
-__device__ __forceinline__ uint32_t lds_read16(const uint32_t* tab, int idx) {
-    return (tab[idx >> 1] >> ((idx & 1) * 16)) & 0xffffu;
-}
-
-__device__ __forceinline__ void lds_set16_ffff(uint32_t* tab, int idx) {
-    atomicOr(tab + (idx >> 1), 0xffffu << ((idx & 1) * 16));
-}
-
-// numpy DOUBLE_pairwise_sum leaf (n <= 128), 8 accumulators, aligned double2 loads.
-__device__ inline double np_pairwise_leaf(const double* a, int n) {
-    if (n < 8) {
-        double res = 0.;
-        for (int i = 0; i < n; i++) res += a[i];
-        return res;
-    }
-    const double2* a2 = reinterpret_cast<const double2*>(a);
-    double2 q0 = a2[0], q1 = a2[1], q2 = a2[2], q3 = a2[3];
-    double r0 = q0.x, r1 = q0.y, r2 = q1.x, r3 = q1.y, r4 = q2.x, r5 = q2.y, r6 = q3.x, r7 = q3.y;
-    int i;
-    for (i = 8; i < n - (n % 8); i += 8) {
-        q0 = a2[i / 2]; q1 = a2[i / 2 + 1]; q2 = a2[i / 2 + 2]; q3 = a2[i / 2 + 3];
-        r0 += q0.x; r1 += q0.y; r2 += q1.x; r3 += q1.y;
-        r4 += q2.x; r5 += q2.y; r6 += q3.x; r7 += q3.y;
-    }
-    double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
-    for (; i < n; i++) res += a[i];
-    return res;
-}
-
-// Leaves of numpy's pairwise split tree for n elements, left to right.
-// Returns the number of leaves (<= cap) written to off/len.
-__device__ inline int np_pairwise_leaves(int n, int* off, int* len, int cap) {
-    int so[32], sl[32];
-    int sp = 0, nl = 0;
-    so[0] = 0; sl[0] = n; sp = 1;
+// Leaves of numpy's pairwise split tree (DOUBLE_pairwise_sum: blocks <= 128
+// elements, split at n/2 rounded down to a multiple of 8), left to right.
+// Single lane; `stk` is 64 ints of LDS (no private-memory stack). Returns the
+// number of leaves (<= cap written to off/len).
+__device__ inline int np_pairwise_leaves(int n, int* off, int* len, int cap, int* stk) {
+    int* so = stk;
+    int* sl = stk + 32;
+    int sp = 1, nl = 0;
+    so[0] = 0;
+    sl[0] = n;
     while (sp > 0) {
         sp--;
         const int o = so[sp], l = sl[sp];
         if (l <= 128) {
-            if (nl < cap) { off[nl] = o; len[nl] = l; }
+            if (nl < cap) {
+                off[nl] = o;
+                len[nl] = l;
+            }
             nl++;
         } else {
             int n2 = l / 2;
@@ -208,12 +117,14 @@ __device__ inline int np_pairwise_leaves(int n, int* off, int* len, int cap) {
     return nl;
 }
 
-// Combine leaf sums in numpy's tree order (single lane).
-__device__ inline double np_pairwise_combine(int n, const double* leafsum) {
-    int ol[32], st[32];
-    double left[32];
+// Combine leaf sums in numpy's tree order (single lane). `stk`: 64 ints and
+// `left`: 32 doubles of LDS.
+__device__ inline double np_pairwise_combine(int n, const double* leafsum, int* stk, double* left) {
+    int* ol = stk;
+    int* st = stk + 32;
     int sp = 0, li = 0;
-    ol[0] = n; st[0] = 0;
+    ol[0] = n;
+    st[0] = 0;
     double ret = 0.0;
     while (true) {
         if (ol[sp] <= 128) {

@@ -24,13 +24,13 @@ class evx_layout(C.Structure):
                [(n, C.c_double) for n in ["repel_k", "repel_range", "evac_reward", "death_penalty",
                                          "death_acc_penalty", "alive_bonus"]] + \
                [(n, C.c_void_p) for n in ["floor", "cellinfo", "valid_bits", "danger_p", "danger_o",
-                                         "danger_o32", "robot_init"]]
+                                         "danger_o32", "robot_init", "nbr_valid"]]
 
 
 class evx_state(C.Structure):
     _fields_ = [("E", C.c_int32)] + [(n, C.c_void_p) for n in
                                      ["pk", "health", "acc", "rmap", "thmap", "robots", "view", "scal",
-                                      "py_mt", "np_mt"]]
+                                      "py_mt", "np_mt", "scratch"]]
 
 
 class evx_step_out(C.Structure):
@@ -48,6 +48,9 @@ def lib():
         L = C.CDLL(LIB_PATH)
         L.evx_last_error.restype = C.c_char_p
         L.evx_step_lds_bytes.restype = C.c_int64
+        L.evx_step_scratch_words.restype = C.c_int64
+        L.evx_step_lds_bytes.argtypes = [C.POINTER(evx_layout)]
+        L.evx_step_scratch_words.argtypes = [C.POINTER(evx_layout)]
         for name in ["evx_env_step", "evx_env_reset", "evx_obs_expand_f32", "evx_obs_expand_f64",
                      "evx_seed_host"]:
             getattr(L, name).restype = C.c_int
@@ -69,4 +72,4 @@ def check(rc: int, what: str):
 
 # every C symbol include/evacx.h declares (checked by tests/test_abi.py)
 EXPORTS = ["evx_env_step", "evx_env_reset", "evx_obs_expand_f32", "evx_obs_expand_f64", "evx_seed_host",
-           "evx_step_lds_bytes", "evx_last_error"]
+           "evx_step_lds_bytes", "evx_step_scratch_words", "evx_last_error"]

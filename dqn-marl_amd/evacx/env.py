@@ -52,6 +52,25 @@ def repel_threshold(repel_range: float) -> int:
     return n
 
 
+# People.MoveTO order (envs/people.py:8-17): direction d moves by (MOVE_DX[d], MOVE_DY[d])
+MOVE_DX = [((0x8246 >> (2 * d)) & 3) - 1 for d in range(8)]
+MOVE_DY = [((0xA091 >> (2 * d)) & 3) - 1 for d in range(8)]
+
+
+def neighbour_valid_mask(valid: np.ndarray, L: int, W: int) -> np.ndarray:
+    """[G] uint8, bit d set iff Map.Check_Valid(x + dx_d, y + dy_d) (envs/map.py:85-92)."""
+    GX, GY = L + 2, W + 2
+    v = np.asarray(valid, bool).reshape(GX, GY)
+    inner = np.zeros((GX, GY), bool)
+    inner[1:L + 1, 1:W + 1] = v[1:L + 1, 1:W + 1]
+    pad = np.zeros((GX + 2, GY + 2), bool)
+    pad[1:-1, 1:-1] = inner
+    m = np.zeros((GX, GY), np.uint8)
+    for d in range(8):
+        m |= (pad[1 + MOVE_DX[d]:1 + MOVE_DX[d] + GX, 1 + MOVE_DY[d]:1 + MOVE_DY[d] + GY].astype(np.uint8) << d)
+    return m.reshape(-1)
+
+
 class DeviceLayout:
     """Static tables of one layout in HBM + the evx_layout descriptor."""
 
@@ -77,6 +96,7 @@ class DeviceLayout:
             danger_o=torch.from_numpy(np.ascontiguousarray(tables.danger_o.reshape(-1))).to(d),
             robot_init=torch.from_numpy(np.asarray(spec.robot_init, np.int32).reshape(-1)).to(d),
         )
+        self.t["nbr_valid"] = torch.from_numpy(neighbour_valid_mask(tables.valid, spec.L, spec.W)).to(d)
         self.t["danger_o32"] = self.t["danger_o"].to(torch.float32)
         T = tables.danger_p.shape[0] - 1
         OX, OY = tables.danger_o.shape[1:]
@@ -125,6 +145,10 @@ class VecEnv:
         self.scal = torch.zeros(E * 4, **i32)
         self.py_mt = torch.zeros(E * 625, **i32)
         self.np_mt = torch.zeros(E * 625, **i32)
+        sw = int(_lib.lib().evx_step_scratch_words(C.byref(layout.c)))
+        if sw < 0:
+            raise _lib.EvacxError(_lib.lib().evx_last_error().decode())
+        self.scratch = torch.zeros(E * sw, **i32)
         # outputs
         self.reward = torch.zeros(E, **f64)
         self.done = torch.zeros(E, dtype=torch.uint8, device=d)
@@ -134,7 +158,7 @@ class VecEnv:
         self.c = _lib.evx_state(E=E, pk=_ptr(self.pk), health=_ptr(self.health), acc=_ptr(self.acc),
                                 rmap=_ptr(self.rmap), thmap=_ptr(self.thmap), robots=_ptr(self.robots),
                                 view=_ptr(self.view), scal=_ptr(self.scal), py_mt=_ptr(self.py_mt),
-                                np_mt=_ptr(self.np_mt))
+                                np_mt=_ptr(self.np_mt), scratch=_ptr(self.scratch))
         self.out = _lib.evx_step_out(reward=_ptr(self.reward), done=_ptr(self.done), counts=_ptr(self.counts),
                                      obs=_ptr(self.obs), err=_ptr(self.err))
 

@@ -50,6 +50,7 @@ typedef struct {
     const double *danger_o;   /* [(t_max+1)*OX*OY] danger at integer obs coordinates */
     const float *danger_o32;  /* same, float32 (network input path) */
     const int32_t *robot_init;/* [R*2] robot positions after a multi-robot reset */
+    const uint8_t *nbr_valid; /* [G] bit d: Check_Valid of the MoveTO[d] neighbour (envs/people.py:259-265) */
 } evx_layout;
 
 /* Structure-of-arrays state of E env instances (env-major). */
@@ -65,6 +66,7 @@ typedef struct {
     int32_t *scal;     /* [E*4] fire_step, current_step, prev_evacuated, prev_dead */
     uint32_t *py_mt;   /* [E*625] CPython `random` MT19937 state per env */
     uint32_t *np_mt;   /* [E*625] legacy numpy.random MT19937 state per env */
+    uint32_t *scratch; /* [E*evx_step_scratch_words] step scratch: move plan, contested lists beyond LDS */
 } evx_state;
 
 /* Compact per-robot observation (32 B). Expands to the reference's 11x11x6
@@ -109,6 +111,8 @@ int evx_seed_host(const uint32_t *seeds_host, int32_t n, uint32_t *py_mt_host, u
 
 /* Bytes of dynamic LDS the step kernel needs for a layout (diagnostics). */
 int64_t evx_step_lds_bytes(const evx_layout *lay);
+/* 32-bit words of evx_state.scratch the step needs per env. */
+int64_t evx_step_scratch_words(const evx_layout *lay);
 
 const char *evx_last_error(void);
 

@@ -14,8 +14,9 @@ import torch  # noqa: E402
 from evacx.env import DeviceLayout, VecEnv, _ptr  # noqa: E402
 from evacx.layout import build_tables, synthetic  # noqa: E402
 
-NAMES = ["load", "regs", "rows(health+plan)", "claims", "shuffle", "execute", "mt_store+rmap", "reward-par",
-         "reward-seq", "obs", "store"]
+# stamp slots written by env_step_kernel (one wave per env)
+SLOTS = [(0, "start"), (1, "load+robots+near"), (2, "rows(health+plan)"), (3, "contested+mt_store"),
+         (4, "execute+rmap"), (5, "reward rows"), (8, "reward+obs")]
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--envs", type=int, default=4096)
@@ -40,11 +41,15 @@ for i in range(3):
     env.step(acts[args.warmup + i])
 torch.cuda.synchronize()
 s = stamps.view(E, 16).cpu().numpy()
-d = np.diff(s[:, :11], axis=1)
-tot = s[:, 10] - s[:, 0]
-print(f"envs={E} median total cycles/env-step={np.median(tot):.0f} (wave-lifetime, one env)")
-for i, n in enumerate(NAMES[:10]):
+cols = [c for c, _ in SLOTS]
+d = np.diff(s[:, cols], axis=1)
+tot = s[:, cols[-1]] - s[:, 0]
+print(f"envs={E} median total cycles/env-step={np.median(tot):.0f} (wave-lifetime, one env; s_memtime ticks = shader cycles)")
+for i, (_, n) in enumerate(SLOTS[1:]):
     print(f"  {n:20s} median {np.median(d[:, i]):9.0f}  mean {d[:, i].mean():9.0f}  share {d[:, i].sum() / tot.sum():6.1%}")
-print("py words/step median", np.median(s[:, 12]), " np words/step median", np.median(s[:, 13]))
+print("py words/step median", np.median(s[:, 12]), " np words/step median", np.median(s[:, 13]),
+      " contested movers median", np.median(s[:, 14]), " planners median", np.median(s[:, 11]))
+span = s[:, cols[-1]].max() - s[:, 0].min()
+print(f"launch span {span} ticks; sum of env lifetimes / span = {tot.sum() / span:.1f} concurrent envs")
 cnt = env.counts.view(E, 2).cpu().numpy()
 print("evacuated median", np.median(cnt[:, 0]), "dead median", np.median(cnt[:, 1]))
