@@ -50,13 +50,14 @@ constexpr int WR = 1024;             // MT ring words per stream (>= 624 + 227)
 constexpr int WRM = WR - 1;
 constexpr int WWIN = WR - 64 - 16;   // scoring words made readable per ensure
 constexpr int SHUF_WORDS = 384;      // words per lane-0 shuffle round (keeps mt_store_w's window valid)
-constexpr int CL_CAP = 1024;         // contested movers sorted in LDS (more: global scratch)
-constexpr int GH_CAP = 512;          // contested targets (groups) in LDS
+constexpr int CL_CAP = 510;          // contested movers sorted in LDS (more: global scratch); the np
+                                     // ring holds list (512 with sort padding) | heads 256 | starts 256
 constexpr int EV_CAP = 256;          // order-sensitive occupancy events
 constexpr int LEAF_CAP = 256;        // numpy pairwise leaves (n <= 16383 needs <= 128)
 constexpr int GRP_MAX = 128;         // movers of one contested target
 constexpr int GBITS = 13;            // group index bits in a sorted group head
 constexpr uint32_t DONEPK = 3u << 24;
+constexpr int GQ = 4;                // 64-person groups per pipelined iteration
 
 struct Geo {
     int L, W, GY, G, RW, P, R;
@@ -191,12 +192,6 @@ __device__ __forceinline__ void mt_store_w(uint32_t* ring, int& front, int head,
     if (lane == 0) gst[MT_N] = (uint32_t)(head - b);
 }
 
-__device__ __forceinline__ void mt_load_w(uint32_t* ring, const uint32_t* gst, int& head) {
-    for (int i = threadIdx.x; i < MT_N; i += 64) ring[i] = gst[i];
-    head = (int)gst[MT_N];
-    wave_fence();
-}
-
 // Ascending bitonic sort of a[0..n), n a power of two, by one wave.
 template <typename T>
 __device__ __forceinline__ void wave_sort(T* a, int n) {
@@ -214,6 +209,25 @@ __device__ __forceinline__ void wave_sort(T* a, int n) {
             }
             __syncthreads();  // one wave: waits for its own LDS / memory traffic
         }
+}
+
+// Sort a[0..n) ascending (distinct keys): n <= 64 by rank (each lane counts the
+// keys below its own, readlane broadcast), else bitonic over the power-of-two
+// padded array (the caller pads with 0xffffffff).
+template <typename T>
+__device__ __forceinline__ void wave_sort_keys(T* a, int n, int n2) {
+    const int lane = threadIdx.x;
+    if (n <= 64) {
+        uint32_t k = 0xffffffffu;
+        if (lane < n) k = a[lane];
+        int rank = 0;
+        for (int j = 0; j < n; j++) rank += (uint32_t)__builtin_amdgcn_readlane((int)k, j) < k;
+        __syncthreads();
+        if (lane < n) a[rank] = k;
+        __syncthreads();
+    } else {
+        wave_sort(a, n2);
+    }
 }
 
 __host__ __device__ __forceinline__ int pow2_ceil(int n) {
@@ -237,7 +251,7 @@ __device__ __forceinline__ void contested_groups(T* Lp, T* heads, T* gstart, int
     const int n2 = pow2_ceil(n);
     for (int i = n + lane; i < n2; i += 64) Lp[i] = 0xffffffffu;
     __syncthreads();
-    wave_sort(Lp, n2);
+    wave_sort_keys(Lp, n, n2);
     int ngrp = 0;
     for (int i0 = 0; i0 < n; i0 += 64) {
         const int i = i0 + lane;
@@ -259,7 +273,7 @@ __device__ __forceinline__ void contested_groups(T* Lp, T* heads, T* gstart, int
     const int h2 = pow2_ceil(ngrp);
     for (int i = ngrp + lane; i < h2; i += 64) heads[i] = 0xffffffffu;
     __syncthreads();
-    wave_sort(heads, h2);
+    wave_sort_keys(heads, ngrp, h2);
     int k = 0;
     while (k < ngrp) {
         mt_ensure_w(pyring, py_front, py_head + SHUF_WORDS);
@@ -275,29 +289,71 @@ __device__ __forceinline__ void contested_groups(T* Lp, T* heads, T* gstart, int
                     nk++;
                     continue;
                 }
-                for (int j = 0; j < cnt; j++) grp[j] = Lp[s + j] & pmask;
                 int head = nh;
                 bool ok = true;
-                for (int i = cnt - 1; i >= 1 && ok; i--) {  // random.shuffle: _randbelow(i + 1)
-                    const uint32_t bound = (uint32_t)(i + 1);
-                    const int kb = bit_length(bound);
-                    uint32_t r;
-                    do {
-                        if (head >= avail) {
-                            ok = false;
-                            break;
-                        }
-                        r = mt_word(pyring, WRM, head++) >> (32 - kb);
-                    } while (r >= bound);
-                    if (ok) {
-                        const uint32_t t = grp[i];
-                        grp[i] = grp[r];
-                        grp[r] = t;
+                if (cnt <= 8) {  // the usual case: movers and the next stream words in registers
+                    uint32_t a[8];
+#pragma unroll
+                    for (int j = 0; j < 8; j++) {
+                        a[j] = 0u;
+                        if (j < cnt) a[j] = Lp[s + j] & pmask;
                     }
+                    uint32_t w0 = pyring[head & WRM], w1 = pyring[(head + 1) & WRM], w2 = pyring[(head + 2) & WRM];
+#pragma unroll
+                    for (int i = 7; i >= 1; i--) {  // random.shuffle: _randbelow(i + 1)
+                        if (i < cnt && ok) {
+                            const uint32_t bound = (uint32_t)(i + 1);
+                            const int kb = bit_length(bound);
+                            uint32_t r;
+                            do {
+                                if (head >= avail) {
+                                    ok = false;
+                                    break;
+                                }
+                                r = mt_temper(w0) >> (32 - kb);
+                                w0 = w1;
+                                w1 = w2;
+                                w2 = pyring[(head + 3) & WRM];
+                                head++;
+                            } while (r >= bound);
+                            if (ok) {  // swap a[i], a[r] by selects (r is data-dependent)
+                                uint32_t ar = a[0];
+#pragma unroll
+                                for (int j = 1; j < i; j++) ar = (r == (uint32_t)j) ? a[j] : ar;
+                                const uint32_t ai = a[i];
+#pragma unroll
+                                for (int j = 0; j < i; j++) a[j] = (r == (uint32_t)j) ? ai : a[j];
+                                a[i] = (r == (uint32_t)i) ? ai : ar;
+                            }
+                        }
+                    }
+                    if (!ok) break;  // out of words: retry this group next round
+#pragma unroll
+                    for (int j = 1; j < 8; j++)
+                        if (j < cnt) lost[a[j] >> 5] |= 1u << (a[j] & 31);
+                } else {
+                    for (int j = 0; j < cnt; j++) grp[j] = Lp[s + j] & pmask;
+                    for (int i = cnt - 1; i >= 1 && ok; i--) {  // random.shuffle: _randbelow(i + 1)
+                        const uint32_t bound = (uint32_t)(i + 1);
+                        const int kb = bit_length(bound);
+                        uint32_t r;
+                        do {
+                            if (head >= avail) {
+                                ok = false;
+                                break;
+                            }
+                            r = mt_word(pyring, WRM, head++) >> (32 - kb);
+                        } while (r >= bound);
+                        if (ok) {
+                            const uint32_t t = grp[i];
+                            grp[i] = grp[r];
+                            grp[r] = t;
+                        }
+                    }
+                    if (!ok) break;  // out of words: retry this group next round
+                    for (int j = 1; j < cnt; j++) lost[grp[j] >> 5] |= 1u << (grp[j] & 31);
                 }
-                if (!ok) break;  // out of words: retry this group next round
                 nh = head;
-                for (int j = 1; j < cnt; j++) lost[grp[j] >> 5] |= 1u << (grp[j] & 31);
                 nk++;
             }
         }
@@ -326,20 +382,27 @@ __device__ __forceinline__ int find_pf(const uint32_t* Lp, int n, int t, int pb)
 }
 
 struct WaveLds {  // word offsets into dynamic LDS
-    int pyring, npring, aux, rmapb, tbits, cbits, obits, lost, robots, misc, total;
+    int pyring, npring, aux, rmapb, tbits, cbits, vac, nearc, lost, robots, misc, total;
 };
 
-__host__ __device__ inline WaveLds wave_lds(int G, int P, int R) {
+__host__ __device__ inline WaveLds wave_lds(int L, int W, int P, int R) {
     WaveLds s;
+    const int G = (L + 2) * (W + 2);
     const int RW = (G + 31) / 32;
+    const int NCW = (((L + 2 + 3) >> 2) * ((W + 2 + 3) >> 2) + 31) / 32;
     int o = 0;
-    s.pyring = o; o += WR;                 // reward phase: leaf sums | leaf buffer
-    s.npring = o; o += WR;                 // after the rows: contested list (CL_CAP)
-    s.aux = o; o += 2 * GH_CAP + 16;       // group heads | group starts; events; leaf table
+    s.pyring = o; o += WR;                 // after the shuffles: vacated-cell bitmap; reward: leaf sums | leaf buffer
+    s.npring = o; o += WR;                 // after the rows: contested list | group heads | group starts
+    s.aux = o; o += 512 + 16;              // planner queue + health group; events; leaf table
     s.rmapb = o; o += RW;
     s.tbits = o; o += RW;
     s.cbits = o; o += RW;
-    s.obits = o; o += RW;                  // near-robot cells while planning, vacated cells after
+    if (RW <= WR) {
+        s.vac = s.pyring;
+    } else {
+        s.vac = o; o += RW;
+    }
+    s.nearc = o; o += NCW;
     s.lost = o; o += (P + 31) / 32;
     s.robots = o; o += R;
     o = (o + 1) & ~1;
@@ -362,17 +425,37 @@ __device__ __forceinline__ int pb_bits(int P) { return P > 1 ? bit_length((uint3
 #define EVX_STAMP(i)                                                                                   \
     do {                                                                                               \
         if (out.stamps && threadIdx.x == 0)                                                            \
-            out.stamps[(size_t)blockIdx.x * 16 + (i)] = (int64_t)__builtin_amdgcn_s_memtime();         \
+            out.stamps[(size_t)blockIdx.x * 32 + (i)] = (int64_t)__builtin_amdgcn_s_memtime();         \
     } while (0)
 #define EVX_RSTAMP(i)                                                                                  \
     do {                                                                                               \
         if (out.stamps && threadIdx.x == 0)                                                            \
-            out.stamps[(size_t)blockIdx.x * 16 + (i)] = (int64_t)__builtin_amdgcn_s_memrealtime();     \
+            out.stamps[(size_t)blockIdx.x * 32 + (i)] = (int64_t)__builtin_amdgcn_s_memrealtime();     \
     } while (0)
 #define EVX_COUNT(i, v)                                                                                \
     do {                                                                                               \
-        if (out.stamps && threadIdx.x == 0) out.stamps[(size_t)blockIdx.x * 16 + (i)] = (v);           \
+        if (out.stamps && threadIdx.x == 0) out.stamps[(size_t)blockIdx.x * 32 + (i)] = (v);           \
     } while (0)
+
+// EVX_PROFILE builds only: cycle accumulators of sub-phases, stored to slots 16..31
+#ifdef EVX_PROFILE
+#define PT_DECL(n) long long pt_##n = 0, pt0_##n = 0
+#define PT_BEGIN(n) pt0_##n = __builtin_amdgcn_s_memtime()
+#define PT_END(n) pt_##n += __builtin_amdgcn_s_memtime() - pt0_##n
+#define PT_STORE(n, slot) EVX_COUNT(slot, pt_##n)
+#else
+#define PT_DECL(n)
+#define PT_BEGIN(n)
+#define PT_END(n)
+#define PT_STORE(n, slot)
+#endif
+
+// Pin a loaded value: the wait for its load happens here, before any later load
+// is issued (vmcnt waits are in-order, so a first use placed after the next
+// prefetch would also wait for that prefetch).
+__device__ __forceinline__ void pin(uint32_t v) { asm volatile("" ::"v"(v)); }
+__device__ __forceinline__ void pin(uint2 v) { asm volatile("" ::"v"(v.x), "v"(v.y)); }
+__device__ __forceinline__ void pin(double v) { asm volatile("" ::"v"(v)); }
 
 __device__ __forceinline__ double readlane_d(double v, int k) {
     const int lo = __builtin_amdgcn_readlane(__double2loint(v), k);
@@ -393,14 +476,16 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
     const int P = g.P, R = g.R, GY = g.GY;
     const int NR = (P + 63) >> 6;
     const int pb = pb_bits(P);
-    const WaveLds S = wave_lds(g.G, P, R);
+    const WaveLds S = wave_lds(g.L, g.W, P, R);
     uint32_t* pyring = smem + S.pyring;
     uint32_t* npring = smem + S.npring;
     uint32_t* aux = smem + S.aux;
     uint32_t* rmapb = smem + S.rmapb;
     uint32_t* tbits = smem + S.tbits;
     uint32_t* cbits = smem + S.cbits;
-    uint32_t* obits = smem + S.obits;
+    uint32_t* vac = smem + S.vac;
+    uint32_t* nearc = smem + S.nearc;
+    const int NCW = (((g.L + 2 + 3) >> 2) * ((GY + 3) >> 2) + 31) / 32;
     uint32_t* lost = smem + S.lost;
     uint32_t* robots = smem + S.robots;
     uint32_t* misc = smem + S.misc;
@@ -422,16 +507,52 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
     const int* scal_g = st.scal + (size_t)e * 4;
     const int fs = scal_g[0], cur_step = scal_g[1], prev_evac = scal_g[2], prev_dead = scal_g[3];
     uint32_t view = st.view[e];
-    for (int i = lane; i < g.RW; i += 64) {
-        rmapb[i] = st.rmap[(size_t)e * g.RW + i];
-        tbits[i] = 0;
-        cbits[i] = 0;
-        obits[i] = 0;
+    PT_DECL(ld1);
+    PT_DECL(ld2);
+    PT_DECL(ld3);
+    PT_BEGIN(ld1);
+    // every global read of this phase is issued before any of it is used
+    const uint32_t* gpy = st.py_mt + (size_t)e * EVX_MT_WORDS;
+    const uint32_t* gnp = st.np_mt + (size_t)e * EVX_MT_WORDS;
+    uint32_t wpy[10], wnp[10];
+#pragma unroll
+    for (int j = 0; j < 10; j++) {
+        wpy[j] = 0u;
+        wnp[j] = 0u;
+        if (lane + 64 * j < EVX_MT_WORDS) {
+            wpy[j] = gpy[lane + 64 * j];
+            wnp[j] = gnp[lane + 64 * j];
+        }
     }
+    const uint32_t* grm = st.rmap + (size_t)e * g.RW;
+    for (int i0 = 0; i0 < g.RW; i0 += 16 * 64) {
+        uint32_t w[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            w[j] = 0u;
+            if (i0 + 64 * j + lane < g.RW) w[j] = grm[i0 + 64 * j + lane];
+        }
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            const int i = i0 + 64 * j + lane;
+            if (i < g.RW) {
+                rmapb[i] = w[j];
+                tbits[i] = 0;
+                cbits[i] = 0;
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 10; j++) {
+        if (lane + 64 * j < MT_N) {
+            pyring[lane + 64 * j] = wpy[j];
+            npring[lane + 64 * j] = wnp[j];
+        }
+    }
+    int py_head = __builtin_amdgcn_readlane((int)wpy[9], MT_N - 576);  // word 624 = index
+    int np_head = __builtin_amdgcn_readlane((int)wnp[9], MT_N - 576);
     for (int i = lane; i < (P + 31) / 32; i += 64) lost[i] = 0;
-    int py_head, np_head;
-    mt_load_w(pyring, st.py_mt + (size_t)e * EVX_MT_WORDS, py_head);
-    mt_load_w(npring, st.np_mt + (size_t)e * EVX_MT_WORDS, np_head);
+    for (int i = lane; i < NCW; i += 64) nearc[i] = 0;
     int py_front = MT_N, np_front = MT_N;
     // Map.move_robot for every robot (envs/map.py:160-201); robots never interact.
     bool valid_a0 = false;
@@ -454,6 +575,8 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
         st.robots[(size_t)e * R + r] = rp;
         if (r == 0) valid_a0 = (a >= 0 && a <= 4);
     }
+    PT_END(ld1);
+    PT_BEGIN(ld2);
     // the not-dead persons in person order (sum(... if not p.dead) and the movers
     // never look at anyone else)
     int nnd = 0, n_safe = 0;
@@ -476,29 +599,35 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
         }
     }
     wave_fence();
+    PT_END(ld2);
+    PT_BEGIN(ld3);
     if (__shfl((int)valid_a0, 0)) view = robots[0];  // robot_position refreshed only after a valid action
-    // cells within repel range of some robot (d^2 < repel_d2): the only place the
-    // per-robot distance loop can change a score (People.find_best_direction)
+    // Coarse near-robot map: 4x4-cell blocks that may hold a cell within the repel
+    // range of some robot; only there does find_best_direction's robot loop run.
     const int rd2 = lay.repel_d2;
+    const int BY = (GY + 3) >> 2;
     if (rd2 > 0) {
         int rr = 0;
         while ((rr + 1) * (rr + 1) < rd2) rr++;
-        const int side = 2 * rr + 1, win = side * side;
-        const float inv_side = 1.0f / (float)side;
         for (int r = 0; r < R; r++) {
             const uint32_t rp = robots[r];
-            for (int c = lane; c < win; c += 64) {
-                const int q = (int)(((float)c + 0.5f) * inv_side);  // c / side, exact for c < 2^20
-                const int dx = q - rr, dy = c - q * side - rr;
-                const int x = rp_x(rp) + dx, y = rp_y(rp) + dy;
-                if (dx * dx + dy * dy < rd2 && x >= 0 && x <= g.L + 1 && y >= 0 && y <= g.W + 1) {
-                    const int cc = x * GY + y;
-                    atomicOr(&obits[cc >> 5], 1u << (cc & 31));
-                }
+            const int bx0 = max(rp_x(rp) - rr, 0) >> 2, bx1 = min(rp_x(rp) + rr, g.L + 1) >> 2;
+            const int by0 = max(rp_y(rp) - rr, 0) >> 2, by1 = min(rp_y(rp) + rr, g.W + 1) >> 2;
+            if (bx1 < bx0 || by1 < by0) continue;
+            const int nby = by1 - by0 + 1;
+            const float inv = 1.0f / (float)nby;
+            for (int c = lane; c < (bx1 - bx0 + 1) * nby; c += 64) {
+                const int q = (int)(((float)c + 0.5f) * inv);  // c / nby, exact for c < 2^20
+                const int b = (bx0 + q) * BY + by0 + (c - q * nby);
+                atomicOr(&nearc[b >> 5], 1u << (b & 31));
             }
         }
     }
     __syncthreads();  // not-dead list and LDS tables complete
+    PT_END(ld3);
+    PT_STORE(ld1, 27);
+    PT_STORE(ld2, 28);
+    PT_STORE(ld3, 29);
     EVX_STAMP(1);
 
     // --------------------- People.run phases 1+2 (health, accumulate, plan)
@@ -509,32 +638,23 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
 #pragma unroll
     for (int d = 0; d < 8; d++) doff[d] = move_dx(d) * GY + move_dy(d);
 
-    // one-row-ahead prefetch of what a row reads from HBM
-    const uint2 NOONE = make_uint2(0u, DONEPK);
-    uint2 eN = NOONE, eNN = NOONE;
-    if (lane < nnd) eN = ndl[lane];
-    if (64 + lane < nnd) eNN = ndl[64 + lane];
-    double hN = 0.0, aN = 0.0, dN = 0.0;
-    uint32_t nvN = 0;
-    if (lane < nnd) {
-        hN = h_g[eN.x];
-        if (!((eN.y >> 24) & 3u)) {
-            const int c = pk_x(eN.y) * GY + pk_y(eN.y);
-            aN = a_g[eN.x];
-            dN = dpt[c];
-            nvN = nbv[c];
-        }
-    }
-    const int NRD = (nnd + 63) >> 6;
     int nplan = 0, n_died = 0;
     bool any_cont = false;
+    PT_DECL(np);
+    PT_DECL(hsum);
+    PT_DECL(plan);
+    PT_DECL(drain);
+    PT_DECL(top);
+    PT_DECL(rew);
+    PT_DECL(leaf);
+    PT_DECL(rtop);
     double total = 0.0;  // CPython sum(p.health for p in self.people.list if not p.dead): sequential
-    double* hc = reinterpret_cast<double*>(aux + 384);  // one row of not-dead healths (lane 0 sums them)
     // Planners wait in an LDS queue and are scored 64 at a time (scoring is the
     // heavy part and only a few persons per row plan).
-    uint32_t* qa = aux;        // person | candidate mask << 16
+    uint32_t* qa = aux;        // person | candidate mask << 16   (<= 127 queued)
     uint32_t* qb = aux + 128;  // x | y << 12
-    int* qc = reinterpret_cast<int*>(aux + 256);  // first Python-stream word
+    int* qc = reinterpret_cast<int*>(aux + 256);        // first Python-stream word
+    double* hc = reinterpret_cast<double*>(aux + 384);  // one group of not-dead healths (lane 0 sums them)
     int qn = 0;
     auto score_batch = [&](int n) {  // People.find_best_direction for queue entries [0, n)
         const bool has = lane < n;
@@ -568,11 +688,10 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
 #pragma unroll
                 for (int d = 0; d < 8; d++) {
                     if ((cand >> d) & 1u) {
-                        const int nc = cold + doff[d];
+                        const int nx = x + move_dx(d), ny = y + move_dy(d);
                         const double delta_p = f0 - f[d];
                         double effect = 0.0;
-                        if (bit_get(obits, nc)) {
-                            const int nx = x + move_dx(d), ny = y + move_dy(d);
+                        if (bit_get(nearc, (nx >> 2) * BY + (ny >> 2))) {
                             int md2 = 0x7fffffff;
                             for (int r = 0; r < R; r++) {
                                 const uint32_t rp = robots[r];
@@ -607,28 +726,12 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
         }
         nplan += __popcll(mm);
     };
-    for (int row = 0; row < NRD; row++) {
-        const int i = row * 64 + lane;
+    // one group (64 list entries, in person order) of People.run phases 1+2
+    auto person_half = [&](int i, uint2 en, double hh, double ac, double dg, uint32_t nv) {
+        PT_BEGIN(np);
         const bool inr = i < nnd;
-        const int p = (int)eN.x;
-        const uint32_t v = eN.y;
-        double hh = hN, ac = aN;
-        const double dg = dN;
-        const uint32_t nv = nvN;
-        // issue the next row's loads
-        eN = eNN;
-        if (i + 64 < nnd) {
-            hN = h_g[eN.x];
-            if (!((eN.y >> 24) & 3u)) {
-                const int c = pk_x(eN.y) * GY + pk_y(eN.y);
-                aN = a_g[eN.x];
-                dN = dpt[c];
-                nvN = nbv[c];
-            }
-        }
-        eNN = NOONE;
-        if (i + 128 < nnd) eNN = ndl[i + 128];
-
+        const int p = (int)en.x;
+        const uint32_t v = en.y;
         const bool act = inr && !((v >> 24) & 3u);
         const int x = pk_x(v), y = pk_y(v), cold = x * GY + y;
         // phase 1: Person.update_state -> update_health (numpy stream)
@@ -648,23 +751,39 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
             np_head += tot;
         }
         n_died += __popcll(__ballot(died));
-        {  // health total over the still-not-dead, in person order (lane 0)
-            const unsigned long long hm = __ballot(inr && !died);
-            if (inr && !died) hc[lanes_below(hm)] = hh;
+        PT_END(np);
+        PT_BEGIN(hsum);
+        {  // health total over the still-not-dead, in person order (lane 0). The
+           // group's values are compacted to the front of 64 slots, the rest +0.0
+           // (healths are >= +0, so adding +0.0 leaves the running sum unchanged),
+           // and folded with 16 values in flight.
+            const bool hv = inr && !died;
+            const unsigned long long hm = __ballot(hv);
+            hc[hv ? lanes_below(hm) : __popcll(hm) + lanes_below(~hm)] = hv ? hh : 0.0;
             wave_fence();
             if (lane == 0) {
-                const int nh = __popcll(hm);
                 const double2* h2 = reinterpret_cast<const double2*>(hc);
-                int k = 0;
-                for (; k + 8 <= nh; k += 8) {
-                    const double2 a0 = h2[k / 2], a1 = h2[k / 2 + 1], a2 = h2[k / 2 + 2], a3 = h2[k / 2 + 3];
-                    total += a0.x; total += a0.y; total += a1.x; total += a1.y;
-                    total += a2.x; total += a2.y; total += a3.x; total += a3.y;
+                double2 q0 = h2[0], q1 = h2[1], q2 = h2[2], q3 = h2[3];
+                double2 r0 = h2[4], r1 = h2[5], r2 = h2[6], r3 = h2[7];
+#pragma unroll
+                for (int c = 0; c < 8; c++) {
+                    double2 s0 = q0, s1 = q1, s2 = q2, s3 = q3;
+                    if (c + 2 < 8) {
+                        s0 = h2[4 * (c + 2)];
+                        s1 = h2[4 * (c + 2) + 1];
+                        s2 = h2[4 * (c + 2) + 2];
+                        s3 = h2[4 * (c + 2) + 3];
+                    }
+                    total += q0.x; total += q0.y; total += q1.x; total += q1.y;
+                    total += q2.x; total += q2.y; total += q3.x; total += q3.y;
+                    q0 = r0; q1 = r1; q2 = r2; q3 = r3;
+                    r0 = s0; r1 = s1; r2 = s2; r3 = s3;
                 }
-                for (; k < nh; k++) total += hc[k];
             }
             wave_fence();
         }
+        PT_END(hsum);
+        PT_BEGIN(plan);
         // phase 2: accumulate; candidates of find_best_direction
         bool planner = false;
         if (alive) {
@@ -703,30 +822,109 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
         if (need) h_g[p] = hh;
         if (alive) a_g[p] = ac;
         if (died) pk_g[p] = v | (2u << 24);
-        if (qn >= 64) {
-            wave_fence();
-            score_batch(64);
-            const int rest = qn - 64;  // move entries [64, qn) to the front
-            uint32_t ta = 0, tb = 0;
-            int tc = 0;
-            if (lane < rest) {
-                ta = qa[64 + lane];
-                tb = qb[64 + lane];
-                tc = qc[64 + lane];
+        PT_END(plan);
+    };
+    // Four 64-person groups per iteration: the next iteration's data and the
+    // list entries of the one after are in flight while this one computes. The
+    // per-group body exists once (a group is picked by selects), as does the scorer.
+    const uint2 NOONE = make_uint2(0u, DONEPK);
+    auto load_entry = [&](int i) -> uint2 {
+        uint2 en = NOONE;
+        if (i < nnd) en = ndl[i];
+        return en;
+    };
+    auto load_data = [&](int i, uint2 en, double& h, double& a, double& dg, uint32_t& nv) {
+        h = 0.0; a = 0.0; dg = 0.0; nv = 0u;
+        if (i < nnd) {
+            h = h_g[en.x];
+            if (!((en.y >> 24) & 3u)) {
+                const int c = pk_x(en.y) * GY + pk_y(en.y);
+                a = a_g[en.x];
+                dg = dpt[c];
+                nv = nbv[c];
             }
-            wave_fence();
-            if (lane < rest) {
-                qa[lane] = ta;
-                qb[lane] = tb;
-                qc[lane] = tc;
-            }
-            qn = rest;
-            wave_fence();
         }
+    };
+    uint2 nxe[GQ], nne[GQ];
+    double nxh[GQ], nxa[GQ], nxg[GQ];
+    uint32_t nxv[GQ];
+#pragma unroll
+    for (int k = 0; k < GQ; k++) {
+        nxe[k] = load_entry(64 * k + lane);
+        nne[k] = load_entry(64 * (GQ + k) + lane);
     }
-    if (qn > 0) {
-        wave_fence();
-        score_batch(qn);
+#pragma unroll
+    for (int k = 0; k < GQ; k++) load_data(64 * k + lane, nxe[k], nxh[k], nxa[k], nxg[k], nxv[k]);
+    const int NIT = (nnd + 64 * GQ - 1) / (64 * GQ);
+    for (int it = 0; it <= NIT; it++) {  // the extra iteration only drains the planner queue
+        PT_BEGIN(top);
+        const int i0 = it * 64 * GQ + lane;
+        uint2 ce[GQ];
+        double chh[GQ], caa[GQ], cgg[GQ];
+        uint32_t cvv[GQ];
+#pragma unroll
+        for (int k = 0; k < GQ; k++) {
+            ce[k] = nxe[k];
+            chh[k] = nxh[k];
+            caa[k] = nxa[k];
+            cgg[k] = nxg[k];
+            cvv[k] = nxv[k];
+            nxe[k] = nne[k];
+            pin(ce[k]);
+            pin(chh[k]);
+            pin(caa[k]);
+            pin(cgg[k]);
+            pin(cvv[k]);
+            pin(nxe[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < GQ; k++) load_data(i0 + 64 * (GQ + k), nxe[k], nxh[k], nxa[k], nxg[k], nxv[k]);
+#pragma unroll
+        for (int k = 0; k < GQ; k++) nne[k] = load_entry(i0 + 64 * (2 * GQ + k));
+#pragma clang loop unroll(disable)
+        for (int k = 0; k < GQ; k++) {
+            uint2 en = ce[0];
+            double hh = chh[0], ac = caa[0], dg = cgg[0];
+            uint32_t nv = cvv[0];
+#pragma unroll
+            for (int j = 1; j < GQ; j++) {
+                if (k == j) {
+                    en = ce[j];
+                    hh = chh[j];
+                    ac = caa[j];
+                    dg = cgg[j];
+                    nv = cvv[j];
+                }
+            }
+            PT_END(top);
+            person_half(i0 + 64 * k, en, hh, ac, dg, nv);
+            const bool fin = it == NIT && k == GQ - 1;
+            PT_BEGIN(drain);
+            while (qn >= 64 || (fin && qn > 0)) {
+                const int n = min(qn, 64);
+                wave_fence();
+                score_batch(n);
+                const int rest = qn - n;  // move entries [n, qn) to the front (rest <= 63)
+                uint32_t ta = 0, tb = 0;
+                int tc = 0;
+                if (lane < rest) {
+                    ta = qa[n + lane];
+                    tb = qb[n + lane];
+                    tc = qc[n + lane];
+                }
+                wave_fence();
+                if (lane < rest) {
+                    qa[lane] = ta;
+                    qb[lane] = tb;
+                    qc[lane] = tc;
+                }
+                qn = rest;
+                wave_fence();
+            }
+            PT_END(drain);
+            PT_BEGIN(top);
+        }
+        PT_END(top);
     }
     // the numpy stream is finished for this step
     mt_store_w(npring, np_front, np_head, st.np_mt + (size_t)e * EVX_MT_WORDS);
@@ -739,6 +937,10 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
     // ------------------------- contested targets: groups, shuffle, losers
     int err = 0;
     int ncont = 0;
+    PT_DECL(lp);
+    PT_DECL(grp);
+    PT_DECL(mts);
+    PT_BEGIN(lp);
     uint32_t* Lp = npring;  // the numpy ring is free now
     if (any_cont) {
         for (int i0 = 0; i0 < nplan; i0 += 64) {
@@ -756,8 +958,10 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
             if (c && pos < CL_CAP) Lp[pos] = key;
             ncont += __popcll(m);
         }
+        PT_END(lp);
+        PT_BEGIN(grp);
         if (ncont <= CL_CAP) {
-            contested_groups(Lp, aux, aux + GH_CAP, ncont, pb, pyring, py_front, py_head, lost, misc, err);
+            contested_groups(Lp, npring + 512, npring + 768, ncont, pb, pyring, py_front, py_head, lost, misc, err);
         } else {  // rare: sort in this env's global scratch
             Lp = Lg;
             int k = 0;
@@ -779,12 +983,18 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
             contested_groups(Lg, Hg, Sg, ncont, pb, pyring, py_front, py_head, lost, misc, err);
         }
     }
+    PT_END(grp);
+    PT_BEGIN(mts);
     EVX_COUNT(14, ncont);
     mt_store_w(pyring, py_front, py_head, st.py_mt + (size_t)e * EVX_MT_WORDS);
     EVX_COUNT(12, py_head);
-    // near-robot bits are done: obits becomes "vacated by a winner"
-    for (int i = lane; i < g.RW; i += 64) obits[i] = 0;
+    // the Python stream is stored: its ring becomes the "vacated by a winner" bitmap
+    for (int i = lane; i < g.RW; i += 64) vac[i] = 0;
     __syncthreads();
+    PT_END(mts);
+    PT_STORE(lp, 24);
+    PT_STORE(grp, 25);
+    PT_STORE(mts, 26);
     EVX_STAMP(3);
 
     // --------------------------------------------- execute_move, in order
@@ -795,7 +1005,7 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
             const int cold = (int)(en.y & 0xffffffu);
             const int t = cold + doff_of(en.y >> 24, GY);
             const bool win = !bit_get(cbits, t) || !bit_get(lost, (int)en.x);
-            if (win) atomicOr(&obits[cold >> 5], 1u << (cold & 31));
+            if (win) atomicOr(&vac[cold >> 5], 1u << (cold & 31));
             if (st.thmap) atomicAdd(&st.thmap[(size_t)e * g.G + (win ? t : cold)], 1);
         }
     }
@@ -816,7 +1026,7 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
             if (!cont || !bit_get(lost, p)) {
                 const bool ex = (lay.cellinfo[t] >> 1) & 1u;
                 exw = ex;
-                const bool ev_old = bit_get(tbits, cold), ev_new = bit_get(obits, t);
+                const bool ev_old = bit_get(tbits, cold), ev_new = bit_get(vac, t);
                 int pf = p;
                 if ((ev_old || ev_new) && cont) pf = find_pf(Lp, ncont, t, pb);
                 if (ev_old) {
@@ -887,23 +1097,8 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
     double gq_t = 0.0;
     int q = 0, lb_base = 0, cur = 0;
     // remaining persons = the not-dead list minus this step's deaths and evacuations
-    uint32_t iNN = 0u, wN = DONEPK;
-    double hvN = 0.0;
-    if (lane < nnd) {
-        const uint32_t iN = ndl[lane].x;
-        wN = pk_g[iN];
-        hvN = h_g[iN];
-    }
-    if (64 + lane < nnd) iNN = ndl[64 + lane].x;
-    for (int row = 0; row < NRD; row++) {
-        const int i = row * 64 + lane;
-        const uint32_t v = wN;
-        const double hv = hvN;
-        if (i + 64 < nnd) {
-            wN = pk_g[iNN];
-            hvN = h_g[iNN];
-        }
-        if (i + 128 < nnd) iNN = ndl[i + 128].x;
+    auto reward_half = [&](int i, uint32_t v, double hv) {
+        PT_BEGIN(rew);
         const bool rem = i < nnd && !pk_safe(v) && !pk_dead(v);
         const long long x2 = 2 * pk_x(v) + 1, y2 = 2 * pk_y(v) + 1;
         const long long dxr = x2 - 2LL * vx, dyr = y2 - 2LL * vy;
@@ -920,14 +1115,23 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
         if (rem) lb[q + lanes_below(rm) - lb_base] = 0.5 * sqrt((double)n4);
         q += __popcll(rm);
         wave_fence();
+        PT_END(rew);
+        PT_BEGIN(leaf);
         // numpy pairwise leaves that are now complete
         while (cur < nleaf && q >= ltab[cur] + ltab[LEAF_CAP + cur]) {
             const int len = ltab[LEAF_CAP + cur], o = ltab[cur] - lb_base;
             const int len8 = len - (len % 8);
             double r = 0.0;
-            if (len >= 8 && lane < 8) {
-                r = lb[o + lane];
-                for (int k = 8 + lane; k < len8; k += 8) r += lb[o + k];
+            if (len >= 8 && lane < 8) {  // chain `lane`: a[lane] + a[lane+8] + ..., all 16 reads in flight
+                double a[16];
+#pragma unroll
+                for (int k = 0; k < 16; k++) {
+                    a[k] = 0.0;  // padding: d + 0.0 == d for the non-negative distances
+                    if (8 * k < len8) a[k] = lb[o + 8 * k + lane];
+                }
+                r = a[0];
+#pragma unroll
+                for (int k = 1; k < 16; k++) r += a[k];
             }
             if (len >= 8) {
                 const double r0 = readlane_d(r, 0), r1 = readlane_d(r, 1), r2 = readlane_d(r, 2),
@@ -960,8 +1164,74 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
             lb_base = nb;
         }
         wave_fence();
+        PT_END(leaf);
+    };
+    auto load_idx = [&](int i) -> uint32_t {
+        uint32_t p = 0u;
+        if (i < nnd) p = ndl[i].x;
+        return p;
+    };
+    auto load_pw = [&](int i, uint32_t p, uint32_t& w, double& h) {
+        w = DONEPK;
+        h = 0.0;
+        if (i < nnd) {
+            w = pk_g[p];
+            h = h_g[p];
+        }
+    };
+    uint32_t nxj[GQ], nnj[GQ], nxw[GQ];
+    double nxhv[GQ];
+#pragma unroll
+    for (int k = 0; k < GQ; k++) {
+        nxj[k] = load_idx(64 * k + lane);
+        nnj[k] = load_idx(64 * (GQ + k) + lane);
+    }
+#pragma unroll
+    for (int k = 0; k < GQ; k++) load_pw(64 * k + lane, nxj[k], nxw[k], nxhv[k]);
+    for (int it = 0; it < NIT; it++) {
+        PT_BEGIN(rtop);
+        const int i0 = it * 64 * GQ + lane;
+        uint32_t cw[GQ];
+        double ch[GQ];
+#pragma unroll
+        for (int k = 0; k < GQ; k++) {
+            cw[k] = nxw[k];
+            ch[k] = nxhv[k];
+            nxj[k] = nnj[k];
+            pin(cw[k]);
+            pin(ch[k]);
+            pin(nxj[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < GQ; k++) load_pw(i0 + 64 * (GQ + k), nxj[k], nxw[k], nxhv[k]);
+#pragma unroll
+        for (int k = 0; k < GQ; k++) nnj[k] = load_idx(i0 + 64 * (2 * GQ + k));
+#pragma clang loop unroll(disable)
+        for (int k = 0; k < GQ; k++) {
+            uint32_t w = cw[0];
+            double h = ch[0];
+#pragma unroll
+            for (int j = 1; j < GQ; j++) {
+                if (k == j) {
+                    w = cw[j];
+                    h = ch[j];
+                }
+            }
+            PT_END(rtop);
+            reward_half(i0 + 64 * k, w, h);
+            PT_BEGIN(rtop);
+        }
+        PT_END(rtop);
     }
     const double gq = wave_sum_d(gq_t);  // multiples of 0.5: exact in any order
+    PT_STORE(np, 16);
+    PT_STORE(hsum, 17);
+    PT_STORE(plan, 18);
+    PT_STORE(drain, 19);
+    PT_STORE(top, 20);
+    PT_STORE(rew, 21);
+    PT_STORE(leaf, 22);
+    PT_STORE(rtop, 23);
     EVX_STAMP(5);
     if (lane == 0) {
         const int remaining = nrem;
@@ -1238,7 +1508,7 @@ const char* evx_last_error(void) { return g_err; }
 int64_t evx_step_lds_bytes(const evx_layout* l) {
     if (check_layout(l)) return -1;
     const int G = (l->L + 2) * (l->W + 2);
-    return (int64_t)evx::wave_lds(G, l->P, l->R).total * 4;
+    return (int64_t)evx::wave_lds(l->L, l->W, l->P, l->R).total * 4;
 }
 
 int64_t evx_step_scratch_words(const evx_layout* l) {
@@ -1260,7 +1530,7 @@ int evx_env_step(const evx_layout* l, const evx_state* s, const int32_t* actions
         while ((1LL << gb) < (long long)G) gb++;
         if (pb + gb > 32) return fail(-22, "grid cells x people too large for 32-bit move keys");
     }
-    const size_t lds = (size_t)evx::wave_lds(G, l->P, l->R).total * 4;
+    const size_t lds = (size_t)evx::wave_lds(l->L, l->W, l->P, l->R).total * 4;
     if (lds > 160 * 1024) return fail(-7, "layout needs more than 160 KiB of LDS");
     static bool attr_set = false;
     if (!attr_set) {

@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libevacx.so")
+# EVACX_LIB selects another in-tree build (e.g. libevacx_prof.so, the diagnostic one)
+LIB_PATH = os.path.join(HERE, os.environ.get("EVACX_LIB", "libevacx.so"))
 
 
 class EvacxError(RuntimeError):

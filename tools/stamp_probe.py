@@ -35,12 +35,12 @@ acts = torch.randint(0, 5, (args.warmup + 3, E * R), device="cuda", dtype=torch.
 for i in range(args.warmup):
     env.step(acts[i])
     env.reset(mask=env.done)
-stamps = torch.zeros(E * 16, dtype=torch.int64, device="cuda")
+stamps = torch.zeros(E * 32, dtype=torch.int64, device="cuda")
 env.out.stamps = _ptr(stamps)
 for i in range(3):
     env.step(acts[args.warmup + i])
 torch.cuda.synchronize()
-s = stamps.view(E, 16).cpu().numpy()
+s = stamps.view(E, 32).cpu().numpy()
 cols = [c for c, _ in SLOTS]
 d = np.diff(s[:, cols], axis=1)
 tot = s[:, cols[-1]] - s[:, 0]
@@ -49,7 +49,18 @@ for i, (_, n) in enumerate(SLOTS[1:]):
     print(f"  {n:20s} median {np.median(d[:, i]):9.0f}  mean {d[:, i].mean():9.0f}  share {d[:, i].sum() / tot.sum():6.1%}")
 print("py words/step median", np.median(s[:, 12]), " np words/step median", np.median(s[:, 13]),
       " contested movers median", np.median(s[:, 14]), " planners median", np.median(s[:, 11]))
-span = s[:, cols[-1]].max() - s[:, 0].min()
-print(f"launch span {span} ticks; sum of env lifetimes / span = {tot.sum() / span:.1f} concurrent envs")
+life = s[:, 10] - s[:, 9]  # s_memrealtime: constant 100 MHz on every XCD
+span = s[:, 10].max() - s[:, 9].min()
+print(f"launch span {span / 100:.1f} us; median env lifetime {np.median(life) / 100:.1f} us; "
+      f"mean concurrent envs {life.sum() / span:.0f} ({life.sum() / span / 256:.2f} per CU)")
+PROF = [(16, "rows: np draws+health"), (17, "rows: health sum"), (18, "rows: plan+queue+stores"),
+        (19, "rows: score batches"), (20, "rows: loop top+selects"), (21, "reward: per group"),
+        (22, "reward: leaves"), (23, "reward: loop top"), (24, "contested: list"), (25, "contested: groups"),
+        (26, "contested: mt_store+clear"), (27, "load: mt+rmap+robots"), (28, "load: not-dead list"),
+        (29, "load: near map+sync")]
+if s[:, 16:30].any():
+    print("sub-phase cycle accumulators (EVX_PROFILE build):")
+    for c, n in PROF:
+        print(f"  {n:28s} median {np.median(s[:, c]):9.0f}")
 cnt = env.counts.view(E, 2).cpu().numpy()
 print("evacuated median", np.median(cnt[:, 0]), "dead median", np.median(cnt[:, 1]))
