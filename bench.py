@@ -53,7 +53,10 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=1300)
+    ap.add_argument("--stagger", type=int, default=1200,
+                    help="warmup step w force-resets envs with global id %% stagger == w, so the timed steps see "
+                         "env ages spread over a whole episode (the stationary mix of a long run); 0 = off")
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
     ap.add_argument("--grid", type=int, default=128)
     ap.add_argument("--people", type=int, default=2276)
@@ -105,12 +108,19 @@ def main():
         return float(t.item())
 
     # ------------------------------------------------------------ warmup
-    for _ in range(args.warmup):
+    # Env ages are staggered over one episode length: a synchronised start would time
+    # only one episode phase (per-step cost varies several-fold over an episode).
+    gid = torch.arange(E, device="cuda") + rank * E
+    S = args.stagger
+    for w in range(args.warmup):
+        force = (gid % S == w) if 0 < S and w < S else None
         if args.mode == "train":
             tr.step()
+            if force is not None:
+                env.reset(mask=force)
         else:
             env.step(torch.randint(0, 5, (E * R,), device="cuda", dtype=torch.int32))
-            env.reset(mask=env.done)
+            env.reset(mask=env.done if force is None else (env.done.bool() | force))
     barrier()
 
     # the CPU baseline continues from exactly this state (same envs, same episode phase)
@@ -175,6 +185,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "stagger": args.stagger,
             "ms_per_step": 1e3 * elapsed / args.steps,
             "higher_is_better": True,
             "scaling": "weak",

@@ -169,9 +169,18 @@ __device__ __forceinline__ void mt_ensure_w(uint32_t* ring, int& front, int upto
     const int lane = threadIdx.x;
     while (front < upto) {
         const int cnt = min(MT_LAG, upto - front);
-        for (int t = lane; t < cnt; t += 64) {
-            const int n = front + t;
-            ring[n & WRM] = mt_twist1(ring[(n - MT_LAG) & WRM], ring[(n - 624) & WRM], ring[(n - 623) & WRM]);
+        uint32_t lag[4], a[4], b[4];  // every operand of the round is read before any word is written
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int n = front + lane + 64 * j;
+            lag[j] = ring[(n - MT_LAG) & WRM];
+            a[j] = ring[(n - 624) & WRM];
+            b[j] = ring[(n - 623) & WRM];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int n = front + lane + 64 * j;
+            if (lane + 64 * j < cnt) ring[n & WRM] = mt_twist1(lag[j], a[j], b[j]);
         }
         front += cnt;
         wave_fence();
@@ -239,8 +248,9 @@ __host__ __device__ __forceinline__ int pow2_ceil(int n) {
 // Contested targets of move_plan (envs/people.py:284-297): L[0..n) holds
 // (target << pb | person) of every planner whose target has >= 2 planners.
 // Sort -> groups (one per target, movers in person order); group heads sorted
-// by first planner = dict insertion order; lane 0 runs Lib/random.py shuffle
-// per group on the Python stream and marks the losers.
+// by first planner = dict insertion order; Lib/random.py shuffle per group on
+// the Python stream (positions found wave-uniformly, shuffles lane-parallel);
+// the losers are marked.
 __device__ __forceinline__ int doff_of(uint32_t d, int GY) { return move_dx((int)d) * GY + move_dy((int)d); }
 
 template <typename T>
@@ -274,100 +284,138 @@ __device__ __forceinline__ void contested_groups(T* Lp, T* heads, T* gstart, int
     for (int i = ngrp + lane; i < h2; i += 64) heads[i] = 0xffffffffu;
     __syncthreads();
     wave_sort_keys(heads, ngrp, h2);
+    // group descriptors in dict order: (first mover's position in Lp << 8) | size
+    for (int k = lane; k < ngrp; k += 64) {
+        const int gi = (int)(heads[k] & ((1u << GBITS) - 1u));
+        const int s0 = (int)gstart[gi], cnt = (int)gstart[gi + 1] - s0;
+        heads[k] = ((uint32_t)s0 << 8) | (uint32_t)min(cnt, 255);
+        if (cnt > GRP_MAX) err |= 1;  // > 128 movers on one target: not representable, flagged
+    }
+    err = __ballot(err != 0) ? (err | 1) : err;
+    __syncthreads();
+    // Pass 1 (wave-uniform): where each group's random.shuffle starts on the Python
+    // stream. _randbelow(b) accepts a word iff its top bit_length(b) bits are < b;
+    // per 64-word window the acceptance sets of b = 2..8 are ballots (lane b of
+    // mlo/mhi), so consuming one bound is a shift + count-trailing-zeros.
+    // Pass 2 (lane per group): every shuffle of the chunk runs in parallel from its
+    // recorded start word; only the winner (position 0 afterwards) moves.
+    int pos = py_head;
+    int B = -(1 << 30);  // window [B, B + 64) of the acceptance masks
+    uint32_t mlo = 0, mhi = 0;
     int k = 0;
     while (k < ngrp) {
-        mt_ensure_w(pyring, py_front, py_head + SHUF_WORDS);
-        __syncthreads();
-        int nk = k, nh = py_head, bad = 0;
-        if (lane == 0) {
-            const int avail = py_front;
-            while (nk < ngrp) {
-                const int gi = (int)(heads[nk] & ((1u << GBITS) - 1u));
-                const int s = (int)gstart[gi], cnt = (int)gstart[gi + 1] - s;
-                if (cnt > GRP_MAX) {  // > 128 movers on one target: not representable, flagged
-                    bad |= 1;
-                    nk++;
-                    continue;
-                }
-                int head = nh;
-                bool ok = true;
-                if (cnt <= 8) {  // the usual case: movers and the next stream words in registers
-                    uint32_t a[8];
+        const int k0 = k, W0 = pos;
+        uint32_t desc = 0;
+        if (k0 + lane < ngrp) desc = heads[k0 + lane];
+        int wv = 0;
+        int nk = 0;
+        while (nk < 64 && k < ngrp && pos - W0 < SHUF_WORDS) {
+            const uint32_t dsc = (uint32_t)__builtin_amdgcn_readlane((int)desc, nk);
+            const int cnt = (int)(dsc & 255u);
+            wv = lane == nk ? pos : wv;
+            for (int i = cnt - 1; i >= 1; i--) {
+                const int b = i + 1;
+                const int kb = bit_length((uint32_t)b);
+                while (true) {
+                    if (pos - B >= 64 || pos < B) {  // new window at pos
+                        B = pos;
+                        mt_ensure_w(pyring, py_front, B + 64);
+                        const uint32_t t = mt_temper(pyring[(B + lane) & WRM]);
+                        mlo = 0;
+                        mhi = 0;
 #pragma unroll
-                    for (int j = 0; j < 8; j++) {
-                        a[j] = 0u;
-                        if (j < cnt) a[j] = Lp[s + j] & pmask;
-                    }
-                    uint32_t w0 = pyring[head & WRM], w1 = pyring[(head + 1) & WRM], w2 = pyring[(head + 2) & WRM];
-#pragma unroll
-                    for (int i = 7; i >= 1; i--) {  // random.shuffle: _randbelow(i + 1)
-                        if (i < cnt && ok) {
-                            const uint32_t bound = (uint32_t)(i + 1);
-                            const int kb = bit_length(bound);
-                            uint32_t r;
-                            do {
-                                if (head >= avail) {
-                                    ok = false;
-                                    break;
-                                }
-                                r = mt_temper(w0) >> (32 - kb);
-                                w0 = w1;
-                                w1 = w2;
-                                w2 = pyring[(head + 3) & WRM];
-                                head++;
-                            } while (r >= bound);
-                            if (ok) {  // swap a[i], a[r] by selects (r is data-dependent)
-                                uint32_t ar = a[0];
-#pragma unroll
-                                for (int j = 1; j < i; j++) ar = (r == (uint32_t)j) ? a[j] : ar;
-                                const uint32_t ai = a[i];
-#pragma unroll
-                                for (int j = 0; j < i; j++) a[j] = (r == (uint32_t)j) ? ai : a[j];
-                                a[i] = (r == (uint32_t)i) ? ai : ar;
-                            }
+                        for (int bb = 2; bb <= 8; bb++) {
+                            const int kbb = bb < 4 ? 2 : (bb < 8 ? 3 : 4);
+                            const unsigned long long m = __ballot((t >> (32 - kbb)) < (uint32_t)bb);
+                            mlo = lane == bb ? (uint32_t)m : mlo;
+                            mhi = lane == bb ? (uint32_t)(m >> 32) : mhi;
                         }
                     }
-                    if (!ok) break;  // out of words: retry this group next round
+                    unsigned long long m;
+                    if (b <= 8) {
+                        m = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)mhi, b) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((int)mlo, b);
+                    } else {  // large group: test the words one by one
+                        const uint32_t t = mt_temper(pyring[(pos & WRM)]);
+                        m = ((t >> (32 - kb)) < (uint32_t)b) ? (1ull << (pos - B)) : 0ull;
+                    }
+                    m >>= (pos - B);
+                    if (b > 8 && !(m & 1ull)) {
+                        pos++;
+                        continue;
+                    }
+                    if (m) {
+                        pos += __builtin_ctzll(m) + 1;
+                        break;
+                    }
+                    pos = B + 64;
+                }
+            }
+            nk++;
+            k++;
+        }
+        __syncthreads();  // ring words [W0, pos) are in place
+        // Pass 2: lane j shuffles group k0 + j (Lib/random.py shuffle, in registers)
+        if (lane < nk) {
+            const int s0 = (int)(desc >> 8), cnt = (int)(desc & 255u);
+            int head = wv;
+            if (cnt <= 8) {
+                uint32_t a[8];
 #pragma unroll
-                    for (int j = 1; j < 8; j++)
-                        if (j < cnt) lost[a[j] >> 5] |= 1u << (a[j] & 31);
-                } else {
-                    for (int j = 0; j < cnt; j++) grp[j] = Lp[s + j] & pmask;
-                    for (int i = cnt - 1; i >= 1 && ok; i--) {  // random.shuffle: _randbelow(i + 1)
+                for (int j = 0; j < 8; j++) {
+                    a[j] = 0u;
+                    if (j < cnt) a[j] = Lp[s0 + j] & pmask;
+                }
+#pragma unroll
+                for (int i = 7; i >= 1; i--) {
+                    if (i < cnt) {
                         const uint32_t bound = (uint32_t)(i + 1);
                         const int kb = bit_length(bound);
                         uint32_t r;
                         do {
-                            if (head >= avail) {
-                                ok = false;
-                                break;
-                            }
                             r = mt_word(pyring, WRM, head++) >> (32 - kb);
                         } while (r >= bound);
-                        if (ok) {
-                            const uint32_t t = grp[i];
-                            grp[i] = grp[r];
-                            grp[r] = t;
-                        }
+                        uint32_t ar = a[0];
+#pragma unroll
+                        for (int j = 1; j < i; j++) ar = (r == (uint32_t)j) ? a[j] : ar;
+                        const uint32_t ai = a[i];
+#pragma unroll
+                        for (int j = 0; j < i; j++) a[j] = (r == (uint32_t)j) ? ai : a[j];
+                        a[i] = (r == (uint32_t)i) ? ai : ar;
                     }
-                    if (!ok) break;  // out of words: retry this group next round
-                    for (int j = 1; j < cnt; j++) lost[grp[j] >> 5] |= 1u << (grp[j] & 31);
                 }
-                nh = head;
-                nk++;
+#pragma unroll
+                for (int j = 1; j < 8; j++)
+                    if (j < cnt) atomicOr(&lost[a[j] >> 5], 1u << (a[j] & 31));
             }
         }
-        nk = __shfl(nk, 0);
-        nh = __shfl(nh, 0);
-        err |= __shfl(bad, 0);
-        __syncthreads();
-        if (nk == k) {  // a group needs more than SHUF_WORDS words (practically impossible)
-            err |= 2;
-            break;
+        // groups of more than 8 movers (rare): lane 0, same words
+        for (int j = 0; j < nk; j++) {
+            const uint32_t dsc = (uint32_t)__builtin_amdgcn_readlane((int)desc, j);
+            const int cnt = (int)(dsc & 255u);
+            if (cnt <= 8) continue;
+            const int w0 = __builtin_amdgcn_readlane(wv, j);
+            if (lane == 0 && cnt <= GRP_MAX) {
+                const int s0 = (int)(dsc >> 8);
+                for (int q = 0; q < cnt; q++) grp[q] = Lp[s0 + q] & pmask;
+                int head = w0;
+                for (int i = cnt - 1; i >= 1; i--) {
+                    const uint32_t bound = (uint32_t)(i + 1);
+                    const int kb = bit_length(bound);
+                    uint32_t r;
+                    do {
+                        r = mt_word(pyring, WRM, head++) >> (32 - kb);
+                    } while (r >= bound);
+                    const uint32_t t = grp[i];
+                    grp[i] = grp[r];
+                    grp[r] = t;
+                }
+                for (int q = 1; q < cnt; q++) lost[grp[q] >> 5] |= 1u << (grp[q] & 31);
+            }
         }
-        k = nk;
-        py_head = nh;
+        __syncthreads();
     }
+    py_head = pos;
 }
 
 // First planner of contested target t (the group's smallest person index).
@@ -404,7 +452,8 @@ __host__ __device__ inline WaveLds wave_lds(int L, int W, int P, int R) {
     }
     s.nearc = o; o += NCW;
     s.lost = o; o += (P + 31) / 32;
-    s.robots = o; o += R;
+    o = (o + 3) & ~3;
+    s.robots = o; o += (R + 3) & ~3;  // 16-B aligned: read 4 robots at a time
     o = (o + 1) & ~1;
     s.misc = o; o += GRP_MAX + 16;         // shuffle group; event counter; pairwise stacks
     s.total = (o + 3) & ~3;
@@ -439,7 +488,7 @@ __device__ __forceinline__ int pb_bits(int P) { return P > 1 ? bit_length((uint3
 
 // EVX_PROFILE builds only: cycle accumulators of sub-phases, stored to slots 16..31
 #ifdef EVX_PROFILE
-#define PT_DECL(n) long long pt_##n = 0, pt0_##n = 0
+#define PT_DECL(n) long long pt_##n = 0, pt0_##n = __builtin_amdgcn_s_memtime()
 #define PT_BEGIN(n) pt0_##n = __builtin_amdgcn_s_memtime()
 #define PT_END(n) pt_##n += __builtin_amdgcn_s_memtime() - pt0_##n
 #define PT_STORE(n, slot) EVX_COUNT(slot, pt_##n)
@@ -648,6 +697,10 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
     PT_DECL(rew);
     PT_DECL(leaf);
     PT_DECL(rtop);
+    PT_DECL(sbl);
+    PT_DECL(sbm);
+    PT_DECL(sbs);
+    PT_DECL(sbt);
     double total = 0.0;  // CPython sum(p.health for p in self.people.list if not p.dead): sequential
     // Planners wait in an LDS queue and are scored 64 at a time (scoring is the
     // heavy part and only a few persons per row plan).
@@ -657,6 +710,7 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
     double* hc = reinterpret_cast<double*>(aux + 384);  // one group of not-dead healths (lane 0 sums them)
     int qn = 0;
     auto score_batch = [&](int n) {  // People.find_best_direction for queue entries [0, n)
+        PT_BEGIN(sbl);
         const bool has = lane < n;
         uint32_t ea = 0, eb = 0;
         int off = 0;
@@ -680,27 +734,55 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
         const int first = __builtin_amdgcn_readfirstlane(off);
         const int end = __builtin_amdgcn_readlane(off + 2 * __popc(cand), n - 1);
         uint32_t best = NODIR;
+        // squared distance to the nearest robot for the 8 neighbours, only when some
+        // candidate lies in a near-robot block (robots outer: 4 per LDS read)
+        uint32_t nearm = 0;
+#pragma unroll
+        for (int d = 0; d < 8; d++) {
+            const int nx = x + move_dx(d), ny = y + move_dy(d);
+            if (((cand >> d) & 1u) && bit_get(nearc, (nx >> 2) * BY + (ny >> 2))) nearm |= 1u << d;
+        }
+        int md2[8];
+#pragma unroll
+        for (int d = 0; d < 8; d++) md2[d] = 0x7fffffff;
+        if (__ballot(nearm != 0)) {
+            const uint4* r4 = reinterpret_cast<const uint4*>(robots);
+            for (int r0 = 0; r0 < R; r0 += 4) {
+                const uint4 q4 = r4[r0 >> 2];
+                const uint32_t rq[4] = {q4.x, q4.y, q4.z, q4.w};
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    if (r0 + j < R) {
+                        const int rx = rp_x(rq[j]), ry = rp_y(rq[j]);
+#pragma unroll
+                        for (int d = 0; d < 8; d++) {
+                            const int dx = x + move_dx(d) - rx, dy = y + move_dy(d) - ry;
+                            md2[d] = min(md2[d], dx * dx + dy * dy);
+                        }
+                    }
+                }
+            }
+        }
+#ifdef EVX_PROFILE
+        pin(f0);
+#pragma unroll
+        for (int d = 0; d < 8; d++) pin(f[d]);
+#endif
+        PT_END(sbl);
         for (int lo = first; lo < end; lo += WWIN) {  // windowed: a batch may need more words than the ring
+            PT_BEGIN(sbm);
             mt_ensure_w(pyring, py_front, min(end, lo + WWIN + 16));
+            PT_END(sbm);
+            PT_BEGIN(sbs);
             if (has && off >= lo && off < lo + WWIN) {
                 double maxs = -INFINITY;
                 int idx = off;
 #pragma unroll
                 for (int d = 0; d < 8; d++) {
                     if ((cand >> d) & 1u) {
-                        const int nx = x + move_dx(d), ny = y + move_dy(d);
                         const double delta_p = f0 - f[d];
                         double effect = 0.0;
-                        if (bit_get(nearc, (nx >> 2) * BY + (ny >> 2))) {
-                            int md2 = 0x7fffffff;
-                            for (int r = 0; r < R; r++) {
-                                const uint32_t rp = robots[r];
-                                const int dx = nx - rp_x(rp), dy = ny - rp_y(rp);
-                                const int d2 = dx * dx + dy * dy;
-                                md2 = d2 < md2 ? d2 : md2;
-                            }
-                            if (md2 < rd2) effect = lay.repel_k / (sqrt((double)md2) + 0.1);
-                        }
+                        if (((nearm >> d) & 1u) && md2[d] < rd2) effect = lay.repel_k / (sqrt((double)md2[d]) + 0.1);
                         const double u = -0.1 + (0.1 - -0.1) * mt_double(pyring, WRM, idx);
                         idx += 2;
                         const double score = delta_p * 5.0 + effect + u;
@@ -711,7 +793,9 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
                     }
                 }
             }
+            PT_END(sbs);
         }
+        PT_BEGIN(sbt);
         const bool mover = best != NODIR;
         const unsigned long long mm = __ballot(mover);
         if (mover) {
@@ -725,6 +809,7 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
             plan[nplan + lanes_below(mm)] = make_uint2((uint32_t)p, (uint32_t)cold | (best << 24));
         }
         nplan += __popcll(mm);
+        PT_END(sbt);
     };
     // one group (64 list entries, in person order) of People.run phases 1+2
     auto person_half = [&](int i, uint2 en, double hh, double ac, double dg, uint32_t nv) {
@@ -1232,6 +1317,10 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
     PT_STORE(rew, 21);
     PT_STORE(leaf, 22);
     PT_STORE(rtop, 23);
+    PT_STORE(sbl, 30);
+    PT_STORE(sbm, 31);
+    PT_STORE(sbs, 15);
+    PT_STORE(sbt, 7);
     EVX_STAMP(5);
     if (lane == 0) {
         const int remaining = nrem;

@@ -23,7 +23,8 @@ ap.add_argument("--envs", type=int, default=4096)
 ap.add_argument("--grid", type=int, default=128)
 ap.add_argument("--people", type=int, default=2276)
 ap.add_argument("--robots", type=int, default=16)
-ap.add_argument("--warmup", type=int, default=200)
+ap.add_argument("--warmup", type=int, default=1300)
+ap.add_argument("--stagger", type=int, default=1200)
 args = ap.parse_args()
 E, R = args.envs, args.robots
 spec = synthetic(args.grid, args.grid, R)
@@ -32,9 +33,13 @@ env = VecEnv(lay, E)
 env.seed([1234 + i for i in range(E)])
 env.reset()
 acts = torch.randint(0, 5, (args.warmup + 3, E * R), device="cuda", dtype=torch.int32)
+gid = torch.arange(E, device="cuda")
 for i in range(args.warmup):
     env.step(acts[i])
-    env.reset(mask=env.done)
+    m = env.done.bool()
+    if args.stagger and i < args.stagger:
+        m = m | (gid % args.stagger == i)
+    env.reset(mask=m)
 stamps = torch.zeros(E * 32, dtype=torch.int64, device="cuda")
 env.out.stamps = _ptr(stamps)
 for i in range(3):
@@ -44,23 +49,31 @@ s = stamps.view(E, 32).cpu().numpy()
 cols = [c for c, _ in SLOTS]
 d = np.diff(s[:, cols], axis=1)
 tot = s[:, cols[-1]] - s[:, 0]
-print(f"envs={E} median total cycles/env-step={np.median(tot):.0f} (wave-lifetime, one env; s_memtime ticks = shader cycles)")
+order = np.argsort(tot)
+top = order[-max(1, E // 100):]  # the slowest 1 % of envs
+print(f"envs={E} cycles/env-step (wave lifetime, shader cycles): median {np.median(tot):.0f}  p90 "
+      f"{np.percentile(tot, 90):.0f}  p99 {np.percentile(tot, 99):.0f}  max {tot.max():.0f}")
+print(f"  {'phase':28s} {'median':>9s} {'mean':>9s} {'share':>7s} {'slowest1%':>10s}")
 for i, (_, n) in enumerate(SLOTS[1:]):
-    print(f"  {n:20s} median {np.median(d[:, i]):9.0f}  mean {d[:, i].mean():9.0f}  share {d[:, i].sum() / tot.sum():6.1%}")
+    print(f"  {n:28s} {np.median(d[:, i]):9.0f} {d[:, i].mean():9.0f} {d[:, i].sum() / tot.sum():7.1%}"
+          f" {d[top, i].mean():10.0f}")
 print("py words/step median", np.median(s[:, 12]), " np words/step median", np.median(s[:, 13]),
-      " contested movers median", np.median(s[:, 14]), " planners median", np.median(s[:, 11]))
+      " contested movers median/max", np.median(s[:, 14]), s[:, 14].max(), " planners median/max",
+      np.median(s[:, 11]), s[:, 11].max())
+print(f"  slowest 1%: planners {s[top, 11].mean():.0f}, contested {s[top, 14].mean():.0f}")
 life = s[:, 10] - s[:, 9]  # s_memrealtime: constant 100 MHz on every XCD
 span = s[:, 10].max() - s[:, 9].min()
-print(f"launch span {span / 100:.1f} us; median env lifetime {np.median(life) / 100:.1f} us; "
+print(f"launch span {span / 100:.1f} us; median env lifetime {np.median(life) / 100:.1f} us, max {life.max() / 100:.1f} us; "
       f"mean concurrent envs {life.sum() / span:.0f} ({life.sum() / span / 256:.2f} per CU)")
 PROF = [(16, "rows: np draws+health"), (17, "rows: health sum"), (18, "rows: plan+queue+stores"),
         (19, "rows: score batches"), (20, "rows: loop top+selects"), (21, "reward: per group"),
         (22, "reward: leaves"), (23, "reward: loop top"), (24, "contested: list"), (25, "contested: groups"),
         (26, "contested: mt_store+clear"), (27, "load: mt+rmap+robots"), (28, "load: not-dead list"),
-        (29, "load: near map+sync")]
+        (29, "load: near map+sync"), (30, "score: floor loads"), (31, "score: mt ensure"),
+        (15, "score: scoring"), (7, "score: tail")]
 if s[:, 16:30].any():
-    print("sub-phase cycle accumulators (EVX_PROFILE build):")
+    print("sub-phase cycle accumulators (EVX_PROFILE build):        median   slowest1%")
     for c, n in PROF:
-        print(f"  {n:28s} median {np.median(s[:, c]):9.0f}")
+        print(f"  {n:28s} {np.median(s[:, c]):9.0f} {s[top, c].mean():10.0f}")
 cnt = env.counts.view(E, 2).cpu().numpy()
 print("evacuated median", np.median(cnt[:, 0]), "dead median", np.median(cnt[:, 1]))
