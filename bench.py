@@ -8,7 +8,9 @@ batch 4096, replay 2^20 transitions per GPU, gradient all-reduce over RCCL when
 world > 1. One timed "step" = one full vectorised training step:
 act (Q forward for E*R robots + epsilon-greedy) -> env.step (all E envs) ->
 replay push (E*R transitions) -> one learn step (sample, online+target forward,
-TD loss, backward, [all-reduce], clip+Adam) -> auto-reset.
+TD loss, backward, [all-reduce], clip+Adam) || auto-reset (side stream).
+Warmup staggers env ages over one episode length (--stagger), so the timed steps
+see the stationary mix of episode phases a long training run sees.
 
 value = env-steps/s of the whole job (E * n_gpus * steps / time); the JSON line
 also carries agent-transitions/s (x R), the env-only rate, the roofline of the
@@ -115,12 +117,12 @@ def main():
     for w in range(args.warmup):
         force = (gid % S == w) if 0 < S and w < S else None
         if args.mode == "train":
-            tr.step()
-            if force is not None:
-                env.reset(mask=force)
+            tr.step(extra_reset=force)
         else:
             env.step(torch.randint(0, 5, (E * R,), device="cuda", dtype=torch.int32))
             env.reset(mask=env.done if force is None else (env.done.bool() | force))
+    if args.mode == "train":
+        tr.sync()
     barrier()
 
     # the CPU baseline continues from exactly this state (same envs, same episode phase)
@@ -136,22 +138,14 @@ def main():
     t0 = time.perf_counter()
     for s in range(args.steps):
         if args.mode == "train":
-            tr.act()
-            tr.obs_prev.copy_(env.obs)
-            ev_env[s][0].record()
-            env.step(tr.actions)
-            ev_env[s][1].record()
-            tr.replay.push(tr.obs_prev, env.obs, tr.actions, env.reward, env.done, tr.n_agents, R)
-            ev_learn[s][0].record()
-            tr.learn()
-            ev_learn[s][1].record()
-            env.reset(mask=env.done)
-            tr.t += 1
+            tr.step(ev_env=ev_env[s], ev_learn=ev_learn[s])
         else:
             ev_env[s][0].record()
             env.step(rand_actions[s])
             ev_env[s][1].record()
             env.reset(mask=env.done)
+    if args.mode == "train":
+        tr.sync()
     barrier()
     elapsed = max_over_ranks(time.perf_counter() - t0)
     env.check_err()

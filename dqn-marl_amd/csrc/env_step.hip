@@ -40,9 +40,6 @@
 
 namespace evx {
 
-constexpr int RING = 2048;          // MT ring of the reset kernel (words), >= 1078
-constexpr int RMASK = RING - 1;
-constexpr int SHUF_CHUNK = 1024;
 constexpr uint32_t NODIR = 0xffu;
 
 // step kernel (one wave per env)
@@ -135,23 +132,6 @@ __device__ __forceinline__ void write_obs(const Geo& g, const uint32_t* validb, 
         reinterpret_cast<uint4*>(dst)[0] = a;
         reinterpret_cast<uint4*>(dst)[1] = b;
     }
-}
-
-// Store the MT state after consuming up to raw index `head` (CPython index semantics).
-__device__ __forceinline__ void mt_store(uint32_t* ring, int& front, int head, uint32_t* gst) {
-    if (head <= MT_N) {
-        if (threadIdx.x == 0) gst[MT_N] = (uint32_t)head;  // no twist: words unchanged
-        return;
-    }
-    const int b = MT_N * ((head - 1) / MT_N);
-    mt_ensure(ring, RMASK, front, b + MT_N);
-    for (int i = threadIdx.x; i < MT_N; i += NT) gst[i] = ring[(b + i) & RMASK];
-    if (threadIdx.x == 0) gst[MT_N] = (uint32_t)(head - b);
-}
-
-__device__ __forceinline__ void mt_load(uint32_t* ring, const uint32_t* gst, int& head) {
-    for (int i = threadIdx.x; i < MT_N; i += NT) ring[i] = gst[i];
-    head = (int)gst[MT_N];
 }
 
 // ===================================================== step: one wave per env
@@ -1385,28 +1365,34 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
 }
 
 // ------------------------------------------------------------------ reset
+// One wave per env. People.__init__ placement (envs/people.py:183-194) is a
+// sequential rejection sampler on the Python stream: x = randint(1, L-2),
+// y = randint(1, W-2) (each _randbelow: top bit_length bits of a word, retried
+// while >= the bound), retried while the cell is not valid. Over a window of 128
+// stream words, lane j evaluates the attempt that would START at word B+j
+// (acceptance masks by ballot, ctz jumps, word values by lane shuffle, validity
+// from the bitmap) -> (end, success, cell). The wave then follows the chain of
+// attempts from the stream head with readlanes: a few scalar ops per attempt.
 struct ResetLds {
-    int pyring, validb, rmapb, pos, ctrl, total;
+    int pyring, validb, rmapb, total;
 };
 __host__ __device__ inline ResetLds reset_lds(int G, int P) {
     ResetLds s;
     const int RW = (G + 31) / 32;
     int o = 0;
-    s.pyring = o; o += RING;
+    s.pyring = o; o += WR;
     s.validb = o; o += RW;
     s.rmapb = o; o += RW;
-    s.pos = o; o += P;
-    s.ctrl = o; o += 8;
     s.total = (o + 3) & ~3;
     return s;
 }
 
-__global__ __launch_bounds__(NT) void env_reset_kernel(evx_layout lay, evx_state st, const uint8_t* __restrict__ mask,
+__global__ __launch_bounds__(64) void env_reset_kernel(evx_layout lay, evx_state st, const uint8_t* __restrict__ mask,
                                                        evx_obs* obs, int32_t* err) {
     const int e = blockIdx.x;
     if (mask && !mask[e]) return;
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    const int tid = threadIdx.x;
+    const int lane = threadIdx.x;
     Geo g;
     g.L = lay.L; g.W = lay.W; g.GY = lay.W + 2; g.G = (lay.L + 2) * (lay.W + 2);
     g.RW = (g.G + 31) / 32; g.P = lay.P; g.R = lay.R;
@@ -1415,104 +1401,145 @@ __global__ __launch_bounds__(NT) void env_reset_kernel(evx_layout lay, evx_state
     uint32_t* pyring = smem + S.pyring;
     uint32_t* validb = smem + S.validb;
     uint32_t* rmapb = smem + S.rmapb;
-    uint32_t* pos = smem + S.pos;
-    int* ctrl = reinterpret_cast<int*>(smem + S.ctrl);
-    for (int i = tid; i < g.RW; i += NT) {
+    for (int i = lane; i < g.RW; i += 64) {
         validb[i] = lay.valid_bits[i];
         rmapb[i] = 0;
     }
-    int py_head;
-    mt_load(pyring, st.py_mt + (size_t)e * EVX_MT_WORDS, py_head);
+    const uint32_t* gpy = st.py_mt + (size_t)e * EVX_MT_WORDS;
+    for (int i = lane; i < MT_N; i += 64) pyring[i] = gpy[i];
+    const int head0 = (int)gpy[MT_N];
     int py_front = MT_N;
-    if (tid == 0) {
-        ctrl[0] = 0;        // next person
-        ctrl[1] = py_head;  // stream head
-        ctrl[2] = 0;        // done
-    }
-    __syncthreads();
-    // People.__init__ placement (envs/people.py:183-194): sequential rejection
-    // sampling with random.randint(1, L-2) / randint(1, W-2).
-    const uint32_t nx = (uint32_t)(g.L - 2), ny = (uint32_t)(g.W - 2);
-    const int kx = bit_length(nx), ky = bit_length(ny);
-    int last = -1;
-    while (true) {
-        const int h0 = ctrl[1];
-        mt_ensure(pyring, RMASK, py_front, h0 + SHUF_CHUNK);
-        __syncthreads();
-        if (tid == 0) {
-            int i = ctrl[0], head = ctrl[1];
-            const int avail = py_front;
-            while (i < P) {
-                const int hs = head;
-                bool ok = true;
-                int x = 0, y = 0;
-                while (true) {
-                    uint32_t r;
-                    do {
-                        if (head >= avail) { ok = false; break; }
-                        r = mt_word(pyring, RMASK, head++) >> (32 - kx);
-                    } while (r >= nx);
-                    if (!ok) break;
-                    x = 1 + (int)r;
-                    do {
-                        if (head >= avail) { ok = false; break; }
-                        r = mt_word(pyring, RMASK, head++) >> (32 - ky);
-                    } while (r >= ny);
-                    if (!ok) break;
-                    y = 1 + (int)r;
-                    if (check_valid(g, validb, x, y)) break;
-                }
-                if (!ok) {
-                    head = hs;
-                    break;
-                }
-                pos[i] = (uint32_t)x | ((uint32_t)y << 12);
-                i++;
-            }
-            ctrl[0] = i;
-            ctrl[1] = head;
-            ctrl[2] = (i >= P);
-        }
-        __syncthreads();
-        if (ctrl[2]) break;
-        if (ctrl[1] == last) {
-            if (tid == 0 && err) atomicOr(err, 4);
-            break;
-        }
-        last = ctrl[1];
-    }
-    py_head = ctrl[1];
+    wave_fence();
+#ifdef EVX_PROFILE
+    long long tr0 = __builtin_amdgcn_s_memtime(), tw = 0, tc = 0, te = 0, tx;
+    int nwin = 0;
+#endif
     uint32_t* pk_o = st.pk + (size_t)e * P;
     double* h_o = st.health + (size_t)e * P;
     double* a_o = st.acc + (size_t)e * P;
-    for (int p = tid; p < P; p += NT) {
-        const uint32_t v = pos[p];
-        pk_o[p] = v;
-        h_o[p] = 100.0;
-        a_o[p] = 0.0;
-        const int c = (int)(v & 0xfff) * g.GY + (int)((v >> 12) & 0xfff);
-        atomicOr(&rmapb[c >> 5], 1u << (c & 31));
-    }
-    if (st.thmap) {
-        int32_t* th = st.thmap + (size_t)e * g.G;
-        for (int i = tid; i < g.G; i += NT) th[i] = 0;
-        __syncthreads();
-        for (int p = tid; p < P; p += NT) {
-            const uint32_t v = pos[p];
-            th[(int)(v & 0xfff) * g.GY + (int)((v >> 12) & 0xfff)] = 1;
+    const uint32_t nx = (uint32_t)(g.L - 2), ny = (uint32_t)(g.W - 2);
+    const int kx = bit_length(nx), ky = bit_length(ny);
+    constexpr uint32_t UNKNOWN = 1u << 9, SUCC = 1u << 8;
+    int pos = head0, placed = 0;
+    int guard = 0;
+    while (placed < P) {
+        const int B = pos;
+#ifdef EVX_PROFILE
+        tx = __builtin_amdgcn_s_memtime();
+#endif
+        if (py_front < B + 128) mt_ensure_w(pyring, py_front, max(B + 128, py_front + MT_LAG));  // full rounds
+#ifdef EVX_PROFILE
+        te += __builtin_amdgcn_s_memtime() - tx;
+        tx = __builtin_amdgcn_s_memtime();
+        nwin++;
+#endif
+        const uint32_t t0 = mt_temper(pyring[(B + lane) & WRM]), t1 = mt_temper(pyring[(B + 64 + lane) & WRM]);
+        const unsigned long long ax0 = __ballot((t0 >> (32 - kx)) < nx), ax1 = __ballot((t1 >> (32 - kx)) < nx);
+        const unsigned long long ay0 = __ballot((t0 >> (32 - ky)) < ny), ay1 = __ballot((t1 >> (32 - ky)) < ny);
+        // first set bit >= k of the 128-bit mask (m0, m1); 128 = none
+        auto next_set = [](unsigned long long m0, unsigned long long m1, int k) -> int {
+            if (k < 64) {
+                const unsigned long long a = m0 >> k;
+                if (a) return k + __builtin_ctzll(a);
+                return m1 ? 64 + __builtin_ctzll(m1) : 128;
+            }
+            if (k >= 128) return 128;
+            const unsigned long long b = m1 >> (k - 64);
+            return b ? k + __builtin_ctzll(b) : 128;
+        };
+        uint32_t dend = UNKNOWN, dxy = 0;
+        {
+            const int jx = next_set(ax0, ax1, lane);
+            const int jy = jx < 127 ? next_set(ay0, ay1, jx + 1) : 128;
+            const uint32_t wx0 = __shfl(t0, jx & 63), wx1 = __shfl(t1, jx & 63);
+            const uint32_t wy0 = __shfl(t0, jy & 63), wy1 = __shfl(t1, jy & 63);
+            if (jy < 128) {
+                const int x = 1 + (int)(((jx < 64) ? wx0 : wx1) >> (32 - kx));
+                const int y = 1 + (int)(((jy < 64) ? wy0 : wy1) >> (32 - ky));
+                dend = (uint32_t)(jy + 1) | (check_valid(g, validb, x, y) ? SUCC : 0u);
+                dxy = (uint32_t)x | ((uint32_t)y << 12);
+            }
+        }
+        // Follow the chain of attempts from lane 0. Almost every attempt is 2 words,
+        // so the chain runs along one parity and only irregular attempts (other
+        // lengths, or not evaluable in this window) need a scalar step.
+#ifdef EVX_PROFILE
+        tw += __builtin_amdgcn_s_memtime() - tx;
+        tx = __builtin_amdgcn_s_memtime();
+#endif
+        const bool known = !(dend & UNKNOWN);
+        const unsigned long long irr = __ballot(!known || (int)(dend & 0xffu) - lane != 2);
+        constexpr unsigned long long EVEN = 0x5555555555555555ull;
+        unsigned long long vis = 0;
+        int rel = 0;
+        while (rel < 64) {
+            const unsigned long long par = (rel & 1) ? ~EVEN : EVEN;
+            const unsigned long long from = par & (~0ull << rel);
+            const unsigned long long cand = irr & from;
+            if (!cand) {  // regular to the end of the window
+                vis |= from;
+                rel = ((63 - rel) & 1) ? 64 : 65;  // last visited 62 or 63, then +2
+                break;
+            }
+            const int q = __builtin_ctzll(cand);
+            vis |= from & ((1ull << q) - 1);
+            const uint32_t de = (uint32_t)__builtin_amdgcn_readlane((int)dend, q);
+            if (de & UNKNOWN) {
+                rel = q;
+                break;
+            }
+            vis |= 1ull << q;
+            rel = (int)(de & 0xffu);
+        }
+        // emit the successful visited attempts in order; stop exactly at person P
+        const bool emit = ((vis >> lane) & 1ull) && (dend & SUCC);
+        const unsigned long long em = __ballot(emit);
+        const int nem = __popcll(em);
+        if (placed + nem >= P) {  // the P-th person ends this reset: its attempt's end is the stream head
+            unsigned long long m2 = em;
+            for (int t = 0; t < P - placed - 1; t++) m2 &= m2 - 1;
+            const int last = __builtin_ctzll(m2);
+            rel = (int)((uint32_t)__builtin_amdgcn_readlane((int)dend, last) & 0xffu);
+        }
+        const int k = placed + lanes_below(em);
+        if (emit && k < P) {
+            pk_o[k] = dxy;
+            const int c = (int)(dxy & 0xfff) * g.GY + (int)((dxy >> 12) & 0xfff);
+            atomicOr(&rmapb[c >> 5], 1u << (c & 31));
+        }
+        placed = min(P, placed + nem);
+        pos = B + rel;
+#ifdef EVX_PROFILE
+        tc += __builtin_amdgcn_s_memtime() - tx;
+#endif
+        if (rel == 0) {  // an attempt longer than 128 words: cannot happen with a sane stream
+            if (++guard > 4) {
+                if (lane == 0 && err) atomicOr(err, 4);
+                break;
+            }
+            pos = B + 64;
         }
     }
-    __syncthreads();
-    for (int i = tid; i < g.RW; i += NT) st.rmap[(size_t)e * g.RW + i] = rmapb[i];
+    for (int p = lane; p < P; p += 64) {
+        h_o[p] = 100.0;
+        a_o[p] = 0.0;
+    }
+    __syncthreads();  // person words and rmap bits complete
+    if (st.thmap) {
+        int32_t* th = st.thmap + (size_t)e * g.G;
+        for (int i = lane; i < g.G; i += 64) th[i] = (rmapb[i >> 5] >> (i & 31)) & 1u;
+    }
+    for (int i = lane; i < g.RW; i += 64) st.rmap[(size_t)e * g.RW + i] = rmapb[i];
     uint32_t view;
     if (lay.reset_robots) {
-        if (tid < R) st.robots[(size_t)e * R + tid] = rp_pack(lay.robot_init[2 * tid], lay.robot_init[2 * tid + 1]);
+        for (int r = lane; r < R; r += 64)
+            st.robots[(size_t)e * R + r] = rp_pack(lay.robot_init[2 * r], lay.robot_init[2 * r + 1]);
         view = rp_pack(lay.robot_init[0], lay.robot_init[1]);
     } else {
         view = rp_pack(lay.reset_view_x, lay.reset_view_y);
     }
     __syncthreads();
-    if (tid == 0) {
+    if (lane == 0) {
         st.view[e] = view;
         int* sg = st.scal + (size_t)e * 4;
         sg[1] = 0;
@@ -1521,13 +1548,17 @@ __global__ __launch_bounds__(NT) void env_reset_kernel(evx_layout lay, evx_state
     }
     const int fs = st.scal[(size_t)e * 4];
     if (obs) {
-        const int w = tid >> 6;
-        for (int r = w; r < R; r += NWAVE) {
+        for (int r = 0; r < R; r++) {
             const uint32_t c = (r == 0) ? view : st.robots[(size_t)e * R + r];
             write_obs(g, validb, rmapb, rp_x(c), rp_y(c), fs, obs + (size_t)e * R + r);
         }
     }
-    mt_store(pyring, py_front, py_head, st.py_mt + (size_t)e * EVX_MT_WORDS);
+    mt_store_w(pyring, py_front, pos, st.py_mt + (size_t)e * EVX_MT_WORDS);
+#ifdef EVX_PROFILE
+    if (lane == 0 && e == 0)
+        printf("reset env0: total %lld cycles, windows %d, ensure %lld, window eval %lld, chain %lld, words %d\n",
+               __builtin_amdgcn_s_memtime() - tr0, nwin, te, tw, tc, pos - head0);
+#endif
 }
 
 // ---------------------------------------------------- observation expand
@@ -1648,7 +1679,7 @@ int evx_env_reset(const evx_layout* l, const evx_state* s, const uint8_t* mask, 
                                   160 * 1024);
         attr_set = true;
     }
-    hipLaunchKernelGGL(evx::env_reset_kernel, dim3(s->E), dim3(evx::NT), lds, (hipStream_t)stream, *l, *s, mask, obs,
+    hipLaunchKernelGGL(evx::env_reset_kernel, dim3(s->E), dim3(64), lds, (hipStream_t)stream, *l, *s, mask, obs,
                        err);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : hip_fail(e, "env_reset launch");

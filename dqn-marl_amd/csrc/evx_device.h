@@ -3,9 +3,8 @@
 // MT19937 "ring": the reference consumes two Mersenne-Twister streams per env
 // (CPython `random`, legacy `numpy.random`). MT19937's raw state sequence obeys
 //     x[n] = x[n-227] ^ twist(x[n-624], x[n-623]),   n >= 624
-// so a workgroup keeps a window of that sequence in LDS and extends it by up to
-// 454 words per barrier phase (227 threads x 2: the second word of a thread
-// depends only on its own first word and on words older than the phase).
+// so a wave keeps a window of that sequence in an LDS ring and extends it by up
+// to 227 words per round (each depends only on words older than the round).
 // Output j of the stream is temper(x[pos + j]); consumers read words at
 // prefix-sum offsets in parallel.
 #pragma once
@@ -14,11 +13,8 @@
 
 namespace evx {
 
-constexpr int NT = 512;          // threads per env workgroup (8 waves)
-constexpr int NWAVE = NT / 64;
 constexpr int MT_N = 624;
 constexpr int MT_LAG = 227;      // 624 - 397
-constexpr int MT_GEN = 2 * MT_LAG;
 
 __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
     y ^= (y >> 11);
@@ -31,27 +27,6 @@ __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
 __device__ __forceinline__ uint32_t mt_twist1(uint32_t lag, uint32_t a, uint32_t b) {
     const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
     return lag ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
-}
-
-// Extend the raw sequence in `ring` (power-of-two size >= 1078) until front >= upto.
-// Cooperative: every thread of the block calls with the same (front, upto).
-// Generates exactly what is needed, so [upto - RING, upto) stays readable.
-__device__ __forceinline__ void mt_ensure(uint32_t* ring, int mask, int& front, int upto) {
-    while (front < upto) {
-        const int cnt = min(MT_GEN, upto - front);
-        const int t = threadIdx.x;
-        if (t < MT_LAG && t < cnt) {
-            const int n = front + t;
-            const uint32_t v0 = mt_twist1(ring[(n - MT_LAG) & mask], ring[(n - 624) & mask], ring[(n - 623) & mask]);
-            ring[n & mask] = v0;
-            if (t + MT_LAG < cnt) {
-                const int n2 = n + MT_LAG;
-                ring[n2 & mask] = mt_twist1(v0, ring[(n2 - 624) & mask], ring[(n2 - 623) & mask]);
-            }
-        }
-        __syncthreads();
-        front += cnt;
-    }
 }
 
 __device__ __forceinline__ uint32_t mt_word(const uint32_t* ring, int mask, int idx) {

@@ -7,7 +7,8 @@ One ``step()`` = for all E envs x R robots of this rank:
   push     -- E*R transitions into the replay ring (team reward/done per env)
   learn    -- sample B, online + target forwards, TD loss, backward, optional
               gradient all-reduce (RCCL over xGMI when world > 1), clip + Adam
-  reset    -- auto-reset finished envs (reference reset semantics)
+  reset    -- auto-reset finished envs (reference reset semantics), on a side
+              stream concurrently with learn
 
 Reference: runners/train_double_dqn.py:43-69 (independent robots, shared team
 reward) generalised to R robots and E envs; DQNAgent.act/remember/learn
@@ -95,6 +96,10 @@ class VecTrainer:
         self.seed = learner_seed * 7919 + env_offset + 17
         self.t = 0
         self.learn_steps = 0
+        self.side = torch.cuda.Stream(device=self.device)
+        self.ev_push = torch.cuda.Event()
+        self.ev_reset = torch.cuda.Event()
+        self.ev_reset.record(torch.cuda.current_stream(self.device))
         self.last_loss: Optional[torch.Tensor] = None
 
     def act(self):
@@ -118,16 +123,39 @@ class VecTrainer:
             self.learner.sync_target()
         return loss
 
-    def step(self):
+    def step(self, extra_reset: Optional[torch.Tensor] = None, ev_env=None, ev_learn=None):
+        """One training step. The auto-reset of finished envs runs on a side stream
+        concurrently with learn (it needs only the pushed env state; the next act
+        waits for it). extra_reset: bool [E] of further envs to reset (benchmark
+        staggering); ev_env / ev_learn: optional (start, end) CUDA events."""
+        main = torch.cuda.current_stream(self.device)
+        main.wait_event(self.ev_reset)
         self.act()
         self.obs_prev.copy_(self.env.obs)
+        if ev_env is not None:
+            ev_env[0].record(main)
         self.env.step(self.actions)
+        if ev_env is not None:
+            ev_env[1].record(main)
         self.replay.push(self.obs_prev, self.env.obs, self.actions, self.env.reward, self.env.done,
                          self.n_agents, self.R)
+        self.ev_push.record(main)
+        with torch.cuda.stream(self.side):
+            self.side.wait_event(self.ev_push)
+            mask = self.env.done if extra_reset is None else (self.env.done.bool() | extra_reset)
+            self.env.reset(mask=mask)
+            self.ev_reset.record(self.side)
+        if ev_learn is not None:
+            ev_learn[0].record(main)
         if self.t % self.learn_every == 0:
             self.last_loss = self.learn()
-        self.env.reset(mask=self.env.done)
+        if ev_learn is not None:
+            ev_learn[1].record(main)
         self.t += 1
+
+    def sync(self):
+        """Make the current stream wait for the side-stream reset of the last step."""
+        torch.cuda.current_stream(self.device).wait_event(self.ev_reset)
 
 
 def make_allreduce_hook(dist, world: int):

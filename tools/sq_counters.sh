@@ -10,5 +10,5 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace \
     --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU \
     -d "$OUT/sq" -o run --output-format csv -- \
-    python3 "$R/bench.py" --mode env --steps 10 --warmup 300 --no-cpu > "$OUT/sq.log" 2>&1
+    python3 "$R/bench.py" --mode env --steps 10 --no-cpu > "$OUT/sq.log" 2>&1
 echo "profiles in $OUT"
