@@ -1,0 +1,498 @@
+// MI355X (gfx950) fast path of the MLP Q-network (726 -> 512 -> 256 -> 5) on bf16 MFMA.
+//
+// Reference: Louvre_Evacuation/agents/dqn_agent.py DQNNetwork.forward (:40-61, the
+// fc stack; the MLP variant of SURVEY §8a A19 feeds it the flattened 11x11x6
+// patch) and DQNAgent.act (:101-124). The observation tensor of
+// EvacuationEnv._get_state (envs/evacuation_env.py:84-120) is never materialised:
+// fc1's A operand is generated from the 32-B compact observation straight into
+// the LDS tile the MFMAs read (the expanded input would be 190 MB per act step).
+//
+//   qfc1_kernel : H1 = dropout(relu(X W1^T + b1)) -> bf16 [N][512]; X optionally
+//                 written out as bf16 [N][736] (the learner's dW1 operand)
+//   qfc23_kernel: H2 = relu(H1 W2^T + b2) (optionally saved, f32), Q = H2 W3^T + b3,
+//                 optionally the epsilon-greedy action (evx_act's rule and RNG)
+//
+// Tiles: a workgroup owns 64 rows; its 4 waves split the output columns. Weights
+// (L2-resident, bf16, K padded to a multiple of 32) go from global memory straight
+// into the MFMA B-operand registers, one K-chunk ahead; A chunks are double
+// buffered in LDS, one barrier per chunk. v_mfma_f32_32x32x16_bf16 operand map:
+// lane l supplies A[row l&31][k 8(l>>5)..+7] and B[k 8(l>>5)..+7][col l&31];
+// C/D: col = l&31, row = (r&3) + 8(r>>2) + 4(l>>5).
+//
+// Dropout keep bits are a counter-based hash of (seed, stream, row, col), so the
+// backward pass regenerates the mask instead of storing it.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "evacx.h"
+
+namespace evxm {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int HID = 512, HID2 = 256, NACT = 5, K1 = 726, K1P = 768;  // K padded to 128 cells
+constexpr int RM = 64;  // rows per workgroup
+
+__device__ __forceinline__ uint32_t fmix32(uint32_t h) {
+    h ^= h >> 16;
+    h *= 0x85ebca6bu;
+    h ^= h >> 13;
+    h *= 0xc2b2ae35u;
+    h ^= h >> 16;
+    return h;
+}
+// dropout keep test: Bernoulli(1 - p) per (row, col) of one mask stream
+__device__ __forceinline__ uint32_t drop_row(uint32_t seed, uint32_t stream, uint32_t row) {
+    return fmix32(seed ^ fmix32(stream * 0x632be5abu + 0x9e3779b9u) ^ (row * 0x9e3779b1u));
+}
+__device__ __forceinline__ bool drop_keep(uint32_t rowh, uint32_t col, uint32_t thresh) {
+    return fmix32(rowh ^ (col * 0x85ebca77u + 0x27d4eb2fu)) >= thresh;
+}
+
+// Philox4x32-10, as evx_act (qnet.hip) uses it for epsilon-greedy
+struct u4 {
+    uint32_t x, y, z, w;
+};
+__device__ __forceinline__ u4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+        const uint32_t h0 = (uint32_t)(p0 >> 32), l0 = (uint32_t)p0, h1 = (uint32_t)(p1 >> 32), l1 = (uint32_t)p1;
+        c0 = h1 ^ c1 ^ k0;
+        c1 = l1;
+        c2 = h0 ^ c3 ^ k1;
+        c3 = l0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return {c0, c1, c2, c3};
+}
+__device__ __forceinline__ float u01(uint32_t v) { return (float)(v >> 8) * (1.0f / 16777216.0f); }
+
+// Weights in MFMA B-operand order: the block of (32-column tile t, K-chunk kc,
+// 16-wide step s) holds lane l's 8 values (column 32t + (l&31), k = kc*KC + 16s +
+// 8(l>>5) .. +7) at l*8, so a wave's operand load is one contiguous 1-KB read.
+__host__ __device__ __forceinline__ size_t w1_tile(int t, int kc, int s) {
+    return ((size_t)(t * (K1P / 48) + kc) * 3 + s) * 512;
+}
+__host__ __device__ __forceinline__ size_t w2_tile(int t, int kc, int s) {
+    return ((size_t)(t * (HID / 32) + kc) * 2 + s) * 512;
+}
+
+struct Fwd {
+    int N;
+    const evx_obs* obs;
+    // layout (EvacuationEnv._get_state inputs)
+    const uint8_t* cellinfo;
+    const float* danger;
+    int L, W, ox0, oy0, OX, OY, exit_x, exit_y;
+    // parameters
+    const __bf16* w1;  // [512][768] in w1_tile order
+    const float* b1;
+    const __bf16* w2;  // [256][512] in w2_tile order
+    const float* b2;
+    const float* w3;   // [5][256]
+    const float* b3;
+    // dropout on fc1's output
+    uint32_t drop_seed, drop_stream, drop_thresh;
+    float drop_scale;
+    // outputs
+    __bf16* h1;  // [N][512]
+    __bf16* x;   // [N][768] or null
+    float* h2;   // [N][256] or null
+    float* q;    // [N][5] or null
+    int32_t* actions;
+    float epsilon;
+    uint64_t act_seed, act_offset;
+};
+
+// _get_state of one cell around (cx, cy) (envs/evacuation_env.py:84-120, as
+// obs_expand_kernel evaluates it), packed: bf16(danger) | occ<<16 | barrier<<17 |
+// exit<<18 | centre<<19 (channel 0 is all zeros); cells >= 121 are K padding (0).
+__device__ __forceinline__ uint32_t cell_pack(const Fwd& a, const evx_obs& ob, int c, uint32_t ci, float dg) {
+    if (c >= 121) return 0u;
+    const int i = c / 11, j = c - 11 * (c / 11);
+    const int mx = ob.cx + i - 5, my = ob.cy + j - 5;
+    const bool inb = mx >= 0 && mx <= a.L + 1 && my >= 0 && my <= a.W + 1;
+    const bool valid = mx >= 1 && mx <= a.L && my >= 1 && my <= a.W && (ci & 1u);
+    uint32_t v = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)dg);
+    v |= ((ob.occ[c >> 5] >> (c & 31)) & 1u) << 16;
+    v |= ((!valid || (inb && ((ci >> 2) & 1u))) ? 1u : 0u) << 17;
+    v |= ((mx == a.exit_x && my == a.exit_y) ? 1u : 0u) << 18;
+    v |= ((i == 5 && j == 5) ? 1u : 0u) << 19;
+    return v;
+}
+// the table reads of cell c (cellinfo byte, danger value), issued ahead of cell_pack
+__device__ __forceinline__ void cell_reads(const Fwd& a, const evx_obs& ob, int c, uint32_t& ci, float& dg) {
+    const int cc = c < 121 ? c : 0;
+    const int i = cc / 11, j = cc - 11 * (cc / 11);
+    const int mx = ob.cx + i - 5, my = ob.cy + j - 5;
+    const bool inb = mx >= 0 && mx <= a.L + 1 && my >= 0 && my <= a.W + 1;
+    const int ti = mx - a.ox0, tj = my - a.oy0;
+    ci = 0u;
+    dg = 0.f;
+    if (inb) ci = a.cellinfo[mx * (a.W + 2) + my];
+    if (ti >= 0 && ti < a.OX && tj >= 0 && tj < a.OY) dg = a.danger[((size_t)ob.fire_step * a.OX + ti) * a.OY + tj];
+}
+// 6 bf16 features of a packed cell, as three 16-bit pairs (lo | hi << 16)
+__device__ __forceinline__ void unpack6(uint32_t v, uint32_t& p01, uint32_t& p23, uint32_t& p45) {
+    const uint32_t one = 0x3f80u;  // bf16(1.0)
+    p01 = ((v >> 16) & 1u) ? (one << 16) : 0u;                         // ch0 = 0, ch1 = occ
+    p23 = (v & 0xffffu) | ((((v >> 17) & 1u) ? one : 0u) << 16);       // ch2 = danger, ch3 = barrier
+    p45 = (((v >> 18) & 1u) ? one : 0u) | ((((v >> 19) & 1u) ? one : 0u) << 16);  // ch4 = exit, ch5 = centre
+}
+
+// ------------------------------------------------------------------ fc1
+// K chunks of 48 = 8 whole cells: thread (row tid>>2, cell pair tid&3) expands two
+// cells per chunk. NTW = 32-column tiles per wave: 2 -> a workgroup covers 256
+// columns, grid.y = 2 (act batches); 1 -> 128 columns, grid.y = 4 (learner batches).
+template <int NTW>
+__global__ __launch_bounds__(256, 2) void qfc1_kernel(Fwd a) {
+    constexpr int KC = 48, NKC = K1P / KC, APAD = KC + 8;
+    __shared__ __attribute__((aligned(16))) __bf16 As[2][RM][APAD];
+    __shared__ uint32_t Fs[RM][129];  // packed cells of the workgroup's rows
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+    const int m0 = blockIdx.x * RM;
+    const int ncol0 = blockIdx.y * (128 * NTW) + w * (32 * NTW);
+    const int gr = tid >> 2, gp = tid & 3;  // generator: row, cell pair
+    const bool rowok = m0 + gr < a.N;
+    evx_obs ob;
+    if (rowok) {
+        ob = a.obs[m0 + gr];
+    } else {
+        ob = evx_obs{{0u, 0u, 0u, 0u}, -1000, -1000, 0, 0};
+    }
+    const bool wx = a.x && rowok && blockIdx.y == 0;
+    {  // expand every cell of the row once: cells gp, gp+4, ..., 32 table reads in flight
+        uint32_t ci[32];
+        float dg[32];
+#pragma unroll
+        for (int t = 0; t < 32; t++) cell_reads(a, ob, gp + 4 * t, ci[t], dg[t]);
+#pragma unroll
+        for (int t = 0; t < 32; t++) Fs[gr][gp + 4 * t] = cell_pack(a, ob, gp + 4 * t, ci[t], dg[t]);
+    }
+    f32x16 acc[2][NTW];
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int j = 0; j < NTW; j++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc[i][j][r] = 0.f;
+    bf16x8 bc[NTW][3], bn[NTW][3];
+    auto loadB = [&](int kc, bf16x8 (&b)[NTW][3]) {
+#pragma unroll
+        for (int nt = 0; nt < NTW; nt++) {
+            const int n = ncol0 + nt * 32;
+#pragma unroll
+            for (int s = 0; s < 3; s++)  // tiled: one contiguous 1-KB block per wave load
+                b[nt][s] = *reinterpret_cast<const bf16x8*>(a.w1 + w1_tile(n >> 5, kc, s) + lane * 8);
+        }
+    };
+    struct Gen12 {
+        uint2 w[3];
+    };
+    auto gen12 = [&](int kc) -> Gen12 {  // features of cells kc*8 + 2gp, +1 from the packed table
+        uint32_t a01, a23, a45, b01, b23, b45;
+        unpack6(Fs[gr][kc * 8 + 2 * gp], a01, a23, a45);
+        unpack6(Fs[gr][kc * 8 + 2 * gp + 1], b01, b23, b45);
+        Gen12 g;
+        g.w[0] = make_uint2(a01, a23);
+        g.w[1] = make_uint2(a45, b01);
+        g.w[2] = make_uint2(b23, b45);
+        return g;
+    };
+    auto stash = [&](int buf, int kc, const Gen12& g) {
+        uint2* dst = reinterpret_cast<uint2*>(&As[buf][gr][gp * 12]);
+#pragma unroll
+        for (int t = 0; t < 3; t++) dst[t] = g.w[t];
+        if (wx) {
+            uint2* gx = reinterpret_cast<uint2*>(a.x + (size_t)(m0 + gr) * K1P + kc * KC + gp * 12);
+#pragma unroll
+            for (int t = 0; t < 3; t++) gx[t] = g.w[t];
+        }
+    };
+    __syncthreads();  // packed cells complete
+    stash(0, 0, gen12(0));
+    loadB(0, bc);
+    __syncthreads();
+    for (int kc = 0; kc < NKC; kc++) {
+        const int buf = kc & 1;
+        Gen12 gnext;
+        if (kc + 1 < NKC) {
+            gnext = gen12(kc + 1);
+            loadB(kc + 1, bn);
+        }
+#pragma unroll
+        for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+            for (int s = 0; s < 3; s++) {
+                const bf16x8 av = *reinterpret_cast<const bf16x8*>(&As[buf][mt * 32 + (lane & 31)][s * 16 + 8 * h]);
+#pragma unroll
+                for (int nt = 0; nt < NTW; nt++)
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bc[nt][s], acc[mt][nt], 0, 0, 0);
+            }
+        if (kc + 1 < NKC) {
+            stash(buf ^ 1, kc + 1, gnext);
+#pragma unroll
+            for (int nt = 0; nt < NTW; nt++)
+#pragma unroll
+                for (int s = 0; s < 3; s++) bc[nt][s] = bn[nt][s];
+        }
+        __syncthreads();
+    }
+    // epilogue: bias, ReLU, dropout, bf16
+#pragma unroll
+    for (int nt = 0; nt < NTW; nt++) {
+        const int col = ncol0 + nt * 32 + (lane & 31);
+        const float bias = a.b1[col];
+#pragma unroll
+        for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int row = m0 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (row >= a.N) continue;
+                float v = acc[mt][nt][r] + bias;
+                v = v > 0.f ? v : 0.f;
+                if (a.drop_thresh) {
+                    const uint32_t rh = drop_row(a.drop_seed, a.drop_stream, (uint32_t)row);
+                    v = drop_keep(rh, (uint32_t)col, a.drop_thresh) ? v * a.drop_scale : 0.f;
+                }
+                a.h1[(size_t)row * HID + col] = (__bf16)v;
+            }
+    }
+}
+
+// ------------------------------------------------------------ fc2 + fc3
+__global__ __launch_bounds__(256, 2) void qfc23_kernel(Fwd a) {
+    __shared__ __attribute__((aligned(16))) __bf16 As[2][RM][32];
+    __shared__ float Hs[RM][HID2 + 1];
+    __shared__ float W3s[NACT][HID2];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+    const int m0 = blockIdx.x * RM;
+    for (int i = tid; i < NACT * HID2; i += 256) W3s[i / HID2][i % HID2] = a.w3[i];
+    const int gr = tid >> 2, go = (tid & 3) * 8;
+    const bool rowok = m0 + gr < a.N;
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int j = 0; j < 2; j++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc[i][j][r] = 0.f;
+    bf16x8 bc[2][2], bn[2][2];
+    auto loadB = [&](int kc, bf16x8 (&b)[2][2]) {
+#pragma unroll
+        for (int nt = 0; nt < 2; nt++) {
+            const int n = w * 64 + nt * 32;
+#pragma unroll
+            for (int s = 0; s < 2; s++)  // tiled: one contiguous 1-KB block per wave load
+                b[nt][s] = *reinterpret_cast<const bf16x8*>(a.w2 + w2_tile(n >> 5, kc, s) + lane * 8);
+        }
+    };
+    auto loadA = [&](int kc) -> bf16x8 {
+        bf16x8 v;
+        if (rowok) {
+            v = *reinterpret_cast<const bf16x8*>(a.h1 + (size_t)(m0 + gr) * HID + kc * 32 + go);
+        } else {
+#pragma unroll
+            for (int t = 0; t < 8; t++) v[t] = (__bf16)0.f;
+        }
+        return v;
+    };
+    constexpr int NKC = HID / 32;
+    *reinterpret_cast<bf16x8*>(&As[0][gr][go]) = loadA(0);
+    loadB(0, bc);
+    __syncthreads();
+    for (int kc = 0; kc < NKC; kc++) {
+        const int buf = kc & 1;
+        bf16x8 an;
+        if (kc + 1 < NKC) {
+            an = loadA(kc + 1);
+            loadB(kc + 1, bn);
+        }
+#pragma unroll
+        for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+            for (int s = 0; s < 2; s++) {
+                const bf16x8 av = *reinterpret_cast<const bf16x8*>(&As[buf][mt * 32 + (lane & 31)][s * 16 + 8 * h]);
+#pragma unroll
+                for (int nt = 0; nt < 2; nt++)
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bc[nt][s], acc[mt][nt], 0, 0, 0);
+            }
+        if (kc + 1 < NKC) {
+            *reinterpret_cast<bf16x8*>(&As[buf ^ 1][gr][go]) = an;
+#pragma unroll
+            for (int nt = 0; nt < 2; nt++) {
+                bc[nt][0] = bn[nt][0];
+                bc[nt][1] = bn[nt][1];
+            }
+        }
+        __syncthreads();
+    }
+    // H2 = relu(acc + b2) -> LDS (and HBM for the learner)
+#pragma unroll
+    for (int nt = 0; nt < 2; nt++) {
+        const int col = w * 64 + nt * 32 + (lane & 31);
+        const float bias = a.b2[col];
+#pragma unroll
+        for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int rr = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                float v = acc[mt][nt][r] + bias;
+                v = v > 0.f ? v : 0.f;
+                Hs[rr][col] = v;
+                if (a.h2 && m0 + rr < a.N) a.h2[(size_t)(m0 + rr) * HID2 + col] = v;
+            }
+    }
+    __syncthreads();
+    // fc3: thread (row gr, quarter go/8) partial dot products, reduced over the 4 quarters
+    const int part = tid & 3;
+    float qv[NACT];
+#pragma unroll
+    for (int t = 0; t < NACT; t++) qv[t] = 0.f;
+    for (int n = part * 64; n < part * 64 + 64; n++) {
+        const float hv = Hs[gr][n];
+#pragma unroll
+        for (int t = 0; t < NACT; t++) qv[t] += hv * W3s[t][n];
+    }
+#pragma unroll
+    for (int t = 0; t < NACT; t++) {
+        qv[t] += __shfl_xor(qv[t], 1, 64);
+        qv[t] += __shfl_xor(qv[t], 2, 64);
+    }
+    if (part == 0 && rowok) {
+        const int row = m0 + gr;
+#pragma unroll
+        for (int t = 0; t < NACT; t++) qv[t] += a.b3[t];
+        if (a.q) {
+#pragma unroll
+            for (int t = 0; t < NACT; t++) a.q[(size_t)row * NACT + t] = qv[t];
+        }
+        if (a.actions) {  // DQNAgent.act: epsilon-greedy over argmax (first maximum)
+            int best = 0;
+            float bv = qv[0];
+#pragma unroll
+            for (int t = 1; t < NACT; t++)
+                if (qv[t] > bv) {
+                    bv = qv[t];
+                    best = t;
+                }
+            if (a.epsilon > 0.f) {
+                const uint64_t c = (uint64_t)row + a.act_offset;
+                const u4 r = philox((uint32_t)c, (uint32_t)(c >> 32), 0xac7u, 0u, (uint32_t)a.act_seed,
+                                    (uint32_t)(a.act_seed >> 32));
+                if (u01(r.x) <= a.epsilon) best = (int)((uint64_t)r.y * (uint64_t)NACT >> 32);
+            }
+            a.actions[row] = best;
+        }
+    }
+}
+
+// f32 parameters -> bf16 copies: W1 (K padded, w1_tile order), W2 (w2_tile order),
+// W2^T (row-major [512][256])
+__global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ w1, const float* __restrict__ w2,
+                                                   __bf16* __restrict__ w1b, __bf16* __restrict__ w2b,
+                                                   __bf16* __restrict__ w2t) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < HID * K1P) {  // destination index -> (tile, chunk, step, lane, j)
+        const int j = i & 7, l = (i >> 3) & 63, blk = i >> 9;
+        const int s = blk % 3, kc = (blk / 3) % (K1P / 48), t = blk / (3 * (K1P / 48));
+        const int n = t * 32 + (l & 31), k = kc * 48 + s * 16 + 8 * (l >> 5) + j;
+        w1b[i] = (__bf16)(k < K1 ? w1[n * K1 + k] : 0.f);
+    }
+    if (i < HID2 * HID) {
+        const int j = i & 7, l = (i >> 3) & 63, blk = i >> 9;
+        const int s = blk % 2, kc = (blk / 2) % (HID / 32), t = blk / (2 * (HID / 32));
+        const int n = t * 32 + (l & 31), k = kc * 32 + s * 16 + 8 * (l >> 5) + j;
+        w2b[i] = (__bf16)w2[n * HID + k];
+        if (w2t) {
+            const int nn = i / HID, kk = i - nn * HID;  // row-major source index i
+            w2t[(size_t)kk * HID2 + nn] = (__bf16)w2[i];
+        }
+    }
+}
+
+}  // namespace evxm
+
+// ===================================================================== C-ABI
+namespace {
+thread_local char m_err[256] = "";
+int mfail(int code, const char* msg) {
+    snprintf(m_err, sizeof(m_err), "%s", msg);
+    return code;
+}
+int mlaunch(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) return 0;
+    snprintf(m_err, sizeof(m_err), "%s: %s", what, hipGetErrorString(e));
+    return -5;
+}
+}  // namespace
+
+extern "C" {
+
+const char* evx_qmlp_last_error(void) { return m_err; }
+
+int evx_qmlp_pack(const float* w1, const float* w2, uint16_t* w1b, uint16_t* w2b, uint16_t* w2t, void* stream) {
+    if (!w1 || !w2 || !w1b || !w2b) return mfail(-22, "qmlp_pack: NULL argument");
+    const int n = evxm::HID * evxm::K1P;
+    hipLaunchKernelGGL(evxm::pack_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, w1, w2,
+                       reinterpret_cast<__bf16*>(w1b), reinterpret_cast<__bf16*>(w2b), reinterpret_cast<__bf16*>(w2t));
+    return mlaunch("qmlp_pack");
+}
+
+int evx_qmlp_forward(const evx_layout* lay, const evx_obs* obs, int32_t n, const evx_qmlp_params* p,
+                     const evx_qmlp_dropout* drop, const evx_qmlp_fwd_out* out, void* stream) {
+    if (!lay || !obs || !p || !out) return mfail(-22, "qmlp_forward: NULL argument");
+    if (n <= 0) return 0;
+    if (!p->w1 || !p->b1 || !p->w2 || !p->b2 || !p->w3 || !p->b3) return mfail(-22, "qmlp_forward: missing parameter");
+    if (!out->h1) return mfail(-22, "qmlp_forward: h1 buffer required");
+    if (!lay->danger_o32 || !lay->cellinfo) return mfail(-22, "qmlp_forward: layout tables missing");
+    evxm::Fwd a;
+    a.N = n;
+    a.obs = obs;
+    a.cellinfo = lay->cellinfo;
+    a.danger = lay->danger_o32;
+    a.L = lay->L;
+    a.W = lay->W;
+    a.ox0 = lay->ox0;
+    a.oy0 = lay->oy0;
+    a.OX = lay->OX;
+    a.OY = lay->OY;
+    a.exit_x = lay->exit_x;
+    a.exit_y = lay->exit_y;
+    a.w1 = reinterpret_cast<const __bf16*>(p->w1);
+    a.b1 = p->b1;
+    a.w2 = reinterpret_cast<const __bf16*>(p->w2);
+    a.b2 = p->b2;
+    a.w3 = p->w3;
+    a.b3 = p->b3;
+    a.drop_seed = drop ? drop->seed : 0u;
+    a.drop_stream = drop ? drop->stream : 0u;
+    const float dp = drop ? drop->p : 0.f;
+    a.drop_thresh = dp > 0.f ? (uint32_t)((double)dp * 4294967296.0) : 0u;
+    a.drop_scale = dp > 0.f ? 1.f / (1.f - dp) : 1.f;
+    a.h1 = reinterpret_cast<__bf16*>(out->h1);
+    a.x = reinterpret_cast<__bf16*>(out->x);
+    a.h2 = out->h2;
+    a.q = out->q;
+    a.actions = out->actions;
+    a.epsilon = out->epsilon;
+    a.act_seed = out->act_seed;
+    a.act_offset = out->act_offset;
+    const unsigned blocks = (unsigned)((n + evxm::RM - 1) / evxm::RM);
+    if (blocks >= 512)  // enough row tiles to fill the chip: workgroups of 64 rows x 256 columns
+        hipLaunchKernelGGL(evxm::qfc1_kernel<2>, dim3(blocks, 2), dim3(256), 0, (hipStream_t)stream, a);
+    else
+        hipLaunchKernelGGL(evxm::qfc1_kernel<1>, dim3(blocks, 4), dim3(256), 0, (hipStream_t)stream, a);
+    int rc = mlaunch("qfc1");
+    if (rc) return rc;
+    if (!out->q && !out->actions && !out->h2) return 0;
+    hipLaunchKernelGGL(evxm::qfc23_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a);
+    return mlaunch("qfc23");
+}
+
+}  // extern "C"

@@ -1,0 +1,111 @@
+"""Host driver of the bf16 MLP Q-network fast path (csrc/qmlp.hip, include/evacx.h).
+
+The MLP variant of DQNNetwork (agents/dqn_agent.py:15-61; 726 -> 512 -> 256 -> 5)
+evaluated straight from compact observations: fc1 expands them on the fly, fc2+fc3
+and DQNAgent.act's epsilon-greedy (:101-124) run in one more kernel. bf16 copies of
+fc1/fc2 weights are re-packed from the fp32 master parameters after every update.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _lib
+from .env import _stream
+
+HID, HID2, NACT, K1, K1P = 512, 256, 5, 726, 768
+
+
+class evx_qmlp_params(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ["w1", "b1", "w2", "w2t", "b2", "w3", "b3"]]
+
+
+class evx_qmlp_dropout(C.Structure):
+    _fields_ = [("seed", C.c_uint32), ("stream", C.c_uint32), ("p", C.c_float)]
+
+
+class evx_qmlp_fwd_out(C.Structure):
+    _fields_ = [("h1", C.c_void_p), ("x", C.c_void_p), ("h2", C.c_void_p), ("q", C.c_void_p),
+                ("actions", C.c_void_p), ("epsilon", C.c_float), ("act_seed", C.c_uint64),
+                ("act_offset", C.c_uint64)]
+
+
+_inited = False
+
+
+def mlib():
+    global _inited
+    L = _lib.lib()
+    if not _inited:
+        L.evx_qmlp_last_error.restype = C.c_char_p
+        L.evx_qmlp_pack.argtypes = [C.c_void_p] * 6
+        L.evx_qmlp_forward.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(evx_qmlp_params),
+                                       C.POINTER(evx_qmlp_dropout), C.POINTER(evx_qmlp_fwd_out), C.c_void_p]
+        _inited = True
+    return L
+
+
+def mcheck(rc, what):
+    if rc != 0:
+        raise _lib.EvacxError(f"{what} failed ({rc}): {mlib().evx_qmlp_last_error().decode()}")
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+class MLPFast:
+    """bf16 weight copies of one MLP parameter set (evacx.qnet.FlatParams) + forward."""
+
+    def __init__(self, params, device):
+        self.P = params
+        self.device = torch.device(device)
+        i16 = dict(dtype=torch.int16, device=self.device)
+        self.w1b = torch.zeros(HID * K1P, **i16)
+        self.w2b = torch.zeros(HID2 * HID, **i16)
+        self.w2t = torch.zeros(HID * HID2, **i16)
+        self.c = evx_qmlp_params(w1=self.w1b.data_ptr(), b1=params["fc1.bias"].data_ptr(), w2=self.w2b.data_ptr(),
+                                 w2t=self.w2t.data_ptr(), b2=params["fc2.bias"].data_ptr(),
+                                 w3=params["fc3.weight"].data_ptr(), b3=params["fc3.bias"].data_ptr())
+        self.repack()
+
+    def repack(self):
+        mcheck(mlib().evx_qmlp_pack(self.P["fc1.weight"].data_ptr(), self.P["fc2.weight"].data_ptr(),
+                                    self.w1b.data_ptr(), self.w2b.data_ptr(), self.w2t.data_ptr(), _stream()),
+               "qmlp_pack")
+
+    def forward(self, lay_c, obs: torch.Tensor, n: int, h1: torch.Tensor, drop=None, x=None, h2=None, q=None,
+                actions=None, epsilon=0.0, act_seed=0, act_offset=0):
+        """obs: compact observations (int32 words, 8 per row). drop: (seed, stream, p) or None."""
+        d = evx_qmlp_dropout(seed=drop[0] & 0xFFFFFFFF, stream=drop[1] & 0xFFFFFFFF, p=drop[2]) if drop else None
+        o = evx_qmlp_fwd_out(h1=_p(h1), x=_p(x), h2=_p(h2), q=_p(q), actions=_p(actions), epsilon=float(epsilon),
+                             act_seed=act_seed, act_offset=act_offset)
+        mcheck(mlib().evx_qmlp_forward(C.byref(lay_c), obs.data_ptr(), n, C.byref(self.c),
+                                       C.byref(d) if d is not None else None, C.byref(o), _stream()),
+               "qmlp_forward")
+
+
+# ------------------------------------------------------------ host restatements
+def _fmix32(h):
+    h = np.asarray(h, np.uint64) & 0xFFFFFFFF
+    h ^= h >> 16
+    h = (h * 0x85EBCA6B) & 0xFFFFFFFF
+    h ^= h >> 13
+    h = (h * 0xC2B2AE35) & 0xFFFFFFFF
+    h ^= h >> 16
+    return h
+
+
+def dropout_keep(seed: int, stream: int, p: float, rows: int, cols: int = HID) -> np.ndarray:
+    """The kernels' dropout keep mask [rows][cols] (bool), restated on the host (tests)."""
+    seed, stream = seed & 0xFFFFFFFF, stream & 0xFFFFFFFF
+    s = int(_fmix32((stream * 0x632BE5AB + 0x9E3779B9) & 0xFFFFFFFF))
+    r = np.arange(rows, dtype=np.uint64)
+    rowh = _fmix32(np.uint64(seed ^ s) ^ ((r * 0x9E3779B1) & 0xFFFFFFFF))
+    c = np.arange(cols, dtype=np.uint64)
+    ch = (c * 0x85EBCA77 + 0x27D4EB2F) & 0xFFFFFFFF
+    h = _fmix32(rowh[:, None] ^ ch[None, :])
+    thresh = int(p * 4294967296.0) if p > 0 else 0
+    return h >= thresh

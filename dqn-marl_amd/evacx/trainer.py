@@ -23,7 +23,8 @@ import torch
 
 from . import _lib
 from .env import OBS_WORDS, DeviceLayout, VecEnv, _stream
-from .qnet import Learner, qcheck, qlib
+from .qnet import DROPOUT_P, Learner, qcheck, qlib
+from .qmlp import HID, MLPFast
 
 
 class evx_replay(C.Structure):
@@ -101,8 +102,20 @@ class VecTrainer:
         self.ev_reset = torch.cuda.Event()
         self.ev_reset.record(torch.cuda.current_stream(self.device))
         self.last_loss: Optional[torch.Tensor] = None
+        # bf16 MLP: act straight from compact observations (csrc/qmlp.hip)
+        self.fast = MLPFast(self.learner.online, self.device) if (kind == "mlp" and precision == "bf16") else None
+        if self.fast is not None:
+            self.h1_act = torch.empty(n * HID, dtype=torch.int16, device=self.device)
+            self.drop_stream = 0
 
     def act(self):
+        if self.fast is not None:
+            # DQNAgent.act in train mode: dropout active, epsilon-greedy over argmax Q
+            self.drop_stream += 1
+            self.fast.forward(self.lay.c, self.env.obs, self.n_agents, self.h1_act,
+                              drop=(self.seed, self.drop_stream, DROPOUT_P), actions=self.actions,
+                              epsilon=float(self.epsilon), act_seed=self.seed, act_offset=self.t * self.n_agents)
+            return self.actions
         x = self.env.expand_obs(torch.float32)  # [E, R, 11, 11, 6]
         Q = self.learner.q_values(x.view(self.n_agents, 11, 11, 6), train=True)
         qcheck(qlib().evx_act(Q.data_ptr(), self.n_agents, self.learner.actions, float(self.epsilon), self.seed,
@@ -116,6 +129,8 @@ class VecTrainer:
         s = self.env.expand_obs(torch.float32, self.samp["s"]).view(self.batch, 11, 11, 6)
         s2 = self.env.expand_obs(torch.float32, self.samp["s2"]).view(self.batch, 11, 11, 6)
         loss = self.learner.learn(s, self.samp["a"], self.samp["r"], self.samp["done"], s2)
+        if self.fast is not None:
+            self.fast.repack()  # bf16 copies follow the updated fp32 parameters
         self.learn_steps += 1
         if self.epsilon > self.epsilon_min:  # DQNAgent.learn epsilon schedule (agents/dqn_agent.py:163-164)
             self.epsilon *= self.epsilon_decay

@@ -187,6 +187,43 @@ int evx_pix_nchw(const float *src, int32_t B, int32_t C, int32_t to_nchw, float 
 int evx_relu_grad(float *dy, const float *y, int64_t n, void *stream);
 const char *evx_q_last_error(void);
 
+/* ------------------------------------------------- MLP Q-network fast path (bf16 MFMA)
+ * DQNNetwork's fc stack (agents/dqn_agent.py:40-61; MLP variant 726-512-256-5) with the
+ * observation expansion of EvacuationEnv._get_state (envs/evacuation_env.py:84-120)
+ * generated inside fc1, and DQNAgent.act's epsilon-greedy (:101-124) fused after fc3.
+ * Dropout keep bits are a counter hash of (seed, stream, row, col): the backward pass
+ * regenerates them. */
+typedef struct {
+    const uint16_t *w1;   /* [512][768] bf16 fc1.weight, k >= 726 zero, MFMA operand-tiled (evx_qmlp_pack) */
+    const float *b1;      /* [512] */
+    const uint16_t *w2;   /* [256][512] bf16 fc2.weight, MFMA operand-tiled (evx_qmlp_pack) */
+    const uint16_t *w2t;  /* [512][256] bf16 fc2.weight transposed (backward), may be NULL for forward */
+    const float *b2;      /* [256] */
+    const float *w3;      /* [5][256] f32 fc3.weight */
+    const float *b3;      /* [5] */
+} evx_qmlp_params;
+
+typedef struct {
+    uint32_t seed, stream; /* mask identity */
+    float p;               /* drop probability; 0 = eval (no dropout) */
+} evx_qmlp_dropout;
+
+typedef struct {
+    uint16_t *h1;          /* [n][512] bf16 fc1 output after ReLU + dropout (required) */
+    uint16_t *x;           /* [n][768] bf16 expanded observation (k >= 726 zero), or NULL */
+    float *h2;             /* [n][256] fc2 output after ReLU, or NULL */
+    float *q;              /* [n][5] Q values, or NULL */
+    int32_t *actions;      /* [n] epsilon-greedy actions (evx_act's rule and RNG), or NULL */
+    float epsilon;
+    uint64_t act_seed, act_offset;
+} evx_qmlp_fwd_out;
+
+/* bf16 copies of fc1.weight [512][726] and fc2.weight [256][512] (w2t may be NULL) */
+int evx_qmlp_pack(const float *w1, const float *w2, uint16_t *w1b, uint16_t *w2b, uint16_t *w2t, void *stream);
+int evx_qmlp_forward(const evx_layout *lay, const evx_obs *obs, int32_t n, const evx_qmlp_params *p,
+                     const evx_qmlp_dropout *drop, const evx_qmlp_fwd_out *out, void *stream);
+const char *evx_qmlp_last_error(void);
+
 #ifdef __cplusplus
 }
 #endif

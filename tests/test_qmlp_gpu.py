@@ -1,0 +1,100 @@
+"""GPU numerics of the bf16 MLP fast path (csrc/qmlp.hip) against a plain PyTorch fp32
+reference evaluated on the same bf16-rounded operands.
+
+The expanded observation must equal bf16(evx_obs_expand_f32) exactly; H1 (bf16
+output) may differ from the reference by one bf16 rounding step where the f32
+accumulation order changes the rounded value (rtol 1e-2); Q rtol 1e-3 / atol 1e-3.
+The actions of the fused epsilon-greedy must equal evx_act on the kernel's own Q."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _env_obs(E=48, steps=7, R=4, grid=48, people=300):
+    from evacx.env import DeviceLayout, VecEnv
+    from evacx.layout import build_tables, synthetic
+    lay = DeviceLayout(build_tables(synthetic(grid, grid, R)), people)
+    env = VecEnv(lay, E)
+    env.seed([77 + i for i in range(E)])
+    env.reset()
+    g = torch.Generator(device="cuda").manual_seed(0)
+    for _ in range(steps):
+        env.step(torch.randint(0, 5, (E * R,), device="cuda", dtype=torch.int32, generator=g))
+    torch.cuda.synchronize()
+    return lay, env
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).float()
+
+
+@pytest.mark.parametrize("p_drop", [0.0, 0.2])
+def test_fused_forward_matches_torch(p_drop):
+    _need_gpu()
+    from evacx.qmlp import HID, K1, K1P, MLPFast, dropout_keep
+    from evacx.qnet import Learner
+    lay, env = _env_obs()
+    n = env.E * lay.R
+    lr = Learner(kind="mlp", precision="bf16", seed=11)
+    fast = MLPFast(lr.online, "cuda")
+    dev = "cuda"
+    h1 = torch.empty(n * HID, dtype=torch.int16, device=dev)
+    x = torch.empty(n * K1P, dtype=torch.int16, device=dev)
+    h2 = torch.empty(n, 256, device=dev)
+    q = torch.empty(n, 5, device=dev)
+    act = torch.empty(n, dtype=torch.int32, device=dev)
+    drop = (12345, 7, p_drop) if p_drop > 0 else None
+    fast.forward(lay.c, env.obs, n, h1, drop=drop, x=x, h2=h2, q=q, actions=act, epsilon=0.3, act_seed=99,
+                 act_offset=1000)
+    torch.cuda.synchronize()
+    # expanded observation: exactly bf16 of the reference tensor
+    X = env.expand_obs(torch.float32).reshape(n, K1)
+    xk = x.view(torch.bfloat16).view(n, K1P).float()
+    assert torch.equal(xk[:, :K1], _bf(X))
+    assert torch.count_nonzero(xk[:, K1:]) == 0
+    sd = lr.online.state_dict()
+    W1, W2 = _bf(sd["fc1.weight"]), _bf(sd["fc2.weight"])
+    ref1 = F.relu(_bf(X) @ W1.t() + sd["fc1.bias"])
+    if p_drop > 0:
+        keep = torch.from_numpy(dropout_keep(12345, 7, p_drop, n)).to(dev)
+        ref1 = torch.where(keep, ref1 / (1 - p_drop), torch.zeros_like(ref1))
+        frac = keep.float().mean().item()
+        assert abs(frac - (1 - p_drop)) < 0.01, frac
+    got1 = h1.view(torch.bfloat16).view(n, HID).float()
+    torch.testing.assert_close(got1, _bf(ref1), rtol=1e-2, atol=1e-2)
+    # downstream from the kernel's own H1
+    ref2 = F.relu(got1 @ W2.t() + sd["fc2.bias"])
+    torch.testing.assert_close(h2, ref2, rtol=1e-3, atol=1e-3)
+    refq = ref2 @ sd["fc3.weight"].t() + sd["fc3.bias"]
+    torch.testing.assert_close(q, refq, rtol=1e-3, atol=1e-3)
+    # fused epsilon-greedy == evx_act on the same Q
+    from evacx.qnet import qcheck, qlib
+    act2 = torch.empty_like(act)
+    qcheck(qlib().evx_act(q.data_ptr(), n, 5, 0.3, 99, 1000, act2.data_ptr(), 0), "act")
+    torch.cuda.synchronize()
+    assert torch.equal(act, act2)
+
+
+def test_fused_forward_large_batch_runs():
+    """Act-sized batch with a ragged tail (N not a multiple of 64)."""
+    _need_gpu()
+    from evacx.qmlp import HID, MLPFast
+    from evacx.qnet import Learner
+    lay, env = _env_obs(E=1000, steps=2)
+    n = env.E * lay.R - 37
+    lr = Learner(kind="mlp", precision="bf16", seed=12)
+    fast = MLPFast(lr.online, "cuda")
+    h1 = torch.empty(n * HID, dtype=torch.int16, device="cuda")
+    q = torch.full((n + 5, 5), 7.0, device="cuda")
+    fast.forward(lay.c, env.obs, n, h1, drop=(1, 2, 0.2), q=q)
+    torch.cuda.synchronize()
+    assert torch.isfinite(q[:n]).all()
+    assert torch.all(q[n:] == 7.0)  # nothing written past n

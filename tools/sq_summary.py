@@ -1,13 +1,14 @@
 #!/usr/bin/env python3
-"""Average SQ counters of env_step_kernel over the last launches of a tools/sq_counters.sh run."""
+"""Average SQ counters of one kernel (default env_step_kernel) over its last launches: sq_summary.py CSV [name]."""
 import collections
 import csv
 import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
+kname = sys.argv[2] if len(sys.argv) > 2 else "env_step_kernel"
 v = collections.defaultdict(collections.OrderedDict)
 for r in rows:
-    if "env_step_kernel" in r["Kernel_Name"]:
+    if kname in r["Kernel_Name"]:
         d = v[r["Counter_Name"]]
         k = int(r["Dispatch_Id"])
         d[k] = d.get(k, 0.0) + float(r["Counter_Value"])
