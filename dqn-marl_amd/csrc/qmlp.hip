@@ -25,6 +25,8 @@
 #include <stdint.h>
 #include <stdio.h>
 
+#include <algorithm>
+
 #include "evacx.h"
 
 namespace evxm {
@@ -79,6 +81,10 @@ __host__ __device__ __forceinline__ size_t w1_tile(int t, int kc, int s) {
 }
 __host__ __device__ __forceinline__ size_t w2_tile(int t, int kc, int s) {
     return ((size_t)(t * (HID / 32) + kc) * 2 + s) * 512;
+}
+// fc2.weight^T for the backward (columns = fc2 inputs, K = fc2 outputs)
+__host__ __device__ __forceinline__ size_t w2t_tile(int t, int kc, int s) {
+    return ((size_t)(t * (HID2 / 32) + kc) * 2 + s) * 512;
 }
 
 struct Fwd {
@@ -392,7 +398,7 @@ __global__ __launch_bounds__(256, 2) void qfc23_kernel(Fwd a) {
 }
 
 // f32 parameters -> bf16 copies: W1 (K padded, w1_tile order), W2 (w2_tile order),
-// W2^T (row-major [512][256])
+// W2^T (w2t_tile order, the backward's operand)
 __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ w1, const float* __restrict__ w2,
                                                    __bf16* __restrict__ w1b, __bf16* __restrict__ w2b,
                                                    __bf16* __restrict__ w2t) {
@@ -408,11 +414,235 @@ __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ w1,
         const int s = blk % 2, kc = (blk / 2) % (HID / 32), t = blk / (2 * (HID / 32));
         const int n = t * 32 + (l & 31), k = kc * 32 + s * 16 + 8 * (l >> 5) + j;
         w2b[i] = (__bf16)w2[n * HID + k];
-        if (w2t) {
-            const int nn = i / HID, kk = i - nn * HID;  // row-major source index i
-            w2t[(size_t)kk * HID2 + nn] = (__bf16)w2[i];
+        if (w2t) {  // w2t_tile order: columns = fc2 inputs (512), K = fc2 outputs (256)
+            const int tt = blk / (2 * (HID2 / 32)), kc2 = (blk / 2) % (HID2 / 32);
+            const int nn = tt * 32 + (l & 31), kk = kc2 * 32 + s * 16 + 8 * (l >> 5) + j;
+            w2t[i] = (__bf16)w2[kk * HID + nn];
         }
     }
+}
+
+// ================================================================ backward
+// DQNAgent.learn's loss.backward() for the MLP (agents/dqn_agent.py:150-158):
+//   fc3: dW3 = dQ^T H2, db3 = sum dQ, dZ2 = (dQ W3) * [H2 > 0], db2 = sum dZ2
+//   fc2: dW2 = dZ2^T H1, dZ1 = (dZ2 W2) * scale * [H1 > 0], db1 = sum dZ1
+//        ([H1 > 0] is keep AND relu' since H1 = keep * scale * relu(z))
+//   fc1: dW1 = dZ1^T X
+// Gradients accumulate with f32 atomics into a zeroed buffer (split-K).
+struct Bwd {
+    int B;
+    const float* dq;    // [B][5]
+    const float* h2;    // [B][256]
+    const __bf16* h1;   // [B][512]
+    const __bf16* x;    // [B][768]
+    const float* w3;    // [5][256]
+    const __bf16* w2t;  // fc2.weight^T in w2t_tile order
+    float scale;
+    __bf16* dz2;        // [B][256]
+    __bf16* dz1;        // [B][512]
+    float *gw1, *gb1, *gw2, *gb2, *gw3, *gb3;
+};
+
+// fc3 backward: thread n of a 32-row block walks the rows (coalesced over n)
+constexpr int R3 = 32;
+__global__ __launch_bounds__(256) void qbwd3_kernel(Bwd a) {
+    __shared__ float dqs[R3][NACT];
+    const int n = threadIdx.x, b0 = blockIdx.x * R3;
+    for (int i = n; i < R3 * NACT; i += 256) {
+        const int r = i / NACT;
+        dqs[r][i - r * NACT] = b0 + r < a.B ? a.dq[(size_t)(b0 + r) * NACT + (i - r * NACT)] : 0.f;
+    }
+    __syncthreads();
+    float w3[NACT], gw[NACT], gb2 = 0.f;
+#pragma unroll
+    for (int t = 0; t < NACT; t++) {
+        w3[t] = a.w3[t * HID2 + n];
+        gw[t] = 0.f;
+    }
+    for (int r = 0; r < R3 && b0 + r < a.B; r++) {
+        const float hv = a.h2[(size_t)(b0 + r) * HID2 + n];
+        float dz = 0.f;
+#pragma unroll
+        for (int t = 0; t < NACT; t++) {
+            const float d = dqs[r][t];
+            gw[t] += d * hv;
+            dz += d * w3[t];
+        }
+        dz = hv > 0.f ? dz : 0.f;
+        a.dz2[(size_t)(b0 + r) * HID2 + n] = (__bf16)dz;
+        gb2 += dz;
+    }
+#pragma unroll
+    for (int t = 0; t < NACT; t++) atomicAdd(&a.gw3[t * HID2 + n], gw[t]);
+    atomicAdd(&a.gb2[n], gb2);
+    if (n < NACT) {
+        float s = 0.f;
+        for (int r = 0; r < R3; r++) s += dqs[r][n];
+        atomicAdd(&a.gb3[n], s);
+    }
+}
+
+// dZ1 = (dZ2 W2) * scale * [H1 > 0]: 64 rows x 128 columns per workgroup (4 waves x
+// 32 columns), K = 256 in chunks of 32; dZ2 staged through LDS, W2^T operand-tiled.
+__global__ __launch_bounds__(256, 2) void qdz1_kernel(Bwd a) {
+    __shared__ __attribute__((aligned(16))) __bf16 As[2][RM][32];
+    __shared__ float colsum[4][32];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+    const int m0 = blockIdx.x * RM, n0 = blockIdx.y * 128 + w * 32;
+    const int gr = tid >> 2, go = (tid & 3) * 8;
+    const bool rowok = m0 + gr < a.B;
+    f32x16 acc[2];
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int r = 0; r < 16; r++) acc[i][r] = 0.f;
+    auto loadA = [&](int kc) -> bf16x8 {
+        bf16x8 v;
+        if (rowok) {
+            v = *reinterpret_cast<const bf16x8*>(a.dz2 + (size_t)(m0 + gr) * HID2 + kc * 32 + go);
+        } else {
+#pragma unroll
+            for (int t = 0; t < 8; t++) v[t] = (__bf16)0.f;
+        }
+        return v;
+    };
+    bf16x8 bc[2], bn[2];
+    auto loadB = [&](int kc, bf16x8 (&b)[2]) {
+#pragma unroll
+        for (int s = 0; s < 2; s++) b[s] = *reinterpret_cast<const bf16x8*>(a.w2t + w2t_tile(n0 >> 5, kc, s) + lane * 8);
+    };
+    constexpr int NKC = HID2 / 32;
+    *reinterpret_cast<bf16x8*>(&As[0][gr][go]) = loadA(0);
+    loadB(0, bc);
+    __syncthreads();
+    for (int kc = 0; kc < NKC; kc++) {
+        const int buf = kc & 1;
+        bf16x8 an;
+        if (kc + 1 < NKC) {
+            an = loadA(kc + 1);
+            loadB(kc + 1, bn);
+        }
+#pragma unroll
+        for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+            for (int s = 0; s < 2; s++) {
+                const bf16x8 av = *reinterpret_cast<const bf16x8*>(&As[buf][mt * 32 + (lane & 31)][s * 16 + 8 * h]);
+                acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bc[s], acc[mt], 0, 0, 0);
+            }
+        if (kc + 1 < NKC) {
+            *reinterpret_cast<bf16x8*>(&As[buf ^ 1][gr][go]) = an;
+            bc[0] = bn[0];
+            bc[1] = bn[1];
+        }
+        __syncthreads();
+    }
+    const int col = n0 + (lane & 31);
+    float cs = 0.f;
+#pragma unroll
+    for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+            const int row = m0 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (row >= a.B) continue;
+            const float hv = (float)a.h1[(size_t)row * HID + col];
+            const float v = hv > 0.f ? acc[mt][r] * a.scale : 0.f;
+            a.dz1[(size_t)row * HID + col] = (__bf16)v;
+            cs += v;
+        }
+    cs += __shfl_xor(cs, 32, 64);  // the two row halves of the column
+    if (h == 0) atomicAdd(&a.gb1[col], cs);
+}
+
+// C[m][n] += sum_k A[k][m] B[k][n] (both operands K-major bf16), 128x128 tiles of
+// 4 waves (2x2 of 64x64), K chunks of 32 staged transposed in LDS; gridDim.z splits
+// K and the partial tiles are added with f32 atomics. Columns n >= Nc are skipped.
+constexpr int TT = 128, TKC = 32, TPAD = TKC + 8;
+__global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const __bf16* __restrict__ A, int lda,
+                                                         const __bf16* __restrict__ Bm, int ldb, int K, int M, int Nc,
+                                                         int kper, float* __restrict__ C, int ldc) {
+    __shared__ __attribute__((aligned(16))) __bf16 As[TT][TPAD];
+    __shared__ __attribute__((aligned(16))) __bf16 Bs[TT][TPAD];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+    const int wm = w >> 1, wn = w & 1;
+    const int m0 = blockIdx.y * TT, n0 = blockIdx.x * TT;
+    const int kb = blockIdx.z * kper, ke = min(K, kb + kper);
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int j = 0; j < 2; j++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc[i][j][r] = 0.f;
+    // loader: k row = tid >> 3, 16 consecutive m (n) at (tid & 7) * 16
+    const int lk = tid >> 3, lm = (tid & 7) * 16;
+    bf16x8 ra[2], rb[2];
+    auto fetch = [&](int k0) {
+        const int k = k0 + lk;
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            bf16x8 va, vb;
+            const bool okk = k < ke;
+            if (okk && m0 + lm + 8 * j < M) {
+                va = *reinterpret_cast<const bf16x8*>(A + (size_t)k * lda + m0 + lm + 8 * j);
+            } else {
+#pragma unroll
+                for (int t = 0; t < 8; t++) va[t] = (__bf16)0.f;
+            }
+            if (okk && n0 + lm + 8 * j < ldb) {
+                vb = *reinterpret_cast<const bf16x8*>(Bm + (size_t)k * ldb + n0 + lm + 8 * j);
+            } else {
+#pragma unroll
+                for (int t = 0; t < 8; t++) vb[t] = (__bf16)0.f;
+            }
+            ra[j] = va;
+            rb[j] = vb;
+        }
+    };
+    auto stash = [&]() {
+#pragma unroll
+        for (int j = 0; j < 2; j++)
+#pragma unroll
+            for (int t = 0; t < 8; t++) {
+                As[lm + 8 * j + t][lk] = ra[j][t];
+                Bs[lm + 8 * j + t][lk] = rb[j][t];
+            }
+    };
+    if (kb < ke) fetch(kb);
+    for (int k0 = kb; k0 < ke; k0 += TKC) {
+        stash();
+        __syncthreads();
+        if (k0 + TKC < ke) fetch(k0 + TKC);
+#pragma unroll
+        for (int s = 0; s < TKC / 16; s++) {
+            bf16x8 av[2], bv[2];
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+                av[i] = *reinterpret_cast<const bf16x8*>(&As[wm * 64 + i * 32 + (lane & 31)][s * 16 + 8 * h]);
+                bv[i] = *reinterpret_cast<const bf16x8*>(&Bs[wn * 64 + i * 32 + (lane & 31)][s * 16 + 8 * h]);
+            }
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+#pragma unroll
+                for (int j = 0; j < 2; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        const int n = n0 + wn * 64 + j * 32 + (lane & 31);
+        if (n >= Nc) continue;
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (m < M) atomicAdd(&C[(size_t)m * ldc + n], acc[i][j][r]);
+            }
+    }
+}
+
+__global__ __launch_bounds__(256) void zero_kernel(float* __restrict__ p, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) p[i] = 0.f;
 }
 
 }  // namespace evxm
@@ -493,6 +723,64 @@ int evx_qmlp_forward(const evx_layout* lay, const evx_obs* obs, int32_t n, const
     if (!out->q && !out->actions && !out->h2) return 0;
     hipLaunchKernelGGL(evxm::qfc23_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a);
     return mlaunch("qfc23");
+}
+
+int evx_qmlp_backward(const evx_qmlp_params* p, int32_t B, const float* dq, const uint16_t* x, const uint16_t* h1,
+                      const float* h2, float drop_p, uint16_t* dz2, uint16_t* dz1, const evx_qmlp_grads* g,
+                      int32_t zero_grads, void* stream) {
+    if (!p || !g || !dq || !x || !h1 || !h2 || !dz2 || !dz1) return mfail(-22, "qmlp_backward: NULL argument");
+    if (!p->w2t || !p->w3) return mfail(-22, "qmlp_backward: w2t / w3 required");
+    if (!g->w1 || !g->b1 || !g->w2 || !g->b2 || !g->w3 || !g->b3) return mfail(-22, "qmlp_backward: missing grad");
+    if (B <= 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    if (zero_grads) {
+        float* gz[6] = {g->w1, g->b1, g->w2, g->b2, g->w3, g->b3};
+        const int64_t nz[6] = {(int64_t)evxm::HID * evxm::K1, evxm::HID, (int64_t)evxm::HID2 * evxm::HID, evxm::HID2,
+                               (int64_t)evxm::NACT * evxm::HID2, evxm::NACT};
+        for (int i = 0; i < 6; i++)
+            hipLaunchKernelGGL(evxm::zero_kernel, dim3((unsigned)std::min<int64_t>(1024, (nz[i] + 255) / 256)), dim3(256),
+                               0, st, gz[i], nz[i]);
+    }
+    evxm::Bwd a;
+    a.B = B;
+    a.dq = dq;
+    a.h2 = h2;
+    a.h1 = reinterpret_cast<const __bf16*>(h1);
+    a.x = reinterpret_cast<const __bf16*>(x);
+    a.w3 = p->w3;
+    a.w2t = reinterpret_cast<const __bf16*>(p->w2t);
+    a.scale = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+    a.dz2 = reinterpret_cast<__bf16*>(dz2);
+    a.dz1 = reinterpret_cast<__bf16*>(dz1);
+    a.gw1 = g->w1;
+    a.gb1 = g->b1;
+    a.gw2 = g->w2;
+    a.gb2 = g->b2;
+    a.gw3 = g->w3;
+    a.gb3 = g->b3;
+    hipLaunchKernelGGL(evxm::qbwd3_kernel, dim3((unsigned)((B + evxm::R3 - 1) / evxm::R3)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(evxm::qdz1_kernel, dim3((unsigned)((B + evxm::RM - 1) / evxm::RM), evxm::HID / 128), dim3(256),
+                       0, st, a);
+    // dW2 = dZ2^T H1 (256 x 512), dW1 = dZ1^T X (512 x 726); K = B split over gridDim.z
+    auto ksplit = [&](int tiles) {
+        int S = (256 + tiles - 1) / tiles;
+        int kper = (B + S - 1) / S;
+        kper = (kper + evxm::TKC - 1) / evxm::TKC * evxm::TKC;
+        return kper;
+    };
+    {
+        const int kper = ksplit(8);
+        hipLaunchKernelGGL(evxm::gemm_tn_kernel, dim3(evxm::HID / evxm::TT, evxm::HID2 / evxm::TT, (B + kper - 1) / kper),
+                           dim3(256), 0, st, a.dz2, evxm::HID2, a.h1, evxm::HID, B, evxm::HID2, evxm::HID, kper, g->w2,
+                           evxm::HID);
+    }
+    {
+        const int kper = ksplit(24);
+        hipLaunchKernelGGL(evxm::gemm_tn_kernel, dim3(evxm::K1P / evxm::TT, evxm::HID / evxm::TT, (B + kper - 1) / kper),
+                           dim3(256), 0, st, a.dz1, evxm::HID, a.x, evxm::K1P, B, evxm::HID, evxm::K1, kper, g->w1,
+                           evxm::K1);
+    }
+    return mlaunch("qmlp_backward");
 }
 
 }  // extern "C"

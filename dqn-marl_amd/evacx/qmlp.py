@@ -26,6 +26,10 @@ class evx_qmlp_dropout(C.Structure):
     _fields_ = [("seed", C.c_uint32), ("stream", C.c_uint32), ("p", C.c_float)]
 
 
+class evx_qmlp_grads(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ["w1", "b1", "w2", "b2", "w3", "b3"]]
+
+
 class evx_qmlp_fwd_out(C.Structure):
     _fields_ = [("h1", C.c_void_p), ("x", C.c_void_p), ("h2", C.c_void_p), ("q", C.c_void_p),
                 ("actions", C.c_void_p), ("epsilon", C.c_float), ("act_seed", C.c_uint64),
@@ -43,6 +47,9 @@ def mlib():
         L.evx_qmlp_pack.argtypes = [C.c_void_p] * 6
         L.evx_qmlp_forward.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(evx_qmlp_params),
                                        C.POINTER(evx_qmlp_dropout), C.POINTER(evx_qmlp_fwd_out), C.c_void_p]
+        L.evx_qmlp_backward.argtypes = [C.POINTER(evx_qmlp_params), C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                        C.c_void_p, C.c_float, C.c_void_p, C.c_void_p, C.POINTER(evx_qmlp_grads),
+                                        C.c_int32, C.c_void_p]
         _inited = True
     return L
 
@@ -85,6 +92,16 @@ class MLPFast:
         mcheck(mlib().evx_qmlp_forward(C.byref(lay_c), obs.data_ptr(), n, C.byref(self.c),
                                        C.byref(d) if d is not None else None, C.byref(o), _stream()),
                "qmlp_forward")
+
+
+    def backward(self, B: int, dq: torch.Tensor, x: torch.Tensor, h1: torch.Tensor, h2: torch.Tensor, drop_p: float,
+                 dz2: torch.Tensor, dz1: torch.Tensor, grads, zero=True):
+        """d loss / d params of the saved forward into `grads` (evacx.qnet.FlatParams)."""
+        g = evx_qmlp_grads(**{k: grads[f"fc{k[1]}.{'weight' if k[0] == 'w' else 'bias'}"].data_ptr()
+                              for k in ["w1", "b1", "w2", "b2", "w3", "b3"]})
+        mcheck(mlib().evx_qmlp_backward(C.byref(self.c), B, dq.data_ptr(), x.data_ptr(), h1.data_ptr(), h2.data_ptr(),
+                                        float(drop_p), dz2.data_ptr(), dz1.data_ptr(), C.byref(g), int(zero),
+                                        _stream()), "qmlp_backward")
 
 
 # ------------------------------------------------------------ host restatements

@@ -292,6 +292,13 @@ class Learner:
         self.seed = seed
         self.rng_offset = 0
         self.grad_hook = None  # e.g. an all-reduce over the flat grad buffer
+        # bf16 MLP: the fused kernels of csrc/qmlp.hip (forward from compact observations)
+        self.fast = self.fast_t = None
+        if kind == "mlp" and precision == "bf16":
+            from .qmlp import MLPFast
+            self.fast = MLPFast(self.online, self.device)
+            self.fast_t = MLPFast(self.target, self.device)
+        self.drop_stream = 0
 
     # ------------------------------------------------------------ dropout
     def dropout_mask(self, B, tag="m"):
@@ -327,6 +334,32 @@ class Learner:
         self.step_optimizer()
         return self.loss
 
+    def learn_obs(self, lay_c, s_obs, a, r, done, s2_obs, B):
+        """DQNAgent.learn on compact observations with the fused bf16 kernels:
+        online forward (saves X, H1, H2), target forward, TD loss, backward, clip+Adam."""
+        from .qmlp import HID, HID2, K1P
+        ws, dev = self.net.ws, self.device
+        X = ws.get("fx", (B * K1P,), torch.int16, dev)
+        H1 = ws.get("fh1", (B * HID,), torch.int16, dev)
+        H2 = ws.get("fh2", (B, HID2), torch.float32, dev)
+        Q = ws.get("fq", (B, self.actions), torch.float32, dev)
+        H1t = ws.get("fh1t", (B * HID,), torch.int16, dev)
+        Qt = ws.get("fqt", (B, self.actions), torch.float32, dev)
+        dQ = ws.get("fdq", (B, self.actions), torch.float32, dev)
+        dz2 = ws.get("fdz2", (B * HID2,), torch.int16, dev)
+        dz1 = ws.get("fdz1", (B * HID,), torch.int16, dev)
+        self.drop_stream += 2
+        self.fast.forward(lay_c, s_obs, B, H1, drop=(self.seed, self.drop_stream, DROPOUT_P), x=X, h2=H2, q=Q)
+        self.fast_t.forward(lay_c, s2_obs, B, H1t, drop=(self.seed, self.drop_stream + 1, DROPOUT_P), q=Qt)
+        L = qlib()
+        qcheck(L.evx_td_loss(_p(Q), _p(Qt), self.actions, _p(a), _p(r), _p(done), self.gamma, B, _p(dQ),
+                             _p(self.loss), _stream()), "td_loss")
+        self.fast.backward(B, dQ, X, H1, H2, DROPOUT_P, dz2, dz1, self.grads)
+        if self.grad_hook is not None:
+            self.grad_hook(self.grads.flat)
+        self.step_optimizer()
+        return self.loss
+
     def step_optimizer(self):
         L = qlib()
         n = self.online.numel
@@ -338,7 +371,11 @@ class Learner:
         qcheck(L.evx_clip_adam(_p(self.online.flat), _p(self.grads.flat), _p(self.m), _p(self.v), n,
                                _p(self.norm) if self.max_norm else None, float(self.max_norm or 0.0), C.byref(h),
                                _stream()), "clip_adam")
+        if self.fast is not None:
+            self.fast.repack()  # bf16 copies follow the fp32 master parameters
 
     def sync_target(self):
         """DQNAgent.update_target_network (agents/dqn_agent.py:170-172)."""
         self.target.flat.copy_(self.online.flat)
+        if self.fast_t is not None:
+            self.fast_t.repack()

@@ -24,7 +24,7 @@ import torch
 from . import _lib
 from .env import OBS_WORDS, DeviceLayout, VecEnv, _stream
 from .qnet import DROPOUT_P, Learner, qcheck, qlib
-from .qmlp import HID, MLPFast
+from .qmlp import HID
 
 
 class evx_replay(C.Structure):
@@ -102,18 +102,17 @@ class VecTrainer:
         self.ev_reset = torch.cuda.Event()
         self.ev_reset.record(torch.cuda.current_stream(self.device))
         self.last_loss: Optional[torch.Tensor] = None
-        # bf16 MLP: act straight from compact observations (csrc/qmlp.hip)
-        self.fast = MLPFast(self.learner.online, self.device) if (kind == "mlp" and precision == "bf16") else None
+        # bf16 MLP: act and learn straight from compact observations (csrc/qmlp.hip)
+        self.fast = self.learner.fast
         if self.fast is not None:
             self.h1_act = torch.empty(n * HID, dtype=torch.int16, device=self.device)
-            self.drop_stream = 0
 
     def act(self):
         if self.fast is not None:
             # DQNAgent.act in train mode: dropout active, epsilon-greedy over argmax Q
-            self.drop_stream += 1
+            self.learner.drop_stream += 1
             self.fast.forward(self.lay.c, self.env.obs, self.n_agents, self.h1_act,
-                              drop=(self.seed, self.drop_stream, DROPOUT_P), actions=self.actions,
+                              drop=(self.seed, self.learner.drop_stream, DROPOUT_P), actions=self.actions,
                               epsilon=float(self.epsilon), act_seed=self.seed, act_offset=self.t * self.n_agents)
             return self.actions
         x = self.env.expand_obs(torch.float32)  # [E, R, 11, 11, 6]
@@ -126,11 +125,13 @@ class VecTrainer:
         if self.replay.size < self.batch:
             return None
         self.replay.sample(self.batch, self.seed + 1, self.learn_steps * self.batch, self.samp)
-        s = self.env.expand_obs(torch.float32, self.samp["s"]).view(self.batch, 11, 11, 6)
-        s2 = self.env.expand_obs(torch.float32, self.samp["s2"]).view(self.batch, 11, 11, 6)
-        loss = self.learner.learn(s, self.samp["a"], self.samp["r"], self.samp["done"], s2)
         if self.fast is not None:
-            self.fast.repack()  # bf16 copies follow the updated fp32 parameters
+            loss = self.learner.learn_obs(self.lay.c, self.samp["s"], self.samp["a"], self.samp["r"],
+                                          self.samp["done"], self.samp["s2"], self.batch)
+        else:
+            s = self.env.expand_obs(torch.float32, self.samp["s"]).view(self.batch, 11, 11, 6)
+            s2 = self.env.expand_obs(torch.float32, self.samp["s2"]).view(self.batch, 11, 11, 6)
+            loss = self.learner.learn(s, self.samp["a"], self.samp["r"], self.samp["done"], s2)
         self.learn_steps += 1
         if self.epsilon > self.epsilon_min:  # DQNAgent.learn epsilon schedule (agents/dqn_agent.py:163-164)
             self.epsilon *= self.epsilon_decay

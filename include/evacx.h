@@ -222,6 +222,18 @@ typedef struct {
 int evx_qmlp_pack(const float *w1, const float *w2, uint16_t *w1b, uint16_t *w2b, uint16_t *w2t, void *stream);
 int evx_qmlp_forward(const evx_layout *lay, const evx_obs *obs, int32_t n, const evx_qmlp_params *p,
                      const evx_qmlp_dropout *drop, const evx_qmlp_fwd_out *out, void *stream);
+/* fp32 gradient tensors (the reference's parameter shapes: fc1.weight [512][726], ...) */
+typedef struct {
+    float *w1, *b1, *w2, *b2, *w3, *b3;
+} evx_qmlp_grads;
+
+/* loss.backward() of DQNAgent.learn (agents/dqn_agent.py:150-158) for the saved online
+ * forward (x, h1, h2 of evx_qmlp_forward) given dQ = d loss / d Q [B][5]. Gradients are
+ * accumulated with atomics (zero_grads = 1 clears them first). dz2 [B][256] and dz1
+ * [B][512] are bf16 scratch. Needs p->w2t. */
+int evx_qmlp_backward(const evx_qmlp_params *p, int32_t B, const float *dq, const uint16_t *x, const uint16_t *h1,
+                      const float *h2, float drop_p, uint16_t *dz2, uint16_t *dz1, const evx_qmlp_grads *g,
+                      int32_t zero_grads, void *stream);
 const char *evx_qmlp_last_error(void);
 
 #ifdef __cplusplus
