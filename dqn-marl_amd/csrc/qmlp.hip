@@ -155,7 +155,8 @@ __device__ __forceinline__ void unpack6(uint32_t v, uint32_t& p01, uint32_t& p23
 // cells per chunk. NTW = 32-column tiles per wave: 2 -> a workgroup covers 256
 // columns, grid.y = 2 (act batches); 1 -> 128 columns, grid.y = 4 (learner batches).
 template <int NTW>
-__global__ __launch_bounds__(256, 2) void qfc1_kernel(Fwd a) {
+__global__ __launch_bounds__(256, 2) void qfc1_kernel(Fwd a0, Fwd a1) {
+    const Fwd& a = blockIdx.z ? a1 : a0;  // two independent problems in one launch (online / target)
     constexpr int KC = 48, NKC = K1P / KC, APAD = KC + 8;
     __shared__ __attribute__((aligned(16))) __bf16 As[2][RM][APAD];
     __shared__ uint32_t Fs[RM][129];  // packed cells of the workgroup's rows
@@ -271,7 +272,8 @@ __global__ __launch_bounds__(256, 2) void qfc1_kernel(Fwd a) {
 }
 
 // ------------------------------------------------------------ fc2 + fc3
-__global__ __launch_bounds__(256, 2) void qfc23_kernel(Fwd a) {
+__global__ __launch_bounds__(256, 2) void qfc23_kernel(Fwd a0, Fwd a1) {
+    const Fwd& a = blockIdx.z ? a1 : a0;
     __shared__ __attribute__((aligned(16))) __bf16 As[2][RM][32];
     __shared__ float Hs[RM][HID2 + 1];
     __shared__ float W3s[NACT][HID2];
@@ -641,7 +643,13 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const __bf16* __restric
     }
 }
 
-__global__ __launch_bounds__(256) void zero_kernel(float* __restrict__ p, int64_t n) {
+struct Zero6 {
+    float* p[6];
+    int64_t n[6];
+};
+__global__ __launch_bounds__(256) void zero_kernel(Zero6 z) {
+    float* p = z.p[blockIdx.y];
+    const int64_t n = z.n[blockIdx.y];
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) p[i] = 0.f;
 }
 
@@ -674,14 +682,12 @@ int evx_qmlp_pack(const float* w1, const float* w2, uint16_t* w1b, uint16_t* w2b
     return mlaunch("qmlp_pack");
 }
 
-int evx_qmlp_forward(const evx_layout* lay, const evx_obs* obs, int32_t n, const evx_qmlp_params* p,
-                     const evx_qmlp_dropout* drop, const evx_qmlp_fwd_out* out, void* stream) {
+static int make_fwd(const evx_layout* lay, const evx_obs* obs, int32_t n, const evx_qmlp_params* p,
+                    const evx_qmlp_dropout* drop, const evx_qmlp_fwd_out* out, evxm::Fwd& a) {
     if (!lay || !obs || !p || !out) return mfail(-22, "qmlp_forward: NULL argument");
-    if (n <= 0) return 0;
     if (!p->w1 || !p->b1 || !p->w2 || !p->b2 || !p->w3 || !p->b3) return mfail(-22, "qmlp_forward: missing parameter");
     if (!out->h1) return mfail(-22, "qmlp_forward: h1 buffer required");
     if (!lay->danger_o32 || !lay->cellinfo) return mfail(-22, "qmlp_forward: layout tables missing");
-    evxm::Fwd a;
     a.N = n;
     a.obs = obs;
     a.cellinfo = lay->cellinfo;
@@ -713,16 +719,42 @@ int evx_qmlp_forward(const evx_layout* lay, const evx_obs* obs, int32_t n, const
     a.epsilon = out->epsilon;
     a.act_seed = out->act_seed;
     a.act_offset = out->act_offset;
+    return 0;
+}
+
+static int launch_fwd(const evxm::Fwd& a0, const evxm::Fwd& a1, int32_t n, int pairs, bool fc23, hipStream_t st) {
     const unsigned blocks = (unsigned)((n + evxm::RM - 1) / evxm::RM);
-    if (blocks >= 512)  // enough row tiles to fill the chip: workgroups of 64 rows x 256 columns
-        hipLaunchKernelGGL(evxm::qfc1_kernel<2>, dim3(blocks, 2), dim3(256), 0, (hipStream_t)stream, a);
+    if (blocks * pairs >= 512)  // enough row tiles to fill the chip: workgroups of 64 rows x 256 columns
+        hipLaunchKernelGGL(evxm::qfc1_kernel<2>, dim3(blocks, 2, pairs), dim3(256), 0, st, a0, a1);
     else
-        hipLaunchKernelGGL(evxm::qfc1_kernel<1>, dim3(blocks, 4), dim3(256), 0, (hipStream_t)stream, a);
+        hipLaunchKernelGGL(evxm::qfc1_kernel<1>, dim3(blocks, 4, pairs), dim3(256), 0, st, a0, a1);
     int rc = mlaunch("qfc1");
-    if (rc) return rc;
-    if (!out->q && !out->actions && !out->h2) return 0;
-    hipLaunchKernelGGL(evxm::qfc23_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a);
+    if (rc || !fc23) return rc;
+    hipLaunchKernelGGL(evxm::qfc23_kernel, dim3(blocks, 1, pairs), dim3(256), 0, st, a0, a1);
     return mlaunch("qfc23");
+}
+
+int evx_qmlp_forward(const evx_layout* lay, const evx_obs* obs, int32_t n, const evx_qmlp_params* p,
+                     const evx_qmlp_dropout* drop, const evx_qmlp_fwd_out* out, void* stream) {
+    if (n <= 0) return 0;
+    evxm::Fwd a;
+    int rc = make_fwd(lay, obs, n, p, drop, out, a);
+    if (rc) return rc;
+    return launch_fwd(a, a, n, 1, out->q || out->actions || out->h2, (hipStream_t)stream);
+}
+
+int evx_qmlp_forward2(const evx_layout* lay, int32_t n, const evx_obs* obs0, const evx_qmlp_params* p0,
+                      const evx_qmlp_dropout* drop0, const evx_qmlp_fwd_out* out0, const evx_obs* obs1,
+                      const evx_qmlp_params* p1, const evx_qmlp_dropout* drop1, const evx_qmlp_fwd_out* out1,
+                      void* stream) {
+    if (n <= 0) return 0;
+    evxm::Fwd a0, a1;
+    int rc = make_fwd(lay, obs0, n, p0, drop0, out0, a0);
+    if (!rc) rc = make_fwd(lay, obs1, n, p1, drop1, out1, a1);
+    if (rc) return rc;
+    if (!(out0->q || out0->actions || out0->h2) || !(out1->q || out1->actions || out1->h2))
+        return mfail(-22, "qmlp_forward2: both problems need an fc2/fc3 output");
+    return launch_fwd(a0, a1, n, 2, true, (hipStream_t)stream);
 }
 
 int evx_qmlp_backward(const evx_qmlp_params* p, int32_t B, const float* dq, const uint16_t* x, const uint16_t* h1,
@@ -734,12 +766,10 @@ int evx_qmlp_backward(const evx_qmlp_params* p, int32_t B, const float* dq, cons
     if (B <= 0) return 0;
     hipStream_t st = (hipStream_t)stream;
     if (zero_grads) {
-        float* gz[6] = {g->w1, g->b1, g->w2, g->b2, g->w3, g->b3};
-        const int64_t nz[6] = {(int64_t)evxm::HID * evxm::K1, evxm::HID, (int64_t)evxm::HID2 * evxm::HID, evxm::HID2,
-                               (int64_t)evxm::NACT * evxm::HID2, evxm::NACT};
-        for (int i = 0; i < 6; i++)
-            hipLaunchKernelGGL(evxm::zero_kernel, dim3((unsigned)std::min<int64_t>(1024, (nz[i] + 255) / 256)), dim3(256),
-                               0, st, gz[i], nz[i]);
+        evxm::Zero6 z = {{g->w1, g->b1, g->w2, g->b2, g->w3, g->b3},
+                         {(int64_t)evxm::HID * evxm::K1, evxm::HID, (int64_t)evxm::HID2 * evxm::HID, evxm::HID2,
+                          (int64_t)evxm::NACT * evxm::HID2, evxm::NACT}};
+        hipLaunchKernelGGL(evxm::zero_kernel, dim3(256, 6), dim3(256), 0, st, z);
     }
     evxm::Bwd a;
     a.B = B;

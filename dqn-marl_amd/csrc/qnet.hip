@@ -267,21 +267,26 @@ __global__ __launch_bounds__(256) void colsum_finish(const float* __restrict__ p
 // --------------------------------------------------------------- TD loss
 // DQNAgent.learn (agents/dqn_agent.py:143-151): q = Q(s).gather(a); y = r + gamma *
 // max Q_tgt(s') * ~done; loss = mean((q - y)^2); dQ[i, a_i] = 2 (q - y) / B.
+// One row per thread over many blocks; the last block to finish sums the block
+// partials in block order (deterministic).
+__device__ float g_td_part[4096];
+__device__ unsigned int g_td_ticket = 0;
 __global__ __launch_bounds__(256) void td_loss_kernel(const float* __restrict__ Q, const float* __restrict__ Qt,
                                                       int A, const int32_t* __restrict__ act,
                                                       const float* __restrict__ rew, const uint8_t* __restrict__ done,
                                                       float gamma, int B, float* __restrict__ dQ,
                                                       float* __restrict__ loss_out) {
     __shared__ float red[256];
+    __shared__ bool last;
+    const int i = blockIdx.x * 256 + threadIdx.x;
     float part = 0.f;
-    for (int i = threadIdx.x; i < B; i += 256) {
+    if (i < B) {
         float mx = Qt[(int64_t)i * A];
         for (int j = 1; j < A; j++) mx = fmaxf(mx, Qt[(int64_t)i * A + j]);
         const float y = rew[i] + gamma * mx * (done[i] ? 0.f : 1.f);
         const int a = act[i];
-        const float q = Q[(int64_t)i * A + a];
-        const float d = q - y;
-        part += d * d;
+        const float d = Q[(int64_t)i * A + a] - y;
+        part = d * d;
         for (int j = 0; j < A; j++) dQ[(int64_t)i * A + j] = (j == a) ? 2.f * d / (float)B : 0.f;
     }
     red[threadIdx.x] = part;
@@ -290,7 +295,19 @@ __global__ __launch_bounds__(256) void td_loss_kernel(const float* __restrict__ 
         if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
         __syncthreads();
     }
-    if (threadIdx.x == 0) loss_out[0] = red[0] / (float)B;
+    if (threadIdx.x == 0) {
+        g_td_part[blockIdx.x] = red[0];
+        __threadfence();
+        last = atomicAdd(&g_td_ticket, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (last && threadIdx.x == 0) {
+        __threadfence();
+        float t = 0.f;
+        for (unsigned k = 0; k < gridDim.x; k++) t += __hip_atomic_load(&g_td_part[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        loss_out[0] = t / (float)B;
+        g_td_ticket = 0;
+    }
 }
 
 // ------------------------------------------------- clip_grad_norm_ + Adam
@@ -556,7 +573,8 @@ int evx_colsum(const float* X, int64_t ld, int32_t M, int32_t N, float* out, int
 int evx_td_loss(const float* Q, const float* Qt, int32_t A, const int32_t* act, const float* rew, const uint8_t* done,
                 float gamma, int32_t B, float* dQ, float* loss, void* stream) {
     if (B <= 0) return 0;
-    hipLaunchKernelGGL(evxq::td_loss_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, Q, Qt, A, act, rew, done,
+    if (B > 4096 * 256) return qfail(-22, "td_loss: batch too large");
+    hipLaunchKernelGGL(evxq::td_loss_kernel, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream, Q, Qt, A, act, rew, done,
                        gamma, B, dQ, loss);
     return qlaunch("td_loss");
 }

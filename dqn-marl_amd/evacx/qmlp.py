@@ -47,6 +47,10 @@ def mlib():
         L.evx_qmlp_pack.argtypes = [C.c_void_p] * 6
         L.evx_qmlp_forward.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(evx_qmlp_params),
                                        C.POINTER(evx_qmlp_dropout), C.POINTER(evx_qmlp_fwd_out), C.c_void_p]
+        L.evx_qmlp_forward2.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.POINTER(evx_qmlp_params),
+                                        C.POINTER(evx_qmlp_dropout), C.POINTER(evx_qmlp_fwd_out), C.c_void_p,
+                                        C.POINTER(evx_qmlp_params), C.POINTER(evx_qmlp_dropout),
+                                        C.POINTER(evx_qmlp_fwd_out), C.c_void_p]
         L.evx_qmlp_backward.argtypes = [C.POINTER(evx_qmlp_params), C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
                                         C.c_void_p, C.c_float, C.c_void_p, C.c_void_p, C.POINTER(evx_qmlp_grads),
                                         C.c_int32, C.c_void_p]
@@ -93,6 +97,23 @@ class MLPFast:
                                        C.byref(d) if d is not None else None, C.byref(o), _stream()),
                "qmlp_forward")
 
+
+    @staticmethod
+    def _drop(drop):
+        return evx_qmlp_dropout(seed=drop[0] & 0xFFFFFFFF, stream=drop[1] & 0xFFFFFFFF, p=drop[2])
+
+    @staticmethod
+    def _out(h1, x=None, h2=None, q=None):
+        return evx_qmlp_fwd_out(h1=_p(h1), x=_p(x), h2=_p(h2), q=_p(q))
+
+    @staticmethod
+    def forward_pair(lay_c, n, net0, obs0, drop0, out0: dict, net1, obs1, drop1, out1: dict):
+        """Two forwards (e.g. online and target) in one launch pair; out*: h1, x, h2, q tensors."""
+        d0, d1 = MLPFast._drop(drop0), MLPFast._drop(drop1)
+        o0, o1 = MLPFast._out(**out0), MLPFast._out(**out1)
+        mcheck(mlib().evx_qmlp_forward2(C.byref(lay_c), n, obs0.data_ptr(), C.byref(net0.c), C.byref(d0), C.byref(o0),
+                                        obs1.data_ptr(), C.byref(net1.c), C.byref(d1), C.byref(o1), _stream()),
+               "qmlp_forward2")
 
     def backward(self, B: int, dq: torch.Tensor, x: torch.Tensor, h1: torch.Tensor, h2: torch.Tensor, drop_p: float,
                  dz2: torch.Tensor, dz1: torch.Tensor, grads, zero=True):

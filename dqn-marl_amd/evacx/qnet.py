@@ -349,8 +349,9 @@ class Learner:
         dz2 = ws.get("fdz2", (B * HID2,), torch.int16, dev)
         dz1 = ws.get("fdz1", (B * HID,), torch.int16, dev)
         self.drop_stream += 2
-        self.fast.forward(lay_c, s_obs, B, H1, drop=(self.seed, self.drop_stream, DROPOUT_P), x=X, h2=H2, q=Q)
-        self.fast_t.forward(lay_c, s2_obs, B, H1t, drop=(self.seed, self.drop_stream + 1, DROPOUT_P), q=Qt)
+        type(self.fast).forward_pair(lay_c, B, self.fast, s_obs, (self.seed, self.drop_stream, DROPOUT_P),
+                                     dict(h1=H1, x=X, h2=H2, q=Q), self.fast_t, s2_obs,
+                                     (self.seed, self.drop_stream + 1, DROPOUT_P), dict(h1=H1t, q=Qt))
         L = qlib()
         qcheck(L.evx_td_loss(_p(Q), _p(Qt), self.actions, _p(a), _p(r), _p(done), self.gamma, B, _p(dQ),
                              _p(self.loss), _stream()), "td_loss")

@@ -222,6 +222,12 @@ typedef struct {
 int evx_qmlp_pack(const float *w1, const float *w2, uint16_t *w1b, uint16_t *w2b, uint16_t *w2t, void *stream);
 int evx_qmlp_forward(const evx_layout *lay, const evx_obs *obs, int32_t n, const evx_qmlp_params *p,
                      const evx_qmlp_dropout *drop, const evx_qmlp_fwd_out *out, void *stream);
+/* Two forwards of n rows in one launch pair (the learner's online and target nets). */
+int evx_qmlp_forward2(const evx_layout *lay, int32_t n, const evx_obs *obs0, const evx_qmlp_params *p0,
+                      const evx_qmlp_dropout *drop0, const evx_qmlp_fwd_out *out0, const evx_obs *obs1,
+                      const evx_qmlp_params *p1, const evx_qmlp_dropout *drop1, const evx_qmlp_fwd_out *out1,
+                      void *stream);
+
 /* fp32 gradient tensors (the reference's parameter shapes: fc1.weight [512][726], ...) */
 typedef struct {
     float *w1, *b1, *w2, *b2, *w3, *b3;
