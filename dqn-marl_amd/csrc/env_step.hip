@@ -454,16 +454,16 @@ __device__ __forceinline__ int pb_bits(int P) { return P > 1 ? bit_length((uint3
 #define EVX_STAMP(i)                                                                                   \
     do {                                                                                               \
         if (out.stamps && threadIdx.x == 0)                                                            \
-            out.stamps[(size_t)blockIdx.x * 32 + (i)] = (int64_t)__builtin_amdgcn_s_memtime();         \
+            out.stamps[(size_t)e * 32 + (i)] = (int64_t)__builtin_amdgcn_s_memtime();         \
     } while (0)
 #define EVX_RSTAMP(i)                                                                                  \
     do {                                                                                               \
         if (out.stamps && threadIdx.x == 0)                                                            \
-            out.stamps[(size_t)blockIdx.x * 32 + (i)] = (int64_t)__builtin_amdgcn_s_memrealtime();     \
+            out.stamps[(size_t)e * 32 + (i)] = (int64_t)__builtin_amdgcn_s_memrealtime();     \
     } while (0)
 #define EVX_COUNT(i, v)                                                                                \
     do {                                                                                               \
-        if (out.stamps && threadIdx.x == 0) out.stamps[(size_t)blockIdx.x * 32 + (i)] = (v);           \
+        if (out.stamps && threadIdx.x == 0) out.stamps[(size_t)e * 32 + (i)] = (v);           \
     } while (0)
 
 // EVX_PROFILE builds only: cycle accumulators of sub-phases, stored to slots 16..31
@@ -495,7 +495,7 @@ __device__ __forceinline__ double readlane_d(double v, int k) {
 __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state st, const int32_t* __restrict__ actions,
                                                       evx_step_out out) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    const int e = blockIdx.x;
+    const int e = st.order ? st.order[blockIdx.x] : (int)blockIdx.x;  // heavy envs first (evx_env_order)
     const int lane = threadIdx.x;
     EVX_RSTAMP(9);
     EVX_STAMP(0);
@@ -635,9 +635,10 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
     // range of some robot; only there does find_best_direction's robot loop run.
     const int rd2 = lay.repel_d2;
     const int BY = (GY + 3) >> 2;
+    int rr = 0;
+    while ((rr + 1) * (rr + 1) < rd2) rr++;
+    const int rb = rr + 1;  // a neighbour within range of a robot lies within rb of it in x and y
     if (rd2 > 0) {
-        int rr = 0;
-        while ((rr + 1) * (rr + 1) < rd2) rr++;
         for (int r = 0; r < R; r++) {
             const uint32_t rp = robots[r];
             const int bx0 = max(rp_x(rp) - rr, 0) >> 2, bx1 = min(rp_x(rp) + rr, g.L + 1) >> 2;
@@ -661,7 +662,7 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
 
     // --------------------- People.run phases 1+2 (health, accumulate, plan)
     const double* __restrict__ dpt = lay.danger_p + (size_t)fs * g.G;
-    const double* __restrict__ flo = lay.floor;
+    const double* __restrict__ fd5 = lay.floor_d5;
     const uint8_t* __restrict__ nbv = lay.nbr_valid;
     int doff[8];
 #pragma unroll
@@ -702,14 +703,18 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
         const int p = (int)(ea & 0xffffu);
         const uint32_t cand = ea >> 16;
         const int x = pk_x(eb), y = pk_y(eb), cold = x * GY + y;
-        double f0 = 0.0, f[8];
+        // (floor[c] - floor[c + MoveTO[d]]) * 5.0 for the 8 directions: one 64-B row
+        double f[8];
 #pragma unroll
         for (int d = 0; d < 8; d++) f[d] = 0.0;
         if (has) {
-            f0 = flo[cold];
+            const double2* fr = reinterpret_cast<const double2*>(fd5 + (size_t)cold * 8);
 #pragma unroll
-            for (int d = 0; d < 8; d++)
-                if ((cand >> d) & 1u) f[d] = flo[cold + doff[d]];
+            for (int q2 = 0; q2 < 4; q2++) {
+                const double2 v = fr[q2];
+                f[2 * q2] = v.x;
+                f[2 * q2 + 1] = v.y;
+            }
         }
         const int first = __builtin_amdgcn_readfirstlane(off);
         const int end = __builtin_amdgcn_readlane(off + 2 * __popc(cand), n - 1);
@@ -732,8 +737,9 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
                 const uint32_t rq[4] = {q4.x, q4.y, q4.z, q4.w};
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
-                    if (r0 + j < R) {
-                        const int rx = rp_x(rq[j]), ry = rp_y(rq[j]);
+                    const int rx = rp_x(rq[j]), ry = rp_y(rq[j]);
+                    // robots no lane is near cannot be the nearest within range: skipped
+                    if (r0 + j < R && __ballot(abs(x - rx) <= rb && abs(y - ry) <= rb)) {
 #pragma unroll
                         for (int d = 0; d < 8; d++) {
                             const int dx = x + move_dx(d) - rx, dy = y + move_dy(d) - ry;
@@ -744,7 +750,6 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
             }
         }
 #ifdef EVX_PROFILE
-        pin(f0);
 #pragma unroll
         for (int d = 0; d < 8; d++) pin(f[d]);
 #endif
@@ -760,12 +765,11 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
 #pragma unroll
                 for (int d = 0; d < 8; d++) {
                     if ((cand >> d) & 1u) {
-                        const double delta_p = f0 - f[d];
                         double effect = 0.0;
                         if (((nearm >> d) & 1u) && md2[d] < rd2) effect = lay.repel_k / (sqrt((double)md2[d]) + 0.1);
                         const double u = -0.1 + (0.1 - -0.1) * mt_double(pyring, WRM, idx);
                         idx += 2;
-                        const double score = delta_p * 5.0 + effect + u;
+                        const double score = f[d] + effect + u;  // delta_p * 5.0 + robot_effect + uniform
                         if (score > maxs) {
                             maxs = score;
                             best = (uint32_t)d;
@@ -1561,6 +1565,59 @@ __global__ __launch_bounds__(64) void env_reset_kernel(evx_layout lay, evx_state
 #endif
 }
 
+// ------------------------------------------------------- dispatch order
+// A step's cost grows with the persons still in play, and one env is one wave:
+// the launch ends with its slowest env. Dispatching envs by descending remaining
+// persons (16 buckets, stable counting sort in one workgroup) starts the heavy
+// ones first so the light ones fill in around them.
+__global__ __launch_bounds__(1024) void env_order_kernel(evx_layout lay, evx_state st) {
+    __shared__ int cnt[16], base[16];
+    const int tid = threadIdx.x, E = st.E, P = lay.P;
+    if (tid < 16) cnt[tid] = 0;
+    __syncthreads();
+    auto bucket = [&](int e) {
+        const int rem = P - st.scal[(size_t)e * 4 + 2] - st.scal[(size_t)e * 4 + 3];
+        return 15 - min(15, max(0, rem) * 16 / (P + 1));  // 0 = most remaining
+    };
+    for (int e = tid; e < E; e += 1024) atomicAdd(&cnt[bucket(e)], 1);
+    __syncthreads();
+    if (tid == 0) {
+        int o = 0;
+        for (int b = 0; b < 16; b++) {
+            base[b] = o;
+            o += cnt[b];
+        }
+    }
+    __syncthreads();
+    // stable within a bucket: chunks of 1024 envs in order; rank = bucket base + the
+    // same-bucket envs of lower waves + lower lanes (ballots)
+    __shared__ int wcnt[16][16];
+    const int lane = tid & 63, w = tid >> 6;
+    for (int e0 = 0; e0 < E; e0 += 1024) {
+        const int e = e0 + tid;
+        const int bk = e < E ? bucket(e) : -1;
+        int inw = 0;
+        for (int bb = 0; bb < 16; bb++) {
+            const unsigned long long m = __ballot(bk == bb);
+            if (lane == 0) wcnt[w][bb] = __popcll(m);
+            if (bk == bb) inw = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        }
+        __syncthreads();
+        if (e < E) {
+            int r = base[bk] + inw;
+            for (int ww = 0; ww < w; ww++) r += wcnt[ww][bk];
+            st.order[r] = e;
+        }
+        __syncthreads();
+        if (tid < 16) {
+            int c = 0;
+            for (int ww = 0; ww < 16; ww++) c += wcnt[ww][tid];
+            base[tid] += c;
+        }
+        __syncthreads();
+    }
+}
+
 // ---------------------------------------------------- observation expand
 // EvacuationEnv._get_state (envs/evacuation_env.py:84-120) from the compact form.
 template <typename T>
@@ -1641,7 +1698,7 @@ int evx_env_step(const evx_layout* l, const evx_state* s, const int32_t* actions
     if (rc) return rc;
     if (!s || !o || !actions || !o->reward || !o->done || !o->obs) return fail(-22, "NULL argument");
     if (!s->scratch) return fail(-22, "state scratch is NULL (evx_step_scratch_words per env)");
-    if (!l->nbr_valid) return fail(-22, "missing table nbr_valid");
+    if (!l->nbr_valid || !l->floor_d5) return fail(-22, "missing table nbr_valid / floor_d5");
     if (s->E <= 0) return 0;
     const int G = (l->L + 2) * (l->W + 2);
     {  // contested-list keys are (target << bits(P-1)) | person in 32 bits
@@ -1683,6 +1740,16 @@ int evx_env_reset(const evx_layout* l, const evx_state* s, const uint8_t* mask, 
                        err);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : hip_fail(e, "env_reset launch");
+}
+
+int evx_env_order(const evx_layout* l, const evx_state* s, void* stream) {
+    int rc = check_layout(l);
+    if (rc) return rc;
+    if (!s || !s->order) return fail(-22, "env_order: state.order is NULL");
+    if (s->E <= 0) return 0;
+    hipLaunchKernelGGL(evx::env_order_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, *l, *s);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : hip_fail(e, "env_order launch");
 }
 
 int evx_obs_expand_f32(const evx_layout* l, const evx_obs* obs, int64_t n, float* out, void* stream) {

@@ -25,13 +25,13 @@ class evx_layout(C.Structure):
                [(n, C.c_double) for n in ["repel_k", "repel_range", "evac_reward", "death_penalty",
                                          "death_acc_penalty", "alive_bonus"]] + \
                [(n, C.c_void_p) for n in ["floor", "cellinfo", "valid_bits", "danger_p", "danger_o",
-                                         "danger_o32", "robot_init", "nbr_valid"]]
+                                         "danger_o32", "robot_init", "nbr_valid", "floor_d5"]]
 
 
 class evx_state(C.Structure):
     _fields_ = [("E", C.c_int32)] + [(n, C.c_void_p) for n in
                                      ["pk", "health", "acc", "rmap", "thmap", "robots", "view", "scal",
-                                      "py_mt", "np_mt", "scratch"]]
+                                      "py_mt", "np_mt", "scratch", "order"]]
 
 
 class evx_step_out(C.Structure):
@@ -53,7 +53,7 @@ def lib():
         L.evx_step_lds_bytes.argtypes = [C.POINTER(evx_layout)]
         L.evx_step_scratch_words.argtypes = [C.POINTER(evx_layout)]
         for name in ["evx_env_step", "evx_env_reset", "evx_obs_expand_f32", "evx_obs_expand_f64",
-                     "evx_seed_host"]:
+                     "evx_seed_host", "evx_env_order"]:
             getattr(L, name).restype = C.c_int
         L.evx_env_step.argtypes = [C.POINTER(evx_layout), C.POINTER(evx_state), C.c_void_p,
                                    C.POINTER(evx_step_out), C.c_void_p]
@@ -62,6 +62,7 @@ def lib():
         L.evx_obs_expand_f32.argtypes = [C.POINTER(evx_layout), C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p]
         L.evx_obs_expand_f64.argtypes = [C.POINTER(evx_layout), C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p]
         L.evx_seed_host.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
+        L.evx_env_order.argtypes = [C.POINTER(evx_layout), C.POINTER(evx_state), C.c_void_p]
         _lib = L
     return _lib
 

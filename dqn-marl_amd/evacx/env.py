@@ -71,6 +71,28 @@ def neighbour_valid_mask(valid: np.ndarray, L: int, W: int) -> np.ndarray:
     return m.reshape(-1)
 
 
+def floor_delta5(floor: np.ndarray, L: int, W: int) -> np.ndarray:
+    """[G][8] float64: (floor[c] - floor[c + MoveTO[d]]) * 5.0 -- Map.getDeltaP * 5.0 of
+    People.find_best_direction (envs/people.py:268,282), evaluated once in IEEE double
+    exactly as the reference does per candidate; 0 where the neighbour is off the grid."""
+    GX, GY = L + 2, W + 2
+    f = np.asarray(floor, np.float64).reshape(GX, GY)
+    out = np.zeros((GX, GY, 8), np.float64)
+    with np.errstate(invalid="ignore"):  # inf - inf on invalid cells: never a candidate
+        _fill_delta5(f, out, GX, GY)
+    return out.reshape(-1)
+
+
+def _fill_delta5(f, out, GX, GY):
+    for d in range(8):
+        dx, dy = MOVE_DX[d], MOVE_DY[d]
+        xs = slice(max(0, -dx), GX - max(0, dx))
+        ys = slice(max(0, -dy), GY - max(0, dy))
+        xn = slice(max(0, -dx) + dx, GX - max(0, dx) + dx)
+        yn = slice(max(0, -dy) + dy, GY - max(0, dy) + dy)
+        out[xs, ys, d] = (f[xs, ys] - f[xn, yn]) * 5.0
+
+
 class DeviceLayout:
     """Static tables of one layout in HBM + the evx_layout descriptor."""
 
@@ -97,6 +119,7 @@ class DeviceLayout:
             robot_init=torch.from_numpy(np.asarray(spec.robot_init, np.int32).reshape(-1)).to(d),
         )
         self.t["nbr_valid"] = torch.from_numpy(neighbour_valid_mask(tables.valid, spec.L, spec.W)).to(d)
+        self.t["floor_d5"] = torch.from_numpy(floor_delta5(tables.floor, spec.L, spec.W)).to(d)
         self.t["danger_o32"] = self.t["danger_o"].to(torch.float32)
         T = tables.danger_p.shape[0] - 1
         OX, OY = tables.danger_o.shape[1:]
@@ -149,6 +172,7 @@ class VecEnv:
         if sw < 0:
             raise _lib.EvacxError(_lib.lib().evx_last_error().decode())
         self.scratch = torch.zeros(E * sw, **i32)
+        self.order = torch.arange(E, **i32)  # dispatch order (evx_env_order), scheduling only
         # outputs
         self.reward = torch.zeros(E, **f64)
         self.done = torch.zeros(E, dtype=torch.uint8, device=d)
@@ -158,7 +182,7 @@ class VecEnv:
         self.c = _lib.evx_state(E=E, pk=_ptr(self.pk), health=_ptr(self.health), acc=_ptr(self.acc),
                                 rmap=_ptr(self.rmap), thmap=_ptr(self.thmap), robots=_ptr(self.robots),
                                 view=_ptr(self.view), scal=_ptr(self.scal), py_mt=_ptr(self.py_mt),
-                                np_mt=_ptr(self.np_mt), scratch=_ptr(self.scratch))
+                                np_mt=_ptr(self.np_mt), scratch=_ptr(self.scratch), order=_ptr(self.order))
         self.out = _lib.evx_step_out(reward=_ptr(self.reward), done=_ptr(self.done), counts=_ptr(self.counts),
                                      obs=_ptr(self.obs), err=_ptr(self.err))
 
@@ -195,6 +219,8 @@ class VecEnv:
     def step(self, actions: torch.Tensor):
         a = actions.to(torch.int32).contiguous()
         assert a.numel() == self.E * self.lay.R
+        if self.E >= 256:  # heavy env-steps first (scheduling only)
+            _lib.check(_lib.lib().evx_env_order(C.byref(self.lay.c), C.byref(self.c), _stream()), "evx_env_order")
         _lib.check(_lib.lib().evx_env_step(C.byref(self.lay.c), C.byref(self.c), a.data_ptr(), C.byref(self.out),
                                            _stream()), "evx_env_step")
 

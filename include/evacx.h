@@ -51,6 +51,7 @@ typedef struct {
     const float *danger_o32;  /* same, float32 (network input path) */
     const int32_t *robot_init;/* [R*2] robot positions after a multi-robot reset */
     const uint8_t *nbr_valid; /* [G] bit d: Check_Valid of the MoveTO[d] neighbour (envs/people.py:259-265) */
+    const double *floor_d5;   /* [G][8] (floor[c] - floor[c + MoveTO[d]]) * 5.0 = getDeltaP * 5.0 (envs/people.py:268,282) */
 } evx_layout;
 
 /* Structure-of-arrays state of E env instances (env-major). */
@@ -67,6 +68,7 @@ typedef struct {
     uint32_t *py_mt;   /* [E*625] CPython `random` MT19937 state per env */
     uint32_t *np_mt;   /* [E*625] legacy numpy.random MT19937 state per env */
     uint32_t *scratch; /* [E*evx_step_scratch_words] step scratch: move plan, contested lists beyond LDS */
+    int32_t *order;    /* [E] dispatch order of the step's envs (evx_env_order), or NULL = 0..E-1 */
 } evx_state;
 
 /* Compact per-robot observation (32 B). Expands to the reference's 11x11x6
@@ -108,6 +110,10 @@ int evx_obs_expand_f64(const evx_layout *lay, const evx_obs *obs, int64_t n, dou
 /* Host helper: MT19937 states for integer seeds as random.seed(s) (init_by_array)
  * and numpy.random.seed(s) (init_genrand) produce them. Host pointers. */
 int evx_seed_host(const uint32_t *seeds_host, int32_t n, uint32_t *py_mt_host, uint32_t *np_mt_host);
+
+/* Scheduling only (results do not depend on it): st->order = envs by descending
+ * persons still in play, so the heaviest env-steps start first. */
+int evx_env_order(const evx_layout *lay, const evx_state *st, void *stream);
 
 /* Bytes of dynamic LDS the step kernel needs for a layout (diagnostics). */
 int64_t evx_step_lds_bytes(const evx_layout *lay);
