@@ -235,13 +235,25 @@ __device__ __forceinline__ int doff_of(uint32_t d, int GY) { return move_dx((int
 
 template <typename T>
 __device__ __forceinline__ void contested_groups(T* Lp, T* heads, T* gstart, int n, int pb, uint32_t* pyring, int& py_front,
-                                 int& py_head, uint32_t* lost, uint32_t* grp, int& err) {
+                                 int& py_head, uint32_t* lost, uint32_t* grp, int& err, long long* prof) {
     const int lane = threadIdx.x;
+#ifdef EVX_PROFILE
+    long long tq = __builtin_amdgcn_s_memtime();
+#define CG_T(i)                                          \
+    do {                                                 \
+        const long long t2 = __builtin_amdgcn_s_memtime(); \
+        prof[i] += t2 - tq;                              \
+        tq = t2;                                         \
+    } while (0)
+#else
+#define CG_T(i)
+#endif
     const uint32_t pmask = (1u << pb) - 1u;
     const int n2 = pow2_ceil(n);
     for (int i = n + lane; i < n2; i += 64) Lp[i] = 0xffffffffu;
     __syncthreads();
     wave_sort_keys(Lp, n, n2);
+    CG_T(0);
     int ngrp = 0;
     for (int i0 = 0; i0 < n; i0 += 64) {
         const int i = i0 + lane;
@@ -264,6 +276,7 @@ __device__ __forceinline__ void contested_groups(T* Lp, T* heads, T* gstart, int
     for (int i = ngrp + lane; i < h2; i += 64) heads[i] = 0xffffffffu;
     __syncthreads();
     wave_sort_keys(heads, ngrp, h2);
+    CG_T(1);
     // group descriptors in dict order: (first mover's position in Lp << 8) | size
     for (int k = lane; k < ngrp; k += 64) {
         const int gi = (int)(heads[k] & ((1u << GBITS) - 1u));
@@ -280,8 +293,41 @@ __device__ __forceinline__ void contested_groups(T* Lp, T* heads, T* gstart, int
     // Pass 2 (lane per group): every shuffle of the chunk runs in parallel from its
     // recorded start word; only the winner (position 0 afterwards) moves.
     int pos = py_head;
-    int B = -(1 << 30);  // window [B, B + 64) of the acceptance masks
-    uint32_t mlo = 0, mhi = 0;
+    int B = -(1 << 30);  // window of the end tables: attempts may start at [B, B + 64)
+    // end[c-2] (lane j): where the shuffle of a group of c <= 8 movers starting at word
+    // B + j ends (relative to B), 255 if it needs words beyond B + 128
+    uint32_t endt[7];
+#pragma unroll
+    for (int c = 0; c < 7; c++) endt[c] = 255u;
+    auto build_window = [&](int b0) {
+        B = b0;
+        mt_ensure_w(pyring, py_front, B + 128);
+        const uint32_t t0 = mt_temper(pyring[(B + lane) & WRM]), t1 = mt_temper(pyring[(B + 64 + lane) & WRM]);
+        unsigned long long lo[7], hi[7];  // acceptance of bound 2..8 over the 128 words
+#pragma unroll
+        for (int bb = 2; bb <= 8; bb++) {
+            const int kbb = bb < 4 ? 2 : (bb < 8 ? 3 : 4);
+            lo[bb - 2] = __ballot((t0 >> (32 - kbb)) < (uint32_t)bb);
+            hi[bb - 2] = __ballot((t1 >> (32 - kbb)) < (uint32_t)bb);
+        }
+        auto next_acc = [&](int bi, int s0) -> int {  // first accepted word >= s0 for bound bi+2, else 128
+            if (s0 < 64) {
+                const unsigned long long m = lo[bi] >> s0;
+                if (m) return s0 + __builtin_ctzll(m);
+                return hi[bi] ? 64 + __builtin_ctzll(hi[bi]) : 128;
+            }
+            if (s0 >= 128) return 128;
+            const unsigned long long m = hi[bi] >> (s0 - 64);
+            return m ? s0 + __builtin_ctzll(m) : 128;
+        };
+#pragma unroll
+        for (int c = 2; c <= 8; c++) {
+            int sp = lane;
+#pragma unroll
+            for (int bb = c; bb >= 2; bb--) sp = sp < 128 ? next_acc(bb - 2, sp) + 1 : 129;
+            endt[c - 2] = sp <= 128 ? (uint32_t)sp : 255u;
+        }
+    };
     int k = 0;
     while (k < ngrp) {
         const int k0 = k, W0 = pos;
@@ -293,47 +339,44 @@ __device__ __forceinline__ void contested_groups(T* Lp, T* heads, T* gstart, int
             const uint32_t dsc = (uint32_t)__builtin_amdgcn_readlane((int)desc, nk);
             const int cnt = (int)(dsc & 255u);
             wv = lane == nk ? pos : wv;
-            for (int i = cnt - 1; i >= 1; i--) {
-                const int b = i + 1;
-                const int kb = bit_length((uint32_t)b);
+            if (cnt <= 8) {
                 while (true) {
-                    if (pos - B >= 64 || pos < B) {  // new window at pos
-                        B = pos;
-                        mt_ensure_w(pyring, py_front, B + 64);
-                        const uint32_t t = mt_temper(pyring[(B + lane) & WRM]);
-                        mlo = 0;
-                        mhi = 0;
-#pragma unroll
-                        for (int bb = 2; bb <= 8; bb++) {
-                            const int kbb = bb < 4 ? 2 : (bb < 8 ? 3 : 4);
-                            const unsigned long long m = __ballot((t >> (32 - kbb)) < (uint32_t)bb);
-                            mlo = lane == bb ? (uint32_t)m : mlo;
-                            mhi = lane == bb ? (uint32_t)(m >> 32) : mhi;
-                        }
-                    }
-                    unsigned long long m;
-                    if (b <= 8) {
-                        m = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)mhi, b) << 32) |
-                            (uint32_t)__builtin_amdgcn_readlane((int)mlo, b);
-                    } else {  // large group: test the words one by one
-                        const uint32_t t = mt_temper(pyring[(pos & WRM)]);
-                        m = ((t >> (32 - kb)) < (uint32_t)b) ? (1ull << (pos - B)) : 0ull;
-                    }
-                    m >>= (pos - B);
-                    if (b > 8 && !(m & 1ull)) {
-                        pos++;
-                        continue;
-                    }
-                    if (m) {
-                        pos += __builtin_ctzll(m) + 1;
+                    if (pos - B >= 64 || pos < B) build_window(pos);
+                    const uint32_t tab = cnt == 2 ? endt[0] : cnt == 3 ? endt[1] : cnt == 4 ? endt[2] : cnt == 5 ? endt[3]
+                                       : cnt == 6 ? endt[4] : cnt == 7 ? endt[5] : endt[6];
+                    const uint32_t en = (uint32_t)__builtin_amdgcn_readlane((int)tab, pos - B);
+                    if (en != 255u) {
+                        pos = B + (int)en;
                         break;
                     }
-                    pos = B + 64;
+                    build_window(pos);  // the group runs past B + 128 from here: restart the window at it
+                    const uint32_t tab2 = cnt == 2 ? endt[0] : cnt == 3 ? endt[1] : cnt == 4 ? endt[2] : cnt == 5 ? endt[3]
+                                        : cnt == 6 ? endt[4] : cnt == 7 ? endt[5] : endt[6];
+                    const uint32_t en2 = (uint32_t)__builtin_amdgcn_readlane((int)tab2, 0);
+                    if (en2 != 255u) {
+                        pos = B + (int)en2;
+                        break;
+                    }
+                    err |= 2;  // > 128 words for <= 8 movers: not a sane stream
+                    break;
                 }
+            } else {  // large group: bounds > 8 word by word (rare)
+                for (int i = cnt - 1; i >= 1; i--) {
+                    const uint32_t bound = (uint32_t)(i + 1);
+                    const int kb = bit_length(bound);
+                    while (true) {
+                        if (py_front < pos + 1) mt_ensure_w(pyring, py_front, pos + 64);
+                        const uint32_t t = mt_temper(pyring[pos & WRM]);
+                        pos++;
+                        if ((t >> (32 - kb)) < bound) break;
+                    }
+                }
+                B = -(1 << 30);  // end tables are stale
             }
             nk++;
             k++;
         }
+        CG_T(2);
         __syncthreads();  // ring words [W0, pos) are in place
         // Pass 2: lane j shuffles group k0 + j (Lib/random.py shuffle, in registers)
         if (lane < nk) {
@@ -394,8 +437,10 @@ __device__ __forceinline__ void contested_groups(T* Lp, T* heads, T* gstart, int
             }
         }
         __syncthreads();
+        CG_T(3);
     }
     py_head = pos;
+#undef CG_T
 }
 
 // First planner of contested target t (the group's smallest person index).
@@ -454,16 +499,16 @@ __device__ __forceinline__ int pb_bits(int P) { return P > 1 ? bit_length((uint3
 #define EVX_STAMP(i)                                                                                   \
     do {                                                                                               \
         if (out.stamps && threadIdx.x == 0)                                                            \
-            out.stamps[(size_t)e * 32 + (i)] = (int64_t)__builtin_amdgcn_s_memtime();         \
+            out.stamps[(size_t)e * 48 + (i)] = (int64_t)__builtin_amdgcn_s_memtime();         \
     } while (0)
 #define EVX_RSTAMP(i)                                                                                  \
     do {                                                                                               \
         if (out.stamps && threadIdx.x == 0)                                                            \
-            out.stamps[(size_t)e * 32 + (i)] = (int64_t)__builtin_amdgcn_s_memrealtime();     \
+            out.stamps[(size_t)e * 48 + (i)] = (int64_t)__builtin_amdgcn_s_memrealtime();     \
     } while (0)
 #define EVX_COUNT(i, v)                                                                                \
     do {                                                                                               \
-        if (out.stamps && threadIdx.x == 0) out.stamps[(size_t)e * 32 + (i)] = (v);           \
+        if (out.stamps && threadIdx.x == 0) out.stamps[(size_t)e * 48 + (i)] = (v);           \
     } while (0)
 
 // EVX_PROFILE builds only: cycle accumulators of sub-phases, stored to slots 16..31
@@ -1003,21 +1048,34 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
     __syncthreads();  // plan[] and the person writes are visible to every lane
     EVX_STAMP(2);
 
+    // The move plan in HBM is walked 4 x 64 entries at a time, loads first.
+    auto plan_pass = [&](auto&& fn) {
+        for (int i0 = 0; i0 < nplan; i0 += 256) {
+            uint2 en[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                en[j] = make_uint2(0u, 0u);
+                if (i0 + 64 * j + lane < nplan) en[j] = plan[i0 + 64 * j + lane];
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) fn(en[j], i0 + 64 * j + lane < nplan);
+        }
+    };
+
     // ------------------------- contested targets: groups, shuffle, losers
     int err = 0;
     int ncont = 0;
     PT_DECL(lp);
     PT_DECL(grp);
     PT_DECL(mts);
+    long long cgp[4] = {0, 0, 0, 0};  // EVX_PROFILE: sort, heads, pass 1, pass 2
     PT_BEGIN(lp);
     uint32_t* Lp = npring;  // the numpy ring is free now
     if (any_cont) {
-        for (int i0 = 0; i0 < nplan; i0 += 64) {
-            const int i = i0 + lane;
+        plan_pass([&](const uint2 en, bool ok) {
             bool c = false;
             uint32_t key = 0;
-            if (i < nplan) {
-                const uint2 en = plan[i];
+            if (ok) {
                 const int t = (int)(en.y & 0xffffffu) + doff_of(en.y >> 24, GY);
                 c = bit_get(cbits, t);
                 key = ((uint32_t)t << pb) | en.x;
@@ -1026,20 +1084,18 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
             const int pos = ncont + lanes_below(m);
             if (c && pos < CL_CAP) Lp[pos] = key;
             ncont += __popcll(m);
-        }
+        });
         PT_END(lp);
         PT_BEGIN(grp);
         if (ncont <= CL_CAP) {
-            contested_groups(Lp, npring + 512, npring + 768, ncont, pb, pyring, py_front, py_head, lost, misc, err);
+            contested_groups(Lp, npring + 512, npring + 768, ncont, pb, pyring, py_front, py_head, lost, misc, err, cgp);
         } else {  // rare: sort in this env's global scratch
             Lp = Lg;
             int k = 0;
-            for (int i0 = 0; i0 < nplan; i0 += 64) {
-                const int i = i0 + lane;
+            plan_pass([&](const uint2 en, bool ok) {
                 bool c = false;
                 uint32_t key = 0;
-                if (i < nplan) {
-                    const uint2 en = plan[i];
+                if (ok) {
                     const int t = (int)(en.y & 0xffffffu) + doff_of(en.y >> 24, GY);
                     c = bit_get(cbits, t);
                     key = ((uint32_t)t << pb) | en.x;
@@ -1047,9 +1103,9 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
                 const unsigned long long m = __ballot(c);
                 if (c) Lg[k + lanes_below(m)] = key;
                 k += __popcll(m);
-            }
+            });
             __syncthreads();
-            contested_groups(Lg, Hg, Sg, ncont, pb, pyring, py_front, py_head, lost, misc, err);
+            contested_groups(Lg, Hg, Sg, ncont, pb, pyring, py_front, py_head, lost, misc, err, cgp);
         }
     }
     PT_END(grp);
@@ -1064,36 +1120,54 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
     PT_STORE(lp, 24);
     PT_STORE(grp, 25);
     PT_STORE(mts, 26);
+#ifdef EVX_PROFILE
+    EVX_COUNT(32, cgp[0]);
+    EVX_COUNT(33, cgp[1]);
+    EVX_COUNT(34, cgp[2]);
+    EVX_COUNT(35, cgp[3]);
+#endif
     EVX_STAMP(3);
 
     // --------------------------------------------- execute_move, in order
-    for (int i0 = 0; i0 < nplan; i0 += 64) {
-        const int i = i0 + lane;
-        if (i < nplan) {
-            const uint2 en = plan[i];
+    plan_pass([&](const uint2 en, bool ok) {
+        if (ok) {
             const int cold = (int)(en.y & 0xffffffu);
             const int t = cold + doff_of(en.y >> 24, GY);
             const bool win = !bit_get(cbits, t) || !bit_get(lost, (int)en.x);
             if (win) atomicOr(&vac[cold >> 5], 1u << (cold & 31));
             if (st.thmap) atomicAdd(&st.thmap[(size_t)e * g.G + (win ? t : cold)], 1);
         }
-    }
+    });
     if (lane == 0) misc[0] = 0;
     __syncthreads();
     uint32_t* ev = aux;  // (cell, key) pairs; groups are done
     int n_evac_new = 0;
-    for (int i0 = 0; i0 < nplan; i0 += 64) {
-        const int i = i0 + lane;
+    for (int i0 = 0; i0 < nplan; i0 += 256) {
+      uint2 en4[4];
+      uint32_t ci4[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+          en4[j] = make_uint2(0u, 0u);
+          if (i0 + 64 * j + lane < nplan) en4[j] = plan[i0 + 64 * j + lane];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j++) {  // exit bits of the targets, all in flight
+          ci4[j] = 0u;
+          if (i0 + 64 * j + lane < nplan) ci4[j] = lay.cellinfo[(int)(en4[j].y & 0xffffffu) + doff_of(en4[j].y >> 24, GY)];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int i = i0 + 64 * j + lane;
         bool exw = false;
         if (i < nplan) {
-            const uint2 en = plan[i];
+            const uint2 en = en4[j];
             const int p = (int)en.x;
             const int cold = (int)(en.y & 0xffffffu);
             const int dd = (int)(en.y >> 24);
             const int t = cold + doff_of((uint32_t)dd, GY);
             const bool cont = bit_get(cbits, t);
             if (!cont || !bit_get(lost, p)) {
-                const bool ex = (lay.cellinfo[t] >> 1) & 1u;
+                const bool ex = (ci4[j] >> 1) & 1u;
                 exw = ex;
                 const bool ev_old = bit_get(tbits, cold), ev_new = bit_get(vac, t);
                 int pf = p;
@@ -1123,6 +1197,7 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
             }
         }
         n_evac_new += __popcll(__ballot(exw));
+      }
     }
     __syncthreads();
     {

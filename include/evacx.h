@@ -87,7 +87,7 @@ typedef struct {
     int32_t *counts;   /* [E*2] evacuated, dead after the step (may be NULL) */
     evx_obs *obs;      /* [E*R] observation after the step */
     int32_t *err;      /* [1] sticky device error word (may be NULL) */
-    int64_t *stamps;   /* [E*32] diagnostic per-phase s_memtime stamps + counters (NULL = off) */
+    int64_t *stamps;   /* [E*48] diagnostic per-phase s_memtime stamps + counters (NULL = off) */
 } evx_step_out;
 
 /* Replaces EvacuationEnv.step / EvacuationEnvMulti.step (envs/evacuation_env.py:122-172,

@@ -40,12 +40,12 @@ for i in range(args.warmup):
     if args.stagger and i < args.stagger:
         m = m | (gid % args.stagger == i)
     env.reset(mask=m)
-stamps = torch.zeros(E * 32, dtype=torch.int64, device="cuda")
+stamps = torch.zeros(E * 48, dtype=torch.int64, device="cuda")
 env.out.stamps = _ptr(stamps)
 for i in range(3):
     env.step(acts[args.warmup + i])
 torch.cuda.synchronize()
-s = stamps.view(E, 32).cpu().numpy()
+s = stamps.view(E, 48).cpu().numpy()
 cols = [c for c, _ in SLOTS]
 d = np.diff(s[:, cols], axis=1)
 tot = s[:, cols[-1]] - s[:, 0]
@@ -70,7 +70,8 @@ PROF = [(16, "rows: np draws+health"), (17, "rows: health sum"), (18, "rows: pla
         (22, "reward: leaves"), (23, "reward: loop top"), (24, "contested: list"), (25, "contested: groups"),
         (26, "contested: mt_store+clear"), (27, "load: mt+rmap+robots"), (28, "load: not-dead list"),
         (29, "load: near map+sync"), (30, "score: floor loads"), (31, "score: mt ensure"),
-        (15, "score: scoring"), (7, "score: tail")]
+        (15, "score: scoring"), (7, "score: tail"), (32, "groups: sort"), (33, "groups: heads+sort"),
+        (34, "groups: pass1 (positions)"), (35, "groups: pass2 (shuffles)")]
 if s[:, 16:30].any():
     print("sub-phase cycle accumulators (EVX_PROFILE build):        median   slowest1%")
     for c, n in PROF:
