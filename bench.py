@@ -6,9 +6,13 @@ layout, 2276 people and 16 robots per env, 4096 envs per GPU (weak scaling;
 env ids global, seeds 1234 + global env id), uniform-init MLP Q-net (bf16 MFMA),
 batch 4096, replay 2^20 transitions per GPU, gradient all-reduce over RCCL when
 world > 1. One timed "step" = one full vectorised training step:
-act (Q forward for E*R robots + epsilon-greedy) -> env.step (all E envs) ->
-replay push (E*R transitions) -> one learn step (sample, online+target forward,
-TD loss, backward, [all-reduce], clip+Adam) || auto-reset (side stream).
+act (Q forward for E*R robots + epsilon-greedy) -> env.step (all E envs, finished
+envs auto-reset inside the launch) -> replay push (E*R transitions) -> one learn
+step (sample, online+target forward, TD loss, backward, [all-reduce], clip+Adam).
+Default schedule "lagged": learn t samples the ring as it stood before push t and
+runs on its own stream concurrently with env.step t (the next act waits for it);
+"strict" keeps the reference's act -> step -> remember -> learn order, and its rate
+on the same state is reported beside the value (strict_schedule_steps_per_s).
 Warmup staggers env ages over one episode length (--stagger), so the timed steps
 see the stationary mix of episode phases a long training run sees.
 
@@ -67,9 +71,16 @@ def parse():
     ap.add_argument("--precision", choices=["bf16", "f32"], default="bf16")
     ap.add_argument("--mode", choices=["train", "env"], default="train")
     ap.add_argument("--env-steps", type=int, default=100, help="extra env-only timed steps (0 = skip)")
+    ap.add_argument("--strict-steps", type=int, default=100,
+                    help="extra timed steps in the strict schedule after a lagged run (0 = skip)")
     ap.add_argument("--cpu-envs", type=int, default=2048)
-    ap.add_argument("--cpu-steps", type=int, default=100)
+    ap.add_argument("--cpu-steps", type=int, default=600)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--schedule", choices=["strict", "lagged"], default="lagged",
+                    help="strict: act, env.step, push, learn (the reference's order); lagged: learn t samples "
+                         "the ring before push t and overlaps env.step t (evacx.trainer.VecTrainer)")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r1", "env_traffic.json"),
+                    help="PMC traffic record of env_step_kernel on this workload (tools/parse_prof.py)")
     return ap.parse_args()
 
 
@@ -94,7 +105,8 @@ def main():
     tables = build_tables(spec)
     lay = DeviceLayout(tables, P)
     hook = make_allreduce_hook(dist, world) if dist is not None else None
-    tr = VecTrainer(lay, E, env_offset=rank * E, precision=args.precision, batch=args.batch, grad_hook=hook)
+    tr = VecTrainer(lay, E, env_offset=rank * E, precision=args.precision, batch=args.batch, grad_hook=hook,
+                    lagged_learn=args.schedule == "lagged")
     env = tr.env
 
     def barrier():
@@ -119,8 +131,9 @@ def main():
         if args.mode == "train":
             tr.step(extra_reset=force)
         else:
-            env.step(torch.randint(0, 5, (E * R,), device="cuda", dtype=torch.int32))
-            env.reset(mask=env.done if force is None else (env.done.bool() | force))
+            env.step(torch.randint(0, 5, (E * R,), device="cuda", dtype=torch.int32), auto_reset=True)
+            if force is not None:
+                env.reset(mask=force & ~env.done.bool())
     if args.mode == "train":
         tr.sync()
     barrier()
@@ -140,10 +153,10 @@ def main():
         if args.mode == "train":
             tr.step(ev_env=ev_env[s], ev_learn=ev_learn[s])
         else:
+            env.compute_order()
             ev_env[s][0].record()
-            env.step(rand_actions[s])
+            env.step(rand_actions[s], order=False, auto_reset=True)  # finished envs reset in the launch
             ev_env[s][1].record()
-            env.reset(mask=env.done)
     if args.mode == "train":
         tr.sync()
     barrier()
@@ -153,6 +166,23 @@ def main():
     learn_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_learn])) if args.mode == "train" else None
     loss = float(tr.last_loss.item()) if tr.last_loss is not None else None
 
+    # ------------------- the reference's strict order on the same state (extra)
+    strict = None
+    if args.mode == "train" and args.schedule == "lagged" and args.strict_steps > 0:
+        tr.sync()
+        tr.lagged = False
+        for _ in range(20):
+            tr.step()
+        tr.sync()
+        barrier()
+        t1 = time.perf_counter()
+        for _ in range(args.strict_steps):
+            tr.step()
+        tr.sync()
+        barrier()
+        strict = E * world * args.strict_steps / max_over_ranks(time.perf_counter() - t1)
+        tr.lagged = True
+
     # --------------------------------------------- env-only rate (extra)
     env_only = None
     if args.env_steps > 0 and args.mode == "train":
@@ -160,8 +190,7 @@ def main():
         barrier()
         t1 = time.perf_counter()
         for s in range(args.env_steps):
-            env.step(acts[s])
-            env.reset(mask=env.done)
+            env.step(acts[s], auto_reset=True)
         barrier()
         env_only = E * world * args.env_steps / max_over_ranks(time.perf_counter() - t1)
 
@@ -169,6 +198,13 @@ def main():
     G = (L + 2) * (W + 2)
     bpe = bytes_per_env_step(P, R, G)
     achieved = bpe * E / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.traffic):
+        # HBM bytes per launch from rocprofv3 PMC passes of this same workload (separate
+        # --pmc FETCH_SIZE / WRITE_SIZE runs; cannot be collected inside the timed run)
+        rec = json.load(open(args.traffic))
+        if rec.get("kernel") == "env_step_kernel":
+            traffic = rec["bytes_per_env_step"] * E
     cpu = cpu_baseline(cpu_snap, env.lay.R, tables, P, args) if cpu_snap is not None else None
     if rank == 0:
         line = {
@@ -192,15 +228,16 @@ def main():
                                 f"{args.batch}) + auto-reset" if args.mode == "train"
                                 else "env.step + auto-reset, uniform random actions")),
                 "envs_per_gpu": E, "grid": f"{L}x{W}", "people": P, "robots": R, "mode": args.mode,
-                "batch": args.batch, "qnet": "MLP 726-512-256-5",
+                "batch": args.batch, "qnet": "MLP 726-512-256-5", "schedule": args.schedule,
                 "parallelism": f"data-parallel over {world} GPU(s): envs sharded, grad all-reduce (RCCL) per learn",
             },
+            "strict_schedule_steps_per_s": strict,
             "env_only_steps_per_s": env_only,
             "env_step_kernel_ms": kern_ms,
             "learn_ms": learn_ms,
             "last_loss": loss,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "env_step_kernel",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "env_step_kernel",
                          "kernel_ms": kern_ms, "bytes_per_env_step": bpe, "env_steps_per_launch": E},
             "cpu_baseline": cpu,
         }

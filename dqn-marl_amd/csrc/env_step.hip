@@ -30,6 +30,7 @@
 // numpy's pairwise mean over streamed leaves, CPython's sequential health sum
 // on lane 0. f64 arithmetic is compiled with -ffp-contract=off (no FMA).
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -536,6 +537,10 @@ __device__ __forceinline__ double readlane_d(double v, int k) {
     const int hi = __builtin_amdgcn_readlane(__double2hiint(v), k);
     return __hiloint2double(hi, lo);
 }
+
+struct ResetLds;
+__device__ __forceinline__ void reset_one(const evx_layout& lay, const evx_state& st, const int e, uint32_t* smem,
+                                          evx_obs* obs, int32_t* err);
 
 __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state st, const int32_t* __restrict__ actions,
                                                       evx_step_out out) {
@@ -1435,11 +1440,21 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
     // ------------------------------------------------- observations
     // People.rmap is only ever set on valid cells, so Check_Valid reduces to the
     // interior range test here (no table reads).
+    // with auto-reset, a finished env's terminal observation goes to obs_term and
+    // the env is reset right here (its wave is light by then: few persons left)
+    const bool fin = __builtin_amdgcn_readfirstlane((int)((evac + dead == P) || (0.5 * (double)(cur_step + 1) >= 600.0)));
+    const bool ar = out.obs_term != nullptr && fin;
+    evx_obs* obs_dst = ar ? out.obs_term : out.obs;
     for (int r = 0; r < R; r++) {
         const uint32_t c = (r == 0) ? view : robots[r];
-        write_obs(g, nullptr, rmapb, rp_x(c), rp_y(c), fs1, out.obs + (size_t)e * R + r);
+        write_obs(g, nullptr, rmapb, rp_x(c), rp_y(c), fs1, obs_dst + (size_t)e * R + r);
     }
     EVX_STAMP(8);
+    if (ar) {
+        __threadfence();  // this wave's state writes complete and visible before the reset reads them
+        __syncthreads();
+        reset_one(lay, st, e, smem, out.obs, out.err);
+    }
     EVX_RSTAMP(10);
 }
 
@@ -1466,11 +1481,9 @@ __host__ __device__ inline ResetLds reset_lds(int G, int P) {
     return s;
 }
 
-__global__ __launch_bounds__(64) void env_reset_kernel(evx_layout lay, evx_state st, const uint8_t* __restrict__ mask,
-                                                       evx_obs* obs, int32_t* err) {
-    const int e = blockIdx.x;
-    if (mask && !mask[e]) return;
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+// Reset of env e by the calling wave; smem: >= reset_lds(G, P).total words.
+__device__ __forceinline__ void reset_one(const evx_layout& lay, const evx_state& st, const int e, uint32_t* smem,
+                                          evx_obs* obs, int32_t* err) {
     const int lane = threadIdx.x;
     Geo g;
     g.L = lay.L; g.W = lay.W; g.GY = lay.W + 2; g.G = (lay.L + 2) * (lay.W + 2);
@@ -1640,6 +1653,14 @@ __global__ __launch_bounds__(64) void env_reset_kernel(evx_layout lay, evx_state
 #endif
 }
 
+__global__ __launch_bounds__(64) void env_reset_kernel(evx_layout lay, evx_state st, const uint8_t* __restrict__ mask,
+                                                       evx_obs* obs, int32_t* err) {
+    const int e = blockIdx.x;
+    if (mask && !mask[e]) return;
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    reset_one(lay, st, e, smem, obs, err);
+}
+
 // ------------------------------------------------------- dispatch order
 // A step's cost grows with the persons still in play, and one env is one wave:
 // the launch ends with its slowest env. Dispatching envs by descending remaining
@@ -1733,6 +1754,12 @@ __global__ __launch_bounds__(256) void obs_expand_kernel(evx_layout lay, const e
 }  // namespace evx
 
 // ===================================================================== C-ABI
+// the step kernel's dynamic LDS also hosts a fused auto-reset
+static size_t step_lds_bytes(const evx_layout& l) {
+    const int G = (l.L + 2) * (l.W + 2);
+    return (size_t)std::max(evx::wave_lds(l.L, l.W, l.P, l.R).total, evx::reset_lds(G, l.P).total) * 4;
+}
+
 namespace {
 thread_local char g_err[512] = "";
 int fail(int code, const char* msg) {
@@ -1760,7 +1787,7 @@ const char* evx_last_error(void) { return g_err; }
 int64_t evx_step_lds_bytes(const evx_layout* l) {
     if (check_layout(l)) return -1;
     const int G = (l->L + 2) * (l->W + 2);
-    return (int64_t)evx::wave_lds(l->L, l->W, l->P, l->R).total * 4;
+    return (int64_t)step_lds_bytes(*l);
 }
 
 int64_t evx_step_scratch_words(const evx_layout* l) {
@@ -1782,7 +1809,7 @@ int evx_env_step(const evx_layout* l, const evx_state* s, const int32_t* actions
         while ((1LL << gb) < (long long)G) gb++;
         if (pb + gb > 32) return fail(-22, "grid cells x people too large for 32-bit move keys");
     }
-    const size_t lds = (size_t)evx::wave_lds(l->L, l->W, l->P, l->R).total * 4;
+    const size_t lds = step_lds_bytes(*l);
     if (lds > 160 * 1024) return fail(-7, "layout needs more than 160 KiB of LDS");
     static bool attr_set = false;
     if (!attr_set) {

@@ -401,7 +401,8 @@ __global__ __launch_bounds__(256) void act_kernel(const float* __restrict__ Q, i
 // Uniform replay ring (DQNAgent.memory, agents/dqn_agent.py:88-99) with compact
 // observations; per-agent transitions share the env's team reward/done.
 __global__ __launch_bounds__(256) void replay_push_kernel(evx_replay rp, const evx_obs* __restrict__ s,
-                                                          const evx_obs* __restrict__ s2, const int32_t* __restrict__ a,
+                                                          const evx_obs* __restrict__ s2,
+                                                          const evx_obs* __restrict__ s2_term, const int32_t* __restrict__ a,
                                                           const double* __restrict__ r_env,
                                                           const uint8_t* __restrict__ done_env, int n, int agents_per_env,
                                                           int64_t pos) {
@@ -410,13 +411,13 @@ __global__ __launch_bounds__(256) void replay_push_kernel(evx_replay rp, const e
     const int64_t slot = (pos + i) % rp.capacity;
     const int e = i / agents_per_env;
     rp.s[slot] = s[i];
-    rp.s2[slot] = s2[i];
+    rp.s2[slot] = (s2_term && done_env[e]) ? s2_term[i] : s2[i];
     rp.a[slot] = a[i];
     rp.r[slot] = (float)r_env[e];
     rp.done[slot] = done_env[e];
 }
 
-__global__ __launch_bounds__(256) void replay_sample_kernel(evx_replay rp, int64_t size, int B, uint64_t seed,
+__global__ __launch_bounds__(256) void replay_sample_kernel(evx_replay rp, int64_t base, int64_t size, int B, uint64_t seed,
                                                             uint64_t offset, evx_obs* __restrict__ s,
                                                             evx_obs* __restrict__ s2, int32_t* __restrict__ a,
                                                             float* __restrict__ r, uint8_t* __restrict__ done,
@@ -426,7 +427,8 @@ __global__ __launch_bounds__(256) void replay_sample_kernel(evx_replay rp, int64
     const uint64_t c = (uint64_t)i + offset;
     const u4 q = philox((uint32_t)c, (uint32_t)(c >> 32), 0x5a3b1eu, 0u, (uint32_t)seed, (uint32_t)(seed >> 32));
     const uint64_t r64 = ((uint64_t)q.x << 32) | q.y;
-    const int64_t j = (int64_t)(r64 % (uint64_t)size);
+    int64_t j = base + (int64_t)(r64 % (uint64_t)size);
+    if (j >= rp.capacity) j -= rp.capacity;
     s[i] = rp.s[j];
     s2[i] = rp.s2[j];
     a[i] = rp.a[j];
@@ -623,18 +625,40 @@ int evx_replay_push(const evx_replay* rp, const evx_obs* s, const evx_obs* s2, c
                     const uint8_t* done_env, int32_t n, int32_t agents_per_env, int64_t pos, void* stream) {
     if (!rp || rp->capacity <= 0) return qfail(-22, "replay: bad ring");
     if (n <= 0) return 0;
-    hipLaunchKernelGGL(evxq::replay_push_kernel, dim3(nblk(n)), dim3(256), 0, (hipStream_t)stream, *rp, s, s2, a,
-                       r_env, done_env, n, agents_per_env, pos);
+    hipLaunchKernelGGL(evxq::replay_push_kernel, dim3(nblk(n)), dim3(256), 0, (hipStream_t)stream, *rp, s, s2,
+                       (const evx_obs*)nullptr, a, r_env, done_env, n, agents_per_env, pos);
     return qlaunch("replay_push");
+}
+
+int evx_replay_push_term(const evx_replay* rp, const evx_obs* s, const evx_obs* s2, const evx_obs* s2_term,
+                         const int32_t* a, const double* r_env, const uint8_t* done_env, int32_t n,
+                         int32_t agents_per_env, int64_t pos, void* stream) {
+    if (!rp || rp->capacity <= 0) return qfail(-22, "replay: bad ring");
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(evxq::replay_push_kernel, dim3(nblk(n)), dim3(256), 0, (hipStream_t)stream, *rp, s, s2, s2_term,
+                       a, r_env, done_env, n, agents_per_env, pos);
+    return qlaunch("replay_push_term");
 }
 
 int evx_replay_sample(const evx_replay* rp, int64_t size, int32_t B, uint64_t seed, uint64_t offset, evx_obs* s,
                       evx_obs* s2, int32_t* a, float* r, uint8_t* done, int64_t* idx_out, void* stream) {
     if (!rp || size <= 0) return qfail(-22, "replay: empty");
     if (B <= 0) return 0;
-    hipLaunchKernelGGL(evxq::replay_sample_kernel, dim3(nblk(B)), dim3(256), 0, (hipStream_t)stream, *rp, size, B,
-                       seed, offset, s, s2, a, r, done, idx_out);
+    if (size > rp->capacity) return qfail(-22, "replay: size > capacity");
+    hipLaunchKernelGGL(evxq::replay_sample_kernel, dim3(nblk(B)), dim3(256), 0, (hipStream_t)stream, *rp, (int64_t)0,
+                       size, B, seed, offset, s, s2, a, r, done, idx_out);
     return qlaunch("replay_sample");
+}
+
+int evx_replay_sample_window(const evx_replay* rp, int64_t base, int64_t count, int32_t B, uint64_t seed,
+                             uint64_t offset, evx_obs* s, evx_obs* s2, int32_t* a, float* r, uint8_t* done,
+                             int64_t* idx_out, void* stream) {
+    if (!rp || count <= 0) return qfail(-22, "replay: empty window");
+    if (count > rp->capacity || base < 0 || base >= rp->capacity) return qfail(-22, "replay: bad window");
+    if (B <= 0) return 0;
+    hipLaunchKernelGGL(evxq::replay_sample_kernel, dim3(nblk(B)), dim3(256), 0, (hipStream_t)stream, *rp, base, count,
+                       B, seed, offset, s, s2, a, r, done, idx_out);
+    return qlaunch("replay_sample_window");
 }
 
 int evx_gather_obs(const evx_obs* src, const int64_t* idx, int32_t n, evx_obs* dst, void* stream) {

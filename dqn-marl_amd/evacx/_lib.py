@@ -35,7 +35,7 @@ class evx_state(C.Structure):
 
 
 class evx_step_out(C.Structure):
-    _fields_ = [(n, C.c_void_p) for n in ["reward", "done", "counts", "obs", "err", "stamps"]]
+    _fields_ = [(n, C.c_void_p) for n in ["reward", "done", "counts", "obs", "err", "stamps", "obs_term"]]
 
 
 _lib = None

@@ -183,6 +183,7 @@ class VecEnv:
                                 rmap=_ptr(self.rmap), thmap=_ptr(self.thmap), robots=_ptr(self.robots),
                                 view=_ptr(self.view), scal=_ptr(self.scal), py_mt=_ptr(self.py_mt),
                                 np_mt=_ptr(self.np_mt), scratch=_ptr(self.scratch), order=_ptr(self.order))
+        self.obs_term: Optional[torch.Tensor] = None
         self.out = _lib.evx_step_out(reward=_ptr(self.reward), done=_ptr(self.done), counts=_ptr(self.counts),
                                      obs=_ptr(self.obs), err=_ptr(self.err))
 
@@ -216,11 +217,24 @@ class VecEnv:
         _lib.check(_lib.lib().evx_env_reset(C.byref(self.lay.c), C.byref(self.c), _ptr(m), _ptr(self.obs),
                                             _ptr(self.err), _stream()), "evx_env_reset")
 
-    def step(self, actions: torch.Tensor):
+    def compute_order(self):
+        """Dispatch order of the next step: heavy env-steps first (scheduling only; the
+        results do not depend on it). Small batches keep the identity order."""
+        if self.E >= 256:
+            _lib.check(_lib.lib().evx_env_order(C.byref(self.lay.c), C.byref(self.c), _stream()), "evx_env_order")
+
+    def step(self, actions: torch.Tensor, order: bool = True, auto_reset: bool = False):
+        """order=False: the caller already ran compute_order() for this state (see
+        evacx.trainer). auto_reset: envs that finish are reset inside the same launch
+        (evx_env_reset semantics); their terminal observations land in self.obs_term
+        and self.obs holds the post-reset ones (self.done still flags them)."""
         a = actions.to(torch.int32).contiguous()
         assert a.numel() == self.E * self.lay.R
-        if self.E >= 256:  # heavy env-steps first (scheduling only)
-            _lib.check(_lib.lib().evx_env_order(C.byref(self.lay.c), C.byref(self.c), _stream()), "evx_env_order")
+        if order:
+            self.compute_order()
+        if auto_reset and self.obs_term is None:
+            self.obs_term = torch.zeros_like(self.obs)
+        self.out.obs_term = self.obs_term.data_ptr() if auto_reset else None
         _lib.check(_lib.lib().evx_env_step(C.byref(self.lay.c), C.byref(self.c), a.data_ptr(), C.byref(self.out),
                                            _stream()), "evx_env_step")
 

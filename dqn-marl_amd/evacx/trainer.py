@@ -7,8 +7,9 @@ One ``step()`` = for all E envs x R robots of this rank:
   push     -- E*R transitions into the replay ring (team reward/done per env)
   learn    -- sample B, online + target forwards, TD loss, backward, optional
               gradient all-reduce (RCCL over xGMI when world > 1), clip + Adam
-  reset    -- auto-reset finished envs (reference reset semantics), on a side
-              stream concurrently with learn
+  reset    -- auto-reset of finished envs (reference reset semantics) fused into
+              the env.step launch; the heavy-first dispatch order of the next
+              env.step (evx_env_order) runs on a side stream
 
 Reference: runners/train_double_dqn.py:43-69 (independent robots, shared team
 reward) generalised to R robots and E envs; DQNAgent.act/remember/learn
@@ -48,14 +49,37 @@ class Replay:
         self.pos = 0
         self.size = 0
 
-    def push(self, s, s2, a, r_env, done_env, n, agents_per_env):
+    def push(self, s, s2, a, r_env, done_env, n, agents_per_env, s2_term=None):
+        """s2_term: terminal observations of auto-reset envs (taken where done_env)."""
         L = _lib.lib()
-        L.evx_replay_push.argtypes = [C.POINTER(evx_replay), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
-                                      C.c_void_p, C.c_int32, C.c_int32, C.c_int64, C.c_void_p]
-        qcheck(L.evx_replay_push(C.byref(self.c), s.data_ptr(), s2.data_ptr(), a.data_ptr(), r_env.data_ptr(),
-                                 done_env.data_ptr(), n, agents_per_env, self.pos, _stream()), "replay_push")
+        if s2_term is None:
+            L.evx_replay_push.argtypes = [C.POINTER(evx_replay), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                          C.c_void_p, C.c_int32, C.c_int32, C.c_int64, C.c_void_p]
+            qcheck(L.evx_replay_push(C.byref(self.c), s.data_ptr(), s2.data_ptr(), a.data_ptr(), r_env.data_ptr(),
+                                     done_env.data_ptr(), n, agents_per_env, self.pos, _stream()), "replay_push")
+        else:
+            L.evx_replay_push_term.argtypes = [C.POINTER(evx_replay)] + [C.c_void_p] * 6 + [C.c_int32, C.c_int32,
+                                                                                          C.c_int64, C.c_void_p]
+            qcheck(L.evx_replay_push_term(C.byref(self.c), s.data_ptr(), s2.data_ptr(), s2_term.data_ptr(),
+                                          a.data_ptr(), r_env.data_ptr(), done_env.data_ptr(), n, agents_per_env,
+                                          self.pos, _stream()), "replay_push_term")
         self.pos = (self.pos + n) % self.capacity
         self.size = min(self.capacity, self.size + n)
+
+    def window(self, n_next):
+        """(base, count): the entries already in the ring that a push of n_next
+        transitions does not overwrite -- the newest min(size, capacity - n_next)."""
+        count = min(self.size, self.capacity - n_next)
+        return (self.pos - count) % self.capacity, count
+
+    def sample_window(self, base, count, B, seed, offset, out):
+        L = _lib.lib()
+        L.evx_replay_sample_window.argtypes = [C.POINTER(evx_replay), C.c_int64, C.c_int64, C.c_int32, C.c_uint64,
+                                               C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                               C.c_void_p, C.c_void_p, C.c_void_p]
+        qcheck(L.evx_replay_sample_window(C.byref(self.c), base, count, B, seed, offset, out["s"].data_ptr(),
+                                          out["s2"].data_ptr(), out["a"].data_ptr(), out["r"].data_ptr(),
+                                          out["done"].data_ptr(), None, _stream()), "replay_sample_window")
 
     def sample(self, B, seed, offset, out):
         L = _lib.lib()
@@ -72,12 +96,13 @@ class VecTrainer:
                  kind: str = "mlp", precision: str = "bf16", batch: int = 4096, replay_capacity: int = 1 << 20,
                  lr: float = 1e-4, gamma: float = 0.99, epsilon: float = 1.0, epsilon_min: float = 0.02,
                  epsilon_decay: float = 0.9995, target_every: int = 1000, learner_seed: int = 0,
-                 grad_hook=None, learn_every: int = 1):
+                 grad_hook=None, learn_every: int = 1, lagged_learn: bool = False):
         self.lay, self.E, self.R = layout, E, layout.R
         self.device = layout.device
         self.env = VecEnv(layout, E)
         self.env.seed([seed_base + env_offset + i for i in range(E)])
         self.env.reset()
+        self.env.compute_order()
         self.learner = Learner(kind=kind, device=self.device, lr=lr, gamma=gamma, precision=precision,
                                seed=learner_seed)
         self.learner.grad_hook = grad_hook
@@ -85,6 +110,9 @@ class VecTrainer:
         self.batch = batch
         self.epsilon, self.epsilon_min, self.epsilon_decay = epsilon, epsilon_min, epsilon_decay
         self.target_every, self.learn_every = target_every, learn_every
+        # lagged_learn: learn step t samples the transitions pushed up to step t-1 and runs
+        # on its own stream concurrently with env.step t (see step())
+        self.lagged = lagged_learn
         n = E * self.R
         self.n_agents = n
         self.obs_prev = torch.zeros(n * OBS_WORDS, dtype=torch.int32, device=self.device)
@@ -101,6 +129,12 @@ class VecTrainer:
         self.ev_push = torch.cuda.Event()
         self.ev_reset = torch.cuda.Event()
         self.ev_reset.record(torch.cuda.current_stream(self.device))
+        self.lstream = torch.cuda.Stream(device=self.device)
+        self.ev_act = torch.cuda.Event()
+        self.ev_learned = torch.cuda.Event()
+        self.ev_learned.record(torch.cuda.current_stream(self.device))
+        self.ev_order = torch.cuda.Event()
+        self.ev_order.record(torch.cuda.current_stream(self.device))
         self.last_loss: Optional[torch.Tensor] = None
         # bf16 MLP: act and learn straight from compact observations (csrc/qmlp.hip)
         self.fast = self.learner.fast
@@ -121,10 +155,15 @@ class VecTrainer:
                               self.t * self.n_agents, self.actions.data_ptr(), _stream()), "act")
         return self.actions
 
-    def learn(self):
-        if self.replay.size < self.batch:
+    def learn(self, window=None):
+        """window: (base, count) of the replay ring to sample from (default: all of it)."""
+        if (self.replay.size if window is None else window[1]) < self.batch:
             return None
-        self.replay.sample(self.batch, self.seed + 1, self.learn_steps * self.batch, self.samp)
+        if window is None:
+            self.replay.sample(self.batch, self.seed + 1, self.learn_steps * self.batch, self.samp)
+        else:
+            self.replay.sample_window(window[0], window[1], self.batch, self.seed + 1, self.learn_steps * self.batch,
+                                      self.samp)
         if self.fast is not None:
             loss = self.learner.learn_obs(self.lay.c, self.samp["s"], self.samp["a"], self.samp["r"],
                                           self.samp["done"], self.samp["s2"], self.batch)
@@ -140,38 +179,66 @@ class VecTrainer:
         return loss
 
     def step(self, extra_reset: Optional[torch.Tensor] = None, ev_env=None, ev_learn=None):
-        """One training step. The auto-reset of finished envs runs on a side stream
-        concurrently with learn (it needs only the pushed env state; the next act
-        waits for it). extra_reset: bool [E] of further envs to reset (benchmark
-        staggering); ev_env / ev_learn: optional (start, end) CUDA events."""
+        """One training step. Finished envs are reset inside the env.step launch
+        (auto-reset: the reset of an env that ends runs in its own wave, in the shadow
+        of the launch's heavy envs); the replay push takes their terminal observations.
+        The heavy-first dispatch order of the next env.step is computed on a side
+        stream, concurrently with push / learn / act. extra_reset: bool [E] of further
+        envs to reset (benchmark staggering, side stream); ev_env / ev_learn: optional
+        (start, end) CUDA events.
+
+        Default order is the reference's (act, env.step, remember, learn). With
+        lagged_learn the learn step is issued right after act on its own stream: it
+        samples the ring as it was before this step's push (minus the slots the push
+        overwrites), so it overlaps env.step; the next act waits for it."""
         main = torch.cuda.current_stream(self.device)
         main.wait_event(self.ev_reset)
+        if self.lagged:
+            main.wait_event(self.ev_learned)
         self.act()
+        if self.lagged:
+            self.ev_act.record(main)  # learn's optimizer rewrites the weights act has read
+            win = self.replay.window(self.n_agents)
+            with torch.cuda.stream(self.lstream):
+                self.lstream.wait_event(self.ev_act)
+                if ev_learn is not None:
+                    ev_learn[0].record(self.lstream)
+                if self.t % self.learn_every == 0:
+                    self.last_loss = self.learn(window=win)
+                if ev_learn is not None:
+                    ev_learn[1].record(self.lstream)
+                self.ev_learned.record(self.lstream)
         self.obs_prev.copy_(self.env.obs)
+        main.wait_event(self.ev_order)
         if ev_env is not None:
             ev_env[0].record(main)
-        self.env.step(self.actions)
+        self.env.step(self.actions, order=False, auto_reset=True)
         if ev_env is not None:
             ev_env[1].record(main)
         self.replay.push(self.obs_prev, self.env.obs, self.actions, self.env.reward, self.env.done,
-                         self.n_agents, self.R)
+                         self.n_agents, self.R, s2_term=self.env.obs_term)
         self.ev_push.record(main)
         with torch.cuda.stream(self.side):
             self.side.wait_event(self.ev_push)
-            mask = self.env.done if extra_reset is None else (self.env.done.bool() | extra_reset)
-            self.env.reset(mask=mask)
+            if extra_reset is not None:
+                self.env.reset(mask=extra_reset & ~self.env.done.bool())
             self.ev_reset.record(self.side)
-        if ev_learn is not None:
-            ev_learn[0].record(main)
-        if self.t % self.learn_every == 0:
-            self.last_loss = self.learn()
-        if ev_learn is not None:
-            ev_learn[1].record(main)
+            self.env.compute_order()
+            self.ev_order.record(self.side)
+        if not self.lagged:
+            if ev_learn is not None:
+                ev_learn[0].record(main)
+            if self.t % self.learn_every == 0:
+                self.last_loss = self.learn()
+            if ev_learn is not None:
+                ev_learn[1].record(main)
         self.t += 1
 
     def sync(self):
-        """Make the current stream wait for the side-stream reset of the last step."""
-        torch.cuda.current_stream(self.device).wait_event(self.ev_reset)
+        """Make the current stream wait for the side-stream work of the last step."""
+        cur = torch.cuda.current_stream(self.device)
+        cur.wait_event(self.ev_reset)
+        cur.wait_event(self.ev_learned)
 
 
 def make_allreduce_hook(dist, world: int):

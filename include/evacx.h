@@ -88,6 +88,10 @@ typedef struct {
     evx_obs *obs;      /* [E*R] observation after the step */
     int32_t *err;      /* [1] sticky device error word (may be NULL) */
     int64_t *stamps;   /* [E*48] diagnostic per-phase s_memtime stamps + counters (NULL = off) */
+    /* Auto-reset (NULL = off, the reference's separate env.reset): envs that finish this
+     * step are reset in the same launch (evx_env_reset semantics); their terminal
+     * observations go to obs_term [E*R] and obs receives the post-reset ones. */
+    evx_obs *obs_term;
 } evx_step_out;
 
 /* Replaces EvacuationEnv.step / EvacuationEnvMulti.step (envs/evacuation_env.py:122-172,
@@ -183,8 +187,19 @@ int evx_replay_push(const evx_replay *rp, const evx_obs *s, const evx_obs *s2, c
                     const double *r_env, const uint8_t *done_env, int32_t n, int32_t agents_per_env, int64_t pos,
                     void *stream);
 /* random.sample replacement for the vectorised learner: B uniform indices < size */
+/* evx_replay_push with s2 = done_env[e] ? s2_term : s2 (the terminal observations of
+ * envs that evx_env_step auto-reset) */
+int evx_replay_push_term(const evx_replay *rp, const evx_obs *s, const evx_obs *s2, const evx_obs *s2_term,
+                         const int32_t *a, const double *r_env, const uint8_t *done_env, int32_t n,
+                         int32_t agents_per_env, int64_t pos, void *stream);
 int evx_replay_sample(const evx_replay *rp, int64_t size, int32_t B, uint64_t seed, uint64_t offset, evx_obs *s,
                       evx_obs *s2, int32_t *a, float *r, uint8_t *done, int64_t *idx_out, void *stream);
+/* B uniform indices over the ring window [base, base+count) mod capacity (same draws as
+ * evx_replay_sample with base 0): lets a learn step sample the transitions already pushed
+ * while the next push overwrites the slots outside the window (lagged-replay schedule) */
+int evx_replay_sample_window(const evx_replay *rp, int64_t base, int64_t count, int32_t B, uint64_t seed,
+                             uint64_t offset, evx_obs *s, evx_obs *s2, int32_t *a, float *r, uint8_t *done,
+                             int64_t *idx_out, void *stream);
 int evx_gather_obs(const evx_obs *src, const int64_t *idx, int32_t n, evx_obs *dst, void *stream);
 /* DQNNetwork conv layers (agents/dqn_agent.py:22-24) as im2col + GEMM on 11x11 maps */
 int evx_im2col3x3(const float *x, int32_t B, int32_t C, int32_t nhwc, float *cols, void *stream);

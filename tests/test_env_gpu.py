@@ -75,8 +75,10 @@ def test_gpu_replays_reference_trajectory(traj):
     assert np.array_equal(py[0], tr["rng_py_final"]) and np.array_equal(nps[0], tr["rng_np_final"])
 
 
-def _oracle_pair(spec, P, E, steps, seed0=1234, act_seed=7, thmap=True, check_every=1):
-    """Run E envs on the GPU and in the oracle with identical seeds/actions."""
+def _oracle_pair(spec, P, E, steps, seed0=1234, act_seed=7, thmap=True, check_every=1, auto_reset=False):
+    """Run E envs on the GPU and in the oracle with identical seeds/actions.
+    auto_reset: finished envs are reset inside the step launch (VecEnv.step
+    auto_reset); their terminal observations are checked from env.obs_term."""
     from evacx.env import DeviceLayout, VecEnv
     from evacx.layout import build_tables
     from oracle import oracle as orc
@@ -97,7 +99,7 @@ def _oracle_pair(spec, P, E, steps, seed0=1234, act_seed=7, thmap=True, check_ev
         if s > 0:
             acts = rng.randint(0, 5, size=(E, R)).astype(np.int32)
             acts[rng.rand(E, R) < 0.02] = 7  # invalid actions are ignored by the reference
-            env.step(torch.from_numpy(acts.reshape(-1)).cuda())
+            env.step(torch.from_numpy(acts.reshape(-1)).cuda(), auto_reset=auto_reset)
             res = [oe.step(acts[i]) for i, oe in enumerate(oenvs)]
             oobs = [r[0] for r in res]
             rew = env.reward.cpu().numpy()
@@ -105,6 +107,12 @@ def _oracle_pair(spec, P, E, steps, seed0=1234, act_seed=7, thmap=True, check_ev
             for i in range(E):
                 assert rew[i] == res[i][1], (s, i, rew[i], res[i][1])
                 assert done[i] == res[i][2], (s, i)
+            if auto_reset and done.any():
+                term = env.expand_obs(torch.float64, env.obs_term).cpu().numpy()
+                for i in np.nonzero(done)[0]:
+                    assert np.array_equal(term[i], oobs[i]), (s, i, "terminal obs")
+                    oobs[i] = oenvs[i].reset()
+                    n_resets += 1
         if s % check_every == 0 or s == steps:
             obs64 = env.expand_obs(torch.float64).cpu().numpy()
             obs32 = env.expand_obs(torch.float32).cpu().numpy()
@@ -120,7 +128,7 @@ def _oracle_pair(spec, P, E, steps, seed0=1234, act_seed=7, thmap=True, check_ev
                 assert np.array_equal(st["np_mt"], ost["np_mt"]), (s, i, "np_mt")
                 assert np.array_equal(obs64[i], oobs[i]), (s, i, "obs")
                 assert np.array_equal(obs32[i], oobs[i].astype(np.float32)), (s, i, "obs32")
-        if s > 0:
+        if s > 0 and not auto_reset:
             d = env.done.clone()
             if d.any():
                 n_resets += int(d.sum())
@@ -136,6 +144,21 @@ def test_gpu_vs_oracle_cfg1_many_envs_with_resets():
     from evacx.layout import reference_single
     n = _oracle_pair(reference_single(), 150, E=48, steps=260, check_every=13)
     assert n > 48  # every env went through several episodes (fire saturated)
+
+
+def test_gpu_auto_reset_vs_oracle_cfg1():
+    """Resets fused into the step launch: same states, observations and streams."""
+    _need_gpu()
+    from evacx.layout import reference_single
+    n = _oracle_pair(reference_single(), 150, E=48, steps=260, check_every=13, auto_reset=True)
+    assert n > 48
+
+
+def test_gpu_auto_reset_vs_oracle_dense():
+    _need_gpu()
+    from evacx.layout import synthetic
+    n = _oracle_pair(synthetic(24, 20, 4), 380, E=16, steps=120, check_every=3, auto_reset=True)
+    assert n > 0
 
 
 def test_gpu_vs_oracle_multi_cfg1():
