@@ -31,6 +31,7 @@
 // on lane 0. f64 arithmetic is compiled with -ffp-contract=off (no FMA).
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <stdlib.h>
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -139,6 +140,13 @@ __device__ __forceinline__ void write_obs(const Geo& g, const uint32_t* validb, 
 // Ordering inside one wave: LDS instructions of a wave execute in issue order,
 // so lane-to-lane LDS hand-offs only need the compiler not to reorder them.
 __device__ __forceinline__ void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront"); }
+// A wave's own memory traffic complete (every lane sees every lane's LDS and global
+// writes); no s_barrier: the waves of a workgroup may run different envs.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
 
 __device__ __forceinline__ int lanes_below(unsigned long long m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -147,7 +155,7 @@ __device__ __forceinline__ int lanes_below(unsigned long long m) {
 // Extend the raw MT sequence in a WR-word ring until front >= upto. A batch of
 // up to 227 words depends only on older words (x[n-227], x[n-624], x[n-623]).
 __device__ __forceinline__ void mt_ensure_w(uint32_t* ring, int& front, int upto) {
-    const int lane = threadIdx.x;
+    const int lane = (int)(threadIdx.x & 63);
     while (front < upto) {
         const int cnt = min(MT_LAG, upto - front);
         uint32_t lag[4], a[4], b[4];  // every operand of the round is read before any word is written
@@ -171,7 +179,7 @@ __device__ __forceinline__ void mt_ensure_w(uint32_t* ring, int& front, int upto
 // Store the state after consuming up to raw index `head` (CPython index
 // semantics). Needs front <= head + 400 so [b, b+624) is still in the ring.
 __device__ __forceinline__ void mt_store_w(uint32_t* ring, int& front, int head, uint32_t* gst) {
-    const int lane = threadIdx.x;
+    const int lane = (int)(threadIdx.x & 63);
     if (head <= MT_N) {
         if (lane == 0) gst[MT_N] = (uint32_t)head;  // no twist: words unchanged
         return;
@@ -185,7 +193,7 @@ __device__ __forceinline__ void mt_store_w(uint32_t* ring, int& front, int head,
 // Ascending bitonic sort of a[0..n), n a power of two, by one wave.
 template <typename T>
 __device__ __forceinline__ void wave_sort(T* a, int n) {
-    const int lane = threadIdx.x;
+    const int lane = (int)(threadIdx.x & 63);
     for (int k = 2; k <= n; k <<= 1)
         for (int j = k >> 1; j > 0; j >>= 1) {
             for (int q = lane; q < (n >> 1); q += 64) {
@@ -197,7 +205,7 @@ __device__ __forceinline__ void wave_sort(T* a, int n) {
                     a[l] = x;
                 }
             }
-            __syncthreads();  // one wave: waits for its own LDS / memory traffic
+            wave_sync();  // one wave: waits for its own LDS / memory traffic
         }
 }
 
@@ -206,15 +214,15 @@ __device__ __forceinline__ void wave_sort(T* a, int n) {
 // padded array (the caller pads with 0xffffffff).
 template <typename T>
 __device__ __forceinline__ void wave_sort_keys(T* a, int n, int n2) {
-    const int lane = threadIdx.x;
+    const int lane = (int)(threadIdx.x & 63);
     if (n <= 64) {
         uint32_t k = 0xffffffffu;
         if (lane < n) k = a[lane];
         int rank = 0;
         for (int j = 0; j < n; j++) rank += (uint32_t)__builtin_amdgcn_readlane((int)k, j) < k;
-        __syncthreads();
+        wave_sync();
         if (lane < n) a[rank] = k;
-        __syncthreads();
+        wave_sync();
     } else {
         wave_sort(a, n2);
     }
@@ -237,7 +245,7 @@ __device__ __forceinline__ int doff_of(uint32_t d, int GY) { return move_dx((int
 template <typename T>
 __device__ __forceinline__ void contested_groups(T* Lp, T* heads, T* gstart, int n, int pb, uint32_t* pyring, int& py_front,
                                  int& py_head, uint32_t* lost, uint32_t* grp, int& err, long long* prof) {
-    const int lane = threadIdx.x;
+    const int lane = (int)(threadIdx.x & 63);
 #ifdef EVX_PROFILE
     long long tq = __builtin_amdgcn_s_memtime();
 #define CG_T(i)                                          \
@@ -252,7 +260,7 @@ __device__ __forceinline__ void contested_groups(T* Lp, T* heads, T* gstart, int
     const uint32_t pmask = (1u << pb) - 1u;
     const int n2 = pow2_ceil(n);
     for (int i = n + lane; i < n2; i += 64) Lp[i] = 0xffffffffu;
-    __syncthreads();
+    wave_sync();
     wave_sort_keys(Lp, n, n2);
     CG_T(0);
     int ngrp = 0;
@@ -275,7 +283,7 @@ __device__ __forceinline__ void contested_groups(T* Lp, T* heads, T* gstart, int
     if (lane == 0) gstart[ngrp] = (uint32_t)n;
     const int h2 = pow2_ceil(ngrp);
     for (int i = ngrp + lane; i < h2; i += 64) heads[i] = 0xffffffffu;
-    __syncthreads();
+    wave_sync();
     wave_sort_keys(heads, ngrp, h2);
     CG_T(1);
     // group descriptors in dict order: (first mover's position in Lp << 8) | size
@@ -286,7 +294,7 @@ __device__ __forceinline__ void contested_groups(T* Lp, T* heads, T* gstart, int
         if (cnt > GRP_MAX) err |= 1;  // > 128 movers on one target: not representable, flagged
     }
     err = __ballot(err != 0) ? (err | 1) : err;
-    __syncthreads();
+    wave_sync();
     // Pass 1 (wave-uniform): where each group's random.shuffle starts on the Python
     // stream. _randbelow(b) accepts a word iff its top bit_length(b) bits are < b;
     // per 64-word window the acceptance sets of b = 2..8 are ballots (lane b of
@@ -378,7 +386,7 @@ __device__ __forceinline__ void contested_groups(T* Lp, T* heads, T* gstart, int
             k++;
         }
         CG_T(2);
-        __syncthreads();  // ring words [W0, pos) are in place
+        wave_sync();  // ring words [W0, pos) are in place
         // Pass 2: lane j shuffles group k0 + j (Lib/random.py shuffle, in registers)
         if (lane < nk) {
             const int s0 = (int)(desc >> 8), cnt = (int)(desc & 255u);
@@ -437,7 +445,7 @@ __device__ __forceinline__ void contested_groups(T* Lp, T* heads, T* gstart, int
                 for (int q = 1; q < cnt; q++) lost[grp[q] >> 5] |= 1u << (grp[q] & 31);
             }
         }
-        __syncthreads();
+        wave_sync();
         CG_T(3);
     }
     py_head = pos;
@@ -487,11 +495,13 @@ __host__ __device__ inline WaveLds wave_lds(int L, int W, int P, int R) {
 }
 
 // per env: move plan [P] uint2 | not-dead list [P] uint2 | spill: contested list,
-// group heads, group starts (each a power of two >= P)
-__host__ __device__ inline int64_t wave_scratch_words(int P) {
+// group heads, group starts (each a power of two >= P) | healths [P] double
+__host__ __device__ inline int64_t wave_hv_offset(int P) {
     const int n2 = pow2_ceil(P < 64 ? 64 : P);
     return ((int64_t)4 * P + 3 * (int64_t)n2 + 2 + 1) & ~(int64_t)1;
 }
+// ... | health of every not-dead person after update_health, list order (wide rows)
+__host__ __device__ inline int64_t wave_scratch_words(int P) { return wave_hv_offset(P) + 2 * (int64_t)P; }
 
 __device__ __forceinline__ int pb_bits(int P) { return P > 1 ? bit_length((uint32_t)(P - 1)) : 1; }
 
@@ -499,17 +509,17 @@ __device__ __forceinline__ int pb_bits(int P) { return P > 1 ? bit_length((uint3
 // clock, 9/10 constant-rate clock at start/end, 11-14 counters.
 #define EVX_STAMP(i)                                                                                   \
     do {                                                                                               \
-        if (out.stamps && threadIdx.x == 0)                                                            \
+        if (out.stamps && (threadIdx.x & 63) == 0)                                                            \
             out.stamps[(size_t)e * 48 + (i)] = (int64_t)__builtin_amdgcn_s_memtime();         \
     } while (0)
 #define EVX_RSTAMP(i)                                                                                  \
     do {                                                                                               \
-        if (out.stamps && threadIdx.x == 0)                                                            \
+        if (out.stamps && (threadIdx.x & 63) == 0)                                                            \
             out.stamps[(size_t)e * 48 + (i)] = (int64_t)__builtin_amdgcn_s_memrealtime();     \
     } while (0)
 #define EVX_COUNT(i, v)                                                                                \
     do {                                                                                               \
-        if (out.stamps && threadIdx.x == 0) out.stamps[(size_t)e * 48 + (i)] = (v);           \
+        if (out.stamps && (threadIdx.x & 63) == 0) out.stamps[(size_t)e * 48 + (i)] = (v);           \
     } while (0)
 
 // EVX_PROFILE builds only: cycle accumulators of sub-phases, stored to slots 16..31
@@ -538,15 +548,533 @@ __device__ __forceinline__ double readlane_d(double v, int k) {
     return __hiloint2double(hi, lo);
 }
 
-struct ResetLds;
 __device__ __forceinline__ void reset_one(const evx_layout& lay, const evx_state& st, const int e, uint32_t* smem,
                                           evx_obs* obs, int32_t* err);
 
-__global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state st, const int32_t* __restrict__ actions,
-                                                      evx_step_out out) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    const int e = st.order ? st.order[blockIdx.x] : (int)blockIdx.x;  // heavy envs first (evx_env_order)
-    const int lane = threadIdx.x;
+struct ResetLds {
+    int pyring, validb, rmapb, total;
+};
+__host__ __device__ inline ResetLds reset_lds(int G, int P) {
+    ResetLds s;
+    const int RW = (G + 31) / 32;
+    int o = 0;
+    s.pyring = o; o += WR;
+    s.validb = o; o += RW;
+    s.rmapb = o; o += RW;
+    s.total = (o + 3) & ~3;
+    return s;
+}
+
+// dynamic LDS words of one env's wave: the step's layout, which also hosts a fused reset
+__host__ __device__ inline int step_lds_words(const evx_layout& l) {
+    const int G = (l.L + 2) * (l.W + 2);
+    const int a = wave_lds(l.L, l.W, l.P, l.R).total, b = reset_lds(G, l.P).total;
+    return ((a > b ? a : b) + 3) & ~3;
+}
+
+// People.find_best_direction (envs/people.py:232-262) for one planner per lane, split
+// in two: dir_prep gathers the operands (floor deltas, robot distances), dir_score
+// consumes the planner's Python-stream words (uniform(-0.1, 0.1) per candidate, in
+// direction order) from ring[(idx - base) & mask].
+struct DirPrep {
+    double f[8];     // (floor[c] - floor[c + MoveTO[d]]) * 5.0
+    int md2[8];      // squared distance to the nearest robot (only where nearm)
+    uint32_t nearm;  // candidates inside a near-robot block
+};
+__device__ __forceinline__ void dir_prep(DirPrep& d, bool has, int x, int y, uint32_t cand, int GY,
+                                         const double* __restrict__ fd5, const uint32_t* nearc, int BY,
+                                         const uint32_t* robots, int R, int rb) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) d.f[k] = 0.0;
+    if (has) {
+        const double2* fr = reinterpret_cast<const double2*>(fd5 + (size_t)(x * GY + y) * 8);
+#pragma unroll
+        for (int q2 = 0; q2 < 4; q2++) {
+            const double2 v = fr[q2];
+            d.f[2 * q2] = v.x;
+            d.f[2 * q2 + 1] = v.y;
+        }
+    }
+    // squared distance to the nearest robot for the 8 neighbours, only when some
+    // candidate lies in a near-robot block (robots outer: 4 per LDS read)
+    uint32_t nearm = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const int nx = x + move_dx(k), ny = y + move_dy(k);
+        if (((cand >> k) & 1u) && bit_get(nearc, (nx >> 2) * BY + (ny >> 2))) nearm |= 1u << k;
+    }
+    d.nearm = nearm;
+#pragma unroll
+    for (int k = 0; k < 8; k++) d.md2[k] = 0x7fffffff;
+    if (__ballot(nearm != 0)) {
+        const uint4* r4 = reinterpret_cast<const uint4*>(robots);
+        for (int r0 = 0; r0 < R; r0 += 4) {
+            const uint4 q4 = r4[r0 >> 2];
+            const uint32_t rq[4] = {q4.x, q4.y, q4.z, q4.w};
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int rx = rp_x(rq[j]), ry = rp_y(rq[j]);
+                // robots no lane is near cannot be the nearest within range: skipped
+                if (r0 + j < R && __ballot(abs(x - rx) <= rb && abs(y - ry) <= rb)) {
+#pragma unroll
+                    for (int k = 0; k < 8; k++) {
+                        const int dx = x + move_dx(k) - rx, dy = y + move_dy(k) - ry;
+                        d.md2[k] = min(d.md2[k], dx * dx + dy * dy);
+                    }
+                }
+            }
+        }
+    }
+}
+__device__ __forceinline__ uint32_t dir_score(const DirPrep& d, uint32_t cand, int idx, const uint32_t* ring, int base,
+                                              int mask, double repel_k, int rd2) {
+    double maxs = -INFINITY;
+    uint32_t best = NODIR;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        if ((cand >> k) & 1u) {
+            double effect = 0.0;
+            if (((d.nearm >> k) & 1u) && d.md2[k] < rd2) effect = repel_k / (sqrt((double)d.md2[k]) + 0.1);
+            const double u = -0.1 + (0.1 - -0.1) * mt_double(ring, mask, idx - base);
+            idx += 2;
+            const double score = d.f[k] + effect + u;  // delta_p * 5.0 + robot_effect + uniform
+            if (score > maxs) {
+                maxs = score;
+                best = (uint32_t)k;
+            }
+        }
+    }
+    return best;
+}
+
+// ============================================ wide rows: one heavy env, WNW waves
+// An env-step early in an episode has thousands of persons in play, and one wave
+// per env makes the launch wait for the heaviest. For the heaviest envs (listed
+// first by evx_env_order) the rows phase (update_health, accumulate, planning,
+// find_best_direction) runs on all WNW waves of a workgroup: the not-dead list is
+// dealt out in 64-person groups round-robin (group g to wave g % WNW), each
+// group's numpy / Python stream offsets follow from per-group counts (the reference
+// consumes both streams in person order), the MT19937 words are generated
+// cooperatively (227 per round, one block barrier per round) into a linear LDS
+// buffer, and the planners are scored in word windows that every wave shares in.
+// Wave 0 then carries on alone (contested targets, execute, reward), while wave 1
+// folds the health total (CPython's sequential sum) in parallel.
+constexpr int WNW = 4;
+struct WideCtl {
+    int nnd, np_head, py_head, fs;  // in: published by wave 0
+    int ndc[WNW];                   // deaths per wave
+    int any_cont, nplan, n_died, py_front, py_head_out, pad0;
+    double total;  // health total (wave 1)
+    int total_ready, pad1;
+};
+// Workgroup LDS (WNW waves): WNW env regions of step_lds_words, then WideCtl. A heavy
+// env keeps wave 0's region; the rows buffers overlay regions 1.. (dead once the
+// rows are done, when waves 1.. go on with other envs).
+struct WideLds {
+    int ctl, grp, NGmax, lin, LINW, lists, CHmax, end, total;
+};
+__host__ __device__ inline WideLds wide_lds(const evx_layout& l) {
+    WideLds s;
+    const int LW = step_lds_words(l);
+    s.ctl = WNW * LW;
+    s.total = s.ctl + 32;
+    s.NGmax = (l.P + 63) / 64;
+    s.grp = LW;                 // per group: numpy words | Python words | movers | Python offset
+    s.lin = s.grp + ((4 * s.NGmax + 3) & ~3);
+    s.LINW = ((2 * l.P + 1280) + 3) & ~3;  // numpy words of the step + MT history + slack
+    s.lists = s.lin + s.LINW;
+    s.CHmax = ((s.NGmax + WNW - 1) / WNW) * 64;  // planners per wave
+    s.end = s.lists + WNW * s.CHmax * 3;          // must be <= ctl
+    return s;
+}
+
+// Extend the raw MT sequence held linearly (word n at lin[n - base]) to upto; all
+// WNW waves, uniform arguments, one block barrier per 227-word round.
+__device__ __forceinline__ void coop_gen(uint32_t* lin, int base, int& front, int upto) {
+    const int tid = (int)threadIdx.x;
+    while (front < upto) {
+        const int cnt = min(MT_LAG, upto - front);
+        for (int j = tid; j < cnt; j += 64 * WNW) {
+            const int n = front + j - base;
+            lin[n] = mt_twist1(lin[n - MT_LAG], lin[n - MT_N], lin[n - MT_N + 1]);
+        }
+        front += cnt;
+        __syncthreads();
+    }
+}
+
+// sum of cnt[0..g) (wave-uniform g)
+__device__ __forceinline__ int group_prefix(const int* cnt, int g) {
+    int acc = 0;
+    for (int i = (int)(threadIdx.x & 63); i < g; i += 64) acc += cnt[i];
+    return wave_sum(acc);
+}
+
+// People.run phases 1+2 of env e on all WNW waves (wave 0 has published WideCtl and
+// its LDS tables: rmap snapshot, near map, robots, zeroed target bitmaps, the two MT
+// states at ring positions [0, 624)). Outputs in WideCtl; the plan list and person
+// writes in HBM; the numpy state stored; the Python stream handed back to wave 0's
+// ring.
+__device__ __forceinline__ void rows_wide(const evx_layout& lay, const evx_state& st, const int e, uint32_t* smem,
+                                          int64_t* prof = nullptr) {
+    const int tid = (int)threadIdx.x, lane = tid & 63, w = tid >> 6;
+#ifdef EVX_PROFILE
+    long long wt = __builtin_amdgcn_s_memtime(), wacc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#define WT(i)                                              \
+    do {                                                   \
+        const long long t2 = __builtin_amdgcn_s_memtime(); \
+        wacc[i] += t2 - wt;                                \
+        wt = t2;                                           \
+    } while (0)
+#else
+#define WT(i)
+#endif
+    const int P = lay.P, R = lay.R, GY = lay.W + 2, G = (lay.L + 2) * (lay.W + 2);
+    const WaveLds S = wave_lds(lay.L, lay.W, P, R);
+    const WideLds WL = wide_lds(lay);
+    WideCtl* ctl = reinterpret_cast<WideCtl*>(smem + WL.ctl);
+    int* npg = reinterpret_cast<int*>(smem + WL.grp);  // numpy words per group
+    int* pyg = npg + WL.NGmax;                          // Python words per group
+    int* mvg = pyg + WL.NGmax;                          // movers per group
+    int* pyo = mvg + WL.NGmax;                          // first Python word per group (owner wave only)
+    uint32_t* lin = smem + WL.lin;
+    // this wave's planners: (person | cand << 16 | best << 24, x | y << 12 | group << 24, first word)
+    uint32_t* myl = smem + WL.lists + w * WL.CHmax * 3;
+    const uint32_t* rmapb = smem + S.rmapb;
+    uint32_t* tbits = smem + S.tbits;
+    uint32_t* cbits = smem + S.cbits;
+    const uint32_t* nearc = smem + S.nearc;
+    const uint32_t* robots = smem + S.robots;
+    uint32_t* pyring = smem + S.pyring;
+    const uint32_t* npring = smem + S.npring;
+    const int nnd = ctl->nnd, np_head0 = ctl->np_head, py_head0 = ctl->py_head, fs = ctl->fs;
+
+    uint32_t* pk_g = st.pk + (size_t)e * P;
+    double* h_g = st.health + (size_t)e * P;
+    double* a_g = st.acc + (size_t)e * P;
+    uint32_t* scr = st.scratch + (size_t)e * wave_scratch_words(P);
+    uint2* plan = reinterpret_cast<uint2*>(scr);
+    const uint2* ndl = reinterpret_cast<const uint2*>(scr + 2 * P);
+    double* hv = reinterpret_cast<double*>(scr + wave_hv_offset(P));
+    const double* __restrict__ dpt = lay.danger_p + (size_t)fs * G;
+    const double* __restrict__ fd5 = lay.floor_d5;
+    const uint8_t* __restrict__ nbv = lay.nbr_valid;
+    int doff[8];
+#pragma unroll
+    for (int d = 0; d < 8; d++) doff[d] = move_dx(d) * GY + move_dy(d);
+    const int rd2 = lay.repel_d2;
+    const int BY = (GY + 3) >> 2;
+    int rr = 0;
+    while ((rr + 1) * (rr + 1) < rd2) rr++;
+    const int rb = rr + 1;
+
+    const int NG = (nnd + 63) >> 6;
+    const uint2 NOONE = make_uint2(0u, DONEPK);
+    constexpr int GS = 4 * WNW;  // groups per iteration of a pass: w, w + WNW, w + 2 WNW, w + 3 WNW
+
+    // pass 1: numpy draws per group (alive, not safe, danger > 0)
+    for (int g0 = w; g0 < NG; g0 += GS) {
+        uint2 en[4];
+        double dg[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int i = 64 * (g0 + WNW * j) + lane;
+            en[j] = NOONE;
+            if (i < nnd) en[j] = ndl[i];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            dg[j] = 0.0;
+            if (!((en[j].y >> 24) & 3u)) dg[j] = dpt[pk_x(en[j].y) * GY + pk_y(en[j].y)];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int c = 2 * __popcll(__ballot(!((en[j].y >> 24) & 3u) && dg[j] > 0));
+            if (lane == 0 && g0 + WNW * j < NG) {
+                npg[g0 + WNW * j] = c;
+                mvg[g0 + WNW * j] = 0;
+            }
+        }
+    }
+    WT(0);
+    for (int i = tid; i < MT_N; i += 64 * WNW) lin[i] = npring[i];
+    __syncthreads();
+    WT(1);
+    const int Tnp = group_prefix(npg, NG);
+    int front = MT_N;
+    coop_gen(lin, 0, front, np_head0 + Tnp);
+    WT(2);
+
+    // pass 2: health, accumulate, candidates; planners into this wave's list
+    int nq = 0, nd = 0;
+    for (int g0 = w; g0 < NG; g0 += GS) {
+        uint2 en[4];
+        double hh[4], ac[4], dg[4];
+        uint32_t nv[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int i = 64 * (g0 + WNW * j) + lane;
+            en[j] = NOONE;
+            if (i < nnd) en[j] = ndl[i];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int i = 64 * (g0 + WNW * j) + lane;
+            hh[j] = 0.0;
+            ac[j] = 0.0;
+            dg[j] = 0.0;
+            nv[j] = 0u;
+            if (i < nnd) {
+                hh[j] = h_g[en[j].x];
+                if (!((en[j].y >> 24) & 3u)) {
+                    const int c = pk_x(en[j].y) * GY + pk_y(en[j].y);
+                    ac[j] = a_g[en[j].x];
+                    dg[j] = dpt[c];
+                    nv[j] = nbv[c];
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int gi = g0 + WNW * j;
+            if (gi >= NG) break;
+            const int off = np_head0 + group_prefix(npg, gi);
+            const int i = 64 * gi + lane;
+            const bool inr = i < nnd;
+            const int p = (int)en[j].x;
+            const uint32_t v = en[j].y;
+            const bool act = inr && !((v >> 24) & 3u);
+            const int x = pk_x(v), y = pk_y(v), cold = x * GY + y;
+            double h = hh[j], a = ac[j];
+            const bool need = act && dg[j] > 0;
+            const unsigned long long nm = __ballot(need);
+            bool alive = act, died = false;
+            if (need) {
+                const double u = mt_double(lin, -1, off + 2 * lanes_below(nm));
+                if (update_health(h, dg[j], u)) {
+                    died = true;
+                    alive = false;
+                }
+            }
+            nd += __popcll(__ballot(died));
+            if (inr) hv[i] = died ? 0.0 : h;  // +0.0 leaves CPython's running sum unchanged
+            bool planner = false;
+            if (alive) {
+                a += person_speed(h) * 0.5;
+                if (a >= 1.0) {
+                    a -= 1.0;
+                    planner = true;
+                }
+            }
+            uint32_t cand = 0;
+            if (planner) {
+                uint32_t occ = 0;
+#pragma unroll
+                for (int d = 0; d < 8; d++) occ |= (uint32_t)bit_get(rmapb, cold + doff[d]) << d;
+                cand = nv[j] & ~occ;
+            }
+            // Python words: exclusive prefix of 2 * |cand| within the group (bit-sliced ballots)
+            const int nc = __popc(cand);
+            int off2 = 0, tot2 = 0;
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                const unsigned long long m = __ballot((nc >> b) & 1);
+                off2 += lanes_below(m) << (b + 1);
+                tot2 += __popcll(m) << (b + 1);
+            }
+            const unsigned long long qm = __ballot(cand != 0);
+            if (cand) {
+                const int k = nq + lanes_below(qm);
+                myl[3 * k] = (uint32_t)p | (cand << 16) | (NODIR << 24);
+                myl[3 * k + 1] = (uint32_t)x | ((uint32_t)y << 12) | ((uint32_t)gi << 24);
+                myl[3 * k + 2] = (uint32_t)off2;
+            }
+            nq += __popcll(qm);
+            if (lane == 0) pyg[gi] = tot2;
+            if (need) h_g[p] = h;
+            if (alive) a_g[p] = a;
+            if (died) pk_g[p] = v | (2u << 24);
+        }
+    }
+    WT(3);
+    if (lane == 0) ctl->ndc[w] = nd;
+    // the numpy stream is finished for this step: store its state (mt_store_w)
+    {
+        const int head = np_head0 + Tnp;
+        uint32_t* gst = st.np_mt + (size_t)e * EVX_MT_WORDS;
+        if (head <= MT_N) {
+            if (tid == 0) gst[MT_N] = (uint32_t)head;
+        } else {
+            const int b = MT_N * ((head - 1) / MT_N);
+            coop_gen(lin, 0, front, b + MT_N);
+            for (int i = tid; i < MT_N; i += 64 * WNW) gst[i] = lin[b + i];
+            if (tid == 0) gst[MT_N] = (uint32_t)(head - b);
+        }
+    }
+    WT(4);
+    __syncthreads();  // pass 2 done everywhere: the buffer takes the Python stream
+    for (int i = tid; i < MT_N; i += 64 * WNW) lin[i] = pyring[i];
+    const int Tpy = group_prefix(pyg, NG);
+    int nd_all = 0;
+    for (int v = 0; v < WNW; v++) nd_all += ctl->ndc[v];
+    // absolute first words of this wave's planners (its own groups only: no barrier)
+    for (int gi = w; gi < NG; gi += WNW) {
+        const int o = py_head0 + group_prefix(pyg, gi);
+        if (lane == 0) pyo[gi] = o;
+    }
+    wave_fence();
+    for (int k = lane; k < nq; k += 64) myl[3 * k + 2] += (uint32_t)pyo[myl[3 * k + 1] >> 24];
+    __syncthreads();
+    WT(5);
+
+    // find_best_direction in word windows of the linear buffer
+    front = MT_N;
+    int base = 0, cursor = 0;
+    const int pend = py_head0 + Tpy;
+    bool anyc = false;
+    while (true) {
+        const int whi = min(pend, base + WL.LINW - 16);
+        coop_gen(lin, base, front, min(whi + 16, pend));
+        WT(6);
+        while (cursor < nq) {  // this wave's planners whose first word lies below whi
+            const int k = cursor + lane;
+            const bool has = k < nq;
+            uint32_t e0 = 0, e1 = 0;
+            int sidx = 0x7fffffff;
+            if (has) {
+                e0 = myl[3 * k];
+                e1 = myl[3 * k + 1];
+                sidx = (int)myl[3 * k + 2];
+            }
+            const bool in = has && sidx < whi;
+            const int nin = __popcll(__ballot(in));
+            if (nin == 0) break;
+            const uint32_t cand = (e0 >> 16) & 0xffu;
+            const int x = pk_x(e1), y = pk_y(e1);
+            DirPrep dp;
+            dir_prep(dp, in, x, y, in ? cand : 0u, GY, fd5, nearc, BY, robots, R, rb);
+            uint32_t best = NODIR;
+            if (in) best = dir_score(dp, cand, sidx, lin, base, -1, lay.repel_k, rd2);
+            if (in) {
+                myl[3 * k] = (e0 & 0x00ffffffu) | (best << 24);
+                if (best != NODIR) {
+                    const int t = x * GY + y + doff_of(best, GY);
+                    const uint32_t bit = 1u << (t & 31);
+                    const uint32_t old = atomicOr(&tbits[t >> 5], bit);
+                    if (old & bit) {
+                        atomicOr(&cbits[t >> 5], bit);
+                        anyc = true;
+                    }
+                }
+            }
+            cursor += nin;
+            if (nin < 64) break;
+        }
+        WT(7);
+        if (whi >= pend) break;
+        __syncthreads();  // every wave is done with this window
+        const int nb = max(0, front - 1040);  // keep 1040 words: MT history + wave 0's ring
+        if (nb > base) {
+            const int cnt = front - nb;
+            uint32_t tmp[(1040 + 64 * WNW - 1) / (64 * WNW)];
+#pragma unroll
+            for (int q = 0; q < (1040 + 64 * WNW - 1) / (64 * WNW); q++) {
+                const int j = tid + 64 * WNW * q;
+                if (j < cnt) tmp[q] = lin[nb - base + j];
+            }
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < (1040 + 64 * WNW - 1) / (64 * WNW); q++) {
+                const int j = tid + 64 * WNW * q;
+                if (j < cnt) lin[j] = tmp[q];
+            }
+            base = nb;
+            __syncthreads();
+        }
+    }
+    WT(8);
+    if (__ballot(anyc) && lane == 0) atomicOr(&ctl->any_cont, 1);
+    // the movers of People.move_plan in person order: per-group counts, then offsets
+    for (int k0 = 0; k0 < nq; k0 += 64) {
+        const int k = k0 + lane;
+        if (k < nq && (myl[3 * k] >> 24) != NODIR) atomicAdd(&mvg[myl[3 * k + 1] >> 24], 1);
+    }
+    __syncthreads();
+    const int nplan = group_prefix(mvg, NG);
+    {
+        int gcur = -1, pos = 0;
+        for (int k0 = 0; k0 < nq; k0 += 64) {
+            const int k = k0 + lane;
+            const bool has = k < nq;
+            uint32_t e0 = NODIR << 24, e1 = 0;
+            if (has) {
+                e0 = myl[3 * k];
+                e1 = myl[3 * k + 1];
+            }
+            const uint32_t best = e0 >> 24;
+            const bool mover = has && best != NODIR;
+            const int gk = (int)(e1 >> 24);
+            int dst = 0;
+            unsigned long long left = __ballot(has);
+            while (left) {  // the batch's groups in order (this wave's groups only)
+                const int gsel = __builtin_amdgcn_readlane(gk, __builtin_ctzll(left));
+                const bool ing = has && gk == gsel;
+                if (gsel != gcur) {
+                    gcur = gsel;
+                    pos = group_prefix(mvg, gsel);
+                }
+                const unsigned long long mm = __ballot(ing && mover);
+                if (ing && mover) dst = pos + lanes_below(mm);
+                pos += __popcll(mm);
+                left &= ~__ballot(ing);
+            }
+            if (mover) plan[dst] = make_uint2(e0 & 0xffffu, (uint32_t)(pk_x(e1) * GY + pk_y(e1)) | (best << 24));
+        }
+    }
+    // hand the Python stream back to wave 0's ring: words [front - 1024, front)
+    for (int n = max(0, front - WR) + tid; n < front; n += 64 * WNW) pyring[n & WRM] = lin[n - base];
+    if (tid == 0) {
+        ctl->nplan = nplan;
+        ctl->n_died = nd_all;
+        ctl->py_front = front;
+        ctl->py_head_out = pend;
+    }
+    __syncthreads();
+    WT(9);
+#ifdef EVX_PROFILE
+    if (prof && tid == 0)
+        for (int i = 0; i < 10; i++) prof[36 + i] = wacc[i];
+#endif
+#undef WT
+}
+
+// Wave 1 after rows_wide: sum(p.health for p in people if not p.dead), in list order.
+__device__ __forceinline__ void wide_health_sum(const evx_layout& lay, const evx_state& st, const int e, uint32_t* smem) {
+    const int lane = (int)(threadIdx.x & 63);
+    const int P = lay.P;
+    WideCtl* ctl = reinterpret_cast<WideCtl*>(smem + wide_lds(lay).ctl);
+    const int nnd = ctl->nnd;
+    const double* hv = reinterpret_cast<const double*>(st.scratch + (size_t)e * wave_scratch_words(P) + wave_hv_offset(P));
+    double total = 0.0;
+    double cur = lane < nnd ? hv[lane] : 0.0;
+    for (int i0 = 0; i0 < nnd; i0 += 64) {
+        const double nxt = i0 + 64 + lane < nnd ? hv[i0 + 64 + lane] : 0.0;
+        const int n = min(64, nnd - i0);
+        for (int j = 0; j < n; j++) total += readlane_d(cur, j);
+        cur = nxt;
+    }
+    if (lane == 0) {
+        ctl->total = total;
+        __hip_atomic_store(&ctl->total_ready, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+}
+
+// One env-step of env e by the calling wave (smem: its wave_lds region).
+// WIDE: wave 0 of a heavy env's workgroup; the rows phase runs on all its waves.
+template <bool WIDE>
+__device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state& st, const int32_t* __restrict__ actions,
+                                         const evx_step_out& out, const int e, uint32_t* smem) {
+    const int lane = (int)(threadIdx.x & 63);
     EVX_RSTAMP(9);
     EVX_STAMP(0);
     Geo g;
@@ -703,7 +1231,7 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
             }
         }
     }
-    __syncthreads();  // not-dead list and LDS tables complete
+    wave_sync();  // not-dead list and LDS tables complete
     PT_END(ld3);
     PT_STORE(ld1, 27);
     PT_STORE(ld2, 28);
@@ -733,6 +1261,26 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
     PT_DECL(sbs);
     PT_DECL(sbt);
     double total = 0.0;  // CPython sum(p.health for p in self.people.list if not p.dead): sequential
+    if constexpr (WIDE) {
+        WideCtl* ctl = reinterpret_cast<WideCtl*>(smem + wide_lds(lay).ctl);
+        if (lane == 0) {
+            ctl->nnd = nnd;
+            ctl->np_head = np_head;
+            ctl->py_head = py_head;
+            ctl->fs = fs;
+            ctl->any_cont = 0;
+            ctl->total_ready = 0;
+        }
+        wave_sync();
+        __syncthreads();  // the other waves of the workgroup join here
+        rows_wide(lay, st, e, smem, out.stamps ? out.stamps + (size_t)e * 48 : nullptr);
+        nplan = ctl->nplan;
+        n_died = ctl->n_died;
+        any_cont = ctl->any_cont != 0;
+        py_front = ctl->py_front;
+        py_head = ctl->py_head_out;
+        EVX_COUNT(11, nplan);
+    } else {
     // Planners wait in an LDS queue and are scored 64 at a time (scoring is the
     // heavy part and only a few persons per row plan).
     uint32_t* qa = aux;        // person | candidate mask << 16   (<= 127 queued)
@@ -753,80 +1301,22 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
         const int p = (int)(ea & 0xffffu);
         const uint32_t cand = ea >> 16;
         const int x = pk_x(eb), y = pk_y(eb), cold = x * GY + y;
-        // (floor[c] - floor[c + MoveTO[d]]) * 5.0 for the 8 directions: one 64-B row
-        double f[8];
-#pragma unroll
-        for (int d = 0; d < 8; d++) f[d] = 0.0;
-        if (has) {
-            const double2* fr = reinterpret_cast<const double2*>(fd5 + (size_t)cold * 8);
-#pragma unroll
-            for (int q2 = 0; q2 < 4; q2++) {
-                const double2 v = fr[q2];
-                f[2 * q2] = v.x;
-                f[2 * q2 + 1] = v.y;
-            }
-        }
         const int first = __builtin_amdgcn_readfirstlane(off);
         const int end = __builtin_amdgcn_readlane(off + 2 * __popc(cand), n - 1);
-        uint32_t best = NODIR;
-        // squared distance to the nearest robot for the 8 neighbours, only when some
-        // candidate lies in a near-robot block (robots outer: 4 per LDS read)
-        uint32_t nearm = 0;
-#pragma unroll
-        for (int d = 0; d < 8; d++) {
-            const int nx = x + move_dx(d), ny = y + move_dy(d);
-            if (((cand >> d) & 1u) && bit_get(nearc, (nx >> 2) * BY + (ny >> 2))) nearm |= 1u << d;
-        }
-        int md2[8];
-#pragma unroll
-        for (int d = 0; d < 8; d++) md2[d] = 0x7fffffff;
-        if (__ballot(nearm != 0)) {
-            const uint4* r4 = reinterpret_cast<const uint4*>(robots);
-            for (int r0 = 0; r0 < R; r0 += 4) {
-                const uint4 q4 = r4[r0 >> 2];
-                const uint32_t rq[4] = {q4.x, q4.y, q4.z, q4.w};
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const int rx = rp_x(rq[j]), ry = rp_y(rq[j]);
-                    // robots no lane is near cannot be the nearest within range: skipped
-                    if (r0 + j < R && __ballot(abs(x - rx) <= rb && abs(y - ry) <= rb)) {
-#pragma unroll
-                        for (int d = 0; d < 8; d++) {
-                            const int dx = x + move_dx(d) - rx, dy = y + move_dy(d) - ry;
-                            md2[d] = min(md2[d], dx * dx + dy * dy);
-                        }
-                    }
-                }
-            }
-        }
+        DirPrep dp;
+        dir_prep(dp, has, x, y, cand, GY, fd5, nearc, BY, robots, R, rb);
 #ifdef EVX_PROFILE
 #pragma unroll
-        for (int d = 0; d < 8; d++) pin(f[d]);
+        for (int d = 0; d < 8; d++) pin(dp.f[d]);
 #endif
         PT_END(sbl);
+        uint32_t best = NODIR;
         for (int lo = first; lo < end; lo += WWIN) {  // windowed: a batch may need more words than the ring
             PT_BEGIN(sbm);
             mt_ensure_w(pyring, py_front, min(end, lo + WWIN + 16));
             PT_END(sbm);
             PT_BEGIN(sbs);
-            if (has && off >= lo && off < lo + WWIN) {
-                double maxs = -INFINITY;
-                int idx = off;
-#pragma unroll
-                for (int d = 0; d < 8; d++) {
-                    if ((cand >> d) & 1u) {
-                        double effect = 0.0;
-                        if (((nearm >> d) & 1u) && md2[d] < rd2) effect = lay.repel_k / (sqrt((double)md2[d]) + 0.1);
-                        const double u = -0.1 + (0.1 - -0.1) * mt_double(pyring, WRM, idx);
-                        idx += 2;
-                        const double score = f[d] + effect + u;  // delta_p * 5.0 + robot_effect + uniform
-                        if (score > maxs) {
-                            maxs = score;
-                            best = (uint32_t)d;
-                        }
-                    }
-                }
-            }
+            if (has && off >= lo && off < lo + WWIN) best = dir_score(dp, cand, off, pyring, 0, WRM, lay.repel_k, rd2);
             PT_END(sbs);
         }
         PT_BEGIN(sbt);
@@ -1049,8 +1539,9 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
     mt_store_w(npring, np_front, np_head, st.np_mt + (size_t)e * EVX_MT_WORDS);
     EVX_COUNT(13, np_head);
     EVX_COUNT(11, nplan);
+    }  // !WIDE
     any_cont = __ballot(any_cont) != 0;
-    __syncthreads();  // plan[] and the person writes are visible to every lane
+    wave_sync();  // plan[] and the person writes are visible to every lane
     EVX_STAMP(2);
 
     // The move plan in HBM is walked 4 x 64 entries at a time, loads first.
@@ -1109,7 +1600,7 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
                 if (c) Lg[k + lanes_below(m)] = key;
                 k += __popcll(m);
             });
-            __syncthreads();
+            wave_sync();
             contested_groups(Lg, Hg, Sg, ncont, pb, pyring, py_front, py_head, lost, misc, err, cgp);
         }
     }
@@ -1120,7 +1611,7 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
     EVX_COUNT(12, py_head);
     // the Python stream is stored: its ring becomes the "vacated by a winner" bitmap
     for (int i = lane; i < g.RW; i += 64) vac[i] = 0;
-    __syncthreads();
+    wave_sync();
     PT_END(mts);
     PT_STORE(lp, 24);
     PT_STORE(grp, 25);
@@ -1144,7 +1635,7 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
         }
     });
     if (lane == 0) misc[0] = 0;
-    __syncthreads();
+    wave_sync();
     uint32_t* ev = aux;  // (cell, key) pairs; groups are done
     int n_evac_new = 0;
     for (int i0 = 0; i0 < nplan; i0 += 256) {
@@ -1204,7 +1695,7 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
         n_evac_new += __popcll(__ballot(exw));
       }
     }
-    __syncthreads();
+    wave_sync();
     {
         const int nev = (int)misc[0];
         if (nev > EV_CAP) err |= 16;
@@ -1220,7 +1711,7 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
             }
         }
     }
-    __syncthreads();
+    wave_sync();
     for (int i = lane; i < g.RW; i += 64) st.rmap[(size_t)e * g.RW + i] = rmapb[i];
     EVX_STAMP(4);
 
@@ -1337,7 +1828,8 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
     }
 #pragma unroll
     for (int k = 0; k < GQ; k++) load_pw(64 * k + lane, nxj[k], nxw[k], nxhv[k]);
-    for (int it = 0; it < NIT; it++) {
+    const int NITR = (nnd + 64 * GQ - 1) / (64 * GQ);
+    for (int it = 0; it < NITR; it++) {
         PT_BEGIN(rtop);
         const int i0 = it * 64 * GQ + lane;
         uint32_t cw[GQ];
@@ -1386,6 +1878,12 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
     PT_STORE(sbs, 15);
     PT_STORE(sbt, 7);
     EVX_STAMP(5);
+    if constexpr (WIDE) {  // the health total folded by wave 1
+        WideCtl* ctl = reinterpret_cast<WideCtl*>(smem + wide_lds(lay).ctl);
+        while (__hip_atomic_load(&ctl->total_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+            __builtin_amdgcn_s_sleep(4);
+        total = ctl->total;
+    }
     if (lane == 0) {
         const int remaining = nrem;
         double reward = 0.0;
@@ -1452,7 +1950,7 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
     EVX_STAMP(8);
     if (ar) {
         __threadfence();  // this wave's state writes complete and visible before the reset reads them
-        __syncthreads();
+        wave_sync();
         reset_one(lay, st, e, smem, out.obs, out.err);
     }
     EVX_RSTAMP(10);
@@ -1467,24 +1965,11 @@ __global__ __launch_bounds__(64) void env_step_kernel(evx_layout lay, evx_state 
 // (acceptance masks by ballot, ctz jumps, word values by lane shuffle, validity
 // from the bitmap) -> (end, success, cell). The wave then follows the chain of
 // attempts from the stream head with readlanes: a few scalar ops per attempt.
-struct ResetLds {
-    int pyring, validb, rmapb, total;
-};
-__host__ __device__ inline ResetLds reset_lds(int G, int P) {
-    ResetLds s;
-    const int RW = (G + 31) / 32;
-    int o = 0;
-    s.pyring = o; o += WR;
-    s.validb = o; o += RW;
-    s.rmapb = o; o += RW;
-    s.total = (o + 3) & ~3;
-    return s;
-}
 
 // Reset of env e by the calling wave; smem: >= reset_lds(G, P).total words.
 __device__ __forceinline__ void reset_one(const evx_layout& lay, const evx_state& st, const int e, uint32_t* smem,
                                           evx_obs* obs, int32_t* err) {
-    const int lane = threadIdx.x;
+    const int lane = (int)(threadIdx.x & 63);
     Geo g;
     g.L = lay.L; g.W = lay.W; g.GY = lay.W + 2; g.G = (lay.L + 2) * (lay.W + 2);
     g.RW = (g.G + 31) / 32; g.P = lay.P; g.R = lay.R;
@@ -1616,7 +2101,7 @@ __device__ __forceinline__ void reset_one(const evx_layout& lay, const evx_state
         h_o[p] = 100.0;
         a_o[p] = 0.0;
     }
-    __syncthreads();  // person words and rmap bits complete
+    wave_sync();  // person words and rmap bits complete
     if (st.thmap) {
         int32_t* th = st.thmap + (size_t)e * g.G;
         for (int i = lane; i < g.G; i += 64) th[i] = (rmapb[i >> 5] >> (i & 31)) & 1u;
@@ -1630,7 +2115,7 @@ __device__ __forceinline__ void reset_one(const evx_layout& lay, const evx_state
     } else {
         view = rp_pack(lay.reset_view_x, lay.reset_view_y);
     }
-    __syncthreads();
+    wave_sync();
     if (lane == 0) {
         st.view[e] = view;
         int* sg = st.scal + (size_t)e * 4;
@@ -1661,22 +2146,67 @@ __global__ __launch_bounds__(64) void env_reset_kernel(evx_layout lay, evx_state
     reset_one(lay, st, e, smem, obs, err);
 }
 
+// NWB waves per workgroup, one env per wave, no block barrier between envs, in the
+// dispatch order evx_env_order chose (heavy envs first). With NWB == WNW the first H
+// workgroups take one heavy env each (its rows phase on all waves); once the rows
+// are done, waves 1.. of heavy workgroup b take the light envs at the tail of the
+// order (3 per heavy env), the remaining envs go 4 per workgroup.
+template <int NWB>
+__global__ __launch_bounds__(64 * NWB) void env_step_kernel(evx_layout lay, evx_state st,
+                                                            const int32_t* __restrict__ actions, evx_step_out out,
+                                                            int hcap) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    const int w = (int)(threadIdx.x >> 6);
+    const int words = step_lds_words(lay);
+    const int H = (NWB == WNW && st.order && hcap > 0) ? min(hcap, st.order[st.E]) : 0;
+    // light envs order[H, E): the last nt of them go to the heavy workgroups' spare waves
+    const int nt = min((NWB - 1) * H, st.E - H);
+    if ((int)blockIdx.x < H) {
+        const int e = st.order[blockIdx.x];
+        int slot = -1;
+        if (w == 0) {
+            step_env<true>(lay, st, actions, out, e, smem);
+        } else {
+            __syncthreads();  // wave 0 has published the rows inputs
+            rows_wide(lay, st, e, smem);
+            if (w == 1) wide_health_sum(lay, st, e, smem);
+            const int t = (int)blockIdx.x * (NWB - 1) + (w - 1);
+            if (t < nt) slot = st.E - nt + t;
+        }
+        if (slot >= 0) step_env<false>(lay, st, actions, out, st.order[slot], smem + (size_t)w * words);
+        return;
+    }
+    const int slot = H + ((int)blockIdx.x - H) * NWB + w;
+    if (slot >= st.E - nt) return;
+    const int e = st.order ? st.order[slot] : slot;
+    step_env<false>(lay, st, actions, out, e, smem + (size_t)w * words);
+}
+
 // ------------------------------------------------------- dispatch order
 // A step's cost grows with the persons still in play, and one env is one wave:
 // the launch ends with its slowest env. Dispatching envs by descending remaining
 // persons (16 buckets, stable counting sort in one workgroup) starts the heavy
 // ones first so the light ones fill in around them.
-__global__ __launch_bounds__(1024) void env_order_kernel(evx_layout lay, evx_state st) {
-    __shared__ int cnt[16], base[16];
+// order[E] = H: the first H envs of the order (at most hcap, each with >= hmin persons
+// in play) run their rows phase on a whole workgroup (rows_wide).
+__global__ __launch_bounds__(1024) void env_order_kernel(evx_layout lay, evx_state st, int hcap, int hmin) {
+    __shared__ int cnt[16], base[16], nheavy;
     const int tid = threadIdx.x, E = st.E, P = lay.P;
     if (tid < 16) cnt[tid] = 0;
+    if (tid == 0) nheavy = 0;
     __syncthreads();
+    auto remaining = [&](int e) { return P - st.scal[(size_t)e * 4 + 2] - st.scal[(size_t)e * 4 + 3]; };
     auto bucket = [&](int e) {
-        const int rem = P - st.scal[(size_t)e * 4 + 2] - st.scal[(size_t)e * 4 + 3];
-        return 15 - min(15, max(0, rem) * 16 / (P + 1));  // 0 = most remaining
+        return 15 - min(15, max(0, remaining(e)) * 16 / (P + 1));  // 0 = most remaining
     };
-    for (int e = tid; e < E; e += 1024) atomicAdd(&cnt[bucket(e)], 1);
+    int nh = 0;
+    for (int e = tid; e < E; e += 1024) {
+        atomicAdd(&cnt[bucket(e)], 1);
+        nh += remaining(e) >= hmin;
+    }
+    if (nh) atomicAdd(&nheavy, nh);
     __syncthreads();
+    if (tid == 0) st.order[E] = min(hcap, nheavy);
     if (tid == 0) {
         int o = 0;
         for (int b = 0; b < 16; b++) {
@@ -1755,9 +2285,27 @@ __global__ __launch_bounds__(256) void obs_expand_kernel(evx_layout lay, const e
 
 // ===================================================================== C-ABI
 // the step kernel's dynamic LDS also hosts a fused auto-reset
-static size_t step_lds_bytes(const evx_layout& l) {
-    const int G = (l.L + 2) * (l.W + 2);
-    return (size_t)std::max(evx::wave_lds(l.L, l.W, l.P, l.R).total, evx::reset_lds(G, l.P).total) * 4;
+static size_t step_lds_bytes(const evx_layout& l) { return (size_t)evx::step_lds_words(l) * 4; }
+// dynamic LDS of a step workgroup of nwb waves: nwb envs, or (nwb == 4) one heavy env
+static size_t step_launch_lds(const evx_layout& l, int nwb) {
+    if (nwb != evx::WNW) return step_lds_bytes(l) * nwb;
+    return (size_t)evx::wide_lds(l).total * 4;  // WNW env regions + WideCtl
+}
+// Heavy envs per step (rows_wide workgroups): at most the cap, each with >= *hmin
+// persons in play; 0 when the 4-wave workgroup does not fit in LDS. EVX_HEAVY_CAP /
+// EVX_HEAVY_MIN override (tuning).
+static int heavy_cap(const evx_layout& l, int* hmin) {
+    static int cap_env = -2, min_env = -2;
+    if (cap_env == -2) {
+        const char* v = getenv("EVX_HEAVY_CAP");
+        cap_env = v ? atoi(v) : -1;
+        const char* m = getenv("EVX_HEAVY_MIN");
+        min_env = m ? atoi(m) : -1;
+    }
+    *hmin = std::max(1, min_env >= 0 ? min_env : l.P / 4);
+    const evx::WideLds wl = evx::wide_lds(l);
+    if (step_launch_lds(l, evx::WNW) > 160 * 1024 || wl.end > wl.ctl) return 0;
+    return cap_env >= 0 ? cap_env : 256;
 }
 
 namespace {
@@ -1813,11 +2361,35 @@ int evx_env_step(const evx_layout* l, const evx_state* s, const int32_t* actions
     if (lds > 160 * 1024) return fail(-7, "layout needs more than 160 KiB of LDS");
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)evx::env_step_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void*)evx::env_step_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        (void)hipFuncSetAttribute((const void*)evx::env_step_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        (void)hipFuncSetAttribute((const void*)evx::env_step_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024);
         attr_set = true;
     }
-    hipLaunchKernelGGL(evx::env_step_kernel, dim3(s->E), dim3(64), lds, (hipStream_t)stream, *l, *s, actions, *o);
+    // envs per workgroup (one per wave): EVX_STEP_NWB overrides (diagnostics)
+    static int nwb_env = -1;
+    if (nwb_env < 0) {
+        const char* v = getenv("EVX_STEP_NWB");
+        nwb_env = v ? atoi(v) : 0;
+    }
+    int nwb = nwb_env == 1 || nwb_env == 2 || nwb_env == 4 ? nwb_env : 4;
+    while (nwb > 1 && step_launch_lds(*l, nwb) > 160 * 1024) nwb >>= 1;
+    int hmin = 0;
+    const int hcap = (nwb == evx::WNW && s->order) ? heavy_cap(*l, &hmin) : 0;
+    const size_t blds = step_launch_lds(*l, nwb);
+    const int nblk = (s->E + nwb - 1) / nwb + hcap;  // heavy envs take a workgroup each
+    if (nwb == 4)
+        hipLaunchKernelGGL(evx::env_step_kernel<4>, dim3(nblk), dim3(256), blds, (hipStream_t)stream, *l, *s, actions, *o,
+                           hcap);
+    else if (nwb == 2)
+        hipLaunchKernelGGL(evx::env_step_kernel<2>, dim3(nblk), dim3(128), blds, (hipStream_t)stream, *l, *s, actions, *o,
+                           0);
+    else
+        hipLaunchKernelGGL(evx::env_step_kernel<1>, dim3(nblk), dim3(64), blds, (hipStream_t)stream, *l, *s, actions, *o,
+                           0);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : hip_fail(e, "env_step launch");
 }
@@ -1849,7 +2421,9 @@ int evx_env_order(const evx_layout* l, const evx_state* s, void* stream) {
     if (rc) return rc;
     if (!s || !s->order) return fail(-22, "env_order: state.order is NULL");
     if (s->E <= 0) return 0;
-    hipLaunchKernelGGL(evx::env_order_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, *l, *s);
+    int hmin = 0;
+    const int hcap = heavy_cap(*l, &hmin);
+    hipLaunchKernelGGL(evx::env_order_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, *l, *s, hcap, hmin);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : hip_fail(e, "env_order launch");
 }

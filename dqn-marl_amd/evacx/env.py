@@ -172,7 +172,9 @@ class VecEnv:
         if sw < 0:
             raise _lib.EvacxError(_lib.lib().evx_last_error().decode())
         self.scratch = torch.zeros(E * sw, **i32)
-        self.order = torch.arange(E, **i32)  # dispatch order (evx_env_order), scheduling only
+        # dispatch order (evx_env_order), scheduling only; order[E] = envs whose rows
+        # phase runs on a whole workgroup (0: none)
+        self.order = torch.cat([torch.arange(E, **i32), torch.zeros(1, **i32)])
         # outputs
         self.reward = torch.zeros(E, **f64)
         self.done = torch.zeros(E, dtype=torch.uint8, device=d)
@@ -217,10 +219,11 @@ class VecEnv:
         _lib.check(_lib.lib().evx_env_reset(C.byref(self.lay.c), C.byref(self.c), _ptr(m), _ptr(self.obs),
                                             _ptr(self.err), _stream()), "evx_env_reset")
 
-    def compute_order(self):
-        """Dispatch order of the next step: heavy env-steps first (scheduling only; the
-        results do not depend on it). Small batches keep the identity order."""
-        if self.E >= 256:
+    def compute_order(self, force: bool = False):
+        """Dispatch order of the next step: heavy env-steps first, the heaviest with a
+        whole workgroup each (scheduling only; the results do not depend on it). Small
+        batches keep the identity order unless forced (tests)."""
+        if self.E >= 256 or force:
             _lib.check(_lib.lib().evx_env_order(C.byref(self.lay.c), C.byref(self.c), _stream()), "evx_env_order")
 
     def step(self, actions: torch.Tensor, order: bool = True, auto_reset: bool = False):

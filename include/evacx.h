@@ -68,7 +68,8 @@ typedef struct {
     uint32_t *py_mt;   /* [E*625] CPython `random` MT19937 state per env */
     uint32_t *np_mt;   /* [E*625] legacy numpy.random MT19937 state per env */
     uint32_t *scratch; /* [E*evx_step_scratch_words] step scratch: move plan, contested lists beyond LDS */
-    int32_t *order;    /* [E] dispatch order of the step's envs (evx_env_order), or NULL = 0..E-1 */
+    int32_t *order;    /* [E+1] dispatch order of the step's envs (evx_env_order), or NULL = 0..E-1;
+                        * order[E] = H: the first H of them are heavy (rows phase on a 4-wave workgroup) */
 } evx_state;
 
 /* Compact per-robot observation (32 B). Expands to the reference's 11x11x6
@@ -116,7 +117,9 @@ int evx_obs_expand_f64(const evx_layout *lay, const evx_obs *obs, int64_t n, dou
 int evx_seed_host(const uint32_t *seeds_host, int32_t n, uint32_t *py_mt_host, uint32_t *np_mt_host);
 
 /* Scheduling only (results do not depend on it): st->order = envs by descending
- * persons still in play, so the heaviest env-steps start first. */
+ * persons still in play, so the heaviest env-steps start first; order[E] = how many
+ * of the first get a whole workgroup each (at most 256, each with >= P/4 persons in
+ * play; EVX_HEAVY_CAP / EVX_HEAVY_MIN override). */
 int evx_env_order(const evx_layout *lay, const evx_state *st, void *stream);
 
 /* Bytes of dynamic LDS the step kernel needs for a layout (diagnostics). */

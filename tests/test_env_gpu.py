@@ -75,10 +75,13 @@ def test_gpu_replays_reference_trajectory(traj):
     assert np.array_equal(py[0], tr["rng_py_final"]) and np.array_equal(nps[0], tr["rng_np_final"])
 
 
-def _oracle_pair(spec, P, E, steps, seed0=1234, act_seed=7, thmap=True, check_every=1, auto_reset=False):
+def _oracle_pair(spec, P, E, steps, seed0=1234, act_seed=7, thmap=True, check_every=1, auto_reset=False,
+                 wide=False):
     """Run E envs on the GPU and in the oracle with identical seeds/actions.
     auto_reset: finished envs are reset inside the step launch (VecEnv.step
-    auto_reset); their terminal observations are checked from env.obs_term."""
+    auto_reset); their terminal observations are checked from env.obs_term.
+    wide: evx_env_order before every step, so envs with >= P/4 persons in play run
+    their rows phase on a whole workgroup (rows_wide)."""
     from evacx.env import DeviceLayout, VecEnv
     from evacx.layout import build_tables
     from oracle import oracle as orc
@@ -95,11 +98,15 @@ def _oracle_pair(spec, P, E, steps, seed0=1234, act_seed=7, thmap=True, check_ev
     oobs = [oe.reset() for oe in oenvs]
     rng = np.random.RandomState(act_seed)
     n_resets = 0
+    max_heavy = 0
     for s in range(steps + 1):
         if s > 0:
             acts = rng.randint(0, 5, size=(E, R)).astype(np.int32)
             acts[rng.rand(E, R) < 0.02] = 7  # invalid actions are ignored by the reference
-            env.step(torch.from_numpy(acts.reshape(-1)).cuda(), auto_reset=auto_reset)
+            if wide:
+                env.compute_order(force=True)
+                max_heavy = max(max_heavy, int(env.order[E].item()))
+            env.step(torch.from_numpy(acts.reshape(-1)).cuda(), order=not wide, auto_reset=auto_reset)
             res = [oe.step(acts[i]) for i, oe in enumerate(oenvs)]
             oobs = [r[0] for r in res]
             rew = env.reward.cpu().numpy()
@@ -136,6 +143,7 @@ def _oracle_pair(spec, P, E, steps, seed0=1234, act_seed=7, thmap=True, check_ev
                 for i in np.nonzero(d.cpu().numpy())[0]:
                     oobs[i] = oenvs[i].reset()
     env.check_err()
+    _oracle_pair.max_heavy = max_heavy
     return n_resets
 
 
@@ -159,6 +167,29 @@ def test_gpu_auto_reset_vs_oracle_dense():
     from evacx.layout import synthetic
     n = _oracle_pair(synthetic(24, 20, 4), 380, E=16, steps=120, check_every=3, auto_reset=True)
     assert n > 0
+
+
+def test_gpu_wide_rows_vs_oracle_128_r16():
+    """Heavy envs (rows phase on 4 waves) against the oracle at the benchmark layout."""
+    _need_gpu()
+    from evacx.layout import synthetic
+    _oracle_pair(synthetic(128, 128, 16), 2276, E=6, steps=40, check_every=5, wide=True)
+    assert _oracle_pair.max_heavy == 6
+
+
+def test_gpu_wide_rows_vs_oracle_dense():
+    """Wide and single-wave envs in one launch, big shuffles, episodes ending."""
+    _need_gpu()
+    from evacx.layout import synthetic
+    _oracle_pair(synthetic(24, 20, 4), 380, E=16, steps=120, check_every=1, wide=True, auto_reset=True)
+    assert _oracle_pair.max_heavy == 16
+
+
+def test_gpu_wide_rows_vs_oracle_cfg1_resets():
+    _need_gpu()
+    from evacx.layout import reference_single
+    n = _oracle_pair(reference_single(), 150, E=48, steps=260, check_every=13, wide=True, auto_reset=True)
+    assert n > 48 and _oracle_pair.max_heavy > 0
 
 
 def test_gpu_vs_oracle_multi_cfg1():

@@ -76,5 +76,23 @@ if s[:, 16:30].any():
     print("sub-phase cycle accumulators (EVX_PROFILE build):        median   slowest1%")
     for c, n in PROF:
         print(f"  {n:28s} {np.median(s[:, c]):9.0f} {s[top, c].mean():10.0f}")
+WIDE = [(36, "wide: pass1 (np counts)"), (37, "wide: barrier+copy"), (38, "wide: np gen"), (39, "wide: pass2"),
+        (40, "wide: np store"), (41, "wide: py setup"), (42, "wide: py gen"), (43, "wide: scoring"),
+        (44, "wide: movers+plan+handoff"), (45, "wide: final barrier")]
+if s[:, 36:46].any():
+    hv = s[:, 36:46].sum(1) > 0
+    tw = order[-max(1, E // 100):]
+    print(f"wide rows (EVX_PROFILE build), {hv.sum()} heavy envs:   median(heavy)  slowest1%")
+    for c, n in WIDE:
+        print(f"  {n:28s} {np.median(s[hv, c]):9.0f} {s[tw, c].mean():10.0f}")
+    t0 = s[:, 9].min()
+    st_us, en_us = (s[:, 9] - t0) / 100, (s[:, 10] - t0) / 100
+    for nm, m in [("wide", hv), ("single-wave", ~hv)]:
+        if m.any():
+            print(f"  {nm:12s} n={m.sum():5d} lifetime us median {np.median(life[m]) / 100:6.1f} max {life[m].max() / 100:6.1f}"
+                  f"  start max {st_us[m].max():6.1f}  end max {en_us[m].max():6.1f}  planners median {np.median(s[m, 11]):.0f}")
+    nw = ~hv
+    top_single = np.argsort(life * nw)[-10:]
+    print("  slowest single-wave envs: life us", (life[top_single] / 100).round(1), "planners", s[top_single, 11])
 cnt = env.counts.view(E, 2).cpu().numpy()
 print("evacuated median", np.median(cnt[:, 0]), "dead median", np.median(cnt[:, 1]))
