@@ -334,9 +334,10 @@ class Learner:
         self.step_optimizer()
         return self.loss
 
-    def learn_obs(self, lay_c, s_obs, a, r, done, s2_obs, B):
+    def learn_obs(self, lay_c, s_obs, a, r, done, s2_obs, B, update: bool = True):
         """DQNAgent.learn on compact observations with the fused bf16 kernels:
-        online forward (saves X, H1, H2), target forward, TD loss, backward, clip+Adam."""
+        online forward (saves X, H1, H2), target forward, TD loss, backward, clip+Adam.
+        update=False stops after the gradients (the caller runs step_optimizer later)."""
         from .qmlp import HID, HID2, K1P
         ws, dev = self.net.ws, self.device
         X = ws.get("fx", (B * K1P,), torch.int16, dev)
@@ -358,7 +359,8 @@ class Learner:
         self.fast.backward(B, dQ, X, H1, H2, DROPOUT_P, dz2, dz1, self.grads)
         if self.grad_hook is not None:
             self.grad_hook(self.grads.flat)
-        self.step_optimizer()
+        if update:
+            self.step_optimizer()
         return self.loss
 
     def step_optimizer(self):

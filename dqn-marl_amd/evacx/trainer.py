@@ -18,6 +18,7 @@ reward) generalised to R robots and E envs; DQNAgent.act/remember/learn
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import Optional
 
 import torch
@@ -125,11 +126,18 @@ class VecTrainer:
         self.seed = learner_seed * 7919 + env_offset + 17
         self.t = 0
         self.learn_steps = 0
+        # the step's own chain (act, env.step, push) on a high-priority stream: with the
+        # lagged schedule the learn stream's workgroups then fill the env launch's tail
+        # instead of competing for its first slots
+        self.main = torch.cuda.Stream(device=self.device, priority=int(os.environ.get("EVX_MAIN_PRIO", "-1")))
         self.side = torch.cuda.Stream(device=self.device)
         self.ev_push = torch.cuda.Event()
+        self.ev_push.record(torch.cuda.current_stream(self.device))
         self.ev_reset = torch.cuda.Event()
         self.ev_reset.record(torch.cuda.current_stream(self.device))
-        self.lstream = torch.cuda.Stream(device=self.device)
+        self.reset_pending = False
+        self.join_caller = True  # the first step waits for the caller's stream (set-up work)
+        self.lstream = torch.cuda.Stream(device=self.device, priority=int(os.environ.get("EVX_LEARN_PRIO", "0")))
         self.ev_act = torch.cuda.Event()
         self.ev_learned = torch.cuda.Event()
         self.ev_learned.record(torch.cuda.current_stream(self.device))
@@ -140,6 +148,8 @@ class VecTrainer:
         self.fast = self.learner.fast
         if self.fast is not None:
             self.h1_act = torch.empty(n * HID, dtype=torch.int16, device=self.device)
+        if self.fast is None:
+            self.lagged = False  # the split learn step needs the fused bf16 MLP path
 
     def act(self):
         if self.fast is not None:
@@ -155,22 +165,31 @@ class VecTrainer:
                               self.t * self.n_agents, self.actions.data_ptr(), _stream()), "act")
         return self.actions
 
-    def learn(self, window=None):
-        """window: (base, count) of the replay ring to sample from (default: all of it)."""
-        if (self.replay.size if window is None else window[1]) < self.batch:
-            return None
-        if window is None:
-            self.replay.sample(self.batch, self.seed + 1, self.learn_steps * self.batch, self.samp)
+    def learn(self, window=None, phase: str = "all"):
+        """window: (base, count) of the replay ring to sample from (default: all of it).
+        phase: "all", or "grads" (sample .. backward) then "update" (clip+Adam, bf16
+        repack, epsilon, target sync) -- the update may wait for readers of the weights."""
+        if phase != "update":
+            if (self.replay.size if window is None else window[1]) < self.batch:
+                return None
+            if window is None:
+                self.replay.sample(self.batch, self.seed + 1, self.learn_steps * self.batch, self.samp)
+            else:
+                self.replay.sample_window(window[0], window[1], self.batch, self.seed + 1,
+                                          self.learn_steps * self.batch, self.samp)
+            if self.fast is not None:
+                loss = self.learner.learn_obs(self.lay.c, self.samp["s"], self.samp["a"], self.samp["r"],
+                                              self.samp["done"], self.samp["s2"], self.batch, update=phase == "all")
+            else:
+                assert phase == "all", "split learn needs the fused bf16 MLP path"
+                s = self.env.expand_obs(torch.float32, self.samp["s"]).view(self.batch, 11, 11, 6)
+                s2 = self.env.expand_obs(torch.float32, self.samp["s2"]).view(self.batch, 11, 11, 6)
+                loss = self.learner.learn(s, self.samp["a"], self.samp["r"], self.samp["done"], s2)
+            if phase == "grads":
+                return loss
         else:
-            self.replay.sample_window(window[0], window[1], self.batch, self.seed + 1, self.learn_steps * self.batch,
-                                      self.samp)
-        if self.fast is not None:
-            loss = self.learner.learn_obs(self.lay.c, self.samp["s"], self.samp["a"], self.samp["r"],
-                                          self.samp["done"], self.samp["s2"], self.batch)
-        else:
-            s = self.env.expand_obs(torch.float32, self.samp["s"]).view(self.batch, 11, 11, 6)
-            s2 = self.env.expand_obs(torch.float32, self.samp["s2"]).view(self.batch, 11, 11, 6)
-            loss = self.learner.learn(s, self.samp["a"], self.samp["r"], self.samp["done"], s2)
+            self.learner.step_optimizer()
+            loss = self.learner.loss
         self.learn_steps += 1
         if self.epsilon > self.epsilon_min:  # DQNAgent.learn epsilon schedule (agents/dqn_agent.py:163-164)
             self.epsilon *= self.epsilon_decay
@@ -188,23 +207,43 @@ class VecTrainer:
         (start, end) CUDA events.
 
         Default order is the reference's (act, env.step, remember, learn). With
-        lagged_learn the learn step is issued right after act on its own stream: it
-        samples the ring as it was before this step's push (minus the slots the push
-        overwrites), so it overlaps env.step; the next act waits for it."""
-        main = torch.cuda.current_stream(self.device)
-        main.wait_event(self.ev_reset)
+        lagged_learn the learn step runs on its own stream from the ring as it was
+        before this step's push (minus the slots the push overwrites): its gradients
+        overlap act and env.step, its weight update waits for act to have read the
+        weights, and the next act waits for the update."""
+        caller = torch.cuda.current_stream(self.device)
+        main = self.main
+        if self.join_caller or extra_reset is not None:  # inputs made on the caller's stream
+            main.wait_stream(caller)
+            self.join_caller = False
+        if extra_reset is not None:
+            extra_reset.record_stream(main)  # the caller may free it before main reads it
+        with torch.cuda.stream(main):
+            self._step(main, extra_reset, ev_env, ev_learn)
+
+    def _step(self, main, extra_reset, ev_env, ev_learn):
+        if self.reset_pending:  # a cross-stream wait costs tens of us: only when there was a reset
+            main.wait_event(self.ev_reset)
+            self.reset_pending = False
         if self.lagged:
+            # learn t: gradients from the ring as it stood after push t-1 (minus the slots
+            # push t overwrites), overlapping act t and env.step t; the weight update
+            # waits until act t has read the weights, and act t+1 waits for it
             main.wait_event(self.ev_learned)
-        self.act()
-        if self.lagged:
-            self.ev_act.record(main)  # learn's optimizer rewrites the weights act has read
             win = self.replay.window(self.n_agents)
+            do_learn = self.t % self.learn_every == 0 and win[1] >= self.batch and self.fast is not None
             with torch.cuda.stream(self.lstream):
-                self.lstream.wait_event(self.ev_act)
+                self.lstream.wait_event(self.ev_push)
                 if ev_learn is not None:
                     ev_learn[0].record(self.lstream)
-                if self.t % self.learn_every == 0:
-                    self.last_loss = self.learn(window=win)
+                if do_learn:
+                    self.learn(window=win, phase="grads")
+        self.act()
+        if self.lagged:
+            self.ev_act.record(main)
+            with torch.cuda.stream(self.lstream):
+                self.lstream.wait_event(self.ev_act)
+                self.last_loss = self.learn(phase="update") if do_learn else None
                 if ev_learn is not None:
                     ev_learn[1].record(self.lstream)
                 self.ev_learned.record(self.lstream)
@@ -217,12 +256,17 @@ class VecTrainer:
             ev_env[1].record(main)
         self.replay.push(self.obs_prev, self.env.obs, self.actions, self.env.reward, self.env.done,
                          self.n_agents, self.R, s2_term=self.env.obs_term)
+        mask = None
+        if extra_reset is not None:
+            mask = extra_reset & ~self.env.done.bool()  # made on main; read on the side stream
+            mask.record_stream(self.side)
         self.ev_push.record(main)
         with torch.cuda.stream(self.side):
             self.side.wait_event(self.ev_push)
-            if extra_reset is not None:
-                self.env.reset(mask=extra_reset & ~self.env.done.bool())
-            self.ev_reset.record(self.side)
+            if mask is not None:
+                self.env.reset(mask=mask)
+                self.ev_reset.record(self.side)
+                self.reset_pending = True
             self.env.compute_order()
             self.ev_order.record(self.side)
         if not self.lagged:
@@ -235,10 +279,15 @@ class VecTrainer:
         self.t += 1
 
     def sync(self):
-        """Make the current stream wait for the side-stream work of the last step."""
+        """Make the current stream wait for all work of the steps so far. step() runs on
+        the trainer's own streams and does not join the caller's stream each step (a
+        cross-stream round trip costs tens of microseconds); read results after sync()."""
         cur = torch.cuda.current_stream(self.device)
+        cur.wait_stream(self.main)
         cur.wait_event(self.ev_reset)
         cur.wait_event(self.ev_learned)
+        cur.wait_event(self.ev_order)
+        self.join_caller = True
 
 
 def make_allreduce_hook(dist, world: int):

@@ -25,6 +25,7 @@ def test_vec_trainer_runs_and_learns(precision):
     losses = []
     for _ in range(20):
         tr.step()
+        tr.sync()  # the trainer runs on its own streams
         if tr.last_loss is not None:
             losses.append(tr.last_loss.item())
     tr.env.check_err()

@@ -11,7 +11,7 @@ OUT=$R/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/train" -o run --output-format csv -- \
-    python3 "$R/bench.py" --steps 20 --no-cpu --env-steps 0 > "$OUT/train.log" 2>&1
+    python3 "$R/bench.py" --steps 20 --no-cpu --env-steps 0 --strict-steps 0 > "$OUT/train.log" 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/env" -o run --output-format csv -- \
     python3 "$R/bench.py" --mode env --steps 30 --no-cpu > "$OUT/env.log" 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv -- \

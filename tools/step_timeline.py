@@ -21,3 +21,11 @@ for a, b in zip(idx[-11:-1], idx[-10:]):
 print("mean per step over the last 10 windows (us):")
 for n, v in sorted(agg.items(), key=lambda x: -x[1]):
     print(f"  {v:8.1f}  {n}")
+# one window in detail: start / end offsets (us) and the stream of every kernel
+a, b = idx[-3], idx[-2]
+t0 = int(rows[a]["Start_Timestamp"])
+print("one step window in detail (offsets from its env_step_kernel start, us):")
+for r in rows[a - 12:b + 2]:
+    s0 = (int(r["Start_Timestamp"]) - t0) / 1e3
+    s1 = (int(r["End_Timestamp"]) - t0) / 1e3
+    print(f"  {s0:8.1f} {s1:8.1f}  q{r.get('Queue_Id', '?'):>3s} s{r.get('Stream_Id', '?'):>3s}  {r['Kernel_Name'][:70]}")
