@@ -226,10 +226,12 @@ class VecTrainer:
             main.wait_event(self.ev_reset)
             self.reset_pending = False
         if self.lagged:
+            main.wait_event(self.ev_learned)
+        self.act()  # issued first: its workgroups are dispatched ahead of the learn step's
+        if self.lagged:
             # learn t: gradients from the ring as it stood after push t-1 (minus the slots
             # push t overwrites), overlapping act t and env.step t; the weight update
             # waits until act t has read the weights, and act t+1 waits for it
-            main.wait_event(self.ev_learned)
             win = self.replay.window(self.n_agents)
             do_learn = self.t % self.learn_every == 0 and win[1] >= self.batch and self.fast is not None
             with torch.cuda.stream(self.lstream):
@@ -238,8 +240,6 @@ class VecTrainer:
                     ev_learn[0].record(self.lstream)
                 if do_learn:
                     self.learn(window=win, phase="grads")
-        self.act()
-        if self.lagged:
             self.ev_act.record(main)
             with torch.cuda.stream(self.lstream):
                 self.lstream.wait_event(self.ev_act)
