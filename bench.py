@@ -79,6 +79,9 @@ def parse():
     ap.add_argument("--schedule", choices=["strict", "lagged"], default="lagged",
                     help="strict: act, env.step, push, learn (the reference's order); lagged: learn t samples "
                          "the ring before push t and overlaps env.step t (evacx.trainer.VecTrainer)")
+    ap.add_argument("--replay", choices=["uniform", "prioritized"], default="uniform",
+                    help="prioritized: GPU sum/min-tree proportional replay (cfg5; evacx.prio)")
+    ap.add_argument("--replay-capacity", type=int, default=1 << 20)
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r1", "env_traffic.json"),
                     help="PMC traffic record of env_step_kernel on this workload (tools/parse_prof.py)")
     return ap.parse_args()
@@ -106,7 +109,8 @@ def main():
     lay = DeviceLayout(tables, P)
     hook = make_allreduce_hook(dist, world) if dist is not None else None
     tr = VecTrainer(lay, E, env_offset=rank * E, precision=args.precision, batch=args.batch, grad_hook=hook,
-                    lagged_learn=args.schedule == "lagged")
+                    lagged_learn=args.schedule == "lagged", replay=args.replay,
+                    replay_capacity=args.replay_capacity)
     env = tr.env
 
     def barrier():
@@ -223,12 +227,13 @@ def main():
             "dtype": "f64" if args.mode == "env" else f"f64 env + {args.precision} Q-net",
             "data": "synthetic",
             "config": {
-                "workload": (f"cfg3 per-GPU share: {L}x{W} synthetic layout, {P} people, {R} robots, {E} envs/GPU; "
+                "workload": (f"{'cfg5' if R == 32 and args.replay == 'prioritized' else 'cfg3'} per-GPU share: {L}x{W} synthetic layout, {P} people, {R} robots, {E} envs/GPU; "
                              + ("full training step: act + env.step + replay push + learn (B="
                                 f"{args.batch}) + auto-reset" if args.mode == "train"
                                 else "env.step + auto-reset, uniform random actions")),
                 "envs_per_gpu": E, "grid": f"{L}x{W}", "people": P, "robots": R, "mode": args.mode,
                 "batch": args.batch, "qnet": "MLP 726-512-256-5", "schedule": args.schedule,
+                "replay": args.replay,
                 "parallelism": f"data-parallel over {world} GPU(s): envs sharded, grad all-reduce (RCCL) per learn",
             },
             "strict_schedule_steps_per_s": strict,

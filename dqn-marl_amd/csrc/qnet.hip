@@ -266,7 +266,8 @@ __global__ __launch_bounds__(256) void colsum_finish(const float* __restrict__ p
 
 // --------------------------------------------------------------- TD loss
 // DQNAgent.learn (agents/dqn_agent.py:143-151): q = Q(s).gather(a); y = r + gamma *
-// max Q_tgt(s') * ~done; loss = mean((q - y)^2); dQ[i, a_i] = 2 (q - y) / B.
+// max Q_tgt(s') * ~done; loss = mean((q - y)^2); dQ[i, a_i] = 2 (q - y) / B. With
+// importance weights w (prioritized replay): loss = mean(w (q - y)^2), and |q - y| out.
 // One row per thread over many blocks; the last block to finish sums the block
 // partials in block order (deterministic).
 __device__ float g_td_part[4096];
@@ -274,8 +275,9 @@ __device__ unsigned int g_td_ticket = 0;
 __global__ __launch_bounds__(256) void td_loss_kernel(const float* __restrict__ Q, const float* __restrict__ Qt,
                                                       int A, const int32_t* __restrict__ act,
                                                       const float* __restrict__ rew, const uint8_t* __restrict__ done,
-                                                      float gamma, int B, float* __restrict__ dQ,
-                                                      float* __restrict__ loss_out) {
+                                                      float gamma, int B, const float* __restrict__ w,
+                                                      float* __restrict__ dQ, float* __restrict__ loss_out,
+                                                      float* __restrict__ td_abs) {
     __shared__ float red[256];
     __shared__ bool last;
     const int i = blockIdx.x * 256 + threadIdx.x;
@@ -286,8 +288,12 @@ __global__ __launch_bounds__(256) void td_loss_kernel(const float* __restrict__ 
         const float y = rew[i] + gamma * mx * (done[i] ? 0.f : 1.f);
         const int a = act[i];
         const float d = Q[(int64_t)i * A + a] - y;
-        part = d * d;
-        for (int j = 0; j < A; j++) dQ[(int64_t)i * A + j] = (j == a) ? 2.f * d / (float)B : 0.f;
+        // prioritized replay: importance weights scale each squared error and its gradient
+        const float wi = w ? w[i] : 1.f;
+        part = w ? wi * (d * d) : d * d;
+        const float g = w ? wi * (2.f * d) : 2.f * d;
+        for (int j = 0; j < A; j++) dQ[(int64_t)i * A + j] = (j == a) ? g / (float)B : 0.f;
+        if (td_abs) td_abs[i] = fabsf(d);
     }
     red[threadIdx.x] = part;
     __syncthreads();
@@ -572,13 +578,19 @@ int evx_colsum(const float* X, int64_t ld, int32_t M, int32_t N, float* out, int
     return qlaunch("colsum");
 }
 
-int evx_td_loss(const float* Q, const float* Qt, int32_t A, const int32_t* act, const float* rew, const uint8_t* done,
-                float gamma, int32_t B, float* dQ, float* loss, void* stream) {
+int evx_td_loss_w(const float* Q, const float* Qt, int32_t A, const int32_t* act, const float* rew,
+                  const uint8_t* done, float gamma, int32_t B, const float* w, float* dQ, float* loss, float* td_abs,
+                  void* stream) {
     if (B <= 0) return 0;
     if (B > 4096 * 256) return qfail(-22, "td_loss: batch too large");
     hipLaunchKernelGGL(evxq::td_loss_kernel, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream, Q, Qt, A, act, rew, done,
-                       gamma, B, dQ, loss);
+                       gamma, B, w, dQ, loss, td_abs);
     return qlaunch("td_loss");
+}
+
+int evx_td_loss(const float* Q, const float* Qt, int32_t A, const int32_t* act, const float* rew, const uint8_t* done,
+                float gamma, int32_t B, float* dQ, float* loss, void* stream) {
+    return evx_td_loss_w(Q, Qt, A, act, rew, done, gamma, B, nullptr, dQ, loss, nullptr, stream);
 }
 
 int evx_sumsq_norm(const float* g, int64_t n, float* scratch, int32_t scratch_elems, float* norm, void* stream) {

@@ -57,6 +57,9 @@ def qlib():
                                  C.c_int32, C.c_void_p]
         L.evx_td_loss.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_float,
                                   C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.evx_td_loss_w.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                    C.c_float, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                    C.c_void_p]
         L.evx_sumsq_norm.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
         L.evx_clip_adam.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p,
                                     C.c_float, C.POINTER(evx_adam), C.c_void_p]
@@ -315,8 +318,9 @@ class Learner:
         net = self.tnet if target else self.net
         return net.forward(x, mask if train else None, save=False, tag="act_")
 
-    def learn(self, s, a, r, done, s2, mask_online=None, mask_target=None):
-        """One DQNAgent.learn step on device tensors; returns the loss tensor (no host sync)."""
+    def learn(self, s, a, r, done, s2, mask_online=None, mask_target=None, weights=None, td_abs=None):
+        """One DQNAgent.learn step on device tensors; returns the loss tensor (no host sync).
+        weights / td_abs: prioritized replay's importance weights in, |TD error| out."""
         B = s.shape[0]
         if mask_online is None:
             mask_online = self.dropout_mask(B, "on")
@@ -326,15 +330,15 @@ class Learner:
         Qt = self.tnet.forward(s2, mask_target, save=False, tag="t_")
         dQ = self.net.ws.get("dq", (B, self.actions), torch.float32, self.device)
         L = qlib()
-        qcheck(L.evx_td_loss(_p(Q), _p(Qt), self.actions, _p(a), _p(r), _p(done), self.gamma, B, _p(dQ),
-                             _p(self.loss), _stream()), "td_loss")
+        qcheck(L.evx_td_loss_w(_p(Q), _p(Qt), self.actions, _p(a), _p(r), _p(done), self.gamma, B, _p(weights),
+                               _p(dQ), _p(self.loss), _p(td_abs), _stream()), "td_loss")
         self.net.backward(dQ, self.grads)
         if self.grad_hook is not None:
             self.grad_hook(self.grads.flat)
         self.step_optimizer()
         return self.loss
 
-    def learn_obs(self, lay_c, s_obs, a, r, done, s2_obs, B, update: bool = True):
+    def learn_obs(self, lay_c, s_obs, a, r, done, s2_obs, B, update: bool = True, weights=None, td_abs=None):
         """DQNAgent.learn on compact observations with the fused bf16 kernels:
         online forward (saves X, H1, H2), target forward, TD loss, backward, clip+Adam.
         update=False stops after the gradients (the caller runs step_optimizer later)."""
@@ -354,8 +358,8 @@ class Learner:
                                      dict(h1=H1, x=X, h2=H2, q=Q), self.fast_t, s2_obs,
                                      (self.seed, self.drop_stream + 1, DROPOUT_P), dict(h1=H1t, q=Qt))
         L = qlib()
-        qcheck(L.evx_td_loss(_p(Q), _p(Qt), self.actions, _p(a), _p(r), _p(done), self.gamma, B, _p(dQ),
-                             _p(self.loss), _stream()), "td_loss")
+        qcheck(L.evx_td_loss_w(_p(Q), _p(Qt), self.actions, _p(a), _p(r), _p(done), self.gamma, B, _p(weights),
+                               _p(dQ), _p(self.loss), _p(td_abs), _stream()), "td_loss")
         self.fast.backward(B, dQ, X, H1, H2, DROPOUT_P, dz2, dz1, self.grads)
         if self.grad_hook is not None:
             self.grad_hook(self.grads.flat)

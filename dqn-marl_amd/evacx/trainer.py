@@ -97,7 +97,9 @@ class VecTrainer:
                  kind: str = "mlp", precision: str = "bf16", batch: int = 4096, replay_capacity: int = 1 << 20,
                  lr: float = 1e-4, gamma: float = 0.99, epsilon: float = 1.0, epsilon_min: float = 0.02,
                  epsilon_decay: float = 0.9995, target_every: int = 1000, learner_seed: int = 0,
-                 grad_hook=None, learn_every: int = 1, lagged_learn: bool = False):
+                 grad_hook=None, learn_every: int = 1, lagged_learn: bool = False, replay: str = "uniform",
+                 prio_alpha: float = 0.6, prio_beta0: float = 0.4, prio_beta_steps: int = 100000,
+                 prio_eps: float = 1e-6):
         self.lay, self.E, self.R = layout, E, layout.R
         self.device = layout.device
         self.env = VecEnv(layout, E)
@@ -107,7 +109,17 @@ class VecTrainer:
         self.learner = Learner(kind=kind, device=self.device, lr=lr, gamma=gamma, precision=precision,
                                seed=learner_seed)
         self.learner.grad_hook = grad_hook
-        self.replay = Replay(replay_capacity, self.device)
+        # replay: "uniform" (DQNAgent.memory's random.sample) or "prioritized" (evacx.prio:
+        # device sum/min trees, importance-weighted loss, beta annealed to 1)
+        self.prio = replay == "prioritized"
+        if self.prio:
+            from .prio import PrioReplay
+            self.replay = PrioReplay(replay_capacity, self.device, alpha=prio_alpha, eps=prio_eps)
+        elif replay == "uniform":
+            self.replay = Replay(replay_capacity, self.device)
+        else:
+            raise ValueError(f"replay must be 'uniform' or 'prioritized', not {replay!r}")
+        self.prio_beta0, self.prio_beta_steps = prio_beta0, prio_beta_steps
         self.batch = batch
         self.epsilon, self.epsilon_min, self.epsilon_decay = epsilon, epsilon_min, epsilon_decay
         self.target_every, self.learn_every = target_every, learn_every
@@ -123,6 +135,10 @@ class VecTrainer:
                          a=torch.zeros(batch, dtype=torch.int32, device=self.device),
                          r=torch.zeros(batch, dtype=torch.float32, device=self.device),
                          done=torch.zeros(batch, dtype=torch.uint8, device=self.device))
+        if self.prio:
+            self.samp.update(idx=torch.zeros(batch, dtype=torch.int64, device=self.device),
+                             w=torch.zeros(batch, dtype=torch.float32, device=self.device),
+                             td=torch.zeros(batch, dtype=torch.float32, device=self.device))
         self.seed = learner_seed * 7919 + env_offset + 17
         self.t = 0
         self.learn_steps = 0
@@ -172,19 +188,30 @@ class VecTrainer:
         if phase != "update":
             if (self.replay.size if window is None else window[1]) < self.batch:
                 return None
-            if window is None:
+            w = td = None
+            if self.prio:
+                # the trees only hold exposed slots: the window is implicit (hidden slots have 0 mass)
+                beta = min(1.0, self.prio_beta0 + (1.0 - self.prio_beta0) * self.learn_steps / self.prio_beta_steps)
+                w, td = self.samp["w"], self.samp["td"]
+                self.replay.sample_prio(self.batch, beta, self.seed + 1, self.learn_steps * self.batch, self.samp,
+                                        self.samp["idx"], w)
+            elif window is None:
                 self.replay.sample(self.batch, self.seed + 1, self.learn_steps * self.batch, self.samp)
             else:
                 self.replay.sample_window(window[0], window[1], self.batch, self.seed + 1,
                                           self.learn_steps * self.batch, self.samp)
             if self.fast is not None:
                 loss = self.learner.learn_obs(self.lay.c, self.samp["s"], self.samp["a"], self.samp["r"],
-                                              self.samp["done"], self.samp["s2"], self.batch, update=phase == "all")
+                                              self.samp["done"], self.samp["s2"], self.batch, update=phase == "all",
+                                              weights=w, td_abs=td)
             else:
                 assert phase == "all", "split learn needs the fused bf16 MLP path"
                 s = self.env.expand_obs(torch.float32, self.samp["s"]).view(self.batch, 11, 11, 6)
                 s2 = self.env.expand_obs(torch.float32, self.samp["s2"]).view(self.batch, 11, 11, 6)
-                loss = self.learner.learn(s, self.samp["a"], self.samp["r"], self.samp["done"], s2)
+                loss = self.learner.learn(s, self.samp["a"], self.samp["r"], self.samp["done"], s2, weights=w,
+                                          td_abs=td)
+            if self.prio:
+                self.replay.update(self.samp["idx"], td, self.batch)
             if phase == "grads":
                 return loss
         else:
@@ -238,6 +265,8 @@ class VecTrainer:
                 self.lstream.wait_event(self.ev_push)
                 if ev_learn is not None:
                     ev_learn[0].record(self.lstream)
+                if self.prio:  # push t-1 visible, the slots push t overwrites hidden
+                    self.replay.expose(n_hide=self.n_agents)
                 if do_learn:
                     self.learn(window=win, phase="grads")
             self.ev_act.record(main)
@@ -256,6 +285,8 @@ class VecTrainer:
             ev_env[1].record(main)
         self.replay.push(self.obs_prev, self.env.obs, self.actions, self.env.reward, self.env.done,
                          self.n_agents, self.R, s2_term=self.env.obs_term)
+        if self.prio and not self.lagged:
+            self.replay.expose()
         mask = None
         if extra_reset is not None:
             mask = extra_reset & ~self.env.done.bool()  # made on main; read on the side stream

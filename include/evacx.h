@@ -176,6 +176,12 @@ int evx_colsum(const float *X, int64_t ld, int32_t M, int32_t N, float *out, int
  * dQ = d loss / d Q. Q, Qt: [B][A]. */
 int evx_td_loss(const float *Q, const float *Qt, int32_t A, const int32_t *act, const float *rew,
                 const uint8_t *done, float gamma, int32_t B, float *dQ, float *loss, void *stream);
+/* evx_td_loss with optional importance weights w [B] (prioritized replay: loss = mean(w (q - y)^2),
+ * dQ scaled by w) and optional td_abs [B] = |q - y| (the new priorities); w = td_abs = NULL is
+ * evx_td_loss. */
+int evx_td_loss_w(const float *Q, const float *Qt, int32_t A, const int32_t *act, const float *rew,
+                  const uint8_t *done, float gamma, int32_t B, const float *w, float *dQ, float *loss,
+                  float *td_abs, void *stream);
 /* ||g||_2 into norm[0] (clip_grad_norm_'s total norm) */
 int evx_sumsq_norm(const float *g, int64_t n, float *scratch, int32_t scratch_elems, float *norm, void *stream);
 /* g *= min(1, max_norm/(norm+1e-6)) (skipped if norm NULL) then one torch.optim.Adam step */
@@ -203,6 +209,44 @@ int evx_replay_sample(const evx_replay *rp, int64_t size, int32_t B, uint64_t se
 int evx_replay_sample_window(const evx_replay *rp, int64_t base, int64_t count, int32_t B, uint64_t seed,
                              uint64_t offset, evx_obs *s, evx_obs *s2, int32_t *a, float *r, uint8_t *done,
                              int64_t *idx_out, void *stream);
+/* ------------------------------------------- prioritized replay
+ * Proportional prioritized replay (Schaul et al. 2016) over the slots of an evx_replay
+ * ring; the reference samples uniformly (random.sample, agents/dqn_agent.py:132), so
+ * this is the build's own extension, pinned by oracle/prio_oracle.c. Two segment trees
+ * in heap layout over capacity C = 2^k slots (node n = child 2n (op) child 2n+1, root 1,
+ * slot i at leaf C + i): sums and minima of the leaf priorities p_i^alpha. Empty or
+ * hidden slots hold 0 in the sum tree and +inf in the min tree. New transitions get the
+ * largest leaf priority set so far (max_leaf, initially 1). */
+typedef struct {
+    int64_t capacity;   /* power of two, 2^10 <= C <= 2^26 */
+    double *sum;        /* [2C] */
+    double *mn;         /* [2C] */
+    double *max_leaf;   /* [1] */
+    int32_t *owner;     /* [C] scratch for evx_prio_update, all -1 (evx_prio_init sets it) */
+} evx_prio;
+
+/* all leaves empty (sum 0, min +inf), max_leaf = 1, owner = -1 */
+int evx_prio_init(const evx_prio *t, void *stream);
+/* Slots [pos, pos + n_new) mod C get priority max_leaf (newly pushed transitions) and
+ * slots [pos + n_new, pos + n_new + n_hide) mod C get priority 0 (hidden: about to be
+ * overwritten by a push running concurrently -- the lagged schedule); both trees are
+ * rebuilt over the touched leaf blocks. n_new + n_hide <= C. */
+int evx_prio_set_range(const evx_prio *t, int64_t pos, int64_t n_new, int64_t n_hide, void *stream);
+/* Leaf idx[k] = (td_abs[k] + eps)^alpha for k = 0..B-1 (a later k wins over an earlier
+ * one with the same slot, as a sequential loop), max_leaf updated, trees rebuilt. */
+int evx_prio_update(const evx_prio *t, const int64_t *idx, const float *td_abs, int32_t B, double eps,
+                    double alpha, void *stream);
+/* Stratified proportional sampling: for k = 0..B-1, u = (k + U_k) * (total / B) with U_k a
+ * 53-bit uniform from Philox4x32-10(counter offset + k, key seed); descend the sum tree
+ * (left if u < sum[left] or sum[right] <= 0, else u -= sum[left] and right). Gathers the
+ * transitions like evx_replay_sample and writes the importance weights
+ * w_k = (p_k / p_min)^(-beta) (= (N P(k))^-beta / max_j (N P(j))^-beta). */
+int evx_prio_sample(const evx_replay *rp, const evx_prio *t, int32_t B, double beta, uint64_t seed,
+                    uint64_t offset, evx_obs *s, evx_obs *s2, int32_t *a, float *r, uint8_t *done,
+                    int64_t *idx_out, float *w_out, void *stream);
+
+const char *evx_prio_last_error(void);
+
 int evx_gather_obs(const evx_obs *src, const int64_t *idx, int32_t n, evx_obs *dst, void *stream);
 /* DQNNetwork conv layers (agents/dqn_agent.py:22-24) as im2col + GEMM on 11x11 maps */
 int evx_im2col3x3(const float *x, int32_t B, int32_t C, int32_t nhwc, float *cols, void *stream);

@@ -175,3 +175,42 @@ def run_batch(layout: Layout, envs, steps, actions, nthreads=0):
 def pairwise_sum(a):
     a = np.ascontiguousarray(a, np.float64)
     return lib().orc_pairwise_sum(_p(a), len(a))
+
+
+def philox4x32_10(ctr, key):
+    """Philox4x32-10 block (prio_oracle.c) -> 4 uint32 words."""
+    c = np.ascontiguousarray(ctr, np.uint32)
+    k = np.ascontiguousarray(key, np.uint32)
+    out = np.zeros(4, np.uint32)
+    lib().orc_philox4x32_10(_p(c), _p(k), _p(out))
+    return out
+
+
+class PrioTrees:
+    """Sequential CPU restatement of evx_prio_* (prio_oracle.c): sum / min trees in heap
+    layout, max leaf priority; the checker of the GPU prioritized replay."""
+
+    def __init__(self, capacity):
+        assert capacity & (capacity - 1) == 0
+        self.C = int(capacity)
+        self.sum = np.zeros(2 * self.C, np.float64)
+        self.mn = np.zeros(2 * self.C, np.float64)
+        self.max_leaf = np.zeros(1, np.float64)
+        lib().orc_prio_init(_p(self.sum), _p(self.mn), C.c_int64(self.C), _p(self.max_leaf))
+
+    def set_range(self, pos, n_new, n_hide=0):
+        lib().orc_prio_set_range(_p(self.sum), _p(self.mn), C.c_int64(self.C), _p(self.max_leaf),
+                                 C.c_int64(pos), C.c_int64(n_new), C.c_int64(n_hide))
+
+    def update(self, idx, td_abs, eps, alpha):
+        idx = np.ascontiguousarray(idx, np.int64)
+        td = np.ascontiguousarray(td_abs, np.float32)
+        lib().orc_prio_update(_p(self.sum), _p(self.mn), C.c_int64(self.C), _p(self.max_leaf), _p(idx), _p(td),
+                              C.c_int(len(idx)), C.c_double(eps), C.c_double(alpha))
+
+    def sample(self, B, beta, seed, offset):
+        idx = np.zeros(B, np.int64)
+        w = np.zeros(B, np.float32)
+        lib().orc_prio_sample(_p(self.sum), _p(self.mn), C.c_int64(self.C), C.c_int(B), C.c_double(beta),
+                              C.c_uint64(seed), C.c_uint64(offset), _p(idx), _p(w))
+        return idx, w

@@ -215,3 +215,18 @@ def test_gpu_vs_oracle_dense_conflicts():
     _need_gpu()
     from evacx.layout import synthetic
     _oracle_pair(synthetic(24, 20, 4), 380, E=16, steps=50, check_every=1)
+
+
+def test_gpu_vs_oracle_cfg4_256_single_robot():
+    """BASELINE cfg4 geometry: 256x256 grid, 9102 people, one robot (two envs per
+    workgroup: the layout's LDS does not fit four)."""
+    _need_gpu()
+    from evacx.layout import synthetic
+    _oracle_pair(synthetic(256, 256, 1), 9102, E=3, steps=24, check_every=8, thmap=False)
+
+
+def test_gpu_vs_oracle_cfg5_128_r32():
+    """BASELINE cfg5 geometry: 128x128, 2276 people, 32 robots; heavy envs on 4 waves."""
+    _need_gpu()
+    from evacx.layout import synthetic
+    _oracle_pair(synthetic(128, 128, 32), 2276, E=5, steps=30, check_every=6, wide=True, auto_reset=True)
