@@ -48,8 +48,10 @@ def bytes_per_env_step(P, R, G):
     return 40 * P + 8 * RW + 2 * 2 * 2500 + R * 44 + 48
 
 
-def qnet_flops(n_act, B, hidden=512, in_dim=726, actions=5):
-    """Dense MLP FLOPs: act forward over n_act rows + learn (online fwd, target fwd, backward dW+dX)."""
+def qnet_flops(n_act, B, hidden=512, in_dim=484, actions=5):
+    """Dense MLP FLOPs: act forward over n_act rows + learn (online fwd, target fwd, backward dW+dX).
+    in_dim 484: the live inputs of the 726 (channel 0 is identically zero, channel 5 a constant
+    folded into the bias; csrc/qmlp.hip)."""
     fwd = 2 * (in_dim * hidden + hidden * (hidden // 2) + (hidden // 2) * actions)
     bwd = 2 * fwd - 2 * in_dim * hidden  # no dX for the input layer
     return n_act * fwd + B * (2 * fwd + bwd)

@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include <algorithm>
 
@@ -34,8 +35,16 @@ namespace evxm {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-constexpr int HID = 512, HID2 = 256, NACT = 5, K1 = 726, K1P = 768;  // K padded to 128 cells
-constexpr int RM = 64;  // rows per workgroup
+constexpr int HID = 512, HID2 = 256, NACT = 5, K1 = 726, NCELL = 121;
+// fc1's compact K: 4 features per cell (occ, danger, barrier, exit = the reference's
+// channels 1-4), 128 cells (>= 121 zero). Channel 0 is identically 0 (space / max(space)
+// with max = inf) and channel 5 is the constant centre one-hot, folded into the bias:
+// b1c = b1 + bf16(W1[:, CENTRE_COL]). 726 -> 512 contraction length, same products.
+constexpr int K1P = 512, KC1 = 32, NKC1 = K1P / KC1;
+constexpr int CENTRE_COL = 60 * 6 + 5;
+constexpr int RM = 64;  // rows per workgroup (fc23, backward)
+// reference column (of the 726) of compact feature k < 4 * NCELL
+__host__ __device__ __forceinline__ int ref_col(int k) { return (k >> 2) * 6 + (k & 3) + 1; }
 
 __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
     h ^= h >> 16;
@@ -77,7 +86,7 @@ __device__ __forceinline__ float u01(uint32_t v) { return (float)(v >> 8) * (1.0
 // 16-wide step s) holds lane l's 8 values (column 32t + (l&31), k = kc*KC + 16s +
 // 8(l>>5) .. +7) at l*8, so a wave's operand load is one contiguous 1-KB read.
 __host__ __device__ __forceinline__ size_t w1_tile(int t, int kc, int s) {
-    return ((size_t)(t * (K1P / 48) + kc) * 3 + s) * 512;
+    return ((size_t)(t * NKC1 + kc) * 2 + s) * 512;
 }
 __host__ __device__ __forceinline__ size_t w2_tile(int t, int kc, int s) {
     return ((size_t)(t * (HID / 32) + kc) * 2 + s) * 512;
@@ -93,10 +102,11 @@ struct Fwd {
     // layout (EvacuationEnv._get_state inputs)
     const uint8_t* cellinfo;
     const float* danger;
-    int L, W, ox0, oy0, OX, OY, exit_x, exit_y;
+    const uint32_t* feat;  // evx_layout.obs_feat: static per-cell features, padded grid per fire step
+    int L, W, ox0, oy0, OX, OY, exit_x, exit_y, t_max;
     // parameters
-    const __bf16* w1;  // [512][768] in w1_tile order
-    const float* b1;
+    const __bf16* w1;  // [512][512] compact K, w1_tile order
+    const float* b1;   // b1c: fc1.bias with the centre channel folded in
     const __bf16* w2;  // [256][512] in w2_tile order
     const float* b2;
     const float* w3;   // [5][256]
@@ -106,7 +116,7 @@ struct Fwd {
     float drop_scale;
     // outputs
     __bf16* h1;  // [N][512]
-    __bf16* x;   // [N][768] or null
+    __bf16* x;   // [N][512] compact K, or null
     float* h2;   // [N][256] or null
     float* q;    // [N][5] or null
     int32_t* actions;
@@ -114,160 +124,155 @@ struct Fwd {
     uint64_t act_seed, act_offset;
 };
 
-// _get_state of one cell around (cx, cy) (envs/evacuation_env.py:84-120, as
-// obs_expand_kernel evaluates it), packed: bf16(danger) | occ<<16 | barrier<<17 |
-// exit<<18 | centre<<19 (channel 0 is all zeros); cells >= 121 are K padding (0).
-__device__ __forceinline__ uint32_t cell_pack(const Fwd& a, const evx_obs& ob, int c, uint32_t ci, float dg) {
-    if (c >= 121) return 0u;
-    const int i = c / 11, j = c - 11 * (c / 11);
-    const int mx = ob.cx + i - 5, my = ob.cy + j - 5;
-    const bool inb = mx >= 0 && mx <= a.L + 1 && my >= 0 && my <= a.W + 1;
-    const bool valid = mx >= 1 && mx <= a.L && my >= 1 && my <= a.W && (ci & 1u);
-    uint32_t v = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)dg);
-    v |= ((ob.occ[c >> 5] >> (c & 31)) & 1u) << 16;
-    v |= ((!valid || (inb && ((ci >> 2) & 1u))) ? 1u : 0u) << 17;
-    v |= ((mx == a.exit_x && my == a.exit_y) ? 1u : 0u) << 18;
-    v |= ((i == 5 && j == 5) ? 1u : 0u) << 19;
-    return v;
+// One row's window in the static feature map (evx_layout.obs_feat): base index of
+// window cell (0, 0) = map cell (cx - 5, cy - 5) at the row's fire step. Rows past N
+// and out-of-range centres are clamped into the map (their outputs are not stored).
+__device__ __forceinline__ int feat_base(const Fwd& a, const evx_obs& ob) {
+    const int PX = a.L + 2 + 2 * EVX_FEAT_PAD, PY = a.W + 2 + 2 * EVX_FEAT_PAD;
+    const int cx = min(max(ob.cx, 0), a.L + 1), cy = min(max(ob.cy, 0), a.W + 1);
+    const int fs = min(max(ob.fire_step, 0), a.t_max);
+    return (fs * PX + cx + EVX_FEAT_PAD - 5) * PY + cy + EVX_FEAT_PAD - 5;
 }
-// the table reads of cell c (cellinfo byte, danger value), issued ahead of cell_pack
-__device__ __forceinline__ void cell_reads(const Fwd& a, const evx_obs& ob, int c, uint32_t& ci, float& dg) {
-    const int cc = c < 121 ? c : 0;
-    const int i = cc / 11, j = cc - 11 * (cc / 11);
-    const int mx = ob.cx + i - 5, my = ob.cy + j - 5;
-    const bool inb = mx >= 0 && mx <= a.L + 1 && my >= 0 && my <= a.W + 1;
-    const int ti = mx - a.ox0, tj = my - a.oy0;
-    ci = 0u;
-    dg = 0.f;
-    if (inb) ci = a.cellinfo[mx * (a.W + 2) + my];
-    if (ti >= 0 && ti < a.OX && tj >= 0 && tj < a.OY) dg = a.danger[((size_t)ob.fire_step * a.OX + ti) * a.OY + tj];
+// map offset of window cell c = 11 i + j (c < 128; (c * 373) >> 12 == c / 11 there)
+__device__ __forceinline__ int feat_off(const Fwd& a, int c) {
+    const int i = (c * 373) >> 12;
+    return c + i * (a.W + 2 + 2 * EVX_FEAT_PAD - 11);
 }
-// 6 bf16 features of a packed cell, as three 16-bit pairs (lo | hi << 16)
-__device__ __forceinline__ void unpack6(uint32_t v, uint32_t& p01, uint32_t& p23, uint32_t& p45) {
+// _get_state of window cell c (envs/evacuation_env.py:84-120, as obs_expand_kernel
+// evaluates it) as fc1's 4 compact bf16 features, two per word: (occ | danger << 16,
+// barrier | exit << 16), from the cell's static feature word and the occupancy bits;
+// cells >= 121 are K padding (0). Branch-free.
+__device__ __forceinline__ uint2 cell_feat(const evx_obs& ob, int c, uint32_t v) {
     const uint32_t one = 0x3f80u;  // bf16(1.0)
-    p01 = ((v >> 16) & 1u) ? (one << 16) : 0u;                         // ch0 = 0, ch1 = occ
-    p23 = (v & 0xffffu) | ((((v >> 17) & 1u) ? one : 0u) << 16);       // ch2 = danger, ch3 = barrier
-    p45 = (((v >> 18) & 1u) ? one : 0u) | ((((v >> 19) & 1u) ? one : 0u) << 16);  // ch4 = exit, ch5 = centre
+    const int q = c >> 5;          // no dynamic index into ob.occ (it would live in scratch)
+    const uint32_t ow = q == 0 ? ob.occ[0] : q == 1 ? ob.occ[1] : q == 2 ? ob.occ[2] : ob.occ[3];
+    const uint32_t occ = ((ow >> (c & 31)) & 1u) * one;
+    uint32_t w0 = occ | (v << 16);
+    uint32_t w1 = ((v >> 16) & 1u) * one | (((v >> 17) & 1u) * one) << 16;
+    w0 = c < NCELL ? w0 : 0u;
+    w1 = c < NCELL ? w1 : 0u;
+    return make_uint2(w0, w1);
 }
 
 // ------------------------------------------------------------------ fc1
-// K chunks of 48 = 8 whole cells: thread (row tid>>2, cell pair tid&3) expands two
-// cells per chunk. NTW = 32-column tiles per wave: 2 -> a workgroup covers 256
-// columns, grid.y = 2 (act batches); 1 -> 128 columns, grid.y = 4 (learner batches).
-template <int NTW>
-__global__ __launch_bounds__(256, 2) void qfc1_kernel(Fwd a0, Fwd a1) {
+// Workgroup tile: 32*MT rows x 128*NTW*NWV/4 columns; wave w owns all rows and
+// columns [32*NTW*w, +32*NTW) of it, so every B fragment (global, L2-resident, one
+// 1-KB block per wave load) feeds MT MFMAs. K in 16 chunks of 32 (8 cells): each
+// thread expands 2 cells of one row per chunk from their static feature words
+// (loaded two chunks ahead) into a double-buffered LDS A tile, one barrier per
+// chunk. Epilogue: bias, ReLU, dropout, bf16, staged per 32-row slab through LDS so
+// H1 leaves in 16-B row segments. Act batches: <4, 2, 8> (128 rows x all 512
+// columns: every row expanded once); learner batches <2, 1, 4> (64 x 128).
+template <int MT, int NTW, int NWV>
+__global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void qfc1_kernel(Fwd a0, Fwd a1) {
     const Fwd& a = blockIdx.z ? a1 : a0;  // two independent problems in one launch (online / target)
-    constexpr int KC = 48, NKC = K1P / KC, APAD = KC + 8;
-    __shared__ __attribute__((aligned(16))) __bf16 As[2][RM][APAD];
-    __shared__ uint32_t Fs[RM][129];  // packed cells of the workgroup's rows
+    constexpr int NT = 64 * NWV, RT = 32 * MT, NW = 32 * NTW * NWV;
+    constexpr int CPT = 8 * RT / NT, TPR = 8 / CPT;  // cells per thread and chunk, threads per row
+    static_assert(CPT == 2, "generator: one 16-B A store per thread and chunk");
+    constexpr int APAD = KC1 + 8, CPAD = NW + 8;
+    constexpr int ABYTES = 2 * RT * APAD * 2, CBYTES = 32 * CPAD * 2;
+    __shared__ __attribute__((aligned(16))) char smem[ABYTES > CBYTES ? ABYTES : CBYTES];
+    auto As = reinterpret_cast<__bf16 (*)[RT][APAD]>(smem);
+    auto Cs = reinterpret_cast<__bf16 (*)[CPAD]>(smem);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
-    const int m0 = blockIdx.x * RM;
-    const int ncol0 = blockIdx.y * (128 * NTW) + w * (32 * NTW);
-    const int gr = tid >> 2, gp = tid & 3;  // generator: row, cell pair
+    const int m0 = blockIdx.x * RT;
+    const int ncol0 = blockIdx.y * NW + w * (32 * NTW);
+    const int gr = tid / TPR, gc = (tid % TPR) * CPT;
     const bool rowok = m0 + gr < a.N;
     evx_obs ob;
     if (rowok) {
         ob = a.obs[m0 + gr];
     } else {
-        ob = evx_obs{{0u, 0u, 0u, 0u}, -1000, -1000, 0, 0};
+        ob = evx_obs{{0u, 0u, 0u, 0u}, 0, 0, 0, 0};
     }
     const bool wx = a.x && rowok && blockIdx.y == 0;
-    {  // expand every cell of the row once: cells gp, gp+4, ..., 32 table reads in flight
-        uint32_t ci[32];
-        float dg[32];
+    const uint32_t* fb = a.feat + feat_base(a, ob);
+    uint32_t fv[CPT];
+    auto reads = [&](int kc) {
 #pragma unroll
-        for (int t = 0; t < 32; t++) cell_reads(a, ob, gp + 4 * t, ci[t], dg[t]);
+        for (int t = 0; t < CPT; t++) fv[t] = fb[feat_off(a, kc * 8 + gc + t)];
+    };
+    auto stash = [&](int buf, int kc) {
+        const uint2 f0 = cell_feat(ob, kc * 8 + gc, fv[0]), f1 = cell_feat(ob, kc * 8 + gc + 1, fv[1]);
+        const uint4 v = make_uint4(f0.x, f0.y, f1.x, f1.y);
+        *reinterpret_cast<uint4*>(&As[buf][gr][gc * 4]) = v;
+        if (wx) *reinterpret_cast<uint4*>(a.x + (size_t)(m0 + gr) * K1P + kc * KC1 + gc * 4) = v;
+    };
+    f32x16 acc[MT][NTW];
 #pragma unroll
-        for (int t = 0; t < 32; t++) Fs[gr][gp + 4 * t] = cell_pack(a, ob, gp + 4 * t, ci[t], dg[t]);
-    }
-    f32x16 acc[2][NTW];
-#pragma unroll
-    for (int i = 0; i < 2; i++)
+    for (int i = 0; i < MT; i++)
 #pragma unroll
         for (int j = 0; j < NTW; j++)
 #pragma unroll
             for (int r = 0; r < 16; r++) acc[i][j][r] = 0.f;
-    bf16x8 bc[NTW][3], bn[NTW][3];
-    auto loadB = [&](int kc, bf16x8 (&b)[NTW][3]) {
+    bf16x8 bc[NTW][2], bn[NTW][2];
+    auto loadB = [&](int kc, bf16x8 (&b)[NTW][2]) {
 #pragma unroll
         for (int nt = 0; nt < NTW; nt++) {
             const int n = ncol0 + nt * 32;
 #pragma unroll
-            for (int s = 0; s < 3; s++)  // tiled: one contiguous 1-KB block per wave load
+            for (int s = 0; s < 2; s++)
                 b[nt][s] = *reinterpret_cast<const bf16x8*>(a.w1 + w1_tile(n >> 5, kc, s) + lane * 8);
         }
     };
-    struct Gen12 {
-        uint2 w[3];
-    };
-    auto gen12 = [&](int kc) -> Gen12 {  // features of cells kc*8 + 2gp, +1 from the packed table
-        uint32_t a01, a23, a45, b01, b23, b45;
-        unpack6(Fs[gr][kc * 8 + 2 * gp], a01, a23, a45);
-        unpack6(Fs[gr][kc * 8 + 2 * gp + 1], b01, b23, b45);
-        Gen12 g;
-        g.w[0] = make_uint2(a01, a23);
-        g.w[1] = make_uint2(a45, b01);
-        g.w[2] = make_uint2(b23, b45);
-        return g;
-    };
-    auto stash = [&](int buf, int kc, const Gen12& g) {
-        uint2* dst = reinterpret_cast<uint2*>(&As[buf][gr][gp * 12]);
-#pragma unroll
-        for (int t = 0; t < 3; t++) dst[t] = g.w[t];
-        if (wx) {
-            uint2* gx = reinterpret_cast<uint2*>(a.x + (size_t)(m0 + gr) * K1P + kc * KC + gp * 12);
-#pragma unroll
-            for (int t = 0; t < 3; t++) gx[t] = g.w[t];
-        }
-    };
-    __syncthreads();  // packed cells complete
-    stash(0, 0, gen12(0));
+    reads(0);
+    stash(0, 0);
+    reads(1);
     loadB(0, bc);
     __syncthreads();
-    for (int kc = 0; kc < NKC; kc++) {
+    for (int kc = 0; kc < NKC1; kc++) {
         const int buf = kc & 1;
-        Gen12 gnext;
-        if (kc + 1 < NKC) {
-            gnext = gen12(kc + 1);
-            loadB(kc + 1, bn);
-        }
+        if (kc + 1 < NKC1) loadB(kc + 1, bn);
 #pragma unroll
-        for (int mt = 0; mt < 2; mt++)
+        for (int s = 0; s < 2; s++)
 #pragma unroll
-            for (int s = 0; s < 3; s++) {
+            for (int mt = 0; mt < MT; mt++) {
                 const bf16x8 av = *reinterpret_cast<const bf16x8*>(&As[buf][mt * 32 + (lane & 31)][s * 16 + 8 * h]);
 #pragma unroll
                 for (int nt = 0; nt < NTW; nt++)
                     acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bc[nt][s], acc[mt][nt], 0, 0, 0);
             }
-        if (kc + 1 < NKC) {
-            stash(buf ^ 1, kc + 1, gnext);
+        if (kc + 1 < NKC1) {
+            stash(buf ^ 1, kc + 1);
+            if (kc + 2 < NKC1) reads(kc + 2);
 #pragma unroll
-            for (int nt = 0; nt < NTW; nt++)
-#pragma unroll
-                for (int s = 0; s < 3; s++) bc[nt][s] = bn[nt][s];
+            for (int nt = 0; nt < NTW; nt++) {
+                bc[nt][0] = bn[nt][0];
+                bc[nt][1] = bn[nt][1];
+            }
         }
         __syncthreads();
     }
-    // epilogue: bias, ReLU, dropout, bf16
+    // epilogue: bias (centre channel folded in), ReLU, dropout, bf16
+    float bias[NTW];
 #pragma unroll
-    for (int nt = 0; nt < NTW; nt++) {
-        const int col = ncol0 + nt * 32 + (lane & 31);
-        const float bias = a.b1[col];
+    for (int nt = 0; nt < NTW; nt++) bias[nt] = a.b1[ncol0 + nt * 32 + (lane & 31)];
 #pragma unroll
-        for (int mt = 0; mt < 2; mt++)
+    for (int mt = 0; mt < MT; mt++) {
+        if (mt) __syncthreads();  // the previous slab has been stored
 #pragma unroll
-            for (int r = 0; r < 16; r++) {
-                const int row = m0 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (row >= a.N) continue;
-                float v = acc[mt][nt][r] + bias;
+        for (int r = 0; r < 16; r++) {
+            const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;
+            const uint32_t rh = a.drop_thresh ? drop_row(a.drop_seed, a.drop_stream, (uint32_t)(m0 + mt * 32 + rl)) : 0u;
+#pragma unroll
+            for (int nt = 0; nt < NTW; nt++) {
+                const int cl = w * (32 * NTW) + nt * 32 + (lane & 31);
+                float v = acc[mt][nt][r] + bias[nt];
                 v = v > 0.f ? v : 0.f;
-                if (a.drop_thresh) {
-                    const uint32_t rh = drop_row(a.drop_seed, a.drop_stream, (uint32_t)row);
-                    v = drop_keep(rh, (uint32_t)col, a.drop_thresh) ? v * a.drop_scale : 0.f;
-                }
-                a.h1[(size_t)row * HID + col] = (__bf16)v;
+                if (a.drop_thresh)
+                    v = drop_keep(rh, (uint32_t)(blockIdx.y * NW + cl), a.drop_thresh) ? v * a.drop_scale : 0.f;
+                Cs[rl][cl] = (__bf16)v;
             }
+        }
+        __syncthreads();
+        constexpr int SEG = NW / 8;  // 16-B segments per row
+        for (int i = tid; i < 32 * SEG; i += NT) {
+            const int rl = i / SEG, cc = (i - rl * SEG) * 8;
+            const int row = m0 + mt * 32 + rl;
+            if (row < a.N)
+                *reinterpret_cast<uint4*>(a.h1 + (size_t)row * HID + blockIdx.y * NW + cc) =
+                    *reinterpret_cast<const uint4*>(&Cs[rl][cc]);
+        }
     }
 }
 
@@ -399,18 +404,20 @@ __global__ __launch_bounds__(256, 2) void qfc23_kernel(Fwd a0, Fwd a1) {
     }
 }
 
-// f32 parameters -> bf16 copies: W1 (K padded, w1_tile order), W2 (w2_tile order),
-// W2^T (w2t_tile order, the backward's operand)
-__global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ w1, const float* __restrict__ w2,
-                                                   __bf16* __restrict__ w1b, __bf16* __restrict__ w2b,
+// f32 parameters -> bf16 copies: W1 (compact K, w1_tile order) + the folded fc1 bias,
+// W2 (w2_tile order), W2^T (w2t_tile order, the backward's operand)
+__global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ w1, const float* __restrict__ b1,
+                                                   const float* __restrict__ w2, __bf16* __restrict__ w1b,
+                                                   float* __restrict__ b1c, __bf16* __restrict__ w2b,
                                                    __bf16* __restrict__ w2t) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i < HID * K1P) {  // destination index -> (tile, chunk, step, lane, j)
         const int j = i & 7, l = (i >> 3) & 63, blk = i >> 9;
-        const int s = blk % 3, kc = (blk / 3) % (K1P / 48), t = blk / (3 * (K1P / 48));
-        const int n = t * 32 + (l & 31), k = kc * 48 + s * 16 + 8 * (l >> 5) + j;
-        w1b[i] = (__bf16)(k < K1 ? w1[n * K1 + k] : 0.f);
+        const int s = blk & 1, kc = (blk >> 1) % NKC1, t = blk / (2 * NKC1);
+        const int n = t * 32 + (l & 31), k = kc * KC1 + s * 16 + 8 * (l >> 5) + j;
+        w1b[i] = (__bf16)(k < 4 * NCELL ? w1[n * K1 + ref_col(k)] : 0.f);
     }
+    if (i < HID) b1c[i] = b1[i] + (float)(__bf16)w1[i * K1 + CENTRE_COL];
     if (i < HID2 * HID) {
         const int j = i & 7, l = (i >> 3) & 63, blk = i >> 9;
         const int s = blk % 2, kc = (blk / 2) % (HID / 32), t = blk / (2 * (HID / 32));
@@ -429,14 +436,16 @@ __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ w1,
 //   fc3: dW3 = dQ^T H2, db3 = sum dQ, dZ2 = (dQ W3) * [H2 > 0], db2 = sum dZ2
 //   fc2: dW2 = dZ2^T H1, dZ1 = (dZ2 W2) * scale * [H1 > 0], db1 = sum dZ1
 //        ([H1 > 0] is keep AND relu' since H1 = keep * scale * relu(z))
-//   fc1: dW1 = dZ1^T X
+//   fc1: dW1 = dZ1^T X over the compact K, scattered to the reference's columns;
+//        the constant centre column (channel 5, x = 1) gets sum dZ1 = db1, channel 0
+//        (x = 0) gets nothing
 // Gradients accumulate with f32 atomics into a zeroed buffer (split-K).
 struct Bwd {
     int B;
     const float* dq;    // [B][5]
     const float* h2;    // [B][256]
     const __bf16* h1;   // [B][512]
-    const __bf16* x;    // [B][768]
+    const __bf16* x;    // [B][512] compact K (qfc1's X)
     const float* w3;    // [5][256]
     const __bf16* w2t;  // fc2.weight^T in w2t_tile order
     float scale;
@@ -552,16 +561,20 @@ __global__ __launch_bounds__(256, 2) void qdz1_kernel(Bwd a) {
             cs += v;
         }
     cs += __shfl_xor(cs, 32, 64);  // the two row halves of the column
-    if (h == 0) atomicAdd(&a.gb1[col], cs);
+    if (h == 0) {
+        atomicAdd(&a.gb1[col], cs);
+        atomicAdd(&a.gw1[(size_t)col * K1 + CENTRE_COL], cs);  // d/dW1 of the constant centre input
+    }
 }
 
 // C[m][n] += sum_k A[k][m] B[k][n] (both operands K-major bf16), 128x128 tiles of
 // 4 waves (2x2 of 64x64), K chunks of 32 staged transposed in LDS; gridDim.z splits
-// K and the partial tiles are added with f32 atomics. Columns n >= Nc are skipped.
+// K and the partial tiles are added with f32 atomics. Columns n >= Nc are skipped;
+// remap: column n goes to ref_col(n) (fc1's compact K -> the reference's 726).
 constexpr int TT = 128, TKC = 32, TPAD = TKC + 8;
 __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const __bf16* __restrict__ A, int lda,
                                                          const __bf16* __restrict__ Bm, int ldb, int K, int M, int Nc,
-                                                         int kper, float* __restrict__ C, int ldc) {
+                                                         int kper, float* __restrict__ C, int ldc, int remap) {
     __shared__ __attribute__((aligned(16))) __bf16 As[TT][TPAD];
     __shared__ __attribute__((aligned(16))) __bf16 Bs[TT][TPAD];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
@@ -633,12 +646,13 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const __bf16* __restric
     for (int j = 0; j < 2; j++) {
         const int n = n0 + wn * 64 + j * 32 + (lane & 31);
         if (n >= Nc) continue;
+        const int nc = remap ? ref_col(n) : n;
 #pragma unroll
         for (int i = 0; i < 2; i++)
 #pragma unroll
             for (int r = 0; r < 16; r++) {
                 const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (m < M) atomicAdd(&C[(size_t)m * ldc + n], acc[i][j][r]);
+                if (m < M) atomicAdd(&C[(size_t)m * ldc + nc], acc[i][j][r]);
             }
     }
 }
@@ -674,24 +688,29 @@ extern "C" {
 
 const char* evx_qmlp_last_error(void) { return m_err; }
 
-int evx_qmlp_pack(const float* w1, const float* w2, uint16_t* w1b, uint16_t* w2b, uint16_t* w2t, void* stream) {
-    if (!w1 || !w2 || !w1b || !w2b) return mfail(-22, "qmlp_pack: NULL argument");
+int evx_qmlp_pack(const float* w1, const float* b1, const float* w2, uint16_t* w1b, float* b1c, uint16_t* w2b,
+                  uint16_t* w2t, void* stream) {
+    if (!w1 || !b1 || !w2 || !w1b || !b1c || !w2b) return mfail(-22, "qmlp_pack: NULL argument");
     const int n = evxm::HID * evxm::K1P;
-    hipLaunchKernelGGL(evxm::pack_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, w1, w2,
-                       reinterpret_cast<__bf16*>(w1b), reinterpret_cast<__bf16*>(w2b), reinterpret_cast<__bf16*>(w2t));
+    hipLaunchKernelGGL(evxm::pack_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, w1, b1, w2,
+                       reinterpret_cast<__bf16*>(w1b), b1c, reinterpret_cast<__bf16*>(w2b),
+                       reinterpret_cast<__bf16*>(w2t));
     return mlaunch("qmlp_pack");
 }
 
 static int make_fwd(const evx_layout* lay, const evx_obs* obs, int32_t n, const evx_qmlp_params* p,
                     const evx_qmlp_dropout* drop, const evx_qmlp_fwd_out* out, evxm::Fwd& a) {
     if (!lay || !obs || !p || !out) return mfail(-22, "qmlp_forward: NULL argument");
-    if (!p->w1 || !p->b1 || !p->w2 || !p->b2 || !p->w3 || !p->b3) return mfail(-22, "qmlp_forward: missing parameter");
+    if (!p->w1 || !p->b1c || !p->w2 || !p->b2 || !p->w3 || !p->b3) return mfail(-22, "qmlp_forward: missing parameter");
     if (!out->h1) return mfail(-22, "qmlp_forward: h1 buffer required");
-    if (!lay->danger_o32 || !lay->cellinfo) return mfail(-22, "qmlp_forward: layout tables missing");
+    if (!lay->danger_o32 || !lay->cellinfo || !lay->obs_feat)
+        return mfail(-22, "qmlp_forward: layout tables missing (obs_feat)");
     a.N = n;
     a.obs = obs;
     a.cellinfo = lay->cellinfo;
     a.danger = lay->danger_o32;
+    a.feat = lay->obs_feat;
+    a.t_max = lay->t_max;
     a.L = lay->L;
     a.W = lay->W;
     a.ox0 = lay->ox0;
@@ -701,7 +720,7 @@ static int make_fwd(const evx_layout* lay, const evx_obs* obs, int32_t n, const 
     a.exit_x = lay->exit_x;
     a.exit_y = lay->exit_y;
     a.w1 = reinterpret_cast<const __bf16*>(p->w1);
-    a.b1 = p->b1;
+    a.b1 = p->b1c;
     a.w2 = reinterpret_cast<const __bf16*>(p->w2);
     a.b2 = p->b2;
     a.w3 = p->w3;
@@ -724,10 +743,11 @@ static int make_fwd(const evx_layout* lay, const evx_obs* obs, int32_t n, const 
 
 static int launch_fwd(const evxm::Fwd& a0, const evxm::Fwd& a1, int32_t n, int pairs, bool fc23, hipStream_t st) {
     const unsigned blocks = (unsigned)((n + evxm::RM - 1) / evxm::RM);
-    if (blocks * pairs >= 512)  // enough row tiles to fill the chip: workgroups of 64 rows x 256 columns
-        hipLaunchKernelGGL(evxm::qfc1_kernel<2>, dim3(blocks, 2, pairs), dim3(256), 0, st, a0, a1);
+    const unsigned big = (unsigned)((n + 127) / 128);
+    if (big * pairs >= 384)  // enough 128-row tiles (all 512 columns each) to fill the chip
+        hipLaunchKernelGGL((evxm::qfc1_kernel<4, 2, 8>), dim3(big, 1, pairs), dim3(512), 0, st, a0, a1);
     else
-        hipLaunchKernelGGL(evxm::qfc1_kernel<1>, dim3(blocks, 4, pairs), dim3(256), 0, st, a0, a1);
+        hipLaunchKernelGGL((evxm::qfc1_kernel<2, 1, 4>), dim3(blocks, 4, pairs), dim3(256), 0, st, a0, a1);
     int rc = mlaunch("qfc1");
     if (rc || !fc23) return rc;
     hipLaunchKernelGGL(evxm::qfc23_kernel, dim3(blocks, 1, pairs), dim3(256), 0, st, a0, a1);
@@ -791,7 +811,7 @@ int evx_qmlp_backward(const evx_qmlp_params* p, int32_t B, const float* dq, cons
     hipLaunchKernelGGL(evxm::qbwd3_kernel, dim3((unsigned)((B + evxm::R3 - 1) / evxm::R3)), dim3(256), 0, st, a);
     hipLaunchKernelGGL(evxm::qdz1_kernel, dim3((unsigned)((B + evxm::RM - 1) / evxm::RM), evxm::HID / 128), dim3(256),
                        0, st, a);
-    // dW2 = dZ2^T H1 (256 x 512), dW1 = dZ1^T X (512 x 726); K = B split over gridDim.z
+    // dW2 = dZ2^T H1 (256 x 512), dW1 = dZ1^T X (512 x 484 compact -> 726); K = B split over gridDim.z
     auto ksplit = [&](int tiles) {
         int S = (256 + tiles - 1) / tiles;
         int kper = (B + S - 1) / S;
@@ -802,13 +822,13 @@ int evx_qmlp_backward(const evx_qmlp_params* p, int32_t B, const float* dq, cons
         const int kper = ksplit(8);
         hipLaunchKernelGGL(evxm::gemm_tn_kernel, dim3(evxm::HID / evxm::TT, evxm::HID2 / evxm::TT, (B + kper - 1) / kper),
                            dim3(256), 0, st, a.dz2, evxm::HID2, a.h1, evxm::HID, B, evxm::HID2, evxm::HID, kper, g->w2,
-                           evxm::HID);
+                           evxm::HID, 0);
     }
     {
         const int kper = ksplit(24);
         hipLaunchKernelGGL(evxm::gemm_tn_kernel, dim3(evxm::K1P / evxm::TT, evxm::HID / evxm::TT, (B + kper - 1) / kper),
-                           dim3(256), 0, st, a.dz1, evxm::HID, a.x, evxm::K1P, B, evxm::HID, evxm::K1, kper, g->w1,
-                           evxm::K1);
+                           dim3(256), 0, st, a.dz1, evxm::HID, a.x, evxm::K1P, B, evxm::HID, 4 * evxm::NCELL, kper,
+                           g->w1, evxm::K1, 1);
     }
     return mlaunch("qmlp_backward");
 }

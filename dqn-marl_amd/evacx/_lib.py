@@ -25,7 +25,9 @@ class evx_layout(C.Structure):
                [(n, C.c_double) for n in ["repel_k", "repel_range", "evac_reward", "death_penalty",
                                          "death_acc_penalty", "alive_bonus"]] + \
                [(n, C.c_void_p) for n in ["floor", "cellinfo", "valid_bits", "danger_p", "danger_o",
-                                         "danger_o32", "robot_init", "nbr_valid", "floor_d5"]]
+                                         "danger_o32", "robot_init", "nbr_valid", "floor_d5", "obs_feat"]]
+
+FEAT_PAD = 6  # EVX_FEAT_PAD
 
 
 class evx_state(C.Structure):

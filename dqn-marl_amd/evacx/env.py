@@ -93,6 +93,39 @@ def _fill_delta5(f, out, GX, GY):
         out[xs, ys, d] = (f[xs, ys] - f[xn, yn]) * 5.0
 
 
+def bf16_bits(x: np.ndarray) -> np.ndarray:
+    """float32 -> bf16 bit patterns, round to nearest even (no NaNs here)."""
+    u = np.ascontiguousarray(x, np.float32).view(np.uint32).astype(np.uint64)
+    return ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint32)
+
+
+def obs_feature_map(tables: LayoutTables) -> np.ndarray:
+    """evx_layout.obs_feat: the observation channels of EvacuationEnv._get_state
+    (envs/evacuation_env.py:84-120) that do not depend on the people, for every map cell
+    of a grid padded by FEAT_PAD on each side and every fire step -- bf16(danger) in bits
+    0-15, barrier (!Check_Valid or barrier_list) in bit 16, exit in bit 17 -- exactly as
+    obs_expand_kernel evaluates them cell by cell."""
+    spec, pad = tables.spec, _lib.FEAT_PAD
+    L, W = spec.L, spec.W
+    mx = np.arange(-pad, L + 2 + pad)[:, None]
+    my = np.arange(-pad, W + 2 + pad)[None, :]
+    inb = (mx >= 0) & (mx <= L + 1) & (my >= 0) & (my <= W + 1)
+    cx, cy = np.clip(mx, 0, L + 1), np.clip(my, 0, W + 1)
+    valid_t = np.asarray(tables.valid, bool)[cx, cy]
+    barrier_t = np.asarray(tables.barrier, bool)[cx, cy]
+    valid = (mx >= 1) & (mx <= L) & (my >= 1) & (my <= W) & valid_t
+    bar = ~valid | (inb & barrier_t)
+    ext = (mx == spec.exit[0]) & (my == spec.exit[1])
+    static = (bar.astype(np.uint32) << 16) | (ext.astype(np.uint32) << 17)
+    do32 = np.asarray(tables.danger_o, np.float64).astype(np.float32)
+    T, OX, OY = do32.shape
+    ti, tj = mx - tables.obs_origin[0], my - tables.obs_origin[1]
+    inside = (ti >= 0) & (ti < OX) & (tj >= 0) & (tj < OY)
+    dg = np.zeros((T,) + inside.shape, np.float32)
+    dg[:, inside] = do32[:, np.broadcast_to(ti, inside.shape)[inside], np.broadcast_to(tj, inside.shape)[inside]]
+    return (bf16_bits(dg) | static[None]).astype(np.uint32)
+
+
 class DeviceLayout:
     """Static tables of one layout in HBM + the evx_layout descriptor."""
 
@@ -121,6 +154,7 @@ class DeviceLayout:
         self.t["nbr_valid"] = torch.from_numpy(neighbour_valid_mask(tables.valid, spec.L, spec.W)).to(d)
         self.t["floor_d5"] = torch.from_numpy(floor_delta5(tables.floor, spec.L, spec.W)).to(d)
         self.t["danger_o32"] = self.t["danger_o"].to(torch.float32)
+        self.t["obs_feat"] = torch.from_numpy(obs_feature_map(tables).view(np.int32).reshape(-1)).to(d)
         T = tables.danger_p.shape[0] - 1
         OX, OY = tables.danger_o.shape[1:]
         self.c = _lib.evx_layout(

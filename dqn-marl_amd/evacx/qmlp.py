@@ -15,11 +15,19 @@ import torch
 from . import _lib
 from .env import _stream
 
-HID, HID2, NACT, K1, K1P = 512, 256, 5, 726, 768
+HID, HID2, NACT, K1, K1P = 512, 256, 5, 726, 512
+NCELL, CENTRE_COL = 121, 60 * 6 + 5
+
+
+def compact_ref_cols() -> np.ndarray:
+    """Reference column (of the 726 flattened 11x11x6 inputs) of each of fc1's compact
+    features k < 484 (k = 4 * cell + f <-> channel f + 1; evx_qmlp_pack)."""
+    k = np.arange(4 * NCELL)
+    return (k >> 2) * 6 + (k & 3) + 1
 
 
 class evx_qmlp_params(C.Structure):
-    _fields_ = [(n, C.c_void_p) for n in ["w1", "b1", "w2", "w2t", "b2", "w3", "b3"]]
+    _fields_ = [(n, C.c_void_p) for n in ["w1", "b1c", "w2", "w2t", "b2", "w3", "b3"]]
 
 
 class evx_qmlp_dropout(C.Structure):
@@ -44,7 +52,7 @@ def mlib():
     L = _lib.lib()
     if not _inited:
         L.evx_qmlp_last_error.restype = C.c_char_p
-        L.evx_qmlp_pack.argtypes = [C.c_void_p] * 6
+        L.evx_qmlp_pack.argtypes = [C.c_void_p] * 8
         L.evx_qmlp_forward.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(evx_qmlp_params),
                                        C.POINTER(evx_qmlp_dropout), C.POINTER(evx_qmlp_fwd_out), C.c_void_p]
         L.evx_qmlp_forward2.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.POINTER(evx_qmlp_params),
@@ -77,15 +85,16 @@ class MLPFast:
         self.w1b = torch.zeros(HID * K1P, **i16)
         self.w2b = torch.zeros(HID2 * HID, **i16)
         self.w2t = torch.zeros(HID * HID2, **i16)
-        self.c = evx_qmlp_params(w1=self.w1b.data_ptr(), b1=params["fc1.bias"].data_ptr(), w2=self.w2b.data_ptr(),
+        self.b1c = torch.zeros(HID, dtype=torch.float32, device=self.device)
+        self.c = evx_qmlp_params(w1=self.w1b.data_ptr(), b1c=self.b1c.data_ptr(), w2=self.w2b.data_ptr(),
                                  w2t=self.w2t.data_ptr(), b2=params["fc2.bias"].data_ptr(),
                                  w3=params["fc3.weight"].data_ptr(), b3=params["fc3.bias"].data_ptr())
         self.repack()
 
     def repack(self):
-        mcheck(mlib().evx_qmlp_pack(self.P["fc1.weight"].data_ptr(), self.P["fc2.weight"].data_ptr(),
-                                    self.w1b.data_ptr(), self.w2b.data_ptr(), self.w2t.data_ptr(), _stream()),
-               "qmlp_pack")
+        mcheck(mlib().evx_qmlp_pack(self.P["fc1.weight"].data_ptr(), self.P["fc1.bias"].data_ptr(),
+                                    self.P["fc2.weight"].data_ptr(), self.w1b.data_ptr(), self.b1c.data_ptr(),
+                                    self.w2b.data_ptr(), self.w2t.data_ptr(), _stream()), "qmlp_pack")
 
     def forward(self, lay_c, obs: torch.Tensor, n: int, h1: torch.Tensor, drop=None, x=None, h2=None, q=None,
                 actions=None, epsilon=0.0, act_seed=0, act_offset=0):

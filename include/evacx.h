@@ -52,7 +52,14 @@ typedef struct {
     const int32_t *robot_init;/* [R*2] robot positions after a multi-robot reset */
     const uint8_t *nbr_valid; /* [G] bit d: Check_Valid of the MoveTO[d] neighbour (envs/people.py:259-265) */
     const double *floor_d5;   /* [G][8] (floor[c] - floor[c + MoveTO[d]]) * 5.0 = getDeltaP * 5.0 (envs/people.py:268,282) */
+    /* [(t_max+1)][L+2+2*EVX_FEAT_PAD][W+2+2*EVX_FEAT_PAD] static observation features of map
+     * cell (x, y) at index (t, x + PAD, y + PAD): bf16(danger_o32) in bits 0-15, the
+     * barrier channel (!valid || barrier_list) in bit 16, the exit channel in bit 17
+     * (_get_state's channels 2-4, envs/evacuation_env.py:84-120); read by the MLP fast path */
+    const uint32_t *obs_feat;
 } evx_layout;
+
+#define EVX_FEAT_PAD 6
 
 /* Structure-of-arrays state of E env instances (env-major). */
 typedef struct {
@@ -262,8 +269,8 @@ const char *evx_q_last_error(void);
  * Dropout keep bits are a counter hash of (seed, stream, row, col): the backward pass
  * regenerates them. */
 typedef struct {
-    const uint16_t *w1;   /* [512][768] bf16 fc1.weight, k >= 726 zero, MFMA operand-tiled (evx_qmlp_pack) */
-    const float *b1;      /* [512] */
+    const uint16_t *w1;   /* [512][512] bf16 fc1.weight over the compact K (evx_qmlp_pack), MFMA operand-tiled */
+    const float *b1c;     /* [512] fc1.bias + bf16(fc1.weight[:, 365]) (the constant centre channel), evx_qmlp_pack */
     const uint16_t *w2;   /* [256][512] bf16 fc2.weight, MFMA operand-tiled (evx_qmlp_pack) */
     const uint16_t *w2t;  /* [512][256] bf16 fc2.weight transposed (backward), may be NULL for forward */
     const float *b2;      /* [256] */
@@ -278,7 +285,7 @@ typedef struct {
 
 typedef struct {
     uint16_t *h1;          /* [n][512] bf16 fc1 output after ReLU + dropout (required) */
-    uint16_t *x;           /* [n][768] bf16 expanded observation (k >= 726 zero), or NULL */
+    uint16_t *x;           /* [n][512] bf16 compact expanded observation, or NULL */
     float *h2;             /* [n][256] fc2 output after ReLU, or NULL */
     float *q;              /* [n][5] Q values, or NULL */
     int32_t *actions;      /* [n] epsilon-greedy actions (evx_act's rule and RNG), or NULL */
@@ -286,8 +293,13 @@ typedef struct {
     uint64_t act_seed, act_offset;
 } evx_qmlp_fwd_out;
 
-/* bf16 copies of fc1.weight [512][726] and fc2.weight [256][512] (w2t may be NULL) */
-int evx_qmlp_pack(const float *w1, const float *w2, uint16_t *w1b, uint16_t *w2b, uint16_t *w2t, void *stream);
+/* bf16 copies of fc1.weight [512][726] over fc1's compact K and fc2.weight [256][512]
+ * (w2t may be NULL), and b1c. Compact K: 4 features per cell c < 121 at k = 4c + f for
+ * the reference's channels f + 1 (occupancy, danger, barrier, exit), k >= 484 zero; the
+ * reference's channel 0 is identically zero and channel 5 is the constant centre
+ * one-hot, folded into b1c. */
+int evx_qmlp_pack(const float *w1, const float *b1, const float *w2, uint16_t *w1b, float *b1c, uint16_t *w2b,
+                  uint16_t *w2t, void *stream);
 int evx_qmlp_forward(const evx_layout *lay, const evx_obs *obs, int32_t n, const evx_qmlp_params *p,
                      const evx_qmlp_dropout *drop, const evx_qmlp_fwd_out *out, void *stream);
 /* Two forwards of n rows in one launch pair (the learner's online and target nets). */

@@ -1,7 +1,9 @@
 """GPU numerics of the bf16 MLP fast path (csrc/qmlp.hip) against a plain PyTorch fp32
 reference evaluated on the same bf16-rounded operands.
 
-The expanded observation must equal bf16(evx_obs_expand_f32) exactly; H1 (bf16
+The compact expanded observation (fc1's 484 live inputs: channels 1-4 of every cell;
+channel 0 is identically zero, channel 5 the constant centre one-hot folded into the
+bias) must equal bf16(evx_obs_expand_f32) exactly on those columns; H1 (bf16
 output) may differ from the reference by one bf16 rounding step where the f32
 accumulation order changes the rounded value (rtol 1e-2); Q rtol 1e-3 / atol 1e-3.
 The actions of the fused epsilon-greedy must equal evx_act on the kernel's own Q."""
@@ -39,7 +41,7 @@ def _bf(t):
 @pytest.mark.parametrize("p_drop", [0.0, 0.2])
 def test_fused_forward_matches_torch(p_drop):
     _need_gpu()
-    from evacx.qmlp import HID, K1, K1P, MLPFast, dropout_keep
+    from evacx.qmlp import CENTRE_COL, HID, K1, K1P, MLPFast, compact_ref_cols, dropout_keep
     from evacx.qnet import Learner
     lay, env = _env_obs()
     n = env.E * lay.R
@@ -58,8 +60,15 @@ def test_fused_forward_matches_torch(p_drop):
     # expanded observation: exactly bf16 of the reference tensor
     X = env.expand_obs(torch.float32).reshape(n, K1)
     xk = x.view(torch.bfloat16).view(n, K1P).float()
-    assert torch.equal(xk[:, :K1], _bf(X))
-    assert torch.count_nonzero(xk[:, K1:]) == 0
+    cols = torch.from_numpy(compact_ref_cols()).cuda()
+    assert torch.equal(xk[:, :cols.numel()], _bf(X)[:, cols])
+    assert torch.count_nonzero(xk[:, cols.numel():]) == 0
+    # the columns fc1 leaves out: channel 0 all zero, channel 5 the centre one-hot
+    assert torch.count_nonzero(X.view(n, 121, 6)[:, :, 0]) == 0
+    c5 = torch.zeros(121, device=dev)
+    c5[60] = 1.0
+    assert torch.equal(X.view(n, 121, 6)[:, :, 5], c5.expand(n, 121))
+    assert CENTRE_COL == 60 * 6 + 5
     sd = lr.online.state_dict()
     W1, W2 = _bf(sd["fc1.weight"]), _bf(sd["fc2.weight"])
     ref1 = F.relu(_bf(X) @ W1.t() + sd["fc1.bias"])
@@ -136,7 +145,7 @@ def test_fused_backward_matches_torch_autograd():
     torch.cuda.synchronize()
     # torch reference
     sd = lr.online.state_dict()
-    Xf = X.view(torch.bfloat16).view(B, K1P).float()[:, :K1]
+    Xf = _bf(env.expand_obs(torch.float32, obs_s).reshape(B, K1))  # the full reference input
     W1 = _bf(sd["fc1.weight"]).requires_grad_()
     b1 = sd["fc1.bias"].clone().requires_grad_()
     W2 = _bf(sd["fc2.weight"]).requires_grad_()
