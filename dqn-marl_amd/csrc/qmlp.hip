@@ -19,8 +19,8 @@
 // lane l supplies A[row l&31][k 8(l>>5)..+7] and B[k 8(l>>5)..+7][col l&31];
 // C/D: col = l&31, row = (r&3) + 8(r>>2) + 4(l>>5).
 //
-// Dropout keep bits are a counter-based hash of (seed, stream, row, col), so the
-// backward pass regenerates the mask instead of storing it.
+// Dropout keep bits are a counter-based hash of (seed, stream, row pair, col), 16 bits
+// per element; the backward pass reads the mask back as [H1 > 0] instead of storing it.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -58,8 +58,10 @@ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
 __device__ __forceinline__ uint32_t drop_row(uint32_t seed, uint32_t stream, uint32_t row) {
     return fmix32(seed ^ fmix32(stream * 0x632be5abu + 0x9e3779b9u) ^ (row * 0x9e3779b1u));
 }
-__device__ __forceinline__ bool drop_keep(uint32_t rowh, uint32_t col, uint32_t thresh) {
-    return fmix32(rowh ^ (col * 0x85ebca77u + 0x27d4eb2fu)) >= thresh;
+// one 32-bit hash per (row pair, column): the low half decides the even row, the high
+// half the odd row; keep iff the 16-bit uniform >= thresh16 = floor(p * 65536)
+__device__ __forceinline__ uint32_t drop_pair(uint32_t pairh, uint32_t col) {
+    return fmix32(pairh ^ (col * 0x85ebca77u + 0x27d4eb2fu));
 }
 
 // Philox4x32-10, as evx_act (qnet.hip) uses it for epsilon-greedy
@@ -112,7 +114,7 @@ struct Fwd {
     const float* w3;   // [5][256]
     const float* b3;
     // dropout on fc1's output
-    uint32_t drop_seed, drop_stream, drop_thresh;
+    uint32_t drop_seed, drop_stream, drop_thresh;  // thresh: floor(p * 65536) on 16-bit uniforms
     float drop_scale;
     // outputs
     __bf16* h1;  // [N][512]
@@ -168,7 +170,7 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void qfc1_kernel(Fwd a0
     const Fwd& a = blockIdx.z ? a1 : a0;  // two independent problems in one launch (online / target)
     constexpr int NT = 64 * NWV, RT = 32 * MT, NW = 32 * NTW * NWV;
     constexpr int CPT = 8 * RT / NT, TPR = 8 / CPT;  // cells per thread and chunk, threads per row
-    static_assert(CPT == 2, "generator: one 16-B A store per thread and chunk");
+    static_assert(CPT == 2 || CPT == 4, "generator: 16-B A stores");
     constexpr int APAD = KC1 + 8, CPAD = NW + 8;
     constexpr int ABYTES = 2 * RT * APAD * 2, CBYTES = 32 * CPAD * 2;
     __shared__ __attribute__((aligned(16))) char smem[ABYTES > CBYTES ? ABYTES : CBYTES];
@@ -193,10 +195,13 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void qfc1_kernel(Fwd a0
         for (int t = 0; t < CPT; t++) fv[t] = fb[feat_off(a, kc * 8 + gc + t)];
     };
     auto stash = [&](int buf, int kc) {
-        const uint2 f0 = cell_feat(ob, kc * 8 + gc, fv[0]), f1 = cell_feat(ob, kc * 8 + gc + 1, fv[1]);
-        const uint4 v = make_uint4(f0.x, f0.y, f1.x, f1.y);
-        *reinterpret_cast<uint4*>(&As[buf][gr][gc * 4]) = v;
-        if (wx) *reinterpret_cast<uint4*>(a.x + (size_t)(m0 + gr) * K1P + kc * KC1 + gc * 4) = v;
+#pragma unroll
+        for (int t = 0; t < CPT; t += 2) {
+            const uint2 f0 = cell_feat(ob, kc * 8 + gc + t, fv[t]), f1 = cell_feat(ob, kc * 8 + gc + t + 1, fv[t + 1]);
+            const uint4 v = make_uint4(f0.x, f0.y, f1.x, f1.y);
+            *reinterpret_cast<uint4*>(&As[buf][gr][(gc + t) * 4]) = v;
+            if (wx) *reinterpret_cast<uint4*>(a.x + (size_t)(m0 + gr) * K1P + kc * KC1 + (gc + t) * 4) = v;
+        }
     };
     f32x16 acc[MT][NTW];
 #pragma unroll
@@ -251,17 +256,22 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void qfc1_kernel(Fwd a0
     for (int mt = 0; mt < MT; mt++) {
         if (mt) __syncthreads();  // the previous slab has been stored
 #pragma unroll
-        for (int r = 0; r < 16; r++) {
+        for (int r = 0; r < 16; r += 2) {  // rows rl, rl + 1: one dropout hash per pair
             const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;
-            const uint32_t rh = a.drop_thresh ? drop_row(a.drop_seed, a.drop_stream, (uint32_t)(m0 + mt * 32 + rl)) : 0u;
+            const uint32_t ph = a.drop_thresh ? drop_row(a.drop_seed, a.drop_stream, (uint32_t)(m0 + mt * 32 + rl) >> 1) : 0u;
 #pragma unroll
             for (int nt = 0; nt < NTW; nt++) {
                 const int cl = w * (32 * NTW) + nt * 32 + (lane & 31);
-                float v = acc[mt][nt][r] + bias[nt];
-                v = v > 0.f ? v : 0.f;
-                if (a.drop_thresh)
-                    v = drop_keep(rh, (uint32_t)(blockIdx.y * NW + cl), a.drop_thresh) ? v * a.drop_scale : 0.f;
-                Cs[rl][cl] = (__bf16)v;
+                float v0 = acc[mt][nt][r] + bias[nt], v1 = acc[mt][nt][r + 1] + bias[nt];
+                v0 = v0 > 0.f ? v0 : 0.f;
+                v1 = v1 > 0.f ? v1 : 0.f;
+                if (a.drop_thresh) {
+                    const uint32_t hh = drop_pair(ph, (uint32_t)(blockIdx.y * NW + cl));
+                    v0 = (hh & 0xffffu) >= a.drop_thresh ? v0 * a.drop_scale : 0.f;
+                    v1 = (hh >> 16) >= a.drop_thresh ? v1 * a.drop_scale : 0.f;
+                }
+                Cs[rl][cl] = (__bf16)v0;
+                Cs[rl + 1][cl] = (__bf16)v1;
             }
         }
         __syncthreads();
@@ -728,7 +738,8 @@ static int make_fwd(const evx_layout* lay, const evx_obs* obs, int32_t n, const 
     a.drop_seed = drop ? drop->seed : 0u;
     a.drop_stream = drop ? drop->stream : 0u;
     const float dp = drop ? drop->p : 0.f;
-    a.drop_thresh = dp > 0.f ? (uint32_t)((double)dp * 4294967296.0) : 0u;
+    a.drop_thresh = dp > 0.f ? (uint32_t)((double)dp * 65536.0) : 0u;  // 16-bit uniforms
+    if (dp > 0.f && a.drop_thresh == 0u) a.drop_thresh = 1u;
     a.drop_scale = dp > 0.f ? 1.f / (1.f - dp) : 1.f;
     a.h1 = reinterpret_cast<__bf16*>(out->h1);
     a.x = reinterpret_cast<__bf16*>(out->x);
@@ -744,7 +755,14 @@ static int make_fwd(const evx_layout* lay, const evx_obs* obs, int32_t n, const 
 static int launch_fwd(const evxm::Fwd& a0, const evxm::Fwd& a1, int32_t n, int pairs, bool fc23, hipStream_t st) {
     const unsigned blocks = (unsigned)((n + evxm::RM - 1) / evxm::RM);
     const unsigned big = (unsigned)((n + 127) / 128);
-    if (big * pairs >= 384)  // enough 128-row tiles (all 512 columns each) to fill the chip
+    static int nwv = -1;  // EVX_FC1_NWV=4: 128 x 256 tiles of 4 waves (tuning)
+    if (nwv < 0) {
+        const char* v = getenv("EVX_FC1_NWV");
+        nwv = v ? atoi(v) : 8;
+    }
+    if (big * pairs >= 384 && nwv == 4)
+        hipLaunchKernelGGL((evxm::qfc1_kernel<4, 2, 4>), dim3(big, 2, pairs), dim3(256), 0, st, a0, a1);
+    else if (big * pairs >= 384)  // enough 128-row tiles (all 512 columns each) to fill the chip
         hipLaunchKernelGGL((evxm::qfc1_kernel<4, 2, 8>), dim3(big, 1, pairs), dim3(512), 0, st, a0, a1);
     else
         hipLaunchKernelGGL((evxm::qfc1_kernel<2, 1, 4>), dim3(blocks, 4, pairs), dim3(256), 0, st, a0, a1);

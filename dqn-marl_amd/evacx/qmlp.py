@@ -146,13 +146,17 @@ def _fmix32(h):
 
 
 def dropout_keep(seed: int, stream: int, p: float, rows: int, cols: int = HID) -> np.ndarray:
-    """The kernels' dropout keep mask [rows][cols] (bool), restated on the host (tests)."""
+    """The kernels' dropout keep mask [rows][cols] (bool), restated on the host (tests):
+    one hash per (row pair, column), low 16 bits for the even row, high for the odd;
+    keep iff the 16-bit value >= floor(p * 65536)."""
     seed, stream = seed & 0xFFFFFFFF, stream & 0xFFFFFFFF
     s = int(_fmix32((stream * 0x632BE5AB + 0x9E3779B9) & 0xFFFFFFFF))
     r = np.arange(rows, dtype=np.uint64)
-    rowh = _fmix32(np.uint64(seed ^ s) ^ ((r * 0x9E3779B1) & 0xFFFFFFFF))
+    pair = r >> 1
+    ph = _fmix32(np.uint64(seed ^ s) ^ ((pair * 0x9E3779B1) & 0xFFFFFFFF))
     c = np.arange(cols, dtype=np.uint64)
     ch = (c * 0x85EBCA77 + 0x27D4EB2F) & 0xFFFFFFFF
-    h = _fmix32(rowh[:, None] ^ ch[None, :])
-    thresh = int(p * 4294967296.0) if p > 0 else 0
-    return h >= thresh
+    h = _fmix32(ph[:, None] ^ ch[None, :])
+    half = np.where((r & 1)[:, None] == 1, h >> 16, h & 0xFFFF)
+    thresh = max(1, int(p * 65536.0)) if p > 0 else 0
+    return half >= thresh
