@@ -157,28 +157,21 @@ __device__ __forceinline__ uint2 cell_feat(const evx_obs& ob, int c, uint32_t v)
 }
 
 // ------------------------------------------------------------------ fc1
-// Workgroup tile: 32*MT rows x 128*NTW*NWV/4 columns; wave w owns all rows and
+// Workgroup tile: 32*MT rows x 32*NTW*NWV columns; wave w owns all rows and
 // columns [32*NTW*w, +32*NTW) of it, so every B fragment (global, L2-resident, one
 // 1-KB block per wave load) feeds MT MFMAs. K in 16 chunks of 32 (8 cells): each
-// thread expands 2 cells of one row per chunk from their static feature words
-// (loaded two chunks ahead) into a double-buffered LDS A tile, one barrier per
-// chunk. Epilogue: bias, ReLU, dropout, bf16, staged per 32-row slab through LDS so
-// H1 leaves in 16-B row segments. Act batches: <4, 2, 8> (128 rows x all 512
-// columns: every row expanded once); learner batches <2, 1, 4> (64 x 128).
+// thread expands 2 (or 4) cells of one row per chunk from their static feature
+// words (loaded two chunks ahead) into a double-buffered LDS A tile, one barrier per
+// chunk. Returns after a barrier with the A buffers free.
 template <int MT, int NTW, int NWV>
-__global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void qfc1_kernel(Fwd a0, Fwd a1) {
-    const Fwd& a = blockIdx.z ? a1 : a0;  // two independent problems in one launch (online / target)
-    constexpr int NT = 64 * NWV, RT = 32 * MT, NW = 32 * NTW * NWV;
+__device__ __forceinline__ void fc1_tile(const Fwd& a, int m0, int ncol0, bool want_x, char* smem,
+                                         f32x16 (&acc)[MT][NTW]) {
+    constexpr int NT = 64 * NWV, RT = 32 * MT;
     constexpr int CPT = 8 * RT / NT, TPR = 8 / CPT;  // cells per thread and chunk, threads per row
     static_assert(CPT == 2 || CPT == 4, "generator: 16-B A stores");
-    constexpr int APAD = KC1 + 8, CPAD = NW + 8;
-    constexpr int ABYTES = 2 * RT * APAD * 2, CBYTES = 32 * CPAD * 2;
-    __shared__ __attribute__((aligned(16))) char smem[ABYTES > CBYTES ? ABYTES : CBYTES];
+    constexpr int APAD = KC1 + 8;
     auto As = reinterpret_cast<__bf16 (*)[RT][APAD]>(smem);
-    auto Cs = reinterpret_cast<__bf16 (*)[CPAD]>(smem);
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
-    const int m0 = blockIdx.x * RT;
-    const int ncol0 = blockIdx.y * NW + w * (32 * NTW);
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
     const int gr = tid / TPR, gc = (tid % TPR) * CPT;
     const bool rowok = m0 + gr < a.N;
     evx_obs ob;
@@ -187,7 +180,7 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void qfc1_kernel(Fwd a0
     } else {
         ob = evx_obs{{0u, 0u, 0u, 0u}, 0, 0, 0, 0};
     }
-    const bool wx = a.x && rowok && blockIdx.y == 0;
+    const bool wx = a.x && rowok && want_x;
     const uint32_t* fb = a.feat + feat_base(a, ob);
     uint32_t fv[CPT];
     auto reads = [&](int kc) {
@@ -203,7 +196,6 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void qfc1_kernel(Fwd a0
             if (wx) *reinterpret_cast<uint4*>(a.x + (size_t)(m0 + gr) * K1P + kc * KC1 + (gc + t) * 4) = v;
         }
     };
-    f32x16 acc[MT][NTW];
 #pragma unroll
     for (int i = 0; i < MT; i++)
 #pragma unroll
@@ -248,32 +240,59 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void qfc1_kernel(Fwd a0
         }
         __syncthreads();
     }
-    // epilogue: bias (centre channel folded in), ReLU, dropout, bf16
+}
+
+// fc1 epilogue of one 32-row slab: bias (centre channel folded in), ReLU, dropout
+// (one hash per row pair), bf16 into dst[row within slab][column within tile]
+template <int NTW, int LD>
+__device__ __forceinline__ void fc1_slab(const Fwd& a, const f32x16 (&accm)[NTW], const float (&bias)[NTW],
+                                         int row0, int col0, int cl0, __bf16 (*dst)[LD]) {
+    const int lane = threadIdx.x & 63, h = lane >> 5;
+#pragma unroll
+    for (int r = 0; r < 16; r += 2) {  // rows rl, rl + 1: one dropout hash per pair
+        const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;
+        const uint32_t ph = a.drop_thresh ? drop_row(a.drop_seed, a.drop_stream, (uint32_t)(row0 + rl) >> 1) : 0u;
+#pragma unroll
+        for (int nt = 0; nt < NTW; nt++) {
+            const int cl = cl0 + nt * 32 + (lane & 31);
+            float v0 = accm[nt][r] + bias[nt], v1 = accm[nt][r + 1] + bias[nt];
+            v0 = v0 > 0.f ? v0 : 0.f;
+            v1 = v1 > 0.f ? v1 : 0.f;
+            if (a.drop_thresh) {
+                const uint32_t hh = drop_pair(ph, (uint32_t)(col0 + cl));
+                v0 = (hh & 0xffffu) >= a.drop_thresh ? v0 * a.drop_scale : 0.f;
+                v1 = (hh >> 16) >= a.drop_thresh ? v1 * a.drop_scale : 0.f;
+            }
+            dst[rl][cl] = (__bf16)v0;
+            dst[rl + 1][cl] = (__bf16)v1;
+        }
+    }
+}
+
+// H1 = dropout(relu(X W1^T + b1)) -> bf16 [N][512] (and X when a.x). Act batches:
+// <4, 2, 8> (128 rows x all 512 columns: every row expanded once); learner batches
+// <2, 1, 4> (64 x 128). H1 is staged per 32-row slab through LDS so it leaves in
+// 16-B row segments.
+template <int MT, int NTW, int NWV>
+__global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void qfc1_kernel(Fwd a0, Fwd a1) {
+    const Fwd& a = blockIdx.z ? a1 : a0;  // two independent problems in one launch (online / target)
+    constexpr int NT = 64 * NWV, RT = 32 * MT, NW = 32 * NTW * NWV;
+    constexpr int APAD = KC1 + 8, CPAD = NW + 8;
+    constexpr int ABYTES = 2 * RT * APAD * 2, CBYTES = 32 * CPAD * 2;
+    __shared__ __attribute__((aligned(16))) char smem[ABYTES > CBYTES ? ABYTES : CBYTES];
+    auto Cs = reinterpret_cast<__bf16 (*)[CPAD]>(smem);
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int m0 = blockIdx.x * RT;
+    const int ncol0 = blockIdx.y * NW + w * (32 * NTW);
+    f32x16 acc[MT][NTW];
+    fc1_tile<MT, NTW, NWV>(a, m0, ncol0, blockIdx.y == 0, smem, acc);
     float bias[NTW];
 #pragma unroll
     for (int nt = 0; nt < NTW; nt++) bias[nt] = a.b1[ncol0 + nt * 32 + (lane & 31)];
 #pragma unroll
     for (int mt = 0; mt < MT; mt++) {
         if (mt) __syncthreads();  // the previous slab has been stored
-#pragma unroll
-        for (int r = 0; r < 16; r += 2) {  // rows rl, rl + 1: one dropout hash per pair
-            const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;
-            const uint32_t ph = a.drop_thresh ? drop_row(a.drop_seed, a.drop_stream, (uint32_t)(m0 + mt * 32 + rl) >> 1) : 0u;
-#pragma unroll
-            for (int nt = 0; nt < NTW; nt++) {
-                const int cl = w * (32 * NTW) + nt * 32 + (lane & 31);
-                float v0 = acc[mt][nt][r] + bias[nt], v1 = acc[mt][nt][r + 1] + bias[nt];
-                v0 = v0 > 0.f ? v0 : 0.f;
-                v1 = v1 > 0.f ? v1 : 0.f;
-                if (a.drop_thresh) {
-                    const uint32_t hh = drop_pair(ph, (uint32_t)(blockIdx.y * NW + cl));
-                    v0 = (hh & 0xffffu) >= a.drop_thresh ? v0 * a.drop_scale : 0.f;
-                    v1 = (hh >> 16) >= a.drop_thresh ? v1 * a.drop_scale : 0.f;
-                }
-                Cs[rl][cl] = (__bf16)v0;
-                Cs[rl + 1][cl] = (__bf16)v1;
-            }
-        }
+        fc1_slab<NTW, CPAD>(a, acc[mt], bias, m0 + mt * 32, blockIdx.y * NW, w * (32 * NTW), Cs);
         __syncthreads();
         constexpr int SEG = NW / 8;  // 16-B segments per row
         for (int i = tid; i < 32 * SEG; i += NT) {
@@ -284,6 +303,126 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void qfc1_kernel(Fwd a0
                     *reinterpret_cast<const uint4*>(&Cs[rl][cc]);
         }
     }
+}
+
+// fc3 + DQNAgent.act's epsilon-greedy (agents/dqn_agent.py:101-124) for one row: 4
+// consecutive threads (part = tid & 3) hold quarter dot products of H2 row `hrow`
+// (LDS, f32) with W3 (LDS); the sums are combined by two xor shuffles
+__device__ __forceinline__ void fc3_act(const Fwd& a, const float* hrow, const float (*W3s)[HID2], int row,
+                                        bool rowok) {
+    const int part = threadIdx.x & 3;
+    float qv[NACT];
+#pragma unroll
+    for (int t = 0; t < NACT; t++) qv[t] = 0.f;
+    for (int n = part * 64; n < part * 64 + 64; n++) {
+        const float hv = hrow[n];
+#pragma unroll
+        for (int t = 0; t < NACT; t++) qv[t] += hv * W3s[t][n];
+    }
+#pragma unroll
+    for (int t = 0; t < NACT; t++) {
+        qv[t] += __shfl_xor(qv[t], 1, 64);
+        qv[t] += __shfl_xor(qv[t], 2, 64);
+    }
+    if (part == 0 && rowok) {
+#pragma unroll
+        for (int t = 0; t < NACT; t++) qv[t] += a.b3[t];
+        if (a.q) {
+#pragma unroll
+            for (int t = 0; t < NACT; t++) a.q[(size_t)row * NACT + t] = qv[t];
+        }
+        if (a.actions) {  // DQNAgent.act: epsilon-greedy over argmax (first maximum)
+            int best = 0;
+            float bv = qv[0];
+#pragma unroll
+            for (int t = 1; t < NACT; t++)
+                if (qv[t] > bv) {
+                    bv = qv[t];
+                    best = t;
+                }
+            if (a.epsilon > 0.f) {
+                const uint64_t c = (uint64_t)row + a.act_offset;
+                const u4 r = philox((uint32_t)c, (uint32_t)(c >> 32), 0xac7u, 0u, (uint32_t)a.act_seed,
+                                    (uint32_t)(a.act_seed >> 32));
+                if (u01(r.x) <= a.epsilon) best = (int)((uint64_t)r.y * (uint64_t)NACT >> 32);
+            }
+            a.actions[row] = best;
+        }
+    }
+}
+
+// ------------------------------------------------------------ fused act
+// DQNAgent.act for 128 rows per workgroup (8 waves) in one launch: fc1 as
+// qfc1_kernel<4, 2, 8>, H1 kept in LDS (bf16, never written to HBM), fc2 with wave w
+// on columns [32w, 32w + 32) over all 128 rows (A fragments from the H1 tile, W2
+// fragments from L2), H2 (f32) back into the same LDS, fc3 + epsilon-greedy as
+// qfc23_kernel. Q and actions are bit-identical to qfc1 + qfc23 (same MFMA k order,
+// same fc3 summation). Dynamic LDS: ACT_LDS bytes.
+constexpr int ACT_HP = HID + 8;                                  // H1 row pitch (bf16)
+constexpr int ACT_H2P = HID2 + 1;                                // H2 row pitch (f32)
+constexpr int ACT_HBYTES = 128 * ACT_HP * 2;                     // 133,120 >= 128 * 257 * 4
+constexpr int ACT_LDS = ACT_HBYTES + NACT * HID2 * 4;            // + W3
+__global__ __launch_bounds__(512, 1) void qact_kernel(Fwd a) {
+    extern __shared__ __attribute__((aligned(16))) char dsm[];
+    auto H1s = reinterpret_cast<__bf16 (*)[ACT_HP]>(dsm);
+    auto H2s = reinterpret_cast<float (*)[ACT_H2P]>(dsm);
+    auto W3s = reinterpret_cast<float (*)[HID2]>(dsm + ACT_HBYTES);
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+    const int m0 = blockIdx.x * 128;
+    for (int i = tid; i < NACT * HID2; i += 512) W3s[i / HID2][i % HID2] = a.w3[i];
+    {  // fc1 -> H1 tile
+        f32x16 acc[4][2];
+        fc1_tile<4, 2, 8>(a, m0, w * 64, false, dsm, acc);  // ends with a barrier: A buffers free
+        float bias[2];
+#pragma unroll
+        for (int nt = 0; nt < 2; nt++) bias[nt] = a.b1[w * 64 + nt * 32 + (lane & 31)];
+#pragma unroll
+        for (int mt = 0; mt < 4; mt++)
+            fc1_slab<2, ACT_HP>(a, acc[mt], bias, m0 + mt * 32, 0, w * 64,
+                                reinterpret_cast<__bf16 (*)[ACT_HP]>(&H1s[mt * 32][0]));
+    }
+    __syncthreads();
+    // fc2: wave w -> columns [32w, 32w + 32), all 128 rows; K = 512 as 16 chunks x 2 steps
+    f32x16 acc2[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; mt++)
+#pragma unroll
+        for (int r = 0; r < 16; r++) acc2[mt][r] = 0.f;
+    bf16x8 bc[2], bn[2];
+#pragma unroll
+    for (int s = 0; s < 2; s++) bc[s] = *reinterpret_cast<const bf16x8*>(a.w2 + w2_tile(w, 0, s) + lane * 8);
+    for (int kc = 0; kc < HID / 32; kc++) {
+        if (kc + 1 < HID / 32) {
+#pragma unroll
+            for (int s = 0; s < 2; s++)
+                bn[s] = *reinterpret_cast<const bf16x8*>(a.w2 + w2_tile(w, kc + 1, s) + lane * 8);
+        }
+#pragma unroll
+        for (int s = 0; s < 2; s++)
+#pragma unroll
+            for (int mt = 0; mt < 4; mt++) {
+                const bf16x8 av =
+                    *reinterpret_cast<const bf16x8*>(&H1s[mt * 32 + (lane & 31)][kc * 32 + s * 16 + 8 * h]);
+                acc2[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bc[s], acc2[mt], 0, 0, 0);
+            }
+        bc[0] = bn[0];
+        bc[1] = bn[1];
+    }
+    __syncthreads();  // every wave is done with H1: H2 reuses the space
+    {
+        const int col = w * 32 + (lane & 31);
+        const float bias = a.b2[col];
+#pragma unroll
+        for (int mt = 0; mt < 4; mt++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const float v = acc2[mt][r] + bias;
+                H2s[mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h][col] = v > 0.f ? v : 0.f;
+            }
+    }
+    __syncthreads();
+    const int row = tid >> 2;
+    fc3_act(a, &H2s[row][0], W3s, m0 + row, m0 + row < a.N);
 }
 
 // ------------------------------------------------------------ fc2 + fc3
@@ -371,47 +510,7 @@ __global__ __launch_bounds__(256, 2) void qfc23_kernel(Fwd a0, Fwd a1) {
             }
     }
     __syncthreads();
-    // fc3: thread (row gr, quarter go/8) partial dot products, reduced over the 4 quarters
-    const int part = tid & 3;
-    float qv[NACT];
-#pragma unroll
-    for (int t = 0; t < NACT; t++) qv[t] = 0.f;
-    for (int n = part * 64; n < part * 64 + 64; n++) {
-        const float hv = Hs[gr][n];
-#pragma unroll
-        for (int t = 0; t < NACT; t++) qv[t] += hv * W3s[t][n];
-    }
-#pragma unroll
-    for (int t = 0; t < NACT; t++) {
-        qv[t] += __shfl_xor(qv[t], 1, 64);
-        qv[t] += __shfl_xor(qv[t], 2, 64);
-    }
-    if (part == 0 && rowok) {
-        const int row = m0 + gr;
-#pragma unroll
-        for (int t = 0; t < NACT; t++) qv[t] += a.b3[t];
-        if (a.q) {
-#pragma unroll
-            for (int t = 0; t < NACT; t++) a.q[(size_t)row * NACT + t] = qv[t];
-        }
-        if (a.actions) {  // DQNAgent.act: epsilon-greedy over argmax (first maximum)
-            int best = 0;
-            float bv = qv[0];
-#pragma unroll
-            for (int t = 1; t < NACT; t++)
-                if (qv[t] > bv) {
-                    bv = qv[t];
-                    best = t;
-                }
-            if (a.epsilon > 0.f) {
-                const uint64_t c = (uint64_t)row + a.act_offset;
-                const u4 r = philox((uint32_t)c, (uint32_t)(c >> 32), 0xac7u, 0u, (uint32_t)a.act_seed,
-                                    (uint32_t)(a.act_seed >> 32));
-                if (u01(r.x) <= a.epsilon) best = (int)((uint64_t)r.y * (uint64_t)NACT >> 32);
-            }
-            a.actions[row] = best;
-        }
-    }
+    fc3_act(a, &Hs[gr][0], W3s, m0 + gr, rowok);
 }
 
 // f32 parameters -> bf16 copies: W1 (compact K, w1_tile order) + the folded fc1 bias,
@@ -779,6 +878,30 @@ int evx_qmlp_forward(const evx_layout* lay, const evx_obs* obs, int32_t n, const
     int rc = make_fwd(lay, obs, n, p, drop, out, a);
     if (rc) return rc;
     return launch_fwd(a, a, n, 1, out->q || out->actions || out->h2, (hipStream_t)stream);
+}
+
+int evx_qmlp_act(const evx_layout* lay, const evx_obs* obs, int32_t n, const evx_qmlp_params* p,
+                 const evx_qmlp_dropout* drop, const evx_qmlp_fwd_out* out, void* stream) {
+    if (n <= 0) return 0;
+    if (!out) return mfail(-22, "qmlp_act: NULL out");
+    if (!out->q && !out->actions) return mfail(-22, "qmlp_act: needs q or actions");
+    evx_qmlp_fwd_out o = *out;
+    o.h1 = o.h1 ? o.h1 : reinterpret_cast<uint16_t*>(1);  // unused: H1 stays in LDS
+    o.x = nullptr;
+    o.h2 = nullptr;
+    evxm::Fwd a;
+    int rc = make_fwd(lay, obs, n, p, drop, &o, a);
+    if (rc) return rc;
+    a.h1 = nullptr;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)evxm::qact_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  evxm::ACT_LDS);
+        attr = true;
+    }
+    hipLaunchKernelGGL(evxm::qact_kernel, dim3((unsigned)((n + 127) / 128)), dim3(512), evxm::ACT_LDS,
+                       (hipStream_t)stream, a);
+    return mlaunch("qact");
 }
 
 int evx_qmlp_forward2(const evx_layout* lay, int32_t n, const evx_obs* obs0, const evx_qmlp_params* p0,

@@ -55,6 +55,8 @@ def mlib():
         L.evx_qmlp_pack.argtypes = [C.c_void_p] * 8
         L.evx_qmlp_forward.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(evx_qmlp_params),
                                        C.POINTER(evx_qmlp_dropout), C.POINTER(evx_qmlp_fwd_out), C.c_void_p]
+        L.evx_qmlp_act.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(evx_qmlp_params),
+                                   C.POINTER(evx_qmlp_dropout), C.POINTER(evx_qmlp_fwd_out), C.c_void_p]
         L.evx_qmlp_forward2.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.POINTER(evx_qmlp_params),
                                         C.POINTER(evx_qmlp_dropout), C.POINTER(evx_qmlp_fwd_out), C.c_void_p,
                                         C.POINTER(evx_qmlp_params), C.POINTER(evx_qmlp_dropout),
@@ -106,6 +108,15 @@ class MLPFast:
                                        C.byref(d) if d is not None else None, C.byref(o), _stream()),
                "qmlp_forward")
 
+
+    def act(self, lay_c, obs: torch.Tensor, n: int, drop=None, q=None, actions=None, epsilon=0.0, act_seed=0,
+            act_offset=0):
+        """DQNAgent.act in one launch (evx_qmlp_act): Q values and/or epsilon-greedy actions."""
+        d = self._drop(drop) if drop else None
+        o = evx_qmlp_fwd_out(q=_p(q), actions=_p(actions), epsilon=float(epsilon), act_seed=act_seed,
+                             act_offset=act_offset)
+        mcheck(mlib().evx_qmlp_act(C.byref(lay_c), obs.data_ptr(), n, C.byref(self.c),
+                                   C.byref(d) if d is not None else None, C.byref(o), _stream()), "qmlp_act")
 
     @staticmethod
     def _drop(drop):

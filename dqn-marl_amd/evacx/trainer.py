@@ -26,7 +26,6 @@ import torch
 from . import _lib
 from .env import OBS_WORDS, DeviceLayout, VecEnv, _stream
 from .qnet import DROPOUT_P, Learner, qcheck, qlib
-from .qmlp import HID
 
 
 class evx_replay(C.Structure):
@@ -162,8 +161,6 @@ class VecTrainer:
         self.last_loss: Optional[torch.Tensor] = None
         # bf16 MLP: act and learn straight from compact observations (csrc/qmlp.hip)
         self.fast = self.learner.fast
-        if self.fast is not None:
-            self.h1_act = torch.empty(n * HID, dtype=torch.int16, device=self.device)
         if self.fast is None:
             self.lagged = False  # the split learn step needs the fused bf16 MLP path
 
@@ -171,9 +168,9 @@ class VecTrainer:
         if self.fast is not None:
             # DQNAgent.act in train mode: dropout active, epsilon-greedy over argmax Q
             self.learner.drop_stream += 1
-            self.fast.forward(self.lay.c, self.env.obs, self.n_agents, self.h1_act,
-                              drop=(self.seed, self.learner.drop_stream, DROPOUT_P), actions=self.actions,
-                              epsilon=float(self.epsilon), act_seed=self.seed, act_offset=self.t * self.n_agents)
+            self.fast.act(self.lay.c, self.env.obs, self.n_agents,
+                          drop=(self.seed, self.learner.drop_stream, DROPOUT_P), actions=self.actions,
+                          epsilon=float(self.epsilon), act_seed=self.seed, act_offset=self.t * self.n_agents)
             return self.actions
         x = self.env.expand_obs(torch.float32)  # [E, R, 11, 11, 6]
         Q = self.learner.q_values(x.view(self.n_agents, 11, 11, 6), train=True)

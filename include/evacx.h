@@ -302,6 +302,11 @@ int evx_qmlp_pack(const float *w1, const float *b1, const float *w2, uint16_t *w
                   uint16_t *w2t, void *stream);
 int evx_qmlp_forward(const evx_layout *lay, const evx_obs *obs, int32_t n, const evx_qmlp_params *p,
                      const evx_qmlp_dropout *drop, const evx_qmlp_fwd_out *out, void *stream);
+/* DQNAgent.act (agents/dqn_agent.py:101-124) in one launch: the forward of
+ * evx_qmlp_forward with H1 and H2 kept on chip (out->h1, x, h2 ignored), writing
+ * out->q and/or out->actions; bit-identical to evx_qmlp_forward's. */
+int evx_qmlp_act(const evx_layout *lay, const evx_obs *obs, int32_t n, const evx_qmlp_params *p,
+                 const evx_qmlp_dropout *drop, const evx_qmlp_fwd_out *out, void *stream);
 /* Two forwards of n rows in one launch pair (the learner's online and target nets). */
 int evx_qmlp_forward2(const evx_layout *lay, int32_t n, const evx_obs *obs0, const evx_qmlp_params *p0,
                       const evx_qmlp_dropout *drop0, const evx_qmlp_fwd_out *out0, const evx_obs *obs1,

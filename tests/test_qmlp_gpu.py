@@ -183,3 +183,28 @@ def test_learn_obs_step_runs_and_descends():
     for _ in range(40):
         losses.append(lr.learn_obs(lay.c, env.obs[:B * 8], a, r, done, env.obs[B * 8:2 * B * 8], B).item())
     assert losses[-1] < 0.5 * losses[0], (losses[0], losses[-1])
+
+
+@pytest.mark.parametrize("eps", [0.0, 0.25])
+def test_fused_act_matches_two_kernel_forward(eps):
+    """evx_qmlp_act (H1/H2 on chip, one launch) == evx_qmlp_forward's Q and actions, bit
+    for bit, on an act-sized ragged batch with dropout."""
+    _need_gpu()
+    from evacx.qmlp import HID, MLPFast
+    from evacx.qnet import Learner
+    lay, env = _env_obs(E=2000, steps=3, R=16, grid=64, people=500)
+    n = env.E * lay.R - 7
+    lr = Learner(kind="mlp", precision="bf16", seed=31)
+    fast = MLPFast(lr.online, "cuda")
+    h1 = torch.empty(n * HID, dtype=torch.int16, device="cuda")
+    q1 = torch.empty(n, 5, device="cuda")
+    a1 = torch.empty(n, dtype=torch.int32, device="cuda")
+    q2 = torch.full((n + 3, 5), 9.0, device="cuda")
+    a2 = torch.full((n + 3,), -1, dtype=torch.int32, device="cuda")
+    kw = dict(drop=(77, 5, 0.2), epsilon=eps, act_seed=4, act_offset=123)
+    fast.forward(lay.c, env.obs, n, h1, q=q1, actions=a1, **kw)
+    fast.act(lay.c, env.obs, n, q=q2, actions=a2, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(q1, q2[:n])
+    assert torch.equal(a1, a2[:n])
+    assert torch.all(q2[n:] == 9.0) and torch.all(a2[n:] == -1)

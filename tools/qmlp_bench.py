@@ -27,6 +27,16 @@ h2 = torch.empty(n_all, 256, device="cuda")
 q = torch.empty(n_all, 5, device="cuda")
 act = torch.empty(n_all, dtype=torch.int32, device="cuda")
 flops_row = 2 * (726 * 512 + 512 * 256 + 256 * 5)
+for _ in range(3):
+    fast.act(lay.c, env.obs, n_all, drop=(1, 2, 0.2), actions=act, epsilon=0.1)
+a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+a.record()
+for _ in range(20):
+    fast.act(lay.c, env.obs, n_all, drop=(1, 2, 0.2), actions=act, epsilon=0.1)
+b.record()
+torch.cuda.synchronize()
+us = a.elapsed_time(b) / 20 * 1e3
+print(f"{'fused act (qact_kernel)':26s} n={n_all:6d}: {us:8.1f} us  {flops_row * n_all / us / 1e6:7.1f} TF/s (whole MLP flops)")
 for n, kw, name in [(n_all, dict(actions=act, epsilon=0.1), "act (fc1+fc23+egreedy)"),
                     (n_all, dict(), "fc1 only"),
                     (4096, dict(x=x, h2=h2, q=q), "learn fwd (saves x,h2)"),
