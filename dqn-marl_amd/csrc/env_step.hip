@@ -2189,20 +2189,26 @@ __global__ __launch_bounds__(64 * NWB) void env_step_kernel(evx_layout lay, evx_
 // ones first so the light ones fill in around them.
 // order[E] = H: the first H envs of the order (at most hcap, each with >= hmin persons
 // in play) run their rows phase on a whole workgroup (rows_wide).
+// Every env's bucket is read from the state ONCE, into LDS (bk[E]): with the lagged
+// training schedule this kernel runs while an env.step may be updating the counters,
+// and a bucket that changed between the counting and the ranking pass would break the
+// permutation.
 __global__ __launch_bounds__(1024) void env_order_kernel(evx_layout lay, evx_state st, int hcap, int hmin) {
     __shared__ int cnt[16], base[16], nheavy;
+    extern __shared__ uint8_t bk[];  // [E] bucket (0 = most persons remaining)
     const int tid = threadIdx.x, E = st.E, P = lay.P;
     if (tid < 16) cnt[tid] = 0;
     if (tid == 0) nheavy = 0;
     __syncthreads();
-    auto remaining = [&](int e) { return P - st.scal[(size_t)e * 4 + 2] - st.scal[(size_t)e * 4 + 3]; };
-    auto bucket = [&](int e) {
-        return 15 - min(15, max(0, remaining(e)) * 16 / (P + 1));  // 0 = most remaining
-    };
     int nh = 0;
     for (int e = tid; e < E; e += 1024) {
-        atomicAdd(&cnt[bucket(e)], 1);
-        nh += remaining(e) >= hmin;
+        const int s2 = __hip_atomic_load(&st.scal[(size_t)e * 4 + 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int s3 = __hip_atomic_load(&st.scal[(size_t)e * 4 + 3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int rem = P - s2 - s3;
+        const int b = 15 - min(15, max(0, rem) * 16 / (P + 1));
+        bk[e] = (uint8_t)b;
+        atomicAdd(&cnt[b], 1);
+        nh += rem >= hmin;
     }
     if (nh) atomicAdd(&nheavy, nh);
     __syncthreads();
@@ -2221,17 +2227,17 @@ __global__ __launch_bounds__(1024) void env_order_kernel(evx_layout lay, evx_sta
     const int lane = tid & 63, w = tid >> 6;
     for (int e0 = 0; e0 < E; e0 += 1024) {
         const int e = e0 + tid;
-        const int bk = e < E ? bucket(e) : -1;
+        const int b = e < E ? (int)bk[e] : -1;
         int inw = 0;
         for (int bb = 0; bb < 16; bb++) {
-            const unsigned long long m = __ballot(bk == bb);
+            const unsigned long long m = __ballot(b == bb);
             if (lane == 0) wcnt[w][bb] = __popcll(m);
-            if (bk == bb) inw = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            if (b == bb) inw = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
         }
         __syncthreads();
         if (e < E) {
-            int r = base[bk] + inw;
-            for (int ww = 0; ww < w; ww++) r += wcnt[ww][bk];
+            int r = base[b] + inw;
+            for (int ww = 0; ww < w; ww++) r += wcnt[ww][b];
             st.order[r] = e;
         }
         __syncthreads();
@@ -2421,9 +2427,17 @@ int evx_env_order(const evx_layout* l, const evx_state* s, void* stream) {
     if (rc) return rc;
     if (!s || !s->order) return fail(-22, "env_order: state.order is NULL");
     if (s->E <= 0) return 0;
+    if (s->E > 160 * 1024 - 4096) return fail(-22, "env_order: too many envs for one workgroup's LDS");
     int hmin = 0;
     const int hcap = heavy_cap(*l, &hmin);
-    hipLaunchKernelGGL(evx::env_order_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, *l, *s, hcap, hmin);
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)evx::env_order_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024 - 4096);
+        attr_set = true;
+    }
+    const size_t lds = ((size_t)s->E + 3) & ~(size_t)3;  // one bucket byte per env
+    hipLaunchKernelGGL(evx::env_order_kernel, dim3(1), dim3(1024), lds, (hipStream_t)stream, *l, *s, hcap, hmin);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : hip_fail(e, "env_order launch");
 }

@@ -183,7 +183,9 @@ class DeviceLayout:
 class VecEnv:
     """E env instances of one layout, state resident in HBM (SoA, env-major)."""
 
-    def __init__(self, layout: DeviceLayout, E: int, thmap: bool = False):
+    def __init__(self, layout: DeviceLayout, E: int, thmap: bool = False, obs_buffers: int = 1):
+        """obs_buffers=2: every step writes its observations into the other of two
+        buffers, so the previous step's stay readable (``obs_prev``) without a copy."""
         self.lay = layout
         self.E = int(E)
         P, R, d = layout.P, layout.R, layout.device
@@ -207,13 +209,18 @@ class VecEnv:
             raise _lib.EvacxError(_lib.lib().evx_last_error().decode())
         self.scratch = torch.zeros(E * sw, **i32)
         # dispatch order (evx_env_order), scheduling only; order[E] = envs whose rows
-        # phase runs on a whole workgroup (0: none)
-        self.order = torch.cat([torch.arange(E, **i32), torch.zeros(1, **i32)])
+        # phase runs on a whole workgroup (0: none). Two buffers: compute_order(ahead=True)
+        # fills the one the step after the next reads while the next step reads the other.
+        self._orders = [torch.cat([torch.arange(E, **i32), torch.zeros(1, **i32)]) for _ in range(2)]
+        self._ord = 0
+        self._order_ahead = False
         # outputs
         self.reward = torch.zeros(E, **f64)
         self.done = torch.zeros(E, dtype=torch.uint8, device=d)
         self.counts = torch.zeros(E * 2, **i32)
-        self.obs = torch.zeros(E * R * OBS_WORDS, **i32)
+        assert obs_buffers in (1, 2)
+        self._obs = [torch.zeros(E * R * OBS_WORDS, **i32) for _ in range(obs_buffers)]
+        self._ob = 0
         self.err = torch.zeros(1, **i32)
         self.c = _lib.evx_state(E=E, pk=_ptr(self.pk), health=_ptr(self.health), acc=_ptr(self.acc),
                                 rmap=_ptr(self.rmap), thmap=_ptr(self.thmap), robots=_ptr(self.robots),
@@ -222,6 +229,21 @@ class VecEnv:
         self.obs_term: Optional[torch.Tensor] = None
         self.out = _lib.evx_step_out(reward=_ptr(self.reward), done=_ptr(self.done), counts=_ptr(self.counts),
                                      obs=_ptr(self.obs), err=_ptr(self.err))
+
+    @property
+    def obs(self) -> torch.Tensor:
+        """Compact observations of the current state (int32 words, OBS_WORDS per robot)."""
+        return self._obs[self._ob]
+
+    @property
+    def obs_prev(self) -> torch.Tensor:
+        """With obs_buffers=2: the observations before the last step (until the next one)."""
+        return self._obs[self._ob ^ 1]
+
+    @property
+    def order(self) -> torch.Tensor:
+        """The dispatch order the next step reads ([E] env ids + heavy count)."""
+        return self._orders[self._ord]
 
     # -------------------------------------------------------------- seeding
     def seed(self, seeds: Sequence[int]):
@@ -253,12 +275,20 @@ class VecEnv:
         _lib.check(_lib.lib().evx_env_reset(C.byref(self.lay.c), C.byref(self.c), _ptr(m), _ptr(self.obs),
                                             _ptr(self.err), _stream()), "evx_env_reset")
 
-    def compute_order(self, force: bool = False):
+    def compute_order(self, force: bool = False, ahead: bool = False):
         """Dispatch order of the next step: heavy env-steps first, the heaviest with a
         whole workgroup each (scheduling only; the results do not depend on it). Small
-        batches keep the identity order unless forced (tests)."""
-        if self.E >= 256 or force:
-            _lib.check(_lib.lib().evx_env_order(C.byref(self.lay.c), C.byref(self.c), _stream()), "evx_env_order")
+        batches keep the identity order unless forced (tests). ahead=True: fill the other
+        order buffer, for the step after the next one, from the state as it is when the
+        kernel runs (it may overlap the next step, which reads the current buffer)."""
+        if self.E < 256 and not force:
+            return
+        c = self.c
+        if ahead:
+            c = _lib.evx_state.from_buffer_copy(self.c)
+            c.order = _ptr(self._orders[self._ord ^ 1])
+            self._order_ahead = True
+        _lib.check(_lib.lib().evx_env_order(C.byref(self.lay.c), C.byref(c), _stream()), "evx_env_order")
 
     def step(self, actions: torch.Tensor, order: bool = True, auto_reset: bool = False):
         """order=False: the caller already ran compute_order() for this state (see
@@ -269,11 +299,18 @@ class VecEnv:
         assert a.numel() == self.E * self.lay.R
         if order:
             self.compute_order()
+        if len(self._obs) == 2:  # write into the other buffer: the current one becomes obs_prev
+            self._ob ^= 1
+            self.out.obs = _ptr(self._obs[self._ob])
         if auto_reset and self.obs_term is None:
             self.obs_term = torch.zeros_like(self.obs)
         self.out.obs_term = self.obs_term.data_ptr() if auto_reset else None
         _lib.check(_lib.lib().evx_env_step(C.byref(self.lay.c), C.byref(self.c), a.data_ptr(), C.byref(self.out),
                                            _stream()), "evx_env_step")
+        if self._order_ahead:  # the order computed ahead is the one the following step reads
+            self._ord ^= 1
+            self.c.order = _ptr(self._orders[self._ord])
+            self._order_ahead = False
 
     def expand_obs(self, dtype=torch.float32, obs: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Reference-layout observation tensor [E, R, 11, 11, 6]."""

@@ -101,7 +101,7 @@ class VecTrainer:
                  prio_eps: float = 1e-6):
         self.lay, self.E, self.R = layout, E, layout.R
         self.device = layout.device
-        self.env = VecEnv(layout, E)
+        self.env = VecEnv(layout, E, obs_buffers=2)  # the push reads env.obs_prev: no copy per step
         self.env.seed([seed_base + env_offset + i for i in range(E)])
         self.env.reset()
         self.env.compute_order()
@@ -127,7 +127,6 @@ class VecTrainer:
         self.lagged = lagged_learn
         n = E * self.R
         self.n_agents = n
-        self.obs_prev = torch.zeros(n * OBS_WORDS, dtype=torch.int32, device=self.device)
         self.actions = torch.zeros(n, dtype=torch.int32, device=self.device)
         self.samp = dict(s=torch.zeros(batch * OBS_WORDS, dtype=torch.int32, device=self.device),
                          s2=torch.zeros(batch * OBS_WORDS, dtype=torch.int32, device=self.device),
@@ -273,14 +272,17 @@ class VecTrainer:
                 if ev_learn is not None:
                     ev_learn[1].record(self.lstream)
                 self.ev_learned.record(self.lstream)
-        self.obs_prev.copy_(self.env.obs)
+        # the order was computed on the side stream from the state after the previous step,
+        # concurrently with act; by now the event is complete, so the wait costs no gap
+        # (an order one step older would miss the envs that just auto-reset: they would be
+        # dispatched as light envs and become the launch's tail)
         main.wait_event(self.ev_order)
         if ev_env is not None:
             ev_env[0].record(main)
         self.env.step(self.actions, order=False, auto_reset=True)
         if ev_env is not None:
             ev_env[1].record(main)
-        self.replay.push(self.obs_prev, self.env.obs, self.actions, self.env.reward, self.env.done,
+        self.replay.push(self.env.obs_prev, self.env.obs, self.actions, self.env.reward, self.env.done,
                          self.n_agents, self.R, s2_term=self.env.obs_term)
         if self.prio and not self.lagged:
             self.replay.expose()

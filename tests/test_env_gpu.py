@@ -217,6 +217,44 @@ def test_gpu_vs_oracle_dense_conflicts():
     _oracle_pair(synthetic(24, 20, 4), 380, E=16, steps=50, check_every=1)
 
 
+def test_order_ahead_and_obs_double_buffer_do_not_change_results():
+    """The lagged trainer's scheduling: the dispatch order computed one step ahead on
+    another stream (racing the step that reads the other order buffer) and observations
+    double-buffered. Same states bit for bit as the plain path; every order a permutation."""
+    _need_gpu()
+    from evacx.env import DeviceLayout, VecEnv
+    from evacx.layout import build_tables, synthetic
+    lay = DeviceLayout(build_tables(synthetic(24, 20, 4)), 380)
+    E = 300
+    a = VecEnv(lay, E)
+    b = VecEnv(lay, E, obs_buffers=2)
+    for v in (a, b):
+        v.seed([55 + i for i in range(E)])
+        v.reset()
+    side = torch.cuda.Stream()
+    g = torch.Generator(device="cuda").manual_seed(3)
+    for t in range(40):
+        acts = torch.randint(0, 5, (E * lay.R,), device="cuda", dtype=torch.int32, generator=g)
+        a.step(acts, auto_reset=True)
+        prev = b.obs
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):  # overlaps b's step below
+            b.compute_order(ahead=True)
+        b.step(acts, order=False, auto_reset=True)
+        torch.cuda.current_stream().wait_stream(side)
+        assert b.obs_prev.data_ptr() == prev.data_ptr() and b.obs.data_ptr() != prev.data_ptr()
+        torch.cuda.synchronize()
+        ordr = b.order.cpu().numpy()
+        assert np.array_equal(np.sort(ordr[:E]), np.arange(E)), t
+        assert np.array_equal(a.obs.cpu().numpy(), b.obs.cpu().numpy()), t
+        assert np.array_equal(a.obs_term.cpu().numpy(), b.obs_term.cpu().numpy()), t
+        assert np.array_equal(a.reward.cpu().numpy(), b.reward.cpu().numpy()), t
+    for name in ["pk", "health", "acc", "rmap", "scal", "py_mt", "np_mt"]:
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
+    a.check_err()
+    b.check_err()
+
+
 def test_gpu_vs_oracle_cfg4_256_single_robot():
     """BASELINE cfg4 geometry: 256x256 grid, 9102 people, one robot (two envs per
     workgroup: the layout's LDS does not fit four)."""
