@@ -85,6 +85,9 @@ def parse():
     ap.add_argument("--replay", choices=["uniform", "prioritized"], default="uniform",
                     help="prioritized: GPU sum/min-tree proportional replay (cfg5; evacx.prio)")
     ap.add_argument("--replay-capacity", type=int, default=1 << 20)
+    ap.add_argument("--groups", type=int, default=1,
+                    help="env groups per GPU, each with its own act -> env.step -> push stream chain "
+                         "(evacx.trainer._Group): one group's env.step tail overlaps the others' work")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r1", "env_traffic.json"),
                     help="PMC traffic record of env_step_kernel on this workload (tools/parse_prof.py)")
     return ap.parse_args()
@@ -113,7 +116,7 @@ def main():
     hook = make_allreduce_hook(dist, world) if dist is not None else None
     tr = VecTrainer(lay, E, env_offset=rank * E, precision=args.precision, batch=args.batch, grad_hook=hook,
                     lagged_learn=args.schedule == "lagged", replay=args.replay,
-                    replay_capacity=args.replay_capacity)
+                    replay_capacity=args.replay_capacity, groups=args.groups if args.mode == "train" else 1)
     env = tr.env
 
     def barrier():
@@ -213,14 +216,15 @@ def main():
     value = E * world * args.steps / elapsed
     G = (L + 2) * (W + 2)
     bpe = bytes_per_env_step(P, R, G)
-    achieved = bpe * E / (kern_ms * 1e-3) / 1e9
+    per_launch = E // args.groups if args.mode == "train" else E  # env.step launches of group 0 are timed
+    achieved = bpe * per_launch / (kern_ms * 1e-3) / 1e9
     traffic = None
     if os.path.exists(args.traffic):
         # HBM bytes per launch from rocprofv3 PMC passes of this same workload (separate
         # --pmc FETCH_SIZE / WRITE_SIZE runs; cannot be collected inside the timed run)
         rec = json.load(open(args.traffic))
         if rec.get("kernel") == "env_step_kernel":
-            traffic = rec["bytes_per_env_step"] * E
+            traffic = rec["bytes_per_env_step"] * per_launch
     cpu = cpu_baseline(cpu_snap, env.lay.R, tables, P, args) if cpu_snap is not None else None
     if rank == 0:
         line = {
@@ -245,7 +249,7 @@ def main():
                                 else "env.step + auto-reset, uniform random actions")),
                 "envs_per_gpu": E, "grid": f"{L}x{W}", "people": P, "robots": R, "mode": args.mode,
                 "batch": args.batch, "qnet": "MLP 726-512-256-5", "schedule": args.schedule,
-                "replay": args.replay,
+                "replay": args.replay, "groups": args.groups if args.mode == "train" else 1,
                 "parallelism": f"data-parallel over {world} GPU(s): envs sharded, grad all-reduce (RCCL) per learn",
             },
             "strict_schedule_steps_per_s": strict,
@@ -255,7 +259,7 @@ def main():
             "last_loss": loss,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "env_step_kernel",
-                         "kernel_ms": kern_ms, "bytes_per_env_step": bpe, "env_steps_per_launch": E,
+                         "kernel_ms": kern_ms, "bytes_per_env_step": bpe, "env_steps_per_launch": per_launch,
                          "launches_timed": len(timed)},
             "cpu_baseline": cpu,
         }

@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import ctypes as C
 import math
-from typing import Optional, Sequence
+from typing import List, Optional, Sequence
 
 import numpy as np
 import torch
@@ -227,18 +227,62 @@ class VecEnv:
                                 view=_ptr(self.view), scal=_ptr(self.scal), py_mt=_ptr(self.py_mt),
                                 np_mt=_ptr(self.np_mt), scratch=_ptr(self.scratch), order=_ptr(self.order))
         self.obs_term: Optional[torch.Tensor] = None
+        self._parts: List["VecEnv"] = []
         self.out = _lib.evx_step_out(reward=_ptr(self.reward), done=_ptr(self.done), counts=_ptr(self.counts),
                                      obs=_ptr(self.obs), err=_ptr(self.err))
+
+    def split(self, G: int) -> List["VecEnv"]:
+        """G VecEnvs over consecutive E/G envs each, sharing this one's storage: they step
+        independently (e.g. on their own streams, so one part's launch tail overlaps the
+        next part's work), while this object still reads and resets all E envs (its step
+        steps every part). The parts must step together: each flips its observation
+        buffers once per step."""
+        if G < 2 or self.E % G:
+            raise ValueError("split: E must be a multiple of G >= 2")
+        if self.obs_term is None:
+            self.obs_term = torch.zeros_like(self._obs[0])
+        n, lay = self.E // G, self.lay
+        P, R, RW, GG = lay.P, lay.R, lay.RW, lay.G
+        sw = self.scratch.numel() // self.E
+        i32 = dict(dtype=torch.int32, device=lay.device)
+        parts = []
+        for g in range(G):
+            lo = g * n
+
+            def cut(t, k):
+                return None if t is None else t[lo * k:(lo + n) * k]
+            p = VecEnv.__new__(VecEnv)
+            p.lay, p.E, p._parts = lay, n, []
+            p.pk, p.health, p.acc = cut(self.pk, P), cut(self.health, P), cut(self.acc, P)
+            p.rmap, p.thmap = cut(self.rmap, RW), cut(self.thmap, GG)
+            p.robots, p.view, p.scal = cut(self.robots, R), cut(self.view, 1), cut(self.scal, 4)
+            p.py_mt, p.np_mt, p.scratch = cut(self.py_mt, 625), cut(self.np_mt, 625), cut(self.scratch, sw)
+            p._orders = [torch.cat([torch.arange(n, **i32), torch.zeros(1, **i32)]) for _ in range(2)]
+            p._ord, p._order_ahead = 0, False
+            p.reward, p.done, p.counts = cut(self.reward, 1), cut(self.done, 1), cut(self.counts, 2)
+            p._obs = [cut(b, R * OBS_WORDS) for b in self._obs]
+            p._ob = self._ob
+            p.err = self.err
+            p.obs_term = cut(self.obs_term, R * OBS_WORDS)
+            p.c = _lib.evx_state(E=n, pk=_ptr(p.pk), health=_ptr(p.health), acc=_ptr(p.acc), rmap=_ptr(p.rmap),
+                                 thmap=_ptr(p.thmap), robots=_ptr(p.robots), view=_ptr(p.view), scal=_ptr(p.scal),
+                                 py_mt=_ptr(p.py_mt), np_mt=_ptr(p.np_mt), scratch=_ptr(p.scratch),
+                                 order=_ptr(p.order))
+            p.out = _lib.evx_step_out(reward=_ptr(p.reward), done=_ptr(p.done), counts=_ptr(p.counts),
+                                      obs=_ptr(p.obs), err=_ptr(p.err))
+            parts.append(p)
+        self._parts = parts
+        return parts
 
     @property
     def obs(self) -> torch.Tensor:
         """Compact observations of the current state (int32 words, OBS_WORDS per robot)."""
-        return self._obs[self._ob]
+        return self._obs[self._parts[0]._ob if self._parts else self._ob]
 
     @property
     def obs_prev(self) -> torch.Tensor:
         """With obs_buffers=2: the observations before the last step (until the next one)."""
-        return self._obs[self._ob ^ 1]
+        return self._obs[(self._parts[0]._ob if self._parts else self._ob) ^ 1]
 
     @property
     def order(self) -> torch.Tensor:
@@ -281,6 +325,10 @@ class VecEnv:
         batches keep the identity order unless forced (tests). ahead=True: fill the other
         order buffer, for the step after the next one, from the state as it is when the
         kernel runs (it may overlap the next step, which reads the current buffer)."""
+        if self._parts:
+            for p in self._parts:
+                p.compute_order(force=force, ahead=ahead)
+            return
         if self.E < 256 and not force:
             return
         c = self.c
@@ -297,6 +345,11 @@ class VecEnv:
         and self.obs holds the post-reset ones (self.done still flags them)."""
         a = actions.to(torch.int32).contiguous()
         assert a.numel() == self.E * self.lay.R
+        if self._parts:  # split: every part steps its envs (same stream here)
+            k = self._parts[0].E * self.lay.R
+            for i, p in enumerate(self._parts):
+                p.step(a[i * k:(i + 1) * k], order=order, auto_reset=auto_reset)
+            return
         if order:
             self.compute_order()
         if len(self._obs) == 2:  # write into the other buffer: the current one becomes obs_prev

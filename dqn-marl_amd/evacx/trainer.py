@@ -10,6 +10,8 @@ One ``step()`` = for all E envs x R robots of this rank:
   reset    -- auto-reset of finished envs (reference reset semantics) fused into
               the env.step launch; the heavy-first dispatch order of the next
               env.step (evx_env_order) runs on a side stream
+With groups > 1 the envs are split into parts that run act -> env.step -> push on
+their own streams, so one part's env.step tail overlaps the others' work.
 
 Reference: runners/train_double_dqn.py:43-69 (independent robots, shared team
 reward) generalised to R robots and E envs; DQNAgent.act/remember/learn
@@ -19,7 +21,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
-from typing import Optional
+from typing import List, Optional
 
 import torch
 
@@ -91,6 +93,27 @@ class Replay:
                                    out["done"].data_ptr(), None, _stream()), "replay_sample")
 
 
+class _Group:
+    """One part of the envs with its own stream chain (act -> env.step -> push): with
+    several groups, one group's env.step launch tail (its heaviest envs, few waves)
+    overlaps the other groups' act and env.step instead of idling the chip."""
+
+    def __init__(self, env: VecEnv, g: int, row0: int, actions: torch.Tensor, device):
+        self.env, self.g, self.row0 = env, g, row0
+        self.n = env.E * env.lay.R
+        self.actions = actions  # this group's rows of the trainer's action buffer
+        # act, env.step, push on a high-priority stream: the learn stream's workgroups
+        # then fill the env launch's tail instead of competing for its first slots
+        self.main = torch.cuda.Stream(device=device, priority=int(os.environ.get("EVX_MAIN_PRIO", "-1")))
+        self.side = torch.cuda.Stream(device=device)  # dispatch order (and extra resets)
+        cur = torch.cuda.current_stream(device)
+        self.ev_push = torch.cuda.Event()
+        self.ev_push.record(cur)
+        self.ev_order = torch.cuda.Event()
+        self.ev_order.record(cur)
+        self.ev_act = torch.cuda.Event()
+
+
 class VecTrainer:
     def __init__(self, layout: DeviceLayout, E: int, seed_base: int = 1234, env_offset: int = 0,
                  kind: str = "mlp", precision: str = "bf16", batch: int = 4096, replay_capacity: int = 1 << 20,
@@ -98,12 +121,16 @@ class VecTrainer:
                  epsilon_decay: float = 0.9995, target_every: int = 1000, learner_seed: int = 0,
                  grad_hook=None, learn_every: int = 1, lagged_learn: bool = False, replay: str = "uniform",
                  prio_alpha: float = 0.6, prio_beta0: float = 0.4, prio_beta_steps: int = 100000,
-                 prio_eps: float = 1e-6):
+                 prio_eps: float = 1e-6, groups: int = 1):
+        """groups: the envs are split into this many parts, each stepping on its own
+        stream chain (see _Group); the env results do not depend on it (every env is
+        still stepped once per step with its own streams), the act's dropout masks do."""
         self.lay, self.E, self.R = layout, E, layout.R
         self.device = layout.device
         self.env = VecEnv(layout, E, obs_buffers=2)  # the push reads env.obs_prev: no copy per step
         self.env.seed([seed_base + env_offset + i for i in range(E)])
         self.env.reset()
+        parts = self.env.split(groups) if groups > 1 else [self.env]
         self.env.compute_order()
         self.learner = Learner(kind=kind, device=self.device, lr=lr, gamma=gamma, precision=precision,
                                seed=learner_seed)
@@ -128,6 +155,10 @@ class VecTrainer:
         n = E * self.R
         self.n_agents = n
         self.actions = torch.zeros(n, dtype=torch.int32, device=self.device)
+        ng = n // len(parts)
+        self.groups: List[_Group] = [_Group(p, g, g * ng, self.actions[g * ng:(g + 1) * ng], self.device)
+                                     for g, p in enumerate(parts)]
+        self.main = self.groups[0].main
         self.samp = dict(s=torch.zeros(batch * OBS_WORDS, dtype=torch.int32, device=self.device),
                          s2=torch.zeros(batch * OBS_WORDS, dtype=torch.int32, device=self.device),
                          a=torch.zeros(batch, dtype=torch.int32, device=self.device),
@@ -140,41 +171,37 @@ class VecTrainer:
         self.seed = learner_seed * 7919 + env_offset + 17
         self.t = 0
         self.learn_steps = 0
-        # the step's own chain (act, env.step, push) on a high-priority stream: with the
-        # lagged schedule the learn stream's workgroups then fill the env launch's tail
-        # instead of competing for its first slots
-        self.main = torch.cuda.Stream(device=self.device, priority=int(os.environ.get("EVX_MAIN_PRIO", "-1")))
-        self.side = torch.cuda.Stream(device=self.device)
-        self.ev_push = torch.cuda.Event()
-        self.ev_push.record(torch.cuda.current_stream(self.device))
+        cur = torch.cuda.current_stream(self.device)
         self.ev_reset = torch.cuda.Event()
-        self.ev_reset.record(torch.cuda.current_stream(self.device))
+        self.ev_reset.record(cur)
         self.reset_pending = False
         self.join_caller = True  # the first step waits for the caller's stream (set-up work)
         self.lstream = torch.cuda.Stream(device=self.device, priority=int(os.environ.get("EVX_LEARN_PRIO", "0")))
-        self.ev_act = torch.cuda.Event()
         self.ev_learned = torch.cuda.Event()
-        self.ev_learned.record(torch.cuda.current_stream(self.device))
-        self.ev_order = torch.cuda.Event()
-        self.ev_order.record(torch.cuda.current_stream(self.device))
+        self.ev_learned.record(cur)
         self.last_loss: Optional[torch.Tensor] = None
         # bf16 MLP: act and learn straight from compact observations (csrc/qmlp.hip)
         self.fast = self.learner.fast
         if self.fast is None:
             self.lagged = False  # the split learn step needs the fused bf16 MLP path
 
-    def act(self):
+    def _act(self, grp: _Group):
+        """DQNAgent.act in train mode for one group's robots: dropout active, epsilon-greedy
+        over argmax Q; the epsilon draws are counted over all E*R robots of the step."""
+        off = self.t * self.n_agents + grp.row0
         if self.fast is not None:
-            # DQNAgent.act in train mode: dropout active, epsilon-greedy over argmax Q
             self.learner.drop_stream += 1
-            self.fast.act(self.lay.c, self.env.obs, self.n_agents,
-                          drop=(self.seed, self.learner.drop_stream, DROPOUT_P), actions=self.actions,
-                          epsilon=float(self.epsilon), act_seed=self.seed, act_offset=self.t * self.n_agents)
-            return self.actions
-        x = self.env.expand_obs(torch.float32)  # [E, R, 11, 11, 6]
-        Q = self.learner.q_values(x.view(self.n_agents, 11, 11, 6), train=True)
-        qcheck(qlib().evx_act(Q.data_ptr(), self.n_agents, self.learner.actions, float(self.epsilon), self.seed,
-                              self.t * self.n_agents, self.actions.data_ptr(), _stream()), "act")
+            self.fast.act(self.lay.c, grp.env.obs, grp.n, drop=(self.seed, self.learner.drop_stream, DROPOUT_P),
+                          actions=grp.actions, epsilon=float(self.epsilon), act_seed=self.seed, act_offset=off)
+            return
+        x = grp.env.expand_obs(torch.float32)  # [E/G, R, 11, 11, 6]
+        Q = self.learner.q_values(x.view(grp.n, 11, 11, 6), train=True)
+        qcheck(qlib().evx_act(Q.data_ptr(), grp.n, self.learner.actions, float(self.epsilon), self.seed, off,
+                              grp.actions.data_ptr(), _stream()), "act")
+
+    def act(self):
+        for grp in self.groups:
+            self._act(grp)
         return self.actions
 
     def learn(self, window=None, phase: str = "all"):
@@ -224,88 +251,108 @@ class VecTrainer:
         """One training step. Finished envs are reset inside the env.step launch
         (auto-reset: the reset of an env that ends runs in its own wave, in the shadow
         of the launch's heavy envs); the replay push takes their terminal observations.
-        The heavy-first dispatch order of the next env.step is computed on a side
-        stream, concurrently with push / learn / act. extra_reset: bool [E] of further
-        envs to reset (benchmark staggering, side stream); ev_env / ev_learn: optional
-        (start, end) CUDA events.
+        The heavy-first dispatch order of each group's next env.step is computed on a
+        side stream, concurrently with push / learn / act. extra_reset: bool [E] of
+        further envs to reset (benchmark staggering, side stream); ev_env / ev_learn:
+        optional (start, end) CUDA events (env: group 0's env.step).
 
         Default order is the reference's (act, env.step, remember, learn). With
         lagged_learn the learn step runs on its own stream from the ring as it was
         before this step's push (minus the slots the push overwrites): its gradients
-        overlap act and env.step, its weight update waits for act to have read the
-        weights, and the next act waits for the update."""
+        overlap act and env.step, its weight update waits for every group's act to have
+        read the weights, and the next acts wait for the update."""
         caller = torch.cuda.current_stream(self.device)
-        main = self.main
         if self.join_caller or extra_reset is not None:  # inputs made on the caller's stream
-            main.wait_stream(caller)
+            for grp in self.groups:
+                grp.main.wait_stream(caller)
             self.join_caller = False
-        if extra_reset is not None:
-            extra_reset.record_stream(main)  # the caller may free it before main reads it
-        with torch.cuda.stream(main):
-            self._step(main, extra_reset, ev_env, ev_learn)
-
-    def _step(self, main, extra_reset, ev_env, ev_learn):
-        if self.reset_pending:  # a cross-stream wait costs tens of us: only when there was a reset
-            main.wait_event(self.ev_reset)
-            self.reset_pending = False
-        if self.lagged:
-            main.wait_event(self.ev_learned)
-        self.act()  # issued first: its workgroups are dispatched ahead of the learn step's
+        G = self.groups
+        reset_wait, self.reset_pending = self.reset_pending, False
+        # act: every group on its own stream, after the previous update (lagged) or learn
+        for grp in G:
+            with torch.cuda.stream(grp.main):
+                if reset_wait:  # a cross-stream wait costs a gap: only when there was a reset
+                    grp.main.wait_event(self.ev_reset)
+                if self.lagged or grp.g > 0:
+                    grp.main.wait_event(self.ev_learned)
+                self._act(grp)
+                if self.lagged:
+                    grp.ev_act.record(grp.main)
         if self.lagged:
             # learn t: gradients from the ring as it stood after push t-1 (minus the slots
             # push t overwrites), overlapping act t and env.step t; the weight update
-            # waits until act t has read the weights, and act t+1 waits for it
+            # waits until every act t has read the weights, and act t+1 waits for it
             win = self.replay.window(self.n_agents)
             do_learn = self.t % self.learn_every == 0 and win[1] >= self.batch and self.fast is not None
             with torch.cuda.stream(self.lstream):
-                self.lstream.wait_event(self.ev_push)
+                for grp in G:
+                    self.lstream.wait_event(grp.ev_push)
                 if ev_learn is not None:
                     ev_learn[0].record(self.lstream)
                 if self.prio:  # push t-1 visible, the slots push t overwrites hidden
                     self.replay.expose(n_hide=self.n_agents)
                 if do_learn:
                     self.learn(window=win, phase="grads")
-            self.ev_act.record(main)
-            with torch.cuda.stream(self.lstream):
-                self.lstream.wait_event(self.ev_act)
+                for grp in G:
+                    self.lstream.wait_event(grp.ev_act)
                 self.last_loss = self.learn(phase="update") if do_learn else None
                 if ev_learn is not None:
                     ev_learn[1].record(self.lstream)
                 self.ev_learned.record(self.lstream)
-        # the order was computed on the side stream from the state after the previous step,
-        # concurrently with act; by now the event is complete, so the wait costs no gap
-        # (an order one step older would miss the envs that just auto-reset: they would be
-        # dispatched as light envs and become the launch's tail)
-        main.wait_event(self.ev_order)
-        if ev_env is not None:
-            ev_env[0].record(main)
-        self.env.step(self.actions, order=False, auto_reset=True)
-        if ev_env is not None:
-            ev_env[1].record(main)
-        self.replay.push(self.env.obs_prev, self.env.obs, self.actions, self.env.reward, self.env.done,
-                         self.n_agents, self.R, s2_term=self.env.obs_term)
-        if self.prio and not self.lagged:
-            self.replay.expose()
-        mask = None
-        if extra_reset is not None:
-            mask = extra_reset & ~self.env.done.bool()  # made on main; read on the side stream
-            mask.record_stream(self.side)
-        self.ev_push.record(main)
-        with torch.cuda.stream(self.side):
-            self.side.wait_event(self.ev_push)
-            if mask is not None:
-                self.env.reset(mask=mask)
-                self.ev_reset.record(self.side)
-                self.reset_pending = True
-            self.env.compute_order()
-            self.ev_order.record(self.side)
-        if not self.lagged:
-            if ev_learn is not None:
-                ev_learn[0].record(main)
-            if self.t % self.learn_every == 0:
-                self.last_loss = self.learn()
-            if ev_learn is not None:
-                ev_learn[1].record(main)
+        for grp in G:
+            with torch.cuda.stream(grp.main):
+                # the order was computed on the side stream from the state after the previous
+                # step, concurrently with act: by now the event is complete and the wait costs
+                # no gap (an order one step older would miss the envs that just auto-reset:
+                # they would be dispatched as light envs and become the launch's tail)
+                if len(G) == 1:
+                    grp.main.wait_event(grp.ev_order)
+                if ev_env is not None and grp.g == 0:
+                    ev_env[0].record(grp.main)
+                grp.env.step(grp.actions, order=False, auto_reset=True)
+                if ev_env is not None and grp.g == 0:
+                    ev_env[1].record(grp.main)
+                self.replay.push(grp.env.obs_prev, grp.env.obs, grp.actions, grp.env.reward, grp.env.done, grp.n,
+                                 self.R, s2_term=grp.env.obs_term)
+                grp.ev_push.record(grp.main)
+        if extra_reset is not None:  # after every group's push, on group 0's side stream (warm-up only)
+            side = G[0].side
+            extra_reset.record_stream(side)  # the caller may free it before the side stream reads it
+            with torch.cuda.stream(side):
+                side.wait_stream(caller)
+                for grp in G:
+                    side.wait_event(grp.ev_push)
+                self.env.reset(mask=extra_reset & ~self.env.done.bool())
+                self.ev_reset.record(side)
+            self.reset_pending = True
+        for grp in G:
+            # one group: the order on a side stream (overlaps act); several: on the group's own
+            # stream after its push (the groups overlap each other, and more streams than
+            # the GPU_MAX_HW_QUEUES hardware queues would serialise unrelated work)
+            st = grp.side if len(G) == 1 else grp.main
+            with torch.cuda.stream(st):
+                if st is grp.side:
+                    st.wait_event(grp.ev_push)
+                if extra_reset is not None:
+                    st.wait_event(self.ev_reset)
+                grp.env.compute_order()
+                if st is grp.side:
+                    grp.ev_order.record(st)
+        if not self.lagged:  # the reference's order: learn after every group's push, on group 0's stream
+            m = G[0].main
+            with torch.cuda.stream(m):
+                for grp in G[1:]:
+                    m.wait_event(grp.ev_push)
+                if self.prio:
+                    self.replay.expose()
+                if ev_learn is not None:
+                    ev_learn[0].record(m)
+                if self.t % self.learn_every == 0:
+                    self.last_loss = self.learn()
+                if ev_learn is not None:
+                    ev_learn[1].record(m)
+                if len(G) > 1:
+                    self.ev_learned.record(m)
         self.t += 1
 
     def sync(self):
@@ -313,10 +360,11 @@ class VecTrainer:
         the trainer's own streams and does not join the caller's stream each step (a
         cross-stream round trip costs tens of microseconds); read results after sync()."""
         cur = torch.cuda.current_stream(self.device)
-        cur.wait_stream(self.main)
+        for grp in self.groups:
+            cur.wait_stream(grp.main)
+            cur.wait_event(grp.ev_order)
         cur.wait_event(self.ev_reset)
         cur.wait_event(self.ev_learned)
-        cur.wait_event(self.ev_order)
         self.join_caller = True
 
 

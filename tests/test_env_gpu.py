@@ -268,3 +268,46 @@ def test_gpu_vs_oracle_cfg5_128_r32():
     _need_gpu()
     from evacx.layout import synthetic
     _oracle_pair(synthetic(128, 128, 32), 2276, E=5, steps=30, check_every=6, wide=True, auto_reset=True)
+
+
+def test_split_parts_on_two_streams_match_unsplit():
+    """VecEnv.split: parts sharing the parent's storage, stepped concurrently on their own
+    streams (the grouped trainer's schedule), give the unsplit env's results bit for bit;
+    the parent still reads and resets all envs."""
+    _need_gpu()
+    from evacx.env import DeviceLayout, VecEnv
+    from evacx.layout import build_tables, synthetic
+    lay = DeviceLayout(build_tables(synthetic(24, 20, 4)), 380)
+    E = 512
+    a = VecEnv(lay, E)
+    b = VecEnv(lay, E, obs_buffers=2)
+    for v in (a, b):
+        v.seed([99 + i for i in range(E)])
+        v.reset()
+    parts = b.split(2)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    g = torch.Generator(device="cuda").manual_seed(5)
+    k = (E // 2) * lay.R
+    for t in range(30):
+        acts = torch.randint(0, 5, (E * lay.R,), device="cuda", dtype=torch.int32, generator=g)
+        a.step(acts, auto_reset=True)
+        cur = torch.cuda.current_stream()
+        for i, (p, s) in enumerate(zip(parts, streams)):
+            s.wait_stream(cur)
+            with torch.cuda.stream(s):
+                p.step(acts[i * k:(i + 1) * k], auto_reset=True)
+        for s in streams:
+            cur.wait_stream(s)
+        if t == 17:  # the parent resets across both parts
+            m = torch.zeros(E, dtype=torch.bool, device="cuda")
+            m[::7] = True
+            a.reset(mask=m)
+            b.reset(mask=m)
+        torch.cuda.synchronize()
+        assert torch.equal(a.obs, b.obs), t
+        assert torch.equal(a.reward, b.reward) and torch.equal(a.done, b.done), t
+    for name in ["pk", "health", "acc", "rmap", "scal", "py_mt", "np_mt", "robots", "view"]:
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
+    st_a, st_b = a.host_state(300), b.host_state(300)
+    assert all(np.array_equal(st_a[f], st_b[f]) for f in ["pos", "health", "acc"])
+    b.check_err()

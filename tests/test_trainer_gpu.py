@@ -117,3 +117,30 @@ def test_vec_trainer_schedules(lagged):
     assert len(losses) == (40 - 1 if lagged else 40)  # lagged: the first step has an empty ring
     assert all(np.isfinite(losses))
     assert tr.replay.size == 2048
+
+
+@pytest.mark.parametrize("lagged", [False, True])
+def test_vec_trainer_groups(lagged):
+    """Two env groups on their own stream chains: the schedule trains (strict and lagged),
+    every transition lands in the ring, the env state stays valid."""
+    _need_gpu()
+    from evacx.env import DeviceLayout
+    from evacx.layout import build_tables, synthetic
+    from evacx.trainer import VecTrainer
+    lay = DeviceLayout(build_tables(synthetic(24, 20, 4)), 380)
+    tr = VecTrainer(lay, 512, batch=256, replay_capacity=1 << 15, target_every=5, lagged_learn=lagged, lr=1e-3,
+                    groups=2)
+    losses = []
+    for _ in range(12):
+        tr.step()
+        if tr.last_loss is not None:
+            losses.append(tr.last_loss)
+    tr.sync()
+    torch.cuda.synchronize()
+    tr.env.check_err()
+    assert len(losses) == (11 if lagged else 12) and all(np.isfinite([x.item() for x in losses]))
+    assert tr.replay.size == 12 * 512 * 4
+    a = tr.replay.a[:tr.replay.size].cpu().numpy()
+    assert a.min() >= 0 and a.max() <= 4
+    obs = tr.replay.s.view(-1, 8)[:tr.replay.size].cpu().numpy()
+    assert (obs[:, 4] >= 0).all() and (obs[:, 4] <= 25).all()

@@ -25,6 +25,7 @@ ap.add_argument("--people", type=int, default=2276)
 ap.add_argument("--robots", type=int, default=16)
 ap.add_argument("--warmup", type=int, default=1300)
 ap.add_argument("--stagger", type=int, default=1200)
+ap.add_argument("--no-order", action="store_true", help="identity dispatch order (no heavy workgroups)")
 args = ap.parse_args()
 E, R = args.envs, args.robots
 spec = synthetic(args.grid, args.grid, R)
@@ -35,7 +36,7 @@ env.reset()
 acts = torch.randint(0, 5, (args.warmup + 3, E * R), device="cuda", dtype=torch.int32)
 gid = torch.arange(E, device="cuda")
 for i in range(args.warmup):
-    env.step(acts[i])
+    env.step(acts[i], order=not args.no_order)
     m = env.done.bool()
     if args.stagger and i < args.stagger:
         m = m | (gid % args.stagger == i)
@@ -43,7 +44,7 @@ for i in range(args.warmup):
 stamps = torch.zeros(E * 48, dtype=torch.int64, device="cuda")
 env.out.stamps = _ptr(stamps)
 for i in range(3):
-    env.step(acts[args.warmup + i])
+    env.step(acts[args.warmup + i], order=not args.no_order)
 torch.cuda.synchronize()
 s = stamps.view(E, 48).cpu().numpy()
 cols = [c for c, _ in SLOTS]
