@@ -309,6 +309,10 @@ __device__ __forceinline__ void contested_groups(T* Lp, T* heads, T* gstart, int
 #pragma unroll
     for (int c = 0; c < 7; c++) endt[c] = 255u;
     auto build_window = [&](int b0) {
+#ifdef EVX_PROFILE
+        prof[4] += 1;
+        const long long tb0 = __builtin_amdgcn_s_memtime();
+#endif
         B = b0;
         mt_ensure_w(pyring, py_front, B + 128);
         const uint32_t t0 = mt_temper(pyring[(B + lane) & WRM]), t1 = mt_temper(pyring[(B + 64 + lane) & WRM]);
@@ -336,7 +340,13 @@ __device__ __forceinline__ void contested_groups(T* Lp, T* heads, T* gstart, int
             for (int bb = c; bb >= 2; bb--) sp = sp < 128 ? next_acc(bb - 2, sp) + 1 : 129;
             endt[c - 2] = sp <= 128 ? (uint32_t)sp : 255u;
         }
+#ifdef EVX_PROFILE
+        prof[6] += __builtin_amdgcn_s_memtime() - tb0;
+#endif
     };
+#ifdef EVX_PROFILE
+    prof[5] = ngrp;
+#endif
     int k = 0;
     while (k < ngrp) {
         const int k0 = k, W0 = pos;
@@ -1564,7 +1574,7 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     PT_DECL(lp);
     PT_DECL(grp);
     PT_DECL(mts);
-    long long cgp[4] = {0, 0, 0, 0};  // EVX_PROFILE: sort, heads, pass 1, pass 2
+    long long cgp[7] = {0, 0, 0, 0, 0, 0, 0};  // EVX_PROFILE: sort, heads, pass 1, pass 2, windows, groups, window cycles
     PT_BEGIN(lp);
     uint32_t* Lp = npring;  // the numpy ring is free now
     if (any_cont) {
@@ -1621,6 +1631,8 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     EVX_COUNT(33, cgp[1]);
     EVX_COUNT(34, cgp[2]);
     EVX_COUNT(35, cgp[3]);
+    EVX_COUNT(46, cgp[4] * 65536 + cgp[5]);
+    EVX_COUNT(47, cgp[6]);
 #endif
     EVX_STAMP(3);
 
@@ -2151,10 +2163,13 @@ __global__ __launch_bounds__(64) void env_reset_kernel(evx_layout lay, evx_state
 // workgroups take one heavy env each (its rows phase on all waves); once the rows
 // are done, waves 1.. of heavy workgroup b take the light envs at the tail of the
 // order (3 per heavy env), the remaining envs go 4 per workgroup.
+// pslots > 0: the launch ends with its heaviest envs, so their waves issue ahead of
+// the light envs' waves sharing a SIMD (s_setprio): the heavy workgroups' waves while
+// they work on their heavy env, and single-wave envs at order slots < H + pslots.
 template <int NWB>
 __global__ __launch_bounds__(64 * NWB) void env_step_kernel(evx_layout lay, evx_state st,
                                                             const int32_t* __restrict__ actions, evx_step_out out,
-                                                            int hcap) {
+                                                            int hcap, int pslots) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const int w = (int)(threadIdx.x >> 6);
     const int words = step_lds_words(lay);
@@ -2163,6 +2178,7 @@ __global__ __launch_bounds__(64 * NWB) void env_step_kernel(evx_layout lay, evx_
     const int nt = min((NWB - 1) * H, st.E - H);
     if ((int)blockIdx.x < H) {
         const int e = st.order[blockIdx.x];
+        if (pslots > 0) __builtin_amdgcn_s_setprio(2);
         int slot = -1;
         if (w == 0) {
             step_env<true>(lay, st, actions, out, e, smem);
@@ -2173,11 +2189,13 @@ __global__ __launch_bounds__(64 * NWB) void env_step_kernel(evx_layout lay, evx_
             const int t = (int)blockIdx.x * (NWB - 1) + (w - 1);
             if (t < nt) slot = st.E - nt + t;
         }
+        if (pslots > 0) __builtin_amdgcn_s_setprio(0);
         if (slot >= 0) step_env<false>(lay, st, actions, out, st.order[slot], smem + (size_t)w * words);
         return;
     }
     const int slot = H + ((int)blockIdx.x - H) * NWB + w;
     if (slot >= st.E - nt) return;
+    if (slot < H + pslots) __builtin_amdgcn_s_setprio(1);
     const int e = st.order ? st.order[slot] : slot;
     step_env<false>(lay, st, actions, out, e, smem + (size_t)w * words);
 }
@@ -2385,17 +2403,25 @@ int evx_env_step(const evx_layout* l, const evx_state* s, const int32_t* actions
     while (nwb > 1 && step_launch_lds(*l, nwb) > 160 * 1024) nwb >>= 1;
     int hmin = 0;
     const int hcap = (nwb == evx::WNW && s->order) ? heavy_cap(*l, &hmin) : 0;
+    // EVX_PRIO_SLOTS: single-wave envs at order slots < H + this run at raised priority
+    // (0 disables the priority raise, the heavy workgroups' included)
+    static int pslots_env = -2;
+    if (pslots_env == -2) {
+        const char* v = getenv("EVX_PRIO_SLOTS");
+        pslots_env = v ? atoi(v) : -1;
+    }
+    const int pslots = s->order ? (pslots_env >= 0 ? pslots_env : 0) : 0;
     const size_t blds = step_launch_lds(*l, nwb);
     const int nblk = (s->E + nwb - 1) / nwb + hcap;  // heavy envs take a workgroup each
     if (nwb == 4)
         hipLaunchKernelGGL(evx::env_step_kernel<4>, dim3(nblk), dim3(256), blds, (hipStream_t)stream, *l, *s, actions, *o,
-                           hcap);
+                           hcap, pslots);
     else if (nwb == 2)
         hipLaunchKernelGGL(evx::env_step_kernel<2>, dim3(nblk), dim3(128), blds, (hipStream_t)stream, *l, *s, actions, *o,
-                           0);
+                           0, 0);
     else
         hipLaunchKernelGGL(evx::env_step_kernel<1>, dim3(nblk), dim3(64), blds, (hipStream_t)stream, *l, *s, actions, *o,
-                           0);
+                           0, 0);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : hip_fail(e, "env_step launch");
 }

@@ -77,6 +77,10 @@ if s[:, 16:30].any():
     print("sub-phase cycle accumulators (EVX_PROFILE build):        median   slowest1%")
     for c, n in PROF:
         print(f"  {n:28s} {np.median(s[:, c]):9.0f} {s[top, c].mean():10.0f}")
+if s[:, 46].any():
+    nw, ng = s[:, 46] >> 16, s[:, 46] & 0xFFFF
+    print(f"contested pass 1: windows built median {np.median(nw):.0f} slowest1% {nw[top].mean():.1f}; groups median "
+          f"{np.median(ng):.0f} slowest1% {ng[top].mean():.1f}; window cycles slowest1% {s[top, 47].mean():.0f}")
 WIDE = [(36, "wide: pass1 (np counts)"), (37, "wide: barrier+copy"), (38, "wide: np gen"), (39, "wide: pass2"),
         (40, "wide: np store"), (41, "wide: py setup"), (42, "wide: py gen"), (43, "wide: scoring"),
         (44, "wide: movers+plan+handoff"), (45, "wide: final barrier")]
