@@ -209,9 +209,54 @@ __device__ __forceinline__ void wave_sort(T* a, int n) {
         }
 }
 
+// Ascending bitonic sort of a[0..64*R) by one wave in registers: element i = lane*R + r
+// lives in register r of lane `lane`; stages with j < R are compare-exchanges between
+// a lane's own registers, the others exchange register r with lane ^ (j / R) by
+// shuffle. One load and one store of the array instead of an LDS round trip and a
+// wave fence per stage (the LDS network's 45 stages at 512 keys).
+template <int R, typename T>
+__device__ __forceinline__ void wave_sort_reg(T* a) {
+    const int lane = (int)(threadIdx.x & 63);
+    constexpr int N = 64 * R;
+    uint32_t v[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) v[r] = a[lane * R + r];
+#pragma unroll
+    for (int k = 2; k <= N; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            if (j < R) {
+#pragma unroll
+                for (int r = 0; r < R; r++) {
+                    if (r & j) continue;
+                    const bool asc = ((lane * R + r) & k) == 0;
+                    const uint32_t x = v[r], y = v[r | j];
+                    const uint32_t lo = x < y ? x : y, hi = x < y ? y : x;
+                    v[r] = asc ? lo : hi;
+                    v[r | j] = asc ? hi : lo;
+                }
+            } else {
+                const int m = j / R;
+                const bool upper = (lane & m) != 0;
+                const bool asc = ((lane * R) & k) == 0;
+#pragma unroll
+                for (int r = 0; r < R; r++) {
+                    const uint32_t o = (uint32_t)__shfl_xor((int)v[r], m, 64);
+                    const uint32_t lo = v[r] < o ? v[r] : o, hi = v[r] < o ? o : v[r];
+                    v[r] = (upper != asc) ? lo : hi;  // the lower element keeps min when ascending
+                }
+            }
+        }
+    }
+    wave_sync();
+#pragma unroll
+    for (int r = 0; r < R; r++) a[lane * R + r] = v[r];
+    wave_sync();
+}
+
 // Sort a[0..n) ascending (distinct keys): n <= 64 by rank (each lane counts the
-// keys below its own, readlane broadcast), else bitonic over the power-of-two
-// padded array (the caller pads with 0xffffffff).
+// keys below its own, readlane broadcast); power-of-two padded n2 <= 512 (the caller
+// pads with 0xffffffff) by a register bitonic network, larger by the LDS one.
 template <typename T>
 __device__ __forceinline__ void wave_sort_keys(T* a, int n, int n2) {
     const int lane = (int)(threadIdx.x & 63);
@@ -223,6 +268,12 @@ __device__ __forceinline__ void wave_sort_keys(T* a, int n, int n2) {
         wave_sync();
         if (lane < n) a[rank] = k;
         wave_sync();
+    } else if (n2 == 128) {
+        wave_sort_reg<2>(a);
+    } else if (n2 == 256) {
+        wave_sort_reg<4>(a);
+    } else if (n2 == 512) {
+        wave_sort_reg<8>(a);
     } else {
         wave_sort(a, n2);
     }
@@ -308,6 +359,7 @@ __device__ __forceinline__ void contested_groups(T* Lp, T* heads, T* gstart, int
     uint32_t endt[7];
 #pragma unroll
     for (int c = 0; c < 7; c++) endt[c] = 255u;
+    uint32_t need = 0;  // bit c: the current chunk has groups of c <= 8 movers (only their tables are built)
     auto build_window = [&](int b0) {
 #ifdef EVX_PROFILE
         prof[4] += 1;
@@ -335,6 +387,7 @@ __device__ __forceinline__ void contested_groups(T* Lp, T* heads, T* gstart, int
         };
 #pragma unroll
         for (int c = 2; c <= 8; c++) {
+            if (!((need >> c) & 1u)) continue;
             int sp = lane;
 #pragma unroll
             for (int bb = c; bb >= 2; bb--) sp = sp < 128 ? next_acc(bb - 2, sp) + 1 : 129;
@@ -352,6 +405,14 @@ __device__ __forceinline__ void contested_groups(T* Lp, T* heads, T* gstart, int
         const int k0 = k, W0 = pos;
         uint32_t desc = 0;
         if (k0 + lane < ngrp) desc = heads[k0 + lane];
+        {
+            uint32_t nd = 0;
+#pragma unroll
+            for (int c = 2; c <= 8; c++)
+                if (__ballot(k0 + lane < ngrp && (desc & 255u) == (uint32_t)c)) nd |= 1u << c;
+            if (nd & ~need) B = -(1 << 30);  // tables of the new counts are missing: rebuild at first use
+            need |= nd;
+        }
         int wv = 0;
         int nk = 0;
         while (nk < 64 && k < ngrp && pos - W0 < SHUF_WORDS) {
@@ -2195,7 +2256,8 @@ __global__ __launch_bounds__(64 * NWB) void env_step_kernel(evx_layout lay, evx_
     }
     const int slot = H + ((int)blockIdx.x - H) * NWB + w;
     if (slot >= st.E - nt) return;
-    if (slot < H + pslots) __builtin_amdgcn_s_setprio(1);
+    // s_setprio ignores EXEC: the condition must be provably wave-uniform (readfirstlane)
+    if (__builtin_amdgcn_readfirstlane(slot) < H + pslots) __builtin_amdgcn_s_setprio(1);
     const int e = st.order ? st.order[slot] : slot;
     step_env<false>(lay, st, actions, out, e, smem + (size_t)w * words);
 }
