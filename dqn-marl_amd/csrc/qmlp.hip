@@ -202,7 +202,8 @@ __device__ __forceinline__ void fc1_tile(const Fwd& a, int m0, int ncol0, bool w
         for (int j = 0; j < NTW; j++)
 #pragma unroll
             for (int r = 0; r < 16; r++) acc[i][j][r] = 0.f;
-    bf16x8 bc[NTW][2], bn[NTW][2];
+    // B fragments two K chunks ahead (bc: this chunk, bn: the next, bf: the one after)
+    bf16x8 bc[NTW][2], bn[NTW][2], bf[NTW][2];
     auto loadB = [&](int kc, bf16x8 (&b)[NTW][2]) {
 #pragma unroll
         for (int nt = 0; nt < NTW; nt++) {
@@ -216,10 +217,11 @@ __device__ __forceinline__ void fc1_tile(const Fwd& a, int m0, int ncol0, bool w
     stash(0, 0);
     reads(1);
     loadB(0, bc);
+    loadB(1, bn);
     __syncthreads();
     for (int kc = 0; kc < NKC1; kc++) {
         const int buf = kc & 1;
-        if (kc + 1 < NKC1) loadB(kc + 1, bn);
+        if (kc + 2 < NKC1) loadB(kc + 2, bf);
 #pragma unroll
         for (int s = 0; s < 2; s++)
 #pragma unroll
@@ -236,6 +238,8 @@ __device__ __forceinline__ void fc1_tile(const Fwd& a, int m0, int ncol0, bool w
             for (int nt = 0; nt < NTW; nt++) {
                 bc[nt][0] = bn[nt][0];
                 bc[nt][1] = bn[nt][1];
+                bn[nt][0] = bf[nt][0];
+                bn[nt][1] = bf[nt][1];
             }
         }
         __syncthreads();

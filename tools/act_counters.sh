@@ -1,0 +1,15 @@
+#!/bin/bash
+# SQ counters of qact_kernel (fused act) on the MLP microbenchmark: two PMC passes.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/actpmc
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+timeout -s KILL 120 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU \
+    -d "$OUT/p1" -o run --output-format csv -- python3 "$R/tools/qmlp_bench.py" > "$OUT/p1.log" 2>&1 || exit 1
+timeout -s KILL 120 rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE \
+    -d "$OUT/p2" -o run --output-format csv -- python3 "$R/tools/qmlp_bench.py" > "$OUT/p2.log" 2>&1 || exit 1
+for p in p1 p2; do
+  f=$(find "$OUT/$p" -name "*counter_collection.csv" | head -1)
+  python3 "$R/tools/sq_summary.py" "$f" qact_kernel
+done
