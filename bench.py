@@ -58,6 +58,18 @@ def qnet_flops(n_act, B, hidden=512, in_dim=484, actions=5):
     return n_act * fwd + B * (2 * fwd + bwd)
 
 
+def cfg_name(args):
+    """BASELINE.json configs: cfg2 64x64 x 8 robots, cfg3 128x128 x 16 (the headline), cfg4
+    256x256 conv Q-net, cfg5 128x128 x 32 with prioritized replay."""
+    if args.grid == 64 and args.robots == 8:
+        return "cfg2"
+    if args.grid == 256:
+        return "cfg4"
+    if args.robots == 32 and args.replay == "prioritized":
+        return "cfg5"
+    return "cfg3" if (args.grid, args.robots) == (128, 16) else f"custom {args.grid}x{args.grid} R{args.robots}"
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -72,6 +84,9 @@ def parse():
     ap.add_argument("--robots", type=int, default=16)
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--precision", choices=["bf16", "f32"], default="bf16")
+    ap.add_argument("--qnet", choices=["mlp", "conv"], default="mlp",
+                    help="conv: the reference's DQNNetwork (3 conv3x3 + fc stack) on the general MFMA GEMMs "
+                         "(cfg4); mlp: the fused 726-512-256-5 kernels")
     ap.add_argument("--mode", choices=["train", "env"], default="train")
     ap.add_argument("--env-steps", type=int, default=100, help="extra env-only timed steps (0 = skip)")
     ap.add_argument("--strict-steps", type=int, default=100,
@@ -114,7 +129,8 @@ def main():
     tables = build_tables(spec)
     lay = DeviceLayout(tables, P)
     hook = make_allreduce_hook(dist, world) if dist is not None else None
-    tr = VecTrainer(lay, E, env_offset=rank * E, precision=args.precision, batch=args.batch, grad_hook=hook,
+    tr = VecTrainer(lay, E, env_offset=rank * E, kind=args.qnet, precision=args.precision, batch=args.batch,
+                    grad_hook=hook,
                     lagged_learn=args.schedule == "lagged", replay=args.replay,
                     replay_capacity=args.replay_capacity, groups=args.groups if args.mode == "train" else 1)
     env = tr.env
@@ -243,12 +259,14 @@ def main():
             "dtype": "f64" if args.mode == "env" else f"f64 env + {args.precision} Q-net",
             "data": "synthetic",
             "config": {
-                "workload": (f"{'cfg5' if R == 32 and args.replay == 'prioritized' else 'cfg3'} per-GPU share: {L}x{W} synthetic layout, {P} people, {R} robots, {E} envs/GPU; "
+                "workload": (f"{cfg_name(args)} per-GPU share: {L}x{W} synthetic layout, {P} people, {R} robots, {E} envs/GPU; "
                              + ("full training step: act + env.step + replay push + learn (B="
                                 f"{args.batch}) + auto-reset" if args.mode == "train"
                                 else "env.step + auto-reset, uniform random actions")),
                 "envs_per_gpu": E, "grid": f"{L}x{W}", "people": P, "robots": R, "mode": args.mode,
-                "batch": args.batch, "qnet": "MLP 726-512-256-5", "schedule": args.schedule,
+                "batch": args.batch, "schedule": args.schedule if tr.fast is not None else "strict",
+                "qnet": ("MLP 726-512-256-5" if args.qnet == "mlp"
+                         else "DQNNetwork conv 6-32-64-128 + 15488-512-256-5"),
                 "replay": args.replay, "groups": args.groups if args.mode == "train" else 1,
                 "parallelism": f"data-parallel over {world} GPU(s): envs sharded, grad all-reduce (RCCL) per learn",
             },
@@ -263,7 +281,7 @@ def main():
                          "launches_timed": len(timed)},
             "cpu_baseline": cpu,
         }
-        if learn_ms is not None:
+        if learn_ms is not None and args.qnet == "mlp":
             fl = qnet_flops(0, args.batch)
             line["roofline_learn"] = {"bound": "mfma", "achieved": fl / (learn_ms * 1e-3) / 1e12,
                                       "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
