@@ -93,6 +93,9 @@ __host__ __device__ __forceinline__ size_t w1_tile(int t, int kc, int s) {
 __host__ __device__ __forceinline__ size_t w2_tile(int t, int kc, int s) {
     return ((size_t)(t * (HID / 32) + kc) * 2 + s) * 512;
 }
+// fc1's occupancy columns (reference channel 1 of cells 0..127, >= 121 zero), K = 128
+// in 4 chunks of 32
+__host__ __device__ __forceinline__ size_t w1o_tile(int t, int kc, int s) { return ((size_t)(t * 4 + kc) * 2 + s) * 512; }
 // fc2.weight^T for the backward (columns = fc2 inputs, K = fc2 outputs)
 __host__ __device__ __forceinline__ size_t w2t_tile(int t, int kc, int s) {
     return ((size_t)(t * (HID2 / 32) + kc) * 2 + s) * 512;
@@ -124,6 +127,14 @@ struct Fwd {
     int32_t* actions;
     float epsilon;
     uint64_t act_seed, act_offset;
+    // act fast path (qact_kernel): fc1's pre-activation at zero occupancy per window centre
+    // at fire step stat_fs ([(L+2)(W+2)][512] f32, bias included), and fc1's occupancy
+    // columns in w1o_tile order; null = the full path only
+    const float* stat;
+    const __bf16* w1o;
+    int stat_fs;
+    // qfc1_kernel raw mode: f32 pre-activation (acc + bias, no ReLU / dropout) [N][512]
+    float* raw;
 };
 
 // One row's window in the static feature map (evx_layout.obs_feat): base index of
@@ -293,6 +304,18 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void qfc1_kernel(Fwd a0
     float bias[NTW];
 #pragma unroll
     for (int nt = 0; nt < NTW; nt++) bias[nt] = a.b1[ncol0 + nt * 32 + (lane & 31)];
+    if (a.raw) {  // pre-activation table (evx_qmlp_stat): acc + bias as f32, 128-B row segments
+#pragma unroll
+        for (int mt = 0; mt < MT; mt++)
+#pragma unroll
+            for (int nt = 0; nt < NTW; nt++)
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    const int row = m0 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                    if (row < a.N) a.raw[(size_t)row * HID + ncol0 + nt * 32 + (lane & 31)] = acc[mt][nt][r] + bias[nt];
+                }
+        return;
+    }
 #pragma unroll
     for (int mt = 0; mt < MT; mt++) {
         if (mt) __syncthreads();  // the previous slab has been stored
@@ -360,21 +383,95 @@ __device__ __forceinline__ void fc3_act(const Fwd& a, const float* hrow, const f
 // qfc1_kernel<4, 2, 8>, H1 kept in LDS (bf16, never written to HBM), fc2 with wave w
 // on columns [32w, 32w + 32) over all 128 rows (A fragments from the H1 tile, W2
 // fragments from L2), H2 (f32) back into the same LDS, fc3 + epsilon-greedy as
-// qfc23_kernel. Q and actions are bit-identical to qfc1 + qfc23 (same MFMA k order,
-// same fc3 summation). Dynamic LDS: ACT_LDS bytes.
+// qfc23_kernel. Dynamic LDS: ACT_LDS bytes.
+//
+// Fast path (a.stat set, every row of the tile at fire step stat_fs -- every env older
+// than 180 steps: the fire never resets): fc1's inputs other than the occupancy bits
+// depend only on the window centre and the fire step, so fc1 = stat[centre] (the
+// pre-activation at zero occupancy, bias included, rebuilt by evx_qmlp_stat after each
+// weight update) + the occupancy columns times the 121 bits: the accumulators start
+// from the table and K shrinks from 512 to 128, with the A fragments made in registers
+// from the bits (no LDS staging, no barriers). Same products, f32 sums in another order
+// (Q within f32 rounding of the full path).
 constexpr int ACT_HP = HID + 8;                                  // H1 row pitch (bf16)
 constexpr int ACT_H2P = HID2 + 1;                                // H2 row pitch (f32)
 constexpr int ACT_HBYTES = 128 * ACT_HP * 2;                     // 133,120 >= 128 * 257 * 4
-constexpr int ACT_LDS = ACT_HBYTES + NACT * HID2 * 4;            // + W3
+constexpr int ACT_LDS = ACT_HBYTES + NACT * HID2 * 4 + 128 * 4;  // + W3 + window centres
 __global__ __launch_bounds__(512, 1) void qact_kernel(Fwd a) {
     extern __shared__ __attribute__((aligned(16))) char dsm[];
     auto H1s = reinterpret_cast<__bf16 (*)[ACT_HP]>(dsm);
     auto H2s = reinterpret_cast<float (*)[ACT_H2P]>(dsm);
     auto W3s = reinterpret_cast<float (*)[HID2]>(dsm + ACT_HBYTES);
+    int* posS = reinterpret_cast<int*>(dsm + ACT_HBYTES + NACT * HID2 * 4);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
     const int m0 = blockIdx.x * 128;
     for (int i = tid; i < NACT * HID2; i += 512) W3s[i / HID2][i % HID2] = a.w3[i];
-    {  // fc1 -> H1 tile
+    bool fast = false;
+    if (a.stat) {  // tile-uniform: every row at the table's fire step, centre inside the map
+        bool ok = true;
+        if (tid < 128) {
+            int pos = 0;
+            if (m0 + tid < a.N) {
+                const evx_obs ob = a.obs[m0 + tid];
+                ok = min(max(ob.fire_step, 0), a.t_max) == a.stat_fs && ob.cx >= 0 && ob.cx <= a.L + 1 && ob.cy >= 0 && ob.cy <= a.W + 1;
+                pos = ok ? ob.cx * (a.W + 2) + ob.cy : 0;
+            }
+            posS[tid] = pos;
+        }
+        fast = __syncthreads_and(ok);  // also publishes posS
+    }
+    if (fast) {  // fc1 = stat[centre] + occupancy columns x bits -> H1 tile
+        f32x16 acc[4][2];
+        const int col0 = w * 64 + (lane & 31);
+#pragma unroll
+        for (int mt = 0; mt < 4; mt++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int rl = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const float* srow = a.stat + (size_t)posS[rl] * HID + col0;
+                acc[mt][0][r] = srow[0];
+                acc[mt][1][r] = srow[32];
+            }
+        uint32_t occ[4][4];
+#pragma unroll
+        for (int mt = 0; mt < 4; mt++) {
+            const int row = m0 + mt * 32 + (lane & 31);
+            uint4 o = make_uint4(0u, 0u, 0u, 0u);
+            if (row < a.N) o = *reinterpret_cast<const uint4*>(&a.obs[row].occ[0]);
+            occ[mt][0] = o.x;
+            occ[mt][1] = o.y;
+            occ[mt][2] = o.z;
+            occ[mt][3] = o.w;
+        }
+        const uint32_t one = 0x3f80u;
+#pragma unroll
+        for (int ks = 0; ks < 8; ks++) {  // k-step: cells 16 ks + 8 h .. + 7 of the 128
+            bf16x8 b[2];
+#pragma unroll
+            for (int nt = 0; nt < 2; nt++)
+                b[nt] = *reinterpret_cast<const bf16x8*>(a.w1o + w1o_tile(w * 2 + nt, ks >> 1, ks & 1) + lane * 8);
+            const int c0 = ks * 16 + 8 * h;  // multiple of 8: the 8 bits sit in one word
+#pragma unroll
+            for (int mt = 0; mt < 4; mt++) {
+                const uint32_t wd = (c0 >> 5) == 0 ? occ[mt][0] : (c0 >> 5) == 1 ? occ[mt][1]
+                                  : (c0 >> 5) == 2 ? occ[mt][2] : occ[mt][3];
+                const uint32_t bits = (wd >> (c0 & 31)) & 0xffu;
+                uint32_t av4[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    av4[j] = ((bits >> (2 * j)) & 1u) * one | (((bits >> (2 * j + 1)) & 1u) * one) << 16;
+                const bf16x8 av = __builtin_bit_cast(bf16x8, av4);
+#pragma unroll
+                for (int nt = 0; nt < 2; nt++)
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, b[nt], acc[mt][nt], 0, 0, 0);
+            }
+        }
+        const float zero[2] = {0.f, 0.f};  // the table holds the bias
+#pragma unroll
+        for (int mt = 0; mt < 4; mt++)
+            fc1_slab<2, ACT_HP>(a, acc[mt], zero, m0 + mt * 32, 0, w * 64,
+                                reinterpret_cast<__bf16 (*)[ACT_HP]>(&H1s[mt * 32][0]));
+    } else {  // fc1 -> H1 tile
         f32x16 acc[4][2];
         fc1_tile<4, 2, 8>(a, m0, w * 64, false, dsm, acc);  // ends with a barrier: A buffers free
         float bias[2];
@@ -522,8 +619,14 @@ __global__ __launch_bounds__(256, 2) void qfc23_kernel(Fwd a0, Fwd a1) {
 __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ w1, const float* __restrict__ b1,
                                                    const float* __restrict__ w2, __bf16* __restrict__ w1b,
                                                    float* __restrict__ b1c, __bf16* __restrict__ w2b,
-                                                   __bf16* __restrict__ w2t) {
+                                                   __bf16* __restrict__ w2t, __bf16* __restrict__ w1o) {
     const int i = blockIdx.x * 256 + threadIdx.x;
+    if (w1o && i < HID * 128) {  // occupancy columns, w1o_tile order
+        const int j = i & 7, l = (i >> 3) & 63, blk = i >> 9;
+        const int s = blk & 1, kc = (blk >> 1) & 3, t = blk >> 3;
+        const int n = t * 32 + (l & 31), c = kc * 32 + s * 16 + 8 * (l >> 5) + j;
+        w1o[i] = (__bf16)(c < NCELL ? w1[n * K1 + c * 6 + 1] : 0.f);
+    }
     if (i < HID * K1P) {  // destination index -> (tile, chunk, step, lane, j)
         const int j = i & 7, l = (i >> 3) & 63, blk = i >> 9;
         const int s = blk & 1, kc = (blk >> 1) % NKC1, t = blk / (2 * NKC1);
@@ -802,12 +905,12 @@ extern "C" {
 const char* evx_qmlp_last_error(void) { return m_err; }
 
 int evx_qmlp_pack(const float* w1, const float* b1, const float* w2, uint16_t* w1b, float* b1c, uint16_t* w2b,
-                  uint16_t* w2t, void* stream) {
+                  uint16_t* w2t, uint16_t* w1o, void* stream) {
     if (!w1 || !b1 || !w2 || !w1b || !b1c || !w2b) return mfail(-22, "qmlp_pack: NULL argument");
     const int n = evxm::HID * evxm::K1P;
     hipLaunchKernelGGL(evxm::pack_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, w1, b1, w2,
                        reinterpret_cast<__bf16*>(w1b), b1c, reinterpret_cast<__bf16*>(w2b),
-                       reinterpret_cast<__bf16*>(w2t));
+                       reinterpret_cast<__bf16*>(w2t), reinterpret_cast<__bf16*>(w1o));
     return mlaunch("qmlp_pack");
 }
 
@@ -852,6 +955,10 @@ static int make_fwd(const evx_layout* lay, const evx_obs* obs, int32_t n, const 
     a.epsilon = out->epsilon;
     a.act_seed = out->act_seed;
     a.act_offset = out->act_offset;
+    a.w1o = reinterpret_cast<const __bf16*>(p->w1o);
+    a.stat = p->w1o ? p->stat : nullptr;
+    a.stat_fs = p->stat_fs;
+    a.raw = nullptr;
     return 0;
 }
 
@@ -906,6 +1013,21 @@ int evx_qmlp_act(const evx_layout* lay, const evx_obs* obs, int32_t n, const evx
     hipLaunchKernelGGL(evxm::qact_kernel, dim3((unsigned)((n + 127) / 128)), dim3(512), evxm::ACT_LDS,
                        (hipStream_t)stream, a);
     return mlaunch("qact");
+}
+
+int evx_qmlp_stat(const evx_layout* lay, const evx_obs* obs, int32_t n, const evx_qmlp_params* p, float* out,
+                  void* stream) {
+    if (n <= 0) return 0;
+    if (!out) return mfail(-22, "qmlp_stat: NULL out");
+    evx_qmlp_fwd_out o{};
+    o.h1 = reinterpret_cast<uint16_t*>(out);  // not written in raw mode
+    evxm::Fwd a;
+    int rc = make_fwd(lay, obs, n, p, nullptr, &o, a);
+    if (rc) return rc;
+    a.h1 = nullptr;
+    a.stat = nullptr;
+    a.raw = out;
+    return launch_fwd(a, a, n, 1, false, (hipStream_t)stream);
 }
 
 int evx_qmlp_forward2(const evx_layout* lay, int32_t n, const evx_obs* obs0, const evx_qmlp_params* p0,

@@ -27,7 +27,8 @@ def compact_ref_cols() -> np.ndarray:
 
 
 class evx_qmlp_params(C.Structure):
-    _fields_ = [(n, C.c_void_p) for n in ["w1", "b1c", "w2", "w2t", "b2", "w3", "b3"]]
+    _fields_ = [(n, C.c_void_p) for n in ["w1", "b1c", "w2", "w2t", "b2", "w3", "b3", "w1o", "stat"]] + \
+        [("stat_fs", C.c_int32), ("pad0", C.c_int32)]
 
 
 class evx_qmlp_dropout(C.Structure):
@@ -52,7 +53,9 @@ def mlib():
     L = _lib.lib()
     if not _inited:
         L.evx_qmlp_last_error.restype = C.c_char_p
-        L.evx_qmlp_pack.argtypes = [C.c_void_p] * 8
+        L.evx_qmlp_pack.argtypes = [C.c_void_p] * 9
+        L.evx_qmlp_stat.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(evx_qmlp_params), C.c_void_p,
+                                    C.c_void_p]
         L.evx_qmlp_forward.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(evx_qmlp_params),
                                        C.POINTER(evx_qmlp_dropout), C.POINTER(evx_qmlp_fwd_out), C.c_void_p]
         L.evx_qmlp_act.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(evx_qmlp_params),
@@ -88,15 +91,45 @@ class MLPFast:
         self.w2b = torch.zeros(HID2 * HID, **i16)
         self.w2t = torch.zeros(HID * HID2, **i16)
         self.b1c = torch.zeros(HID, dtype=torch.float32, device=self.device)
+        self.w1o = torch.zeros(HID * 128, **i16)  # fc1's occupancy columns (act fast path)
         self.c = evx_qmlp_params(w1=self.w1b.data_ptr(), b1c=self.b1c.data_ptr(), w2=self.w2b.data_ptr(),
                                  w2t=self.w2t.data_ptr(), b2=params["fc2.bias"].data_ptr(),
                                  w3=params["fc3.weight"].data_ptr(), b3=params["fc3.bias"].data_ptr())
+        self._static = None  # (lay_c, centre obs, table) of attach_static
         self.repack()
 
     def repack(self):
         mcheck(mlib().evx_qmlp_pack(self.P["fc1.weight"].data_ptr(), self.P["fc1.bias"].data_ptr(),
                                     self.P["fc2.weight"].data_ptr(), self.w1b.data_ptr(), self.b1c.data_ptr(),
-                                    self.w2b.data_ptr(), self.w2t.data_ptr(), _stream()), "qmlp_pack")
+                                    self.w2b.data_ptr(), self.w2t.data_ptr(), self.w1o.data_ptr(), _stream()),
+               "qmlp_pack")
+        if self._static is not None:
+            self._rebuild_static()
+
+    def attach_static(self, lay_c, L: int, W: int, t_max: int):
+        """Enable act()'s fast path for observations at fire step >= t_max (the fire has
+        stopped spreading): fc1's pre-activation at zero occupancy for every window centre
+        of the layout, [(L+2)(W+2)][512] f32, rebuilt with every repack."""
+        cx, cy = np.meshgrid(np.arange(L + 2), np.arange(W + 2), indexing="ij")
+        ob = np.zeros(((L + 2) * (W + 2), 8), np.int32)
+        ob[:, 4], ob[:, 5], ob[:, 6] = cx.ravel(), cy.ravel(), t_max
+        self._static = (lay_c, torch.from_numpy(ob).to(self.device),
+                        torch.empty((L + 2) * (W + 2), HID, dtype=torch.float32, device=self.device))
+        self._rebuild_static()
+        self.c.w1o, self.c.stat, self.c.stat_fs = self.w1o.data_ptr(), self._static[2].data_ptr(), int(t_max)
+
+    def detach_static(self):
+        self._static = None
+        self.c.w1o = self.c.stat = None
+
+    def _rebuild_static(self):
+        lay_c, ob, T = self._static
+        self.stat_table(lay_c, ob, ob.shape[0], T)
+
+    def stat_table(self, lay_c, obs: torch.Tensor, n: int, out: torch.Tensor):
+        """evx_qmlp_stat: fc1's pre-activation (f32, bias included) of n observations -> out [n][512]."""
+        mcheck(mlib().evx_qmlp_stat(C.byref(lay_c), obs.data_ptr(), n, C.byref(self.c), out.data_ptr(), _stream()),
+               "qmlp_stat")
 
     def forward(self, lay_c, obs: torch.Tensor, n: int, h1: torch.Tensor, drop=None, x=None, h2=None, q=None,
                 actions=None, epsilon=0.0, act_seed=0, act_offset=0):

@@ -184,6 +184,11 @@ class VecTrainer:
         self.fast = self.learner.fast
         if self.fast is None:
             self.lagged = False  # the split learn step needs the fused bf16 MLP path
+        elif os.environ.get("EVX_ACT_STATIC", "0") == "1":
+            # act fast path (off by default: the per-update table rebuild on the learn stream costs what
+            # the act saves, tools/gpu_ab_static.sh): envs past the fire's last step start fc1 from a table
+            lc = self.lay.c
+            self.fast.attach_static(lc, lc.L, lc.W, lc.t_max)
 
     def _act(self, grp: _Group):
         """DQNAgent.act in train mode for one group's robots: dropout active, epsilon-greedy

@@ -276,6 +276,11 @@ typedef struct {
     const float *b2;      /* [256] */
     const float *w3;      /* [5][256] f32 fc3.weight */
     const float *b3;      /* [5] */
+    /* act fast path (evx_qmlp_act), optional: fc1's occupancy columns [512][128] bf16 (evx_qmlp_pack's
+     * w1o) and the pre-activation table of evx_qmlp_stat for observations at fire step stat_fs */
+    const uint16_t *w1o;
+    const float *stat;
+    int32_t stat_fs, pad0;
 } evx_qmlp_params;
 
 typedef struct {
@@ -299,12 +304,19 @@ typedef struct {
  * reference's channel 0 is identically zero and channel 5 is the constant centre
  * one-hot, folded into b1c. */
 int evx_qmlp_pack(const float *w1, const float *b1, const float *w2, uint16_t *w1b, float *b1c, uint16_t *w2b,
-                  uint16_t *w2t, void *stream);
+                  uint16_t *w2t, uint16_t *w1o, void *stream);
+/* fc1's pre-activation (X W1^T + b1, f32, no ReLU / dropout) of n observations -> out [n][512]:
+ * with obs = every window centre of the layout at one fire step and zero occupancy this is the
+ * act fast path's table (evx_qmlp_params.stat; rebuild after every weight update) */
+int evx_qmlp_stat(const evx_layout *lay, const evx_obs *obs, int32_t n, const evx_qmlp_params *p, float *out,
+                  void *stream);
 int evx_qmlp_forward(const evx_layout *lay, const evx_obs *obs, int32_t n, const evx_qmlp_params *p,
                      const evx_qmlp_dropout *drop, const evx_qmlp_fwd_out *out, void *stream);
 /* DQNAgent.act (agents/dqn_agent.py:101-124) in one launch: the forward of
  * evx_qmlp_forward with H1 and H2 kept on chip (out->h1, x, h2 ignored), writing
- * out->q and/or out->actions; bit-identical to evx_qmlp_forward's. */
+ * out->q and/or out->actions; bit-identical to evx_qmlp_forward's, except that 128-row tiles
+ * whose observations are all at p->stat_fs start fc1 from p->stat (when p->w1o / p->stat are
+ * set): the same products summed in another order. */
 int evx_qmlp_act(const evx_layout *lay, const evx_obs *obs, int32_t n, const evx_qmlp_params *p,
                  const evx_qmlp_dropout *drop, const evx_qmlp_fwd_out *out, void *stream);
 /* Two forwards of n rows in one launch pair (the learner's online and target nets). */

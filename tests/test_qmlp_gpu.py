@@ -208,3 +208,62 @@ def test_fused_act_matches_two_kernel_forward(eps):
     assert torch.equal(q1, q2[:n])
     assert torch.equal(a1, a2[:n])
     assert torch.all(q2[n:] == 9.0) and torch.all(a2[n:] == -1)
+
+
+def test_static_table_is_fc1_preactivation():
+    """evx_qmlp_stat (the act fast path's table) == fc1's pre-activation of the same
+    kernel: bf16(relu(T)) equals evx_qmlp_forward's H1 bit for bit on zero-occupancy
+    observations at the last fire step (no dropout)."""
+    _need_gpu()
+    from evacx.qmlp import HID, MLPFast
+    from evacx.qnet import Learner
+    lay, env = _env_obs(E=8, steps=1, R=4, grid=40, people=100)
+    lr = Learner(kind="mlp", precision="bf16", seed=5)
+    fast = MLPFast(lr.online, "cuda")
+    c = lay.c
+    fast.attach_static(c, c.L, c.W, c.t_max)
+    ob, T = fast._static[1], fast._static[2]
+    n = ob.shape[0]
+    assert n == (c.L + 2) * (c.W + 2)
+    h1 = torch.empty(n * HID, dtype=torch.int16, device="cuda")
+    fast.forward(c, ob, n, h1)
+    torch.cuda.synchronize()
+    ref = torch.relu(T).to(torch.bfloat16).view(torch.int16).view(-1)
+    assert torch.equal(ref, h1)
+
+
+@pytest.mark.parametrize("eps", [0.0, 0.3])
+def test_act_fast_path_matches_full_path(eps):
+    """evx_qmlp_act with the static table (tiles whose rows are all at the last fire step
+    start fc1 from T[centre] + occupancy columns x bits) vs without it: the same products
+    summed in another f32 order, so H1 may differ by one bf16 rounding step -- Q within
+    2e-3 of its scale, greedy actions equal on >= 99% of rows. A tile with one row at
+    an earlier fire step takes the full path (exact)."""
+    _need_gpu()
+    from evacx.qmlp import MLPFast
+    from evacx.qnet import Learner
+    lay, env = _env_obs(E=600, steps=4, R=16, grid=64, people=500)
+    c = lay.c
+    n = env.E * lay.R - 5
+    ob = env.obs.view(-1, 8).clone()
+    ob[:, 6] = c.t_max + 3  # past the last fire step (clamped to it)
+    ob[130, 6] = 2  # tile 1 (rows 128..255) keeps the full path
+    lr = Learner(kind="mlp", precision="bf16", seed=8)
+    slow = MLPFast(lr.online, "cuda")
+    fastp = MLPFast(lr.online, "cuda")
+    fastp.attach_static(c, c.L, c.W, c.t_max)
+    kw = dict(drop=(3, 9, 0.2), epsilon=eps, act_seed=11, act_offset=7)
+    q1 = torch.empty(n, 5, device="cuda")
+    a1 = torch.empty(n, dtype=torch.int32, device="cuda")
+    q2 = torch.empty(n, 5, device="cuda")
+    a2 = torch.empty(n, dtype=torch.int32, device="cuda")
+    slow.act(c, ob, n, q=q1, actions=a1, **kw)
+    fastp.act(c, ob, n, q=q2, actions=a2, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(q1[128:256], q2[128:256]) and torch.equal(a1[128:256], a2[128:256])
+    scale = q1.abs().max().item()
+    err = (q1 - q2).abs().max().item()
+    assert err <= 2e-3 * scale + 1e-6, (err, scale)
+    assert (q1 != q2).any()  # the fast path did run
+    agree = (a1 == a2).float().mean().item()
+    assert agree >= 0.99, agree

@@ -37,6 +37,26 @@ b.record()
 torch.cuda.synchronize()
 us = a.elapsed_time(b) / 20 * 1e3
 print(f"{'fused act (qact_kernel)':26s} n={n_all:6d}: {us:8.1f} us  {flops_row * n_all / us / 1e6:7.1f} TF/s (whole MLP flops)")
+# fast path: every env past the fire's last step (fc1 from the per-centre table)
+obs_late = env.obs.view(-1, 8).clone()
+obs_late[:, 6] = lay.c.t_max
+fast.attach_static(lay.c, lay.c.L, lay.c.W, lay.c.t_max)
+for _ in range(3):
+    fast.act(lay.c, obs_late, n_all, drop=(1, 2, 0.2), actions=act, epsilon=0.1)
+a.record()
+for _ in range(20):
+    fast.act(lay.c, obs_late, n_all, drop=(1, 2, 0.2), actions=act, epsilon=0.1)
+b.record()
+torch.cuda.synchronize()
+us = a.elapsed_time(b) / 20 * 1e3
+print(f"{'fused act, static table':26s} n={n_all:6d}: {us:8.1f} us")
+a.record()
+for _ in range(20):
+    fast._rebuild_static()
+b.record()
+torch.cuda.synchronize()
+print(f"{'static table rebuild':26s} n={fast._static[1].shape[0]:6d}: {a.elapsed_time(b) / 20 * 1e3:8.1f} us")
+fast.detach_static()
 for n, kw, name in [(n_all, dict(actions=act, epsilon=0.1), "act (fc1+fc23+egreedy)"),
                     (n_all, dict(), "fc1 only"),
                     (4096, dict(x=x, h2=h2, q=q), "learn fwd (saves x,h2)"),
