@@ -253,11 +253,12 @@ class LayoutTables:
         return self.spec.W + 2
 
 
-def build_tables(spec: LayoutSpec, t_max: Optional[int] = None) -> LayoutTables:
+def map_space(spec: LayoutSpec):
+    """Map.__init__ (envs/map.py:38-79): the pre-potential grid ``space`` (walls and
+    barriers inf, exit 1, else 0) and ``barrier_list``."""
     L, W = spec.L, spec.W
     GX, GY = L + 2, W + 2
     inf = float("inf")
-    # Map.__init__ (envs/map.py:38-79)
     space = np.zeros((GX, GY))
     barrier_list = []
     for j in range(GY):
@@ -280,11 +281,49 @@ def build_tables(spec: LayoutSpec, t_max: Optional[int] = None) -> LayoutTables:
     if (ex, ey) in barrier_list:
         barrier_list.remove((ex, ey))
 
+    return space, barrier_list
+
+
+def _check_valid(L, W, sp, x, y):
+    """Map.Check_Valid (envs/map.py:85-92) on grid ``sp``."""
+    x, y = int(x), int(y)
+    if x >= L + 1 or x <= 0 or y >= W + 1 or y <= 0:
+        return False
+    return sp[x][y] != float("inf")
+
+
+def potential_inputs(spec: LayoutSpec, danger0: Optional[np.ndarray] = None):
+    """Inputs of the device floor field (evx_floor_field) for one layout:
+    Check_Valid on the pre-potential grid (u8 [GX, GY]), the exit sources (u8), and the
+    fire term 200 * danger(0, (i, j)) ** 2 (f64; envs/map.py:143-146) evaluated with
+    CPython floats as the reference does -- from ``danger0`` [GX, GY] (danger at integer
+    coordinates, t = 0) when given, else from the layout's fire schedule."""
+    L, W = spec.L, spec.W
+    GX, GY = L + 2, W + 2
+    space, _ = map_space(spec)
+    valid = np.zeros((GX, GY), np.uint8)
+    for x in range(GX):
+        for y in range(GY):
+            valid[x, y] = _check_valid(L, W, space, x, y)
+    src = np.zeros((GX, GY), np.uint8)
+    src[spec.exit[0], spec.exit[1]] = 1
+    if danger0 is None:
+        pf = FireSchedule(spec.map_fire(), spec.additional_fire, spec.fire_max_steps, spec.base_radius,
+                          spec.max_radius, spec.min_danger)
+        danger0 = np.array([[pf.danger_scalar(0, (i, j)) for j in range(GY)] for i in range(GX)])
+    pen = np.array([[200 * (float(d) ** 2) for d in row] for row in np.asarray(danger0, np.float64).tolist()])
+    return valid, src, pen
+
+
+def build_tables(spec: LayoutSpec, t_max: Optional[int] = None) -> LayoutTables:
+    L, W = spec.L, spec.W
+    GX, GY = L + 2, W + 2
+    inf = float("inf")
+    ex, ey = spec.exit
+    space, barrier_list = map_space(spec)
+
     def check_valid(sp, x, y):
-        x, y = int(x), int(y)
-        if x >= L + 1 or x <= 0 or y >= W + 1 or y <= 0:
-            return False
-        return sp[x][y] != inf
+        return _check_valid(L, W, sp, x, y)
 
     pfire = FireSchedule(spec.map_fire(), spec.additional_fire, spec.fire_max_steps,
                          spec.base_radius, spec.max_radius, spec.min_danger)

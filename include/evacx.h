@@ -254,6 +254,19 @@ int evx_prio_sample(const evx_replay *rp, const evx_prio *t, int32_t B, double b
 
 const char *evx_prio_last_error(void);
 
+/* ---- static floor field on the device ------------------------------------
+ * Replaces Map.Init_Potential (envs/map.py:127-148) for n_layouts layouts of one padded grid
+ * size GX x GY (= (L+2) x (W+2)), one workgroup each, bit-identical to the reference's heapq
+ * Dijkstra. Per layout, row-major [GX][GY]:
+ *   valid  u8  Map.Check_Valid on the pre-potential grid (1 <= x <= L, 1 <= y <= W, space != inf)
+ *   source u8  the exits (Map.Exit: distance 1)
+ *   pen    f64 200 * danger(t=0, (i, j)) ** 2 (envs/map.py:143-146; NULL = no fire term)
+ *   floor  f64 out: Map.space after Init_Potential (inf where unreachable)
+ *   passes i32 [n_layouts] relaxation passes used (may be NULL; diagnostics) */
+int evx_floor_field(int32_t n_layouts, int32_t GX, int32_t GY, const uint8_t *valid, const uint8_t *source,
+                    const double *pen, double *floor, int32_t *passes, void *stream);
+const char *evx_floor_last_error(void);
+
 int evx_gather_obs(const evx_obs *src, const int64_t *idx, int32_t n, evx_obs *dst, void *stream);
 /* DQNNetwork conv layers (agents/dqn_agent.py:22-24) as im2col + GEMM on 11x11 maps */
 int evx_im2col3x3(const float *x, int32_t B, int32_t C, int32_t nhwc, float *cols, void *stream);

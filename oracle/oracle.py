@@ -214,3 +214,42 @@ class PrioTrees:
         lib().orc_prio_sample(_p(self.sum), _p(self.mn), C.c_int64(self.C), C.c_int(B), C.c_double(beta),
                               C.c_uint64(seed), C.c_uint64(offset), _p(idx), _p(w))
         return idx, w
+
+
+# MoveTO (Louvre_Evacuation/envs/map.py:11-19)
+_MDX = (1, 0, -1, 0, 1, -1, -1, 1)
+_MDY = (0, -1, 0, 1, -1, -1, 1, 1)
+
+
+def floor_field(valid, source, pen=None):
+    """Map.Init_Potential (Louvre_Evacuation/envs/map.py:127-148) restated over arrays:
+    valid u8 [GX, GY] = Check_Valid on the pre-potential grid, source u8 = the exits
+    (distance 1, pushed in row-major order), pen f64 = 200 * danger(t=0) ** 2 added to
+    every finite cell (:143-146). heapq of (dist, x, y), strict '<', no stale-entry skip,
+    exactly as the reference loop. Pure Python: small grids only (tests)."""
+    import heapq
+    valid = np.asarray(valid)
+    GX, GY = valid.shape
+    inf = float("inf")
+    mind = [[inf] * GY for _ in range(GX)]
+    heap = []
+    for x, y in zip(*np.nonzero(np.asarray(source))):
+        x, y = int(x), int(y)
+        mind[x][y] = 1
+        heapq.heappush(heap, (1, x, y))
+    vl = valid.tolist()
+    while heap:
+        cd, x, y = heapq.heappop(heap)
+        for i in range(8):
+            nx, ny = x + _MDX[i], y + _MDY[i]
+            cost = 1.0 if i < 4 else 1.4
+            if 0 <= nx < GX and 0 <= ny < GY and vl[nx][ny]:
+                nd = cd + cost
+                if nd < mind[nx][ny]:
+                    mind[nx][ny] = nd
+                    heapq.heappush(heap, (nd, nx, ny))
+    out = np.array(mind, np.float64)
+    if pen is not None:
+        fin = np.isfinite(out)
+        out[fin] = out[fin] + np.asarray(pen, np.float64)[fin]
+    return out
