@@ -2228,7 +2228,10 @@ __global__ __launch_bounds__(64) void env_reset_kernel(evx_layout lay, evx_state
 // the light envs' waves sharing a SIMD (s_setprio): the heavy workgroups' waves while
 // they work on their heavy env, and single-wave envs at order slots < H + pslots.
 template <int NWB>
-__global__ __launch_bounds__(64 * NWB) void env_step_kernel(evx_layout lay, evx_state st,
+#ifndef EVX_ENV_MINW
+#define EVX_ENV_MINW 1
+#endif
+__global__ __launch_bounds__(64 * NWB, EVX_ENV_MINW) void env_step_kernel(evx_layout lay, evx_state st,
                                                             const int32_t* __restrict__ actions, evx_step_out out,
                                                             int hcap, int pslots) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];

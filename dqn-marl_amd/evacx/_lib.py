@@ -11,7 +11,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 # EVACX_LIB selects another in-tree build (e.g. libevacx_prof.so, the diagnostic one)
-LIB_PATH = os.path.join(HERE, os.environ.get("EVACX_LIB", "libevacx.so"))
+LIB_PATH = os.environ.get("EVX_LIB") or os.path.join(HERE, os.environ.get("EVACX_LIB", "libevacx.so"))  # EVX_LIB: experiment builds (tools/)
 
 
 class EvacxError(RuntimeError):
