@@ -2233,13 +2233,22 @@ template <int NWB>
 #endif
 __global__ __launch_bounds__(64 * NWB, EVX_ENV_MINW) void env_step_kernel(evx_layout lay, evx_state st,
                                                             const int32_t* __restrict__ actions, evx_step_out out,
-                                                            int hcap, int pslots) {
+                                                            int hcap, int pslots, int part) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const int w = (int)(threadIdx.x >> 6);
     const int words = step_lds_words(lay);
     const int H = (NWB == WNW && st.order && hcap > 0) ? min(hcap, st.order[st.E]) : 0;
     // light envs order[H, E): the last nt of them go to the heavy workgroups' spare waves
-    const int nt = min((NWB - 1) * H, st.E - H);
+    // (only when one launch steps them all: part 0)
+    const int nt = part == 0 ? min((NWB - 1) * H, st.E - H) : 0;
+    if (part == 2) {  // light envs only: no heavy workgroups in this launch
+        const int slot = H + (int)blockIdx.x * NWB + w;
+        if (slot >= st.E) return;
+        const int e = st.order ? st.order[slot] : slot;
+        step_env<false>(lay, st, actions, out, e, smem + (size_t)w * words);
+        return;
+    }
+    if (part == 1 && (int)blockIdx.x >= H) return;  // heavy envs only
     if ((int)blockIdx.x < H) {
         const int e = st.order[blockIdx.x];
         if (pslots > 0) __builtin_amdgcn_s_setprio(2);
@@ -2433,6 +2442,12 @@ int64_t evx_step_scratch_words(const evx_layout* l) {
 }
 
 int evx_env_step(const evx_layout* l, const evx_state* s, const int32_t* actions, const evx_step_out* o, void* stream) {
+    return evx_env_step_part(l, s, actions, o, 0, stream);
+}
+
+int evx_env_step_part(const evx_layout* l, const evx_state* s, const int32_t* actions, const evx_step_out* o,
+                      int32_t part, void* stream) {
+    if (part < 0 || part > 2) return fail(-22, "env_step: part must be 0, 1 or 2");
     int rc = check_layout(l);
     if (rc) return rc;
     if (!s || !o || !actions || !o->reward || !o->done || !o->obs) return fail(-22, "NULL argument");
@@ -2477,16 +2492,18 @@ int evx_env_step(const evx_layout* l, const evx_state* s, const int32_t* actions
     }
     const int pslots = s->order ? (pslots_env >= 0 ? pslots_env : 0) : 0;
     const size_t blds = step_launch_lds(*l, nwb);
-    const int nblk = (s->E + nwb - 1) / nwb + hcap;  // heavy envs take a workgroup each
+    // heavy envs take a workgroup each; part 1: only those, part 2: only the rest
+    if (part == 1 && hcap == 0) return 0;  // no heavy workgroups for this layout: part 2 steps every env
+    const int nblk = part == 1 ? hcap : (s->E + nwb - 1) / nwb + (part == 0 ? hcap : 0);
     if (nwb == 4)
         hipLaunchKernelGGL(evx::env_step_kernel<4>, dim3(nblk), dim3(256), blds, (hipStream_t)stream, *l, *s, actions, *o,
-                           hcap, pslots);
+                           hcap, pslots, (int)part);
     else if (nwb == 2)
         hipLaunchKernelGGL(evx::env_step_kernel<2>, dim3(nblk), dim3(128), blds, (hipStream_t)stream, *l, *s, actions, *o,
-                           0, 0);
+                           0, 0, (int)part);
     else
         hipLaunchKernelGGL(evx::env_step_kernel<1>, dim3(nblk), dim3(64), blds, (hipStream_t)stream, *l, *s, actions, *o,
-                           0, 0);
+                           0, 0, (int)part);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : hip_fail(e, "env_step launch");
 }

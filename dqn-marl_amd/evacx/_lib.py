@@ -59,6 +59,9 @@ def lib():
             getattr(L, name).restype = C.c_int
         L.evx_env_step.argtypes = [C.POINTER(evx_layout), C.POINTER(evx_state), C.c_void_p,
                                    C.POINTER(evx_step_out), C.c_void_p]
+        L.evx_env_step_part.restype = C.c_int
+        L.evx_env_step_part.argtypes = [C.POINTER(evx_layout), C.POINTER(evx_state), C.c_void_p,
+                                        C.POINTER(evx_step_out), C.c_int32, C.c_void_p]
         L.evx_env_reset.argtypes = [C.POINTER(evx_layout), C.POINTER(evx_state), C.c_void_p, C.c_void_p,
                                     C.c_void_p, C.c_void_p]
         L.evx_obs_expand_f32.argtypes = [C.POINTER(evx_layout), C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p]

@@ -338,11 +338,14 @@ class VecEnv:
             self._order_ahead = True
         _lib.check(_lib.lib().evx_env_order(C.byref(self.lay.c), C.byref(c), _stream()), "evx_env_order")
 
-    def step(self, actions: torch.Tensor, order: bool = True, auto_reset: bool = False):
+    def step(self, actions: torch.Tensor, order: bool = True, auto_reset: bool = False, part: int = 0):
         """order=False: the caller already ran compute_order() for this state (see
         evacx.trainer). auto_reset: envs that finish are reset inside the same launch
         (evx_env_reset semantics); their terminal observations land in self.obs_term
-        and self.obs holds the post-reset ones (self.done still flags them)."""
+        and self.obs holds the post-reset ones (self.done still flags them).
+        part: 0 = one launch; 1 then 2 = the heavy envs of the dispatch order, then the
+        rest (evx_env_step_part; the two launches may run on different streams, part 1
+        issued first: it flips the observation buffer and computes the order)."""
         a = actions.to(torch.int32).contiguous()
         assert a.numel() == self.E * self.lay.R
         if self._parts:  # split: every part steps its envs (same stream here)
@@ -350,16 +353,23 @@ class VecEnv:
             for i, p in enumerate(self._parts):
                 p.step(a[i * k:(i + 1) * k], order=order, auto_reset=auto_reset)
             return
-        if order:
-            self.compute_order()
-        if len(self._obs) == 2:  # write into the other buffer: the current one becomes obs_prev
-            self._ob ^= 1
-            self.out.obs = _ptr(self._obs[self._ob])
-        if auto_reset and self.obs_term is None:
-            self.obs_term = torch.zeros_like(self.obs)
-        self.out.obs_term = self.obs_term.data_ptr() if auto_reset else None
-        _lib.check(_lib.lib().evx_env_step(C.byref(self.lay.c), C.byref(self.c), a.data_ptr(), C.byref(self.out),
-                                           _stream()), "evx_env_step")
+        if part != 2:
+            if order:
+                self.compute_order()
+            if len(self._obs) == 2:  # write into the other buffer: the current one becomes obs_prev
+                self._ob ^= 1
+                self.out.obs = _ptr(self._obs[self._ob])
+            if auto_reset and self.obs_term is None:
+                self.obs_term = torch.zeros_like(self.obs)
+            self.out.obs_term = self.obs_term.data_ptr() if auto_reset else None
+        if part == 0:
+            _lib.check(_lib.lib().evx_env_step(C.byref(self.lay.c), C.byref(self.c), a.data_ptr(), C.byref(self.out),
+                                               _stream()), "evx_env_step")
+        else:
+            _lib.check(_lib.lib().evx_env_step_part(C.byref(self.lay.c), C.byref(self.c), a.data_ptr(),
+                                                    C.byref(self.out), int(part), _stream()), "evx_env_step_part")
+            if part == 1:
+                return
         if self._order_ahead:  # the order computed ahead is the one the following step reads
             self._ord ^= 1
             self.c.order = _ptr(self._orders[self._ord])

@@ -108,6 +108,12 @@ typedef struct {
  * actions: [E*R] int32; values outside 0..4 are ignored as in the reference. */
 int evx_env_step(const evx_layout *lay, const evx_state *st, const int32_t *actions,
                  const evx_step_out *out, void *stream);
+/* The same step in two launches that may run concurrently on two streams: part 1 steps the
+ * heavy envs of the dispatch order (order[0, order[E]), one workgroup each), part 2 every
+ * other env; part 0 = evx_env_step. Both parts of one step must be launched with the same
+ * state, order, actions and outputs; results are identical to the one-launch step. */
+int evx_env_step_part(const evx_layout *l, const evx_state *s, const int32_t *actions, const evx_step_out *o,
+                      int32_t part, void *stream);
 
 /* Replaces EvacuationEnv.reset / EvacuationEnvMulti.reset (envs/evacuation_env.py:61-82,
  * envs/evacuation_env_multi.py:31-42) incl. People placement (envs/people.py:183-194).

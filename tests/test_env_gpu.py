@@ -311,3 +311,45 @@ def test_split_parts_on_two_streams_match_unsplit():
     st_a, st_b = a.host_state(300), b.host_state(300)
     assert all(np.array_equal(st_a[f], st_b[f]) for f in ["pos", "health", "acc"])
     b.check_err()
+
+
+def test_heavy_and_light_parts_on_two_streams_match_one_launch():
+    """evx_env_step_part: the heavy envs of the dispatch order (part 1) and the rest
+    (part 2) stepped by two launches on two streams, concurrently, give the one-launch
+    step's results bit for bit (fused resets included)."""
+    _need_gpu()
+    from evacx.env import DeviceLayout, VecEnv
+    from evacx.layout import build_tables, synthetic
+    lay = DeviceLayout(build_tables(synthetic(24, 20, 4)), 380)
+    E = 512
+    a = VecEnv(lay, E)
+    b = VecEnv(lay, E, obs_buffers=2)
+    for v in (a, b):
+        v.seed([71 + i for i in range(E)])
+        v.reset()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    g = torch.Generator(device="cuda").manual_seed(9)
+    max_heavy = 0
+    for t in range(40):
+        acts = torch.randint(0, 5, (E * lay.R,), device="cuda", dtype=torch.int32, generator=g)
+        a.step(acts, auto_reset=True)
+        cur = torch.cuda.current_stream()
+        b.compute_order()
+        s1.wait_stream(cur)
+        s2.wait_stream(cur)
+        with torch.cuda.stream(s1):
+            b.step(acts, order=False, auto_reset=True, part=1)
+        with torch.cuda.stream(s2):
+            b.step(acts, order=False, auto_reset=True, part=2)
+        cur.wait_stream(s1)
+        cur.wait_stream(s2)
+        torch.cuda.synchronize()
+        max_heavy = max(max_heavy, int(b.order[E].item()))
+        assert torch.equal(a.obs, b.obs), t
+        assert torch.equal(a.obs_term, b.obs_term), t
+        assert torch.equal(a.reward, b.reward) and torch.equal(a.done, b.done), t
+    for name in ["pk", "health", "acc", "rmap", "scal", "py_mt", "np_mt", "robots", "view"]:
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
+    assert max_heavy > 0
+    a.check_err()
+    b.check_err()
