@@ -785,12 +785,16 @@ __global__ __launch_bounds__(256, 2) void qdz1_kernel(Bwd a) {
 
 // C[m][n] += sum_k A[k][m] B[k][n] (both operands K-major bf16), 128x128 tiles of
 // 4 waves (2x2 of 64x64), K chunks of 32 staged transposed in LDS; gridDim.z splits
-// K and the partial tiles are added with f32 atomics. Columns n >= Nc are skipped;
-// remap: column n goes to ref_col(n) (fc1's compact K -> the reference's 726).
+// K. part == NULL: the partial tiles are added to C with f32 atomics; else split z
+// stores its tile to part[z][m][0, gridDim.x * TT) and gemm_reduce_kernel adds the
+// splits in z order (deterministic, and no atomic traffic through L2). Columns
+// n >= Nc are skipped; remap: column n goes to ref_col(n) (fc1's compact K -> the
+// reference's 726).
 constexpr int TT = 128, TKC = 32, TPAD = TKC + 8;
 __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const __bf16* __restrict__ A, int lda,
                                                          const __bf16* __restrict__ Bm, int ldb, int K, int M, int Nc,
-                                                         int kper, float* __restrict__ C, int ldc, int remap) {
+                                                         int kper, float* __restrict__ C, int ldc, int remap,
+                                                         float* __restrict__ part) {
     __shared__ __attribute__((aligned(16))) __bf16 As[TT][TPAD];
     __shared__ __attribute__((aligned(16))) __bf16 Bs[TT][TPAD];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
@@ -858,6 +862,22 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const __bf16* __restric
         }
         __syncthreads();
     }
+    if (part) {
+        const int Np = (int)gridDim.x * TT;
+        float* pz = part + (size_t)blockIdx.z * M * Np;
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const int n = n0 + wn * 64 + j * 32 + (lane & 31);
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    if (m < M) pz[(size_t)m * Np + n] = acc[i][j][r];
+                }
+        }
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < 2; j++) {
         const int n = n0 + wn * 64 + j * 32 + (lane & 31);
@@ -870,6 +890,29 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const __bf16* __restric
                 const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
                 if (m < M) atomicAdd(&C[(size_t)m * ldc + nc], acc[i][j][r]);
             }
+    }
+}
+
+// C[m][remap(n)] += sum over z = 0.. S-1 (in order) of part[z][m][n], 4 columns per thread
+__global__ __launch_bounds__(256) void gemm_reduce_kernel(const float* __restrict__ part, int S, int M, int Np, int Nc,
+                                                          float* __restrict__ C, int ldc, int remap) {
+    const int q = (int)(blockIdx.x * 256 + threadIdx.x), nq = Nc >> 2;
+    if (q >= M * nq) return;
+    const int m = q / nq, n = (q - m * nq) * 4;
+    const float* src = part + (size_t)m * Np + n;
+    float4 acc = *reinterpret_cast<const float4*>(src);
+    for (int z = 1; z < S; z++) {
+        const float4 v = *reinterpret_cast<const float4*>(src + (size_t)z * M * Np);
+        acc.x += v.x;
+        acc.y += v.y;
+        acc.z += v.z;
+        acc.w += v.w;
+    }
+    const float a4[4] = {acc.x, acc.y, acc.z, acc.w};
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        const int nc = remap ? ref_col(n + t) : n + t;
+        C[(size_t)m * ldc + nc] += a4[t];
     }
 }
 
@@ -1044,6 +1087,20 @@ int evx_qmlp_forward2(const evx_layout* lay, int32_t n, const evx_obs* obs0, con
     return launch_fwd(a0, a1, n, 2, true, (hipStream_t)stream);
 }
 
+// split-K of the weight-gradient GEMMs: about 256 workgroups over `tiles` output tiles
+static int ksplit_kper(int B, int tiles) {
+    const int S = (256 + tiles - 1) / tiles;
+    int kper = (B + S - 1) / S;
+    return (kper + evxm::TKC - 1) / evxm::TKC * evxm::TKC;
+}
+
+int64_t evx_qmlp_backward_part_floats(int32_t B) {
+    if (B <= 0) return 0;
+    const int64_t s2 = (B + ksplit_kper(B, 8) - 1) / ksplit_kper(B, 8);
+    const int64_t s1 = (B + ksplit_kper(B, 24) - 1) / ksplit_kper(B, 24);
+    return std::max(s2 * evxm::HID2 * evxm::HID, s1 * evxm::HID * evxm::K1P);
+}
+
 int evx_qmlp_backward(const evx_qmlp_params* p, int32_t B, const float* dq, const uint16_t* x, const uint16_t* h1,
                       const float* h2, float drop_p, uint16_t* dz2, uint16_t* dz1, const evx_qmlp_grads* g,
                       int32_t zero_grads, void* stream) {
@@ -1079,23 +1136,23 @@ int evx_qmlp_backward(const evx_qmlp_params* p, int32_t B, const float* dq, cons
     hipLaunchKernelGGL(evxm::qdz1_kernel, dim3((unsigned)((B + evxm::RM - 1) / evxm::RM), evxm::HID / 128), dim3(256),
                        0, st, a);
     // dW2 = dZ2^T H1 (256 x 512), dW1 = dZ1^T X (512 x 484 compact -> 726); K = B split over gridDim.z
-    auto ksplit = [&](int tiles) {
-        int S = (256 + tiles - 1) / tiles;
-        int kper = (B + S - 1) / S;
-        kper = (kper + evxm::TKC - 1) / evxm::TKC * evxm::TKC;
-        return kper;
-    };
     {
-        const int kper = ksplit(8);
-        hipLaunchKernelGGL(evxm::gemm_tn_kernel, dim3(evxm::HID / evxm::TT, evxm::HID2 / evxm::TT, (B + kper - 1) / kper),
-                           dim3(256), 0, st, a.dz2, evxm::HID2, a.h1, evxm::HID, B, evxm::HID2, evxm::HID, kper, g->w2,
-                           evxm::HID, 0);
+        const int kper = ksplit_kper(B, 8), S = (B + kper - 1) / kper;
+        hipLaunchKernelGGL(evxm::gemm_tn_kernel, dim3(evxm::HID / evxm::TT, evxm::HID2 / evxm::TT, S), dim3(256), 0, st,
+                           a.dz2, evxm::HID2, a.h1, evxm::HID, B, evxm::HID2, evxm::HID, kper, g->w2, evxm::HID, 0,
+                           g->part);
+        if (g->part)
+            hipLaunchKernelGGL(evxm::gemm_reduce_kernel, dim3((evxm::HID2 * evxm::HID / 4 + 255) / 256), dim3(256), 0, st,
+                               g->part, S, evxm::HID2, evxm::HID, evxm::HID, g->w2, evxm::HID, 0);
     }
     {
-        const int kper = ksplit(24);
-        hipLaunchKernelGGL(evxm::gemm_tn_kernel, dim3(evxm::K1P / evxm::TT, evxm::HID / evxm::TT, (B + kper - 1) / kper),
-                           dim3(256), 0, st, a.dz1, evxm::HID, a.x, evxm::K1P, B, evxm::HID, 4 * evxm::NCELL, kper,
-                           g->w1, evxm::K1, 1);
+        const int kper = ksplit_kper(B, 24), S = (B + kper - 1) / kper;
+        hipLaunchKernelGGL(evxm::gemm_tn_kernel, dim3(evxm::K1P / evxm::TT, evxm::HID / evxm::TT, S), dim3(256), 0, st,
+                           a.dz1, evxm::HID, a.x, evxm::K1P, B, evxm::HID, 4 * evxm::NCELL, kper, g->w1, evxm::K1, 1,
+                           g->part);
+        if (g->part)
+            hipLaunchKernelGGL(evxm::gemm_reduce_kernel, dim3((evxm::HID * evxm::NCELL + 255) / 256), dim3(256), 0, st,
+                               g->part, S, evxm::HID, evxm::K1P, 4 * evxm::NCELL, g->w1, evxm::K1, 1);
     }
     return mlaunch("qmlp_backward");
 }

@@ -8,6 +8,7 @@ fc1/fc2 weights are re-packed from the fp32 master parameters after every update
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import numpy as np
 import torch
@@ -36,7 +37,7 @@ class evx_qmlp_dropout(C.Structure):
 
 
 class evx_qmlp_grads(C.Structure):
-    _fields_ = [(n, C.c_void_p) for n in ["w1", "b1", "w2", "b2", "w3", "b3"]]
+    _fields_ = [(n, C.c_void_p) for n in ["w1", "b1", "w2", "b2", "w3", "b3", "part"]]
 
 
 class evx_qmlp_fwd_out(C.Structure):
@@ -46,6 +47,7 @@ class evx_qmlp_fwd_out(C.Structure):
 
 
 _inited = False
+_BWD_ATOMIC = os.environ.get("EVX_BWD_ATOMIC", "0") == "1"  # weight-gradient split-K by f32 atomics (A/B)
 
 
 def mlib():
@@ -64,6 +66,8 @@ def mlib():
                                         C.POINTER(evx_qmlp_dropout), C.POINTER(evx_qmlp_fwd_out), C.c_void_p,
                                         C.POINTER(evx_qmlp_params), C.POINTER(evx_qmlp_dropout),
                                         C.POINTER(evx_qmlp_fwd_out), C.c_void_p]
+        L.evx_qmlp_backward_part_floats.restype = C.c_int64
+        L.evx_qmlp_backward_part_floats.argtypes = [C.c_int32]
         L.evx_qmlp_backward.argtypes = [C.POINTER(evx_qmlp_params), C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
                                         C.c_void_p, C.c_float, C.c_void_p, C.c_void_p, C.POINTER(evx_qmlp_grads),
                                         C.c_int32, C.c_void_p]
@@ -96,6 +100,7 @@ class MLPFast:
                                  w2t=self.w2t.data_ptr(), b2=params["fc2.bias"].data_ptr(),
                                  w3=params["fc3.weight"].data_ptr(), b3=params["fc3.bias"].data_ptr())
         self._static = None  # (lay_c, centre obs, table) of attach_static
+        self._part = None  # split-K scratch of the weight-gradient GEMMs (backward)
         self.repack()
 
     def repack(self):
@@ -173,6 +178,11 @@ class MLPFast:
         """d loss / d params of the saved forward into `grads` (evacx.qnet.FlatParams)."""
         g = evx_qmlp_grads(**{k: grads[f"fc{k[1]}.{'weight' if k[0] == 'w' else 'bias'}"].data_ptr()
                               for k in ["w1", "b1", "w2", "b2", "w3", "b3"]})
+        if not _BWD_ATOMIC:  # split-K partials summed in a fixed order (deterministic, no f32 atomics)
+            nf = int(mlib().evx_qmlp_backward_part_floats(B))
+            if self._part is None or self._part.numel() < nf:
+                self._part = torch.empty(nf, dtype=torch.float32, device=self.device)
+            g.part = self._part.data_ptr()
         mcheck(mlib().evx_qmlp_backward(C.byref(self.c), B, dq.data_ptr(), x.data_ptr(), h1.data_ptr(), h2.data_ptr(),
                                         float(drop_p), dz2.data_ptr(), dz1.data_ptr(), C.byref(g), int(zero),
                                         _stream()), "qmlp_backward")

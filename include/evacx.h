@@ -347,7 +347,12 @@ int evx_qmlp_forward2(const evx_layout *lay, int32_t n, const evx_obs *obs0, con
 /* fp32 gradient tensors (the reference's parameter shapes: fc1.weight [512][726], ...) */
 typedef struct {
     float *w1, *b1, *w2, *b2, *w3, *b3;
+    /* optional split-K scratch of the weight-gradient GEMMs, evx_qmlp_backward_part_floats(B)
+     * floats: the splits are summed in a fixed order (deterministic gradients, no f32 atomics);
+     * NULL = atomics */
+    float *part;
 } evx_qmlp_grads;
+int64_t evx_qmlp_backward_part_floats(int32_t B);
 
 /* loss.backward() of DQNAgent.learn (agents/dqn_agent.py:150-158) for the saved online
  * forward (x, h1, h2 of evx_qmlp_forward) given dQ = d loss / d Q [B][5]. Gradients are
