@@ -114,7 +114,7 @@ __device__ __forceinline__ bool in_map(const Geo& g, const uint32_t* validb, int
 
 // Compact observation of one robot built by one wave (bits by ballot).
 __device__ __forceinline__ void write_obs(const Geo& g, const uint32_t* validb, const uint32_t* rmapb, int cx,
-                                          int cy, int fs, evx_obs* dst) {
+                                          int cy, int fs, uint32_t lid, evx_obs* dst) {
     const int lane = threadIdx.x & 63;
     bool b0 = false, b1 = false;
     {
@@ -130,7 +130,7 @@ __device__ __forceinline__ void write_obs(const Geo& g, const uint32_t* validb, 
     const unsigned long long m0 = __ballot(b0), m1 = __ballot(b1);
     if (lane == 0) {
         uint4 a = make_uint4((uint32_t)m0, (uint32_t)(m0 >> 32), (uint32_t)m1, (uint32_t)(m1 >> 32));
-        uint4 b = make_uint4((uint32_t)cx, (uint32_t)cy, (uint32_t)fs, 0u);
+        uint4 b = make_uint4((uint32_t)cx, (uint32_t)cy, (uint32_t)fs, lid);
         reinterpret_cast<uint4*>(dst)[0] = a;
         reinterpret_cast<uint4*>(dst)[1] = b;
     }
@@ -2018,7 +2018,8 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     evx_obs* obs_dst = ar ? out.obs_term : out.obs;
     for (int r = 0; r < R; r++) {
         const uint32_t c = (r == 0) ? view : robots[r];
-        write_obs(g, nullptr, rmapb, rp_x(c), rp_y(c), fs1, obs_dst + (size_t)e * R + r);
+        write_obs(g, nullptr, rmapb, rp_x(c), rp_y(c), fs1, st.layout_idx ? (uint32_t)st.layout_idx[e] : 0u,
+                  obs_dst + (size_t)e * R + r);
     }
     EVX_STAMP(8);
     if (ar) {
@@ -2200,7 +2201,8 @@ __device__ __forceinline__ void reset_one(const evx_layout& lay, const evx_state
     if (obs) {
         for (int r = 0; r < R; r++) {
             const uint32_t c = (r == 0) ? view : st.robots[(size_t)e * R + r];
-            write_obs(g, validb, rmapb, rp_x(c), rp_y(c), fs, obs + (size_t)e * R + r);
+            write_obs(g, validb, rmapb, rp_x(c), rp_y(c), fs, st.layout_idx ? (uint32_t)st.layout_idx[e] : 0u,
+                      obs + (size_t)e * R + r);
         }
     }
     mt_store_w(pyring, py_front, pos, st.py_mt + (size_t)e * EVX_MT_WORDS);
@@ -2211,12 +2213,27 @@ __device__ __forceinline__ void reset_one(const evx_layout& lay, const evx_state
 #endif
 }
 
+// The layout of env e: the launch's own (MULTI == false), or its entry of the layout set,
+// read through the constant address space (scalar loads, like the kernel argument's).
+typedef __attribute__((address_space(4))) const evx_layout ConstLayout;
+template <bool MULTI>
+__device__ __forceinline__ const evx_layout& lay_of(const evx_layout& lay, const evx_state& st, int e) {
+    if constexpr (MULTI) {
+        const int li = __builtin_amdgcn_readfirstlane(st.layout_idx[e]);
+        const ConstLayout* p = (const ConstLayout*)(reinterpret_cast<const evx_layout*>(lay.layout_set) + li);
+        return *(const evx_layout*)p;
+    } else {
+        return lay;
+    }
+}
+
+template <bool MULTI>
 __global__ __launch_bounds__(64) void env_reset_kernel(evx_layout lay, evx_state st, const uint8_t* __restrict__ mask,
                                                        evx_obs* obs, int32_t* err) {
     const int e = blockIdx.x;
     if (mask && !mask[e]) return;
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    reset_one(lay, st, e, smem, obs, err);
+    reset_one(lay_of<MULTI>(lay, st, e), st, e, smem, obs, err);
 }
 
 // NWB waves per workgroup, one env per wave, no block barrier between envs, in the
@@ -2227,10 +2244,10 @@ __global__ __launch_bounds__(64) void env_reset_kernel(evx_layout lay, evx_state
 // pslots > 0: the launch ends with its heaviest envs, so their waves issue ahead of
 // the light envs' waves sharing a SIMD (s_setprio): the heavy workgroups' waves while
 // they work on their heavy env, and single-wave envs at order slots < H + pslots.
-template <int NWB>
 #ifndef EVX_ENV_MINW
 #define EVX_ENV_MINW 1
 #endif
+template <int NWB, bool MULTI>
 __global__ __launch_bounds__(64 * NWB, EVX_ENV_MINW) void env_step_kernel(evx_layout lay, evx_state st,
                                                             const int32_t* __restrict__ actions, evx_step_out out,
                                                             int hcap, int pslots, int part) {
@@ -2245,7 +2262,7 @@ __global__ __launch_bounds__(64 * NWB, EVX_ENV_MINW) void env_step_kernel(evx_la
         const int slot = H + (int)blockIdx.x * NWB + w;
         if (slot >= st.E) return;
         const int e = st.order ? st.order[slot] : slot;
-        step_env<false>(lay, st, actions, out, e, smem + (size_t)w * words);
+        step_env<false>(lay_of<MULTI>(lay, st, e), st, actions, out, e, smem + (size_t)w * words);
         return;
     }
     if (part == 1 && (int)blockIdx.x >= H) return;  // heavy envs only
@@ -2254,16 +2271,19 @@ __global__ __launch_bounds__(64 * NWB, EVX_ENV_MINW) void env_step_kernel(evx_la
         if (pslots > 0) __builtin_amdgcn_s_setprio(2);
         int slot = -1;
         if (w == 0) {
-            step_env<true>(lay, st, actions, out, e, smem);
+            step_env<true>(lay_of<MULTI>(lay, st, e), st, actions, out, e, smem);
         } else {
             __syncthreads();  // wave 0 has published the rows inputs
-            rows_wide(lay, st, e, smem);
-            if (w == 1) wide_health_sum(lay, st, e, smem);
+            rows_wide(lay_of<MULTI>(lay, st, e), st, e, smem);
+            if (w == 1) wide_health_sum(lay_of<MULTI>(lay, st, e), st, e, smem);
             const int t = (int)blockIdx.x * (NWB - 1) + (w - 1);
             if (t < nt) slot = st.E - nt + t;
         }
         if (pslots > 0) __builtin_amdgcn_s_setprio(0);
-        if (slot >= 0) step_env<false>(lay, st, actions, out, st.order[slot], smem + (size_t)w * words);
+        if (slot >= 0) {
+            const int e2 = st.order[slot];
+            step_env<false>(lay_of<MULTI>(lay, st, e2), st, actions, out, e2, smem + (size_t)w * words);
+        }
         return;
     }
     const int slot = H + ((int)blockIdx.x - H) * NWB + w;
@@ -2271,7 +2291,7 @@ __global__ __launch_bounds__(64 * NWB, EVX_ENV_MINW) void env_step_kernel(evx_la
     // s_setprio ignores EXEC: the condition must be provably wave-uniform (readfirstlane)
     if (__builtin_amdgcn_readfirstlane(slot) < H + pslots) __builtin_amdgcn_s_setprio(1);
     const int e = st.order ? st.order[slot] : slot;
-    step_env<false>(lay, st, actions, out, e, smem + (size_t)w * words);
+    step_env<false>(lay_of<MULTI>(lay, st, e), st, actions, out, e, smem + (size_t)w * words);
 }
 
 // ------------------------------------------------------- dispatch order
@@ -2345,7 +2365,7 @@ __global__ __launch_bounds__(1024) void env_order_kernel(evx_layout lay, evx_sta
 // ---------------------------------------------------- observation expand
 // EvacuationEnv._get_state (envs/evacuation_env.py:84-120) from the compact form.
 template <typename T>
-__global__ __launch_bounds__(256) void obs_expand_kernel(evx_layout lay, const evx_obs* __restrict__ obs, int64_t n,
+__global__ __launch_bounds__(256) void obs_expand_kernel(evx_layout lay0, const evx_obs* __restrict__ obs, int64_t n,
                                                          T* __restrict__ out) {
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t total = n * 726;
@@ -2355,6 +2375,7 @@ __global__ __launch_bounds__(256) void obs_expand_kernel(evx_layout lay, const e
     const int c = rem / 6, ch = rem - c * 6;
     const int i = c / 11, j = c - i * 11;
     const evx_obs ob = obs[o];
+    const evx_layout& lay = lay0.layout_set ? reinterpret_cast<const evx_layout*>(lay0.layout_set)[ob.layout] : lay0;
     const int mx = ob.cx + i - 5, my = ob.cy + j - 5;
     const int GY = lay.W + 2;
     const bool inb = mx >= 0 && mx <= lay.L + 1 && my >= 0 && my <= lay.W + 1;
@@ -2463,14 +2484,13 @@ int evx_env_step_part(const evx_layout* l, const evx_state* s, const int32_t* ac
     }
     const size_t lds = step_lds_bytes(*l);
     if (lds > 160 * 1024) return fail(-7, "layout needs more than 160 KiB of LDS");
+    const bool multi = l->layout_set && s->layout_idx;
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)evx::env_step_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
-        (void)hipFuncSetAttribute((const void*)evx::env_step_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
-        (void)hipFuncSetAttribute((const void*)evx::env_step_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
+        const void* ks[6] = {(const void*)evx::env_step_kernel<1, false>, (const void*)evx::env_step_kernel<2, false>,
+                             (const void*)evx::env_step_kernel<4, false>, (const void*)evx::env_step_kernel<1, true>,
+                             (const void*)evx::env_step_kernel<2, true>, (const void*)evx::env_step_kernel<4, true>};
+        for (const void* k : ks) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_set = true;
     }
     // envs per workgroup (one per wave): EVX_STEP_NWB overrides (diagnostics)
@@ -2495,15 +2515,25 @@ int evx_env_step_part(const evx_layout* l, const evx_state* s, const int32_t* ac
     // heavy envs take a workgroup each; part 1: only those, part 2: only the rest
     if (part == 1 && hcap == 0) return 0;  // no heavy workgroups for this layout: part 2 steps every env
     const int nblk = part == 1 ? hcap : (s->E + nwb - 1) / nwb + (part == 0 ? hcap : 0);
-    if (nwb == 4)
-        hipLaunchKernelGGL(evx::env_step_kernel<4>, dim3(nblk), dim3(256), blds, (hipStream_t)stream, *l, *s, actions, *o,
-                           hcap, pslots, (int)part);
+    hipStream_t hs = (hipStream_t)stream;
+    if (nwb == 4 && multi)
+        hipLaunchKernelGGL((evx::env_step_kernel<4, true>), dim3(nblk), dim3(256), blds, hs, *l, *s, actions, *o, hcap,
+                           pslots, (int)part);
+    else if (nwb == 4)
+        hipLaunchKernelGGL((evx::env_step_kernel<4, false>), dim3(nblk), dim3(256), blds, hs, *l, *s, actions, *o, hcap,
+                           pslots, (int)part);
+    else if (nwb == 2 && multi)
+        hipLaunchKernelGGL((evx::env_step_kernel<2, true>), dim3(nblk), dim3(128), blds, hs, *l, *s, actions, *o, 0, 0,
+                           (int)part);
     else if (nwb == 2)
-        hipLaunchKernelGGL(evx::env_step_kernel<2>, dim3(nblk), dim3(128), blds, (hipStream_t)stream, *l, *s, actions, *o,
-                           0, 0, (int)part);
+        hipLaunchKernelGGL((evx::env_step_kernel<2, false>), dim3(nblk), dim3(128), blds, hs, *l, *s, actions, *o, 0, 0,
+                           (int)part);
+    else if (multi)
+        hipLaunchKernelGGL((evx::env_step_kernel<1, true>), dim3(nblk), dim3(64), blds, hs, *l, *s, actions, *o, 0, 0,
+                           (int)part);
     else
-        hipLaunchKernelGGL(evx::env_step_kernel<1>, dim3(nblk), dim3(64), blds, (hipStream_t)stream, *l, *s, actions, *o,
-                           0, 0, (int)part);
+        hipLaunchKernelGGL((evx::env_step_kernel<1, false>), dim3(nblk), dim3(64), blds, hs, *l, *s, actions, *o, 0, 0,
+                           (int)part);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : hip_fail(e, "env_step launch");
 }
@@ -2520,12 +2550,18 @@ int evx_env_reset(const evx_layout* l, const evx_state* s, const uint8_t* mask, 
     if (lds > 160 * 1024) return fail(-7, "layout needs more than 160 KiB of LDS");
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)evx::env_reset_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void*)evx::env_reset_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        (void)hipFuncSetAttribute((const void*)evx::env_reset_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024);
         attr_set = true;
     }
-    hipLaunchKernelGGL(evx::env_reset_kernel, dim3(s->E), dim3(64), lds, (hipStream_t)stream, *l, *s, mask, obs,
-                       err);
+    if (l->layout_set && s->layout_idx)
+        hipLaunchKernelGGL(evx::env_reset_kernel<true>, dim3(s->E), dim3(64), lds, (hipStream_t)stream, *l, *s, mask,
+                           obs, err);
+    else
+        hipLaunchKernelGGL(evx::env_reset_kernel<false>, dim3(s->E), dim3(64), lds, (hipStream_t)stream, *l, *s, mask,
+                           obs, err);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : hip_fail(e, "env_reset launch");
 }

@@ -108,6 +108,7 @@ struct Fwd {
     const uint8_t* cellinfo;
     const float* danger;
     const uint32_t* feat;  // evx_layout.obs_feat: static per-cell features, padded grid per fire step
+    const uint32_t* const* feats;  // layout set: obs_feat of layout evx_obs.layout (NULL: feat)
     int L, W, ox0, oy0, OX, OY, exit_x, exit_y, t_max;
     // parameters
     const __bf16* w1;  // [512][512] compact K, w1_tile order
@@ -192,7 +193,7 @@ __device__ __forceinline__ void fc1_tile(const Fwd& a, int m0, int ncol0, bool w
         ob = evx_obs{{0u, 0u, 0u, 0u}, 0, 0, 0, 0};
     }
     const bool wx = a.x && rowok && want_x;
-    const uint32_t* fb = a.feat + feat_base(a, ob);
+    const uint32_t* fb = (a.feats ? a.feats[ob.layout] : a.feat) + feat_base(a, ob);
     uint32_t fv[CPT];
     auto reads = [&](int kc) {
 #pragma unroll
@@ -969,6 +970,7 @@ static int make_fwd(const evx_layout* lay, const evx_obs* obs, int32_t n, const 
     a.cellinfo = lay->cellinfo;
     a.danger = lay->danger_o32;
     a.feat = lay->obs_feat;
+    a.feats = lay->layout_set ? lay->obs_feats : nullptr;
     a.t_max = lay->t_max;
     a.L = lay->L;
     a.W = lay->W;
@@ -999,7 +1001,7 @@ static int make_fwd(const evx_layout* lay, const evx_obs* obs, int32_t n, const 
     a.act_seed = out->act_seed;
     a.act_offset = out->act_offset;
     a.w1o = reinterpret_cast<const __bf16*>(p->w1o);
-    a.stat = p->w1o ? p->stat : nullptr;
+    a.stat = (p->w1o && !a.feats) ? p->stat : nullptr;  // the table is per layout: single layout only
     a.stat_fs = p->stat_fs;
     a.raw = nullptr;
     return 0;

@@ -25,7 +25,8 @@ class evx_layout(C.Structure):
                [(n, C.c_double) for n in ["repel_k", "repel_range", "evac_reward", "death_penalty",
                                          "death_acc_penalty", "alive_bonus"]] + \
                [(n, C.c_void_p) for n in ["floor", "cellinfo", "valid_bits", "danger_p", "danger_o",
-                                         "danger_o32", "robot_init", "nbr_valid", "floor_d5", "obs_feat"]]
+                                         "danger_o32", "robot_init", "nbr_valid", "floor_d5", "obs_feat",
+                                         "layout_set", "obs_feats"]]
 
 FEAT_PAD = 6  # EVX_FEAT_PAD
 
@@ -33,7 +34,7 @@ FEAT_PAD = 6  # EVX_FEAT_PAD
 class evx_state(C.Structure):
     _fields_ = [("E", C.c_int32)] + [(n, C.c_void_p) for n in
                                      ["pk", "health", "acc", "rmap", "thmap", "robots", "view", "scal",
-                                      "py_mt", "np_mt", "scratch", "order"]]
+                                      "py_mt", "np_mt", "scratch", "order", "layout_idx"]]
 
 
 class evx_step_out(C.Structure):

@@ -180,14 +180,69 @@ class DeviceLayout:
         return cls(build_tables(spec), P, device, **kw)
 
 
-class VecEnv:
-    """E env instances of one layout, state resident in HBM (SoA, env-major)."""
+class LayoutSet:
+    """Several layouts of one size for per-env layouts: every env of a
+    VecEnv picks one (``VecEnv(..., layout_of=...)``); the env kernels read the env's
+    entry of a device array of evx_layout descriptors (evx_layout.layout_set), and the
+    observation readers the layout recorded in each evx_obs. Same L, W, P, R, fire steps
+    and observation window for all (the LDS and scratch sizes follow from those)."""
 
-    def __init__(self, layout: DeviceLayout, E: int, thmap: bool = False, obs_buffers: int = 1):
+    def __init__(self, layouts: Sequence["DeviceLayout"]):
+        if not layouts:
+            raise ValueError("LayoutSet: no layouts")
+        l0 = layouts[0]
+        for l in layouts:
+            same = (l.spec.L, l.spec.W, l.P, l.R, l.c.t_max, l.c.OX, l.c.OY, l.c.ox0, l.c.oy0) == \
+                   (l0.spec.L, l0.spec.W, l0.P, l0.R, l0.c.t_max, l0.c.OX, l0.c.OY, l0.c.ox0, l0.c.oy0)
+            if not same:
+                raise ValueError("LayoutSet: layouts must share L, W, P, R, fire steps and the observation window")
+        self.layouts = list(layouts)
+        self.spec, self.tables, self.P, self.R, self.device = l0.spec, l0.tables, l0.P, l0.R, l0.device
+        self.GX, self.GY, self.G, self.RW, self.t = l0.GX, l0.GY, l0.G, l0.RW, l0.t
+        self.c = _lib.evx_layout.from_buffer_copy(l0.c)
+        self._upload()
+
+    def _upload(self):
+        raw = b"".join(bytes(l.c) for l in self.layouts)
+        self._set = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
+        self._feats = torch.tensor([l.c.obs_feat for l in self.layouts], dtype=torch.int64, device=self.device)
+        for name, _ in _lib.evx_layout._fields_:  # the set's own descriptor: layout 0's sizes and coefficients
+            if name not in ("layout_set", "obs_feats"):
+                setattr(self.c, name, getattr(self.layouts[0].c, name))
+        self.c.layout_set = self._set.data_ptr()
+        self.c.obs_feats = self._feats.data_ptr()
+
+    def set_params(self, **kw):
+        """Runtime-mutable coefficients, for every layout of the set."""
+        for l in self.layouts:
+            l.set_params(**kw)
+        self._upload()
+
+    def __len__(self):
+        return len(self.layouts)
+
+
+class VecEnv:
+    """E env instances of one layout (or of a LayoutSet, one layout per env), state
+    resident in HBM (SoA, env-major)."""
+
+    def __init__(self, layout, E: int, thmap: bool = False, obs_buffers: int = 1,
+                 layout_of: Optional[Sequence[int]] = None):
         """obs_buffers=2: every step writes its observations into the other of two
-        buffers, so the previous step's stay readable (``obs_prev``) without a copy."""
+        buffers, so the previous step's stay readable (``obs_prev``) without a copy.
+        layout: a DeviceLayout, or a LayoutSet with ``layout_of`` = each env's layout."""
         self.lay = layout
         self.E = int(E)
+        self.layout_idx = None
+        if isinstance(layout, LayoutSet):
+            if layout_of is None or len(layout_of) != E:
+                raise ValueError("VecEnv over a LayoutSet needs layout_of (one layout index per env)")
+            li = np.asarray(layout_of, np.int32)
+            if li.min() < 0 or li.max() >= len(layout):
+                raise ValueError("layout_of: index out of the set")
+            self.layout_idx = torch.from_numpy(li).to(layout.device)
+        elif layout_of is not None:
+            raise ValueError("layout_of needs a LayoutSet")
         P, R, d = layout.P, layout.R, layout.device
         i32 = dict(dtype=torch.int32, device=d)
         f64 = dict(dtype=torch.float64, device=d)
@@ -196,11 +251,11 @@ class VecEnv:
         self.acc = torch.zeros(E * P, **f64)
         self.rmap = torch.zeros(E * layout.RW, **i32)
         self.thmap = torch.zeros(E * layout.G, **i32) if thmap else None
-        spec = layout.spec
-        ri = pack_xy([p[0] for p in spec.robot_init], [p[1] for p in spec.robot_init])
-        self.robots = torch.from_numpy(np.tile(ri, E)).to(d)
-        v0 = pack_xy(*spec.reset_view)
-        self.view = torch.full((E,), int(v0), **i32)
+        specs = [layout.spec] * E if self.layout_idx is None else \
+            [layout.layouts[i].spec for i in self.layout_idx.cpu().tolist()]
+        self.robots = torch.from_numpy(np.concatenate(
+            [pack_xy([p[0] for p in s.robot_init], [p[1] for p in s.robot_init]) for s in specs])).to(d)
+        self.view = torch.from_numpy(np.array([pack_xy(*s.reset_view) for s in specs]).astype(np.int32).reshape(E)).to(d)
         self.scal = torch.zeros(E * 4, **i32)
         self.py_mt = torch.zeros(E * 625, **i32)
         self.np_mt = torch.zeros(E * 625, **i32)
@@ -225,7 +280,8 @@ class VecEnv:
         self.c = _lib.evx_state(E=E, pk=_ptr(self.pk), health=_ptr(self.health), acc=_ptr(self.acc),
                                 rmap=_ptr(self.rmap), thmap=_ptr(self.thmap), robots=_ptr(self.robots),
                                 view=_ptr(self.view), scal=_ptr(self.scal), py_mt=_ptr(self.py_mt),
-                                np_mt=_ptr(self.np_mt), scratch=_ptr(self.scratch), order=_ptr(self.order))
+                                np_mt=_ptr(self.np_mt), scratch=_ptr(self.scratch), order=_ptr(self.order),
+                                layout_idx=_ptr(self.layout_idx))
         self.obs_term: Optional[torch.Tensor] = None
         self._parts: List["VecEnv"] = []
         self.out = _lib.evx_step_out(reward=_ptr(self.reward), done=_ptr(self.done), counts=_ptr(self.counts),
@@ -267,7 +323,8 @@ class VecEnv:
             p.c = _lib.evx_state(E=n, pk=_ptr(p.pk), health=_ptr(p.health), acc=_ptr(p.acc), rmap=_ptr(p.rmap),
                                  thmap=_ptr(p.thmap), robots=_ptr(p.robots), view=_ptr(p.view), scal=_ptr(p.scal),
                                  py_mt=_ptr(p.py_mt), np_mt=_ptr(p.np_mt), scratch=_ptr(p.scratch),
-                                 order=_ptr(p.order))
+                                 order=_ptr(p.order), layout_idx=_ptr(cut(self.layout_idx, 1)))
+            p.layout_idx = cut(self.layout_idx, 1)
             p.out = _lib.evx_step_out(reward=_ptr(p.reward), done=_ptr(p.done), counts=_ptr(p.counts),
                                       obs=_ptr(p.obs), err=_ptr(p.err))
             parts.append(p)

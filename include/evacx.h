@@ -57,6 +57,12 @@ typedef struct {
      * barrier channel (!valid || barrier_list) in bit 16, the exit channel in bit 17
      * (_get_state's channels 2-4, envs/evacuation_env.py:84-120); read by the MLP fast path */
     const uint32_t *obs_feat;
+    /* Layout set (per-env layouts), or NULL: a device array of the evx_layout
+     * descriptors of every layout of the set -- all of one size (L, W, P, R, t_max, OX, OY) --
+     * indexed by evx_state.layout_idx[e] in the env kernels and by evx_obs.layout in the
+     * observation readers; obs_feats is the device array of their obs_feat tables. */
+    const void *layout_set;
+    const uint32_t *const *obs_feats;
 } evx_layout;
 
 #define EVX_FEAT_PAD 6
@@ -77,6 +83,7 @@ typedef struct {
     uint32_t *scratch; /* [E*evx_step_scratch_words] step scratch: move plan, contested lists beyond LDS */
     int32_t *order;    /* [E+1] dispatch order of the step's envs (evx_env_order), or NULL = 0..E-1;
                         * order[E] = H: the first H of them are heavy (rows phase on a 4-wave workgroup) */
+    const int32_t *layout_idx; /* [E] each env's layout in evx_layout.layout_set, or NULL (one layout) */
 } evx_state;
 
 /* Compact per-robot observation (32 B). Expands to the reference's 11x11x6
@@ -85,7 +92,7 @@ typedef struct {
     uint32_t occ[4];   /* bit c (c = i*11+j): People.rmap at (cx+i-5, cy+j-5) if valid */
     int32_t cx, cy;    /* window centre */
     int32_t fire_step; /* env fire model step the obs was taken at */
-    int32_t pad;
+    int32_t layout;    /* the env's layout in evx_layout.layout_set (0 without a set) */
 } evx_obs;
 
 /* Per-step outputs. */
