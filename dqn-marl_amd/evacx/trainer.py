@@ -121,13 +121,16 @@ class VecTrainer:
                  epsilon_decay: float = 0.9995, target_every: int = 1000, learner_seed: int = 0,
                  grad_hook=None, learn_every: int = 1, lagged_learn: bool = False, replay: str = "uniform",
                  prio_alpha: float = 0.6, prio_beta0: float = 0.4, prio_beta_steps: int = 100000,
-                 prio_eps: float = 1e-6, groups: int = 1):
+                 prio_eps: float = 1e-6, groups: int = 1, layout_of=None):
         """groups: the envs are split into this many parts, each stepping on its own
         stream chain (see _Group); the env results do not depend on it (every env is
-        still stepped once per step with its own streams), the act's dropout masks do."""
+        still stepped once per step with its own streams), the act's dropout masks do.
+        layout: a DeviceLayout, or an evacx.env.LayoutSet with layout_of = each env's
+        layout (per-env layouts; observations in the replay carry their layout)."""
         self.lay, self.E, self.R = layout, E, layout.R
         self.device = layout.device
-        self.env = VecEnv(layout, E, obs_buffers=2)  # the push reads env.obs_prev: no copy per step
+        # the push reads env.obs_prev: no copy per step
+        self.env = VecEnv(layout, E, obs_buffers=2, layout_of=layout_of)
         self.env.seed([seed_base + env_offset + i for i in range(E)])
         self.env.reset()
         parts = self.env.split(groups) if groups > 1 else [self.env]

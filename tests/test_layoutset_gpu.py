@@ -125,3 +125,31 @@ def test_layout_set_mlp_forward_reads_each_rows_layout():
     qref2 = F.relu(h @ bf(sd["fc2.weight"]).t() + sd["fc2.bias"]) @ sd["fc3.weight"].t() + sd["fc3.bias"]
     torch.cuda.synchronize()
     torch.testing.assert_close(q2, qref2, rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("lagged", [False, True])
+def test_vec_trainer_on_a_layout_set(lagged):
+    """The training step over envs of three layouts: it trains (finite losses), and the
+    replay's observations carry each env's layout."""
+    _need_gpu()
+    from evacx.env import DeviceLayout, LayoutSet
+    from evacx.layout import build_tables
+    from evacx.trainer import VecTrainer
+    ls = LayoutSet([DeviceLayout(build_tables(s), 380) for s in _specs()])
+    E = 384
+    layout_of = [i % 3 for i in range(E)]
+    tr = VecTrainer(ls, E, batch=256, replay_capacity=1 << 15, target_every=5, lagged_learn=lagged, lr=1e-3,
+                    layout_of=layout_of)
+    losses = []
+    for _ in range(10):
+        tr.step()
+        if tr.last_loss is not None:
+            losses.append(tr.last_loss)
+    tr.sync()
+    torch.cuda.synchronize()
+    tr.env.check_err()
+    assert losses and all(np.isfinite([x.item() for x in losses]))
+    n = tr.replay.size
+    obs = tr.replay.s.view(-1, 8)[:n].cpu().numpy()
+    env_of_row = (np.arange(n) // ls.R) % E
+    assert (obs[:, 7] == np.asarray(layout_of)[env_of_row]).all()
