@@ -2306,59 +2306,78 @@ __global__ __launch_bounds__(64 * NWB, EVX_ENV_MINW) void env_step_kernel(evx_la
 // and a bucket that changed between the counting and the ranking pass would break the
 // permutation.
 __global__ __launch_bounds__(1024) void env_order_kernel(evx_layout lay, evx_state st, int hcap, int hmin) {
-    __shared__ int cnt[16], base[16], nheavy;
+    // wave w owns the contiguous slice [w * S, (w + 1) * S) of the envs, so a stable rank is
+    // bucket start + the same-bucket envs of lower waves + those earlier in the wave's slice
+    __shared__ int wcnt[16][16], woff[16][16], nheavy;
     extern __shared__ uint8_t bk[];  // [E] bucket (0 = most persons remaining)
     const int tid = threadIdx.x, E = st.E, P = lay.P;
-    if (tid < 16) cnt[tid] = 0;
+    const int lane = tid & 63, w = tid >> 6;
+    const int S = ((E + 16 * 64 - 1) / (16 * 64)) * 64;  // slice length, a multiple of 64
+    if (tid < 256) wcnt[tid >> 4][tid & 15] = 0;
     if (tid == 0) nheavy = 0;
     __syncthreads();
     int nh = 0;
-    for (int e = tid; e < E; e += 1024) {
-        const int s2 = __hip_atomic_load(&st.scal[(size_t)e * 4 + 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int s3 = __hip_atomic_load(&st.scal[(size_t)e * 4 + 3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int rem = P - s2 - s3;
-        const int b = 15 - min(15, max(0, rem) * 16 / (P + 1));
-        bk[e] = (uint8_t)b;
-        atomicAdd(&cnt[b], 1);
-        nh += rem >= hmin;
-    }
-    if (nh) atomicAdd(&nheavy, nh);
-    __syncthreads();
-    if (tid == 0) st.order[E] = min(hcap, nheavy);
-    if (tid == 0) {
-        int o = 0;
-        for (int b = 0; b < 16; b++) {
-            base[b] = o;
-            o += cnt[b];
+    uint32_t mycnt = 0;  // lane b < 16: this wave's count of bucket b
+    // (prev_evacuated, prev_dead) of every env in one 8-byte load, up to 8 loads in flight
+    constexpr int LPT = 8;
+    for (int i0 = 0; i0 < S; i0 += LPT * 64) {
+        unsigned long long v[LPT];
+#pragma unroll
+        for (int j = 0; j < LPT; j++) {
+            const int i = i0 + j * 64 + lane, e = w * S + i;
+            v[j] = (i < S && e < E) ? __hip_atomic_load(reinterpret_cast<const unsigned long long*>(st.scal + (size_t)e * 4 + 2),
+                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                    : 0ull;
+        }
+#pragma unroll
+        for (int j = 0; j < LPT; j++) {
+            const int i = i0 + j * 64 + lane, e = w * S + i;
+            int b = -1;
+            if (i < S && e < E) {
+                const int rem = P - (int)(uint32_t)v[j] - (int)(uint32_t)(v[j] >> 32);
+                b = 15 - min(15, max(0, rem) * 16 / (P + 1));
+                bk[e] = (uint8_t)b;
+                nh += rem >= hmin;
+            }
+            if (__ballot(b >= 0)) {
+#pragma unroll
+                for (int bb = 0; bb < 16; bb++) {
+                    const uint32_t c = (uint32_t)__popcll(__ballot(b == bb));
+                    mycnt += lane == bb ? c : 0u;
+                }
+            }
         }
     }
+    if (lane < 16) wcnt[w][lane] = (int)mycnt;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) nh += __shfl_xor(nh, o, 64);
+    if (lane == 0 && nh) atomicAdd(&nheavy, nh);
     __syncthreads();
-    // stable within a bucket: chunks of 1024 envs in order; rank = bucket base + the
-    // same-bucket envs of lower waves + lower lanes (ballots)
-    __shared__ int wcnt[16][16];
-    const int lane = tid & 63, w = tid >> 6;
-    for (int e0 = 0; e0 < E; e0 += 1024) {
-        const int e = e0 + tid;
+    if (tid < 16) {  // bucket tid: start of every wave's run
+        int below = 0;
+        for (int b = 0; b < tid; b++)
+            for (int ww = 0; ww < 16; ww++) below += wcnt[ww][b];
+        for (int ww = 0; ww < 16; ww++) {
+            woff[ww][tid] = below;
+            below += wcnt[ww][tid];
+        }
+    }
+    if (tid == 0) st.order[E] = min(hcap, nheavy);
+    __syncthreads();
+    int run = lane < 16 ? woff[w][lane] : 0;  // lane b < 16: next rank of bucket b in this wave
+    for (int i0 = 0; i0 < S; i0 += 64) {
+        const int i = i0 + lane, e = w * S + i;
         const int b = e < E ? (int)bk[e] : -1;
-        int inw = 0;
+        if (!__ballot(b >= 0)) break;
+#pragma unroll
         for (int bb = 0; bb < 16; bb++) {
             const unsigned long long m = __ballot(b == bb);
-            if (lane == 0) wcnt[w][bb] = __popcll(m);
-            if (b == bb) inw = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            const int r0 = __shfl(run, bb, 64);
+            if (b == bb)
+                st.order[r0 + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = e;
+            run += lane == bb ? __popcll(m) : 0;
         }
-        __syncthreads();
-        if (e < E) {
-            int r = base[b] + inw;
-            for (int ww = 0; ww < w; ww++) r += wcnt[ww][b];
-            st.order[r] = e;
-        }
-        __syncthreads();
-        if (tid < 16) {
-            int c = 0;
-            for (int ww = 0; ww < 16; ww++) c += wcnt[ww][tid];
-            base[tid] += c;
-        }
-        __syncthreads();
     }
 }
 

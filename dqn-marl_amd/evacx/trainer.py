@@ -93,6 +93,13 @@ class Replay:
                                    out["done"].data_ptr(), None, _stream()), "replay_sample")
 
 
+# The dispatch order of the lagged schedule runs on the env's own stream right before
+# env.step: its ~13 us kernel on the critical path beats the side stream's event pair
+# (tools/gpu_ab_env.sh EVX_ORDER_INLINE: 9.48 vs 9.03 M env-steps/s). The strict schedule
+# keeps the side stream (its act + learn hide the order). EVX_ORDER_INLINE=0/1 forces.
+_ORDER_INLINE_ENV = os.environ.get("EVX_ORDER_INLINE")
+
+
 class _Group:
     """One part of the envs with its own stream chain (act -> env.step -> push): with
     several groups, one group's env.step launch tail (its heaviest envs, few waves)
@@ -275,6 +282,7 @@ class VecTrainer:
                 grp.main.wait_stream(caller)
             self.join_caller = False
         G = self.groups
+        inline = (self.lagged and len(G) == 1) if _ORDER_INLINE_ENV is None else _ORDER_INLINE_ENV == "1"
         reset_wait, self.reset_pending = self.reset_pending, False
         # act: every group on its own stream, after the previous update (lagged) or learn
         for grp in G:
@@ -313,7 +321,9 @@ class VecTrainer:
                 # step, concurrently with act: by now the event is complete and the wait costs
                 # no gap (an order one step older would miss the envs that just auto-reset:
                 # they would be dispatched as light envs and become the launch's tail)
-                if len(G) == 1:
+                if inline:  # on this stream, right before the step: no cross-stream event
+                    grp.env.compute_order()
+                elif len(G) == 1:
                     grp.main.wait_event(grp.ev_order)
                 if ev_env is not None and grp.g == 0:
                     ev_env[0].record(grp.main)
@@ -333,7 +343,7 @@ class VecTrainer:
                 self.env.reset(mask=extra_reset & ~self.env.done.bool())
                 self.ev_reset.record(side)
             self.reset_pending = True
-        for grp in G:
+        for grp in ([] if inline else G):
             # one group: the order on a side stream (overlaps act); several: on the group's own
             # stream after its push (the groups overlap each other, and more streams than
             # the GPU_MAX_HW_QUEUES hardware queues would serialise unrelated work)
