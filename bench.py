@@ -80,6 +80,8 @@ def parse():
                          "env ages spread over a whole episode (the stationary mix of a long run); 0 = off")
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
     ap.add_argument("--grid", type=int, default=128)
+    ap.add_argument("--layouts", type=int, default=1,
+                    help="K > 1: per-env layouts, K random variants of the synthetic layout (env e runs e %% K)")
     ap.add_argument("--people", type=int, default=2276)
     ap.add_argument("--robots", type=int, default=16)
     ap.add_argument("--batch", type=int, default=4096)
@@ -126,13 +128,22 @@ def main():
     L = W = args.grid
     P, R, E = args.people, args.robots, args.envs
     spec = synthetic(L, W, R)
-    tables = build_tables(spec)
-    lay = DeviceLayout(tables, P)
+    layout_of = None
+    if args.layouts > 1:  # per-env layouts: env e runs random layout e % K
+        from evacx.env import LayoutSet
+        from evacx.layout import random_layout
+        lay = LayoutSet([DeviceLayout(build_tables(random_layout(L, W, R, 4242 + k)), P) for k in range(args.layouts)])
+        layout_of = [(rank * E + e) % args.layouts for e in range(E)]
+        tables = lay.tables
+    else:
+        tables = build_tables(spec)
+        lay = DeviceLayout(tables, P)
     hook = make_allreduce_hook(dist, world) if dist is not None else None
     tr = VecTrainer(lay, E, env_offset=rank * E, kind=args.qnet, precision=args.precision, batch=args.batch,
                     grad_hook=hook,
                     lagged_learn=args.schedule == "lagged", replay=args.replay,
-                    replay_capacity=args.replay_capacity, groups=args.groups if args.mode == "train" else 1)
+                    replay_capacity=args.replay_capacity, groups=args.groups if args.mode == "train" else 1,
+                    layout_of=layout_of)
     env = tr.env
 
     def barrier():
@@ -259,7 +270,9 @@ def main():
             "dtype": "f64" if args.mode == "env" else f"f64 env + {args.precision} Q-net",
             "data": "synthetic",
             "config": {
-                "workload": (f"{cfg_name(args)} per-GPU share: {L}x{W} synthetic layout, {P} people, {R} robots, {E} envs/GPU; "
+                "workload": (f"{cfg_name(args)} per-GPU share: {L}x{W} synthetic layout"
+                             + (f" ({args.layouts} random per-env layouts)" if args.layouts > 1 else "")
+                             + f", {P} people, {R} robots, {E} envs/GPU; "
                              + ("full training step: act + env.step + replay push + learn (B="
                                 f"{args.batch}) + auto-reset" if args.mode == "train"
                                 else "env.step + auto-reset, uniform random actions")),

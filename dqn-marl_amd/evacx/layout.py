@@ -123,6 +123,30 @@ def synthetic(L: int, W: int, R: int) -> LayoutSpec:
                       robot_init=tuple(init), reset_robots=True)
 
 
+def random_layout(L: int, W: int, R: int, seed: int, n_barriers: int = 4) -> LayoutSpec:
+    """A randomised variant of synthetic(L, W, R) for per-env layouts:
+    n_barriers rectangles (2..L/12 x 2..W/12 cells) away from the robots' start cells and
+    the exit, the exit moved along the far wall (x = L), the additional fire sources
+    jittered by up to L/8. Deterministic in seed."""
+    base = synthetic(L, W, R)
+    rng = np.random.RandomState(seed)
+    ex = (L, int(rng.randint(2, W - 1)))
+    keep = {tuple(p) for p in base.robot_init} | {ex, (ex[0] - 1, ex[1])}
+    bars = []
+    while len(bars) < n_barriers:
+        w, h = int(rng.randint(2, max(3, L // 12 + 1))), int(rng.randint(2, max(3, W // 12 + 1)))
+        x0, y0 = int(rng.randint(2, L - w)), int(rng.randint(2, W - h))
+        cells = {(x, y) for x in range(x0 - 1, x0 + w + 1) for y in range(y0 - 1, y0 + h + 1)}
+        if cells & keep:
+            continue
+        bars.append(((x0, y0), (x0 + w - 1, y0 + h - 1)))
+    j = max(1, L // 8)
+    add = tuple(dict(s, center=(int(np.clip(s["center"][0] + rng.randint(-j, j + 1), 2, L - 1)),
+                                int(np.clip(s["center"][1] + rng.randint(-j, j + 1), 2, W - 1))))
+                for s in base.additional_fire)
+    return dataclasses.replace(base, exit=ex, barriers=tuple(bars), additional_fire=add)
+
+
 def _norm_barriers(barriers):
     out = []
     for (A, B) in barriers:  # Init_Barrier (envs/map.py:25-33)
