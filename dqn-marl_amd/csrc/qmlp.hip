@@ -342,7 +342,10 @@ __device__ __forceinline__ void fc3_act(const Fwd& a, const float* hrow, const f
     float qv[NACT];
 #pragma unroll
     for (int t = 0; t < NACT; t++) qv[t] = 0.f;
-    for (int n = part * 64; n < part * 64 + 64; n++) {
+    // part p takes columns p, p + 4, ...: with a row pitch of 4 (mod 32) words the 32 lanes
+    // of a half-wave (8 rows x 4 parts) read 32 distinct banks, and W3s is one bank per part
+    for (int j = 0; j < HID2 / 4; j++) {
+        const int n = part + 4 * j;
         const float hv = hrow[n];
 #pragma unroll
         for (int t = 0; t < NACT; t++) qv[t] += hv * W3s[t][n];
@@ -395,8 +398,9 @@ __device__ __forceinline__ void fc3_act(const Fwd& a, const float* hrow, const f
 // from the bits (no LDS staging, no barriers). Same products, f32 sums in another order
 // (Q within f32 rounding of the full path).
 constexpr int ACT_HP = HID + 8;                                  // H1 row pitch (bf16)
-constexpr int ACT_H2P = HID2 + 1;                                // H2 row pitch (f32)
-constexpr int ACT_HBYTES = 128 * ACT_HP * 2;                     // 133,120 >= 128 * 257 * 4
+constexpr int ACT_H2P = HID2 + 4;                                // H2 row pitch (f32; fc3_act banks)
+constexpr int ACT_HBYTES = 128 * ACT_HP * 2;                     // 133,120 = 128 * 260 * 4
+static_assert(ACT_HBYTES >= 128 * ACT_H2P * 4, "H2 overlays the H1 tile");
 constexpr int ACT_LDS = ACT_HBYTES + NACT * HID2 * 4 + 128 * 4;  // + W3 + window centres
 __global__ __launch_bounds__(512, 1) void qact_kernel(Fwd a) {
     extern __shared__ __attribute__((aligned(16))) char dsm[];
@@ -531,7 +535,7 @@ __global__ __launch_bounds__(512, 1) void qact_kernel(Fwd a) {
 __global__ __launch_bounds__(256, 2) void qfc23_kernel(Fwd a0, Fwd a1) {
     const Fwd& a = blockIdx.z ? a1 : a0;
     __shared__ __attribute__((aligned(16))) __bf16 As[2][RM][32];
-    __shared__ float Hs[RM][HID2 + 1];
+    __shared__ float Hs[RM][HID2 + 4];  // pitch 4 (mod 32) words: fc3_act reads conflict-free
     __shared__ float W3s[NACT][HID2];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
     const int m0 = blockIdx.x * RM;
