@@ -795,17 +795,45 @@ __global__ __launch_bounds__(256, 2) void qdz1_kernel(Bwd a) {
 // splits in z order (deterministic, and no atomic traffic through L2). Columns
 // n >= Nc are skipped; remap: column n goes to ref_col(n) (fc1's compact K -> the
 // reference's 726).
-constexpr int TT = 128, TKC = 32, TPAD = TKC + 8;
+constexpr int TT = 128, TKC = 64, TPAD = TKC + 8;
+// 8x8 transpose of bf16: in[r] holds row r (8 consecutive m) -> out[c] holds column c
+// (8 consecutive k); word j of out[c] = in[2j][c] | in[2j+1][c] << 16
+__device__ __forceinline__ void tr8x8(const uint4 (&in)[8], uint4 (&out)[8]) {
+    uint32_t w[8][4];
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+        w[r][0] = in[r].x;
+        w[r][1] = in[r].y;
+        w[r][2] = in[r].z;
+        w[r][3] = in[r].w;
+    }
+#pragma unroll
+    for (int c = 0; c < 8; c++) {
+        const int q = c >> 1, hi = c & 1;
+        uint32_t o[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; jj++) {
+            const uint32_t a = hi ? (w[2 * jj][q] >> 16) : (w[2 * jj][q] & 0xffffu);
+            const uint32_t b = hi ? (w[2 * jj + 1][q] & 0xffff0000u) : (w[2 * jj + 1][q] << 16);
+            o[jj] = a | b;
+        }
+        out[c] = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+}
 __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const __bf16* __restrict__ A, int lda,
                                                          const __bf16* __restrict__ Bm, int ldb, int K, int M, int Nc,
                                                          int kper, float* __restrict__ C, int ldc, int remap,
                                                          float* __restrict__ part) {
+    // K chunks of 64 staged [m][k] in LDS: thread b < 128 of each operand loads an 8 (k) x 8 (m)
+    // block (8 x 16-B row segments, whole cache lines per wave), transposes it in registers
+    // and writes 8 x 16 B (8 consecutive k of one m): ds_write_b128, conflict-free; the MFMA
+    // operand reads (ds_read_b128, pitch 36 words) are conflict-free too.
     __shared__ __attribute__((aligned(16))) __bf16 As[TT][TPAD];
     __shared__ __attribute__((aligned(16))) __bf16 Bs[TT][TPAD];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
     const int wm = w >> 1, wn = w & 1;
     const int m0 = blockIdx.y * TT, n0 = blockIdx.x * TT;
-    const int kb = blockIdx.z * kper, ke = min(K, kb + kper);
+    const int kb0 = blockIdx.z * kper, ke = min(K, kb0 + kper);
     f32x16 acc[2][2];
 #pragma unroll
     for (int i = 0; i < 2; i++)
@@ -813,42 +841,29 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const __bf16* __restric
         for (int j = 0; j < 2; j++)
 #pragma unroll
             for (int r = 0; r < 16; r++) acc[i][j][r] = 0.f;
-    // loader: k row = tid >> 3, 16 consecutive m (n) at (tid & 7) * 16
-    const int lk = tid >> 3, lm = (tid & 7) * 16;
-    bf16x8 ra[2], rb[2];
+    // threads 0..127 stage A, 128..255 stage B: block b = tid & 127 -> k block b & 7, m block b >> 3
+    const bool isA = tid < 128;
+    const int b = tid & 127, kb = b & 7, mb = b >> 3;
+    const __bf16* src = isA ? A : Bm;
+    const int ld = isA ? lda : ldb, mlim = isA ? M : ldb, mbase = (isA ? m0 : n0) + mb * 8;
+    uint4 rv[8];
     auto fetch = [&](int k0) {
-        const int k = k0 + lk;
 #pragma unroll
-        for (int j = 0; j < 2; j++) {
-            bf16x8 va, vb;
-            const bool okk = k < ke;
-            if (okk && m0 + lm + 8 * j < M) {
-                va = *reinterpret_cast<const bf16x8*>(A + (size_t)k * lda + m0 + lm + 8 * j);
-            } else {
-#pragma unroll
-                for (int t = 0; t < 8; t++) va[t] = (__bf16)0.f;
-            }
-            if (okk && n0 + lm + 8 * j < ldb) {
-                vb = *reinterpret_cast<const bf16x8*>(Bm + (size_t)k * ldb + n0 + lm + 8 * j);
-            } else {
-#pragma unroll
-                for (int t = 0; t < 8; t++) vb[t] = (__bf16)0.f;
-            }
-            ra[j] = va;
-            rb[j] = vb;
+        for (int r = 0; r < 8; r++) {
+            const int k = k0 + kb * 8 + r;
+            rv[r] = make_uint4(0u, 0u, 0u, 0u);
+            if (k < ke && mbase < mlim) rv[r] = *reinterpret_cast<const uint4*>(src + (size_t)k * ld + mbase);
         }
     };
     auto stash = [&]() {
+        uint4 t[8];
+        tr8x8(rv, t);
+        __bf16 (*dst)[TPAD] = isA ? As : Bs;
 #pragma unroll
-        for (int j = 0; j < 2; j++)
-#pragma unroll
-            for (int t = 0; t < 8; t++) {
-                As[lm + 8 * j + t][lk] = ra[j][t];
-                Bs[lm + 8 * j + t][lk] = rb[j][t];
-            }
+        for (int c = 0; c < 8; c++) *reinterpret_cast<uint4*>(&dst[mb * 8 + c][kb * 8]) = t[c];
     };
-    if (kb < ke) fetch(kb);
-    for (int k0 = kb; k0 < ke; k0 += TKC) {
+    if (kb0 < ke) fetch(kb0);
+    for (int k0 = kb0; k0 < ke; k0 += TKC) {
         stash();
         __syncthreads();
         if (k0 + TKC < ke) fetch(k0 + TKC);
