@@ -534,8 +534,13 @@ __global__ __launch_bounds__(512, 1) void qact_kernel(Fwd a) {
 // ------------------------------------------------------------ fc2 + fc3
 __global__ __launch_bounds__(256, 2) void qfc23_kernel(Fwd a0, Fwd a1) {
     const Fwd& a = blockIdx.z ? a1 : a0;
-    __shared__ __attribute__((aligned(16))) __bf16 As[2][RM][32];
-    __shared__ float Hs[RM][HID2 + 4];  // pitch 4 (mod 32) words: fc3_act reads conflict-free
+    // A stages (row pitch 40 bf16 = 20 words: conflict-free ds_read_b128), then H2 in the same
+    // bytes (pitch 4 mod 32 words: fc3_act reads conflict-free)
+    constexpr int AP = 40;
+    static_assert(2 * RM * AP * 2 <= RM * (HID2 + 4) * 4, "A stages fit under H2");
+    __shared__ __attribute__((aligned(16))) char sm23[RM * (HID2 + 4) * 4];
+    auto As = reinterpret_cast<__bf16 (*)[RM][AP]>(sm23);
+    auto Hs = reinterpret_cast<float (*)[HID2 + 4]>(sm23);
     __shared__ float W3s[NACT][HID2];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
     const int m0 = blockIdx.x * RM;
@@ -717,7 +722,7 @@ __global__ __launch_bounds__(256) void qbwd3_kernel(Bwd a) {
 // dZ1 = (dZ2 W2) * scale * [H1 > 0]: 64 rows x 128 columns per workgroup (4 waves x
 // 32 columns), K = 256 in chunks of 32; dZ2 staged through LDS, W2^T operand-tiled.
 __global__ __launch_bounds__(256, 2) void qdz1_kernel(Bwd a) {
-    __shared__ __attribute__((aligned(16))) __bf16 As[2][RM][32];
+    __shared__ __attribute__((aligned(16))) __bf16 As[2][RM][40];  // pitch 20 words: conflict-free b128 reads
     __shared__ float colsum[4][32];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
     const int m0 = blockIdx.x * RM, n0 = blockIdx.y * 128 + w * 32;
