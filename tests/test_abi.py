@@ -53,3 +53,17 @@ def test_repel_threshold_exact():
     for r in [5.0, 4.5, 0.3, 7.1, 12.0, 1e-3]:
         n = repel_threshold(r)
         assert math.sqrt(n) >= r and (n == 0 or math.sqrt(n - 1) < r)
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    """No CPU fallback: a product call without libevacx.so raises EvacxError."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from evacx import _lib\n"
+            "try:\n    _lib.lib()\nexcept _lib.EvacxError as e:\n    print('raised', e)\n    sys.exit(0)\n"
+            "sys.exit(3)\n") % os.path.join(ROOT, "dqn-marl_amd")
+    env = dict(os.environ, EVX_LIB=str(tmp_path / "absent" / "libevacx.so"))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "not built" in r.stdout
