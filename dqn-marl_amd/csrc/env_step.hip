@@ -2431,7 +2431,10 @@ static size_t step_launch_lds(const evx_layout& l, int nwb) {
 }
 // Heavy envs per step (rows_wide workgroups): at most the cap, each with >= *hmin
 // persons in play; 0 when the 4-wave workgroup does not fit in LDS. EVX_HEAVY_CAP /
-// EVX_HEAVY_MIN override (tuning).
+// EVX_HEAVY_MIN override (tuning). Cap 176 (tools/tune_heavy_train.sh, tune_heavy_cfgs.sh):
+// with 256 heavy workgroups (one per CU) the light envs' waves start late; 160-192 is a
+// plateau in the training step (cfg3 lagged 9.63 -> 10.07 M, strict 7.44 -> 7.75 M,
+// env-only 13.3 -> 13.9 M, cfg2 17.9 -> 18.3 M, cfg5 8.72 -> 8.88 M env-steps/s).
 static int heavy_cap(const evx_layout& l, int* hmin) {
     static int cap_env = -2, min_env = -2;
     if (cap_env == -2) {
@@ -2443,7 +2446,7 @@ static int heavy_cap(const evx_layout& l, int* hmin) {
     *hmin = std::max(1, min_env >= 0 ? min_env : l.P / 4);
     const evx::WideLds wl = evx::wide_lds(l);
     if (step_launch_lds(l, evx::WNW) > 160 * 1024 || wl.end > wl.ctl) return 0;
-    return cap_env >= 0 ? cap_env : 256;
+    return cap_env >= 0 ? cap_env : 176;
 }
 
 namespace {
