@@ -3,27 +3,35 @@
 
 Workload (BASELINE.json metric; configs[2], per-GPU share): synthetic 128x128
 layout, 2276 people and 16 robots per env, 4096 envs per GPU (weak scaling;
-env ids global, seeds 1234 + global env id), uniform-init MLP Q-net (bf16 MFMA),
-batch 4096, replay 2^20 transitions per GPU, gradient all-reduce over RCCL when
-world > 1. One timed "step" = one full vectorised training step:
+env ids global, seeds 1234 + global env id), uniform-init MLP Q-net, batch 4096,
+replay 2^20 transitions per GPU, gradient all-reduce over RCCL when world > 1.
+One timed "step" = one full vectorised training step in the reference's order
+(DQNAgent act -> env.step -> remember -> learn, runners/train_dqn.py:94-116):
 act (Q forward for E*R robots + epsilon-greedy) -> env.step (all E envs, finished
 envs auto-reset inside the launch) -> replay push (E*R transitions) -> one learn
 step (sample, online+target forward, TD loss, backward, [all-reduce], clip+Adam).
-Default schedule "lagged": learn t samples the ring as it stood before push t and
-runs on its own stream concurrently with env.step t (the next act waits for it);
-"strict" keeps the reference's act -> step -> remember -> learn order, and its rate
-on the same state is reported beside the value (strict_schedule_steps_per_s).
-Warmup staggers env ages over one episode length (--stagger), so the timed steps
-see the stationary mix of episode phases a long training run sees.
 
-value = env-steps/s of the whole job (E * n_gpus * steps / time); the JSON line
-also carries agent-transitions/s (x R), the env-only rate, the roofline of the
-dominant kernel (env_step_kernel, HBM-bound) and the CPU oracle baseline.
-Prints ONE JSON line on rank 0.
+Episode phase. The cost of an env-step varies several-fold over an episode (all
+2276 persons in play at its start, a few at its end), so the phase the timed steps
+see is part of the workload and is built explicitly, independent of --warmup:
+  --phase stationary (default): an env-only preparation of --age-steps steps
+     (uniform random actions) force-resets env g at preparation step g % --stagger,
+     so env ages are spread uniformly over one episode length -- the stationary mix
+     of a long training run;
+  --phase start: the same preparation, then every env is reset (fresh people, the
+     fire kept, as EvacuationEnv.reset does): all envs at the start of an episode.
+The start-of-episode rate is also reported beside the stationary value
+(start_phase), from a full reset after the timed steps.
+
+value = env-steps/s of the whole job (E * n_gpus * steps / time) at the headline
+schedule and precision; the JSON line also carries agent-transitions/s (x R), the
+other schedule's rate, the env-only rate, the roofline of the dominant kernel
+(env_step_kernel, HBM-bound) and the CPU baseline. Prints ONE JSON line on rank 0.
 """
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 
@@ -36,7 +44,7 @@ import torch  # noqa: E402
 
 METRIC = "env steps/sec + agent-transitions/sec (whole node), 128x128 grid, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
-BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (spec)
+BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (spec); f32 via bf16x3 split runs on the same pipe
 EV_EVERY = 5               # timed steps between two HIP-event-bracketed env.step launches
 
 
@@ -74,10 +82,13 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=1300)
+    ap.add_argument("--warmup", type=int, default=10, help="untimed training steps after the preparation")
+    ap.add_argument("--phase", choices=["stationary", "start"], default="stationary",
+                    help="episode phase of the timed steps (module docstring)")
+    ap.add_argument("--age-steps", type=int, default=1300,
+                    help="env-only preparation steps that spread env ages over an episode (before --warmup)")
     ap.add_argument("--stagger", type=int, default=1200,
-                    help="warmup step w force-resets envs with global id %% stagger == w, so the timed steps see "
-                         "env ages spread over a whole episode (the stationary mix of a long run); 0 = off")
+                    help="preparation step w force-resets envs with global id %% stagger == w (0 = no stagger)")
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
     ap.add_argument("--grid", type=int, default=128)
     ap.add_argument("--layouts", type=int, default=1,
@@ -85,18 +96,22 @@ def parse():
     ap.add_argument("--people", type=int, default=2276)
     ap.add_argument("--robots", type=int, default=16)
     ap.add_argument("--batch", type=int, default=4096)
-    ap.add_argument("--precision", choices=["bf16", "f32"], default="bf16")
+    ap.add_argument("--precision", choices=["bf16", "f32"], default="f32",
+                    help="Q-net arithmetic: f32 (the reference's; fused kernels with bf16x3-split MFMA operands) "
+                         "or bf16")
     ap.add_argument("--qnet", choices=["mlp", "conv"], default="mlp",
                     help="conv: the reference's DQNNetwork (3 conv3x3 + fc stack) on the general MFMA GEMMs "
                          "(cfg4); mlp: the fused 726-512-256-5 kernels")
     ap.add_argument("--mode", choices=["train", "env"], default="train")
     ap.add_argument("--env-steps", type=int, default=100, help="extra env-only timed steps (0 = skip)")
-    ap.add_argument("--strict-steps", type=int, default=100,
-                    help="extra timed steps in the strict schedule after a lagged run (0 = skip)")
-    ap.add_argument("--cpu-envs", type=int, default=2048)
+    ap.add_argument("--other-steps", type=int, default=100,
+                    help="extra timed steps in the other schedule (lagged when strict is the headline; 0 = skip)")
+    ap.add_argument("--start-steps", type=int, default=20,
+                    help="extra: timed training steps right after a full reset (start of episode; 0 = skip)")
+    ap.add_argument("--cpu-envs", type=int, default=1024)
     ap.add_argument("--cpu-steps", type=int, default=600)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--schedule", choices=["strict", "lagged"], default="lagged",
+    ap.add_argument("--schedule", choices=["strict", "lagged"], default="strict",
                     help="strict: act, env.step, push, learn (the reference's order); lagged: learn t samples "
                          "the ring before push t and overlaps env.step t (evacx.trainer.VecTrainer)")
     ap.add_argument("--replay", choices=["uniform", "prioritized"], default="uniform",
@@ -105,9 +120,33 @@ def parse():
     ap.add_argument("--groups", type=int, default=1,
                     help="env groups per GPU, each with its own act -> env.step -> push stream chain "
                          "(evacx.trainer._Group): one group's env.step tail overlaps the others' work")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r1", "env_traffic.json"),
-                    help="PMC traffic record of env_step_kernel on this workload (tools/parse_prof.py)")
+    ap.add_argument("--traffic", default=None,
+                    help="PMC traffic record of env_step_kernel on this workload and phase (tools/parse_prof.py); "
+                         "default profiles/r2/env_traffic_<phase>.json")
     return ap.parse_args()
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def host_threads():
+    """Threads the CPU baseline may use: every core of this process's affinity set, capped
+    by OMP_NUM_THREADS when the launcher sets it (a GPU box's per-GPU CPU share)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
 
 
 def main():
@@ -132,12 +171,12 @@ def main():
     if args.layouts > 1:  # per-env layouts: env e runs random layout e % K
         from evacx.env import LayoutSet
         from evacx.layout import random_layout
-        lay = LayoutSet([DeviceLayout(build_tables(random_layout(L, W, R, 4242 + k)), P) for k in range(args.layouts)])
+        lay_tables = [build_tables(random_layout(L, W, R, 4242 + k)) for k in range(args.layouts)]
+        lay = LayoutSet([DeviceLayout(t, P) for t in lay_tables])
         layout_of = [(rank * E + e) % args.layouts for e in range(E)]
-        tables = lay.tables
     else:
-        tables = build_tables(spec)
-        lay = DeviceLayout(tables, P)
+        lay_tables = [build_tables(spec)]
+        lay = DeviceLayout(lay_tables[0], P)
     hook = make_allreduce_hook(dist, world) if dist is not None else None
     tr = VecTrainer(lay, E, env_offset=rank * E, kind=args.qnet, precision=args.precision, batch=args.batch,
                     grad_hook=hook,
@@ -145,6 +184,8 @@ def main():
                     replay_capacity=args.replay_capacity, groups=args.groups if args.mode == "train" else 1,
                     layout_of=layout_of)
     env = tr.env
+    lagged_ok = tr.fast is not None  # the lagged schedule needs the fused MLP path
+    schedule = args.schedule if lagged_ok else "strict"
 
     def barrier():
         if dist is not None:
@@ -158,76 +199,77 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    # ------------------------------------------------------------ warmup
-    # Env ages are staggered over one episode length: a synchronised start would time
-    # only one episode phase (per-step cost varies several-fold over an episode).
+    # --------------------------------------------------- episode-phase preparation
+    # env-only steps (uniform random actions): preparation step w force-resets the envs
+    # with global id % stagger == w, spreading env ages over one episode length
     gid = torch.arange(E, device="cuda") + rank * E
     S = args.stagger
-    for w in range(args.warmup):
-        force = (gid % S == w) if 0 < S and w < S else None
-        if args.mode == "train":
-            tr.step(extra_reset=force)
-        else:
-            env.step(torch.randint(0, 5, (E * R,), device="cuda", dtype=torch.int32), auto_reset=True)
-            if force is not None:
-                env.reset(mask=force & ~env.done.bool())
-    if args.mode == "train":
-        tr.sync()
+    prep_acts = torch.empty(E * R, device="cuda", dtype=torch.int32)
+    g = torch.Generator(device="cuda").manual_seed(4321 + rank)
+    for w in range(args.age_steps):
+        torch.randint(0, 5, (E * R,), device="cuda", dtype=torch.int32, generator=g, out=prep_acts)
+        env.step(prep_acts, auto_reset=True)
+        if 0 < S and w < S:
+            force = (gid % S == w) & ~env.done.bool()
+            env.reset(mask=force)
+    if args.phase == "start":
+        env.reset()  # every env at the start of an episode (people fresh, fire kept)
     barrier()
+
+    def timed_train(n, ev_env=None, ev_learn=None):
+        barrier()
+        t0 = time.perf_counter()
+        for s in range(n):
+            if args.mode == "train":
+                tr.step(ev_env=None if ev_env is None or s % EV_EVERY else ev_env[s],
+                        ev_learn=None if ev_learn is None or s % EV_EVERY else ev_learn[s])
+            else:
+                env.compute_order()
+                if ev_env is not None and s % EV_EVERY == 0:
+                    ev_env[s][0].record()
+                env.step(acts_env[s], order=False, auto_reset=True)
+                if ev_env is not None and s % EV_EVERY == 0:
+                    ev_env[s][1].record()
+        if args.mode == "train":
+            tr.sync()
+        barrier()
+        return max_over_ranks(time.perf_counter() - t0)
+
+    def ev_pairs(n):
+        return [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+
+    def ev_mean(evs, n):
+        return float(np.mean([evs[s][0].elapsed_time(evs[s][1]) for s in range(n) if s % EV_EVERY == 0]))
+
+    # ----------------------------------------------------------------- warmup
+    acts_env = torch.randint(0, 5, (max(args.steps, args.warmup, 1), E * R), device="cuda", dtype=torch.int32)
+    timed_train(args.warmup)
 
     # the CPU baseline continues from exactly this state (same envs, same episode phase)
     cpu_snap = None
     if rank == 0 and not args.no_cpu:
-        cpu_snap = [env.host_state(i) for i in range(min(args.cpu_envs, E))]
+        cpu_snap = [(env.host_state(i), layout_of[i] if layout_of else 0) for i in range(min(args.cpu_envs, E))]
 
-    # ------------------------------------------------------- timed steps
-    ev_env = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    ev_learn = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    rand_actions = torch.randint(0, 5, (args.steps, E * R), device="cuda", dtype=torch.int32)
-    barrier()
-    t0 = time.perf_counter()
+    # ------------------------------------------------------------ timed steps
     # HIP events bracket env.step on its own stream on every EV_EVERY-th step only: an
-    # event record costs the stream a ~6 us gap (tools/gap_probe.py), which would
-    # otherwise be charged to every timed step
-    timed = [s for s in range(args.steps) if s % EV_EVERY == 0]
-    for s in range(args.steps):
-        ee = ev_env[s] if s % EV_EVERY == 0 else None
-        el = ev_learn[s] if s % EV_EVERY == 0 else None
-        if args.mode == "train":
-            tr.step(ev_env=ee, ev_learn=el)
-        else:
-            env.compute_order()
-            if ee is not None:
-                ee[0].record()
-            env.step(rand_actions[s], order=False, auto_reset=True)  # finished envs reset in the launch
-            if ee is not None:
-                ee[1].record()
-    if args.mode == "train":
-        tr.sync()
-    barrier()
-    elapsed = max_over_ranks(time.perf_counter() - t0)
+    # event record costs the stream a ~6 us gap (tools/gap_probe.py)
+    ev_env, ev_learn = ev_pairs(args.steps), ev_pairs(args.steps)
+    elapsed = timed_train(args.steps, ev_env, ev_learn if args.mode == "train" else None)
     env.check_err()
-    kern_ms = float(np.mean([ev_env[s][0].elapsed_time(ev_env[s][1]) for s in timed]))
-    learn_ms = (float(np.mean([ev_learn[s][0].elapsed_time(ev_learn[s][1]) for s in timed]))
-                if args.mode == "train" else None)
+    kern_ms = ev_mean(ev_env, args.steps)
+    learn_ms = ev_mean(ev_learn, args.steps) if args.mode == "train" else None
     loss = float(tr.last_loss.item()) if tr.last_loss is not None else None
+    value = E * world * args.steps / elapsed
 
-    # ------------------- the reference's strict order on the same state (extra)
-    strict = None
-    if args.mode == "train" and args.schedule == "lagged" and args.strict_steps > 0:
+    # ------------------------------- the other schedule on the same state (extra)
+    other = None
+    if args.mode == "train" and lagged_ok and args.other_steps > 0:
         tr.sync()
-        tr.lagged = False
-        for _ in range(20):
-            tr.step()
-        tr.sync()
-        barrier()
-        t1 = time.perf_counter()
-        for _ in range(args.strict_steps):
-            tr.step()
-        tr.sync()
-        barrier()
-        strict = E * world * args.strict_steps / max_over_ranks(time.perf_counter() - t1)
-        tr.lagged = True
+        tr.lagged = schedule == "strict"
+        timed_train(10)
+        other = {"schedule": "lagged" if tr.lagged else "strict",
+                 "steps_per_s": E * world * args.other_steps / timed_train(args.other_steps)}
+        tr.lagged = schedule == "lagged"
 
     # --------------------------------------------- env-only rate (extra)
     env_only = None
@@ -240,20 +282,37 @@ def main():
         barrier()
         env_only = E * world * args.env_steps / max_over_ranks(time.perf_counter() - t1)
 
-    value = E * world * args.steps / elapsed
+    # ------------------------- start of episode: every env freshly reset (extra)
+    start = None
+    if args.start_steps > 0 and args.phase == "stationary":
+        tr.sync()
+        env.reset()
+        ev_s = ev_pairs(args.start_steps)
+        dt = timed_train(args.start_steps, ev_s)
+        start = {"steps_per_s": E * world * args.start_steps / dt, "env_step_kernel_ms": ev_mean(ev_s, args.start_steps),
+                 "steps": args.start_steps,
+                 "what": "every env reset (all persons in play), then the timed training steps"}
+
     G = (L + 2) * (W + 2)
     bpe = bytes_per_env_step(P, R, G)
     per_launch = E // args.groups if args.mode == "train" else E  # env.step launches of group 0 are timed
     achieved = bpe * per_launch / (kern_ms * 1e-3) / 1e9
-    traffic = None
-    if os.path.exists(args.traffic):
-        # HBM bytes per launch from rocprofv3 PMC passes of this same workload (separate
-        # --pmc FETCH_SIZE / WRITE_SIZE runs; cannot be collected inside the timed run)
-        rec = json.load(open(args.traffic))
-        if rec.get("kernel") == "env_step_kernel":
+    traffic, traffic_src = None, None
+    tpath = args.traffic or os.path.join(ROOT, "profiles", "r2", f"env_traffic_{args.phase}.json")
+    if os.path.exists(tpath):
+        # HBM bytes per launch from rocprofv3 PMC passes of this same workload and phase
+        # (separate --pmc FETCH_SIZE / WRITE_SIZE runs; cannot be collected inside the timed run)
+        rec = json.load(open(tpath))
+        if rec.get("kernel") == "env_step_kernel" and rec.get("envs") in (None, per_launch):
             traffic = rec["bytes_per_env_step"] * per_launch
-    cpu = cpu_baseline(cpu_snap, env.lay.R, tables, P, args) if cpu_snap is not None else None
+            traffic_src = os.path.relpath(tpath, ROOT)
+    cpu = None
+    if cpu_snap is not None:
+        cpu = cpu_baseline(cpu_snap, env.lay.R, lay_tables, P, args, E)
     if rank == 0:
+        prec = args.precision
+        qdesc = ("f32 Q-net (bf16x3-split MFMA operands)" if prec == "f32" and tr.fast is not None
+                 else f"{prec} Q-net")
         line = {
             "metric": METRIC,
             "value": value,
@@ -262,77 +321,142 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "stagger": args.stagger,
             "ms_per_step": 1e3 * elapsed / args.steps,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f64" if args.mode == "env" else f"f64 env + {args.precision} Q-net",
+            "dtype": "f64" if args.mode == "env" else f"f64 env + {qdesc}",
             "data": "synthetic",
             "config": {
                 "workload": (f"{cfg_name(args)} per-GPU share: {L}x{W} synthetic layout"
                              + (f" ({args.layouts} random per-env layouts)" if args.layouts > 1 else "")
                              + f", {P} people, {R} robots, {E} envs/GPU; "
-                             + ("full training step: act + env.step + replay push + learn (B="
-                                f"{args.batch}) + auto-reset" if args.mode == "train"
-                                else "env.step + auto-reset, uniform random actions")),
+                             + (f"full training step ({schedule} schedule): act + env.step + replay push + learn "
+                                f"(B={args.batch}) + auto-reset" if args.mode == "train"
+                                else "env.step + auto-reset, uniform random actions")
+                             + ("; episode phase: stationary mix (env ages spread uniformly over "
+                                f"{S} steps by a {args.age_steps}-step env-only preparation)"
+                                if args.phase == "stationary" else
+                                "; episode phase: start (every env freshly reset before the timed steps)")),
+                "episode_phase": args.phase, "age_steps": args.age_steps, "stagger": S,
                 "envs_per_gpu": E, "grid": f"{L}x{W}", "people": P, "robots": R, "mode": args.mode,
-                "batch": args.batch, "schedule": args.schedule if tr.fast is not None else "strict",
+                "batch": args.batch, "schedule": schedule, "precision": prec,
                 "qnet": ("MLP 726-512-256-5" if args.qnet == "mlp"
                          else "DQNNetwork conv 6-32-64-128 + 15488-512-256-5"),
                 "replay": args.replay, "groups": args.groups if args.mode == "train" else 1,
                 "parallelism": f"data-parallel over {world} GPU(s): envs sharded, grad all-reduce (RCCL) per learn",
             },
-            "strict_schedule_steps_per_s": strict,
+            "other_schedule": other,
             "env_only_steps_per_s": env_only,
+            "start_phase": start,
             "env_step_kernel_ms": kern_ms,
             "learn_ms": learn_ms,
             "last_loss": loss,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "env_step_kernel",
-                         "kernel_ms": kern_ms, "bytes_per_env_step": bpe, "env_steps_per_launch": per_launch,
-                         "launches_timed": len(timed)},
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                         "kernel": "env_step_kernel", "kernel_ms": kern_ms, "bytes_per_env_step": bpe,
+                         "env_steps_per_launch": per_launch,
+                         "launches_timed": len([s for s in range(args.steps) if s % EV_EVERY == 0])},
             "cpu_baseline": cpu,
         }
         if learn_ms is not None and args.qnet == "mlp":
             fl = qnet_flops(0, args.batch)
             line["roofline_learn"] = {"bound": "mfma", "achieved": fl / (learn_ms * 1e-3) / 1e12,
                                       "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                                      "frac": fl / (learn_ms * 1e-3) / 1e12 / BF16_PEAK_TFLOPS}
+                                      "frac": fl / (learn_ms * 1e-3) / 1e12 / BF16_PEAK_TFLOPS,
+                                      "flops_basis": "dense f32-equivalent FLOPs of one learn step"}
         print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()
 
 
-def cpu_baseline(snap, R, tables, P, args):
+def cpu_learner_ms(args, threads):
+    """The reference's learn step (agents/dqn_agent.py:126-168) and act forward for the MLP
+    variant, in torch on the host cores: ms per learn at B=batch, ms per act row."""
+    import torch.nn as nn
+    torch.set_num_threads(threads)
+    net = nn.Sequential(nn.Linear(726, 512), nn.ReLU(), nn.Dropout(0.2), nn.Linear(512, 256), nn.ReLU(),
+                        nn.Linear(256, 5))
+    tgt = nn.Sequential(nn.Linear(726, 512), nn.ReLU(), nn.Dropout(0.2), nn.Linear(512, 256), nn.ReLU(),
+                        nn.Linear(256, 5))
+    opt = torch.optim.Adam(net.parameters(), lr=1e-4)
+    B = args.batch
+    s, s2 = torch.rand(B, 726), torch.rand(B, 726)
+    a = torch.randint(0, 5, (B,))
+    r, d = torch.rand(B), torch.zeros(B, dtype=torch.bool)
+
+    def learn():
+        q = net(s).gather(1, a.unsqueeze(1))
+        with torch.no_grad():
+            y = r + 0.99 * tgt(s2).max(1)[0] * ~d
+        loss = nn.functional.mse_loss(q.squeeze(), y)
+        opt.zero_grad()
+        loss.backward()
+        nn.utils.clip_grad_norm_(net.parameters(), 1.0)
+        opt.step()
+
+    n_act = 8192
+    xa = torch.rand(n_act, 726)
+    for _ in range(2):
+        learn()
+        with torch.no_grad():
+            net(xa).argmax(1)
+    t0 = time.perf_counter()
+    for _ in range(5):
+        learn()
+    t_learn = (time.perf_counter() - t0) / 5
+    t0 = time.perf_counter()
+    for _ in range(5):
+        with torch.no_grad():
+            net(xa).argmax(1)
+    t_act_row = (time.perf_counter() - t0) / 5 / n_act
+    return 1e3 * t_learn, 1e3 * t_act_row
+
+
+def cpu_baseline(snap, R, lay_tables, P, args, E):
     """Oracle (C restatement, OpenMP over envs) on the host cores, started from the GPU
     state of the first cpu_envs envs at the beginning of the timed region (same episode
-    phase), stepped with uniform random actions."""
+    phase), stepped with uniform random actions; plus the reference's learn/act in torch
+    on the same cores, composed into the rate of the same full training step."""
     try:
         from oracle import oracle as orc
     except Exception as e:  # oracle not built: report, never fall back
         return {"error": f"oracle unavailable: {e}"}
     n = len(snap)
-    olay = orc.Layout.from_tables(tables, P)
+    olays = [orc.Layout.from_tables(t, P) for t in lay_tables]
     envs = []
-    for st in snap:
-        oe = orc.Env(olay, thmap=False)
+    for st, li in snap:
+        oe = orc.Env(olays[li], thmap=False)
         oe.load_state(st)
-        envs.append(oe)
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, 16))
+        envs.append((li, oe))
+    threads = host_threads()
     steps = args.cpu_steps
-    acts = np.random.RandomState(0).randint(0, 5, size=(steps, n * R)).astype(np.int32)
-    t0 = time.perf_counter()
-    done_steps, _ = orc.run_batch(olay, envs, steps, acts, nthreads=cores)
-    dt = time.perf_counter() - t0
-    return {"value": done_steps / dt, "unit": "env-steps/s", "cores": cores, "kind": "port",
-            "sample": f"{n} envs x {steps} env.steps of the same workload from the GPU's warmed-up state "
-                      f"(env.step only, no learner), OpenMP {cores} threads, {dt:.2f}s wall, "
-                      f"{dt * cores:.1f} core-s"}
+    done_steps, dt = 0, 0.0
+    for li, olay in enumerate(olays):  # per layout: run_batch steps envs of one layout
+        group = [oe for (l, oe) in envs if l == li]
+        if not group:
+            continue
+        acts = np.random.RandomState(li).randint(0, 5, size=(steps, len(group) * R)).astype(np.int32)
+        t0 = time.perf_counter()
+        k, _ = orc.run_batch(olay, group, steps, acts, nthreads=threads)
+        dt += time.perf_counter() - t0
+        done_steps += k
+    env_rate = done_steps / dt
+    out = {"value": env_rate, "unit": "env-steps/s", "cores": threads, "kind": "port",
+           "nproc": os.cpu_count(), "cpu_model": cpu_model(),
+           "sample": f"{n} envs x {steps} env.steps of the same workload from the GPU's state at the start of the "
+                     f"timed region (env.step only), OpenMP {threads} threads (all cores of this process's "
+                     f"affinity set, capped by OMP_NUM_THREADS), {dt:.2f}s wall, {dt * threads:.1f} core-s; "
+                     "compare with env_only_steps_per_s"}
+    if args.mode == "train" and args.qnet == "mlp":
+        t_learn, t_row = cpu_learner_ms(args, threads)
+        t_step = E / env_rate * 1e3 + E * R * t_row + t_learn  # ms per full training step of E envs
+        out["train_step"] = {"value": E / (t_step * 1e-3), "unit": "env-steps/s",
+                             "learn_ms": t_learn, "act_us_per_row": 1e3 * t_row,
+                             "what": "oracle env.step + torch-CPU act forward (E*R rows) + torch-CPU learn "
+                                     f"(B={args.batch}, f32) on the same {threads} threads, composed per step "
+                                     "of E envs; compare with value"}
+    return out
 
 
 if __name__ == "__main__":

@@ -320,8 +320,41 @@ typedef struct {
     int first;     /* index into mover list */
 } target_t;
 
+/* per-thread planner workspace, allocated once per batch (not per step) */
+typedef struct {
+    int *tgt_of;      /* [GXY] cell -> target slot or -1 */
+    int *mover_next;  /* [P] */
+    double *scratch;  /* [P] */
+    target_t *targets;
+    int *mover;
+    int *mover_tail;
+} orc_work;
+
+static int work_alloc(const orc_layout *l, orc_work *w) {
+    const int GXY = (l->L + 2) * (l->W + 2);
+    const int P1 = l->P > 0 ? l->P : 1;
+    w->tgt_of = (int *)malloc(sizeof(int) * GXY);
+    w->mover_next = (int *)malloc(sizeof(int) * P1);
+    w->scratch = (double *)malloc(sizeof(double) * P1);
+    w->targets = (target_t *)malloc(sizeof(target_t) * P1);
+    w->mover = (int *)malloc(sizeof(int) * P1);
+    w->mover_tail = (int *)malloc(sizeof(int) * P1);
+    if (!w->tgt_of || !w->mover_next || !w->scratch || !w->targets || !w->mover || !w->mover_tail) return -12;
+    for (int c = 0; c < GXY; c++) w->tgt_of[c] = -1;
+    return 0;
+}
+
+static void work_free(orc_work *w) {
+    free(w->tgt_of);
+    free(w->mover_next);
+    free(w->scratch);
+    free(w->targets);
+    free(w->mover);
+    free(w->mover_tail);
+}
+
 /* People.run (envs/people.py:196-253) including execute_move (:299-314) */
-static void people_run(const orc_layout *l, orc_env *e, int *tgt_of, int *mover_next) {
+static void people_run(const orc_layout *l, orc_env *e, orc_work *wk) {
     const int P = l->P;
     const int GXY = (l->L + 2) * (l->W + 2);
     const int fs = e->scal[S_FIRE];
@@ -335,11 +368,11 @@ static void people_run(const orc_layout *l, orc_env *e, int *tgt_of, int *mover_
     }
     /* 2. plan against the rmap snapshot; move_plan keeps dict insertion order */
     int ntargets = 0;
-    int *cell_target = tgt_of; /* [GXY] -> target slot or -1 */
-    for (int c = 0; c < GXY; c++) cell_target[c] = -1;
-    target_t *targets = (target_t *)malloc(sizeof(target_t) * (P > 0 ? P : 1));
-    int *mover = (int *)malloc(sizeof(int) * (P > 0 ? P : 1));
-    int *mover_tail = (int *)malloc(sizeof(int) * (P > 0 ? P : 1));
+    int *cell_target = wk->tgt_of; /* [GXY] -> target slot or -1 (all -1 between calls) */
+    int *mover_next = wk->mover_next;
+    target_t *targets = wk->targets;
+    int *mover = wk->mover;
+    int *mover_tail = wk->mover_tail;
     for (int i = 0; i < P; i++) {
         if (e->flags[i] & 3) continue;
         e->acc[i] += person_speed(e->health[i]) * 0.5;
@@ -394,9 +427,6 @@ static void people_run(const orc_layout *l, orc_env *e, int *tgt_of, int *mover_
                 e->thmap[CELL(l, e->pos[2 * mover[m]], e->pos[2 * mover[m] + 1])] += 1;
     }
     for (int t = 0; t < ntargets; t++) cell_target[targets[t].cell] = -1;
-    free(targets);
-    free(mover);
-    free(mover_tail);
 }
 
 /* EvacuationEnv._calculate_reward (envs/evacuation_env.py:174-288) */
@@ -478,13 +508,13 @@ static double calc_reward(const orc_layout *l, orc_env *e, double *scratch) {
 }
 
 static int env_step_impl(const orc_layout *l, orc_env *e, const int32_t *actions, double *reward,
-                         int32_t *done, double *obs, int *tgt_of, int *mover_next, double *scratch) {
+                         int32_t *done, double *obs, orc_work *wk) {
     /* EvacuationEnv.step (envs/evacuation_env.py:122-172) /
      * EvacuationEnvMulti.step (envs/evacuation_env_multi.py:55-89) */
     for (int r = 0; r < l->R; r++) move_robot(l, e, actions[r], r);
-    people_run(l, e, tgt_of, mover_next);
+    people_run(l, e, wk);
     if (e->scal[S_FIRE] < l->t_max) e->scal[S_FIRE] += 1; /* both fire models */
-    *reward = calc_reward(l, e, scratch);
+    *reward = calc_reward(l, e, wk->scratch);
     e->time[0] += 0.5;
     e->scal[S_STEP] += 1;
     int evac = 0, dead = 0;
@@ -499,14 +529,13 @@ static int env_step_impl(const orc_layout *l, orc_env *e, const int32_t *actions
 
 int orc_env_step(const orc_layout *l, orc_env *e, const int32_t *actions, double *reward,
                  int32_t *done, double *obs) {
-    const int GXY = (l->L + 2) * (l->W + 2);
-    int *tgt_of = (int *)malloc(sizeof(int) * GXY);
-    int *mover_next = (int *)malloc(sizeof(int) * (l->P > 0 ? l->P : 1));
-    double *scratch = (double *)malloc(sizeof(double) * (l->P > 0 ? l->P : 1));
-    int rc = env_step_impl(l, e, actions, reward, done, obs, tgt_of, mover_next, scratch);
-    free(tgt_of);
-    free(mover_next);
-    free(scratch);
+    orc_work wk;
+    if (work_alloc(l, &wk)) {
+        work_free(&wk);
+        return -12;
+    }
+    int rc = env_step_impl(l, e, actions, reward, done, obs, &wk);
+    work_free(&wk);
     return rc;
 }
 
@@ -516,29 +545,24 @@ long orc_run_batch(const orc_layout *l, orc_env *envs, int E, int steps, const i
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
 #endif
-    const int GXY = (l->L + 2) * (l->W + 2);
 #pragma omp parallel reduction(+ : total)
     {
-        int *tgt_of = (int *)malloc(sizeof(int) * GXY);
-        int *mover_next = (int *)malloc(sizeof(int) * (l->P > 0 ? l->P : 1));
-        double *scratch = (double *)malloc(sizeof(double) * (l->P > 0 ? l->P : 1));
+        orc_work wk;
+        const int ok = work_alloc(l, &wk) == 0;
 #pragma omp for schedule(dynamic, 1)
         for (int ei = 0; ei < E; ei++) {
             double acc_r = 0.0;
-            for (int s = 0; s < steps; s++) {
+            for (int s = 0; s < steps && ok; s++) {
                 double r;
                 int32_t d;
-                env_step_impl(l, &envs[ei], actions + ((size_t)s * E + ei) * l->R, &r, &d, NULL, tgt_of,
-                              mover_next, scratch);
+                env_step_impl(l, &envs[ei], actions + ((size_t)s * E + ei) * l->R, &r, &d, NULL, &wk);
                 acc_r += r;
                 total++;
                 if (d) orc_env_reset(l, &envs[ei], NULL);
             }
             if (reward_sum) reward_sum[ei] = acc_r;
         }
-        free(tgt_of);
-        free(mover_next);
-        free(scratch);
+        work_free(&wk);
     }
     return total;
 }
