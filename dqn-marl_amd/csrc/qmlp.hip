@@ -21,6 +21,14 @@
 //
 // Dropout keep bits are a counter-based hash of (seed, stream, row pair, col), 16 bits
 // per element; the backward pass reads the mask back as [H1 > 0] instead of storing it.
+//
+// X3 (f32-accurate) mode, the reference's fp32 arithmetic on the bf16 matrix cores: an f32
+// operand v is carried as hi = bf16(v) and lo = bf16(v - hi) (16 significant bits) and a
+// product as hi*hi + hi*lo + lo*hi (relative error ~2^-16 per product, f32 accumulation);
+// operands that are exactly 0/1 (occupancy, barrier, exit) have no lo part. fc1's K grows
+// to 640: the compact 512 (hi of the danger feature) plus one slot per cell for the danger's
+// lo residual (k = 512 + c), which multiplies the danger column's hi weight. Split
+// activations (H1, dZ2, dZ1) are stored as two bf16 planes [2][rows][cols].
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -41,10 +49,21 @@ constexpr int HID = 512, HID2 = 256, NACT = 5, K1 = 726, NCELL = 121;
 // with max = inf) and channel 5 is the constant centre one-hot, folded into the bias:
 // b1c = b1 + bf16(W1[:, CENTRE_COL]). 726 -> 512 contraction length, same products.
 constexpr int K1P = 512, KC1 = 32, NKC1 = K1P / KC1;
+constexpr int K1X = 640, NKC1X = K1X / KC1;  // X3: + the danger residual slot of every cell
 constexpr int CENTRE_COL = 60 * 6 + 5;
 constexpr int RM = 64;  // rows per workgroup (fc23, backward)
 // reference column (of the 726) of compact feature k < 4 * NCELL
 __host__ __device__ __forceinline__ int ref_col(int k) { return (k >> 2) * 6 + (k & 3) + 1; }
+// X3: reference column of x column k < 640 (the danger residual of cell c at 512 + c adds
+// into the danger column of c), -1 for padding
+__host__ __device__ __forceinline__ int ref_col3(int k) {
+    return k < 4 * NCELL ? ref_col(k) : (k >= K1P && k < K1P + NCELL) ? (k - K1P) * 6 + 2 : -1;
+}
+// f32 -> (hi, lo) bf16 pair of the X3 mode; v - hi is exact in f32
+__device__ __forceinline__ void split2(float v, __bf16& hi, __bf16& lo) {
+    hi = (__bf16)v;
+    lo = (__bf16)(v - (float)hi);
+}
 
 __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
     h ^= h >> 16;
@@ -87,8 +106,8 @@ __device__ __forceinline__ float u01(uint32_t v) { return (float)(v >> 8) * (1.0
 // Weights in MFMA B-operand order: the block of (32-column tile t, K-chunk kc,
 // 16-wide step s) holds lane l's 8 values (column 32t + (l&31), k = kc*KC + 16s +
 // 8(l>>5) .. +7) at l*8, so a wave's operand load is one contiguous 1-KB read.
-__host__ __device__ __forceinline__ size_t w1_tile(int t, int kc, int s) {
-    return ((size_t)(t * NKC1 + kc) * 2 + s) * 512;
+__host__ __device__ __forceinline__ size_t w1_tile(int t, int kc, int s, int nkc = NKC1) {
+    return ((size_t)(t * nkc + kc) * 2 + s) * 512;
 }
 __host__ __device__ __forceinline__ size_t w2_tile(int t, int kc, int s) {
     return ((size_t)(t * (HID / 32) + kc) * 2 + s) * 512;
@@ -136,6 +155,15 @@ struct Fwd {
     int stat_fs;
     // qfc1_kernel raw mode: f32 pre-activation (acc + bias, no ReLU / dropout) [N][512]
     float* raw;
+    // X3 mode: danger residual features (evx_layout.obs_feat_lo / obs_feats_lo), lo weight
+    // copies (w1 then spans K1X), the lo plane of h1
+    const uint16_t* feat_lo;
+    const uint16_t* const* feats_lo;
+    const __bf16* w1l;
+    const __bf16* w2l;
+    __bf16* h1l;
+    // explicit dropout keep mask [N][512] (replaces the hash when set)
+    const uint8_t* drop_mask;
 };
 
 // One row's window in the static feature map (evx_layout.obs_feat): base index of
@@ -175,16 +203,22 @@ __device__ __forceinline__ uint2 cell_feat(const evx_obs& ob, int c, uint32_t v)
 // thread expands 2 (or 4) cells of one row per chunk from their static feature
 // words (loaded two chunks ahead) into a double-buffered LDS A tile, one barrier per
 // chunk. Returns after a barrier with the A buffers free.
-template <int MT, int NTW, int NWV>
+// X3: 4 more chunks of 32 cells' danger residuals (8 or 16 per thread), and every
+// compact chunk's fragments meet the lo weights too (the features are exact in bf16
+// except the danger, whose lo rides in the extra chunks).
+// Column tile nt of a wave starts at ncol0 + nt * nstride.
+template <int MT, int NTW, int NWV, bool X3 = false>
 __device__ __forceinline__ void fc1_tile(const Fwd& a, int m0, int ncol0, bool want_x, char* smem,
-                                         f32x16 (&acc)[MT][NTW]) {
+                                         f32x16 (&acc)[MT][NTW], int nstride = 32) {
     constexpr int NT = 64 * NWV, RT = 32 * MT;
     constexpr int CPT = 8 * RT / NT, TPR = 8 / CPT;  // cells per thread and chunk, threads per row
     static_assert(CPT == 2 || CPT == 4, "generator: 16-B A stores");
+    constexpr int NKC = X3 ? NKC1X : NKC1, KX = X3 ? K1X : K1P;
+    constexpr int LPT = 32 / TPR;  // X3 residual chunks: cells per thread
     constexpr int APAD = KC1 + 8;
     auto As = reinterpret_cast<__bf16 (*)[RT][APAD]>(smem);
     const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
-    const int gr = tid / TPR, gc = (tid % TPR) * CPT;
+    const int gr = tid / TPR, gc = (tid % TPR) * CPT, gl = (tid % TPR) * LPT;
     const bool rowok = m0 + gr < a.N;
     evx_obs ob;
     if (rowok) {
@@ -193,19 +227,42 @@ __device__ __forceinline__ void fc1_tile(const Fwd& a, int m0, int ncol0, bool w
         ob = evx_obs{{0u, 0u, 0u, 0u}, 0, 0, 0, 0};
     }
     const bool wx = a.x && rowok && want_x;
-    const uint32_t* fb = (a.feats ? a.feats[ob.layout] : a.feat) + feat_base(a, ob);
+    const int fbase = feat_base(a, ob);
+    const uint32_t* fb = (a.feats ? a.feats[ob.layout] : a.feat) + fbase;
+    const uint16_t* flb = nullptr;
+    if constexpr (X3) flb = (a.feats_lo ? a.feats_lo[ob.layout] : a.feat_lo) + fbase;
     uint32_t fv[CPT];
+    uint32_t lv[X3 ? LPT / 2 : 1];  // residual bf16 pairs
     auto reads = [&](int kc) {
+        if (!X3 || kc < NKC1) {
 #pragma unroll
-        for (int t = 0; t < CPT; t++) fv[t] = fb[feat_off(a, kc * 8 + gc + t)];
+            for (int t = 0; t < CPT; t++) fv[t] = fb[feat_off(a, kc * 8 + gc + t)];
+        } else if constexpr (X3) {
+#pragma unroll
+            for (int t = 0; t < LPT; t += 2) {  // cells 32 (kc - 16) + gl + t, t + 1 (< 128: inside the padded map)
+                const int c0 = (kc - NKC1) * 32 + gl + t;
+                const uint32_t l0 = c0 < NCELL ? (uint32_t)flb[feat_off(a, c0)] : 0u;
+                const uint32_t l1 = c0 + 1 < NCELL ? (uint32_t)flb[feat_off(a, c0 + 1)] : 0u;
+                lv[t >> 1] = l0 | (l1 << 16);
+            }
+        }
     };
     auto stash = [&](int buf, int kc) {
+        if (!X3 || kc < NKC1) {
 #pragma unroll
-        for (int t = 0; t < CPT; t += 2) {
-            const uint2 f0 = cell_feat(ob, kc * 8 + gc + t, fv[t]), f1 = cell_feat(ob, kc * 8 + gc + t + 1, fv[t + 1]);
-            const uint4 v = make_uint4(f0.x, f0.y, f1.x, f1.y);
-            *reinterpret_cast<uint4*>(&As[buf][gr][(gc + t) * 4]) = v;
-            if (wx) *reinterpret_cast<uint4*>(a.x + (size_t)(m0 + gr) * K1P + kc * KC1 + (gc + t) * 4) = v;
+            for (int t = 0; t < CPT; t += 2) {
+                const uint2 f0 = cell_feat(ob, kc * 8 + gc + t, fv[t]), f1 = cell_feat(ob, kc * 8 + gc + t + 1, fv[t + 1]);
+                const uint4 v = make_uint4(f0.x, f0.y, f1.x, f1.y);
+                *reinterpret_cast<uint4*>(&As[buf][gr][(gc + t) * 4]) = v;
+                if (wx) *reinterpret_cast<uint4*>(a.x + (size_t)(m0 + gr) * KX + kc * KC1 + (gc + t) * 4) = v;
+            }
+        } else if constexpr (X3) {
+#pragma unroll
+            for (int t = 0; t < LPT; t += 8) {
+                const uint4 v = make_uint4(lv[t / 2], lv[t / 2 + 1], lv[t / 2 + 2], lv[t / 2 + 3]);
+                *reinterpret_cast<uint4*>(&As[buf][gr][gl + t]) = v;
+                if (wx) *reinterpret_cast<uint4*>(a.x + (size_t)(m0 + gr) * KX + kc * KC1 + gl + t) = v;
+            }
         }
     };
 #pragma unroll
@@ -214,44 +271,74 @@ __device__ __forceinline__ void fc1_tile(const Fwd& a, int m0, int ncol0, bool w
         for (int j = 0; j < NTW; j++)
 #pragma unroll
             for (int r = 0; r < 16; r++) acc[i][j][r] = 0.f;
-    // B fragments two K chunks ahead (bc: this chunk, bn: the next, bf: the one after)
+    // B fragments two K chunks ahead (bc: this chunk, bn: the next, bf: the one after);
+    // X3: the lo fragments of the compact chunks alongside (lc, ln, lf)
+    constexpr int NL = X3 ? NTW : 1;
+    // (the lo fragments one chunk ahead only: register budget of the X3 act kernel)
     bf16x8 bc[NTW][2], bn[NTW][2], bf[NTW][2];
+    bf16x8 lc[NL][2], ln[NL][2];
     auto loadB = [&](int kc, bf16x8 (&b)[NTW][2]) {
 #pragma unroll
         for (int nt = 0; nt < NTW; nt++) {
-            const int n = ncol0 + nt * 32;
+            const int n = ncol0 + nt * nstride;
 #pragma unroll
             for (int s = 0; s < 2; s++)
-                b[nt][s] = *reinterpret_cast<const bf16x8*>(a.w1 + w1_tile(n >> 5, kc, s) + lane * 8);
+                b[nt][s] = *reinterpret_cast<const bf16x8*>(a.w1 + w1_tile(n >> 5, kc, s, NKC) + lane * 8);
         }
     };
+    auto loadL = [&](int kc, bf16x8 (&l)[NL][2]) {
+        if constexpr (X3) {
+            if (kc < NKC1) {
+#pragma unroll
+                for (int nt = 0; nt < NTW; nt++)
+#pragma unroll
+                    for (int s = 0; s < 2; s++)
+                        l[nt][s] = *reinterpret_cast<const bf16x8*>(a.w1l + w1_tile((ncol0 + nt * nstride) >> 5, kc, s) + lane * 8);
+            }
+        }
+    };
+    // X3: hi fragments one chunk ahead as well (bf unused)
+    constexpr int AH = X3 ? 1 : 2;
     reads(0);
     stash(0, 0);
     reads(1);
     loadB(0, bc);
-    loadB(1, bn);
+    if constexpr (AH == 2) loadB(1, bn);
+    loadL(0, lc);
     __syncthreads();
-    for (int kc = 0; kc < NKC1; kc++) {
+    for (int kc = 0; kc < NKC; kc++) {
         const int buf = kc & 1;
-        if (kc + 2 < NKC1) loadB(kc + 2, bf);
+        if (kc + AH < NKC) loadB(kc + AH, AH == 2 ? bf : bn);
+        if (kc + 1 < NKC) loadL(kc + 1, ln);
 #pragma unroll
         for (int s = 0; s < 2; s++)
 #pragma unroll
             for (int mt = 0; mt < MT; mt++) {
                 const bf16x8 av = *reinterpret_cast<const bf16x8*>(&As[buf][mt * 32 + (lane & 31)][s * 16 + 8 * h]);
 #pragma unroll
-                for (int nt = 0; nt < NTW; nt++)
+                for (int nt = 0; nt < NTW; nt++) {
                     acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bc[nt][s], acc[mt][nt], 0, 0, 0);
+                    if constexpr (X3) {
+                        if (kc < NKC1)
+                            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, lc[nt][s], acc[mt][nt], 0, 0, 0);
+                    }
+                }
             }
-        if (kc + 1 < NKC1) {
+        if (kc + 1 < NKC) {
             stash(buf ^ 1, kc + 1);
-            if (kc + 2 < NKC1) reads(kc + 2);
+            if (kc + 2 < NKC) reads(kc + 2);
 #pragma unroll
             for (int nt = 0; nt < NTW; nt++) {
                 bc[nt][0] = bn[nt][0];
                 bc[nt][1] = bn[nt][1];
-                bn[nt][0] = bf[nt][0];
-                bn[nt][1] = bf[nt][1];
+                if constexpr (AH == 2) {
+                    bn[nt][0] = bf[nt][0];
+                    bn[nt][1] = bf[nt][1];
+                }
+                if constexpr (X3) {
+                    lc[nt][0] = ln[nt][0];
+                    lc[nt][1] = ln[nt][1];
+                }
             }
         }
         __syncthreads();
@@ -260,9 +347,10 @@ __device__ __forceinline__ void fc1_tile(const Fwd& a, int m0, int ncol0, bool w
 
 // fc1 epilogue of one 32-row slab: bias (centre channel folded in), ReLU, dropout
 // (one hash per row pair), bf16 into dst[row within slab][column within tile]
-template <int NTW, int LD>
+// (X3: hi into dst, lo into dstl). An explicit keep mask (a.drop_mask) replaces the hash.
+template <int NTW, int LD, bool X3 = false>
 __device__ __forceinline__ void fc1_slab(const Fwd& a, const f32x16 (&accm)[NTW], const float (&bias)[NTW],
-                                         int row0, int col0, int cl0, __bf16 (*dst)[LD]) {
+                                         int row0, int col0, int cl0, __bf16 (*dst)[LD], __bf16 (*dstl)[LD] = nullptr) {
     const int lane = threadIdx.x & 63, h = lane >> 5;
 #pragma unroll
     for (int r = 0; r < 16; r += 2) {  // rows rl, rl + 1: one dropout hash per pair
@@ -274,13 +362,24 @@ __device__ __forceinline__ void fc1_slab(const Fwd& a, const f32x16 (&accm)[NTW]
             float v0 = accm[nt][r] + bias[nt], v1 = accm[nt][r + 1] + bias[nt];
             v0 = v0 > 0.f ? v0 : 0.f;
             v1 = v1 > 0.f ? v1 : 0.f;
-            if (a.drop_thresh) {
+            if (a.drop_mask) {  // the reference's captured torch mask (tests)
+                const int r0 = row0 + rl, c = col0 + cl;
+                const bool k0 = r0 < a.N && a.drop_mask[(size_t)r0 * HID + c];
+                const bool k1 = r0 + 1 < a.N && a.drop_mask[(size_t)(r0 + 1) * HID + c];
+                v0 = k0 ? v0 * a.drop_scale : 0.f;
+                v1 = k1 ? v1 * a.drop_scale : 0.f;
+            } else if (a.drop_thresh) {
                 const uint32_t hh = drop_pair(ph, (uint32_t)(col0 + cl));
                 v0 = (hh & 0xffffu) >= a.drop_thresh ? v0 * a.drop_scale : 0.f;
                 v1 = (hh >> 16) >= a.drop_thresh ? v1 * a.drop_scale : 0.f;
             }
-            dst[rl][cl] = (__bf16)v0;
-            dst[rl + 1][cl] = (__bf16)v1;
+            if constexpr (X3) {
+                split2(v0, dst[rl][cl], dstl[rl][cl]);
+                split2(v1, dst[rl + 1][cl], dstl[rl + 1][cl]);
+            } else {
+                dst[rl][cl] = (__bf16)v0;
+                dst[rl + 1][cl] = (__bf16)v1;
+            }
         }
     }
 }
@@ -289,19 +388,20 @@ __device__ __forceinline__ void fc1_slab(const Fwd& a, const f32x16 (&accm)[NTW]
 // <4, 2, 8> (128 rows x all 512 columns: every row expanded once); learner batches
 // <2, 1, 4> (64 x 128). H1 is staged per 32-row slab through LDS so it leaves in
 // 16-B row segments.
-template <int MT, int NTW, int NWV>
+template <int MT, int NTW, int NWV, bool X3 = false>
 __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void qfc1_kernel(Fwd a0, Fwd a1) {
     const Fwd& a = blockIdx.z ? a1 : a0;  // two independent problems in one launch (online / target)
     constexpr int NT = 64 * NWV, RT = 32 * MT, NW = 32 * NTW * NWV;
     constexpr int APAD = KC1 + 8, CPAD = NW + 8;
-    constexpr int ABYTES = 2 * RT * APAD * 2, CBYTES = 32 * CPAD * 2;
+    constexpr int ABYTES = 2 * RT * APAD * 2, CBYTES = (X3 ? 2 : 1) * 32 * CPAD * 2;
     __shared__ __attribute__((aligned(16))) char smem[ABYTES > CBYTES ? ABYTES : CBYTES];
     auto Cs = reinterpret_cast<__bf16 (*)[CPAD]>(smem);
+    auto Cl = reinterpret_cast<__bf16 (*)[CPAD]>(smem + 32 * CPAD * 2);  // X3: lo plane
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int m0 = blockIdx.x * RT;
     const int ncol0 = blockIdx.y * NW + w * (32 * NTW);
     f32x16 acc[MT][NTW];
-    fc1_tile<MT, NTW, NWV>(a, m0, ncol0, blockIdx.y == 0, smem, acc);
+    fc1_tile<MT, NTW, NWV, X3>(a, m0, ncol0, blockIdx.y == 0, smem, acc);
     float bias[NTW];
 #pragma unroll
     for (int nt = 0; nt < NTW; nt++) bias[nt] = a.b1[ncol0 + nt * 32 + (lane & 31)];
@@ -320,15 +420,16 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void qfc1_kernel(Fwd a0
 #pragma unroll
     for (int mt = 0; mt < MT; mt++) {
         if (mt) __syncthreads();  // the previous slab has been stored
-        fc1_slab<NTW, CPAD>(a, acc[mt], bias, m0 + mt * 32, blockIdx.y * NW, w * (32 * NTW), Cs);
+        fc1_slab<NTW, CPAD, X3>(a, acc[mt], bias, m0 + mt * 32, blockIdx.y * NW, w * (32 * NTW), Cs, Cl);
         __syncthreads();
         constexpr int SEG = NW / 8;  // 16-B segments per row
-        for (int i = tid; i < 32 * SEG; i += NT) {
-            const int rl = i / SEG, cc = (i - rl * SEG) * 8;
+        for (int i = tid; i < (X3 ? 2 : 1) * 32 * SEG; i += NT) {
+            const int pl = i >= 32 * SEG, ii = i - pl * 32 * SEG;
+            const int rl = ii / SEG, cc = (ii - rl * SEG) * 8;
             const int row = m0 + mt * 32 + rl;
             if (row < a.N)
-                *reinterpret_cast<uint4*>(a.h1 + (size_t)row * HID + blockIdx.y * NW + cc) =
-                    *reinterpret_cast<const uint4*>(&Cs[rl][cc]);
+                *reinterpret_cast<uint4*>((pl ? a.h1l : a.h1) + (size_t)row * HID + blockIdx.y * NW + cc) =
+                    *reinterpret_cast<const uint4*>(pl ? &Cl[rl][cc] : &Cs[rl][cc]);
         }
     }
 }
@@ -531,15 +632,102 @@ __global__ __launch_bounds__(512, 1) void qact_kernel(Fwd a) {
     fc3_act(a, &H2s[row][0], W3s, m0 + row, m0 + row < a.N);
 }
 
+// X3 (f32-accurate) act: the H1 tile of 128 rows would need 256 KB as hi + lo planes, so
+// H1 goes through LDS in two column halves. fc1 runs once over all 512 columns (the
+// observations are expanded once), wave w owning column tiles 32w (half 0) and 256 + 32w
+// (half 1); half hh's tiles go into the two LDS planes, then fc2 accumulates over that
+// half of its K (3 MFMAs per fragment pair: hi*hi, hi*lo, lo*hi). The A staging of fc1,
+// the H1 half planes and finally H2 share one LDS region.
+constexpr int A3_HP = 256 + 8;                     // H1 half-plane row pitch (bf16)
+constexpr int A3_HBYTES = 2 * 128 * A3_HP * 2;     // 135,168: both planes
+static_assert(A3_HBYTES >= 128 * ACT_H2P * 4, "H2 overlays the H1 planes");
+static_assert(A3_HBYTES >= 2 * 128 * (KC1 + 8) * 2, "fc1 A staging overlays the H1 planes");
+constexpr int ACT3_LDS = A3_HBYTES + NACT * HID2 * 4;
+__global__ __launch_bounds__(512, 1) void qact3_kernel(Fwd a) {
+    extern __shared__ __attribute__((aligned(16))) char dsm[];
+    auto Hh = reinterpret_cast<__bf16 (*)[A3_HP]>(dsm);
+    auto Hl = reinterpret_cast<__bf16 (*)[A3_HP]>(dsm + 128 * A3_HP * 2);
+    auto H2s = reinterpret_cast<float (*)[ACT_H2P]>(dsm);
+    auto W3s = reinterpret_cast<float (*)[HID2]>(dsm + A3_HBYTES);
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+    const int m0 = blockIdx.x * 128;
+    for (int i = tid; i < NACT * HID2; i += 512) W3s[i / HID2][i % HID2] = a.w3[i];
+    f32x16 acc[4][2];
+    fc1_tile<4, 2, 8, true>(a, m0, w * 32, false, dsm, acc, 256);  // ends with a barrier: A buffers free
+    f32x16 acc2[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; mt++)
+#pragma unroll
+        for (int r = 0; r < 16; r++) acc2[mt][r] = 0.f;
+#pragma unroll
+    for (int hh = 0; hh < 2; hh++) {
+        const float bias[1] = {a.b1[hh * 256 + w * 32 + (lane & 31)]};
+#pragma unroll
+        for (int mt = 0; mt < 4; mt++) {
+            const f32x16 one[1] = {acc[mt][hh]};
+            fc1_slab<1, A3_HP, true>(a, one, bias, m0 + mt * 32, hh * 256, w * 32,
+                                     reinterpret_cast<__bf16 (*)[A3_HP]>(&Hh[mt * 32][0]),
+                                     reinterpret_cast<__bf16 (*)[A3_HP]>(&Hl[mt * 32][0]));
+        }
+        __syncthreads();
+        // fc2 over K = [256 hh, 256 hh + 256): wave w -> columns [32w, 32w + 32)
+        bf16x8 bc[2], bn[2], lc[2], ln[2];
+        auto loadB = [&](int kc, bf16x8 (&b)[2], bf16x8 (&l)[2]) {
+#pragma unroll
+            for (int s = 0; s < 2; s++) {
+                b[s] = *reinterpret_cast<const bf16x8*>(a.w2 + w2_tile(w, hh * 8 + kc, s) + lane * 8);
+                l[s] = *reinterpret_cast<const bf16x8*>(a.w2l + w2_tile(w, hh * 8 + kc, s) + lane * 8);
+            }
+        };
+        loadB(0, bc, lc);
+        for (int kc = 0; kc < 8; kc++) {
+            if (kc + 1 < 8) loadB(kc + 1, bn, ln);
+#pragma unroll
+            for (int s = 0; s < 2; s++)
+#pragma unroll
+                for (int mt = 0; mt < 4; mt++) {
+                    const int rr = mt * 32 + (lane & 31), kk = kc * 32 + s * 16 + 8 * h;
+                    const bf16x8 ah = *reinterpret_cast<const bf16x8*>(&Hh[rr][kk]);
+                    const bf16x8 al = *reinterpret_cast<const bf16x8*>(&Hl[rr][kk]);
+                    acc2[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bc[s], acc2[mt], 0, 0, 0);
+                    acc2[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, lc[s], acc2[mt], 0, 0, 0);
+                    acc2[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bc[s], acc2[mt], 0, 0, 0);
+                }
+#pragma unroll
+            for (int s = 0; s < 2; s++) {
+                bc[s] = bn[s];
+                lc[s] = ln[s];
+            }
+        }
+        __syncthreads();  // every wave is done with this half: the next half / H2 reuse the planes
+    }
+    {
+        const int col = w * 32 + (lane & 31);
+        const float bias = a.b2[col];
+#pragma unroll
+        for (int mt = 0; mt < 4; mt++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const float v = acc2[mt][r] + bias;
+                H2s[mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h][col] = v > 0.f ? v : 0.f;
+            }
+    }
+    __syncthreads();
+    const int row = tid >> 2;
+    fc3_act(a, &H2s[row][0], W3s, m0 + row, m0 + row < a.N);
+}
+
 // ------------------------------------------------------------ fc2 + fc3
+// X3: A = H1 hi / lo planes, B = fc2.weight hi / lo (3 MFMAs per fragment pair)
+template <bool X3 = false>
 __global__ __launch_bounds__(256, 2) void qfc23_kernel(Fwd a0, Fwd a1) {
     const Fwd& a = blockIdx.z ? a1 : a0;
     // A stages (row pitch 40 bf16 = 20 words: conflict-free ds_read_b128), then H2 in the same
     // bytes (pitch 4 mod 32 words: fc3_act reads conflict-free)
-    constexpr int AP = 40;
-    static_assert(2 * RM * AP * 2 <= RM * (HID2 + 4) * 4, "A stages fit under H2");
+    constexpr int AP = 40, NPL = X3 ? 2 : 1;
+    static_assert(NPL * 2 * RM * AP * 2 <= RM * (HID2 + 4) * 4, "A stages fit under H2");
     __shared__ __attribute__((aligned(16))) char sm23[RM * (HID2 + 4) * 4];
-    auto As = reinterpret_cast<__bf16 (*)[RM][AP]>(sm23);
+    auto As = reinterpret_cast<__bf16 (*)[NPL][RM][AP]>(sm23);  // [buf][plane][row][k]
     auto Hs = reinterpret_cast<float (*)[HID2 + 4]>(sm23);
     __shared__ float W3s[NACT][HID2];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
@@ -554,20 +742,22 @@ __global__ __launch_bounds__(256, 2) void qfc23_kernel(Fwd a0, Fwd a1) {
         for (int j = 0; j < 2; j++)
 #pragma unroll
             for (int r = 0; r < 16; r++) acc[i][j][r] = 0.f;
-    bf16x8 bc[2][2], bn[2][2];
-    auto loadB = [&](int kc, bf16x8 (&b)[2][2]) {
+    bf16x8 bc[NPL][2][2], bn[NPL][2][2];  // [plane][column tile][step]
+    auto loadB = [&](int kc, bf16x8 (&b)[NPL][2][2]) {
 #pragma unroll
         for (int nt = 0; nt < 2; nt++) {
             const int n = w * 64 + nt * 32;
 #pragma unroll
-            for (int s = 0; s < 2; s++)  // tiled: one contiguous 1-KB block per wave load
-                b[nt][s] = *reinterpret_cast<const bf16x8*>(a.w2 + w2_tile(n >> 5, kc, s) + lane * 8);
+            for (int s = 0; s < 2; s++) {  // tiled: one contiguous 1-KB block per wave load
+                b[0][nt][s] = *reinterpret_cast<const bf16x8*>(a.w2 + w2_tile(n >> 5, kc, s) + lane * 8);
+                if constexpr (X3) b[NPL - 1][nt][s] = *reinterpret_cast<const bf16x8*>(a.w2l + w2_tile(n >> 5, kc, s) + lane * 8);
+            }
         }
     };
-    auto loadA = [&](int kc) -> bf16x8 {
+    auto loadA = [&](int kc, int pl) -> bf16x8 {
         bf16x8 v;
         if (rowok) {
-            v = *reinterpret_cast<const bf16x8*>(a.h1 + (size_t)(m0 + gr) * HID + kc * 32 + go);
+            v = *reinterpret_cast<const bf16x8*>((pl ? a.h1l : a.h1) + (size_t)(m0 + gr) * HID + kc * 32 + go);
         } else {
 #pragma unroll
             for (int t = 0; t < 8; t++) v[t] = (__bf16)0.f;
@@ -575,32 +765,46 @@ __global__ __launch_bounds__(256, 2) void qfc23_kernel(Fwd a0, Fwd a1) {
         return v;
     };
     constexpr int NKC = HID / 32;
-    *reinterpret_cast<bf16x8*>(&As[0][gr][go]) = loadA(0);
+#pragma unroll
+    for (int pl = 0; pl < NPL; pl++) *reinterpret_cast<bf16x8*>(&As[0][pl][gr][go]) = loadA(0, pl);
     loadB(0, bc);
     __syncthreads();
     for (int kc = 0; kc < NKC; kc++) {
         const int buf = kc & 1;
-        bf16x8 an;
+        bf16x8 an[NPL];
         if (kc + 1 < NKC) {
-            an = loadA(kc + 1);
+#pragma unroll
+            for (int pl = 0; pl < NPL; pl++) an[pl] = loadA(kc + 1, pl);
             loadB(kc + 1, bn);
         }
 #pragma unroll
         for (int mt = 0; mt < 2; mt++)
 #pragma unroll
             for (int s = 0; s < 2; s++) {
-                const bf16x8 av = *reinterpret_cast<const bf16x8*>(&As[buf][mt * 32 + (lane & 31)][s * 16 + 8 * h]);
+                const bf16x8 av = *reinterpret_cast<const bf16x8*>(&As[buf][0][mt * 32 + (lane & 31)][s * 16 + 8 * h]);
 #pragma unroll
                 for (int nt = 0; nt < 2; nt++)
-                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bc[nt][s], acc[mt][nt], 0, 0, 0);
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bc[0][nt][s], acc[mt][nt], 0, 0, 0);
+                if constexpr (X3) {
+                    const bf16x8 al =
+                        *reinterpret_cast<const bf16x8*>(&As[buf][NPL - 1][mt * 32 + (lane & 31)][s * 16 + 8 * h]);
+#pragma unroll
+                    for (int nt = 0; nt < 2; nt++) {
+                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bc[NPL - 1][nt][s], acc[mt][nt], 0, 0, 0);
+                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bc[0][nt][s], acc[mt][nt], 0, 0, 0);
+                    }
+                }
             }
         if (kc + 1 < NKC) {
-            *reinterpret_cast<bf16x8*>(&As[buf ^ 1][gr][go]) = an;
 #pragma unroll
-            for (int nt = 0; nt < 2; nt++) {
-                bc[nt][0] = bn[nt][0];
-                bc[nt][1] = bn[nt][1];
-            }
+            for (int pl = 0; pl < NPL; pl++) *reinterpret_cast<bf16x8*>(&As[buf ^ 1][pl][gr][go]) = an[pl];
+#pragma unroll
+            for (int pl = 0; pl < NPL; pl++)
+#pragma unroll
+                for (int nt = 0; nt < 2; nt++) {
+                    bc[pl][nt][0] = bn[pl][nt][0];
+                    bc[pl][nt][1] = bn[pl][nt][1];
+                }
         }
         __syncthreads();
     }
@@ -657,6 +861,46 @@ __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ w1,
     }
 }
 
+// X3 operand copies (evx_qmlp_pack3): W1 hi over K1X (compact K, then the danger column of
+// cell c at 512 + c) and lo over the compact K, both in w1_tile order; b1c = b1 + W1[:, centre]
+// in f32; W2 / W2^T hi and lo
+__global__ __launch_bounds__(256) void pack3_kernel(const float* __restrict__ w1, const float* __restrict__ b1,
+                                                    const float* __restrict__ w2, __bf16* __restrict__ w1b,
+                                                    __bf16* __restrict__ w1l, float* __restrict__ b1c,
+                                                    __bf16* __restrict__ w2b, __bf16* __restrict__ w2l,
+                                                    __bf16* __restrict__ w2t, __bf16* __restrict__ w2tl) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < HID * K1X) {  // destination index -> (tile, chunk, step, lane, j), NKC1X chunks
+        const int j = i & 7, l = (i >> 3) & 63, blk = i >> 9;
+        const int s = blk & 1, kc = (blk >> 1) % NKC1X, t = blk / (2 * NKC1X);
+        const int n = t * 32 + (l & 31), k = kc * KC1 + s * 16 + 8 * (l >> 5) + j;
+        const int rc = ref_col3(k);
+        const float v = rc >= 0 ? w1[n * K1 + rc] : 0.f;
+        w1b[i] = (__bf16)v;
+    }
+    if (i < HID * K1P) {  // lo over the compact K (NKC1 chunks)
+        const int j = i & 7, l = (i >> 3) & 63, blk = i >> 9;
+        const int s = blk & 1, kc = (blk >> 1) % NKC1, t = blk / (2 * NKC1);
+        const int n = t * 32 + (l & 31), k = kc * KC1 + s * 16 + 8 * (l >> 5) + j;
+        const float v = k < 4 * NCELL ? w1[n * K1 + ref_col(k)] : 0.f;
+        __bf16 hi, lo;
+        split2(v, hi, lo);
+        w1l[i] = lo;
+    }
+    if (i < HID) b1c[i] = b1[i] + w1[i * K1 + CENTRE_COL];
+    if (i < HID2 * HID) {
+        const int j = i & 7, l = (i >> 3) & 63, blk = i >> 9;
+        const int s = blk % 2, kc = (blk / 2) % (HID / 32), t = blk / (2 * (HID / 32));
+        const int n = t * 32 + (l & 31), k = kc * 32 + s * 16 + 8 * (l >> 5) + j;
+        split2(w2[n * HID + k], w2b[i], w2l[i]);
+        if (w2t) {  // w2t_tile order: columns = fc2 inputs (512), K = fc2 outputs (256)
+            const int tt = blk / (2 * (HID2 / 32)), kc2 = (blk / 2) % (HID2 / 32);
+            const int nn = tt * 32 + (l & 31), kk = kc2 * 32 + s * 16 + 8 * (l >> 5) + j;
+            split2(w2[kk * HID + nn], w2t[i], w2tl[i]);
+        }
+    }
+}
+
 // ================================================================ backward
 // DQNAgent.learn's loss.backward() for the MLP (agents/dqn_agent.py:150-158):
 //   fc3: dW3 = dQ^T H2, db3 = sum dQ, dZ2 = (dQ W3) * [H2 > 0], db2 = sum dZ2
@@ -678,10 +922,16 @@ struct Bwd {
     __bf16* dz2;        // [B][256]
     __bf16* dz1;        // [B][512]
     float *gw1, *gb1, *gw2, *gb2, *gw3, *gb3;
+    // X3: lo planes of h1 / dz2 / dz1, fc2.weight^T lo; x is [B][640]
+    const __bf16* h1l;
+    const __bf16* w2tl;
+    __bf16* dz2l;
+    __bf16* dz1l;
 };
 
 // fc3 backward: thread n of a 32-row block walks the rows (coalesced over n)
 constexpr int R3 = 32;
+template <bool X3 = false>
 __global__ __launch_bounds__(256) void qbwd3_kernel(Bwd a) {
     __shared__ float dqs[R3][NACT];
     const int n = threadIdx.x, b0 = blockIdx.x * R3;
@@ -706,7 +956,11 @@ __global__ __launch_bounds__(256) void qbwd3_kernel(Bwd a) {
             dz += d * w3[t];
         }
         dz = hv > 0.f ? dz : 0.f;
-        a.dz2[(size_t)(b0 + r) * HID2 + n] = (__bf16)dz;
+        if constexpr (X3) {
+            split2(dz, a.dz2[(size_t)(b0 + r) * HID2 + n], a.dz2l[(size_t)(b0 + r) * HID2 + n]);
+        } else {
+            a.dz2[(size_t)(b0 + r) * HID2 + n] = (__bf16)dz;
+        }
         gb2 += dz;
     }
 #pragma unroll
@@ -721,9 +975,10 @@ __global__ __launch_bounds__(256) void qbwd3_kernel(Bwd a) {
 
 // dZ1 = (dZ2 W2) * scale * [H1 > 0]: 64 rows x 128 columns per workgroup (4 waves x
 // 32 columns), K = 256 in chunks of 32; dZ2 staged through LDS, W2^T operand-tiled.
+template <bool X3 = false>
 __global__ __launch_bounds__(256, 2) void qdz1_kernel(Bwd a) {
-    __shared__ __attribute__((aligned(16))) __bf16 As[2][RM][40];  // pitch 20 words: conflict-free b128 reads
-    __shared__ float colsum[4][32];
+    constexpr int NPL = X3 ? 2 : 1;
+    __shared__ __attribute__((aligned(16))) __bf16 As[2][NPL][RM][40];  // pitch 20 words: conflict-free b128 reads
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
     const int m0 = blockIdx.x * RM, n0 = blockIdx.y * 128 + w * 32;
     const int gr = tid >> 2, go = (tid & 3) * 8;
@@ -733,43 +988,57 @@ __global__ __launch_bounds__(256, 2) void qdz1_kernel(Bwd a) {
     for (int i = 0; i < 2; i++)
 #pragma unroll
         for (int r = 0; r < 16; r++) acc[i][r] = 0.f;
-    auto loadA = [&](int kc) -> bf16x8 {
+    auto loadA = [&](int kc, int pl) -> bf16x8 {
         bf16x8 v;
         if (rowok) {
-            v = *reinterpret_cast<const bf16x8*>(a.dz2 + (size_t)(m0 + gr) * HID2 + kc * 32 + go);
+            v = *reinterpret_cast<const bf16x8*>((pl ? a.dz2l : a.dz2) + (size_t)(m0 + gr) * HID2 + kc * 32 + go);
         } else {
 #pragma unroll
             for (int t = 0; t < 8; t++) v[t] = (__bf16)0.f;
         }
         return v;
     };
-    bf16x8 bc[2], bn[2];
-    auto loadB = [&](int kc, bf16x8 (&b)[2]) {
+    bf16x8 bc[NPL][2], bn[NPL][2];
+    auto loadB = [&](int kc, bf16x8 (&b)[NPL][2]) {
 #pragma unroll
-        for (int s = 0; s < 2; s++) b[s] = *reinterpret_cast<const bf16x8*>(a.w2t + w2t_tile(n0 >> 5, kc, s) + lane * 8);
+        for (int s = 0; s < 2; s++) {
+            b[0][s] = *reinterpret_cast<const bf16x8*>(a.w2t + w2t_tile(n0 >> 5, kc, s) + lane * 8);
+            if constexpr (X3) b[NPL - 1][s] = *reinterpret_cast<const bf16x8*>(a.w2tl + w2t_tile(n0 >> 5, kc, s) + lane * 8);
+        }
     };
     constexpr int NKC = HID2 / 32;
-    *reinterpret_cast<bf16x8*>(&As[0][gr][go]) = loadA(0);
+#pragma unroll
+    for (int pl = 0; pl < NPL; pl++) *reinterpret_cast<bf16x8*>(&As[0][pl][gr][go]) = loadA(0, pl);
     loadB(0, bc);
     __syncthreads();
     for (int kc = 0; kc < NKC; kc++) {
         const int buf = kc & 1;
-        bf16x8 an;
+        bf16x8 an[NPL];
         if (kc + 1 < NKC) {
-            an = loadA(kc + 1);
+#pragma unroll
+            for (int pl = 0; pl < NPL; pl++) an[pl] = loadA(kc + 1, pl);
             loadB(kc + 1, bn);
         }
 #pragma unroll
         for (int mt = 0; mt < 2; mt++)
 #pragma unroll
             for (int s = 0; s < 2; s++) {
-                const bf16x8 av = *reinterpret_cast<const bf16x8*>(&As[buf][mt * 32 + (lane & 31)][s * 16 + 8 * h]);
-                acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bc[s], acc[mt], 0, 0, 0);
+                const bf16x8 av = *reinterpret_cast<const bf16x8*>(&As[buf][0][mt * 32 + (lane & 31)][s * 16 + 8 * h]);
+                acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bc[0][s], acc[mt], 0, 0, 0);
+                if constexpr (X3) {
+                    const bf16x8 al =
+                        *reinterpret_cast<const bf16x8*>(&As[buf][NPL - 1][mt * 32 + (lane & 31)][s * 16 + 8 * h]);
+                    acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bc[NPL - 1][s], acc[mt], 0, 0, 0);
+                    acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bc[0][s], acc[mt], 0, 0, 0);
+                }
             }
         if (kc + 1 < NKC) {
-            *reinterpret_cast<bf16x8*>(&As[buf ^ 1][gr][go]) = an;
-            bc[0] = bn[0];
-            bc[1] = bn[1];
+#pragma unroll
+            for (int pl = 0; pl < NPL; pl++) {
+                *reinterpret_cast<bf16x8*>(&As[buf ^ 1][pl][gr][go]) = an[pl];
+                bc[pl][0] = bn[pl][0];
+                bc[pl][1] = bn[pl][1];
+            }
         }
         __syncthreads();
     }
@@ -783,7 +1052,11 @@ __global__ __launch_bounds__(256, 2) void qdz1_kernel(Bwd a) {
             if (row >= a.B) continue;
             const float hv = (float)a.h1[(size_t)row * HID + col];
             const float v = hv > 0.f ? acc[mt][r] * a.scale : 0.f;
-            a.dz1[(size_t)row * HID + col] = (__bf16)v;
+            if constexpr (X3) {
+                split2(v, a.dz1[(size_t)row * HID + col], a.dz1l[(size_t)row * HID + col]);
+            } else {
+                a.dz1[(size_t)row * HID + col] = (__bf16)v;
+            }
             cs += v;
         }
     cs += __shfl_xor(cs, 32, 64);  // the two row halves of the column
@@ -825,16 +1098,20 @@ __device__ __forceinline__ void tr8x8(const uint4 (&in)[8], uint4 (&out)[8]) {
         out[c] = make_uint4(o[0], o[1], o[2], o[3]);
     }
 }
+// AP / BP: planes of A / B (2 = X3 hi + lo at Al / Bl: products hi*hi + hi*lo + lo*hi).
+template <int AP = 1, int BP = 1>
 __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const __bf16* __restrict__ A, int lda,
                                                          const __bf16* __restrict__ Bm, int ldb, int K, int M, int Nc,
                                                          int kper, float* __restrict__ C, int ldc, int remap,
-                                                         float* __restrict__ part) {
+                                                         float* __restrict__ part, const __bf16* __restrict__ Al = nullptr,
+                                                         const __bf16* __restrict__ Bl = nullptr) {
     // K chunks of 64 staged [m][k] in LDS: thread b < 128 of each operand loads an 8 (k) x 8 (m)
     // block (8 x 16-B row segments, whole cache lines per wave), transposes it in registers
     // and writes 8 x 16 B (8 consecutive k of one m): ds_write_b128, conflict-free; the MFMA
     // operand reads (ds_read_b128, pitch 36 words) are conflict-free too.
-    __shared__ __attribute__((aligned(16))) __bf16 As[TT][TPAD];
-    __shared__ __attribute__((aligned(16))) __bf16 Bs[TT][TPAD];
+    constexpr int NP = AP > BP ? AP : BP;
+    __shared__ __attribute__((aligned(16))) __bf16 As[AP][TT][TPAD];
+    __shared__ __attribute__((aligned(16))) __bf16 Bs[BP][TT][TPAD];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
     const int wm = w >> 1, wn = w & 1;
     const int m0 = blockIdx.y * TT, n0 = blockIdx.x * TT;
@@ -849,23 +1126,32 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const __bf16* __restric
     // threads 0..127 stage A, 128..255 stage B: block b = tid & 127 -> k block b & 7, m block b >> 3
     const bool isA = tid < 128;
     const int b = tid & 127, kb = b & 7, mb = b >> 3;
-    const __bf16* src = isA ? A : Bm;
+    const int np = isA ? AP : BP;  // planes this thread stages
+    const __bf16* src[NP];
+    src[0] = isA ? A : Bm;
+    if constexpr (NP > 1) src[NP - 1] = isA ? (AP > 1 ? Al : A) : (BP > 1 ? Bl : Bm);
     const int ld = isA ? lda : ldb, mlim = isA ? M : ldb, mbase = (isA ? m0 : n0) + mb * 8;
-    uint4 rv[8];
+    uint4 rv[NP][8];
     auto fetch = [&](int k0) {
 #pragma unroll
-        for (int r = 0; r < 8; r++) {
-            const int k = k0 + kb * 8 + r;
-            rv[r] = make_uint4(0u, 0u, 0u, 0u);
-            if (k < ke && mbase < mlim) rv[r] = *reinterpret_cast<const uint4*>(src + (size_t)k * ld + mbase);
-        }
+        for (int p = 0; p < NP; p++)
+#pragma unroll
+            for (int r = 0; r < 8; r++) {
+                const int k = k0 + kb * 8 + r;
+                rv[p][r] = make_uint4(0u, 0u, 0u, 0u);
+                if (p < np && k < ke && mbase < mlim) rv[p][r] = *reinterpret_cast<const uint4*>(src[p] + (size_t)k * ld + mbase);
+            }
     };
     auto stash = [&]() {
-        uint4 t[8];
-        tr8x8(rv, t);
-        __bf16 (*dst)[TPAD] = isA ? As : Bs;
 #pragma unroll
-        for (int c = 0; c < 8; c++) *reinterpret_cast<uint4*>(&dst[mb * 8 + c][kb * 8]) = t[c];
+        for (int p = 0; p < NP; p++) {
+            if (p >= np) break;
+            uint4 t[8];
+            tr8x8(rv[p], t);
+            __bf16 (*dst)[TPAD] = isA ? As[p < AP ? p : 0] : Bs[p < BP ? p : 0];
+#pragma unroll
+            for (int c = 0; c < 8; c++) *reinterpret_cast<uint4*>(&dst[mb * 8 + c][kb * 8]) = t[c];
+        }
     };
     if (kb0 < ke) fetch(kb0);
     for (int k0 = kb0; k0 < ke; k0 += TKC) {
@@ -874,16 +1160,26 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const __bf16* __restric
         if (k0 + TKC < ke) fetch(k0 + TKC);
 #pragma unroll
         for (int s = 0; s < TKC / 16; s++) {
-            bf16x8 av[2], bv[2];
+            bf16x8 av[AP][2], bv[BP][2];
 #pragma unroll
             for (int i = 0; i < 2; i++) {
-                av[i] = *reinterpret_cast<const bf16x8*>(&As[wm * 64 + i * 32 + (lane & 31)][s * 16 + 8 * h]);
-                bv[i] = *reinterpret_cast<const bf16x8*>(&Bs[wn * 64 + i * 32 + (lane & 31)][s * 16 + 8 * h]);
+#pragma unroll
+                for (int p = 0; p < AP; p++)
+                    av[p][i] = *reinterpret_cast<const bf16x8*>(&As[p][wm * 64 + i * 32 + (lane & 31)][s * 16 + 8 * h]);
+#pragma unroll
+                for (int p = 0; p < BP; p++)
+                    bv[p][i] = *reinterpret_cast<const bf16x8*>(&Bs[p][wn * 64 + i * 32 + (lane & 31)][s * 16 + 8 * h]);
             }
 #pragma unroll
             for (int i = 0; i < 2; i++)
 #pragma unroll
-                for (int j = 0; j < 2; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+                for (int j = 0; j < 2; j++) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[0][j], acc[i][j], 0, 0, 0);
+                    if constexpr (BP > 1)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[BP - 1][j], acc[i][j], 0, 0, 0);
+                    if constexpr (AP > 1)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[AP - 1][i], bv[0][j], acc[i][j], 0, 0, 0);
+                }
         }
         __syncthreads();
     }
@@ -907,7 +1203,8 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const __bf16* __restric
     for (int j = 0; j < 2; j++) {
         const int n = n0 + wn * 64 + j * 32 + (lane & 31);
         if (n >= Nc) continue;
-        const int nc = remap ? ref_col(n) : n;
+        const int nc = remap == 3 ? ref_col3(n) : remap ? ref_col(n) : n;
+        if (nc < 0) continue;
 #pragma unroll
         for (int i = 0; i < 2; i++)
 #pragma unroll
@@ -933,7 +1230,13 @@ __global__ __launch_bounds__(256) void gemm_reduce_kernel(const float* __restric
         acc.z += v.z;
         acc.w += v.w;
     }
-    const float a4[4] = {acc.x, acc.y, acc.z, acc.w};
+    float a4[4] = {acc.x, acc.y, acc.z, acc.w};
+    if (remap == 3) {  // X3 dW1: cell n / 4's danger residual column (512 + n / 4) into its danger column
+        const float* s2 = part + (size_t)m * Np + K1P + (n >> 2);
+        float d = s2[0];
+        for (int z = 1; z < S; z++) d += s2[(size_t)z * M * Np];
+        a4[1] += d;
+    }
 #pragma unroll
     for (int t = 0; t < 4; t++) {
         const int nc = remap ? ref_col(n + t) : n + t;
@@ -982,6 +1285,18 @@ int evx_qmlp_pack(const float* w1, const float* b1, const float* w2, uint16_t* w
     return mlaunch("qmlp_pack");
 }
 
+int evx_qmlp_pack3(const float* w1, const float* b1, const float* w2, uint16_t* w1b, uint16_t* w1l, float* b1c,
+                   uint16_t* w2b, uint16_t* w2l, uint16_t* w2t, uint16_t* w2tl, void* stream) {
+    if (!w1 || !b1 || !w2 || !w1b || !w1l || !b1c || !w2b || !w2l) return mfail(-22, "qmlp_pack3: NULL argument");
+    if ((w2t == nullptr) != (w2tl == nullptr)) return mfail(-22, "qmlp_pack3: w2t and w2tl go together");
+    const int n = evxm::HID * evxm::K1X;
+    hipLaunchKernelGGL(evxm::pack3_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, w1, b1, w2,
+                       reinterpret_cast<__bf16*>(w1b), reinterpret_cast<__bf16*>(w1l), b1c,
+                       reinterpret_cast<__bf16*>(w2b), reinterpret_cast<__bf16*>(w2l), reinterpret_cast<__bf16*>(w2t),
+                       reinterpret_cast<__bf16*>(w2tl));
+    return mlaunch("qmlp_pack3");
+}
+
 static int make_fwd(const evx_layout* lay, const evx_obs* obs, int32_t n, const evx_qmlp_params* p,
                     const evx_qmlp_dropout* drop, const evx_qmlp_fwd_out* out, evxm::Fwd& a) {
     if (!lay || !obs || !p || !out) return mfail(-22, "qmlp_forward: NULL argument");
@@ -1028,12 +1343,40 @@ static int make_fwd(const evx_layout* lay, const evx_obs* obs, int32_t n, const 
     a.stat = (p->w1o && !a.feats) ? p->stat : nullptr;  // the table is per layout: single layout only
     a.stat_fs = p->stat_fs;
     a.raw = nullptr;
+    a.drop_mask = drop ? drop->mask : nullptr;
+    if (a.drop_mask && !(dp > 0.f)) return mfail(-22, "qmlp_forward: an explicit dropout mask needs p > 0 (its scale)");
+    a.feat_lo = nullptr;
+    a.feats_lo = nullptr;
+    a.w1l = a.w2l = nullptr;
+    a.h1l = nullptr;
+    if (p->x3) {
+        if (!p->w1l || !p->w2l) return mfail(-22, "qmlp_forward: x3 needs w1l / w2l (evx_qmlp_pack3)");
+        if (!lay->obs_feat_lo || (lay->layout_set && !lay->obs_feats_lo))
+            return mfail(-22, "qmlp_forward: x3 needs the layout's obs_feat_lo");
+        a.feat_lo = lay->obs_feat_lo;
+        a.feats_lo = lay->layout_set ? lay->obs_feats_lo : nullptr;
+        a.w1l = reinterpret_cast<const __bf16*>(p->w1l);
+        a.w2l = reinterpret_cast<const __bf16*>(p->w2l);
+        a.h1l = a.h1 ? a.h1 + (size_t)n * evxm::HID : nullptr;  // lo plane after the hi plane
+        a.stat = nullptr;  // the act table is a bf16-mode feature
+    }
     return 0;
 }
 
-static int launch_fwd(const evxm::Fwd& a0, const evxm::Fwd& a1, int32_t n, int pairs, bool fc23, hipStream_t st) {
+static int launch_fwd(const evxm::Fwd& a0, const evxm::Fwd& a1, int32_t n, int pairs, bool fc23, hipStream_t st,
+                      bool x3 = false) {
     const unsigned blocks = (unsigned)((n + evxm::RM - 1) / evxm::RM);
     const unsigned big = (unsigned)((n + 127) / 128);
+    if (x3) {  // f32-accurate: 128 x 256 tiles for large batches (register budget), else 64 x 128
+        if (big * pairs >= 384)
+            hipLaunchKernelGGL((evxm::qfc1_kernel<4, 1, 8, true>), dim3(big, 2, pairs), dim3(512), 0, st, a0, a1);
+        else
+            hipLaunchKernelGGL((evxm::qfc1_kernel<2, 1, 4, true>), dim3(blocks, 4, pairs), dim3(256), 0, st, a0, a1);
+        int rc = mlaunch("qfc1");
+        if (rc || !fc23) return rc;
+        hipLaunchKernelGGL(evxm::qfc23_kernel<true>, dim3(blocks, 1, pairs), dim3(256), 0, st, a0, a1);
+        return mlaunch("qfc23");
+    }
     static int nwv = -1;  // EVX_FC1_NWV=4: 128 x 256 tiles of 4 waves (tuning)
     if (nwv < 0) {
         const char* v = getenv("EVX_FC1_NWV");
@@ -1047,7 +1390,7 @@ static int launch_fwd(const evxm::Fwd& a0, const evxm::Fwd& a1, int32_t n, int p
         hipLaunchKernelGGL((evxm::qfc1_kernel<2, 1, 4>), dim3(blocks, 4, pairs), dim3(256), 0, st, a0, a1);
     int rc = mlaunch("qfc1");
     if (rc || !fc23) return rc;
-    hipLaunchKernelGGL(evxm::qfc23_kernel, dim3(blocks, 1, pairs), dim3(256), 0, st, a0, a1);
+    hipLaunchKernelGGL(evxm::qfc23_kernel<false>, dim3(blocks, 1, pairs), dim3(256), 0, st, a0, a1);
     return mlaunch("qfc23");
 }
 
@@ -1057,7 +1400,7 @@ int evx_qmlp_forward(const evx_layout* lay, const evx_obs* obs, int32_t n, const
     evxm::Fwd a;
     int rc = make_fwd(lay, obs, n, p, drop, out, a);
     if (rc) return rc;
-    return launch_fwd(a, a, n, 1, out->q || out->actions || out->h2, (hipStream_t)stream);
+    return launch_fwd(a, a, n, 1, out->q || out->actions || out->h2, (hipStream_t)stream, p->x3 != 0);
 }
 
 int evx_qmlp_act(const evx_layout* lay, const evx_obs* obs, int32_t n, const evx_qmlp_params* p,
@@ -1073,14 +1416,21 @@ int evx_qmlp_act(const evx_layout* lay, const evx_obs* obs, int32_t n, const evx
     int rc = make_fwd(lay, obs, n, p, drop, &o, a);
     if (rc) return rc;
     a.h1 = nullptr;
+    a.h1l = nullptr;
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)evxm::qact_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   evxm::ACT_LDS);
+        (void)hipFuncSetAttribute((const void*)evxm::qact3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  evxm::ACT3_LDS);
         attr = true;
     }
-    hipLaunchKernelGGL(evxm::qact_kernel, dim3((unsigned)((n + 127) / 128)), dim3(512), evxm::ACT_LDS,
-                       (hipStream_t)stream, a);
+    if (p->x3)
+        hipLaunchKernelGGL(evxm::qact3_kernel, dim3((unsigned)((n + 127) / 128)), dim3(512), evxm::ACT3_LDS,
+                           (hipStream_t)stream, a);
+    else
+        hipLaunchKernelGGL(evxm::qact_kernel, dim3((unsigned)((n + 127) / 128)), dim3(512), evxm::ACT_LDS,
+                           (hipStream_t)stream, a);
     return mlaunch("qact");
 }
 
@@ -1094,6 +1444,7 @@ int evx_qmlp_stat(const evx_layout* lay, const evx_obs* obs, int32_t n, const ev
     int rc = make_fwd(lay, obs, n, p, nullptr, &o, a);
     if (rc) return rc;
     a.h1 = nullptr;
+    if (p->x3) return mfail(-22, "qmlp_stat: the act table is a bf16-mode feature");
     a.stat = nullptr;
     a.raw = out;
     return launch_fwd(a, a, n, 1, false, (hipStream_t)stream);
@@ -1110,7 +1461,8 @@ int evx_qmlp_forward2(const evx_layout* lay, int32_t n, const evx_obs* obs0, con
     if (rc) return rc;
     if (!(out0->q || out0->actions || out0->h2) || !(out1->q || out1->actions || out1->h2))
         return mfail(-22, "qmlp_forward2: both problems need an fc2/fc3 output");
-    return launch_fwd(a0, a1, n, 2, true, (hipStream_t)stream);
+    if ((p0->x3 != 0) != (p1->x3 != 0)) return mfail(-22, "qmlp_forward2: both problems in one precision");
+    return launch_fwd(a0, a1, n, 2, true, (hipStream_t)stream, p0->x3 != 0);
 }
 
 // split-K of the weight-gradient GEMMs: about 256 workgroups over `tiles` output tiles
@@ -1123,8 +1475,9 @@ static int ksplit_kper(int B, int tiles) {
 int64_t evx_qmlp_backward_part_floats(int32_t B) {
     if (B <= 0) return 0;
     const int64_t s2 = (B + ksplit_kper(B, 8) - 1) / ksplit_kper(B, 8);
-    const int64_t s1 = (B + ksplit_kper(B, 24) - 1) / ksplit_kper(B, 24);
-    return std::max(s2 * evxm::HID2 * evxm::HID, s1 * evxm::HID * evxm::K1P);
+    const int64_t s1 = std::max((B + ksplit_kper(B, 24) - 1) / ksplit_kper(B, 24),
+                                (B + ksplit_kper(B, 20) - 1) / ksplit_kper(B, 20));  // bf16 / x3 dW1 splits
+    return std::max(s2 * evxm::HID2 * evxm::HID, s1 * evxm::HID * evxm::K1X);  // K1X: the x3 dW1 width
 }
 
 int evx_qmlp_backward(const evx_qmlp_params* p, int32_t B, const float* dq, const uint16_t* x, const uint16_t* h1,
@@ -1158,13 +1511,43 @@ int evx_qmlp_backward(const evx_qmlp_params* p, int32_t B, const float* dq, cons
     a.gb2 = g->b2;
     a.gw3 = g->w3;
     a.gb3 = g->b3;
-    hipLaunchKernelGGL(evxm::qbwd3_kernel, dim3((unsigned)((B + evxm::R3 - 1) / evxm::R3)), dim3(256), 0, st, a);
-    hipLaunchKernelGGL(evxm::qdz1_kernel, dim3((unsigned)((B + evxm::RM - 1) / evxm::RM), evxm::HID / 128), dim3(256),
+    if (p->x3) {
+        if (!p->w2tl) return mfail(-22, "qmlp_backward: x3 needs w2tl (evx_qmlp_pack3)");
+        a.h1l = a.h1 + (size_t)B * evxm::HID;  // lo planes after the hi planes
+        a.w2tl = reinterpret_cast<const __bf16*>(p->w2tl);
+        a.dz2l = a.dz2 + (size_t)B * evxm::HID2;
+        a.dz1l = a.dz1 + (size_t)B * evxm::HID;
+        hipLaunchKernelGGL(evxm::qbwd3_kernel<true>, dim3((unsigned)((B + evxm::R3 - 1) / evxm::R3)), dim3(256), 0, st, a);
+        hipLaunchKernelGGL(evxm::qdz1_kernel<true>, dim3((unsigned)((B + evxm::RM - 1) / evxm::RM), evxm::HID / 128),
+                           dim3(256), 0, st, a);
+        {  // dW2 = dZ2^T H1: both operands split
+            const int kper = ksplit_kper(B, 8), S = (B + kper - 1) / kper;
+            hipLaunchKernelGGL((evxm::gemm_tn_kernel<2, 2>), dim3(evxm::HID / evxm::TT, evxm::HID2 / evxm::TT, S),
+                               dim3(256), 0, st, a.dz2, evxm::HID2, a.h1, evxm::HID, B, evxm::HID2, evxm::HID, kper,
+                               g->w2, evxm::HID, 0, g->part, a.dz2l, a.h1l);
+            if (g->part)
+                hipLaunchKernelGGL(evxm::gemm_reduce_kernel, dim3((evxm::HID2 * evxm::HID / 4 + 255) / 256), dim3(256),
+                                   0, st, g->part, S, evxm::HID2, evxm::HID, evxm::HID, g->w2, evxm::HID, 0);
+        }
+        {  // dW1 = dZ1^T X over the 640 x3 columns (X exact in bf16): the danger residual column of a
+           // cell adds into its danger column
+            const int kper = ksplit_kper(B, 20), S = (B + kper - 1) / kper;
+            hipLaunchKernelGGL((evxm::gemm_tn_kernel<2, 1>), dim3(evxm::K1X / evxm::TT, evxm::HID / evxm::TT, S),
+                               dim3(256), 0, st, a.dz1, evxm::HID, a.x, evxm::K1X, B, evxm::HID, evxm::K1X, kper, g->w1,
+                               evxm::K1, 3, g->part, a.dz1l, nullptr);
+            if (g->part)
+                hipLaunchKernelGGL(evxm::gemm_reduce_kernel, dim3((evxm::HID * evxm::NCELL + 255) / 256), dim3(256), 0,
+                                   st, g->part, S, evxm::HID, evxm::K1X, 4 * evxm::NCELL, g->w1, evxm::K1, 3);
+        }
+        return mlaunch("qmlp_backward");
+    }
+    hipLaunchKernelGGL(evxm::qbwd3_kernel<false>, dim3((unsigned)((B + evxm::R3 - 1) / evxm::R3)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(evxm::qdz1_kernel<false>, dim3((unsigned)((B + evxm::RM - 1) / evxm::RM), evxm::HID / 128), dim3(256),
                        0, st, a);
     // dW2 = dZ2^T H1 (256 x 512), dW1 = dZ1^T X (512 x 484 compact -> 726); K = B split over gridDim.z
     {
         const int kper = ksplit_kper(B, 8), S = (B + kper - 1) / kper;
-        hipLaunchKernelGGL(evxm::gemm_tn_kernel, dim3(evxm::HID / evxm::TT, evxm::HID2 / evxm::TT, S), dim3(256), 0, st,
+        hipLaunchKernelGGL((evxm::gemm_tn_kernel<1, 1>), dim3(evxm::HID / evxm::TT, evxm::HID2 / evxm::TT, S), dim3(256), 0, st,
                            a.dz2, evxm::HID2, a.h1, evxm::HID, B, evxm::HID2, evxm::HID, kper, g->w2, evxm::HID, 0,
                            g->part);
         if (g->part)
@@ -1173,7 +1556,7 @@ int evx_qmlp_backward(const evx_qmlp_params* p, int32_t B, const float* dq, cons
     }
     {
         const int kper = ksplit_kper(B, 24), S = (B + kper - 1) / kper;
-        hipLaunchKernelGGL(evxm::gemm_tn_kernel, dim3(evxm::K1P / evxm::TT, evxm::HID / evxm::TT, S), dim3(256), 0, st,
+        hipLaunchKernelGGL((evxm::gemm_tn_kernel<1, 1>), dim3(evxm::K1P / evxm::TT, evxm::HID / evxm::TT, S), dim3(256), 0, st,
                            a.dz1, evxm::HID, a.x, evxm::K1P, B, evxm::HID, 4 * evxm::NCELL, kper, g->w1, evxm::K1, 1,
                            g->part);
         if (g->part)

@@ -26,7 +26,7 @@ class evx_layout(C.Structure):
                                          "death_acc_penalty", "alive_bonus"]] + \
                [(n, C.c_void_p) for n in ["floor", "cellinfo", "valid_bits", "danger_p", "danger_o",
                                          "danger_o32", "robot_init", "nbr_valid", "floor_d5", "obs_feat",
-                                         "layout_set", "obs_feats"]]
+                                         "layout_set", "obs_feats", "obs_feat_lo", "obs_feats_lo"]]
 
 FEAT_PAD = 6  # EVX_FEAT_PAD
 

@@ -126,6 +126,25 @@ def obs_feature_map(tables: LayoutTables) -> np.ndarray:
     return (bf16_bits(dg) | static[None]).astype(np.uint32)
 
 
+def obs_feature_lo(tables: LayoutTables) -> np.ndarray:
+    """evx_layout.obs_feat_lo: the bf16 residual of obs_feat's danger feature,
+    bf16(d - bf16(d)) of d = float32(danger), same indexing: with it the f32-accurate MLP
+    kernels carry the danger input as hi + lo (16 significant bits)."""
+    hi_bits = obs_feature_map(tables) & 0xFFFF
+    hi = (hi_bits << 16).astype(np.uint32).view(np.float32)
+    spec, pad = tables.spec, _lib.FEAT_PAD
+    L, W = spec.L, spec.W
+    mx = np.arange(-pad, L + 2 + pad)[:, None]
+    my = np.arange(-pad, W + 2 + pad)[None, :]
+    do32 = np.asarray(tables.danger_o, np.float64).astype(np.float32)
+    T, OX, OY = do32.shape
+    ti, tj = mx - tables.obs_origin[0], my - tables.obs_origin[1]
+    inside = (ti >= 0) & (ti < OX) & (tj >= 0) & (tj < OY)
+    dg = np.zeros((T,) + inside.shape, np.float32)
+    dg[:, inside] = do32[:, np.broadcast_to(ti, inside.shape)[inside], np.broadcast_to(tj, inside.shape)[inside]]
+    return bf16_bits(dg - hi).astype(np.uint16)
+
+
 class DeviceLayout:
     """Static tables of one layout in HBM + the evx_layout descriptor."""
 
@@ -155,6 +174,7 @@ class DeviceLayout:
         self.t["floor_d5"] = torch.from_numpy(floor_delta5(tables.floor, spec.L, spec.W)).to(d)
         self.t["danger_o32"] = self.t["danger_o"].to(torch.float32)
         self.t["obs_feat"] = torch.from_numpy(obs_feature_map(tables).view(np.int32).reshape(-1)).to(d)
+        self.t["obs_feat_lo"] = torch.from_numpy(obs_feature_lo(tables).view(np.int16).reshape(-1)).to(d)
         T = tables.danger_p.shape[0] - 1
         OX, OY = tables.danger_o.shape[1:]
         self.c = _lib.evx_layout(
@@ -203,14 +223,26 @@ class LayoutSet:
         self._upload()
 
     def _upload(self):
-        raw = b"".join(bytes(l.c) for l in self.layouts)
-        self._set = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
-        self._feats = torch.tensor([l.c.obs_feat for l in self.layouts], dtype=torch.int64, device=self.device)
+        raw = torch.frombuffer(bytearray(b"".join(bytes(l.c) for l in self.layouts)), dtype=torch.uint8)
+        feats = torch.tensor([l.c.obs_feat for l in self.layouts], dtype=torch.int64)
+        feats_lo = torch.tensor([l.c.obs_feat_lo for l in self.layouts], dtype=torch.int64)
+        if getattr(self, "_set", None) is None:
+            self._set = raw.to(self.device)
+            self._feats = feats.to(self.device)
+            self._feats_lo = feats_lo.to(self.device)
+        else:
+            # set_params: new coefficients go into the SAME device buffers (stream-ordered copies):
+            # kernels already queued on other streams may still read them, so they are never freed
+            # and recycled under a running launch
+            self._set.copy_(raw, non_blocking=False)
+            self._feats.copy_(feats)
+            self._feats_lo.copy_(feats_lo)
         for name, _ in _lib.evx_layout._fields_:  # the set's own descriptor: layout 0's sizes and coefficients
-            if name not in ("layout_set", "obs_feats"):
+            if name not in ("layout_set", "obs_feats", "obs_feats_lo"):
                 setattr(self.c, name, getattr(self.layouts[0].c, name))
         self.c.layout_set = self._set.data_ptr()
         self.c.obs_feats = self._feats.data_ptr()
+        self.c.obs_feats_lo = self._feats_lo.data_ptr()
 
     def set_params(self, **kw):
         """Runtime-mutable coefficients, for every layout of the set."""

@@ -1,9 +1,12 @@
-"""Host driver of the bf16 MLP Q-network fast path (csrc/qmlp.hip, include/evacx.h).
+"""Host driver of the fused MLP Q-network kernels (csrc/qmlp.hip, include/evacx.h).
 
 The MLP variant of DQNNetwork (agents/dqn_agent.py:15-61; 726 -> 512 -> 256 -> 5)
 evaluated straight from compact observations: fc1 expands them on the fly, fc2+fc3
-and DQNAgent.act's epsilon-greedy (:101-124) run in one more kernel. bf16 copies of
-fc1/fc2 weights are re-packed from the fp32 master parameters after every update.
+and DQNAgent.act's epsilon-greedy (:101-124) run in one more kernel. bf16 operand
+copies of fc1/fc2 weights are re-packed from the fp32 master parameters after every
+update. Two arithmetic modes: x3=True (the reference's fp32: every f32 operand as a
+bf16 hi + lo pair, products hi*hi + hi*lo + lo*hi on the bf16 MFMA) and x3=False (bf16
+operands, f32 accumulation).
 """
 from __future__ import annotations
 
@@ -17,6 +20,7 @@ from . import _lib
 from .env import _stream
 
 HID, HID2, NACT, K1, K1P = 512, 256, 5, 726, 512
+K1X = 640  # x3: compact K + one danger-residual slot per cell
 NCELL, CENTRE_COL = 121, 60 * 6 + 5
 
 
@@ -29,11 +33,12 @@ def compact_ref_cols() -> np.ndarray:
 
 class evx_qmlp_params(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in ["w1", "b1c", "w2", "w2t", "b2", "w3", "b3", "w1o", "stat"]] + \
-        [("stat_fs", C.c_int32), ("pad0", C.c_int32)]
+        [("stat_fs", C.c_int32), ("x3", C.c_int32)] + [(n, C.c_void_p) for n in ["w1l", "w2l", "w2tl"]]
 
 
 class evx_qmlp_dropout(C.Structure):
-    _fields_ = [("seed", C.c_uint32), ("stream", C.c_uint32), ("p", C.c_float)]
+    _fields_ = [("seed", C.c_uint32), ("stream", C.c_uint32), ("p", C.c_float), ("pad0", C.c_uint32),
+                ("mask", C.c_void_p)]
 
 
 class evx_qmlp_grads(C.Structure):
@@ -56,6 +61,7 @@ def mlib():
     if not _inited:
         L.evx_qmlp_last_error.restype = C.c_char_p
         L.evx_qmlp_pack.argtypes = [C.c_void_p] * 9
+        L.evx_qmlp_pack3.argtypes = [C.c_void_p] * 11
         L.evx_qmlp_stat.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(evx_qmlp_params), C.c_void_p,
                                     C.c_void_p]
         L.evx_qmlp_forward.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(evx_qmlp_params),
@@ -85,25 +91,45 @@ def _p(t):
 
 
 class MLPFast:
-    """bf16 weight copies of one MLP parameter set (evacx.qnet.FlatParams) + forward."""
+    """bf16 operand copies of one MLP parameter set (evacx.qnet.FlatParams) + forward.
+    x3=True: the f32-accurate mode (hi + lo operand pairs; evx_qmlp_pack3)."""
 
-    def __init__(self, params, device):
+    def __init__(self, params, device, x3: bool = False):
         self.P = params
         self.device = torch.device(device)
+        self.x3 = bool(x3)
         i16 = dict(dtype=torch.int16, device=self.device)
-        self.w1b = torch.zeros(HID * K1P, **i16)
+        self.kx = K1X if self.x3 else K1P  # width of fc1's expanded input (the learner's saved X)
+        self.w1b = torch.zeros(HID * self.kx, **i16)
         self.w2b = torch.zeros(HID2 * HID, **i16)
         self.w2t = torch.zeros(HID * HID2, **i16)
         self.b1c = torch.zeros(HID, dtype=torch.float32, device=self.device)
-        self.w1o = torch.zeros(HID * 128, **i16)  # fc1's occupancy columns (act fast path)
+        self.w1o = None if self.x3 else torch.zeros(HID * 128, **i16)  # fc1's occupancy columns (act fast path)
         self.c = evx_qmlp_params(w1=self.w1b.data_ptr(), b1c=self.b1c.data_ptr(), w2=self.w2b.data_ptr(),
                                  w2t=self.w2t.data_ptr(), b2=params["fc2.bias"].data_ptr(),
                                  w3=params["fc3.weight"].data_ptr(), b3=params["fc3.bias"].data_ptr())
+        if self.x3:
+            self.w1l = torch.zeros(HID * K1P, **i16)
+            self.w2l = torch.zeros(HID2 * HID, **i16)
+            self.w2tl = torch.zeros(HID * HID2, **i16)
+            self.c.x3 = 1
+            self.c.w1l, self.c.w2l, self.c.w2tl = self.w1l.data_ptr(), self.w2l.data_ptr(), self.w2tl.data_ptr()
         self._static = None  # (lay_c, centre obs, table) of attach_static
         self._part = None  # split-K scratch of the weight-gradient GEMMs (backward)
         self.repack()
 
+    @property
+    def planes(self) -> int:
+        """Planes of a split activation buffer (h1, dz2, dz1): 2 in x3 mode (hi, lo)."""
+        return 2 if self.x3 else 1
+
     def repack(self):
+        if self.x3:
+            mcheck(mlib().evx_qmlp_pack3(self.P["fc1.weight"].data_ptr(), self.P["fc1.bias"].data_ptr(),
+                                         self.P["fc2.weight"].data_ptr(), self.w1b.data_ptr(), self.w1l.data_ptr(),
+                                         self.b1c.data_ptr(), self.w2b.data_ptr(), self.w2l.data_ptr(),
+                                         self.w2t.data_ptr(), self.w2tl.data_ptr(), _stream()), "qmlp_pack3")
+            return
         mcheck(mlib().evx_qmlp_pack(self.P["fc1.weight"].data_ptr(), self.P["fc1.bias"].data_ptr(),
                                     self.P["fc2.weight"].data_ptr(), self.w1b.data_ptr(), self.b1c.data_ptr(),
                                     self.w2b.data_ptr(), self.w2t.data_ptr(), self.w1o.data_ptr(), _stream()),
@@ -114,7 +140,9 @@ class MLPFast:
     def attach_static(self, lay_c, L: int, W: int, t_max: int):
         """Enable act()'s fast path for observations at fire step >= t_max (the fire has
         stopped spreading): fc1's pre-activation at zero occupancy for every window centre
-        of the layout, [(L+2)(W+2)][512] f32, rebuilt with every repack."""
+        of the layout, [(L+2)(W+2)][512] f32, rebuilt with every repack. bf16 mode only."""
+        if self.x3:
+            raise ValueError("attach_static: the act table is a bf16-mode feature")
         cx, cy = np.meshgrid(np.arange(L + 2), np.arange(W + 2), indexing="ij")
         ob = np.zeros(((L + 2) * (W + 2), 8), np.int32)
         ob[:, 4], ob[:, 5], ob[:, 6] = cx.ravel(), cy.ravel(), t_max
@@ -139,7 +167,7 @@ class MLPFast:
     def forward(self, lay_c, obs: torch.Tensor, n: int, h1: torch.Tensor, drop=None, x=None, h2=None, q=None,
                 actions=None, epsilon=0.0, act_seed=0, act_offset=0):
         """obs: compact observations (int32 words, 8 per row). drop: (seed, stream, p) or None."""
-        d = evx_qmlp_dropout(seed=drop[0] & 0xFFFFFFFF, stream=drop[1] & 0xFFFFFFFF, p=drop[2]) if drop else None
+        d = self._drop(drop) if drop else None
         o = evx_qmlp_fwd_out(h1=_p(h1), x=_p(x), h2=_p(h2), q=_p(q), actions=_p(actions), epsilon=float(epsilon),
                              act_seed=act_seed, act_offset=act_offset)
         mcheck(mlib().evx_qmlp_forward(C.byref(lay_c), obs.data_ptr(), n, C.byref(self.c),
@@ -158,7 +186,11 @@ class MLPFast:
 
     @staticmethod
     def _drop(drop):
-        return evx_qmlp_dropout(seed=drop[0] & 0xFFFFFFFF, stream=drop[1] & 0xFFFFFFFF, p=drop[2])
+        """drop: (seed, stream, p) or (seed, stream, p, keep_mask uint8 [n][512]) -- an explicit
+        mask (the reference's captured torch masks, tests) replaces the hash."""
+        m = drop[3] if len(drop) > 3 else None
+        return evx_qmlp_dropout(seed=drop[0] & 0xFFFFFFFF, stream=drop[1] & 0xFFFFFFFF, p=drop[2],
+                                mask=None if m is None else m.data_ptr())
 
     @staticmethod
     def _out(h1, x=None, h2=None, q=None):
@@ -175,7 +207,14 @@ class MLPFast:
 
     def backward(self, B: int, dq: torch.Tensor, x: torch.Tensor, h1: torch.Tensor, h2: torch.Tensor, drop_p: float,
                  dz2: torch.Tensor, dz1: torch.Tensor, grads, zero=True):
-        """d loss / d params of the saved forward into `grads` (evacx.qnet.FlatParams)."""
+        """d loss / d params of the saved forward into `grads` (evacx.qnet.FlatParams).
+        Buffer sizes are checked here, before anything is launched: x [B][kx], h1 / dz1
+        [planes][B][512], dz2 [planes][B][256]."""
+        pl = self.planes
+        for name, t, n in [("x", x, B * self.kx), ("h1", h1, pl * B * HID), ("dz1", dz1, pl * B * HID),
+                           ("dz2", dz2, pl * B * HID2), ("h2", h2, B * HID2), ("dq", dq, B * NACT)]:
+            if t.numel() < n:
+                raise ValueError(f"qmlp backward: {name} has {t.numel()} elements, needs {n}")
         g = evx_qmlp_grads(**{k: grads[f"fc{k[1]}.{'weight' if k[0] == 'w' else 'bias'}"].data_ptr()
                               for k in ["w1", "b1", "w2", "b2", "w3", "b3"]})
         if not _BWD_ATOMIC:  # split-K partials summed in a fixed order (deterministic, no f32 atomics)

@@ -295,12 +295,14 @@ class Learner:
         self.seed = seed
         self.rng_offset = 0
         self.grad_hook = None  # e.g. an all-reduce over the flat grad buffer
-        # bf16 MLP: the fused kernels of csrc/qmlp.hip (forward from compact observations)
+        # MLP: the fused kernels of csrc/qmlp.hip (forward from compact observations); f32 runs
+        # them in the x3 (f32-accurate) mode, bf16 with bf16 operands. The dense-tensor path
+        # (forward / learn on expanded observations) keeps evx_gemm at `precision`.
         self.fast = self.fast_t = None
-        if kind == "mlp" and precision == "bf16":
+        if kind == "mlp" and precision in ("bf16", "f32") and hidden == 512 and actions == 5:
             from .qmlp import MLPFast
-            self.fast = MLPFast(self.online, self.device)
-            self.fast_t = MLPFast(self.target, self.device)
+            self.fast = MLPFast(self.online, self.device, x3=precision == "f32")
+            self.fast_t = MLPFast(self.target, self.device, x3=precision == "f32")
         self.drop_stream = 0
 
     # ------------------------------------------------------------ dropout
@@ -338,25 +340,30 @@ class Learner:
         self.step_optimizer()
         return self.loss
 
-    def learn_obs(self, lay_c, s_obs, a, r, done, s2_obs, B, update: bool = True, weights=None, td_abs=None):
-        """DQNAgent.learn on compact observations with the fused bf16 kernels:
-        online forward (saves X, H1, H2), target forward, TD loss, backward, clip+Adam.
-        update=False stops after the gradients (the caller runs step_optimizer later)."""
-        from .qmlp import HID, HID2, K1P
+    def learn_obs(self, lay_c, s_obs, a, r, done, s2_obs, B, update: bool = True, weights=None, td_abs=None,
+                  mask_online=None, mask_target=None):
+        """DQNAgent.learn on compact observations with the fused kernels (x3 = f32-accurate,
+        or bf16): online forward (saves X, H1, H2), target forward, TD loss, backward,
+        clip+Adam. update=False stops after the gradients (the caller runs step_optimizer
+        later). mask_online / mask_target: explicit uint8 [B][512] dropout keep masks (tests:
+        the reference's captured torch masks) in place of the hash."""
+        from .qmlp import HID, HID2
         ws, dev = self.net.ws, self.device
-        X = ws.get("fx", (B * K1P,), torch.int16, dev)
-        H1 = ws.get("fh1", (B * HID,), torch.int16, dev)
+        pl, kx = self.fast.planes, self.fast.kx
+        X = ws.get("fx", (B * kx,), torch.int16, dev)
+        H1 = ws.get("fh1", (pl * B * HID,), torch.int16, dev)
         H2 = ws.get("fh2", (B, HID2), torch.float32, dev)
         Q = ws.get("fq", (B, self.actions), torch.float32, dev)
-        H1t = ws.get("fh1t", (B * HID,), torch.int16, dev)
+        H1t = ws.get("fh1t", (pl * B * HID,), torch.int16, dev)
         Qt = ws.get("fqt", (B, self.actions), torch.float32, dev)
         dQ = ws.get("fdq", (B, self.actions), torch.float32, dev)
-        dz2 = ws.get("fdz2", (B * HID2,), torch.int16, dev)
-        dz1 = ws.get("fdz1", (B * HID,), torch.int16, dev)
+        dz2 = ws.get("fdz2", (pl * B * HID2,), torch.int16, dev)
+        dz1 = ws.get("fdz1", (pl * B * HID,), torch.int16, dev)
         self.drop_stream += 2
-        type(self.fast).forward_pair(lay_c, B, self.fast, s_obs, (self.seed, self.drop_stream, DROPOUT_P),
-                                     dict(h1=H1, x=X, h2=H2, q=Q), self.fast_t, s2_obs,
-                                     (self.seed, self.drop_stream + 1, DROPOUT_P), dict(h1=H1t, q=Qt))
+        d_on = (self.seed, self.drop_stream, DROPOUT_P) + ((mask_online,) if mask_online is not None else ())
+        d_tg = (self.seed, self.drop_stream + 1, DROPOUT_P) + ((mask_target,) if mask_target is not None else ())
+        type(self.fast).forward_pair(lay_c, B, self.fast, s_obs, d_on, dict(h1=H1, x=X, h2=H2, q=Q), self.fast_t,
+                                     s2_obs, d_tg, dict(h1=H1t, q=Qt))
         L = qlib()
         qcheck(L.evx_td_loss_w(_p(Q), _p(Qt), self.actions, _p(a), _p(r), _p(done), self.gamma, B, _p(weights),
                                _p(dQ), _p(self.loss), _p(td_abs), _stream()), "td_loss")
@@ -380,6 +387,14 @@ class Learner:
                                _stream()), "clip_adam")
         if self.fast is not None:
             self.fast.repack()  # bf16 copies follow the fp32 master parameters
+
+    def m_view(self, name: str) -> torch.Tensor:
+        """Adam first moment of one parameter (torch's optimizer.state[p]["exp_avg"])."""
+        return FlatParams(self.shapes, self.device, data=self.m)[name]
+
+    def v_view(self, name: str) -> torch.Tensor:
+        """Adam second moment of one parameter (torch's optimizer.state[p]["exp_avg_sq"])."""
+        return FlatParams(self.shapes, self.device, data=self.v)[name]
 
     def sync_target(self):
         """DQNAgent.update_target_network (agents/dqn_agent.py:170-172)."""

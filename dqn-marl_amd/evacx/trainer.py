@@ -123,7 +123,7 @@ class _Group:
 
 class VecTrainer:
     def __init__(self, layout: DeviceLayout, E: int, seed_base: int = 1234, env_offset: int = 0,
-                 kind: str = "mlp", precision: str = "bf16", batch: int = 4096, replay_capacity: int = 1 << 20,
+                 kind: str = "mlp", precision: str = "f32", batch: int = 4096, replay_capacity: int = 1 << 20,
                  lr: float = 1e-4, gamma: float = 0.99, epsilon: float = 1.0, epsilon_min: float = 0.02,
                  epsilon_decay: float = 0.9995, target_every: int = 1000, learner_seed: int = 0,
                  grad_hook=None, learn_every: int = 1, lagged_learn: bool = False, replay: str = "uniform",
@@ -194,7 +194,7 @@ class VecTrainer:
         self.fast = self.learner.fast
         if self.fast is None:
             self.lagged = False  # the split learn step needs the fused bf16 MLP path
-        elif os.environ.get("EVX_ACT_STATIC", "0") == "1":
+        elif os.environ.get("EVX_ACT_STATIC", "0") == "1" and not self.fast.x3:
             # act fast path (off by default: the per-update table rebuild on the learn stream costs what
             # the act saves, tools/gpu_ab_static.sh): envs past the fire's last step start fc1 from a table
             lc = self.lay.c

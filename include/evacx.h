@@ -63,6 +63,10 @@ typedef struct {
      * observation readers; obs_feats is the device array of their obs_feat tables. */
     const void *layout_set;
     const uint32_t *const *obs_feats;
+    /* f32-accurate MLP inputs (evx_qmlp_params.x3): the bf16 residual of the danger feature,
+     * bf16(danger_o32 - bf16(danger_o32)), indexed as obs_feat; obs_feats_lo: per layout of a set */
+    const uint16_t *obs_feat_lo;
+    const uint16_t *const *obs_feats_lo;
 } evx_layout;
 
 #define EVX_FEAT_PAD 6
@@ -306,12 +310,21 @@ typedef struct {
      * w1o) and the pre-activation table of evx_qmlp_stat for observations at fire step stat_fs */
     const uint16_t *w1o;
     const float *stat;
-    int32_t stat_fs, pad0;
+    int32_t stat_fs;
+    /* x3 = 1: f32-accurate arithmetic (the reference's fp32 DQNNetwork): every f32 operand v is
+     * carried as bf16 hi = bf16(v) plus lo = bf16(v - hi) and a product as hi*hi + hi*lo + lo*hi
+     * on the bf16 MFMA (exact 0/1 operands skip their lo); w1 then spans K = 640 (compact K +
+     * one danger-residual slot per cell), w1l / w2l / w2tl hold the lo parts (evx_qmlp_pack3) */
+    int32_t x3;
+    const uint16_t *w1l, *w2l, *w2tl;
 } evx_qmlp_params;
 
 typedef struct {
     uint32_t seed, stream; /* mask identity */
     float p;               /* drop probability; 0 = eval (no dropout) */
+    uint32_t pad0;
+    const uint8_t *mask;   /* optional explicit keep mask [n][512] (1 = keep; scale 1/(1-p)) in place of
+                            * the hash: replays the reference's captured torch dropout masks */
 } evx_qmlp_dropout;
 
 typedef struct {
@@ -322,6 +335,7 @@ typedef struct {
     int32_t *actions;      /* [n] epsilon-greedy actions (evx_act's rule and RNG), or NULL */
     float epsilon;
     uint64_t act_seed, act_offset;
+    /* x3: h1 holds two planes [2][n][512] (hi, lo) and x spans [n][640] */
 } evx_qmlp_fwd_out;
 
 /* bf16 copies of fc1.weight [512][726] over fc1's compact K and fc2.weight [256][512]
@@ -331,6 +345,11 @@ typedef struct {
  * one-hot, folded into b1c. */
 int evx_qmlp_pack(const float *w1, const float *b1, const float *w2, uint16_t *w1b, float *b1c, uint16_t *w2b,
                   uint16_t *w2t, uint16_t *w1o, void *stream);
+/* x3 (f32-accurate) operand copies: w1b [512][640] hi (compact K, then the danger column of cell
+ * c at k = 512 + c, multiplying the danger residual), w1l [512][512] lo of the compact K, w2b / w2l
+ * hi / lo of fc2.weight, w2t / w2tl of its transpose (may be NULL); b1c = b1 + W1[:, centre] in f32 */
+int evx_qmlp_pack3(const float *w1, const float *b1, const float *w2, uint16_t *w1b, uint16_t *w1l, float *b1c,
+                   uint16_t *w2b, uint16_t *w2l, uint16_t *w2t, uint16_t *w2tl, void *stream);
 /* fc1's pre-activation (X W1^T + b1, f32, no ReLU / dropout) of n observations -> out [n][512]:
  * with obs = every window centre of the layout at one fire step and zero occupancy this is the
  * act fast path's table (evx_qmlp_params.stat; rebuild after every weight update) */
@@ -364,7 +383,9 @@ int64_t evx_qmlp_backward_part_floats(int32_t B);
 /* loss.backward() of DQNAgent.learn (agents/dqn_agent.py:150-158) for the saved online
  * forward (x, h1, h2 of evx_qmlp_forward) given dQ = d loss / d Q [B][5]. Gradients are
  * accumulated with atomics (zero_grads = 1 clears them first). dz2 [B][256] and dz1
- * [B][512] are bf16 scratch. Needs p->w2t. */
+ * [B][512] are bf16 scratch. Needs p->w2t. With p->x3 the activations are the x3 forward's
+ * (h1 two planes, x 640 wide), dz2 / dz1 hold two planes each (hi, lo) and every product
+ * is split as in the forward. */
 int evx_qmlp_backward(const evx_qmlp_params *p, int32_t B, const float *dq, const uint16_t *x, const uint16_t *h1,
                       const float *h2, float drop_p, uint16_t *dz2, uint16_t *dz1, const evx_qmlp_grads *g,
                       int32_t zero_grads, void *stream);

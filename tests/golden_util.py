@@ -58,3 +58,56 @@ def oracle_layout(traj_name):
 def state_fields(st, obs):
     return dict(pos=st["pos"], health=st["health"], acc=st["acc"], flags=st["flags"], rmap=st["rmap"],
                 thmap=st["thmap"], robots=st["robots"], view=st["view"], obs=obs)
+
+
+# ----------------------------------------------------------------------------
+# learner fixtures (tools/capture_golden.py dqn_fixtures)
+# ----------------------------------------------------------------------------
+def fmix32(h):
+    h = np.asarray(h, np.uint64) & 0xFFFFFFFF
+    h ^= h >> 16
+    h = (h * 0x85EBCA6B) & 0xFFFFFFFF
+    h ^= h >> 13
+    h = (h * 0xC2B2AE35) & 0xFFFFFFFF
+    h ^= h >> 16
+    return h
+
+
+def closed_form_params(shapes, salt=0):
+    """Closed-form deterministic parameters, no torch RNG: tensor t of the state_dict
+    (ordered name -> shape) gets w[k] = bound * (2 u - 1), u = fmix32(k ^ hash(t, salt)) / 2^32,
+    bound = 1 / sqrt(fan_in) (nn.Linear / nn.Conv2d default init range). The weights and
+    biases of one layer share the weight's fan-in."""
+    out = {}
+    fan = None
+    for t, (name, shape) in enumerate(shapes.items()):
+        n = int(np.prod(shape))
+        if name.endswith(".weight"):
+            fan = int(np.prod(shape[1:]))
+        key = int(fmix32(np.uint64((t + 1) * 0x9E3779B1 + salt * 0x7F4A7C15)))
+        u = fmix32(np.arange(n, dtype=np.uint64) ^ np.uint64(key)).astype(np.float64) / 2.0 ** 32
+        out[name] = ((2.0 * u - 1.0) / np.sqrt(fan)).astype(np.float32).reshape(shape)
+    return out
+
+
+def mlp_shapes(hidden=512, in_dim=726, actions=5):
+    return {"fc1.weight": (hidden, in_dim), "fc1.bias": (hidden,), "fc2.weight": (hidden // 2, hidden),
+            "fc2.bias": (hidden // 2,), "fc3.weight": (actions, hidden // 2), "fc3.bias": (actions,)}
+
+
+def conv_shapes(hidden=512, actions=5):
+    return {"conv1.weight": (32, 6, 3, 3), "conv1.bias": (32,), "conv2.weight": (64, 32, 3, 3), "conv2.bias": (64,),
+            "conv3.weight": (128, 64, 3, 3), "conv3.bias": (128,), "fc1.weight": (hidden, 15488), "fc1.bias": (hidden,),
+            "fc2.weight": (hidden // 2, hidden), "fc2.bias": (hidden // 2,), "fc3.weight": (actions, hidden // 2),
+            "fc3.bias": (actions,)}
+
+
+SEL_FULL = 16384  # tensors up to this size are stored whole, larger ones at SEL_N fixed positions
+SEL_N = 2048
+
+
+def select_positions(n, t):
+    """Fixed positions at which a large tensor is stored (sorted, deterministic per tensor index)."""
+    if n <= SEL_FULL:
+        return np.arange(n)
+    return np.sort(np.random.RandomState(1000 + t).choice(n, SEL_N, replace=False))

@@ -116,7 +116,7 @@ def test_fused_backward_matches_torch_autograd():
     _need_gpu()
     from evacx.qmlp import HID, K1, K1P, MLPFast, dropout_keep
     from evacx.qnet import Learner, qcheck, qlib
-    lay, env = _env_obs(E=80, R=4)
+    lay, env = _env_obs(E=160, R=4)
     B = 256
     dev = "cuda"
     lr = Learner(kind="mlp", precision="bf16", seed=21)
@@ -192,7 +192,7 @@ def test_learn_obs_step_runs_and_descends():
     """A few fused learn steps on a fixed batch lower the TD loss (Adam lr 1e-3)."""
     _need_gpu()
     from evacx.qnet import Learner
-    lay, env = _env_obs(E=80, R=4)
+    lay, env = _env_obs(E=160, R=4)
     B = 256
     lr = Learner(kind="mlp", precision="bf16", seed=22, lr=1e-3)
     g = torch.Generator().manual_seed(4)

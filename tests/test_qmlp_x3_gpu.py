@@ -1,0 +1,210 @@
+"""GPU numerics of the f32-accurate (x3) fused MLP kernels (csrc/qmlp.hip) against a plain
+PyTorch fp32 reference on the FULL 726-column observation tensor.
+
+x3 carries every f32 operand as bf16 hi + lo (16 significant bits) and a product as
+hi*hi + hi*lo + lo*hi with f32 accumulation (~2^-16 relative per product), so the bars
+are the exact-f32 path's (tests/test_qnet_gpu.py): Q rtol 2e-4 / atol 2e-5, loss and
+gradient norm rtol 2e-4, gradients rtol 2e-3 (atol 1e-5 of the tensor's scale), Adam
+updates as test_learn_steps_match_torch_adam. Dropout: explicit keep masks (the same
+tensor on both sides) or p = 0."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _env_obs(E=48, steps=7, R=4, grid=48, people=300):
+    from evacx.env import DeviceLayout, VecEnv
+    from evacx.layout import build_tables, synthetic
+    lay = DeviceLayout(build_tables(synthetic(grid, grid, R)), people)
+    env = VecEnv(lay, E)
+    env.seed([77 + i for i in range(E)])
+    env.reset()
+    g = torch.Generator(device="cuda").manual_seed(0)
+    for _ in range(steps):
+        env.step(torch.randint(0, 5, (E * R,), device="cuda", dtype=torch.int32, generator=g))
+    torch.cuda.synchronize()
+    return lay, env
+
+
+def torch_q(sd, X, mask):
+    """agents/dqn_agent.py:40-61's fc stack on the flattened observation (the MLP variant)."""
+    h = F.relu(F.linear(X, sd["fc1.weight"], sd["fc1.bias"]))
+    if mask is not None:
+        h = h * mask.float() / 0.8
+    h = F.relu(F.linear(h, sd["fc2.weight"], sd["fc2.bias"]))
+    return F.linear(h, sd["fc3.weight"], sd["fc3.bias"]), h
+
+
+def _planes(h1, n):
+    """f32 value of an x3 activation buffer [2][n][512] (hi + lo)."""
+    v = h1.view(torch.bfloat16).view(2, n, -1).float()
+    return v[0] + v[1]
+
+
+@pytest.mark.parametrize("masked", [False, True])
+def test_x3_forward_matches_torch_fp32(masked):
+    _need_gpu()
+    from evacx.qmlp import HID, K1, K1X, MLPFast
+    from evacx.qnet import Learner
+    lay, env = _env_obs()
+    n = env.E * lay.R
+    lr = Learner(kind="mlp", precision="f32", seed=11)
+    fast = MLPFast(lr.online, "cuda", x3=True)
+    dev = "cuda"
+    mask = (torch.rand(n, HID, device=dev) >= 0.2).to(torch.uint8) if masked else None
+    h1 = torch.empty(2 * n * HID, dtype=torch.int16, device=dev)
+    x = torch.empty(n * K1X, dtype=torch.int16, device=dev)
+    h2 = torch.empty(n, 256, device=dev)
+    q = torch.empty(n, 5, device=dev)
+    drop = (1, 2, 0.2, mask) if masked else None
+    fast.forward(lay.c, env.obs, n, h1, drop=drop, x=x, h2=h2, q=q)
+    torch.cuda.synchronize()
+    X = env.expand_obs(torch.float32).reshape(n, K1)
+    sd = lr.online.state_dict()
+    refq, refh2 = torch_q(sd, X, mask)
+    ref1 = F.relu(F.linear(X, sd["fc1.weight"], sd["fc1.bias"]))
+    if masked:
+        ref1 = ref1 * mask.float() / 0.8
+    torch.testing.assert_close(_planes(h1, n), ref1, rtol=2e-4, atol=2e-5)
+    torch.testing.assert_close(h2, refh2, rtol=2e-4, atol=2e-5)
+    torch.testing.assert_close(q, refq, rtol=2e-4, atol=2e-5)
+    # the saved input: the compact features exact, the danger residual slot = the f32 danger's lo
+    xv = x.view(torch.bfloat16).view(n, K1X).float()
+    from evacx.qmlp import compact_ref_cols
+    cols = torch.from_numpy(compact_ref_cols()).to(dev)
+    danger = X.view(n, 121, 6)[:, :, 2]
+    hi = xv[:, :484].view(n, 121, 4)[:, :, 1]
+    assert torch.equal(hi + xv[:, 512:633], hi + (danger - hi).to(torch.bfloat16).float())
+    assert ((hi + xv[:, 512:633]) - danger).abs().max().item() <= 2.0 ** -16 * danger.abs().max().item()
+    assert torch.equal(xv[:, :484].view(n, 121, 4)[:, :, [0, 2, 3]], X.view(n, 121, 6)[:, :, [1, 3, 4]])
+    assert torch.count_nonzero(xv[:, 484:512]) == 0 and torch.count_nonzero(xv[:, 633:]) == 0
+
+
+@pytest.mark.parametrize("eps", [0.0, 0.25])
+def test_x3_act_matches_forward(eps):
+    """evx_qmlp_act in x3 mode (qact3: H1 through LDS in two column halves) == the two-kernel
+    x3 forward's Q and actions bit for bit (same K order), ragged act-sized batch."""
+    _need_gpu()
+    from evacx.qmlp import HID, MLPFast
+    from evacx.qnet import Learner, qcheck, qlib
+    lay, env = _env_obs(E=700, steps=3, R=16, grid=64, people=500)
+    n = env.E * lay.R - 7
+    lr = Learner(kind="mlp", precision="f32", seed=31)
+    fast = lr.fast
+    assert fast.x3
+    h1 = torch.empty(2 * n * HID, dtype=torch.int16, device="cuda")
+    q1 = torch.empty(n, 5, device="cuda")
+    a1 = torch.empty(n, dtype=torch.int32, device="cuda")
+    q2 = torch.full((n + 3, 5), 9.0, device="cuda")
+    a2 = torch.full((n + 3,), -1, dtype=torch.int32, device="cuda")
+    kw = dict(drop=(77, 5, 0.2), epsilon=eps, act_seed=4, act_offset=123)
+    fast.forward(lay.c, env.obs, n, h1, q=q1, actions=a1, **kw)
+    fast.act(lay.c, env.obs, n, q=q2, actions=a2, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(q1, q2[:n])
+    assert torch.equal(a1, a2[:n])
+    assert torch.all(q2[n:] == 9.0) and torch.all(a2[n:] == -1)
+    a3 = torch.empty_like(a1)
+    qcheck(qlib().evx_act(q1.data_ptr(), n, 5, eps, 4, 123, a3.data_ptr(), 0), "act")
+    torch.cuda.synchronize()
+    assert torch.equal(a1, a3)
+
+
+def test_x3_learn_steps_match_torch_adam():
+    """3 fused learn steps (learn_obs, x3): loss, gradient norm, clipped gradients, Adam
+    parameters vs torch autograd in fp32 on the expanded observations, same masks."""
+    _need_gpu()
+    from evacx.qmlp import HID, K1
+    from evacx.qnet import Learner
+    lay, env = _env_obs(E=160, R=4)
+    B = 256
+    dev = "cuda"
+    lr = Learner(kind="mlp", precision="f32", seed=21, lr=1e-3)
+    sd0 = {k: v.clone() for k, v in lr.online.state_dict().items()}
+    params = {k: torch.nn.Parameter(v.clone()) for k, v in sd0.items()}
+    tgt = {k: v.clone() for k, v in sd0.items()}
+    opt = torch.optim.Adam(params.values(), lr=1e-3)
+    g = torch.Generator().manual_seed(3)
+    for it in range(3):
+        if it > 0:  # each step compared from the same state (params + moments)
+            lr.online.load_state_dict({k: p.detach() for k, p in params.items()})
+            lr.fast.repack()
+            for key, buf in (("exp_avg", lr.m), ("exp_avg_sq", lr.v)):
+                buf.copy_(torch.cat([opt.state[p][key].reshape(-1) for p in params.values()]))
+        perm = torch.randperm(env.E * lay.R, generator=g)
+        s_idx, s2_idx = perm[:B].to(dev), perm[B:2 * B].to(dev)
+        obs = env.obs.view(-1, 8)
+        s_obs, s2_obs = obs[s_idx].contiguous().view(-1), obs[s2_idx].contiguous().view(-1)
+        a = torch.randint(0, 5, (B,), generator=g, dtype=torch.int32).to(dev)
+        r = (torch.randn(B, generator=g) * 30).to(dev)
+        d = (torch.rand(B, generator=g) < 0.2).to(torch.uint8).to(dev)
+        m1 = (torch.rand(B, HID, generator=g) >= 0.2).to(torch.uint8).to(dev)
+        m2 = (torch.rand(B, HID, generator=g) >= 0.2).to(torch.uint8).to(dev)
+        loss = lr.learn_obs(lay.c, s_obs, a, r, d, s2_obs, B, mask_online=m1, mask_target=m2)
+        X = env.expand_obs(torch.float32, s_obs).reshape(B, K1)
+        X2 = env.expand_obs(torch.float32, s2_obs).reshape(B, K1)
+        q = torch_q(params, X, m1)[0].gather(1, a.long().unsqueeze(1))
+        with torch.no_grad():
+            y = r + 0.99 * torch_q(tgt, X2, m2)[0].max(1)[0] * (~d.bool())
+        ref_loss = F.mse_loss(q.squeeze(), y)
+        opt.zero_grad()
+        ref_loss.backward()
+        gnorm = torch.nn.utils.clip_grad_norm_(params.values(), 1.0)
+        grads_ref = {k: p.grad.clone() for k, p in params.items()}
+        opt.step()
+        torch.cuda.synchronize()
+        assert abs(loss.item() - ref_loss.item()) <= 2e-4 * abs(ref_loss.item()) + 1e-5
+        assert abs(lr.norm.item() - gnorm.item()) <= 2e-4 * gnorm.item() + 1e-6
+        for k in params:
+            ref = grads_ref[k]
+            torch.testing.assert_close(lr.grads[k], ref, rtol=2e-3, atol=1e-5 * ref.abs().max().item() + 1e-9)
+            diff = (lr.online[k] - params[k].detach()).abs()
+            assert (diff > 1e-5).float().mean().item() <= 1e-3, (k, diff.max().item())
+            assert diff.max().item() <= 2e-3, (k, diff.max().item())
+
+
+def test_x3_layout_set_reads_each_rows_layout():
+    """x3 forward over a LayoutSet: every row's danger residual comes from its own layout."""
+    _need_gpu()
+    from evacx.env import DeviceLayout, LayoutSet, VecEnv
+    from evacx.layout import build_tables, random_layout
+    from evacx.qmlp import HID, K1
+    from evacx.qnet import Learner
+    E, R, P = 30, 4, 200
+    lays = LayoutSet([DeviceLayout(build_tables(random_layout(40, 40, R, 900 + k)), P) for k in range(3)])
+    env = VecEnv(lays, E, layout_of=[e % 3 for e in range(E)])
+    env.seed([5 + i for i in range(E)])
+    env.reset()
+    for _ in range(4):
+        env.step(torch.randint(0, 5, (E * R,), device="cuda", dtype=torch.int32))
+    n = E * R
+    lr = Learner(kind="mlp", precision="f32", seed=2)
+    h1 = torch.empty(2 * n * HID, dtype=torch.int16, device="cuda")
+    q = torch.empty(n, 5, device="cuda")
+    lr.fast.forward(lays.c, env.obs, n, h1, q=q)
+    torch.cuda.synchronize()
+    X = env.expand_obs(torch.float32).reshape(n, K1)
+    refq, _ = torch_q(lr.online.state_dict(), X, None)
+    torch.testing.assert_close(q, refq, rtol=2e-4, atol=2e-5)
+
+
+def test_x3_rejects_missing_operands():
+    """The product path fails loudly when the x3 operands are absent."""
+    _need_gpu()
+    from evacx import _lib
+    from evacx.qmlp import HID, MLPFast
+    from evacx.qnet import Learner
+    lay, env = _env_obs(E=4, steps=1)
+    lr = Learner(kind="mlp", precision="f32", seed=1)
+    fast = MLPFast(lr.online, "cuda", x3=True)
+    fast.c.w1l = None
+    with pytest.raises(_lib.EvacxError):
+        fast.forward(lay.c, env.obs, 16, torch.empty(2 * 16 * HID, dtype=torch.int16, device="cuda"),
+                     q=torch.empty(16, 5, device="cuda"))

@@ -17,9 +17,19 @@ outputs are small ``.npz`` files under ``tests/golden/`` that pin
   started from recorded MT19937 states of Python ``random`` and legacy
   ``numpy.random`` (the two streams the reference consumes),
 * ``DQNNetwork`` forward outputs and ``DQNAgent.learn`` results
-  (``agents/dqn_agent.py:15-168``) for deterministic, closed-form weights.
+  (``agents/dqn_agent.py:15-168``) for deterministic, closed-form weights
+  (``dqn_forward.npz``, ``dqn_learn.npz``; ``dqn_fixtures``): observations made by the
+  reference's own ``EvacuationEnv._get_state`` (``envs/evacuation_env.py:84-120``),
+  Q-values of the full-size conv network and of the MLP variant, and three ``learn``
+  steps of each with the sampled batch indices, the dropout masks (forward hooks on
+  the ``Dropout`` modules), the loss, the total gradient norm, the gradients and the
+  parameters / Adam moments after every step,
+* a long 128x128 R16 trajectory (``g128_long_traj.npz``: past the fire's last step,
+  with a reset) and the per-step digests of the 128x128 danger tables for all 181
+  fire steps (``g128_danger_digests.npz``).
 
-Usage:  PYTHONPATH=/root/reference PYTHONDONTWRITEBYTECODE=1 python tools/capture_golden.py
+Usage:  PYTHONPATH=/root/reference PYTHONDONTWRITEBYTECODE=1 python tools/capture_golden.py [part ...]
+  parts: base (the round-1 fixtures), dqn, g128long, g128danger; default: all
 """
 import hashlib
 import os
@@ -30,6 +40,7 @@ import numpy as np
 
 REF = os.environ.get("EVX_REFERENCE", "/root/reference")
 sys.path.insert(0, REF)
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests"))
 sys.dont_write_bytecode = True
 
 from Louvre_Evacuation.envs.evacuation_env import EvacuationEnv  # noqa: E402
@@ -166,7 +177,7 @@ def layout_tables(env_kwargs, t_max):
 # trajectories
 # ----------------------------------------------------------------------------
 
-def run_traj(make_env, n_robots, seed, episodes, max_steps_total, full=True, act_seed=None):
+def run_traj(make_env, n_robots, seed, episodes, max_steps_total, full=True, act_seed=None, episode_cap=None):
     random.seed(seed)
     np.random.seed(seed)
     env = make_env()
@@ -184,7 +195,9 @@ def run_traj(make_env, n_robots, seed, episodes, max_steps_total, full=True, act
         _record(env, obs, rec, snaps, digs, full, reward=0.0, done=False, reset=True,
                 actions=np.full(n_robots, -1, np.int32))
         done = False
-        while not done and total < max_steps_total:
+        ep_steps = 0
+        while not done and total < max_steps_total and (episode_cap is None or ep_steps < episode_cap):
+            ep_steps += 1
             a = act_rng.randint(0, 5, size=n_robots).astype(np.int32)
             py, npk = rng_states()
             rec["rng_py"].append(py); rec["rng_np"].append(npk)
@@ -262,8 +275,233 @@ def rng_vectors():
     return out
 
 
+CFG1 = dict(width=36, height=30, fire_zones=[[18, 14], [19, 14], [18, 15], [19, 15], [18, 16], [19, 16]],
+            exit_location=[36, 15], num_people=150)
+
+
+# ----------------------------------------------------------------------------
+# learner fixtures
+# ----------------------------------------------------------------------------
+
+def reference_observations(n, seed):
+    """n observations made by the reference's EvacuationEnv._get_state on the cfg1 layout:
+    window centres anywhere in the padded grid, People.rmap random bits, fire steps 0, 40,
+    90 and 180 (the env's fire model advanced with its own update()). Also returns each
+    one's compact form (occupancy bits of the 121 window cells where Check_Valid, centre,
+    fire step) -- the evx_obs the build's fused kernels read."""
+    rs = np.random.RandomState(seed)
+    random.seed(seed)
+    np.random.seed(seed)
+    env = EvacuationEnv(**CFG1)
+    L, W = env.width, env.height
+    obs, comp = [], []
+    steps = [0, 40, 90, 180]
+    per = [n // 4 + (1 if i < n % 4 else 0) for i in range(4)]
+    for t, k in zip(steps, per):
+        while env.fire_model.progressive_model.current_step < t:
+            env.fire_model.update()
+        for _ in range(k):
+            cx, cy = int(rs.randint(0, L + 2)), int(rs.randint(0, W + 2))
+            rm = (rs.random_sample((L + 2, W + 2)) < rs.uniform(0.05, 0.6)).astype(np.float64)
+            env.people.rmap = rm
+            env.map.robot_position = [cx, cy]
+            o = np.array(env._get_state(), dtype=np.float64)
+            occ = np.zeros(4, np.uint32)
+            for i in range(11):
+                for j in range(11):
+                    x, y = cx + i - 5, cy + j - 5
+                    if env.map.Check_Valid(x, y) and rm[x][y] == 1:
+                        c = i * 11 + j
+                        occ[c >> 5] |= np.uint32(1 << (c & 31))
+            obs.append(o)
+            comp.append(np.concatenate([occ.view(np.int32), np.array([cx, cy, t, 0], np.int32)]))
+    return np.stack(obs), np.stack(comp).astype(np.int32)
+
+
+def _store(prefix, tensors, out):
+    """Tensors by name at golden_util.select_positions (whole when small) + each one's
+    float64 sum of squares."""
+    from golden_util import select_positions
+    for t, (name, v) in enumerate(tensors.items()):
+        a = np.asarray(v, np.float32).reshape(-1)
+        sel = select_positions(a.size, t)
+        out[f"{prefix}{name}"] = a[sel]
+        out[f"{prefix}{name}__ss"] = np.float64(np.sum(a.astype(np.float64) ** 2))
+
+
+def dqn_fixtures():
+    """DQNNetwork forward and DQNAgent.learn vectors (agents/dqn_agent.py:15-168)."""
+    import torch
+    import torch.nn as nn
+    import torch.nn.functional as F
+    from Louvre_Evacuation.agents import dqn_agent as ref_agent
+    from golden_util import closed_form_params, conv_shapes, mlp_shapes
+
+    torch.set_num_threads(8)
+
+    class MLPNet(nn.Module):
+        """The build's MLP variant of DQNNetwork: DQNNetwork's fc stack on the
+        flattened (11, 11, 6) observation -- fc1 726->512, ReLU, Dropout(0.2), fc2, ReLU, fc3.
+        Harness only: the learn() these fixtures record is the reference's own."""
+
+        def __init__(self, hidden=512):
+            super().__init__()
+            self.fc1 = nn.Linear(726, hidden)
+            self.fc2 = nn.Linear(hidden, hidden // 2)
+            self.fc3 = nn.Linear(hidden // 2, 5)
+            self.dropout = nn.Dropout(0.2)
+
+        def forward(self, x):
+            x = x.reshape(x.shape[0], -1)
+            x = self.dropout(F.relu(self.fc1(x)))
+            return self.fc3(F.relu(self.fc2(x)))
+
+    def load(net, params):
+        net.load_state_dict({k: torch.from_numpy(v.copy()) for k, v in params.items()})
+
+    masks = []
+
+    def hook(_m, inp, outp):
+        masks.append((outp[0] if isinstance(outp, tuple) else outp).detach().ne(0).numpy().copy())
+
+    obs, comp = reference_observations(160, seed=11)
+    out = {"obs": obs.astype(np.float32), "obs_compact": comp}
+
+    # ---------------- forward: full-size networks, closed-form weights
+    fw = {}
+    x = torch.from_numpy(obs[:16].astype(np.float32))
+    for kind, net, shapes in [("conv", ref_agent.DQNNetwork((11, 11, 6), 5), conv_shapes()),
+                              ("mlp", MLPNet(), mlp_shapes())]:
+        load(net, closed_form_params(shapes, salt=1))
+        net.eval()
+        with torch.no_grad():
+            fw[f"{kind}_q_eval"] = net(x).numpy()
+        net.train()
+        h = net.dropout.register_forward_hook(hook)
+        masks.clear()
+        torch.manual_seed(5)
+        with torch.no_grad():
+            fw[f"{kind}_q_train"] = net(x).numpy()
+        h.remove()
+        fw[f"{kind}_mask_train"] = masks[0].astype(np.uint8)
+    fw["obs_idx"] = np.arange(16)
+    np.savez_compressed(os.path.join(OUT, "dqn_forward.npz"), **fw)
+    print("  dqn forward", {k: v.shape for k, v in fw.items()})
+
+    # ---------------- learn: 3 steps of the reference's DQNAgent.learn
+    lo = dict(out)  # the observations (f32, as DQNAgent.learn's FloatTensor) and their compact forms
+    cfg = dict(gamma=0.99, epsilon=1.0, epsilon_min=0.02, epsilon_decay=0.9995, learning_rate=1e-4,
+               batch_size=32, warmup_steps=0, memory_size=50000)
+    orig_sample, orig_clip = random.sample, torch.nn.utils.clip_grad_norm_
+    for kind, mk, shapes in [("conv32", lambda: ref_agent.DQNNetwork((11, 11, 6), 5, hidden_size=32),
+                              conv_shapes(hidden=32)),
+                             ("mlp", MLPNet, mlp_shapes())]:
+        random.seed(21)
+        np.random.seed(21)
+        torch.manual_seed(21)
+        agent = ref_agent.DQNAgent((11, 11, 6), 5, torch.device("cpu"), cfg)
+        agent.q_network, agent.target_network = mk(), mk()
+        p0 = closed_form_params(shapes, salt=2)
+        load(agent.q_network, p0)
+        agent.update_target_network()
+        agent.optimizer = torch.optim.Adam(agent.q_network.parameters(), lr=cfg["learning_rate"])
+        rs = np.random.RandomState(31)
+        NM = 48
+        idx_s, idx_s2 = rs.permutation(NM), NM + rs.permutation(NM)
+        acts = rs.randint(0, 5, NM)
+        rews = np.round(rs.normal(0.0, 30.0, NM), 3)
+        dones = rs.random_sample(NM) < 0.25
+        for i in range(NM):
+            agent.remember(obs[idx_s[i]], int(acts[i]), float(rews[i]), obs[idx_s2[i]], bool(dones[i]))
+        lo[f"{kind}_mem_s"], lo[f"{kind}_mem_s2"] = idx_s, idx_s2
+        lo[f"{kind}_mem_a"], lo[f"{kind}_mem_r"], lo[f"{kind}_mem_done"] = acts, rews, dones
+        mem_ids = {id(t): i for i, t in enumerate(agent.memory)}
+        rec = {}
+
+        def rec_sample(pop, k):
+            r = orig_sample(pop, k)
+            rec["idx"] = np.array([mem_ids[id(t)] for t in r], np.int32)
+            return r
+
+        def rec_clip(params, max_norm, *a, **kw):
+            params = list(params)
+            rec["grads"] = {n: p.grad.detach().numpy().copy() for n, p in agent.q_network.named_parameters()}
+            nrm = orig_clip(params, max_norm, *a, **kw)
+            rec["norm"] = float(nrm)
+            return nrm
+
+        hq = agent.q_network.dropout.register_forward_hook(hook)
+        ht = agent.target_network.dropout.register_forward_hook(hook)
+        random.sample, torch.nn.utils.clip_grad_norm_ = rec_sample, rec_clip
+        try:
+            for step in range(3):
+                masks.clear()
+                loss = agent.learn()
+                assert len(masks) == 2, len(masks)
+                lo[f"{kind}_s{step}_idx"] = rec["idx"]
+                lo[f"{kind}_s{step}_mask_online"] = masks[0].astype(np.uint8)
+                lo[f"{kind}_s{step}_mask_target"] = masks[1].astype(np.uint8)
+                lo[f"{kind}_s{step}_loss"] = np.float64(loss)
+                lo[f"{kind}_s{step}_norm"] = np.float64(rec["norm"])
+                lo[f"{kind}_s{step}_epsilon"] = np.float64(agent.epsilon)
+                _store(f"{kind}_s{step}_grad_", rec["grads"], lo)
+                _store(f"{kind}_s{step}_param_", {n: p.detach().numpy() for n, p in
+                                                  agent.q_network.named_parameters()}, lo)
+                st = agent.optimizer.state
+                _store(f"{kind}_s{step}_m_", {n: st[p]["exp_avg"].numpy() for n, p in
+                                              agent.q_network.named_parameters()}, lo)
+                _store(f"{kind}_s{step}_v_", {n: st[p]["exp_avg_sq"].numpy() for n, p in
+                                              agent.q_network.named_parameters()}, lo)
+        finally:
+            random.sample, torch.nn.utils.clip_grad_norm_ = orig_sample, orig_clip
+            hq.remove()
+            ht.remove()
+        print("  dqn learn", kind, [float(lo[f"{kind}_s{s}_loss"]) for s in range(3)])
+    np.savez_compressed(os.path.join(OUT, "dqn_learn.npz"), **lo)
+
+
+def g128_long():
+    """128x128 R16 trajectory past the fire's last step (180) with a reset at step 230
+    (an episode cap, as the runners' `while steps < max_steps` loop does)."""
+    L = W = 128
+    R, P = 16, 2276
+    kw = dict(width=L, height=W, fire_zones=None, exit_location=[L, W // 2], num_people=P)
+    init = [[15 + (i * 15) // max(R - 1, 1), 4 + (i * (W - 8)) // max(R - 1, 1)] for i in range(R)]
+    tr = run_traj(lambda: EvacuationEnvMultiR(init, **kw), R, seed=3, episodes=2, max_steps_total=260,
+                  full=False, episode_cap=230)
+    tr["robot_init"] = np.array(init, np.int32)
+    np.savez_compressed(os.path.join(OUT, "g128_long_traj.npz"), **tr)
+    print("  steps", len(tr["reward"]), "resets", int(tr["is_reset"].sum()))
+
+
+def g128_danger():
+    """sha256 per fire step (0..180) of the 128x128 danger tables (layout_tables' danger_p /
+    danger_o, float64 bytes): pins every step, where g128_layout.npz holds the first 27."""
+    L = W = 128
+    kw = dict(width=L, height=W, fire_zones=None, exit_location=[L, W // 2], num_people=2276)
+    lay = layout_tables(kw, 180)
+    dp = np.stack([np.frombuffer(hashlib.sha256(np.ascontiguousarray(lay["danger_p"][t]).tobytes()).digest(),
+                                 np.uint8) for t in range(181)])
+    do = np.stack([np.frombuffer(hashlib.sha256(np.ascontiguousarray(lay["danger_o"][t]).tobytes()).digest(),
+                                 np.uint8) for t in range(181)])
+    np.savez_compressed(os.path.join(OUT, "g128_danger_digests.npz"), danger_p=dp, danger_o=do,
+                        danger_p_max=lay["danger_p"].max(axis=(1, 2)), danger_o_sum=lay["danger_o"].sum(axis=(1, 2)))
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
+    parts = sys.argv[1:] or ["base", "dqn", "g128long", "g128danger"]
+    if "dqn" in parts:
+        print("dqn fixtures")
+        dqn_fixtures()
+    if "g128danger" in parts:
+        print("g128 danger digests")
+        g128_danger()
+    if "g128long" in parts:
+        print("g128 long trajectory")
+        g128_long()
+    if "base" not in parts:
+        return
     cfg1 = dict(width=36, height=30, fire_zones=[[18, 14], [19, 14], [18, 15], [19, 15], [18, 16], [19, 16]],
                 exit_location=[36, 15], num_people=150)
 
