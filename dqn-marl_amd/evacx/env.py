@@ -480,6 +480,31 @@ class VecEnv:
             raise _lib.EvacxError(f"device error word {v}")
 
     # ----------------------------------------------------- host inspection
+    def host_states(self, ids) -> list:
+        """host_state of several envs with one device-to-host copy per field (tests)."""
+        lay = self.lay
+        P, R = lay.P, lay.R
+        idx = torch.as_tensor(list(ids), dtype=torch.long, device=self.pk.device)
+        pk = self.pk.view(self.E, P)[idx].cpu().numpy().view(np.uint32)
+        health = self.health.view(self.E, P)[idx].cpu().numpy()
+        acc = self.acc.view(self.E, P)[idx].cpu().numpy()
+        bits = self.rmap.view(self.E, lay.RW)[idx].cpu().numpy().view(np.uint32)
+        robots = self.robots.view(self.E, R)[idx].cpu().numpy()
+        view = self.view[idx].cpu().numpy()
+        scal = self.scal.view(self.E, 4)[idx].cpu().numpy()
+        py = self.py_mt.view(self.E, 625)[idx].cpu().numpy().view(np.uint32)
+        nps = self.np_mt.view(self.E, 625)[idx].cpu().numpy().view(np.uint32)
+        th = None if self.thmap is None else self.thmap.view(self.E, lay.GX, lay.GY)[idx].cpu().numpy()
+        out = []
+        for j in range(len(idx)):
+            rm = ((bits[j][:, None] >> np.arange(32, dtype=np.uint32)[None, :]) & 1).astype(np.uint8).reshape(-1)
+            out.append(dict(pos=np.stack([pk[j] & 0xFFF, (pk[j] >> 12) & 0xFFF], -1).astype(np.int32),
+                            flags=((pk[j] >> 24) & 3).astype(np.uint8), health=health[j], acc=acc[j],
+                            rmap=rm[:lay.G].reshape(lay.GX, lay.GY), robots=unpack_xy(robots[j]),
+                            view=unpack_xy(view[j:j + 1])[0], scal=scal[j], py_mt=py[j], np_mt=nps[j],
+                            thmap=None if th is None else th[j]))
+        return out
+
     def host_state(self, e: int) -> dict:
         """One env's state in the oracle's representation (tests / drop-in)."""
         lay = self.lay

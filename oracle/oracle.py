@@ -253,3 +253,34 @@ def floor_field(valid, source, pen=None):
         fin = np.isfinite(out)
         out[fin] = out[fin] + np.asarray(pen, np.float64)[fin]
     return out
+
+
+# ------------------------------------------------------ counter-based draws (draw_oracle.c)
+def epsilon_greedy(Q, epsilon, seed, offset):
+    """evx_act / the fused act's epsilon-greedy restated: actions [n] int32 for Q [n][A] f32."""
+    q = np.ascontiguousarray(Q, np.float32)
+    n, A = q.shape
+    out = np.zeros(n, np.int32)
+    L = lib()
+    L.orc_epsilon_greedy.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_float, C.c_uint64, C.c_uint64, C.c_void_p]
+    L.orc_epsilon_greedy(_p(q), n, A, float(epsilon), int(seed) & (2**64 - 1), int(offset) & (2**64 - 1), _p(out))
+    return out
+
+
+def replay_indices(base, size, capacity, B, seed, offset):
+    """evx_replay_sample(_window)'s ring slots restated: int64 [B]."""
+    idx = np.zeros(B, np.int64)
+    L = lib()
+    L.orc_replay_indices.argtypes = [C.c_int64, C.c_int64, C.c_int64, C.c_int, C.c_uint64, C.c_uint64, C.c_void_p]
+    L.orc_replay_indices(int(base), int(size), int(capacity), int(B), int(seed) & (2**64 - 1),
+                         int(offset) & (2**64 - 1), _p(idx))
+    return idx
+
+
+def dropout_keep(seed, stream, p, rows, cols=512):
+    """The fused MLP kernels' dropout keep mask restated: uint8 [rows][cols]."""
+    keep = np.zeros((rows, cols), np.uint8)
+    L = lib()
+    L.orc_dropout_keep.argtypes = [C.c_uint32, C.c_uint32, C.c_float, C.c_int, C.c_int, C.c_void_p]
+    L.orc_dropout_keep(seed & 0xFFFFFFFF, stream & 0xFFFFFFFF, float(p), rows, cols, _p(keep))
+    return keep

@@ -38,9 +38,28 @@ def traj_spec(name):
         return "cfg1_layout", 150, lay.reference_multi()
     if name == "g64_multi_traj":
         return "g64_layout", 569, lay.reference_scaled_multi(64, 64, 8)
-    if name == "g128_multi_traj":
+    if name in ("g128_multi_traj", "g128_long_traj"):
         return "g128_layout", 2276, lay.reference_scaled_multi(128, 128, 16)
     raise KeyError(name)
+
+
+# trajectories that run past the fire steps of their committed layout tables use the host
+# builder's tables, pinned for every fire step by g128_danger_digests.npz
+# (tests/test_oracle_golden.py::test_g128_danger_tables_all_fire_steps)
+BUILT_TABLES = {"g128_long_traj"}
+
+
+def traj_tables(name):
+    """(LayoutTables, P) of a trajectory fixture: the committed reference tables, or the host
+    builder's (full fire schedule) for BUILT_TABLES."""
+    from evacx.layout import LayoutTables, build_tables
+    lname, P, spec = traj_spec(name)
+    if name in BUILT_TABLES:
+        return build_tables(spec, t_max=180), P
+    t = load(lname)
+    return LayoutTables(spec=spec, floor=t["floor"], valid=t["valid"], exit_mask=t["exit_mask"],
+                        barrier=t["barrier"], danger_p=t["danger_p"], danger_o=t["danger_o"],
+                        obs_origin=tuple(int(v) for v in t["obs_origin"])), P
 
 
 def oracle_layout(traj_name):
@@ -48,6 +67,10 @@ def oracle_layout(traj_name):
     from oracle.oracle import Layout
     lname, P, spec = traj_spec(traj_name)
     t = load(lname)
+    if traj_name in BUILT_TABLES:
+        tb, _ = traj_tables(traj_name)
+        t = dict(floor=tb.floor, valid=tb.valid, exit_mask=tb.exit_mask, barrier=tb.barrier,
+                 danger_p=tb.danger_p, danger_o=tb.danger_o, obs_origin=np.asarray(tb.obs_origin))
     return Layout(L=spec.L, W=spec.W, P=P, R=spec.R, floor=t["floor"], valid=t["valid"],
                   exit_mask=t["exit_mask"], barrier=t["barrier"], danger_p=t["danger_p"],
                   danger_o=t["danger_o"], obs_origin=t["obs_origin"], exit=spec.exit,

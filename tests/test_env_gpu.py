@@ -22,12 +22,8 @@ def _need_gpu():
 
 
 def fixture_tables(traj):
-    from evacx.layout import LayoutTables
-    lname, P, spec = traj_spec(traj)
-    t = load(lname)
-    return LayoutTables(spec=spec, floor=t["floor"], valid=t["valid"], exit_mask=t["exit_mask"],
-                        barrier=t["barrier"], danger_p=t["danger_p"], danger_o=t["danger_o"],
-                        obs_origin=tuple(int(v) for v in t["obs_origin"])), P
+    from golden_util import traj_tables
+    return traj_tables(traj)
 
 
 def gpu_state_fields(env, e, obs64):
@@ -36,7 +32,8 @@ def gpu_state_fields(env, e, obs64):
                 thmap=st["thmap"], robots=st["robots"], view=st["view"], obs=obs64[e]), st
 
 
-@pytest.mark.parametrize("traj", ["cfg1_single_traj", "cfg1_multi_traj", "g64_multi_traj", "g128_multi_traj"])
+@pytest.mark.parametrize("traj", ["cfg1_single_traj", "cfg1_multi_traj", "g64_multi_traj", "g128_multi_traj",
+                                  "g128_long_traj"])
 def test_gpu_replays_reference_trajectory(traj):
     _need_gpu()
     from evacx.env import DeviceLayout, VecEnv
@@ -353,3 +350,60 @@ def test_heavy_and_light_parts_on_two_streams_match_one_launch():
     assert max_heavy > 0
     a.check_err()
     b.check_err()
+
+
+def test_stationary_mix_matches_oracle_at_bench_scale():
+    """Parity where bench.py times: the cfg3 per-GPU share (128x128, P 2276, R 16, 4096 envs)
+    prepared exactly as bench.py --phase stationary does (1300 env-only steps, env g force-reset
+    at preparation step g % 1200: env ages spread over an episode, saturated fire, heavy and
+    light envs, fused auto-resets); then 64 envs spread over the age mix are snapshotted into
+    the oracle and both step 100 more steps with the same actions -- every state field, MT
+    stream, reward and done flag bit-exact on every step (the GPU steps all 4096 envs with the
+    heavy-first dispatch order, as in the bench)."""
+    _need_gpu()
+    from evacx.env import DeviceLayout, VecEnv
+    from evacx.layout import build_tables, synthetic
+    from oracle import oracle as orc
+    E, P, R, L = 4096, 2276, 16, 128
+    tables = build_tables(synthetic(L, L, R))
+    lay = DeviceLayout(tables, P)
+    env = VecEnv(lay, E)
+    env.seed([1234 + i for i in range(E)])
+    env.reset()
+    gid = torch.arange(E, device="cuda")
+    g = torch.Generator(device="cuda").manual_seed(4321)
+    acts = torch.empty(E * R, device="cuda", dtype=torch.int32)
+    for w in range(1300):
+        torch.randint(0, 5, (E * R,), device="cuda", dtype=torch.int32, generator=g, out=acts)
+        env.step(acts, auto_reset=True)
+        if w < 1200:
+            env.reset(mask=(gid % 1200 == w) & ~env.done.bool())
+    ids = list(range(0, E, E // 64))
+    olay = orc.Layout.from_tables(tables, P)
+    oenvs = []
+    for st in env.host_states(ids):
+        oe = orc.Env(olay, thmap=False)
+        oe.load_state(st)
+        oenvs.append(oe)
+    ages = np.array([oe.scal[1] for oe in oenvs])
+    heavy0 = int(env.order[E].item()) if env.order is not None else 0
+    assert ages.max() - ages.min() > 600, ages  # the sample spans the episode-age mix
+    rng = np.random.RandomState(5)
+    n_done = 0
+    for s in range(100):
+        a = rng.randint(0, 5, size=(E, R)).astype(np.int32)
+        env.step(torch.from_numpy(a.reshape(-1)).cuda(), auto_reset=True)
+        rew = env.reward[ids].cpu().numpy()
+        dn = env.done[ids].cpu().numpy()
+        sts = env.host_states(ids)
+        for j, (e, oe) in enumerate(zip(ids, oenvs)):
+            _, r, d = oe.step(a[e])
+            assert rew[j] == r and bool(dn[j]) == d, (s, e, rew[j], r)
+            if d:
+                oe.reset()
+                n_done += 1
+            st = sts[j]
+            for k in ["pos", "flags", "health", "acc", "rmap", "robots", "view", "scal", "py_mt", "np_mt"]:
+                assert np.array_equal(st[k], getattr(oe, k)), (s, e, k)
+    env.check_err()
+    print(f"stationary mix: ages {ages.min()}..{ages.max()}, heavy at start {heavy0}, resets {n_done}")

@@ -63,6 +63,22 @@ def test_layout_builder_matches_reference(lname, spec):
     assert tuple(tb.obs_origin) == tuple(g["obs_origin"])
 
 
+def test_g128_danger_tables_all_fire_steps():
+    """The host builder's 128x128 danger tables equal the reference's for EVERY fire step
+    0..180 (sha256 of each step's float64 table, captured from the reference's
+    FireSpreadModel.get_max_danger: envs/fire_model.py:138-188); g128_layout.npz holds the
+    first 27 steps in full."""
+    import hashlib
+    d = load("g128_danger_digests")
+    tb = lay.build_tables(lay.reference_scaled_multi(128, 128, 16), t_max=180)
+    assert tb.danger_p.shape[0] == 181 and d["danger_p"].shape[0] == 181
+    for t in range(181):
+        dp = np.frombuffer(hashlib.sha256(np.ascontiguousarray(tb.danger_p[t]).tobytes()).digest(), np.uint8)
+        do = np.frombuffer(hashlib.sha256(np.ascontiguousarray(tb.danger_o[t]).tobytes()).digest(), np.uint8)
+        assert np.array_equal(dp, d["danger_p"][t]), t
+        assert np.array_equal(do, d["danger_o"][t]), t
+
+
 def test_known_answers_cfg1():
     g = load("cfg1_layout")
     fin = g["floor"][np.isfinite(g["floor"])]
@@ -78,8 +94,11 @@ def replay(traj_name, check_each):
     env = orc.Env(L)
     for k in range(len(tr["reward"])):
         if tr["is_reset"][k]:
-            env.py_mt[:] = tr["rng_py"][k]
-            env.np_mt[:] = tr["rng_np"][k]
+            if k == 0:  # the recorded start state; later resets continue the streams
+                env.py_mt[:] = tr["rng_py"][k]
+                env.np_mt[:] = tr["rng_np"][k]
+            assert np.array_equal(env.py_mt, tr["rng_py"][k]), k
+            assert np.array_equal(env.np_mt, tr["rng_np"][k]), k
             obs, r, d = env.reset(), 0.0, False
         else:
             assert np.array_equal(env.py_mt, tr["rng_py"][k]), k
@@ -91,7 +110,8 @@ def replay(traj_name, check_each):
     return tr
 
 
-@pytest.mark.parametrize("traj", ["cfg1_single_traj", "cfg1_multi_traj", "g64_multi_traj", "g128_multi_traj"])
+@pytest.mark.parametrize("traj", ["cfg1_single_traj", "cfg1_multi_traj", "g64_multi_traj", "g128_multi_traj",
+                                  "g128_long_traj"])
 def test_oracle_trajectory_bit_exact(traj):
     def check(k, tr, env, obs, r, d):
         st = state_fields(env.state(), obs)
@@ -103,6 +123,8 @@ def test_oracle_trajectory_bit_exact(traj):
         assert env.scal[1] == tr["cur_step"][k] and float(env.time[0]) == tr["time"][k]
     tr = replay(traj, check)
     assert tr["is_reset"].sum() >= 1
+    if traj == "g128_long_traj":  # past the fire's last step, and a reset at 128x128
+        assert tr["fire_step"].max() == 180 and tr["is_reset"].sum() == 2 and len(tr["reward"]) >= 250
 
 
 def test_oracle_quirks_cfg1_single():
