@@ -182,7 +182,7 @@ def main():
                     grad_hook=hook,
                     lagged_learn=args.schedule == "lagged", replay=args.replay,
                     replay_capacity=args.replay_capacity, groups=args.groups if args.mode == "train" else 1,
-                    layout_of=layout_of)
+                    layout_of=layout_of, world_envs=E * world)
     env = tr.env
     lagged_ok = tr.fast is not None  # the lagged schedule needs the fused MLP path
     schedule = args.schedule if lagged_ok else "strict"

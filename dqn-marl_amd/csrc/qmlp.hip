@@ -138,6 +138,7 @@ struct Fwd {
     const float* b3;
     // dropout on fc1's output
     uint32_t drop_seed, drop_stream, drop_thresh;  // thresh: floor(p * 65536) on 16-bit uniforms
+    uint32_t drop_row0;  // global row of row 0 in the hash (even): masks keyed by global agent id
     float drop_scale;
     // outputs
     __bf16* h1;  // [N][512]
@@ -355,7 +356,8 @@ __device__ __forceinline__ void fc1_slab(const Fwd& a, const f32x16 (&accm)[NTW]
 #pragma unroll
     for (int r = 0; r < 16; r += 2) {  // rows rl, rl + 1: one dropout hash per pair
         const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;
-        const uint32_t ph = a.drop_thresh ? drop_row(a.drop_seed, a.drop_stream, (uint32_t)(row0 + rl) >> 1) : 0u;
+        const uint32_t ph =
+            a.drop_thresh ? drop_row(a.drop_seed, a.drop_stream, (a.drop_row0 + (uint32_t)(row0 + rl)) >> 1) : 0u;
 #pragma unroll
         for (int nt = 0; nt < NTW; nt++) {
             const int cl = cl0 + nt * 32 + (lane & 31);
@@ -1327,6 +1329,8 @@ static int make_fwd(const evx_layout* lay, const evx_obs* obs, int32_t n, const 
     a.b3 = p->b3;
     a.drop_seed = drop ? drop->seed : 0u;
     a.drop_stream = drop ? drop->stream : 0u;
+    a.drop_row0 = drop ? drop->row0 : 0u;
+    if (a.drop_row0 & 1u) return mfail(-22, "qmlp_forward: dropout row0 must be even (one hash per row pair)");
     const float dp = drop ? drop->p : 0.f;
     a.drop_thresh = dp > 0.f ? (uint32_t)((double)dp * 65536.0) : 0u;  // 16-bit uniforms
     if (dp > 0.f && a.drop_thresh == 0u) a.drop_thresh = 1u;

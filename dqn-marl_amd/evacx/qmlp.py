@@ -37,7 +37,7 @@ class evx_qmlp_params(C.Structure):
 
 
 class evx_qmlp_dropout(C.Structure):
-    _fields_ = [("seed", C.c_uint32), ("stream", C.c_uint32), ("p", C.c_float), ("pad0", C.c_uint32),
+    _fields_ = [("seed", C.c_uint32), ("stream", C.c_uint32), ("p", C.c_float), ("row0", C.c_uint32),
                 ("mask", C.c_void_p)]
 
 
@@ -186,10 +186,12 @@ class MLPFast:
 
     @staticmethod
     def _drop(drop):
-        """drop: (seed, stream, p) or (seed, stream, p, keep_mask uint8 [n][512]) -- an explicit
-        mask (the reference's captured torch masks, tests) replaces the hash."""
+        """drop: (seed, stream, p[, keep_mask uint8 [n][512] or None[, row0]]) -- an explicit mask
+        (the reference's captured torch masks, tests) replaces the hash; row0 (even) keys the
+        hash rows by global agent id."""
         m = drop[3] if len(drop) > 3 else None
-        return evx_qmlp_dropout(seed=drop[0] & 0xFFFFFFFF, stream=drop[1] & 0xFFFFFFFF, p=drop[2],
+        row0 = int(drop[4]) if len(drop) > 4 else 0
+        return evx_qmlp_dropout(seed=drop[0] & 0xFFFFFFFF, stream=drop[1] & 0xFFFFFFFF, p=drop[2], row0=row0,
                                 mask=None if m is None else m.data_ptr())
 
     @staticmethod
@@ -238,13 +240,13 @@ def _fmix32(h):
     return h
 
 
-def dropout_keep(seed: int, stream: int, p: float, rows: int, cols: int = HID) -> np.ndarray:
+def dropout_keep(seed: int, stream: int, p: float, rows: int, cols: int = HID, row0: int = 0) -> np.ndarray:
     """The kernels' dropout keep mask [rows][cols] (bool), restated on the host (tests):
     one hash per (row pair, column), low 16 bits for the even row, high for the odd;
     keep iff the 16-bit value >= floor(p * 65536)."""
     seed, stream = seed & 0xFFFFFFFF, stream & 0xFFFFFFFF
     s = int(_fmix32((stream * 0x632BE5AB + 0x9E3779B9) & 0xFFFFFFFF))
-    r = np.arange(rows, dtype=np.uint64)
+    r = np.arange(row0, row0 + rows, dtype=np.uint64)
     pair = r >> 1
     ph = _fmix32(np.uint64(seed ^ s) ^ ((pair * 0x9E3779B1) & 0xFFFFFFFF))
     c = np.arange(cols, dtype=np.uint64)

@@ -128,12 +128,16 @@ class VecTrainer:
                  epsilon_decay: float = 0.9995, target_every: int = 1000, learner_seed: int = 0,
                  grad_hook=None, learn_every: int = 1, lagged_learn: bool = False, replay: str = "uniform",
                  prio_alpha: float = 0.6, prio_beta0: float = 0.4, prio_beta_steps: int = 100000,
-                 prio_eps: float = 1e-6, groups: int = 1, layout_of=None):
+                 prio_eps: float = 1e-6, groups: int = 1, layout_of=None, world_envs: Optional[int] = None):
         """groups: the envs are split into this many parts, each stepping on its own
         stream chain (see _Group); the env results do not depend on it (every env is
         still stepped once per step with its own streams), the act's dropout masks do.
         layout: a DeviceLayout, or an evacx.env.LayoutSet with layout_of = each env's
-        layout (per-env layouts; observations in the replay carry their layout)."""
+        layout (per-env layouts; observations in the replay carry their layout).
+        world_envs: envs over all ranks (default E). This rank's envs are global ids
+        env_offset .. env_offset + E - 1; the act's epsilon draws and dropout rows are keyed
+        by global agent id, so every env's trajectory is the same at any GPU count as long
+        as the actions do not depend on the (rank-shared) weights' history."""
         self.lay, self.E, self.R = layout, E, layout.R
         self.device = layout.device
         # the push reads env.obs_prev: no copy per step
@@ -164,6 +168,10 @@ class VecTrainer:
         self.lagged = lagged_learn
         n = E * self.R
         self.n_agents = n
+        self.agent0 = env_offset * self.R  # global agent id of this rank's first robot
+        self.n_world = (E if world_envs is None else int(world_envs)) * self.R
+        if self.agent0 % 2:
+            raise ValueError("env_offset * R must be even (dropout hash rows come in pairs)")
         self.actions = torch.zeros(n, dtype=torch.int32, device=self.device)
         ng = n // len(parts)
         self.groups: List[_Group] = [_Group(p, g, g * ng, self.actions[g * ng:(g + 1) * ng], self.device)
@@ -178,7 +186,10 @@ class VecTrainer:
             self.samp.update(idx=torch.zeros(batch, dtype=torch.int64, device=self.device),
                              w=torch.zeros(batch, dtype=torch.float32, device=self.device),
                              td=torch.zeros(batch, dtype=torch.float32, device=self.device))
+        # replay sampling: per rank (each rank samples its own shard); act draws: one key for
+        # all ranks (counters are global agent ids)
         self.seed = learner_seed * 7919 + env_offset + 17
+        self.act_seed = learner_seed * 7919 + 17
         self.t = 0
         self.learn_steps = 0
         cur = torch.cuda.current_stream(self.device)
@@ -203,15 +214,17 @@ class VecTrainer:
     def _act(self, grp: _Group):
         """DQNAgent.act in train mode for one group's robots: dropout active, epsilon-greedy
         over argmax Q; the epsilon draws are counted over all E*R robots of the step."""
-        off = self.t * self.n_agents + grp.row0
+        g0 = self.agent0 + grp.row0  # global agent id of the group's first robot
+        off = self.t * self.n_world + g0
         if self.fast is not None:
             self.learner.drop_stream += 1
-            self.fast.act(self.lay.c, grp.env.obs, grp.n, drop=(self.seed, self.learner.drop_stream, DROPOUT_P),
-                          actions=grp.actions, epsilon=float(self.epsilon), act_seed=self.seed, act_offset=off)
+            self.fast.act(self.lay.c, grp.env.obs, grp.n,
+                          drop=(self.learner.seed, self.learner.drop_stream, DROPOUT_P, None, g0),
+                          actions=grp.actions, epsilon=float(self.epsilon), act_seed=self.act_seed, act_offset=off)
             return
         x = grp.env.expand_obs(torch.float32)  # [E/G, R, 11, 11, 6]
         Q = self.learner.q_values(x.view(grp.n, 11, 11, 6), train=True)
-        qcheck(qlib().evx_act(Q.data_ptr(), grp.n, self.learner.actions, float(self.epsilon), self.seed, off,
+        qcheck(qlib().evx_act(Q.data_ptr(), grp.n, self.learner.actions, float(self.epsilon), self.act_seed, off,
                               grp.actions.data_ptr(), _stream()), "act")
 
     def act(self):

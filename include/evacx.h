@@ -322,7 +322,8 @@ typedef struct {
 typedef struct {
     uint32_t seed, stream; /* mask identity */
     float p;               /* drop probability; 0 = eval (no dropout) */
-    uint32_t pad0;
+    uint32_t row0;         /* hash row of the batch's first row (even): a rank's act masks keyed by the
+                            * global agent id, so trajectories do not depend on the GPU count */
     const uint8_t *mask;   /* optional explicit keep mask [n][512] (1 = keep; scale 1/(1-p)) in place of
                             * the hash: replays the reference's captured torch dropout masks */
 } evx_qmlp_dropout;

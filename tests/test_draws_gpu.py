@@ -116,16 +116,16 @@ def test_trainer_step_composition(lagged):
         tr.sync()
         torch.cuda.synchronize()
         obs0 = env.obs.clone()
-        eps, off, stream = tr.epsilon, tr.t * tr.n_agents, tr.learner.drop_stream + 1
+        eps, off, stream = tr.epsilon, tr.t * tr.n_world + tr.agent0, tr.learner.drop_stream + 1
         h1 = torch.empty(2 * n * HID, dtype=torch.int16, device="cuda")
         q = torch.empty(n, 5, device="cuda")
-        tr.fast.forward(lay.c, obs0, n, h1, drop=(tr.seed, stream, DROPOUT_P), q=q)
+        tr.fast.forward(lay.c, obs0, n, h1, drop=(tr.learner.seed, stream, DROPOUT_P, None, tr.agent0), q=q)
         pos0 = tr.replay.pos
         tr.step()
         tr.sync()
         torch.cuda.synchronize()
         acts = tr.actions.cpu().numpy()
-        assert np.array_equal(acts, orc.epsilon_greedy(q.cpu().numpy(), eps, tr.seed, off)), t
+        assert np.array_equal(acts, orc.epsilon_greedy(q.cpu().numpy(), eps, tr.act_seed, off)), t
         sl = slice(pos0, pos0 + n)
         rp = tr.replay
         done = env.done.cpu().numpy().astype(bool)

@@ -26,6 +26,8 @@ ap.add_argument("--robots", type=int, default=16)
 ap.add_argument("--warmup", type=int, default=1300)
 ap.add_argument("--stagger", type=int, default=1200)
 ap.add_argument("--no-order", action="store_true", help="identity dispatch order (no heavy workgroups)")
+ap.add_argument("--reset-all", action="store_true",
+                help="after the warm-up reset every env (the bench's start-of-episode phase: fire kept)")
 args = ap.parse_args()
 E, R = args.envs, args.robots
 spec = synthetic(args.grid, args.grid, R)
@@ -41,6 +43,8 @@ for i in range(args.warmup):
     if args.stagger and i < args.stagger:
         m = m | (gid % args.stagger == i)
     env.reset(mask=m)
+if args.reset_all:
+    env.reset()
 stamps = torch.zeros(E * 48, dtype=torch.int64, device="cuda")
 env.out.stamps = _ptr(stamps)
 for i in range(3):
