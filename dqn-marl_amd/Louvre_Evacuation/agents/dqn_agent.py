@@ -71,6 +71,9 @@ class DQNNetwork:
         return self._lr.q_values(x.contiguous(), train=self.training, target=self._target).clone()
 
 
+_AGENTS = 0  # agents built in this process (distinct dropout streams)
+
+
 def _device():
     if not torch.cuda.is_available():
         raise RuntimeError("evacx DQNAgent needs an MI355X (HIP) device; no CPU fallback exists")
@@ -141,11 +144,20 @@ class DQNAgent:
         self.target_update_freq = config.get("target_update_freq", 200)
         self.warmup_steps = config.get("warmup_steps", 1000)
         hidden = config.get("hidden_size", 512)
+        global _AGENTS
+        _AGENTS += 1
+        # dropout seed: derived without drawing from any global stream (the reference's dropout
+        # draws torch's generator, which a counter-based Philox cannot follow draw for draw)
+        seed = (int(torch.initial_seed()) * 1000003 + _AGENTS) & 0x7FFFFFFF if config.get("seed") is None \
+            else int(config["seed"])
         self._learner = Learner(kind="conv", device=self.device, lr=self.learning_rate, gamma=self.gamma,
-                                max_norm=1.0, precision="f32", hidden=hidden, actions=action_size,
-                                # torch's generator, never the global `random` stream the env shares
-                                seed=int(torch.randint(0, 2**31 - 1, (1,)).item()) if config.get("seed") is None
-                                else int(config["seed"]))
+                                max_norm=1.0, precision="f32", hidden=hidden, actions=action_size, seed=seed)
+        # initial weights as the reference draws them: q_network then target_network
+        # (agents/dqn_agent.py:83-84), each from torch's global generator in module order; the
+        # target's draw is consumed and then overwritten by update_target_network (:95)
+        if config.get("seed") is None:
+            self._learner.online.init_from_global_torch()
+            self._learner.target.init_from_global_torch()
         self.q_network = DQNNetwork(state_size, action_size, hidden, _learner=self._learner)
         self.target_network = DQNNetwork(state_size, action_size, hidden, _learner=self._learner, _target=True)
         self.optimizer = _AdamView(self._learner)

@@ -47,9 +47,20 @@ def _get_py_state() -> np.ndarray:
     return np.array(st[1], dtype=np.uint64).astype(np.uint32)
 
 
-def _set_py_state(words: np.ndarray):
+def _set_py_state(words: np.ndarray, gauss_next=None):
+    """Install the MT words back into the global stream. ``gauss_next`` (random.gauss's
+    cached second variate) is not touched by the env, so the caller's value is kept."""
     v = [int(x) for x in words]
-    random.setstate((3, tuple(v), None))
+    random.setstate((3, tuple(v), gauss_next))
+
+
+def _action_code(x) -> int:
+    """Map an action to the device code as Map.move_robot tests it (envs/map.py:180-193):
+    Python equality with 0..4 (so 3.0, np.float64(1), True or a 0-d array move the robot),
+    anything else is ignored (-1)."""
+    if x in (0, 1, 2, 3, 4):
+        return next(v for v in range(5) if x == v)
+    return -1
 
 
 def _get_np_state():
@@ -102,11 +113,12 @@ class EvacuationEnv:
     # ----------------------------------------------------------- plumbing
     def _push_rng(self):
         self._np_state = _get_np_state()
+        self._gauss_next = random.getstate()[2]
         self._venv.set_rng(_get_py_state()[None], _np_words(self._np_state)[None])
 
     def _pull_rng(self):
         py, nps = self._venv.get_rng()
-        _set_py_state(py[0])
+        _set_py_state(py[0], self._gauss_next)
         st = self._np_state
         np.random.set_state((st[0], nps[0][:624].copy(), int(nps[0][624]), st[3], st[4]))
 
@@ -146,6 +158,8 @@ class EvacuationEnv:
         self._venv.reset()
         self._pull_rng()
         self._refresh()
+        # person trajectories (evacuation_env.py:79-80): one log entry per step, materialised on access
+        self._traj_log = [self._host["pos"].copy()]
         self.time = 0
         self.robot_direction = 1
         self.robot_trajectory = [(tuple(self.map.robot_position), 0)]
@@ -155,25 +169,67 @@ class EvacuationEnv:
         return obs[0]
 
     def _actions(self, action):
-        if action is None:
-            raise NotImplementedError("patrol mode (action=None) is not part of the accelerated path")
         return [action]
+
+    def _patrol(self, rid: int):
+        """Map.move_robot(None) (envs/map.py:172-178): robot rid steps one cell along x,
+        turning at the ends of map.robot_range; no validity check. The direction lives on the
+        map (unset until a robot first reaches an end, as in the reference). The move is made
+        here and the device step sees action -1 for this robot (no move)."""
+        pos = self.map.robot_positions
+        x = pos[rid][0]
+        if x >= self.map.robot_range[1]:
+            self.map.robot_direction = -1
+        elif x <= self.map.robot_range[0]:
+            self.map.robot_direction = 1
+        pos[rid][0] = x + self.map.robot_direction
+        self._set_robots(pos)
+        if rid == 0:  # map.robot_position = robot_positions[0]
+            self._set_view(pos[0])
 
     def step(self, action):
         acts = self._actions(action)
-        a = np.array([int(x) if isinstance(x, (int, np.integer)) and 0 <= int(x) <= 4 else -1 for x in acts],
-                     dtype=np.int32)
+        codes = []
+        for rid, x in enumerate(acts):  # robots move in id order (evacuation_env_multi.py:60-61)
+            if x is None:
+                self._patrol(rid)
+                codes.append(-1)
+            else:
+                codes.append(_action_code(x))
+        a = np.array(codes, dtype=np.int32)
         self._sync_params()
         step0 = self.current_step
         self._push_rng()
         self._venv.step(torch.from_numpy(a).to(self._venv.pk.device))
         self._pull_rng()
+        prev = self._host["pos"]
         self._refresh()
+        cur = self._host["pos"].copy()
+        # execute_move records every mover (people.py:303-306); a person moves to a neighbour
+        self._traj_log.append((step0, cur, (cur != prev).any(axis=1), self._host["health"].copy()))
         self.time = 0.5 * self.current_step
         reward = float(self._venv.reward[0].item())
         done = bool(self._venv.done[0].item())
         self._record_robots(step0)
         return self._state_out(self._obs()), reward, done, self._info()
+
+    _step_traj_entries = True  # EvacuationEnv.step appends {'pos', 'step'} per person (:134-135)
+
+    def person_trajectory(self, i: int) -> list:
+        """Person i's ``trajectory`` list as the reference builds it: the reset entry
+        (evacuation_env.py:79-80), then per step the execute_move record of a mover
+        (people.py:52-59, 306: savety/dead still False when recorded) and, in the single-robot
+        env, the per-step entry (evacuation_env.py:134-135)."""
+        log = self._traj_log
+        p0 = log[0][i]
+        out = [{"pos": (int(p0[0]) + 0.5, int(p0[1]) + 0.5), "step": 0}]
+        for step0, cur, moved, health in log[1:]:
+            pos = (int(cur[i][0]) + 0.5, int(cur[i][1]) + 0.5)
+            if moved[i]:
+                out.append({"pos": pos, "health": float(health[i]), "savety": False, "dead": False})
+            if self._step_traj_entries:
+                out.append({"pos": pos, "step": step0})
+        return out
 
     def _record_robots(self, step0):
         self.robot_trajectory.append((tuple(self.map.robot_position), step0))

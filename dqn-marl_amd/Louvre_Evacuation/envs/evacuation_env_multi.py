@@ -14,6 +14,7 @@ from .evacuation_env import EvacuationEnv
 class EvacuationEnvMulti(EvacuationEnv):
     _robot_init = ((10, 15), (20, 15))
     _reset_robots = True
+    _step_traj_entries = False  # the multi-robot step records only execute_move entries (:59-66)
 
     def __init__(self, width=36, height=30, fire_zones=None, exit_location=None, num_people=150):
         self.num_robots = len(self._robot_init)

@@ -15,15 +15,28 @@ class People:
 
 
 class PersonView:
-    __slots__ = ("id", "pos", "health", "savety", "dead", "trajectory")
+    __slots__ = ("id", "pos", "health", "savety", "dead", "_env", "_traj")
 
-    def __init__(self, pid, x, y, health, flags):
+    def __init__(self, pid, x, y, health, flags, env=None):
         self.id = pid
         self.pos = (x + 0.5, y + 0.5)
         self.health = float(health) if not (flags & 2 and health == 0) else 0
         self.savety = bool(flags & 1)
         self.dead = bool(flags & 2)
-        self.trajectory = []
+        self._env = env
+        self._traj = None
+
+    @property
+    def trajectory(self):
+        """The reference's Person.trajectory (people.py:21, 52-59), built from the env's
+        per-step log on first access."""
+        if self._traj is None:
+            self._traj = self._env.person_trajectory(self.id - 1) if self._env is not None else []
+        return self._traj
+
+    @trajectory.setter
+    def trajectory(self, v):
+        self._traj = v
 
     @property
     def speed(self):
@@ -47,7 +60,7 @@ class PeopleView:
     def list(self):
         if self._list is None:
             h = self._env._host
-            self._list = [PersonView(i + 1, int(p[0]), int(p[1]), hv, int(f))
+            self._list = [PersonView(i + 1, int(p[0]), int(p[1]), hv, int(f), self._env)
                           for i, (p, hv, f) in enumerate(zip(h["pos"], h["health"], h["flags"]))]
         return self._list
 

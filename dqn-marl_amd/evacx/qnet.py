@@ -142,6 +142,24 @@ class FlatParams:
         for k, v in self.views.items():
             v.copy_(sd[k].to(v.device, torch.float32).view(v.shape))
 
+    def init_from_global_torch(self):
+        """The reference's own initialisation: each layer's nn.Conv2d / nn.Linear
+        reset_parameters (kaiming_uniform_(w, a=sqrt(5)), then bias ~ U(+-1/sqrt(fan_in)))
+        drawn from torch's global CPU generator in state_dict order, so after
+        torch.manual_seed(s) the weights and the generator's position equal a freshly built
+        reference DQNNetwork's (agents/dqn_agent.py:22-31)."""
+        import math
+        for k, v in self.views.items():
+            if k.endswith(".weight"):
+                w = torch.empty(self.shapes[k])
+                torch.nn.init.kaiming_uniform_(w, a=math.sqrt(5))
+                v.copy_(w)
+            else:
+                ws = self.shapes[k[:-5] + ".weight"]
+                fan_in = ws[1] * (ws[2] * ws[3] if len(ws) == 4 else 1)
+                bound = 1.0 / math.sqrt(fan_in) if fan_in > 0 else 0.0
+                v.copy_(torch.empty(self.shapes[k]).uniform_(-bound, bound))
+
     def init_like_torch(self, seed: int):
         """nn.Conv2d / nn.Linear default init (kaiming_uniform a=sqrt(5) -> U(+-1/sqrt(fan_in)))."""
         g = torch.Generator().manual_seed(seed)

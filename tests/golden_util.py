@@ -32,9 +32,9 @@ def digest(name, a):
 def traj_spec(name):
     """(layout fixture, P, LayoutSpec factory args) for each trajectory fixture."""
     from evacx import layout as lay
-    if name == "cfg1_single_traj":
+    if name in ("cfg1_single_traj", "cfg1_dropin_single"):
         return "cfg1_layout", 150, lay.reference_single()
-    if name == "cfg1_multi_traj":
+    if name in ("cfg1_multi_traj", "cfg1_dropin_multi"):
         return "cfg1_layout", 150, lay.reference_multi()
     if name == "g64_multi_traj":
         return "g64_layout", 569, lay.reference_scaled_multi(64, 64, 8)

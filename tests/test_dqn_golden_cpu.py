@@ -114,3 +114,34 @@ def test_closed_form_params_deterministic():
         bound = 1.0 / np.sqrt(726 if k.startswith("fc1") else 512 if k.startswith("fc2") else 256)
         assert np.abs(a[k]).max() <= bound
     assert not np.array_equal(a["fc1.weight"], closed_form_params(mlp_shapes(), salt=1)["fc1.weight"])
+
+
+def test_flat_params_init_follows_the_global_torch_stream():
+    """FlatParams.init_from_global_torch draws the reference DQNNetwork's initial weights
+    (nn.Conv2d / nn.Linear reset_parameters in module order, agents/dqn_agent.py:22-31) from
+    torch's global generator: same values and the same generator position afterwards."""
+    import torch
+    import torch.nn as nn
+
+    from collections import OrderedDict
+
+    from evacx.qnet import FlatParams, layer_specs, param_shapes
+
+    def reference_like(h):
+        return nn.ModuleDict(OrderedDict([
+            ("conv1", nn.Conv2d(6, 32, 3, padding=1)), ("conv2", nn.Conv2d(32, 64, 3, padding=1)),
+            ("conv3", nn.Conv2d(64, 128, 3, padding=1)), ("fc1", nn.Linear(11 * 11 * 128, h)),
+            ("fc2", nn.Linear(h, h // 2)), ("fc3", nn.Linear(h // 2, 5))]))
+
+    for h in (512, 32):
+        torch.manual_seed(77)
+        ref = reference_like(h).state_dict()
+        after_ref = torch.rand(4)
+        torch.manual_seed(77)
+        fp = FlatParams(param_shapes(layer_specs("conv", h, 5)), "cpu")
+        fp.init_from_global_torch()
+        after = torch.rand(4)
+        assert list(fp.views) == list(ref)
+        for k, v in ref.items():
+            assert torch.equal(fp[k], v), (h, k)
+        assert torch.equal(after, after_ref)

@@ -150,3 +150,104 @@ def test_train_dqn_loop_runs(tmp_path):
     assert os.path.exists(tmp_path / "res" / "dqn_model.pth")
     assert os.path.exists(tmp_path / "res" / "reward_logs" / "episode_data.csv")
     assert agent.steps > 0
+
+
+# action kinds of cfg1_dropin_*.npz (tools/capture_golden.py DROPIN_ACTIONS)
+def _dropin_action(code):
+    return {0: 0, 1: 1, 2: 2, 3: 3, 4: 4, 5: None, 6: 3.0, 7: np.float64(1), 8: True, 9: 7, 10: 2.5,
+            11: np.array(4)}[int(code)]
+
+
+def _traj_arrays(ppl):
+    kind, xy, step, health, flags = [], [], [], [], []
+    off = [0]
+    for p in ppl:
+        for e in p.trajectory:
+            xy.append(e["pos"])
+            if "step" in e:
+                kind.append(0); step.append(e["step"]); health.append(np.nan); flags.append(0)
+            else:
+                kind.append(1); step.append(-1); health.append(float(e["health"]))
+                flags.append((1 if e["savety"] else 0) | (2 if e["dead"] else 0))
+        off.append(len(kind))
+    return dict(traj_kind=np.array(kind, np.int8), traj_pos=np.array(xy, np.float64),
+                traj_step=np.array(step, np.int32), traj_health=np.array(health, np.float64),
+                traj_flags=np.array(flags, np.uint8), traj_off=np.array(off, np.int64))
+
+
+@pytest.mark.parametrize("traj", ["cfg1_dropin_single", "cfg1_dropin_multi"])
+def test_dropin_patrol_float_actions_gauss_and_person_trajectories(traj):
+    """Reference-captured run (tools/capture_golden.py dropin_extras): patrol mode (None,
+    envs/map.py:172-178), float / bool / 0-d array / out-of-range actions (map.py:180),
+    random.gauss draws between steps (the cached gauss_next survives), per-step robot
+    positions and state digests, and every person's trajectory list at the end of each
+    episode (people.py:52-59,306; evacuation_env.py:79-80,134-135)."""
+    _need_gpu()
+    from Louvre_Evacuation.envs.evacuation_env import EvacuationEnv
+    from Louvre_Evacuation.envs.evacuation_env_multi import EvacuationEnvMulti
+    _install_fixture_layout(traj)
+    tr = load(traj)
+    multi = traj.endswith("multi")
+    seed = 11 if multi else 10
+    random.seed(seed)
+    np.random.seed(seed)
+    env = (EvacuationEnvMulti if multi else EvacuationEnv)()
+    ep = 0
+    n = len(tr["reward"])
+    for k in range(n):
+        if tr["is_reset"][k]:
+            obs = env.reset()
+        else:
+            acts = [_dropin_action(c) for c in tr["codes"][k]]
+            obs, r, d, info = env.step(acts if multi else acts[0])
+            assert r == tr["reward"][k] and d == bool(tr["done"][k]), k
+        h = env._host
+        assert np.array_equal(np.array(env.map.robot_positions, np.int32), tr["robots"][k]), k
+        assert env.map.robot_position == list(tr["view"][k]), k
+        assert np.array_equal(digest("pos", h["pos"]), tr["dig_pos"][k]), k
+        assert np.array_equal(digest("health", h["health"]), tr["dig_health"][k]), k
+        ob = np.stack(obs) if multi else obs[None]
+        assert np.array_equal(digest("obs", ob), tr["dig_obs"][k]), k
+        g = tr["gauss"][k]
+        if not np.isnan(g):
+            assert random.gauss(0.0, 1.0) == g, k
+        last = k + 1 == n or tr["is_reset"][k + 1]
+        if last:
+            got = _traj_arrays(env.people.list)
+            for key, v in got.items():
+                assert np.array_equal(v, tr[f"ep{ep}_{key}"], equal_nan=v.dtype.kind == "f"), (ep, key)
+            ep += 1
+    py, nps = _global_rng()
+    assert np.array_equal(py, tr["rng_py_final"]) and np.array_equal(nps, tr["rng_np_final"])
+    rt = np.array([[*p, s] for p, s in env.robot_trajectory], np.float64)
+    assert np.array_equal(rt, tr["robot_traj"])
+
+
+def test_dropin_agent_initial_weights_follow_torch_manual_seed():
+    """After torch.manual_seed(s) the drop-in DQNAgent's initial q_network / target_network
+    weights equal a reference DQNNetwork's built under the same seed, and torch's global
+    generator stands where two reference networks leave it (agents/dqn_agent.py:83-84)."""
+    _need_gpu()
+    from collections import OrderedDict
+
+    import torch.nn as nn
+
+    from Louvre_Evacuation.agents.dqn_agent import DQNAgent
+
+    def net():
+        return nn.ModuleDict(OrderedDict([
+            ("conv1", nn.Conv2d(6, 32, 3, padding=1)), ("conv2", nn.Conv2d(32, 64, 3, padding=1)),
+            ("conv3", nn.Conv2d(64, 128, 3, padding=1)), ("fc1", nn.Linear(11 * 11 * 128, 512)),
+            ("fc2", nn.Linear(512, 256)), ("fc3", nn.Linear(256, 5))]))
+
+    torch.manual_seed(3)
+    q_ref = net().state_dict()
+    net()
+    after_ref = torch.rand(3)
+    torch.manual_seed(3)
+    agent = DQNAgent((11, 11, 6), 5, "cuda", {})
+    after = torch.rand(3)
+    assert torch.equal(after, after_ref)
+    for k, v in q_ref.items():
+        assert torch.equal(agent.q_network.state_dict()[k].cpu(), v), k
+        assert torch.equal(agent.target_network.state_dict()[k].cpu(), v), k

@@ -29,7 +29,7 @@ outputs are small ``.npz`` files under ``tests/golden/`` that pin
   fire steps (``g128_danger_digests.npz``).
 
 Usage:  PYTHONPATH=/root/reference PYTHONDONTWRITEBYTECODE=1 python tools/capture_golden.py [part ...]
-  parts: base (the round-1 fixtures), dqn, g128long, g128danger; default: all
+  parts: base (the round-1 fixtures), dqn, g128long, g128danger, dropin; default: all
 """
 import hashlib
 import os
@@ -488,9 +488,93 @@ def g128_danger():
                         danger_p_max=lay["danger_p"].max(axis=(1, 2)), danger_o_sum=lay["danger_o"].sum(axis=(1, 2)))
 
 
+def _traj_arrays(ppl):
+    """Person.trajectory lists flattened: kind 0 = {'pos','step'} entry, 1 = record_position
+    entry ({'pos','health','savety','dead'}); offsets per person."""
+    kind, xy, step, health, flags, off = [], [], [], [], [], [0]
+    for p in ppl:
+        for e in p.trajectory:
+            xy.append(e["pos"])
+            if "step" in e:
+                kind.append(0); step.append(e["step"]); health.append(np.nan); flags.append(0)
+            else:
+                kind.append(1); step.append(-1); health.append(float(e["health"]))
+                flags.append((1 if e["savety"] else 0) | (2 if e["dead"] else 0))
+        off.append(len(kind))
+    return dict(traj_kind=np.array(kind, np.int8), traj_pos=np.array(xy, np.float64),
+                traj_step=np.array(step, np.int32), traj_health=np.array(health, np.float64),
+                traj_flags=np.array(flags, np.uint8), traj_off=np.array(off, np.int64))
+
+
+# action kinds of the drop-in fixture: code -> the Python object handed to env.step
+DROPIN_ACTIONS = {0: 0, 1: 1, 2: 2, 3: 3, 4: 4, 5: None, 6: 3.0, 7: "f64_1", 8: True, 9: 7, 10: 2.5, 11: "arr_4"}
+
+
+def dropin_action(code):
+    v = DROPIN_ACTIONS[int(code)]
+    return np.float64(1) if v == "f64_1" else np.array(4) if v == "arr_4" else v
+
+
+def dropin_extras(multi, seed, episodes):
+    """EvacuationEnv / EvacuationEnvMulti driven with patrol (None), float, bool, 0-d array and
+    out-of-range actions (envs/map.py:172-197), random.gauss draws between steps (so the
+    cached gauss_next must survive env steps), per-step robot positions and digests, and every
+    person's trajectory at the end of each episode (envs/people.py:52-59,306,
+    envs/evacuation_env.py:79-80,134-135)."""
+    cfg1 = dict(width=36, height=30, fire_zones=None, exit_location=[36, 15], num_people=150)
+    random.seed(seed)
+    np.random.seed(seed)
+    env = EvacuationEnvMulti(**cfg1) if multi else EvacuationEnv(**cfg1)
+    R = 2 if multi else 1
+    arng = np.random.RandomState(500 + seed)
+    rec = {k: [] for k in ["codes", "reward", "done", "is_reset", "robots", "view", "gauss", "rng_py", "rng_np",
+                           "dig_pos", "dig_health", "dig_obs"]}
+    trajs = []
+    for ep in range(episodes):
+        py, npk = rng_states()
+        rec["rng_py"].append(py); rec["rng_np"].append(npk)
+        obs = env.reset()
+        codes = np.full(R, -1, np.int32)
+        r, done, k = 0.0, False, 0
+        while True:
+            st = env_state(env)
+            rec["codes"].append(codes); rec["reward"].append(np.float64(r)); rec["done"].append(bool(done))
+            rec["is_reset"].append(k == 0); rec["robots"].append(st["robots"]); rec["view"].append(st["view"])
+            rec["dig_pos"].append(digest("pos", st["pos"])); rec["dig_health"].append(digest("health", st["health"]))
+            rec["dig_obs"].append(digest("obs", np.array(obs, np.float64).reshape(-1, 11, 11, 6)))
+            # a gauss draw every 3rd step leaves a cached second variate in the stream
+            rec["gauss"].append(random.gauss(0.0, 1.0) if k % 3 == 1 else np.nan)
+            if done or k >= 400:
+                break
+            # the first step patrols every robot (sets map.robot_direction, envs/map.py:174-177)
+            codes = (np.full(R, 5, np.int32) if k == 0 else arng.choice(
+                [0, 1, 2, 3, 4, 5, 5, 5, 6, 7, 8, 9, 10, 11], size=R).astype(np.int32))
+            acts = [dropin_action(c) for c in codes]
+            if k > 0:
+                py, npk = rng_states()
+                rec["rng_py"].append(py); rec["rng_np"].append(npk)
+            obs, r, done, info = env.step(acts if multi else acts[0])
+            k += 1
+        rec["rng_py"].append(rng_states()[0]); rec["rng_np"].append(rng_states()[1])
+        trajs.append(_traj_arrays(env.people.list))
+    out = {k: np.array(v) for k, v in rec.items() if k not in ("rng_py", "rng_np")}
+    out["rng_py_final"], out["rng_np_final"] = rng_states()
+    for i, t in enumerate(trajs):
+        for k, v in t.items():
+            out[f"ep{i}_{k}"] = v
+    out["robot_traj"] = np.array([[*p, s] for p, s in env.robot_trajectory], np.float64)
+    return out
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
-    parts = sys.argv[1:] or ["base", "dqn", "g128long", "g128danger"]
+    parts = sys.argv[1:] or ["base", "dqn", "g128long", "g128danger", "dropin"]
+    if "dropin" in parts:
+        for multi, tag in [(False, "single"), (True, "multi")]:
+            print("drop-in extras", tag)
+            tr = dropin_extras(multi, seed=11 if multi else 10, episodes=2)
+            np.savez_compressed(os.path.join(OUT, f"cfg1_dropin_{tag}.npz"), **tr)
+            print("  steps", len(tr["reward"]))
     if "dqn" in parts:
         print("dqn fixtures")
         dqn_fixtures()
