@@ -161,7 +161,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from evacx.env import DeviceLayout
-    from evacx.layout import build_tables, synthetic
+    from evacx.layout import build_tables_device, synthetic
     from evacx.trainer import VecTrainer, make_allreduce_hook
 
     L = W = args.grid
@@ -171,11 +171,12 @@ def main():
     if args.layouts > 1:  # per-env layouts: env e runs random layout e % K
         from evacx.env import LayoutSet
         from evacx.layout import random_layout
-        lay_tables = [build_tables(random_layout(L, W, R, 4242 + k)) for k in range(args.layouts)]
+        # floor fields of all K layouts in one device launch
+        lay_tables = build_tables_device([random_layout(L, W, R, 4242 + k) for k in range(args.layouts)])
         lay = LayoutSet([DeviceLayout(t, P) for t in lay_tables])
         layout_of = [(rank * E + e) % args.layouts for e in range(E)]
     else:
-        lay_tables = [build_tables(spec)]
+        lay_tables = build_tables_device([spec])
         lay = DeviceLayout(lay_tables[0], P)
     hook = make_allreduce_hook(dist, world) if dist is not None else None
     tr = VecTrainer(lay, E, env_offset=rank * E, kind=args.qnet, precision=args.precision, batch=args.batch,

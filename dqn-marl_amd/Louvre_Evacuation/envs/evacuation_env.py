@@ -18,7 +18,7 @@ import numpy as np
 import torch
 
 from evacx.env import DeviceLayout, VecEnv, pack_xy
-from evacx.layout import FireSchedule, LayoutSpec, build_tables
+from evacx.layout import FireSchedule, LayoutSpec, build_tables_device
 
 from .map import MapView
 from .people import People, PeopleView
@@ -37,7 +37,8 @@ def device_layout(spec: LayoutSpec, P: int) -> DeviceLayout:
            tuple(spec.reset_view), P)
     lay = _LAYOUTS.get(key)
     if lay is None:
-        lay = DeviceLayout(build_tables(spec), P, device=_device())
+        dev = _device()
+        lay = DeviceLayout(build_tables_device([spec], device=dev)[0], P, device=dev)
         _LAYOUTS[key] = lay
     return lay
 

@@ -339,7 +339,9 @@ def potential_inputs(spec: LayoutSpec, danger0: Optional[np.ndarray] = None):
     return valid, src, pen
 
 
-def build_tables(spec: LayoutSpec, t_max: Optional[int] = None) -> LayoutTables:
+def build_tables(spec: LayoutSpec, t_max: Optional[int] = None, floor: Optional[np.ndarray] = None) -> LayoutTables:
+    """The layout's static tables. ``floor``: the floor field computed elsewhere (the device
+    kernel, ``build_tables_device``); default: the reference's heapq Init_Potential on the host."""
     L, W = spec.L, spec.W
     GX, GY = L + 2, W + 2
     inf = float("inf")
@@ -353,27 +355,32 @@ def build_tables(spec: LayoutSpec, t_max: Optional[int] = None) -> LayoutTables:
                          spec.base_radius, spec.max_radius, spec.min_danger)
     ofire = FireSchedule(spec.env_fire(), spec.additional_fire, spec.fire_max_steps,
                          spec.base_radius, spec.max_radius, spec.min_danger)
-    # Init_Potential (envs/map.py:127-148)
-    mind = np.full((GX, GY), inf)
-    heap = []
-    mind[ex][ey] = 1
-    heapq.heappush(heap, (1, ex, ey))
-    while heap:
-        cd, x, y = heapq.heappop(heap)
-        for i in range(8):
-            nx, ny = x + MOVE_DX[i], y + MOVE_DY[i]
-            cost = 1.0 if i < 4 else 1.4
-            if check_valid(space, nx, ny):
-                nd = cd + cost
-                if nd < mind[nx][ny]:
-                    mind[nx][ny] = nd
-                    heapq.heappush(heap, (nd, nx, ny))
-    for i in range(GX):
-        for j in range(GY):
-            if mind[i][j] != inf:
-                danger = pfire.danger_scalar(0, (i, j))
-                mind[i][j] += 200 * (danger ** 2)
-    floor = mind
+    if floor is None:
+        # Init_Potential (envs/map.py:127-148)
+        mind = np.full((GX, GY), inf)
+        heap = []
+        mind[ex][ey] = 1
+        heapq.heappush(heap, (1, ex, ey))
+        while heap:
+            cd, x, y = heapq.heappop(heap)
+            for i in range(8):
+                nx, ny = x + MOVE_DX[i], y + MOVE_DY[i]
+                cost = 1.0 if i < 4 else 1.4
+                if check_valid(space, nx, ny):
+                    nd = cd + cost
+                    if nd < mind[nx][ny]:
+                        mind[nx][ny] = nd
+                        heapq.heappush(heap, (nd, nx, ny))
+        for i in range(GX):
+            for j in range(GY):
+                if mind[i][j] != inf:
+                    danger = pfire.danger_scalar(0, (i, j))
+                    mind[i][j] += 200 * (danger ** 2)
+        floor = mind
+    else:
+        floor = np.asarray(floor, np.float64)
+        if floor.shape != (GX, GY):
+            raise ValueError(f"floor must be [{GX}, {GY}]")
     valid = np.zeros((GX, GY), np.uint8)
     exitm = np.zeros((GX, GY), np.uint8)
     barr = np.zeros((GX, GY), np.uint8)
@@ -395,3 +402,14 @@ def build_tables(spec: LayoutSpec, t_max: Optional[int] = None) -> LayoutTables:
     do = np.stack([ofire.danger_grid(t, oxs, oys) for t in range(T + 1)])
     return LayoutTables(spec=spec, floor=floor, valid=valid, exit_mask=exitm, barrier=barr,
                         danger_p=dp, danger_o=do, obs_origin=(ox0, oy0))
+
+
+def build_tables_device(specs: Sequence[LayoutSpec], t_max: Optional[int] = None, device="cuda") -> List[LayoutTables]:
+    """build_tables for several layouts of one grid size with every floor field computed by
+    the device kernel in one launch (evacx.floor.floor_fields_for, csrc/floor.hip):
+    the same float64 fields as the reference's heapq Init_Potential (tests/test_floor_gpu.py).
+    The danger tables stay on the host: they go through numpy's exp (fire_model.py:183)."""
+    from .floor import floor_fields_for
+    fields, _ = floor_fields_for(list(specs), device=device)
+    fl = fields.cpu().numpy()
+    return [build_tables(s, t_max, floor=fl[i]) for i, s in enumerate(specs)]

@@ -251,3 +251,67 @@ def test_dropin_agent_initial_weights_follow_torch_manual_seed():
     for k, v in q_ref.items():
         assert torch.equal(agent.q_network.state_dict()[k].cpu(), v), k
         assert torch.equal(agent.target_network.state_dict()[k].cpu(), v), k
+
+
+def test_dropin_agent_loads_a_reference_checkpoint(tmp_path):
+    """A checkpoint written by the reference's own DQNAgent.save after two learn steps
+    (tools/capture_golden.py ref_checkpoint: DQNNetwork at hidden_size 2, gzip'd byte for
+    byte) loads into the drop-in DQNAgent: parameters, target, Adam moments and step,
+    epsilon and steps as stored, and the eval-mode Q-values equal the reference's (f32
+    MFMA conv path, rtol 1e-4). The drop-in's own save has the reference file's layout."""
+    _need_gpu()
+    import gzip
+
+    from Louvre_Evacuation.agents.dqn_agent import DQNAgent
+    here = os.path.join(os.path.dirname(__file__), "golden")
+    path = tmp_path / "ref.pt"
+    path.write_bytes(gzip.open(os.path.join(here, "ref_ckpt_h2.pt.gz"), "rb").read())
+    ref = torch.load(path, map_location="cpu", weights_only=True)
+    q = np.load(os.path.join(here, "ref_ckpt_h2_q.npz"))
+    agent = DQNAgent((11, 11, 6), 5, "cuda", {"hidden_size": 2})
+    agent.load(str(path))
+    assert agent.epsilon == ref["epsilon"] == float(q["epsilon"]) and agent.steps == ref["steps"] == int(q["steps"])
+    for k, v in ref["q_network"].items():
+        assert torch.equal(agent.q_network.state_dict()[k].cpu(), v), k
+        assert torch.equal(agent.target_network.state_dict()[k].cpu(), ref["target_network"][k]), k
+    opt = agent.optimizer.state_dict()
+    for i, st in ref["optimizer"]["state"].items():
+        assert torch.equal(opt["state"][i]["exp_avg"], st["exp_avg"]), i
+        assert torch.equal(opt["state"][i]["exp_avg_sq"], st["exp_avg_sq"]), i
+        assert float(opt["state"][i]["step"]) == float(st["step"])
+    agent.q_network.eval()
+    got = agent.q_network(torch.from_numpy(q["obs"])).cpu().numpy()
+    np.testing.assert_allclose(got, q["q_eval"], rtol=1e-4, atol=1e-4 * np.abs(q["q_eval"]).max())
+    out = tmp_path / "ours.pt"
+    agent.save(str(out))
+    mine = torch.load(out, map_location="cpu", weights_only=True)
+    assert set(mine) == set(ref)
+    assert list(mine["q_network"]) == list(ref["q_network"])
+    assert set(mine["optimizer"]) == set(ref["optimizer"])
+    assert set(mine["optimizer"]["state"]) == set(ref["optimizer"]["state"])
+    assert set(mine["optimizer"]["param_groups"][0]) >= {"lr", "betas", "eps", "weight_decay", "params"}
+
+
+def test_evaluate_strategies_runs_a_build_checkpoint(tmp_path):
+    """runners/evaluate_strategies (reference runners/evaluate_strategies.py:34-110): a
+    checkpoint the drop-in DQNAgent saved goes through build_dqn_policy, and evaluate runs
+    the no-robot, static-robot and DQN policies to the end of an episode."""
+    _need_gpu()
+    from Louvre_Evacuation.agents.dqn_agent import DQNAgent
+    from Louvre_Evacuation.runners import evaluate_strategies as ev
+    random.seed(4)
+    np.random.seed(4)
+    torch.manual_seed(4)
+    cfg = {"env": {"num_people": 150}}
+    env_sample = ev.build_env_from_config(cfg)
+    agent = DQNAgent(env_sample.state_size, env_sample.action_size, "cuda", {"epsilon": 0.3})
+    path = tmp_path / "best_model.pth"
+    agent.save(str(path))
+    pol = ev.build_dqn_policy(str(path), torch.device("cuda"), env_sample)
+    for fn in (ev.no_robot_policy, ev.static_robot_policy, pol):
+        r = ev.evaluate(lambda: ev.build_env_from_config(cfg), fn, 1)
+        m = r["records"][0]
+        assert m["evacuated"] + m["dead"] + m["remaining"] == 150
+        assert m["total_steps"] > 0 and np.isfinite(r["avg_time"])
+    a = pol(env_sample.reset(), env_sample)
+    assert int(a) in range(5)

@@ -65,3 +65,17 @@ def test_floor_field_no_exit_and_no_pen():
     f = floor_fields(torch.from_numpy(valid).cuda(), torch.from_numpy(src).cuda()).cpu().numpy()
     assert np.isinf(f[0]).all()
     assert np.array_equal(f[1], orc.floor_field(valid[1], src[1]))
+
+
+def test_build_tables_device_equals_host_build():
+    """The product path's layout tables (build_tables_device: every floor field from the device
+    kernel in one launch) equal the host heapq build, field for field, on the bench's
+    synthetic 128x128 layout and on random per-env layouts."""
+    _need_gpu()
+    import evacx.layout as lay
+    specs = [lay.synthetic(128, 128, 16)] + [lay.random_layout(128, 128, 16, 4242 + k) for k in range(3)]
+    dev = lay.build_tables_device(specs, t_max=8)
+    for s, td in zip(specs, dev):
+        th = lay.build_tables(s, t_max=8)
+        for f in ("floor", "valid", "exit_mask", "barrier", "danger_p", "danger_o"):
+            assert np.array_equal(getattr(td, f), getattr(th, f)), f

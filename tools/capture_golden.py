@@ -29,7 +29,7 @@ outputs are small ``.npz`` files under ``tests/golden/`` that pin
   fire steps (``g128_danger_digests.npz``).
 
 Usage:  PYTHONPATH=/root/reference PYTHONDONTWRITEBYTECODE=1 python tools/capture_golden.py [part ...]
-  parts: base (the round-1 fixtures), dqn, g128long, g128danger, dropin; default: all
+  parts: base (the round-1 fixtures), dqn, g128long, g128danger, dropin, ckpt; default: all
 """
 import hashlib
 import os
@@ -566,9 +566,53 @@ def dropin_extras(multi, seed, episodes):
     return out
 
 
+def ref_checkpoint():
+    """A checkpoint written by the reference's own DQNAgent.save (agents/dqn_agent.py:174-182)
+    after two DQNAgent.learn steps, so the optimizer state holds Adam moments. The network is
+    the reference's DQNNetwork at hidden_size 2 (the constructor default patched in this
+    process only) so the fixture stays ~2 MB; its eval-mode Q-values on 8 reference
+    observations are recorded beside it. The file is committed gzip'd byte for byte."""
+    import gzip
+    import torch
+    from Louvre_Evacuation.agents import dqn_agent as ref_agent
+
+    torch.set_num_threads(8)
+    init = ref_agent.DQNNetwork.__init__
+    init.__defaults__ = (2,)
+    try:
+        random.seed(21)
+        np.random.seed(21)
+        torch.manual_seed(21)
+        agent = ref_agent.DQNAgent((11, 11, 6), 5, torch.device("cpu"),
+                                   {"batch_size": 8, "warmup_steps": 0, "epsilon": 0.5, "memory_size": 100})
+        obs, _ = reference_observations(24, seed=31)
+        obs = obs.astype(np.float32)
+        for i in range(16):
+            agent.remember(obs[i], i % 5, float(i) * 0.25 - 1.0, obs[i + 1], i % 7 == 6)
+        losses = [agent.learn() for _ in range(2)]
+        path = os.path.join(OUT, "ref_ckpt_h2.pt")
+        agent.save(path)
+        raw = open(path, "rb").read()
+        os.remove(path)
+        with gzip.open(path + ".gz", "wb", compresslevel=9) as f:
+            f.write(raw)
+        agent.q_network.eval()
+        with torch.no_grad():
+            q = agent.q_network(torch.from_numpy(obs[16:24])).numpy()
+        np.savez_compressed(os.path.join(OUT, "ref_ckpt_h2_q.npz"), obs=obs[16:24], q_eval=q,
+                            losses=np.array(losses, np.float64), epsilon=np.float64(agent.epsilon),
+                            steps=np.int64(agent.steps))
+        print("  checkpoint bytes", len(raw), "losses", losses)
+    finally:
+        init.__defaults__ = (512,)
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
-    parts = sys.argv[1:] or ["base", "dqn", "g128long", "g128danger", "dropin"]
+    parts = sys.argv[1:] or ["base", "dqn", "g128long", "g128danger", "dropin", "ckpt"]
+    if "ckpt" in parts:
+        print("reference checkpoint")
+        ref_checkpoint()
     if "dropin" in parts:
         for multi, tag in [(False, "single"), (True, "multi")]:
             print("drop-in extras", tag)
