@@ -1796,7 +1796,9 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     const int nrem = P - evac - dead;
     int* ltab = reinterpret_cast<int*>(aux);  // leaf offsets | lengths
     double* leafsum = reinterpret_cast<double*>(pyring);
-    double* lb = leafsum + LEAF_CAP;          // current leaf's elements (<= 128 + 64)
+    // the remaining persons' robot distances, in list order, go to the move-plan scratch
+    // (P doubles; the plan is dead once executed); the numpy leaves are summed after the pass
+    double* dist = reinterpret_cast<double*>(plan);
     int nleaf = 0;
     if (lane == 0 && nrem > 0)
         nleaf = np_pairwise_leaves(nrem, ltab, ltab + LEAF_CAP, LEAF_CAP, reinterpret_cast<int*>(misc));
@@ -1808,7 +1810,7 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     wave_fence();
     const int vx = rp_x(view), vy = rp_y(view);
     double gq_t = 0.0;
-    int q = 0, lb_base = 0, cur = 0;
+    int q = 0;
     // remaining persons = the not-dead list minus this step's deaths and evacuations
     auto reward_half = [&](int i, uint32_t v, double hv) {
         PT_BEGIN(rew);
@@ -1825,59 +1827,9 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
             if (hv < 80) gq_t += 1.0;
         }
         const unsigned long long rm = __ballot(rem);
-        if (rem) lb[q + lanes_below(rm) - lb_base] = 0.5 * sqrt((double)n4);
+        if (rem) dist[q + lanes_below(rm)] = 0.5 * sqrt((double)n4);
         q += __popcll(rm);
-        wave_fence();
         PT_END(rew);
-        PT_BEGIN(leaf);
-        // numpy pairwise leaves that are now complete
-        while (cur < nleaf && q >= ltab[cur] + ltab[LEAF_CAP + cur]) {
-            const int len = ltab[LEAF_CAP + cur], o = ltab[cur] - lb_base;
-            const int len8 = len - (len % 8);
-            double r = 0.0;
-            if (len >= 8 && lane < 8) {  // chain `lane`: a[lane] + a[lane+8] + ..., all 16 reads in flight
-                double a[16];
-#pragma unroll
-                for (int k = 0; k < 16; k++) {
-                    a[k] = 0.0;  // padding: d + 0.0 == d for the non-negative distances
-                    if (8 * k < len8) a[k] = lb[o + 8 * k + lane];
-                }
-                r = a[0];
-#pragma unroll
-                for (int k = 1; k < 16; k++) r += a[k];
-            }
-            if (len >= 8) {
-                const double r0 = readlane_d(r, 0), r1 = readlane_d(r, 1), r2 = readlane_d(r, 2),
-                             r3 = readlane_d(r, 3), r4 = readlane_d(r, 4), r5 = readlane_d(r, 5),
-                             r6 = readlane_d(r, 6), r7 = readlane_d(r, 7);
-                r = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
-            }
-            if (lane == 0) {
-                int k = len8;
-                if (len < 8) {
-                    r = 0.0;
-                    k = 0;
-                }
-                for (; k < len; k++) r += lb[o + k];
-                leafsum[cur] = r;
-            }
-            cur++;
-        }
-        const int nb = cur < nleaf ? ltab[cur] : q;
-        if (nb > lb_base) {  // drop consumed elements: keep [nb, q) at the buffer start
-            const int keep = q - nb, sh = nb - lb_base;
-            double t0 = 0.0, t1 = 0.0, t2 = 0.0;
-            if (lane < keep) t0 = lb[sh + lane];
-            if (lane + 64 < keep) t1 = lb[sh + lane + 64];
-            if (lane + 128 < keep) t2 = lb[sh + lane + 128];
-            wave_fence();
-            if (lane < keep) lb[lane] = t0;
-            if (lane + 64 < keep) lb[lane + 64] = t1;
-            if (lane + 128 < keep) lb[lane + 128] = t2;
-            lb_base = nb;
-        }
-        wave_fence();
-        PT_END(leaf);
     };
     auto load_idx = [&](int i) -> uint32_t {
         uint32_t p = 0u;
@@ -1937,6 +1889,40 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
         }
         PT_END(rtop);
     }
+    PT_BEGIN(leaf);
+    wave_sync();  // the distances are visible to every lane
+    // numpy's pairwise leaves (<= 128 elements), 8 at a time: lane = 8 * leaf + chain j;
+    // chain j sums a[j], a[j + 8], ... (numpy's r[j]), the 8 chains meet as
+    // ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)) by xor-shuffles, and the leaf's
+    // chain-0 lane adds the len % 8 tail in order (or sums a short leaf from 0.0)
+    for (int l0 = 0; l0 < nleaf; l0 += 8) {
+        const int li = l0 + (lane >> 3), j = lane & 7;
+        int o = 0, len = 0;
+        if (li < nleaf) {
+            o = ltab[li];
+            len = ltab[LEAF_CAP + li];
+        }
+        const int len8 = len >= 8 ? len - (len % 8) : 0;
+        double a[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            a[k] = 0.0;  // padding: d + 0.0 == d for the non-negative distances
+            if (8 * k < len8) a[k] = dist[o + 8 * k + j];
+        }
+        double r = a[0];
+#pragma unroll
+        for (int k = 1; k < 16; k++) r += a[k];
+        r += __shfl_xor(r, 1, 64);
+        r += __shfl_xor(r, 2, 64);
+        r += __shfl_xor(r, 4, 64);
+        if (j == 0 && li < nleaf) {
+            double res = len >= 8 ? r : 0.0;
+            for (int k = len8; k < len; k++) res += dist[o + k];
+            leafsum[li] = res;
+        }
+    }
+    wave_fence();
+    PT_END(leaf);
     const double gq = wave_sum_d(gq_t);  // multiples of 0.5: exact in any order
     PT_STORE(np, 16);
     PT_STORE(hsum, 17);

@@ -90,6 +90,12 @@ def _p(t):
     return None if t is None else t.data_ptr()
 
 
+def _need(what, t, n, per_row):
+    """Host-side bounds check before a launch: a kernel indexing past a caller's buffer faults the GPU."""
+    if t is not None and t.numel() < n * per_row:
+        raise ValueError(f"qmlp {what}: {t.numel()} elements, needs {n} x {per_row}")
+
+
 class MLPFast:
     """bf16 operand copies of one MLP parameter set (evacx.qnet.FlatParams) + forward.
     x3=True: the f32-accurate mode (hi + lo operand pairs; evx_qmlp_pack3)."""
@@ -167,6 +173,8 @@ class MLPFast:
     def forward(self, lay_c, obs: torch.Tensor, n: int, h1: torch.Tensor, drop=None, x=None, h2=None, q=None,
                 actions=None, epsilon=0.0, act_seed=0, act_offset=0):
         """obs: compact observations (int32 words, 8 per row). drop: (seed, stream, p) or None."""
+        _need("forward obs", obs, n, 8)
+        _need("forward q", q, n, NACT)
         d = self._drop(drop) if drop else None
         o = evx_qmlp_fwd_out(h1=_p(h1), x=_p(x), h2=_p(h2), q=_p(q), actions=_p(actions), epsilon=float(epsilon),
                              act_seed=act_seed, act_offset=act_offset)
@@ -178,6 +186,9 @@ class MLPFast:
     def act(self, lay_c, obs: torch.Tensor, n: int, drop=None, q=None, actions=None, epsilon=0.0, act_seed=0,
             act_offset=0):
         """DQNAgent.act in one launch (evx_qmlp_act): Q values and/or epsilon-greedy actions."""
+        _need("act obs", obs, n, 8)
+        _need("act q", q, n, NACT)
+        _need("act actions", actions, n, 1)
         d = self._drop(drop) if drop else None
         o = evx_qmlp_fwd_out(q=_p(q), actions=_p(actions), epsilon=float(epsilon), act_seed=act_seed,
                              act_offset=act_offset)
@@ -201,6 +212,10 @@ class MLPFast:
     @staticmethod
     def forward_pair(lay_c, n, net0, obs0, drop0, out0: dict, net1, obs1, drop1, out1: dict):
         """Two forwards (e.g. online and target) in one launch pair; out*: h1, x, h2, q tensors."""
+        _need("forward_pair obs0", obs0, n, 8)
+        _need("forward_pair obs1", obs1, n, 8)
+        for o in (out0, out1):
+            _need("forward_pair q", o.get("q"), n, NACT)
         d0, d1 = MLPFast._drop(drop0), MLPFast._drop(drop1)
         o0, o1 = MLPFast._out(**out0), MLPFast._out(**out1)
         mcheck(mlib().evx_qmlp_forward2(C.byref(lay_c), n, obs0.data_ptr(), C.byref(net0.c), C.byref(d0), C.byref(o0),

@@ -366,6 +366,9 @@ class Learner:
         later). mask_online / mask_target: explicit uint8 [B][512] dropout keep masks (tests:
         the reference's captured torch masks) in place of the hash."""
         from .qmlp import HID, HID2
+        for name, t in (("s_obs", s_obs), ("s2_obs", s2_obs)):  # evx_obs rows are 8 words
+            if t.numel() < B * 8:
+                raise ValueError(f"learn_obs: {name} holds {t.numel() // 8} observations, B = {B}")
         ws, dev = self.net.ws, self.device
         pl, kx = self.fast.planes, self.fast.kx
         X = ws.get("fx", (B * kx,), torch.int16, dev)
