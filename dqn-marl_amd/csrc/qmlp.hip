@@ -30,6 +30,7 @@
 // lo residual (k = 512 + c), which multiplies the danger column's hi weight. Split
 // activations (H1, dZ2, dZ1) are stored as two bf16 planes [2][rows][cols].
 #include <hip/hip_runtime.h>
+#include <math.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -977,12 +978,14 @@ __global__ __launch_bounds__(256) void qbwd3_kernel(Bwd a) {
 
 // dZ1 = (dZ2 W2) * scale * [H1 > 0]: 64 rows x 128 columns per workgroup (4 waves x
 // 32 columns), K = 256 in chunks of 32; dZ2 staged through LDS, W2^T operand-tiled.
+template <bool X3>
+constexpr int qdz1_lds_bytes() { return 2 * (X3 ? 2 : 1) * RM * 40 * 2; }
 template <bool X3 = false>
-__global__ __launch_bounds__(256, 2) void qdz1_kernel(Bwd a) {
+__device__ __forceinline__ void qdz1_body(const Bwd& a, char* smem, int bx, int by) {
     constexpr int NPL = X3 ? 2 : 1;
-    __shared__ __attribute__((aligned(16))) __bf16 As[2][NPL][RM][40];  // pitch 20 words: conflict-free b128 reads
+    auto As = reinterpret_cast<__bf16 (*)[NPL][RM][40]>(smem);  // [2][NPL][RM][40], pitch 20 words: conflict-free b128 reads
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
-    const int m0 = blockIdx.x * RM, n0 = blockIdx.y * 128 + w * 32;
+    const int m0 = bx * RM, n0 = by * 128 + w * 32;
     const int gr = tid >> 2, go = (tid & 3) * 8;
     const bool rowok = m0 + gr < a.B;
     f32x16 acc[2];
@@ -1067,11 +1070,16 @@ __global__ __launch_bounds__(256, 2) void qdz1_kernel(Bwd a) {
         atomicAdd(&a.gw1[(size_t)col * K1 + CENTRE_COL], cs);  // d/dW1 of the constant centre input
     }
 }
+template <bool X3 = false>
+__global__ __launch_bounds__(256, 2) void qdz1_kernel(Bwd a) {
+    __shared__ __attribute__((aligned(16))) char smem[qdz1_lds_bytes<X3>()];
+    qdz1_body<X3>(a, smem, blockIdx.x, blockIdx.y);
+}
 
 // C[m][n] += sum_k A[k][m] B[k][n] (both operands K-major bf16), 128x128 tiles of
 // 4 waves (2x2 of 64x64), K chunks of 32 staged transposed in LDS; gridDim.z splits
 // K. part == NULL: the partial tiles are added to C with f32 atomics; else split z
-// stores its tile to part[z][m][0, gridDim.x * TT) and gemm_reduce_kernel adds the
+// stores its tile to part[z][m][0, gridDim.x * TT) and reduce2_kernel adds the
 // splits in z order (deterministic, and no atomic traffic through L2). Columns
 // n >= Nc are skipped; remap: column n goes to ref_col(n) (fc1's compact K -> the
 // reference's 726).
@@ -1101,23 +1109,40 @@ __device__ __forceinline__ void tr8x8(const uint4 (&in)[8], uint4 (&out)[8]) {
     }
 }
 // AP / BP: planes of A / B (2 = X3 hi + lo at Al / Bl: products hi*hi + hi*lo + lo*hi).
+// one weight-gradient GEMM of the backward (gemm_tn_kernel's arguments; grid = (N tiles, M tiles, splits))
+struct GemmTN {
+    const __bf16* A;
+    int lda;
+    const __bf16* Bm;
+    int ldb, K, M, Nc, kper;
+    float* C;
+    int ldc, remap;
+    float* part;
+    const __bf16 *Al, *Bl;
+    int gx, gy, gz;  // grid
+};
+template <int AP, int BP>
+constexpr int gemm_tn_lds_bytes() { return (AP + BP) * TT * TPAD * 2; }
 template <int AP = 1, int BP = 1>
-__global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const __bf16* __restrict__ A, int lda,
-                                                         const __bf16* __restrict__ Bm, int ldb, int K, int M, int Nc,
-                                                         int kper, float* __restrict__ C, int ldc, int remap,
-                                                         float* __restrict__ part, const __bf16* __restrict__ Al = nullptr,
-                                                         const __bf16* __restrict__ Bl = nullptr) {
+__device__ __forceinline__ void gemm_tn_body(const GemmTN& g, char* smem, int bx, int by, int bz) {
     // K chunks of 64 staged [m][k] in LDS: thread b < 128 of each operand loads an 8 (k) x 8 (m)
     // block (8 x 16-B row segments, whole cache lines per wave), transposes it in registers
     // and writes 8 x 16 B (8 consecutive k of one m): ds_write_b128, conflict-free; the MFMA
     // operand reads (ds_read_b128, pitch 36 words) are conflict-free too.
     constexpr int NP = AP > BP ? AP : BP;
-    __shared__ __attribute__((aligned(16))) __bf16 As[AP][TT][TPAD];
-    __shared__ __attribute__((aligned(16))) __bf16 Bs[BP][TT][TPAD];
+    auto As = reinterpret_cast<__bf16 (*)[TT][TPAD]>(smem);                       // [AP][TT][TPAD]
+    auto Bs = reinterpret_cast<__bf16 (*)[TT][TPAD]>(smem + AP * TT * TPAD * 2);  // [BP][TT][TPAD]
+    const __bf16* __restrict__ A = g.A;
+    const __bf16* __restrict__ Bm = g.Bm;
+    const __bf16* __restrict__ Al = g.Al;
+    const __bf16* __restrict__ Bl = g.Bl;
+    const int lda = g.lda, ldb = g.ldb, K = g.K, M = g.M, Nc = g.Nc, kper = g.kper, ldc = g.ldc, remap = g.remap;
+    float* __restrict__ C = g.C;
+    float* __restrict__ part = g.part;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
     const int wm = w >> 1, wn = w & 1;
-    const int m0 = blockIdx.y * TT, n0 = blockIdx.x * TT;
-    const int kb0 = blockIdx.z * kper, ke = min(K, kb0 + kper);
+    const int m0 = by * TT, n0 = bx * TT;
+    const int kb0 = bz * kper, ke = min(K, kb0 + kper);
     f32x16 acc[2][2];
 #pragma unroll
     for (int i = 0; i < 2; i++)
@@ -1186,8 +1211,8 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const __bf16* __restric
         __syncthreads();
     }
     if (part) {
-        const int Np = (int)gridDim.x * TT;
-        float* pz = part + (size_t)blockIdx.z * M * Np;
+        const int Np = g.gx * TT;
+        float* pz = part + (size_t)bz * M * Np;
 #pragma unroll
         for (int j = 0; j < 2; j++) {
             const int n = n0 + wn * 64 + j * 32 + (lane & 31);
@@ -1216,34 +1241,203 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const __bf16* __restric
             }
     }
 }
+template <int AP = 1, int BP = 1>
+__global__ __launch_bounds__(256, 2) void gemm_tn_kernel(GemmTN g) {
+    __shared__ __attribute__((aligned(16))) char smem[gemm_tn_lds_bytes<AP, BP>()];
+    gemm_tn_body<AP, BP>(g, smem, blockIdx.x, blockIdx.y, blockIdx.z);
+}
+// dZ1 (qdz1) and dW2 = dZ2^T H1 (gemm_tn) in one launch: both need only qbwd3's outputs. Blocks
+// [0, ndz) run qdz1 tiles (grid ndzx x HID / 128), the rest the dW2 split-K tiles; the LDS is one
+// dynamic buffer sized for the larger of the two.
+template <bool X3, int AP, int BP>
+__global__ __launch_bounds__(256, 2) void bwd_mid_kernel(Bwd a, int ndzx, GemmTN g) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int b = (int)blockIdx.x, ndz = ndzx * (HID / 128);
+    if (b < ndz) {
+        qdz1_body<X3>(a, smem, b % ndzx, b / ndzx);
+    } else {
+        const int t = b - ndz, gxy = g.gx * g.gy;
+        gemm_tn_body<AP, BP>(g, smem, t % g.gx, (t % gxy) / g.gx, t / gxy);
+    }
+}
 
-// C[m][remap(n)] += sum over z = 0.. S-1 (in order) of part[z][m][n], 4 columns per thread
-__global__ __launch_bounds__(256) void gemm_reduce_kernel(const float* __restrict__ part, int S, int M, int Np, int Nc,
-                                                          float* __restrict__ C, int ldc, int remap) {
-    const int q = (int)(blockIdx.x * 256 + threadIdx.x), nq = Nc >> 2;
-    if (q >= M * nq) return;
-    const int m = q / nq, n = (q - m * nq) * 4;
-    const float* src = part + (size_t)m * Np + n;
-    float4 acc = *reinterpret_cast<const float4*>(src);
-    for (int z = 1; z < S; z++) {
-        const float4 v = *reinterpret_cast<const float4*>(src + (size_t)z * M * Np);
-        acc.x += v.x;
-        acc.y += v.y;
-        acc.z += v.z;
-        acc.w += v.w;
+// Both split-K reductions of the backward (dW2 then dW1) in one launch, each workgroup also
+// leaving the sum of squares of the final gradient values it produced (clip_grad_norm_'s
+// partials; fixed order). The last workgroup adds the squares of the small gradients the
+// other kernels finished (b1, the centre column of W1, b2, W3, b3); W1's channel-0 and
+// non-centre channel-5 columns stay zero.
+constexpr int NPAR = HID * K1 + HID + HID2 * HID + HID2 + NACT * HID2 + NACT;
+constexpr int OB1 = HID * K1, OW2 = OB1 + HID, OB2 = OW2 + HID2 * HID, OW3 = OB2 + HID2, OB3 = OW3 + NACT * HID2;
+struct Red2 {
+    const float* part2;  // dW2 partials [S2][HID2][HID]
+    int S2;
+    const float* part1;  // dW1 partials [S1][HID][Np1]
+    int S1, Np1, Nc1, remap1;
+    float *gw1, *gb1, *gw2, *gb2, *gw3, *gb3;  // gradients
+    float* ss;           // [gridDim.x] squared-norm partials, or NULL
+    int nb2, nb1;        // workgroups of the two reductions
+};
+__device__ __forceinline__ float red_sum256(float x, float* red) {
+    red[threadIdx.x] = x;
+    __syncthreads();
+    for (int k = 128; k > 0; k >>= 1) {
+        if ((int)threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+        __syncthreads();
     }
-    float a4[4] = {acc.x, acc.y, acc.z, acc.w};
-    if (remap == 3) {  // X3 dW1: cell n / 4's danger residual column (512 + n / 4) into its danger column
-        const float* s2 = part + (size_t)m * Np + K1P + (n >> 2);
-        float d = s2[0];
-        for (int z = 1; z < S; z++) d += s2[(size_t)z * M * Np];
-        a4[1] += d;
-    }
+    return red[0];
+}
+__global__ __launch_bounds__(256) void reduce2_kernel(Red2 r) {
+    __shared__ float red[256];
+    const int b = (int)blockIdx.x;
+    float sq = 0.f;
+    if (b < r.nb2) {  // dW2: 4 columns per thread
+        const int q = b * 256 + (int)threadIdx.x, nq = HID >> 2;
+        if (q < HID2 * nq) {
+            const int m = q / nq, n = (q - m * nq) * 4;
+            const float* src = r.part2 + (size_t)m * HID + n;
+            float4 acc = *reinterpret_cast<const float4*>(src);
+            for (int z = 1; z < r.S2; z++) {
+                const float4 v = *reinterpret_cast<const float4*>(src + (size_t)z * HID2 * HID);
+                acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+            }
+            float* dst = r.gw2 + (size_t)m * HID + n;
+            const float4 old = *reinterpret_cast<const float4*>(dst);
+            const float4 o = make_float4(old.x + acc.x, old.y + acc.y, old.z + acc.z, old.w + acc.w);
+            *reinterpret_cast<float4*>(dst) = o;
+            sq = o.x * o.x + o.y * o.y + o.z * o.z + o.w * o.w;
+        }
+    } else if (b < r.nb2 + r.nb1) {  // dW1: 4 compact columns (one cell) per thread
+        const int q = (b - r.nb2) * 256 + (int)threadIdx.x, nq = r.Nc1 >> 2;
+        if (q < HID * nq) {
+            const int m = q / nq, n = (q - m * nq) * 4;
+            const size_t zs = (size_t)HID * r.Np1;
+            const float* src = r.part1 + (size_t)m * r.Np1 + n;
+            float4 acc = *reinterpret_cast<const float4*>(src);
+            for (int z = 1; z < r.S1; z++) {
+                const float4 v = *reinterpret_cast<const float4*>(src + (size_t)z * zs);
+                acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+            }
+            float a4[4] = {acc.x, acc.y, acc.z, acc.w};
+            if (r.remap1 == 3) {  // X3: cell n / 4's danger residual column (512 + n / 4) into its danger column
+                const float* s2 = r.part1 + (size_t)m * r.Np1 + K1P + (n >> 2);
+                float d = s2[0];
+                for (int z = 1; z < r.S1; z++) d += s2[(size_t)z * zs];
+                a4[1] += d;
+            }
 #pragma unroll
-    for (int t = 0; t < 4; t++) {
-        const int nc = remap ? ref_col(n + t) : n + t;
-        C[(size_t)m * ldc + nc] += a4[t];
+            for (int t = 0; t < 4; t++) {
+                float* dst = r.gw1 + (size_t)m * K1 + ref_col(n + t);
+                const float o = *dst + a4[t];
+                *dst = o;
+                sq += o * o;
+            }
+        }
+    } else {  // the small gradients, complete before this launch
+        for (int i = (int)threadIdx.x; i < HID; i += 256) {
+            const float v = r.gb1[i], c = r.gw1[(size_t)i * K1 + CENTRE_COL];
+            sq += v * v + c * c;
+        }
+        for (int i = (int)threadIdx.x; i < HID2; i += 256) sq += r.gb2[i] * r.gb2[i];
+        for (int i = (int)threadIdx.x; i < NACT * HID2; i += 256) sq += r.gw3[i] * r.gw3[i];
+        if ((int)threadIdx.x < NACT) sq += r.gb3[threadIdx.x] * r.gb3[threadIdx.x];
     }
+    const float t = red_sum256(sq, red);
+    if (threadIdx.x == 0 && r.ss) r.ss[b] = t;
+}
+
+// clip_grad_norm_ + torch.optim.Adam (agents/dqn_agent.py:158-160) with the x3 operand
+// repack (evx_qmlp_pack3) in one launch, from reduce2_kernel's squared-norm partials: every
+// workgroup sums the same partials in the same order (the same norm everywhere), then each
+// thread updates one parameter and writes its bf16 hi / lo copies straight into the MFMA
+// operand tiles (the inverse of pack3's destination -> source map). The thread of b1[n]
+// also owns W1[n][centre] (b1c = b1 + W1[:, centre] needs both updated values).
+struct AdamPack {
+    float *p, *g, *m, *v;
+    const float* ss;
+    int nss;
+    float max_norm, beta1, beta2, eps, step_size, bc2_sqrt, weight_decay;
+    __bf16 *w1b, *w1l, *w2b, *w2l, *w2t, *w2tl;
+    float* b1c;
+    float* norm_out;
+};
+// element (column col, contraction index k) of an operand in w1_tile / w2_tile / w2t_tile order
+__device__ __forceinline__ size_t opnd_off(size_t tile, int col, int k) {
+    return tile + (size_t)(((col & 31) + 32 * ((k >> 3) & 1)) * 8 + (k & 7));
+}
+__device__ __forceinline__ float adam_one(const AdamPack& a, int i, float coef) {
+    float gi = a.g[i] * coef;
+    const float p = a.p[i];
+    if (a.weight_decay != 0.f) gi += a.weight_decay * p;
+    const float mi = a.m[i] + (gi - a.m[i]) * (1.f - a.beta1);
+    const float vi = a.v[i] * a.beta2 + (1.f - a.beta2) * gi * gi;
+    a.m[i] = mi;
+    a.v[i] = vi;
+    a.g[i] = gi;
+    const float denom = sqrtf(vi) / a.bc2_sqrt + a.eps;
+    const float pn = p - a.step_size * (mi / denom);
+    a.p[i] = pn;
+    return pn;
+}
+__global__ __launch_bounds__(256) void adam_pack3_kernel(AdamPack a) {
+    __shared__ float red[256];
+    float t = 0.f;
+    for (int k = (int)threadIdx.x; k < a.nss; k += 256) t += a.ss[k];
+    const float norm = sqrtf(red_sum256(t, red));
+    float coef = 1.f;
+    if (a.max_norm > 0.f) {
+        coef = a.max_norm / (norm + 1e-6f);
+        coef = coef < 1.f ? coef : 1.f;
+    }
+    const int i = (int)blockIdx.x * 256 + (int)threadIdx.x;
+    if (i == 0 && a.norm_out) a.norm_out[0] = norm;
+    if (i >= NPAR) return;
+    if (i < OB1) {  // fc1.weight [512][726]: live columns of channels 1-4 -> compact k = 4c + ch - 1
+        const int n = i / K1, rc = i - n * K1;
+        if (rc == CENTRE_COL) return;  // updated by the b1[n] thread
+        const float pn = adam_one(a, i, coef);
+        const int c = rc / 6, ch = rc - c * 6;
+        if (ch >= 1 && ch <= 4) {
+            const int kk = 4 * c + ch - 1;
+            __bf16 hi, lo;
+            split2(pn, hi, lo);
+            a.w1b[opnd_off(w1_tile(n >> 5, kk >> 5, (kk >> 4) & 1, NKC1X), n, kk)] = hi;
+            a.w1l[opnd_off(w1_tile(n >> 5, kk >> 5, (kk >> 4) & 1, NKC1), n, kk)] = lo;
+            if (ch == 2) {  // the danger column's hi also meets the residual slot 512 + c
+                const int kr = K1P + c;
+                a.w1b[opnd_off(w1_tile(n >> 5, kr >> 5, (kr >> 4) & 1, NKC1X), n, kr)] = hi;
+            }
+        }
+    } else if (i < OW2) {  // fc1.bias and W1[:, centre]: b1c = b1 + W1[:, centre]
+        const int n = i - OB1;
+        const float bn = adam_one(a, i, coef);
+        const float wc = adam_one(a, n * K1 + CENTRE_COL, coef);
+        a.b1c[n] = bn + wc;
+    } else if (i < OB2) {  // fc2.weight [256][512]: W2 (cols = outputs) and W2^T (cols = inputs)
+        const float pn = adam_one(a, i, coef);
+        const int j = i - OW2, n = j / HID, kk = j - n * HID;
+        __bf16 hi, lo;
+        split2(pn, hi, lo);
+        const size_t o2 = opnd_off(w2_tile(n >> 5, kk >> 5, (kk >> 4) & 1), n, kk);
+        a.w2b[o2] = hi;
+        a.w2l[o2] = lo;
+        if (a.w2t) {
+            const size_t ot = opnd_off(w2t_tile(kk >> 5, n >> 5, (n >> 4) & 1), kk, n);
+            a.w2t[ot] = hi;
+            a.w2tl[ot] = lo;
+        }
+    } else {
+        adam_one(a, i, coef);
+    }
+}
+
+// squared-norm partials of the flat gradient buffer (one per workgroup) for adam_pack3_kernel
+// when the gradients changed after the backward (the multi-GPU all-reduce)
+__global__ __launch_bounds__(256) void sumsq_parts_kernel(const float* __restrict__ g, float* __restrict__ ss) {
+    __shared__ float red[256];
+    float sq = 0.f;
+    for (int i = (int)blockIdx.x * 256 + (int)threadIdx.x; i < NPAR; i += (int)gridDim.x * 256) sq += g[i] * g[i];
+    const float t = red_sum256(sq, red);
+    if (threadIdx.x == 0) ss[blockIdx.x] = t;
 }
 
 struct Zero6 {
@@ -1476,20 +1670,72 @@ static int ksplit_kper(int B, int tiles) {
     return (kper + evxm::TKC - 1) / evxm::TKC * evxm::TKC;
 }
 
+// split-K partials: dW2's region, then dW1's (both stay live until reduce2_kernel)
+static int64_t part2_floats(int32_t B) {
+    const int64_t s2 = (B + ksplit_kper(B, 8) - 1) / ksplit_kper(B, 8);
+    return s2 * evxm::HID2 * evxm::HID;
+}
 int64_t evx_qmlp_backward_part_floats(int32_t B) {
     if (B <= 0) return 0;
-    const int64_t s2 = (B + ksplit_kper(B, 8) - 1) / ksplit_kper(B, 8);
     const int64_t s1 = std::max((B + ksplit_kper(B, 24) - 1) / ksplit_kper(B, 24),
                                 (B + ksplit_kper(B, 20) - 1) / ksplit_kper(B, 20));  // bf16 / x3 dW1 splits
-    return std::max(s2 * evxm::HID2 * evxm::HID, s1 * evxm::HID * evxm::K1X);  // K1X: the x3 dW1 width
+    return part2_floats(B) + s1 * evxm::HID * evxm::K1X;  // K1X: the x3 dW1 width
 }
 
-int evx_qmlp_backward(const evx_qmlp_params* p, int32_t B, const float* dq, const uint16_t* x, const uint16_t* h1,
-                      const float* h2, float drop_p, uint16_t* dz2, uint16_t* dz1, const evx_qmlp_grads* g,
-                      int32_t zero_grads, void* stream) {
+// workgroups of reduce2_kernel = squared-norm partials the backward leaves for evx_qmlp_adam_pack3
+static int norm_parts() { return (evxm::HID2 * evxm::HID / 4 + 255) / 256 + (evxm::HID * evxm::NCELL + 255) / 256 + 1; }
+int32_t evx_qmlp_norm_parts(void) { return norm_parts(); }
+int64_t evx_qmlp_nparams(void) { return evxm::NPAR; }
+
+extern "C++" {
+template <bool X3, int AP2, int BP2, int AP1, int BP1>
+static void launch_tail(const evxm::Bwd& a, int32_t B, const evx_qmlp_grads* g, float* ss, hipStream_t st) {
+    // dW2 = dZ2^T H1 (256 x 512); dW1 = dZ1^T X (512 x compact K -> 726); K = B split into S tiles
+    evxm::GemmTN g2{a.dz2, evxm::HID2, a.h1, evxm::HID, B, evxm::HID2, evxm::HID, ksplit_kper(B, 8), g->w2, evxm::HID, 0,
+                    g->part, X3 ? a.dz2l : nullptr, X3 ? a.h1l : nullptr, evxm::HID / evxm::TT, evxm::HID2 / evxm::TT, 0};
+    g2.gz = (B + g2.kper - 1) / g2.kper;
+    const int KX = X3 ? evxm::K1X : evxm::K1P;
+    evxm::GemmTN g1{a.dz1, evxm::HID, a.x, KX, B, evxm::HID, X3 ? evxm::K1X : 4 * evxm::NCELL,
+                    ksplit_kper(B, X3 ? 20 : 24), g->w1, evxm::K1, X3 ? 3 : 1, g->part ? g->part + part2_floats(B) : nullptr,
+                    X3 ? a.dz1l : nullptr, nullptr, KX / evxm::TT, evxm::HID / evxm::TT, 0};
+    g1.gz = (B + g1.kper - 1) / g1.kper;
+    const int ndzx = (B + evxm::RM - 1) / evxm::RM;
+    if (g->part) {
+        // qdz1 and the dW2 tiles in one launch (both read only qbwd3's outputs), then the dW1
+        // tiles, then both reductions + the squared-norm partials in one launch
+        constexpr int lds = std::max(evxm::qdz1_lds_bytes<X3>(), evxm::gemm_tn_lds_bytes<AP2, BP2>());
+        static bool attr = false;
+        if (!attr) {
+            (void)hipFuncSetAttribute((const void*)evxm::bwd_mid_kernel<X3, AP2, BP2>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+            attr = true;
+        }
+        const unsigned nmid = (unsigned)(ndzx * (evxm::HID / 128) + g2.gx * g2.gy * g2.gz);
+        hipLaunchKernelGGL((evxm::bwd_mid_kernel<X3, AP2, BP2>), dim3(nmid), dim3(256), lds, st, a, ndzx, g2);
+        hipLaunchKernelGGL((evxm::gemm_tn_kernel<AP1, BP1>), dim3(g1.gx, g1.gy, g1.gz), dim3(256), 0, st, g1);
+        evxm::Red2 r{g->part, g2.gz, g1.part, g1.gz, g1.gx * evxm::TT, 4 * evxm::NCELL, X3 ? 3 : 1,
+                     g->w1, g->b1, g->w2, g->b2, g->w3, g->b3, ss,
+                     (evxm::HID2 * evxm::HID / 4 + 255) / 256, (evxm::HID * evxm::NCELL + 255) / 256};
+        hipLaunchKernelGGL(evxm::reduce2_kernel, dim3((unsigned)norm_parts()), dim3(256), 0, st, r);
+        return;
+    }
+    // f32 atomics into the gradients (no partials)
+    hipLaunchKernelGGL(evxm::qdz1_kernel<X3>, dim3((unsigned)ndzx, evxm::HID / 128), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((evxm::gemm_tn_kernel<AP2, BP2>), dim3(g2.gx, g2.gy, g2.gz), dim3(256), 0, st, g2);
+    hipLaunchKernelGGL((evxm::gemm_tn_kernel<AP1, BP1>), dim3(g1.gx, g1.gy, g1.gz), dim3(256), 0, st, g1);
+    if (ss) hipLaunchKernelGGL(evxm::sumsq_parts_kernel, dim3((unsigned)norm_parts()), dim3(256), 0, st, g->w1, ss);
+}
+}  // extern "C++"
+
+static int qmlp_backward(const evx_qmlp_params* p, int32_t B, const float* dq, const uint16_t* x, const uint16_t* h1,
+                         const float* h2, float drop_p, uint16_t* dz2, uint16_t* dz1, const evx_qmlp_grads* g,
+                         int32_t zero_grads, float* ss, void* stream) {
     if (!p || !g || !dq || !x || !h1 || !h2 || !dz2 || !dz1) return mfail(-22, "qmlp_backward: NULL argument");
     if (!p->w2t || !p->w3) return mfail(-22, "qmlp_backward: w2t / w3 required");
     if (!g->w1 || !g->b1 || !g->w2 || !g->b2 || !g->w3 || !g->b3) return mfail(-22, "qmlp_backward: missing grad");
+    if (ss && (g->b1 != g->w1 + evxm::OB1 || g->w2 != g->w1 + evxm::OW2 || g->b2 != g->w1 + evxm::OB2 ||
+               g->w3 != g->w1 + evxm::OW3 || g->b3 != g->w1 + evxm::OB3))
+        return mfail(-22, "qmlp_backward: norm partials need the gradients as one flat state_dict-order buffer");
     if (B <= 0) return 0;
     hipStream_t st = (hipStream_t)stream;
     if (zero_grads) {
@@ -1515,6 +1761,9 @@ int evx_qmlp_backward(const evx_qmlp_params* p, int32_t B, const float* dq, cons
     a.gb2 = g->b2;
     a.gw3 = g->w3;
     a.gb3 = g->b3;
+    a.h1l = nullptr;
+    a.w2tl = nullptr;
+    a.dz2l = a.dz1l = nullptr;
     if (p->x3) {
         if (!p->w2tl) return mfail(-22, "qmlp_backward: x3 needs w2tl (evx_qmlp_pack3)");
         a.h1l = a.h1 + (size_t)B * evxm::HID;  // lo planes after the hi planes
@@ -1522,52 +1771,58 @@ int evx_qmlp_backward(const evx_qmlp_params* p, int32_t B, const float* dq, cons
         a.dz2l = a.dz2 + (size_t)B * evxm::HID2;
         a.dz1l = a.dz1 + (size_t)B * evxm::HID;
         hipLaunchKernelGGL(evxm::qbwd3_kernel<true>, dim3((unsigned)((B + evxm::R3 - 1) / evxm::R3)), dim3(256), 0, st, a);
-        hipLaunchKernelGGL(evxm::qdz1_kernel<true>, dim3((unsigned)((B + evxm::RM - 1) / evxm::RM), evxm::HID / 128),
-                           dim3(256), 0, st, a);
-        {  // dW2 = dZ2^T H1: both operands split
-            const int kper = ksplit_kper(B, 8), S = (B + kper - 1) / kper;
-            hipLaunchKernelGGL((evxm::gemm_tn_kernel<2, 2>), dim3(evxm::HID / evxm::TT, evxm::HID2 / evxm::TT, S),
-                               dim3(256), 0, st, a.dz2, evxm::HID2, a.h1, evxm::HID, B, evxm::HID2, evxm::HID, kper,
-                               g->w2, evxm::HID, 0, g->part, a.dz2l, a.h1l);
-            if (g->part)
-                hipLaunchKernelGGL(evxm::gemm_reduce_kernel, dim3((evxm::HID2 * evxm::HID / 4 + 255) / 256), dim3(256),
-                                   0, st, g->part, S, evxm::HID2, evxm::HID, evxm::HID, g->w2, evxm::HID, 0);
-        }
-        {  // dW1 = dZ1^T X over the 640 x3 columns (X exact in bf16): the danger residual column of a
-           // cell adds into its danger column
-            const int kper = ksplit_kper(B, 20), S = (B + kper - 1) / kper;
-            hipLaunchKernelGGL((evxm::gemm_tn_kernel<2, 1>), dim3(evxm::K1X / evxm::TT, evxm::HID / evxm::TT, S),
-                               dim3(256), 0, st, a.dz1, evxm::HID, a.x, evxm::K1X, B, evxm::HID, evxm::K1X, kper, g->w1,
-                               evxm::K1, 3, g->part, a.dz1l, nullptr);
-            if (g->part)
-                hipLaunchKernelGGL(evxm::gemm_reduce_kernel, dim3((evxm::HID * evxm::NCELL + 255) / 256), dim3(256), 0,
-                                   st, g->part, S, evxm::HID, evxm::K1X, 4 * evxm::NCELL, g->w1, evxm::K1, 3);
-        }
+        // dW2: both operands split; dW1 over the 640 x3 columns (X exact in bf16): the danger
+        // residual column of a cell adds into its danger column
+        launch_tail<true, 2, 2, 2, 1>(a, B, g, ss, st);
         return mlaunch("qmlp_backward");
     }
     hipLaunchKernelGGL(evxm::qbwd3_kernel<false>, dim3((unsigned)((B + evxm::R3 - 1) / evxm::R3)), dim3(256), 0, st, a);
-    hipLaunchKernelGGL(evxm::qdz1_kernel<false>, dim3((unsigned)((B + evxm::RM - 1) / evxm::RM), evxm::HID / 128), dim3(256),
-                       0, st, a);
-    // dW2 = dZ2^T H1 (256 x 512), dW1 = dZ1^T X (512 x 484 compact -> 726); K = B split over gridDim.z
-    {
-        const int kper = ksplit_kper(B, 8), S = (B + kper - 1) / kper;
-        hipLaunchKernelGGL((evxm::gemm_tn_kernel<1, 1>), dim3(evxm::HID / evxm::TT, evxm::HID2 / evxm::TT, S), dim3(256), 0, st,
-                           a.dz2, evxm::HID2, a.h1, evxm::HID, B, evxm::HID2, evxm::HID, kper, g->w2, evxm::HID, 0,
-                           g->part);
-        if (g->part)
-            hipLaunchKernelGGL(evxm::gemm_reduce_kernel, dim3((evxm::HID2 * evxm::HID / 4 + 255) / 256), dim3(256), 0, st,
-                               g->part, S, evxm::HID2, evxm::HID, evxm::HID, g->w2, evxm::HID, 0);
-    }
-    {
-        const int kper = ksplit_kper(B, 24), S = (B + kper - 1) / kper;
-        hipLaunchKernelGGL((evxm::gemm_tn_kernel<1, 1>), dim3(evxm::K1P / evxm::TT, evxm::HID / evxm::TT, S), dim3(256), 0, st,
-                           a.dz1, evxm::HID, a.x, evxm::K1P, B, evxm::HID, 4 * evxm::NCELL, kper, g->w1, evxm::K1, 1,
-                           g->part);
-        if (g->part)
-            hipLaunchKernelGGL(evxm::gemm_reduce_kernel, dim3((evxm::HID * evxm::NCELL + 255) / 256), dim3(256), 0, st,
-                               g->part, S, evxm::HID, evxm::K1P, 4 * evxm::NCELL, g->w1, evxm::K1, 1);
-    }
+    launch_tail<false, 1, 1, 1, 1>(a, B, g, ss, st);
     return mlaunch("qmlp_backward");
+}
+
+int evx_qmlp_backward(const evx_qmlp_params* p, int32_t B, const float* dq, const uint16_t* x, const uint16_t* h1,
+                      const float* h2, float drop_p, uint16_t* dz2, uint16_t* dz1, const evx_qmlp_grads* g,
+                      int32_t zero_grads, void* stream) {
+    return qmlp_backward(p, B, dq, x, h1, h2, drop_p, dz2, dz1, g, zero_grads, nullptr, stream);
+}
+
+int evx_qmlp_backward_ss(const evx_qmlp_params* p, int32_t B, const float* dq, const uint16_t* x, const uint16_t* h1,
+                         const float* h2, float drop_p, uint16_t* dz2, uint16_t* dz1, const evx_qmlp_grads* g,
+                         int32_t zero_grads, float* ss, void* stream) {
+    if (!ss) return mfail(-22, "qmlp_backward_ss: NULL ss");
+    return qmlp_backward(p, B, dq, x, h1, h2, drop_p, dz2, dz1, g, zero_grads, ss, stream);
+}
+
+int evx_qmlp_sumsq_parts(const float* g, float* ss, void* stream) {
+    if (!g || !ss) return mfail(-22, "qmlp_sumsq_parts: NULL argument");
+    hipLaunchKernelGGL(evxm::sumsq_parts_kernel, dim3((unsigned)norm_parts()), dim3(256), 0, (hipStream_t)stream, g, ss);
+    return mlaunch("qmlp_sumsq_parts");
+}
+
+int evx_qmlp_adam_pack3(float* p, float* g, float* m, float* v, float max_norm, const evx_adam* h, uint16_t* w1b,
+                        uint16_t* w1l, float* b1c, uint16_t* w2b, uint16_t* w2l, uint16_t* w2t, uint16_t* w2tl,
+                        const float* ss, int32_t nss, float* norm_out, void* stream) {
+    if (!p || !g || !m || !v || !h || !w1b || !w1l || !b1c || !w2b || !w2l || !ss)
+        return mfail(-22, "qmlp_adam_pack3: NULL argument");
+    if ((w2t == nullptr) != (w2tl == nullptr)) return mfail(-22, "qmlp_adam_pack3: w2t and w2tl go together");
+    if (nss <= 0) return mfail(-22, "qmlp_adam_pack3: no norm partials");
+    evxm::AdamPack a;
+    a.p = p; a.g = g; a.m = m; a.v = v;
+    a.ss = ss; a.nss = nss;
+    const double bc1 = 1.0 - pow((double)h->beta1, (double)h->step);
+    const double bc2 = 1.0 - pow((double)h->beta2, (double)h->step);
+    a.max_norm = max_norm; a.beta1 = h->beta1; a.beta2 = h->beta2; a.eps = h->eps;
+    a.step_size = (float)(h->lr / bc1);
+    a.bc2_sqrt = (float)sqrt(bc2);
+    a.weight_decay = h->weight_decay;
+    a.w1b = reinterpret_cast<__bf16*>(w1b); a.w1l = reinterpret_cast<__bf16*>(w1l);
+    a.w2b = reinterpret_cast<__bf16*>(w2b); a.w2l = reinterpret_cast<__bf16*>(w2l);
+    a.w2t = reinterpret_cast<__bf16*>(w2t); a.w2tl = reinterpret_cast<__bf16*>(w2tl);
+    a.b1c = b1c; a.norm_out = norm_out;
+    hipLaunchKernelGGL(evxm::adam_pack3_kernel, dim3((unsigned)((evxm::NPAR + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, a);
+    return mlaunch("qmlp_adam_pack3");
 }
 
 }  // extern "C"

@@ -12,6 +12,7 @@
 // a k-ordered fmaf chain, used where parity with torch fp32 matters) or bf16 inputs
 // with f32 accumulation (v_mfma_f32_32x32x16_bf16, the throughput path).
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -277,9 +278,16 @@ __global__ __launch_bounds__(256) void td_loss_kernel(const float* __restrict__ 
                                                       const float* __restrict__ rew, const uint8_t* __restrict__ done,
                                                       float gamma, int B, const float* __restrict__ w,
                                                       float* __restrict__ dQ, float* __restrict__ loss_out,
-                                                      float* __restrict__ td_abs) {
+                                                      float* __restrict__ td_abs, int ntd = 0,
+                                                      float* __restrict__ zero = nullptr, int64_t nzero = 0) {
     __shared__ float red[256];
     __shared__ bool last;
+    if (zero && (int)blockIdx.x >= ntd) {  // the extra workgroups clear the gradient buffer for the backward
+        const int64_t z0 = ((int64_t)blockIdx.x - ntd) * 256 + threadIdx.x, zs = ((int64_t)gridDim.x - ntd) * 256;
+        for (int64_t k = z0; k < nzero; k += zs) zero[k] = 0.f;
+        return;
+    }
+    const unsigned nb = zero ? (unsigned)ntd : gridDim.x;
     const int i = blockIdx.x * 256 + threadIdx.x;
     float part = 0.f;
     if (i < B) {
@@ -304,13 +312,13 @@ __global__ __launch_bounds__(256) void td_loss_kernel(const float* __restrict__ 
     if (threadIdx.x == 0) {
         g_td_part[blockIdx.x] = red[0];
         __threadfence();
-        last = atomicAdd(&g_td_ticket, 1u) == gridDim.x - 1;
+        last = atomicAdd(&g_td_ticket, 1u) == nb - 1;
     }
     __syncthreads();
     if (last && threadIdx.x == 0) {
         __threadfence();
         float t = 0.f;
-        for (unsigned k = 0; k < gridDim.x; k++) t += __hip_atomic_load(&g_td_part[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (unsigned k = 0; k < nb; k++) t += __hip_atomic_load(&g_td_part[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         loss_out[0] = t / (float)B;
         g_td_ticket = 0;
     }
@@ -586,6 +594,19 @@ int evx_td_loss_w(const float* Q, const float* Qt, int32_t A, const int32_t* act
     hipLaunchKernelGGL(evxq::td_loss_kernel, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream, Q, Qt, A, act, rew, done,
                        gamma, B, w, dQ, loss, td_abs);
     return qlaunch("td_loss");
+}
+
+int evx_td_loss_zero(const float* Q, const float* Qt, int32_t A, const int32_t* act, const float* rew,
+                     const uint8_t* done, float gamma, int32_t B, const float* w, float* dQ, float* loss, float* td_abs,
+                     float* zero, int64_t nzero, void* stream) {
+    if (B <= 0) return 0;
+    if (B > 4096 * 256) return qfail(-22, "td_loss: batch too large");
+    if (!zero || nzero <= 0) return evx_td_loss_w(Q, Qt, A, act, rew, done, gamma, B, w, dQ, loss, td_abs, stream);
+    const int ntd = (B + 255) / 256;
+    const int nz = (int)std::min<int64_t>((nzero + 256 * 16 - 1) / (256 * 16), 512);
+    hipLaunchKernelGGL(evxq::td_loss_kernel, dim3(ntd + nz), dim3(256), 0, (hipStream_t)stream, Q, Qt, A, act, rew, done,
+                       gamma, B, w, dQ, loss, td_abs, ntd, zero, nzero);
+    return qlaunch("td_loss_zero");
 }
 
 int evx_td_loss(const float* Q, const float* Qt, int32_t A, const int32_t* act, const float* rew, const uint8_t* done,

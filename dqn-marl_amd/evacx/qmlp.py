@@ -72,6 +72,14 @@ def mlib():
                                         C.POINTER(evx_qmlp_dropout), C.POINTER(evx_qmlp_fwd_out), C.c_void_p,
                                         C.POINTER(evx_qmlp_params), C.POINTER(evx_qmlp_dropout),
                                         C.POINTER(evx_qmlp_fwd_out), C.c_void_p]
+        L.evx_qmlp_backward_ss.argtypes = [C.POINTER(evx_qmlp_params), C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                           C.c_void_p, C.c_float, C.c_void_p, C.c_void_p, C.POINTER(evx_qmlp_grads),
+                                           C.c_int32, C.c_void_p, C.c_void_p]
+        L.evx_qmlp_norm_parts.restype = C.c_int32
+        L.evx_qmlp_nparams.restype = C.c_int64
+        L.evx_qmlp_sumsq_parts.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        L.evx_qmlp_adam_pack3.argtypes = [C.c_void_p] * 4 + [C.c_float, C.c_void_p] + [C.c_void_p] * 8 + \
+            [C.c_int32, C.c_void_p, C.c_void_p]
         L.evx_qmlp_backward_part_floats.restype = C.c_int64
         L.evx_qmlp_backward_part_floats.argtypes = [C.c_int32]
         L.evx_qmlp_backward.argtypes = [C.POINTER(evx_qmlp_params), C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
@@ -142,6 +150,23 @@ class MLPFast:
                "qmlp_pack")
         if self._static is not None:
             self._rebuild_static()
+
+    def adam_step(self, p, g, m, v, max_norm: float, hyper, ss, norm_out=None):
+        """clip_grad_norm_ (from the squared-norm partials ss) + Adam on the flat buffers and this
+        network's x3 operand repack, one launch (evx_qmlp_adam_pack3); hyper: evacx.qnet.evx_adam."""
+        if not self.x3:
+            raise ValueError("adam_step: the fused repack writes the x3 operand layout")
+        mcheck(mlib().evx_qmlp_adam_pack3(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), float(max_norm),
+                                          C.byref(hyper), self.w1b.data_ptr(), self.w1l.data_ptr(),
+                                          self.b1c.data_ptr(), self.w2b.data_ptr(), self.w2l.data_ptr(),
+                                          self.w2t.data_ptr(), self.w2tl.data_ptr(), ss.data_ptr(),
+                                          int(mlib().evx_qmlp_norm_parts()), _p(norm_out), _stream()),
+               "qmlp_adam_pack3")
+
+    @staticmethod
+    def sumsq_parts(g, ss):
+        """The squared-norm partials of a flat gradient buffer (evx_qmlp_sumsq_parts)."""
+        mcheck(mlib().evx_qmlp_sumsq_parts(g.data_ptr(), ss.data_ptr(), _stream()), "qmlp_sumsq_parts")
 
     def attach_static(self, lay_c, L: int, W: int, t_max: int):
         """Enable act()'s fast path for observations at fire step >= t_max (the fire has
@@ -223,10 +248,11 @@ class MLPFast:
                "qmlp_forward2")
 
     def backward(self, B: int, dq: torch.Tensor, x: torch.Tensor, h1: torch.Tensor, h2: torch.Tensor, drop_p: float,
-                 dz2: torch.Tensor, dz1: torch.Tensor, grads, zero=True):
+                 dz2: torch.Tensor, dz1: torch.Tensor, grads, zero=True, ss: Optional[torch.Tensor] = None):
         """d loss / d params of the saved forward into `grads` (evacx.qnet.FlatParams).
         Buffer sizes are checked here, before anything is launched: x [B][kx], h1 / dz1
-        [planes][B][512], dz2 [planes][B][256]."""
+        [planes][B][512], dz2 [planes][B][256]. ss: f32 [>= evx_qmlp_norm_parts()] receives
+        clip_grad_norm_'s squared-norm partials of the final gradients (evx_qmlp_backward_ss)."""
         pl = self.planes
         for name, t, n in [("x", x, B * self.kx), ("h1", h1, pl * B * HID), ("dz1", dz1, pl * B * HID),
                            ("dz2", dz2, pl * B * HID2), ("h2", h2, B * HID2), ("dq", dq, B * NACT)]:
@@ -239,6 +265,12 @@ class MLPFast:
             if self._part is None or self._part.numel() < nf:
                 self._part = torch.empty(nf, dtype=torch.float32, device=self.device)
             g.part = self._part.data_ptr()
+        if ss is not None:
+            _need("backward ss", ss, 1, int(mlib().evx_qmlp_norm_parts()))
+            mcheck(mlib().evx_qmlp_backward_ss(C.byref(self.c), B, dq.data_ptr(), x.data_ptr(), h1.data_ptr(),
+                                               h2.data_ptr(), float(drop_p), dz2.data_ptr(), dz1.data_ptr(), C.byref(g),
+                                               int(zero), ss.data_ptr(), _stream()), "qmlp_backward_ss")
+            return
         mcheck(mlib().evx_qmlp_backward(C.byref(self.c), B, dq.data_ptr(), x.data_ptr(), h1.data_ptr(), h2.data_ptr(),
                                         float(drop_p), dz2.data_ptr(), dz1.data_ptr(), C.byref(g), int(zero),
                                         _stream()), "qmlp_backward")

@@ -16,6 +16,7 @@ gradient all-reduce is one collective. Every contraction runs in evx_gemm
 from __future__ import annotations
 
 import ctypes as C
+import os
 from collections import OrderedDict
 from typing import Dict, List, Optional, Tuple
 
@@ -60,6 +61,9 @@ def qlib():
         L.evx_td_loss_w.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
                                     C.c_float, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                     C.c_void_p]
+        L.evx_td_loss_zero.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                       C.c_float, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                       C.c_void_p, C.c_int64, C.c_void_p]
         L.evx_sumsq_norm.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
         L.evx_clip_adam.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p,
                                     C.c_float, C.POINTER(evx_adam), C.c_void_p]
@@ -322,6 +326,15 @@ class Learner:
             self.fast = MLPFast(self.online, self.device, x3=precision == "f32")
             self.fast_t = MLPFast(self.target, self.device, x3=precision == "f32")
         self.drop_stream = 0
+        # x3 MLP: TD + gradient clear in one launch, the norm partials out of the backward's
+        # reductions, clip + Adam + operand repack in one launch (EVX_FUSED_OPT=0: the separate
+        # td_loss / zero / sumsq / clip_adam / pack3 launches)
+        self.fused_opt = self.fast is not None and self.fast.x3 and os.environ.get("EVX_FUSED_OPT", "1") != "0"
+        if self.fused_opt:
+            from .qmlp import mlib
+            assert self.online.numel == int(mlib().evx_qmlp_nparams()), "MLP parameter count"
+        self._ss = torch.zeros(1024, dtype=torch.float32, device=self.device)
+        self._ss_fresh = False
 
     # ------------------------------------------------------------ dropout
     def dropout_mask(self, B, tag="m"):
@@ -386,9 +399,20 @@ class Learner:
         type(self.fast).forward_pair(lay_c, B, self.fast, s_obs, d_on, dict(h1=H1, x=X, h2=H2, q=Q), self.fast_t,
                                      s2_obs, d_tg, dict(h1=H1t, q=Qt))
         L = qlib()
-        qcheck(L.evx_td_loss_w(_p(Q), _p(Qt), self.actions, _p(a), _p(r), _p(done), self.gamma, B, _p(weights),
-                               _p(dQ), _p(self.loss), _p(td_abs), _stream()), "td_loss")
-        self.fast.backward(B, dQ, X, H1, H2, DROPOUT_P, dz2, dz1, self.grads)
+        if self.fused_opt:
+            # the TD launch also clears the gradients; the backward leaves the norm partials
+            # (its weight-gradient reductions compute them) unless an all-reduce will change the gradients
+            g = self.grads.flat
+            qcheck(L.evx_td_loss_zero(_p(Q), _p(Qt), self.actions, _p(a), _p(r), _p(done), self.gamma, B,
+                                      _p(weights), _p(dQ), _p(self.loss), _p(td_abs), _p(g), g.numel(), _stream()),
+                   "td_loss_zero")
+            self.fast.backward(B, dQ, X, H1, H2, DROPOUT_P, dz2, dz1, self.grads, zero=False,
+                               ss=self._ss if self.grad_hook is None else None)
+            self._ss_fresh = self.grad_hook is None
+        else:
+            qcheck(L.evx_td_loss_w(_p(Q), _p(Qt), self.actions, _p(a), _p(r), _p(done), self.gamma, B, _p(weights),
+                                   _p(dQ), _p(self.loss), _p(td_abs), _stream()), "td_loss")
+            self.fast.backward(B, dQ, X, H1, H2, DROPOUT_P, dz2, dz1, self.grads)
         if self.grad_hook is not None:
             self.grad_hook(self.grads.flat)
         if update:
@@ -398,6 +422,16 @@ class Learner:
     def step_optimizer(self):
         L = qlib()
         n = self.online.numel
+        if self.fused_opt:  # clip + Adam + x3 repack in one launch from the norm partials
+            if not self._ss_fresh:
+                self.fast.sumsq_parts(self.grads.flat, self._ss)
+            self._ss_fresh = False
+            self.adam_step += 1
+            h = evx_adam(lr=self.lr, beta1=self.betas[0], beta2=self.betas[1], eps=self.eps, weight_decay=0.0,
+                         step=self.adam_step)
+            self.fast.adam_step(self.online.flat, self.grads.flat, self.m, self.v, float(self.max_norm or 0.0), h,
+                                self._ss, self.norm)
+            return
         qcheck(L.evx_sumsq_norm(_p(self.grads.flat), n, _p(self.scratch), self.scratch.numel(), _p(self.norm),
                                 _stream()), "sumsq")
         self.adam_step += 1

@@ -207,6 +207,11 @@ int evx_td_loss_w(const float *Q, const float *Qt, int32_t A, const int32_t *act
                   const uint8_t *done, float gamma, int32_t B, const float *w, float *dQ, float *loss,
                   float *td_abs, void *stream);
 /* ||g||_2 into norm[0] (clip_grad_norm_'s total norm) */
+/* evx_td_loss_w plus clearing zero[0..nzero) (the gradient buffer the backward accumulates into)
+ * in the same launch (extra workgroups) */
+int evx_td_loss_zero(const float *Q, const float *Qt, int32_t A, const int32_t *act, const float *rew,
+                     const uint8_t *done, float gamma, int32_t B, const float *w, float *dQ, float *loss, float *td_abs,
+                     float *zero, int64_t nzero, void *stream);
 int evx_sumsq_norm(const float *g, int64_t n, float *scratch, int32_t scratch_elems, float *norm, void *stream);
 /* g *= min(1, max_norm/(norm+1e-6)) (skipped if norm NULL) then one torch.optim.Adam step */
 int evx_clip_adam(float *p, float *g, float *m, float *v, int64_t n, const float *norm, float max_norm,
@@ -390,6 +395,23 @@ int64_t evx_qmlp_backward_part_floats(int32_t B);
 int evx_qmlp_backward(const evx_qmlp_params *p, int32_t B, const float *dq, const uint16_t *x, const uint16_t *h1,
                       const float *h2, float drop_p, uint16_t *dz2, uint16_t *dz1, const evx_qmlp_grads *g,
                       int32_t zero_grads, void *stream);
+/* evx_qmlp_backward that also leaves clip_grad_norm_'s squared-norm partials of the final gradients
+ * in ss[0 .. evx_qmlp_norm_parts()) (the gradients one flat state_dict-order buffer: g->w1 .. g->b3
+ * contiguous); with g->part the weight-gradient reductions and the partials share one launch. */
+int evx_qmlp_backward_ss(const evx_qmlp_params *p, int32_t B, const float *dq, const uint16_t *x, const uint16_t *h1,
+                         const float *h2, float drop_p, uint16_t *dz2, uint16_t *dz1, const evx_qmlp_grads *g,
+                         int32_t zero_grads, float *ss, void *stream);
+int32_t evx_qmlp_norm_parts(void);
+int64_t evx_qmlp_nparams(void);
+/* the same partials of a flat gradient buffer (after an all-reduce changed it) */
+int evx_qmlp_sumsq_parts(const float *g, float *ss, void *stream);
+/* clip_grad_norm_ + Adam (agents/dqn_agent.py:158-160) on the MLP's flat p / g / m / v (state_dict
+ * order, evx_qmlp_nparams() elements) from the nss norm partials, with the x3 operand repack
+ * (evx_qmlp_pack3's outputs) in the same launch; g receives the clipped gradients, norm_out (or
+ * NULL) the total norm. Replaces evx_sumsq_norm + evx_clip_adam + evx_qmlp_pack3. */
+int evx_qmlp_adam_pack3(float *p, float *g, float *m, float *v, float max_norm, const evx_adam *h, uint16_t *w1b,
+                        uint16_t *w1l, float *b1c, uint16_t *w2b, uint16_t *w2l, uint16_t *w2t, uint16_t *w2tl,
+                        const float *ss, int32_t nss, float *norm_out, void *stream);
 const char *evx_qmlp_last_error(void);
 
 #ifdef __cplusplus

@@ -208,3 +208,59 @@ def test_x3_rejects_missing_operands():
     with pytest.raises(_lib.EvacxError):
         fast.forward(lay.c, env.obs, 16, torch.empty(2 * 16 * HID, dtype=torch.int16, device="cuda"),
                      q=torch.empty(16, 5, device="cuda"))
+
+
+@pytest.mark.parametrize("hook", [False, True])
+def test_fused_learn_chain_matches_separate_launches(hook):
+    """The collapsed x3 learn chain (TD + gradient clear in one launch; qdz1 + dW2 in one launch;
+    both split-K reductions + clip_grad_norm_'s squared-norm partials in one launch; clip + Adam
+    + operand repack in one launch, evx_qmlp_adam_pack3) against the separate launches (td_loss,
+    zero, qdz1, gemm_tn + reduce x2, sumsq, clip_adam, pack3) from the same state over three
+    learn steps: loss, norm, clipped gradients and parameters within f32 reassociation; the
+    fused kernel's bf16 hi / lo operand tiles and b1c bit-identical to pack3 of its own updated
+    parameters. hook: a gradient hook (the multi-GPU all-reduce's slot) makes the norm partials
+    come from a pass over the flat gradients instead (evx_qmlp_sumsq_parts)."""
+    _need_gpu()
+    from evacx.qmlp import HID
+    from evacx.qnet import Learner
+    lay, env = _env_obs(E=320, R=4)
+    B = 512
+    assert 2 * B <= env.E * lay.R
+    dev = "cuda"
+    runs = []
+    for fused in (False, True):
+        lr = Learner(kind="mlp", precision="f32", seed=33, lr=1e-3)
+        lr.fused_opt = fused
+        if hook:
+            lr.grad_hook = lambda g: g.mul_(1.0)
+        g = torch.Generator().manual_seed(9)
+        for it in range(3):
+            perm = torch.randperm(env.E * lay.R, generator=g)
+            obs = env.obs.view(-1, 8)
+            s_obs = obs[perm[:B].to(dev)].contiguous().view(-1)
+            s2_obs = obs[perm[B:2 * B].to(dev)].contiguous().view(-1)
+            a = torch.randint(0, 5, (B,), generator=g, dtype=torch.int32).to(dev)
+            r = (torch.randn(B, generator=g) * 30).to(dev)
+            d = (torch.rand(B, generator=g) < 0.2).to(torch.uint8).to(dev)
+            m1 = (torch.rand(B, HID, generator=g) >= 0.2).to(torch.uint8).to(dev)
+            m2 = (torch.rand(B, HID, generator=g) >= 0.2).to(torch.uint8).to(dev)
+            loss = lr.learn_obs(lay.c, s_obs, a, r, d, s2_obs, B, mask_online=m1, mask_target=m2)
+        torch.cuda.synchronize()
+        runs.append(dict(loss=loss.item(), norm=lr.norm.item(),
+                         grads={k: v.clone() for k, v in lr.grads.state_dict().items()},
+                         params={k: v.clone() for k, v in lr.online.state_dict().items()},
+                         packed=[t.clone() for t in (lr.fast.w1b, lr.fast.w1l, lr.fast.b1c, lr.fast.w2b, lr.fast.w2l,
+                                                     lr.fast.w2t, lr.fast.w2tl)], lr=lr))
+    sep, fus = runs
+    assert abs(sep["loss"] - fus["loss"]) <= 1e-5 * abs(sep["loss"]) + 1e-7
+    assert abs(sep["norm"] - fus["norm"]) <= 1e-5 * sep["norm"] + 1e-9
+    for k in sep["params"]:
+        scale = sep["grads"][k].abs().max().item()
+        torch.testing.assert_close(fus["grads"][k], sep["grads"][k], rtol=1e-4, atol=1e-6 * scale + 1e-12)
+        torch.testing.assert_close(fus["params"][k], sep["params"][k], rtol=1e-5, atol=2e-6)
+    lr = fus["lr"]
+    lr.fast.repack()  # pack3 of the fused run's own parameters
+    torch.cuda.synchronize()
+    for got, want in zip(fus["packed"], (lr.fast.w1b, lr.fast.w1l, lr.fast.b1c, lr.fast.w2b, lr.fast.w2l,
+                                         lr.fast.w2t, lr.fast.w2tl)):
+        assert torch.equal(got, want)
