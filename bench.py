@@ -1,10 +1,13 @@
 #!/usr/bin/env python3
 """Benchmark of the evacuation RL hot path on MI355X.
 
-Workload (BASELINE.json metric; configs[2], per-GPU share): synthetic 128x128
-layout, 2276 people and 16 robots per env, 4096 envs per GPU (weak scaling;
-env ids global, seeds 1234 + global env id), uniform-init MLP Q-net, batch 4096,
-replay 2^20 transitions per GPU, gradient all-reduce over RCCL when world > 1.
+Workload (BASELINE.json metric; configs[2] as stated, which fits one MI355X): synthetic
+128x128 layout, 2276 people and 16 robots per env, 32768 envs per GPU (weak scaling: N GPUs
+step N x 32768 envs; env ids global, seeds 1234 + global env id), uniform-init MLP Q-net,
+learn batch = envs per GPU (one sampled transition per env-step, as the 8-GPU data-parallel
+run's global batch 8 x 4096), replay 16 steps of pushes per GPU (2^23 transitions), gradient
+all-reduce over RCCL when world > 1. --envs 4096 --batch 4096 is the per-GPU share of the
+8-GPU data-parallel run.
 One timed "step" = one full vectorised training step in the reference's order
 (DQNAgent act -> env.step -> remember -> learn, runners/train_dqn.py:94-116):
 act (Q forward for E*R robots + epsilon-greedy) -> env.step (all E envs, finished
@@ -89,13 +92,13 @@ def parse():
                     help="env-only preparation steps that spread env ages over an episode (before --warmup)")
     ap.add_argument("--stagger", type=int, default=1200,
                     help="preparation step w force-resets envs with global id %% stagger == w (0 = no stagger)")
-    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
+    ap.add_argument("--envs", type=int, default=32768, help="envs per GPU")
     ap.add_argument("--grid", type=int, default=128)
     ap.add_argument("--layouts", type=int, default=1,
                     help="K > 1: per-env layouts, K random variants of the synthetic layout (env e runs e %% K)")
     ap.add_argument("--people", type=int, default=2276)
     ap.add_argument("--robots", type=int, default=16)
-    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--batch", type=int, default=0, help="learn batch (0: = envs per GPU)")
     ap.add_argument("--precision", choices=["bf16", "f32"], default="f32",
                     help="Q-net arithmetic: f32 (the reference's; fused kernels with bf16x3-split MFMA operands) "
                          "or bf16")
@@ -116,14 +119,23 @@ def parse():
                          "the ring before push t and overlaps env.step t (evacx.trainer.VecTrainer)")
     ap.add_argument("--replay", choices=["uniform", "prioritized"], default="uniform",
                     help="prioritized: GPU sum/min-tree proportional replay (cfg5; evacx.prio)")
-    ap.add_argument("--replay-capacity", type=int, default=1 << 20)
+    ap.add_argument("--replay-capacity", type=int, default=0,
+                    help="transitions per GPU (0: the power of two >= 16 steps of pushes, envs x robots x 16)")
     ap.add_argument("--groups", type=int, default=1,
                     help="env groups per GPU, each with its own act -> env.step -> push stream chain "
                          "(evacx.trainer._Group): one group's env.step tail overlaps the others' work")
     ap.add_argument("--traffic", default=None,
                     help="PMC traffic record of env_step_kernel on this workload and phase (tools/parse_prof.py); "
                          "default profiles/r2/env_traffic_<phase>.json")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.batch <= 0:
+        args.batch = args.envs
+    if args.replay_capacity <= 0:
+        c = 1
+        while c < 16 * args.envs * args.robots:
+            c <<= 1
+        args.replay_capacity = c
+    return args
 
 
 def cpu_model():
@@ -208,6 +220,8 @@ def main():
     prep_acts = torch.empty(E * R, device="cuda", dtype=torch.int32)
     g = torch.Generator(device="cuda").manual_seed(4321 + rank)
     for w in range(args.age_steps):
+        if rank == 0 and w % 200 == 0:  # progress on stderr (long profiled runs)
+            print(f"preparation step {w}/{args.age_steps}", file=sys.stderr, flush=True)
         torch.randint(0, 5, (E * R,), device="cuda", dtype=torch.int32, generator=g, out=prep_acts)
         env.step(prep_acts, auto_reset=True)
         if 0 < S and w < S:
@@ -329,7 +343,8 @@ def main():
             "dtype": "f64" if args.mode == "env" else f"f64 env + {qdesc}",
             "data": "synthetic",
             "config": {
-                "workload": (f"{cfg_name(args)} per-GPU share: {L}x{W} synthetic layout"
+                "workload": (f"{cfg_name(args)}{' (BASELINE.json configs[2] as stated)' if E == 32768 and (L, R) == (128, 16) else ''}"
+                             f" per GPU: {L}x{W} synthetic layout"
                              + (f" ({args.layouts} random per-env layouts)" if args.layouts > 1 else "")
                              + f", {P} people, {R} robots, {E} envs/GPU; "
                              + (f"full training step ({schedule} schedule): act + env.step + replay push + learn "
@@ -341,7 +356,7 @@ def main():
                                 "; episode phase: start (every env freshly reset before the timed steps)")),
                 "episode_phase": args.phase, "age_steps": args.age_steps, "stagger": S,
                 "envs_per_gpu": E, "grid": f"{L}x{W}", "people": P, "robots": R, "mode": args.mode,
-                "batch": args.batch, "schedule": schedule, "precision": prec,
+                "batch": args.batch, "replay_capacity": args.replay_capacity, "schedule": schedule, "precision": prec,
                 "qnet": ("MLP 726-512-256-5" if args.qnet == "mlp"
                          else "DQNNetwork conv 6-32-64-128 + 15488-512-256-5"),
                 "replay": args.replay, "groups": args.groups if args.mode == "train" else 1,

@@ -2367,6 +2367,32 @@ __global__ __launch_bounds__(1024) void env_order_kernel(evx_layout lay, evx_sta
     }
 }
 
+// ------------------------------------------------------- act permutation
+// evx_act_perm: the envs whose fire has reached the layout's last step (fire_step >= t_max,
+// the x3 act's table fire step) first, then the rest, each part in env order. One workgroup:
+// thread t owns the contiguous envs [t * per, (t + 1) * per); a block scan of the counts
+// places them.
+__global__ __launch_bounds__(1024) void act_perm_kernel(int t_max, evx_state st, int32_t* __restrict__ perm) {
+    __shared__ int cnt[1024];
+    __shared__ int tot;
+    const int t = (int)threadIdx.x, E = st.E;
+    const int per = (E + 1023) / 1024, e0 = min(E, t * per), e1 = min(E, e0 + per);
+    int ns = 0;
+    for (int e = e0; e < e1; e++) ns += st.scal[(size_t)e * 4] >= t_max;
+    cnt[t] = ns;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        const int v = t >= o ? cnt[t - o] : 0;
+        __syncthreads();
+        cnt[t] += v;
+        __syncthreads();
+    }
+    if (t == 1023) tot = cnt[1023];
+    __syncthreads();
+    int ps = cnt[t] - ns, pr = tot + (e0 - (cnt[t] - ns));
+    for (int e = e0; e < e1; e++) perm[st.scal[(size_t)e * 4] >= t_max ? ps++ : pr++] = e;
+}
+
 // ---------------------------------------------------- observation expand
 // EvacuationEnv._get_state (envs/evacuation_env.py:84-120) from the compact form.
 template <typename T>
@@ -2592,6 +2618,16 @@ int evx_env_order(const evx_layout* l, const evx_state* s, void* stream) {
     hipLaunchKernelGGL(evx::env_order_kernel, dim3(1), dim3(1024), lds, (hipStream_t)stream, *l, *s, hcap, hmin);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : hip_fail(e, "env_order launch");
+}
+
+int evx_act_perm(const evx_layout* l, const evx_state* s, int32_t* perm, void* stream) {
+    int rc = check_layout(l);
+    if (rc) return rc;
+    if (!s || !perm) return fail(-22, "act_perm: NULL argument");
+    if (s->E <= 0) return 0;
+    hipLaunchKernelGGL(evx::act_perm_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, l->t_max, *s, perm);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : hip_fail(e, "act_perm launch");
 }
 
 int evx_obs_expand_f32(const evx_layout* l, const evx_obs* obs, int64_t n, float* out, void* stream) {

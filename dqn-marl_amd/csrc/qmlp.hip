@@ -166,7 +166,18 @@ struct Fwd {
     __bf16* h1l;
     // explicit dropout keep mask [N][512] (replaces the hash when set)
     const uint8_t* drop_mask;
+    // X3 act fast path: fc1's occupancy columns lo (w1o_tile order; hi in w1o)
+    const __bf16* w1ol;
+    // act row permutation (evx_act_perm): batch row i reads / writes row
+    // perm[i / rpe] * rpe + i % rpe (dropout rows and epsilon draws keep the original row)
+    const int32_t* perm;
+    int rpe;
 };
+__device__ __forceinline__ int orow(const Fwd& a, int row) {
+    if (!a.perm) return row;
+    const int s = row / a.rpe;
+    return a.perm[s] * a.rpe + (row - s * a.rpe);
+}
 
 // One row's window in the static feature map (evx_layout.obs_feat): base index of
 // window cell (0, 0) = map cell (cx - 5, cy - 5) at the row's fire step. Rows past N
@@ -224,7 +235,7 @@ __device__ __forceinline__ void fc1_tile(const Fwd& a, int m0, int ncol0, bool w
     const bool rowok = m0 + gr < a.N;
     evx_obs ob;
     if (rowok) {
-        ob = a.obs[m0 + gr];
+        ob = a.obs[orow(a, m0 + gr)];
     } else {
         ob = evx_obs{{0u, 0u, 0u, 0u}, 0, 0, 0, 0};
     }
@@ -357,8 +368,9 @@ __device__ __forceinline__ void fc1_slab(const Fwd& a, const f32x16 (&accm)[NTW]
 #pragma unroll
     for (int r = 0; r < 16; r += 2) {  // rows rl, rl + 1: one dropout hash per pair
         const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;
+        // rows rl, rl + 1 (rl even) stay a pair under the act permutation (rpe even)
         const uint32_t ph =
-            a.drop_thresh ? drop_row(a.drop_seed, a.drop_stream, (a.drop_row0 + (uint32_t)(row0 + rl)) >> 1) : 0u;
+            a.drop_thresh ? drop_row(a.drop_seed, a.drop_stream, (a.drop_row0 + (uint32_t)orow(a, row0 + rl)) >> 1) : 0u;
 #pragma unroll
         for (int nt = 0; nt < NTW; nt++) {
             const int cl = cl0 + nt * 32 + (lane & 31);
@@ -521,7 +533,7 @@ __global__ __launch_bounds__(512, 1) void qact_kernel(Fwd a) {
         if (tid < 128) {
             int pos = 0;
             if (m0 + tid < a.N) {
-                const evx_obs ob = a.obs[m0 + tid];
+                const evx_obs ob = a.obs[orow(a, m0 + tid)];
                 ok = min(max(ob.fire_step, 0), a.t_max) == a.stat_fs && ob.cx >= 0 && ob.cx <= a.L + 1 && ob.cy >= 0 && ob.cy <= a.W + 1;
                 pos = ok ? ob.cx * (a.W + 2) + ob.cy : 0;
             }
@@ -546,7 +558,7 @@ __global__ __launch_bounds__(512, 1) void qact_kernel(Fwd a) {
         for (int mt = 0; mt < 4; mt++) {
             const int row = m0 + mt * 32 + (lane & 31);
             uint4 o = make_uint4(0u, 0u, 0u, 0u);
-            if (row < a.N) o = *reinterpret_cast<const uint4*>(&a.obs[row].occ[0]);
+            if (row < a.N) o = *reinterpret_cast<const uint4*>(&a.obs[orow(a, row)].occ[0]);
             occ[mt][0] = o.x;
             occ[mt][1] = o.y;
             occ[mt][2] = o.z;
@@ -632,7 +644,7 @@ __global__ __launch_bounds__(512, 1) void qact_kernel(Fwd a) {
     }
     __syncthreads();
     const int row = tid >> 2;
-    fc3_act(a, &H2s[row][0], W3s, m0 + row, m0 + row < a.N);
+    fc3_act(a, &H2s[row][0], W3s, orow(a, m0 + row), m0 + row < a.N);
 }
 
 // X3 (f32-accurate) act: the H1 tile of 128 rows would need 256 KB as hi + lo planes, so
@@ -645,18 +657,86 @@ constexpr int A3_HP = 256 + 8;                     // H1 half-plane row pitch (b
 constexpr int A3_HBYTES = 2 * 128 * A3_HP * 2;     // 135,168: both planes
 static_assert(A3_HBYTES >= 128 * ACT_H2P * 4, "H2 overlays the H1 planes");
 static_assert(A3_HBYTES >= 2 * 128 * (KC1 + 8) * 2, "fc1 A staging overlays the H1 planes");
-constexpr int ACT3_LDS = A3_HBYTES + NACT * HID2 * 4;
+constexpr int ACT3_LDS = A3_HBYTES + NACT * HID2 * 4 + 128 * 4;  // + W3 + window centres
 __global__ __launch_bounds__(512, 1) void qact3_kernel(Fwd a) {
     extern __shared__ __attribute__((aligned(16))) char dsm[];
     auto Hh = reinterpret_cast<__bf16 (*)[A3_HP]>(dsm);
     auto Hl = reinterpret_cast<__bf16 (*)[A3_HP]>(dsm + 128 * A3_HP * 2);
     auto H2s = reinterpret_cast<float (*)[ACT_H2P]>(dsm);
     auto W3s = reinterpret_cast<float (*)[HID2]>(dsm + A3_HBYTES);
+    int* posS = reinterpret_cast<int*>(dsm + A3_HBYTES + NACT * HID2 * 4);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
     const int m0 = blockIdx.x * 128;
     for (int i = tid; i < NACT * HID2; i += 512) W3s[i / HID2][i % HID2] = a.w3[i];
+    bool fast = false;
+    if (a.stat) {  // tile-uniform: every row at the table's fire step, centre inside the map
+        bool ok = true;
+        if (tid < 128) {
+            int pos = 0;
+            if (m0 + tid < a.N) {
+                const evx_obs ob = a.obs[orow(a, m0 + tid)];
+                ok = min(max(ob.fire_step, 0), a.t_max) == a.stat_fs && ob.cx >= 0 && ob.cx <= a.L + 1 && ob.cy >= 0 &&
+                     ob.cy <= a.W + 1;
+                pos = ok ? ob.cx * (a.W + 2) + ob.cy : 0;
+            }
+            posS[tid] = pos;
+        }
+        fast = __syncthreads_and(ok);  // also publishes posS
+    }
     f32x16 acc[4][2];
-    fc1_tile<4, 2, 8, true>(a, m0, w * 32, false, dsm, acc, 256);  // ends with a barrier: A buffers free
+    if (fast) {
+        // fc1 = table[centre] (f32: static features x W1 + b1, x3-accurate) + the occupancy
+        // columns x bits (K = 128 cells; bits exact in bf16: hi and lo weights, 2 MFMAs)
+#pragma unroll
+        for (int mt = 0; mt < 4; mt++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int rl = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const float* srow = a.stat + (size_t)posS[rl] * HID + w * 32 + (lane & 31);
+                acc[mt][0][r] = srow[0];
+                acc[mt][1][r] = srow[256];
+            }
+        uint32_t occ[4][4];
+#pragma unroll
+        for (int mt = 0; mt < 4; mt++) {
+            const int row = m0 + mt * 32 + (lane & 31);
+            uint4 o = make_uint4(0u, 0u, 0u, 0u);
+            if (row < a.N) o = *reinterpret_cast<const uint4*>(&a.obs[orow(a, row)].occ[0]);
+            occ[mt][0] = o.x;
+            occ[mt][1] = o.y;
+            occ[mt][2] = o.z;
+            occ[mt][3] = o.w;
+        }
+        const uint32_t one = 0x3f80u;
+#pragma unroll 2
+        for (int ks = 0; ks < 8; ks++) {  // k-step: cells 16 ks + 8 h .. + 7 of the 128
+            bf16x8 bh[2], bl[2];
+#pragma unroll
+            for (int nt = 0; nt < 2; nt++) {  // column tiles w and w + 8
+                bh[nt] = *reinterpret_cast<const bf16x8*>(a.w1o + w1o_tile(w + 8 * nt, ks >> 1, ks & 1) + lane * 8);
+                bl[nt] = *reinterpret_cast<const bf16x8*>(a.w1ol + w1o_tile(w + 8 * nt, ks >> 1, ks & 1) + lane * 8);
+            }
+            const int c0 = ks * 16 + 8 * h;  // multiple of 8: the 8 bits sit in one word
+#pragma unroll
+            for (int mt = 0; mt < 4; mt++) {
+                const uint32_t wd = (c0 >> 5) == 0 ? occ[mt][0] : (c0 >> 5) == 1 ? occ[mt][1]
+                                  : (c0 >> 5) == 2 ? occ[mt][2] : occ[mt][3];
+                const uint32_t bits = (wd >> (c0 & 31)) & 0xffu;
+                uint32_t av4[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    av4[j] = ((bits >> (2 * j)) & 1u) * one | (((bits >> (2 * j + 1)) & 1u) * one) << 16;
+                const bf16x8 av = __builtin_bit_cast(bf16x8, av4);
+#pragma unroll
+                for (int nt = 0; nt < 2; nt++) {
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bh[nt], acc[mt][nt], 0, 0, 0);
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bl[nt], acc[mt][nt], 0, 0, 0);
+                }
+            }
+        }
+    } else {
+        fc1_tile<4, 2, 8, true>(a, m0, w * 32, false, dsm, acc, 256);  // ends with a barrier: A buffers free
+    }
     f32x16 acc2[4];
 #pragma unroll
     for (int mt = 0; mt < 4; mt++)
@@ -664,7 +744,7 @@ __global__ __launch_bounds__(512, 1) void qact3_kernel(Fwd a) {
         for (int r = 0; r < 16; r++) acc2[mt][r] = 0.f;
 #pragma unroll
     for (int hh = 0; hh < 2; hh++) {
-        const float bias[1] = {a.b1[hh * 256 + w * 32 + (lane & 31)]};
+        const float bias[1] = {fast ? 0.f : a.b1[hh * 256 + w * 32 + (lane & 31)]};  // the table holds the bias
 #pragma unroll
         for (int mt = 0; mt < 4; mt++) {
             const f32x16 one[1] = {acc[mt][hh]};
@@ -717,7 +797,7 @@ __global__ __launch_bounds__(512, 1) void qact3_kernel(Fwd a) {
     }
     __syncthreads();
     const int row = tid >> 2;
-    fc3_act(a, &H2s[row][0], W3s, m0 + row, m0 + row < a.N);
+    fc3_act(a, &H2s[row][0], W3s, orow(a, m0 + row), m0 + row < a.N);
 }
 
 // ------------------------------------------------------------ fc2 + fc3
@@ -902,6 +982,21 @@ __global__ __launch_bounds__(256) void pack3_kernel(const float* __restrict__ w1
             split2(w2[kk * HID + nn], w2t[i], w2tl[i]);
         }
     }
+}
+
+// X3 act fast path operands: fc1's occupancy columns (reference channel 1 of cells 0..127,
+// >= 121 zero) as hi / lo bf16 pairs, w1o_tile order (K = 128 in 4 chunks of 32)
+__global__ __launch_bounds__(256) void pack_occ3_kernel(const float* __restrict__ w1, __bf16* __restrict__ w1o,
+                                                        __bf16* __restrict__ w1ol) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= HID * 128) return;
+    const int j = i & 7, l = (i >> 3) & 63, blk = i >> 9;
+    const int s = blk & 1, kc = (blk >> 1) & 3, t = blk >> 3;
+    const int n = t * 32 + (l & 31), c = kc * 32 + s * 16 + 8 * (l >> 5) + j;
+    __bf16 hi = (__bf16)0.f, lo = (__bf16)0.f;
+    if (c < NCELL) split2(w1[n * K1 + c * 6 + 1], hi, lo);
+    w1o[i] = hi;
+    w1ol[i] = lo;
 }
 
 // ================================================================ backward
@@ -1357,6 +1452,7 @@ struct AdamPack {
     int nss;
     float max_norm, beta1, beta2, eps, step_size, bc2_sqrt, weight_decay;
     __bf16 *w1b, *w1l, *w2b, *w2l, *w2t, *w2tl;
+    __bf16 *w1o, *w1ol;  // x3 act fast path occupancy columns, or NULL
     float* b1c;
     float* norm_out;
 };
@@ -1405,6 +1501,11 @@ __global__ __launch_bounds__(256) void adam_pack3_kernel(AdamPack a) {
             if (ch == 2) {  // the danger column's hi also meets the residual slot 512 + c
                 const int kr = K1P + c;
                 a.w1b[opnd_off(w1_tile(n >> 5, kr >> 5, (kr >> 4) & 1, NKC1X), n, kr)] = hi;
+            }
+            if (ch == 1 && a.w1o) {  // occupancy column of cell c: the act fast path's operands
+                const size_t oo = opnd_off(w1o_tile(n >> 5, c >> 5, (c >> 4) & 1), n, c);
+                a.w1o[oo] = hi;
+                a.w1ol[oo] = lo;
             }
         }
     } else if (i < OW2) {  // fc1.bias and W1[:, centre]: b1c = b1 + W1[:, centre]
@@ -1481,6 +1582,13 @@ int evx_qmlp_pack(const float* w1, const float* b1, const float* w2, uint16_t* w
     return mlaunch("qmlp_pack");
 }
 
+int evx_qmlp_pack_occ3(const float* w1, uint16_t* w1o, uint16_t* w1ol, void* stream) {
+    if (!w1 || !w1o || !w1ol) return mfail(-22, "qmlp_pack_occ3: NULL argument");
+    hipLaunchKernelGGL(evxm::pack_occ3_kernel, dim3(evxm::HID * 128 / 256), dim3(256), 0, (hipStream_t)stream, w1,
+                       reinterpret_cast<__bf16*>(w1o), reinterpret_cast<__bf16*>(w1ol));
+    return mlaunch("qmlp_pack_occ3");
+}
+
 int evx_qmlp_pack3(const float* w1, const float* b1, const float* w2, uint16_t* w1b, uint16_t* w1l, float* b1c,
                    uint16_t* w2b, uint16_t* w2l, uint16_t* w2t, uint16_t* w2tl, void* stream) {
     if (!w1 || !b1 || !w2 || !w1b || !w1l || !b1c || !w2b || !w2l) return mfail(-22, "qmlp_pack3: NULL argument");
@@ -1547,6 +1655,7 @@ static int make_fwd(const evx_layout* lay, const evx_obs* obs, int32_t n, const 
     a.feats_lo = nullptr;
     a.w1l = a.w2l = nullptr;
     a.h1l = nullptr;
+    a.w1ol = nullptr;
     if (p->x3) {
         if (!p->w1l || !p->w2l) return mfail(-22, "qmlp_forward: x3 needs w1l / w2l (evx_qmlp_pack3)");
         if (!lay->obs_feat_lo || (lay->layout_set && !lay->obs_feats_lo))
@@ -1556,8 +1665,12 @@ static int make_fwd(const evx_layout* lay, const evx_obs* obs, int32_t n, const 
         a.w1l = reinterpret_cast<const __bf16*>(p->w1l);
         a.w2l = reinterpret_cast<const __bf16*>(p->w2l);
         a.h1l = a.h1 ? a.h1 + (size_t)n * evxm::HID : nullptr;  // lo plane after the hi plane
-        a.stat = nullptr;  // the act table is a bf16-mode feature
+        a.w1ol = reinterpret_cast<const __bf16*>(p->w1ol);
+        if (!a.w1ol) a.stat = nullptr;  // the x3 table path needs the occupancy columns' lo part
     }
+    a.perm = out->perm;
+    a.rpe = out->rows_per_env > 0 ? out->rows_per_env : 1;
+    if (a.perm && (a.rpe & 1)) return mfail(-22, "qmlp_forward: rows_per_env must be even (dropout row pairs)");
     return 0;
 }
 
@@ -1642,10 +1755,11 @@ int evx_qmlp_stat(const evx_layout* lay, const evx_obs* obs, int32_t n, const ev
     int rc = make_fwd(lay, obs, n, p, nullptr, &o, a);
     if (rc) return rc;
     a.h1 = nullptr;
-    if (p->x3) return mfail(-22, "qmlp_stat: the act table is a bf16-mode feature");
+    a.h1l = nullptr;
     a.stat = nullptr;
+    a.perm = nullptr;
     a.raw = out;
-    return launch_fwd(a, a, n, 1, false, (hipStream_t)stream);
+    return launch_fwd(a, a, n, 1, false, (hipStream_t)stream, p->x3 != 0);
 }
 
 int evx_qmlp_forward2(const evx_layout* lay, int32_t n, const evx_obs* obs0, const evx_qmlp_params* p0,
@@ -1802,7 +1916,8 @@ int evx_qmlp_sumsq_parts(const float* g, float* ss, void* stream) {
 
 int evx_qmlp_adam_pack3(float* p, float* g, float* m, float* v, float max_norm, const evx_adam* h, uint16_t* w1b,
                         uint16_t* w1l, float* b1c, uint16_t* w2b, uint16_t* w2l, uint16_t* w2t, uint16_t* w2tl,
-                        const float* ss, int32_t nss, float* norm_out, void* stream) {
+                        uint16_t* w1o, uint16_t* w1ol, const float* ss, int32_t nss, float* norm_out, void* stream) {
+    if ((w1o == nullptr) != (w1ol == nullptr)) return mfail(-22, "qmlp_adam_pack3: w1o and w1ol go together");
     if (!p || !g || !m || !v || !h || !w1b || !w1l || !b1c || !w2b || !w2l || !ss)
         return mfail(-22, "qmlp_adam_pack3: NULL argument");
     if ((w2t == nullptr) != (w2tl == nullptr)) return mfail(-22, "qmlp_adam_pack3: w2t and w2tl go together");
@@ -1820,6 +1935,7 @@ int evx_qmlp_adam_pack3(float* p, float* g, float* m, float* v, float max_norm, 
     a.w2b = reinterpret_cast<__bf16*>(w2b); a.w2l = reinterpret_cast<__bf16*>(w2l);
     a.w2t = reinterpret_cast<__bf16*>(w2t); a.w2tl = reinterpret_cast<__bf16*>(w2tl);
     a.b1c = b1c; a.norm_out = norm_out;
+    a.w1o = reinterpret_cast<__bf16*>(w1o); a.w1ol = reinterpret_cast<__bf16*>(w1ol);
     hipLaunchKernelGGL(evxm::adam_pack3_kernel, dim3((unsigned)((evxm::NPAR + 255) / 256)), dim3(256), 0,
                        (hipStream_t)stream, a);
     return mlaunch("qmlp_adam_pack3");

@@ -69,6 +69,7 @@ def lib():
         L.evx_obs_expand_f64.argtypes = [C.POINTER(evx_layout), C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p]
         L.evx_seed_host.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
         L.evx_env_order.argtypes = [C.POINTER(evx_layout), C.POINTER(evx_state), C.c_void_p]
+        L.evx_act_perm.argtypes = [C.POINTER(evx_layout), C.POINTER(evx_state), C.c_void_p, C.c_void_p]
         _lib = L
     return _lib
 

@@ -408,6 +408,15 @@ class VecEnv:
         _lib.check(_lib.lib().evx_env_reset(C.byref(self.lay.c), C.byref(self.c), _ptr(m), _ptr(self.obs),
                                             _ptr(self.err), _stream()), "evx_env_reset")
 
+    def act_perm(self, out: torch.Tensor) -> torch.Tensor:
+        """Env visiting order for the act (evx_act_perm): the envs whose fire has reached the
+        layout's last step first (the x3 act's table path), then the rest, each in env order."""
+        if out.numel() < self.E or out.dtype != torch.int32:
+            raise ValueError("act_perm: out must be int32 with >= E entries")
+        _lib.check(_lib.lib().evx_act_perm(C.byref(self.lay.c), C.byref(self.c), out.data_ptr(), _stream()),
+                   "evx_act_perm")
+        return out
+
     def compute_order(self, force: bool = False, ahead: bool = False):
         """Dispatch order of the next step: heavy env-steps first, the heaviest with a
         whole workgroup each (scheduling only; the results do not depend on it). Small

@@ -33,7 +33,7 @@ def compact_ref_cols() -> np.ndarray:
 
 class evx_qmlp_params(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in ["w1", "b1c", "w2", "w2t", "b2", "w3", "b3", "w1o", "stat"]] + \
-        [("stat_fs", C.c_int32), ("x3", C.c_int32)] + [(n, C.c_void_p) for n in ["w1l", "w2l", "w2tl"]]
+        [("stat_fs", C.c_int32), ("x3", C.c_int32)] + [(n, C.c_void_p) for n in ["w1l", "w2l", "w2tl", "w1ol"]]
 
 
 class evx_qmlp_dropout(C.Structure):
@@ -48,7 +48,7 @@ class evx_qmlp_grads(C.Structure):
 class evx_qmlp_fwd_out(C.Structure):
     _fields_ = [("h1", C.c_void_p), ("x", C.c_void_p), ("h2", C.c_void_p), ("q", C.c_void_p),
                 ("actions", C.c_void_p), ("epsilon", C.c_float), ("act_seed", C.c_uint64),
-                ("act_offset", C.c_uint64)]
+                ("act_offset", C.c_uint64), ("perm", C.c_void_p), ("rows_per_env", C.c_int32)]
 
 
 _inited = False
@@ -78,8 +78,9 @@ def mlib():
         L.evx_qmlp_norm_parts.restype = C.c_int32
         L.evx_qmlp_nparams.restype = C.c_int64
         L.evx_qmlp_sumsq_parts.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
-        L.evx_qmlp_adam_pack3.argtypes = [C.c_void_p] * 4 + [C.c_float, C.c_void_p] + [C.c_void_p] * 8 + \
+        L.evx_qmlp_adam_pack3.argtypes = [C.c_void_p] * 4 + [C.c_float, C.c_void_p] + [C.c_void_p] * 10 + \
             [C.c_int32, C.c_void_p, C.c_void_p]
+        L.evx_qmlp_pack_occ3.argtypes = [C.c_void_p] * 4
         L.evx_qmlp_backward_part_floats.restype = C.c_int64
         L.evx_qmlp_backward_part_floats.argtypes = [C.c_int32]
         L.evx_qmlp_backward.argtypes = [C.POINTER(evx_qmlp_params), C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
@@ -118,7 +119,8 @@ class MLPFast:
         self.w2b = torch.zeros(HID2 * HID, **i16)
         self.w2t = torch.zeros(HID * HID2, **i16)
         self.b1c = torch.zeros(HID, dtype=torch.float32, device=self.device)
-        self.w1o = None if self.x3 else torch.zeros(HID * 128, **i16)  # fc1's occupancy columns (act fast path)
+        self.w1o = torch.zeros(HID * 128, **i16)  # fc1's occupancy columns (act fast path; x3: hi)
+        self.w1ol = torch.zeros(HID * 128, **i16) if self.x3 else None  # x3: their lo part
         self.c = evx_qmlp_params(w1=self.w1b.data_ptr(), b1c=self.b1c.data_ptr(), w2=self.w2b.data_ptr(),
                                  w2t=self.w2t.data_ptr(), b2=params["fc2.bias"].data_ptr(),
                                  w3=params["fc3.weight"].data_ptr(), b3=params["fc3.bias"].data_ptr())
@@ -128,6 +130,7 @@ class MLPFast:
             self.w2tl = torch.zeros(HID * HID2, **i16)
             self.c.x3 = 1
             self.c.w1l, self.c.w2l, self.c.w2tl = self.w1l.data_ptr(), self.w2l.data_ptr(), self.w2tl.data_ptr()
+            self.c.w1ol = self.w1ol.data_ptr()
         self._static = None  # (lay_c, centre obs, table) of attach_static
         self._part = None  # split-K scratch of the weight-gradient GEMMs (backward)
         self.repack()
@@ -143,6 +146,10 @@ class MLPFast:
                                          self.P["fc2.weight"].data_ptr(), self.w1b.data_ptr(), self.w1l.data_ptr(),
                                          self.b1c.data_ptr(), self.w2b.data_ptr(), self.w2l.data_ptr(),
                                          self.w2t.data_ptr(), self.w2tl.data_ptr(), _stream()), "qmlp_pack3")
+            mcheck(mlib().evx_qmlp_pack_occ3(self.P["fc1.weight"].data_ptr(), self.w1o.data_ptr(),
+                                             self.w1ol.data_ptr(), _stream()), "qmlp_pack_occ3")
+            if self._static is not None:
+                self._rebuild_static()
             return
         mcheck(mlib().evx_qmlp_pack(self.P["fc1.weight"].data_ptr(), self.P["fc1.bias"].data_ptr(),
                                     self.P["fc2.weight"].data_ptr(), self.w1b.data_ptr(), self.b1c.data_ptr(),
@@ -159,9 +166,12 @@ class MLPFast:
         mcheck(mlib().evx_qmlp_adam_pack3(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), float(max_norm),
                                           C.byref(hyper), self.w1b.data_ptr(), self.w1l.data_ptr(),
                                           self.b1c.data_ptr(), self.w2b.data_ptr(), self.w2l.data_ptr(),
-                                          self.w2t.data_ptr(), self.w2tl.data_ptr(), ss.data_ptr(),
-                                          int(mlib().evx_qmlp_norm_parts()), _p(norm_out), _stream()),
+                                          self.w2t.data_ptr(), self.w2tl.data_ptr(), self.w1o.data_ptr(),
+                                          self.w1ol.data_ptr(), ss.data_ptr(), int(mlib().evx_qmlp_norm_parts()),
+                                          _p(norm_out), _stream()),
                "qmlp_adam_pack3")
+        if self._static is not None:  # the act table follows the weights
+            self._rebuild_static()
 
     @staticmethod
     def sumsq_parts(g, ss):
@@ -171,9 +181,8 @@ class MLPFast:
     def attach_static(self, lay_c, L: int, W: int, t_max: int):
         """Enable act()'s fast path for observations at fire step >= t_max (the fire has
         stopped spreading): fc1's pre-activation at zero occupancy for every window centre
-        of the layout, [(L+2)(W+2)][512] f32, rebuilt with every repack. bf16 mode only."""
-        if self.x3:
-            raise ValueError("attach_static: the act table is a bf16-mode feature")
+        of the layout, [(L+2)(W+2)][512] f32 (x3: f32-accurate), rebuilt with every repack and
+        every optimizer step (adam_step)."""
         cx, cy = np.meshgrid(np.arange(L + 2), np.arange(W + 2), indexing="ij")
         ob = np.zeros(((L + 2) * (W + 2), 8), np.int32)
         ob[:, 4], ob[:, 5], ob[:, 6] = cx.ravel(), cy.ravel(), t_max
@@ -209,14 +218,19 @@ class MLPFast:
 
 
     def act(self, lay_c, obs: torch.Tensor, n: int, drop=None, q=None, actions=None, epsilon=0.0, act_seed=0,
-            act_offset=0):
-        """DQNAgent.act in one launch (evx_qmlp_act): Q values and/or epsilon-greedy actions."""
+            act_offset=0, perm=None, rows_per_env=0):
+        """DQNAgent.act in one launch (evx_qmlp_act): Q values and/or epsilon-greedy actions.
+        perm (int32 [n / rows_per_env], device; evacx.env.VecEnv.act_perm): the batch visits the
+        envs in this order (results stay at their own rows)."""
         _need("act obs", obs, n, 8)
         _need("act q", q, n, NACT)
         _need("act actions", actions, n, 1)
+        if perm is not None and (rows_per_env <= 0 or rows_per_env % 2 or n % rows_per_env
+                                 or perm.numel() < n // rows_per_env):
+            raise ValueError("qmlp act: perm needs an even rows_per_env dividing n and n / rows_per_env entries")
         d = self._drop(drop) if drop else None
         o = evx_qmlp_fwd_out(q=_p(q), actions=_p(actions), epsilon=float(epsilon), act_seed=act_seed,
-                             act_offset=act_offset)
+                             act_offset=act_offset, perm=_p(perm), rows_per_env=int(rows_per_env))
         mcheck(mlib().evx_qmlp_act(C.byref(lay_c), obs.data_ptr(), n, C.byref(self.c),
                                    C.byref(d) if d is not None else None, C.byref(o), _stream()), "qmlp_act")
 

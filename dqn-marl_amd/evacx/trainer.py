@@ -205,11 +205,18 @@ class VecTrainer:
         self.fast = self.learner.fast
         if self.fast is None:
             self.lagged = False  # the split learn step needs the fused bf16 MLP path
-        elif os.environ.get("EVX_ACT_STATIC", "0") == "1" and not self.fast.x3:
-            # act fast path (off by default: the per-update table rebuild on the learn stream costs what
-            # the act saves, tools/gpu_ab_static.sh): envs past the fire's last step start fc1 from a table
+        self._perm = None
+        if self.fast is not None and layout_of is None and len(self.groups) == 1 and \
+                os.environ.get("EVX_ACT_STATIC", "1" if self.fast.x3 else "0") == "1":
+            # act fast path: envs past the fire's last step start fc1 from a per-centre table of the
+            # static features' contribution (rebuilt with every weight update) and add only the
+            # occupancy columns; the act visits those envs first (VecEnv.act_perm) so its row tiles
+            # are uniform. x3: on by default (the table replaces ~3/4 of fc1's products); bf16: off
+            # by default (the rebuild costs what the act saves, tools/gpu_ab_static.sh)
             lc = self.lay.c
             self.fast.attach_static(lc, lc.L, lc.W, lc.t_max)
+            self._perm = torch.zeros(E, dtype=torch.int32, device=self.device)
+            self.env.act_perm(self._perm)
 
     def _act(self, grp: _Group):
         """DQNAgent.act in train mode for one group's robots: dropout active, epsilon-greedy
@@ -220,7 +227,8 @@ class VecTrainer:
             self.learner.drop_stream += 1
             self.fast.act(self.lay.c, grp.env.obs, grp.n,
                           drop=(self.learner.seed, self.learner.drop_stream, DROPOUT_P, None, g0),
-                          actions=grp.actions, epsilon=float(self.epsilon), act_seed=self.act_seed, act_offset=off)
+                          actions=grp.actions, epsilon=float(self.epsilon), act_seed=self.act_seed, act_offset=off,
+                          perm=self._perm, rows_per_env=self.R if self._perm is not None else 0)
             return
         x = grp.env.expand_obs(torch.float32)  # [E/G, R, 11, 11, 6]
         Q = self.learner.q_values(x.view(grp.n, 11, 11, 6), train=True)
@@ -304,6 +312,8 @@ class VecTrainer:
                     grp.main.wait_event(self.ev_reset)
                 if self.lagged or grp.g > 0:
                     grp.main.wait_event(self.ev_learned)
+                if self._perm is not None and not inline:  # the act order, made after the last push
+                    grp.main.wait_event(grp.ev_order)
                 self._act(grp)
                 if self.lagged:
                     grp.ev_act.record(grp.main)
@@ -345,6 +355,8 @@ class VecTrainer:
                     ev_env[1].record(grp.main)
                 self.replay.push(grp.env.obs_prev, grp.env.obs, grp.actions, grp.env.reward, grp.env.done, grp.n,
                                  self.R, s2_term=grp.env.obs_term)
+                if self._perm is not None and inline:  # the next act's env order, on this stream
+                    grp.env.act_perm(self._perm)
                 grp.ev_push.record(grp.main)
         if extra_reset is not None:  # after every group's push, on group 0's side stream (warm-up only)
             side = G[0].side
@@ -366,6 +378,8 @@ class VecTrainer:
                     st.wait_event(grp.ev_push)
                 if extra_reset is not None:
                     st.wait_event(self.ev_reset)
+                if self._perm is not None:  # the next act's env order (the act waits for ev_order)
+                    grp.env.act_perm(self._perm)
                 grp.env.compute_order()
                 if st is grp.side:
                     grp.ev_order.record(st)

@@ -145,6 +145,9 @@ int evx_seed_host(const uint32_t *seeds_host, int32_t n, uint32_t *py_mt_host, u
  * of the first get a whole workgroup each (at most 256, each with >= P/4 persons in
  * play; EVX_HEAVY_CAP / EVX_HEAVY_MIN override). */
 int evx_env_order(const evx_layout *lay, const evx_state *st, void *stream);
+/* act row permutation for the x3 act fast path: perm[0..E) lists the envs whose fire step is >= the
+ * layout's t_max (the static-table fire step) first, then the rest, each in env order (stable) */
+int evx_act_perm(const evx_layout *l, const evx_state *s, int32_t *perm, void *stream);
 
 /* Bytes of dynamic LDS the step kernel needs for a layout (diagnostics). */
 int64_t evx_step_lds_bytes(const evx_layout *lay);
@@ -322,6 +325,8 @@ typedef struct {
      * one danger-residual slot per cell), w1l / w2l / w2tl hold the lo parts (evx_qmlp_pack3) */
     int32_t x3;
     const uint16_t *w1l, *w2l, *w2tl;
+    /* x3 act fast path: the lo part of w1o (w1o then holds the hi part; evx_qmlp_pack3 / _adam_pack3) */
+    const uint16_t *w1ol;
 } evx_qmlp_params;
 
 typedef struct {
@@ -342,6 +347,11 @@ typedef struct {
     float epsilon;
     uint64_t act_seed, act_offset;
     /* x3: h1 holds two planes [2][n][512] (hi, lo) and x spans [n][640] */
+    /* act only, optional: batch row i is observation / action row perm[i / rows_per_env] * rows_per_env +
+     * i % rows_per_env (evx_act_perm: envs at the table's fire step first, so act tiles are uniform);
+     * dropout rows and epsilon draws stay keyed by that original row */
+    const int32_t *perm;
+    int32_t rows_per_env;
 } evx_qmlp_fwd_out;
 
 /* bf16 copies of fc1.weight [512][726] over fc1's compact K and fc2.weight [256][512]
@@ -356,6 +366,8 @@ int evx_qmlp_pack(const float *w1, const float *b1, const float *w2, uint16_t *w
  * hi / lo of fc2.weight, w2t / w2tl of its transpose (may be NULL); b1c = b1 + W1[:, centre] in f32 */
 int evx_qmlp_pack3(const float *w1, const float *b1, const float *w2, uint16_t *w1b, uint16_t *w1l, float *b1c,
                    uint16_t *w2b, uint16_t *w2l, uint16_t *w2t, uint16_t *w2tl, void *stream);
+/* x3 act fast path operands: fc1's occupancy columns [512][128] as hi (w1o) and lo (w1ol) bf16, w1o_tile order */
+int evx_qmlp_pack_occ3(const float *w1, uint16_t *w1o, uint16_t *w1ol, void *stream);
 /* fc1's pre-activation (X W1^T + b1, f32, no ReLU / dropout) of n observations -> out [n][512]:
  * with obs = every window centre of the layout at one fire step and zero occupancy this is the
  * act fast path's table (evx_qmlp_params.stat; rebuild after every weight update) */
@@ -411,7 +423,7 @@ int evx_qmlp_sumsq_parts(const float *g, float *ss, void *stream);
  * NULL) the total norm. Replaces evx_sumsq_norm + evx_clip_adam + evx_qmlp_pack3. */
 int evx_qmlp_adam_pack3(float *p, float *g, float *m, float *v, float max_norm, const evx_adam *h, uint16_t *w1b,
                         uint16_t *w1l, float *b1c, uint16_t *w2b, uint16_t *w2l, uint16_t *w2t, uint16_t *w2tl,
-                        const float *ss, int32_t nss, float *norm_out, void *stream);
+                        uint16_t *w1o, uint16_t *w1ol, const float *ss, int32_t nss, float *norm_out, void *stream);
 const char *evx_qmlp_last_error(void);
 
 #ifdef __cplusplus

@@ -7,6 +7,7 @@ are the exact-f32 path's (tests/test_qnet_gpu.py): Q rtol 2e-4 / atol 2e-5, loss
 gradient norm rtol 2e-4, gradients rtol 2e-3 (atol 1e-5 of the tensor's scale), Adam
 updates as test_learn_steps_match_torch_adam. Dropout: explicit keep masks (the same
 tensor on both sides) or p = 0."""
+import numpy as np
 import pytest
 import torch
 import torch.nn.functional as F
@@ -264,3 +265,53 @@ def test_fused_learn_chain_matches_separate_launches(hook):
     for got, want in zip(fus["packed"], (lr.fast.w1b, lr.fast.w1l, lr.fast.b1c, lr.fast.w2b, lr.fast.w2l,
                                          lr.fast.w2t, lr.fast.w2tl)):
         assert torch.equal(got, want)
+
+
+def test_x3_act_static_table_and_env_order():
+    """x3 act fast path: rows whose fire has reached the layout's last step start fc1 from the
+    per-centre table of the static features (evx_qmlp_stat, x3) and add the occupancy columns
+    (hi + lo weights); VecEnv.act_perm visits those envs first so act tiles are uniform.
+    Against the plain x3 act on the same observations: Q within f32 reassociation (and not
+    bit-identical on the table rows: the table path ran), greedy actions equal, epsilon draws
+    and dropout rows keyed by the original row (epsilon = 1: identical actions); act_perm is
+    the stable partition of the envs by fire step >= t_max."""
+    _need_gpu()
+    from evacx.qnet import DROPOUT_P, Learner
+    lay, env = _env_obs(E=256, R=4)
+    E, R, n = 256, 4, 256 * 4
+    t_max = int(lay.c.t_max)
+    sat = torch.tensor([e % 3 != 0 for e in range(E)], device="cuda")
+    # envs past the fire's last step: their scalar fire step and their observations' fire step
+    env.scal.view(E, 4)[:, 0] = torch.where(sat, torch.full_like(env.scal.view(E, 4)[:, 0], t_max),
+                                            env.scal.view(E, 4)[:, 0])
+    ob = env.obs.view(E, R, 8)
+    ob[:, :, 6] = torch.where(sat[:, None], torch.full_like(ob[:, :, 6], t_max), ob[:, :, 6])
+    perm = torch.full((E,), -1, dtype=torch.int32, device="cuda")
+    env.act_perm(perm)
+    torch.cuda.synchronize()
+    s = sat.cpu().numpy()
+    want = np.concatenate([np.nonzero(s)[0], np.nonzero(~s)[0]])
+    assert np.array_equal(perm.cpu().numpy(), want)
+    lr = Learner(kind="mlp", precision="f32", seed=3)
+    fast = lr.fast
+    obs = env.obs.view(-1)
+    res = {}
+    for mode in ("plain", "table"):
+        if mode == "table":
+            fast.attach_static(lay.c, int(lay.c.L), int(lay.c.W), t_max)
+        kw = dict(perm=perm, rows_per_env=R) if mode == "table" else {}
+        q = torch.empty(n, 5, device="cuda")
+        a0 = torch.empty(n, dtype=torch.int32, device="cuda")
+        a1 = torch.empty(n, dtype=torch.int32, device="cuda")
+        fast.act(lay.c, obs, n, drop=(9, 4, DROPOUT_P), q=q, actions=a0, epsilon=0.0, **kw)
+        fast.act(lay.c, obs, n, drop=(9, 4, DROPOUT_P), actions=a1, epsilon=1.0, act_seed=5, act_offset=77, **kw)
+        torch.cuda.synchronize()
+        res[mode] = (q, a0, a1)
+    (qp, ap0, ap1), (qt, at0, at1) = res["plain"], res["table"]
+    scale = qp.abs().max().item()
+    assert (qt - qp).abs().max().item() <= 2e-5 * scale
+    rows_sat = sat.repeat_interleave(R)
+    assert not torch.equal(qt[rows_sat], qp[rows_sat])  # the table path ran on those rows
+    assert torch.equal(qt[~rows_sat], qp[~rows_sat])    # the full path, same rows: bit for bit
+    assert (at0 == ap0).float().mean().item() >= 0.99
+    assert torch.equal(at1, ap1)

@@ -1,0 +1,44 @@
+#!/usr/bin/env python3
+"""Microbenchmark of the f32-accurate (x3) fused act (evx_qmlp_act -> qact3_kernel) on
+observations of a stepped 128x128 env batch, tiled to --rows rows; prints us per act and the
+bf16-MFMA rate of its products (fc1: 640 hi*hi + 512 hi*lo K, fc2: 3 x 512 K)."""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "dqn-marl_amd"))
+import torch  # noqa: E402
+
+from evacx.env import DeviceLayout, VecEnv  # noqa: E402
+from evacx.layout import build_tables, synthetic  # noqa: E402
+from evacx.qnet import DROPOUT_P, Learner  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--rows", type=int, default=1 << 19)
+ap.add_argument("--iters", type=int, default=20)
+args = ap.parse_args()
+E, R = 4096, 16
+lay = DeviceLayout(build_tables(synthetic(128, 128, R)), 2276)
+env = VecEnv(lay, E)
+env.seed([1 + i for i in range(E)])
+env.reset()
+for _ in range(200):
+    env.step(torch.randint(0, 5, (E * R,), device="cuda", dtype=torch.int32))
+obs = env.obs.view(-1, 8)
+reps = (args.rows + obs.shape[0] - 1) // obs.shape[0]
+obs = obs.repeat(reps, 1)[:args.rows].contiguous()
+lr = Learner(kind="mlp", precision="f32", seed=1)
+act = torch.empty(args.rows, dtype=torch.int32, device="cuda")
+for i in range(3):
+    lr.fast.act(lay.c, obs.view(-1), args.rows, drop=(1, i, DROPOUT_P), actions=act, epsilon=0.1)
+torch.cuda.synchronize()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record()
+for i in range(args.iters):
+    lr.fast.act(lay.c, obs.view(-1), args.rows, drop=(1, i, DROPOUT_P), actions=act, epsilon=0.1)
+e1.record()
+torch.cuda.synchronize()
+us = e0.elapsed_time(e1) / args.iters * 1e3
+fl = args.rows * 2 * (512 * (640 + 512) + 256 * 512 * 3)
+print(f"rows {args.rows}: {us:.1f} us per act, {fl / us / 1e6:.0f} TF/s of bf16 MFMA products "
+      f"({fl / us / 1e6 / 2500:.1%} of 2.5 PF)")

@@ -59,7 +59,7 @@ def main():
            "Commands: `tools/profile_r2.sh` -- `bench.py --steps 20 --warmup 5` (the driver's command) and, per "
            "episode phase, `rocprofv3 --kernel-trace --stats` / `--pmc FETCH_SIZE` / `--pmc WRITE_SIZE` of "
            "`bench.py --steps 20 --warmup 5 --no-cpu --other-steps 0 --env-steps 0 --start-steps 0 --phase <phase>` "
-           "(cfg3 per-GPU share: 128x128, P=2276, R=16, 4096 envs, strict schedule, f32 Q-net).", ""]
+           "(cfg3: 128x128, P=2276, R=16, the bench's envs per GPU (bench line), strict schedule, f32 Q-net).", ""]
     b = bench_line(os.path.join(src, "bench.json"))
     if b:
         shutil.copy(os.path.join(src, "bench.json"), os.path.join(dst, f"bench_{tag}.json"))
@@ -97,8 +97,10 @@ def main():
             out.append(f"| `{short(k)}` | {cnt} | {avg / 1e3:.1f} |")
         out.append("")
         kern_us = sum(e - s for s, e in env[-n:]) / n / 1e3
-        fetch = pmc(os.path.join(src, f"fetch_{phase}", "run_counter_collection.csv"), "FETCH_SIZE")[-n:]
-        write = pmc(os.path.join(src, f"write_{phase}", "run_counter_collection.csv"), "WRITE_SIZE")[-n:]
+        fp = os.path.join(src, f"fetch_{phase}", "run_counter_collection.csv")
+        wp = os.path.join(src, f"write_{phase}", "run_counter_collection.csv")
+        fetch = pmc(fp, "FETCH_SIZE")[-n:] if os.path.exists(fp) else []
+        write = pmc(wp, "WRITE_SIZE")[-n:] if os.path.exists(wp) else []
         if fetch and write:
             E = bl["config"]["envs_per_gpu"] if bl else 4096
             f_kib, w_kib = sum(fetch) / len(fetch), sum(write) / len(write)
