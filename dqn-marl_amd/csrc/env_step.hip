@@ -2242,20 +2242,15 @@ __global__ __launch_bounds__(64 * NWB, EVX_ENV_MINW) void env_step_kernel(evx_la
     const int words = step_lds_words(lay);
     const int H = (NWB == WNW && st.order && hcap > 0) ? min(hcap, st.order[st.E]) : 0;
     // light envs order[H, E): the last nt of them go to the heavy workgroups' spare waves
-    // (only when one launch steps them all: part 0)
+    // (only when one launch steps them all: part 0). Each step_env variant has ONE call site:
+    // every inlined copy of its body costs instruction-cache space.
     const int nt = part == 0 ? min((NWB - 1) * H, st.E - H) : 0;
-    if (part == 2) {  // light envs only: no heavy workgroups in this launch
-        const int slot = H + (int)blockIdx.x * NWB + w;
-        if (slot >= st.E) return;
-        const int e = st.order ? st.order[slot] : slot;
-        step_env<false>(lay_of<MULTI>(lay, st, e), st, actions, out, e, smem + (size_t)w * words);
-        return;
-    }
-    if (part == 1 && (int)blockIdx.x >= H) return;  // heavy envs only
-    if ((int)blockIdx.x < H) {
+    const bool heavy = part != 2 && (int)blockIdx.x < H;
+    if (part == 1 && !heavy) return;  // heavy envs only
+    int slot = -1;                    // this wave's light env slot in the order
+    if (heavy) {
         const int e = st.order[blockIdx.x];
         if (pslots > 0) __builtin_amdgcn_s_setprio(2);
-        int slot = -1;
         if (w == 0) {
             step_env<true>(lay_of<MULTI>(lay, st, e), st, actions, out, e, smem);
         } else {
@@ -2266,16 +2261,16 @@ __global__ __launch_bounds__(64 * NWB, EVX_ENV_MINW) void env_step_kernel(evx_la
             if (t < nt) slot = st.E - nt + t;
         }
         if (pslots > 0) __builtin_amdgcn_s_setprio(0);
-        if (slot >= 0) {
-            const int e2 = st.order[slot];
-            step_env<false>(lay_of<MULTI>(lay, st, e2), st, actions, out, e2, smem + (size_t)w * words);
+    } else {
+        slot = part == 2 ? H + (int)blockIdx.x * NWB + w : H + ((int)blockIdx.x - H) * NWB + w;
+        if (slot >= (part == 2 ? st.E : st.E - nt)) {
+            slot = -1;
+        } else if (part != 2 && __builtin_amdgcn_readfirstlane(slot) < H + pslots) {
+            // s_setprio ignores EXEC: the condition must be provably wave-uniform (readfirstlane)
+            __builtin_amdgcn_s_setprio(1);
         }
-        return;
     }
-    const int slot = H + ((int)blockIdx.x - H) * NWB + w;
-    if (slot >= st.E - nt) return;
-    // s_setprio ignores EXEC: the condition must be provably wave-uniform (readfirstlane)
-    if (__builtin_amdgcn_readfirstlane(slot) < H + pslots) __builtin_amdgcn_s_setprio(1);
+    if (slot < 0) return;
     const int e = st.order ? st.order[slot] : slot;
     step_env<false>(lay_of<MULTI>(lay, st, e), st, actions, out, e, smem + (size_t)w * words);
 }
