@@ -2528,7 +2528,18 @@ int evx_env_step_part(const evx_layout* l, const evx_state* s, const int32_t* ac
         const char* v = getenv("EVX_STEP_NWB");
         nwb_env = v ? atoi(v) : 0;
     }
-    int nwb = nwb_env == 1 || nwb_env == 2 || nwb_env == 4 ? nwb_env : 4;
+    // Default: 4-wave workgroups with the heavy-env path while a launch is short enough for
+    // its heaviest env to set its length (fewer than 32 envs per CU); one-wave workgroups
+    // beyond, where throughput rules: a wave's VGPRs and LDS free the moment its env is done
+    // instead of when the slowest of four is (32768 envs: env_step 1.50 -> 1.31 ms).
+    static int ncu = 0;
+    if (ncu <= 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+            ncu = 256;
+    }
+    int nwb = nwb_env == 1 || nwb_env == 2 || nwb_env == 4 ? nwb_env : (s->E >= 32 * ncu ? 1 : 4);
     while (nwb > 1 && step_launch_lds(*l, nwb) > 160 * 1024) nwb >>= 1;
     int hmin = 0;
     const int hcap = (nwb == evx::WNW && s->order) ? heavy_cap(*l, &hmin) : 0;

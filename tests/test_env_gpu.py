@@ -352,19 +352,21 @@ def test_heavy_and_light_parts_on_two_streams_match_one_launch():
     b.check_err()
 
 
-def test_stationary_mix_matches_oracle_at_bench_scale():
-    """Parity where bench.py times: the cfg3 per-GPU share (128x128, P 2276, R 16, 4096 envs)
+@pytest.mark.parametrize("E", [4096, 32768])
+def test_stationary_mix_matches_oracle_at_bench_scale(E):
+    """Parity where bench.py times: cfg3 (128x128, P 2276, R 16) at E envs -- 32768 is the bench
+    workload (one-wave workgroups), 4096 the 4-wave workgroups with the heavy-env path --
     prepared exactly as bench.py --phase stationary does (1300 env-only steps, env g force-reset
     at preparation step g % 1200: env ages spread over an episode, saturated fire, heavy and
     light envs, fused auto-resets); then 64 envs spread over the age mix are snapshotted into
     the oracle and both step 100 more steps with the same actions -- every state field, MT
-    stream, reward and done flag bit-exact on every step (the GPU steps all 4096 envs with the
+    stream, reward and done flag bit-exact on every step (the GPU steps all E envs with the
     heavy-first dispatch order, as in the bench)."""
     _need_gpu()
     from evacx.env import DeviceLayout, VecEnv
     from evacx.layout import build_tables, synthetic
     from oracle import oracle as orc
-    E, P, R, L = 4096, 2276, 16, 128
+    P, R, L = 2276, 16, 128
     tables = build_tables(synthetic(L, L, R))
     lay = DeviceLayout(tables, P)
     env = VecEnv(lay, E)
