@@ -56,7 +56,13 @@ constexpr int LEAF_CAP = 256;        // numpy pairwise leaves (n <= 16383 needs 
 constexpr int GRP_MAX = 128;         // movers of one contested target
 constexpr int GBITS = 13;            // group index bits in a sorted group head
 constexpr uint32_t DONEPK = 3u << 24;
-constexpr int GQ = 4;                // 64-person groups per pipelined iteration
+#ifndef EVX_GQ
+#define EVX_GQ 2
+#endif
+// 64-person groups per pipelined iteration of the rows loop: 2 keeps the kernel at 168 VGPRs
+// (3 waves per SIMD) -- 4 needs 218 (2 waves); one-wave workgroups gain more from the
+// occupancy than they lose in prefetch depth (env_step 1.30 -> 1.21 ms at 32768 envs)
+constexpr int GQ = EVX_GQ;
 
 struct Geo {
     int L, W, GY, G, RW, P, R;
@@ -2231,7 +2237,7 @@ __global__ __launch_bounds__(64) void env_reset_kernel(evx_layout lay, evx_state
 // the light envs' waves sharing a SIMD (s_setprio): the heavy workgroups' waves while
 // they work on their heavy env, and single-wave envs at order slots < H + pslots.
 #ifndef EVX_ENV_MINW
-#define EVX_ENV_MINW 1
+#define EVX_ENV_MINW 3
 #endif
 template <int NWB, bool MULTI>
 __global__ __launch_bounds__(64 * NWB, EVX_ENV_MINW) void env_step_kernel(evx_layout lay, evx_state st,
