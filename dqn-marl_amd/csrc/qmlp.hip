@@ -52,6 +52,9 @@ constexpr int HID = 512, HID2 = 256, NACT = 5, K1 = 726, NCELL = 121;
 constexpr int K1P = 512, KC1 = 32, NKC1 = K1P / KC1;
 constexpr int K1X = 640, NKC1X = K1X / KC1;  // X3: + the danger residual slot of every cell
 constexpr int CENTRE_COL = 60 * 6 + 5;
+// the flat parameter buffer (state_dict order: fc1.weight, fc1.bias, fc2.weight, fc2.bias, fc3.*)
+constexpr int NPAR = HID * K1 + HID + HID2 * HID + HID2 + NACT * HID2 + NACT;
+constexpr int OB1 = HID * K1, OW2 = OB1 + HID, OB2 = OW2 + HID2 * HID, OW3 = OB2 + HID2, OB3 = OW3 + NACT * HID2;
 constexpr int RM = 64;  // rows per workgroup (fc23, backward)
 // reference column (of the 726) of compact feature k < 4 * NCELL
 __host__ __device__ __forceinline__ int ref_col(int k) { return (k >> 2) * 6 + (k & 3) + 1; }
@@ -172,11 +175,56 @@ struct Fwd {
     // perm[i / rpe] * rpe + i % rpe (dropout rows and epsilon draws keep the original row)
     const int32_t* perm;
     int rpe;
+    // grouped act (evx_qmlp_act_g): gn nets interleaved in the shared row buffers -- batch row i
+    // of net g reads / writes row i * gn + g (0: not interleaved)
+    int gn, g;
 };
 __device__ __forceinline__ int orow(const Fwd& a, int row) {
-    if (!a.perm) return row;
-    const int s = row / a.rpe;
-    return a.perm[s] * a.rpe + (row - s * a.rpe);
+    int r = row;
+    if (a.perm) {
+        const int s = row / a.rpe;
+        r = a.perm[s] * a.rpe + (row - s * a.rpe);
+    }
+    return a.gn ? r * a.gn + a.g : r;
+}
+// dropout hash row of batch row `row` (+ drop_row0): the data row, except in a grouped act,
+// where it is the net's own batch row (row pairs stay hash pairs)
+__device__ __forceinline__ int krow(const Fwd& a, int row) { return a.gn ? row : orow(a, row); }
+
+template <typename T>
+__device__ __forceinline__ T* adv(T* p, size_t n) { return p ? p + n : p; }
+// Grouped launches (evx_qmlp_*_g, SURVEY §8f F3: independent nets per robot): every per-net
+// buffer is an array [nets][one net's buffer], so net g's view is net 0's pointers advanced by
+// g x the one-net size. x3 operand layout. Blocked problems (the learner) own rows
+// [g N, (g + 1) N) of the row buffers; an interleaved one (the act, gn > 0) shares them. The
+// dropout rows of net g are keyed g N + row.
+__device__ __forceinline__ Fwd fwd_net(const Fwd& a0, int g) {
+    Fwd a = a0;
+    const size_t G = (size_t)g, N = (size_t)a.N;
+    a.w1 += G * HID * K1X;
+    a.w1l = adv(a.w1l, G * HID * K1P);
+    a.w2 += G * HID2 * HID;
+    a.w2l = adv(a.w2l, G * HID2 * HID);
+    a.b1 += G * HID;
+    a.b2 += G * NPAR;
+    a.w3 += G * NPAR;
+    a.b3 += G * NPAR;
+    a.w1o = adv(a.w1o, G * HID * 128);
+    a.w1ol = adv(a.w1ol, G * HID * 128);
+    a.drop_row0 += (uint32_t)(G * N);
+    if (a.gn) {
+        a.g = g;
+        return a;
+    }
+    a.obs += G * N;
+    a.h1 = adv(a.h1, G * 2 * N * HID);
+    a.h1l = a.h1 ? a.h1 + N * HID : nullptr;
+    a.x = adv(a.x, G * N * K1X);
+    a.h2 = adv(a.h2, G * N * HID2);
+    a.q = adv(a.q, G * N * NACT);
+    a.actions = adv(a.actions, G * N);
+    a.drop_mask = adv(a.drop_mask, G * N * HID);
+    return a;
 }
 
 // One row's window in the static feature map (evx_layout.obs_feat): base index of
@@ -319,6 +367,7 @@ __device__ __forceinline__ void fc1_tile(const Fwd& a, int m0, int ncol0, bool w
     if constexpr (AH == 2) loadB(1, bn);
     loadL(0, lc);
     __syncthreads();
+#pragma unroll 2
     for (int kc = 0; kc < NKC; kc++) {
         const int buf = kc & 1;
         if (kc + AH < NKC) loadB(kc + AH, AH == 2 ? bf : bn);
@@ -361,29 +410,39 @@ __device__ __forceinline__ void fc1_tile(const Fwd& a, int m0, int ncol0, bool w
 // fc1 epilogue of one 32-row slab: bias (centre channel folded in), ReLU, dropout
 // (one hash per row pair), bf16 into dst[row within slab][column within tile]
 // (X3: hi into dst, lo into dstl). An explicit keep mask (a.drop_mask) replaces the hash.
-template <int NTW, int LD, bool X3 = false>
-__device__ __forceinline__ void fc1_slab(const Fwd& a, const f32x16 (&accm)[NTW], const float (&bias)[NTW],
-                                         int row0, int col0, int cl0, __bf16 (*dst)[LD], __bf16 (*dstl)[LD] = nullptr) {
+// MODE 0: no dropout, 1: the hash, 2: an explicit keep mask (a.drop_mask: the reference's
+// captured torch masks, tests). One straight-line body per mode: a per-element branch on the
+// mode inside the unrolled loops split it into many blocks and cost the act kernel ~100 VGPRs
+// of spills.
+// phs (MODE 1, or NULL): the row-pair hashes of the slab's 16 pairs, precomputed (the act: the
+// same hashes serve both column halves, and computing them here hoisted 32 row lookups into
+// registers)
+template <int NTW, int LD, bool X3, int MODE>
+__device__ __forceinline__ void fc1_slab_m(const Fwd& a, const f32x16 (&accm)[NTW], const float (&bias)[NTW],
+                                           int row0, int col0, int cl0, __bf16 (*dst)[LD], __bf16 (*dstl)[LD],
+                                           const uint32_t* phs = nullptr) {
     const int lane = threadIdx.x & 63, h = lane >> 5;
 #pragma unroll
     for (int r = 0; r < 16; r += 2) {  // rows rl, rl + 1: one dropout hash per pair
         const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;
         // rows rl, rl + 1 (rl even) stay a pair under the act permutation (rpe even)
-        const uint32_t ph =
-            a.drop_thresh ? drop_row(a.drop_seed, a.drop_stream, (a.drop_row0 + (uint32_t)orow(a, row0 + rl)) >> 1) : 0u;
+        uint32_t ph = 0u;
+        if constexpr (MODE == 1)
+            ph = phs ? phs[rl >> 1]
+                     : drop_row(a.drop_seed, a.drop_stream, (a.drop_row0 + (uint32_t)krow(a, row0 + rl)) >> 1);
 #pragma unroll
         for (int nt = 0; nt < NTW; nt++) {
             const int cl = cl0 + nt * 32 + (lane & 31);
             float v0 = accm[nt][r] + bias[nt], v1 = accm[nt][r + 1] + bias[nt];
             v0 = v0 > 0.f ? v0 : 0.f;
             v1 = v1 > 0.f ? v1 : 0.f;
-            if (a.drop_mask) {  // the reference's captured torch mask (tests)
+            if constexpr (MODE == 2) {
                 const int r0 = row0 + rl, c = col0 + cl;
                 const bool k0 = r0 < a.N && a.drop_mask[(size_t)r0 * HID + c];
                 const bool k1 = r0 + 1 < a.N && a.drop_mask[(size_t)(r0 + 1) * HID + c];
                 v0 = k0 ? v0 * a.drop_scale : 0.f;
                 v1 = k1 ? v1 * a.drop_scale : 0.f;
-            } else if (a.drop_thresh) {
+            } else if constexpr (MODE == 1) {
                 const uint32_t hh = drop_pair(ph, (uint32_t)(col0 + cl));
                 v0 = (hh & 0xffffu) >= a.drop_thresh ? v0 * a.drop_scale : 0.f;
                 v1 = (hh >> 16) >= a.drop_thresh ? v1 * a.drop_scale : 0.f;
@@ -398,14 +457,27 @@ __device__ __forceinline__ void fc1_slab(const Fwd& a, const f32x16 (&accm)[NTW]
         }
     }
 }
+// fc1 epilogue of one 32-row slab: bias (centre channel folded in), ReLU, dropout
+// (one hash per row pair), bf16 into dst[row within slab][column within tile]
+// (X3: hi into dst, lo into dstl). An explicit keep mask (a.drop_mask) replaces the hash.
+template <int NTW, int LD, bool X3 = false>
+__device__ __forceinline__ void fc1_slab(const Fwd& a, const f32x16 (&accm)[NTW], const float (&bias)[NTW],
+                                         int row0, int col0, int cl0, __bf16 (*dst)[LD], __bf16 (*dstl)[LD] = nullptr) {
+    if (a.drop_mask) fc1_slab_m<NTW, LD, X3, 2>(a, accm, bias, row0, col0, cl0, dst, dstl);
+    else if (a.drop_thresh) fc1_slab_m<NTW, LD, X3, 1>(a, accm, bias, row0, col0, cl0, dst, dstl);
+    else fc1_slab_m<NTW, LD, X3, 0>(a, accm, bias, row0, col0, cl0, dst, dstl);
+}
 
 // H1 = dropout(relu(X W1^T + b1)) -> bf16 [N][512] (and X when a.x). Act batches:
 // <4, 2, 8> (128 rows x all 512 columns: every row expanded once); learner batches
 // <2, 1, 4> (64 x 128). H1 is staged per 32-row slab through LDS so it leaves in
 // 16-B row segments.
-template <int MT, int NTW, int NWV, bool X3 = false>
-__global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void qfc1_kernel(Fwd a0, Fwd a1) {
-    const Fwd& a = blockIdx.z ? a1 : a0;  // two independent problems in one launch (online / target)
+// GR (grouped, blocked): blockIdx.z = net * np + problem, net g's view of the problem
+template <int MT, int NTW, int NWV, bool X3 = false, bool GR = false>
+__global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void qfc1_kernel(Fwd a0, Fwd a1, int np) {
+    Fwd ag;
+    if constexpr (GR) ag = fwd_net((int)blockIdx.z % np ? a1 : a0, (int)blockIdx.z / np);
+    const Fwd& a = GR ? ag : (blockIdx.z ? a1 : a0);  // two independent problems in one launch (online / target)
     constexpr int NT = 64 * NWV, RT = 32 * MT, NW = 32 * NTW * NWV;
     constexpr int APAD = KC1 + 8, CPAD = NW + 8;
     constexpr int ABYTES = 2 * RT * APAD * 2, CBYTES = (X3 ? 2 : 1) * 32 * CPAD * 2;
@@ -460,6 +532,7 @@ __device__ __forceinline__ void fc3_act(const Fwd& a, const float* hrow, const f
     for (int t = 0; t < NACT; t++) qv[t] = 0.f;
     // part p takes columns p, p + 4, ...: with a row pitch of 4 (mod 32) words the 32 lanes
     // of a half-wave (8 rows x 4 parts) read 32 distinct banks, and W3s is one bank per part
+#pragma unroll 4  // fully unrolled, its 64 + 320 LDS loads were hoisted together (act kernel spills)
     for (int j = 0; j < HID2 / 4; j++) {
         const int n = part + 4 * j;
         const float hv = hrow[n];
@@ -657,17 +730,27 @@ constexpr int A3_HP = 256 + 8;                     // H1 half-plane row pitch (b
 constexpr int A3_HBYTES = 2 * 128 * A3_HP * 2;     // 135,168: both planes
 static_assert(A3_HBYTES >= 128 * ACT_H2P * 4, "H2 overlays the H1 planes");
 static_assert(A3_HBYTES >= 2 * 128 * (KC1 + 8) * 2, "fc1 A staging overlays the H1 planes");
-constexpr int ACT3_LDS = A3_HBYTES + NACT * HID2 * 4 + 128 * 4;  // + W3 + window centres
-__global__ __launch_bounds__(512, 1) void qact3_kernel(Fwd a) {
+constexpr int ACT3_LDS = A3_HBYTES + NACT * HID2 * 4 + 128 * 4 + 64 * 4;  // + W3 + window centres + pair hashes
+// GR: grouped act, blockIdx.y = net (interleaved rows); DM: the dropout mode (fc1_slab_m)
+template <bool GR = false, int DM = 1>
+__global__ __launch_bounds__(512, 1) void qact3_kernel(Fwd a0) {
+    Fwd ag;
+    if constexpr (GR) ag = fwd_net(a0, (int)blockIdx.y);
+    const Fwd& a = GR ? ag : a0;
     extern __shared__ __attribute__((aligned(16))) char dsm[];
     auto Hh = reinterpret_cast<__bf16 (*)[A3_HP]>(dsm);
     auto Hl = reinterpret_cast<__bf16 (*)[A3_HP]>(dsm + 128 * A3_HP * 2);
     auto H2s = reinterpret_cast<float (*)[ACT_H2P]>(dsm);
     auto W3s = reinterpret_cast<float (*)[HID2]>(dsm + A3_HBYTES);
     int* posS = reinterpret_cast<int*>(dsm + A3_HBYTES + NACT * HID2 * 4);
+    uint32_t* phS = reinterpret_cast<uint32_t*>(dsm + A3_HBYTES + NACT * HID2 * 4 + 128 * 4);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
     const int m0 = blockIdx.x * 128;
     for (int i = tid; i < NACT * HID2; i += 512) W3s[i / HID2][i % HID2] = a.w3[i];
+    if (DM == 1 && tid >= 448) {  // the tile's 64 row-pair dropout hashes (published by the barriers below)
+        const int r2 = m0 + 2 * (tid - 448);
+        phS[tid - 448] = r2 < a.N ? drop_row(a.drop_seed, a.drop_stream, (a.drop_row0 + (uint32_t)krow(a, r2)) >> 1) : 0u;
+    }
     bool fast = false;
     if (a.stat) {  // tile-uniform: every row at the table's fire step, centre inside the map
         bool ok = true;
@@ -683,75 +766,71 @@ __global__ __launch_bounds__(512, 1) void qact3_kernel(Fwd a) {
         }
         fast = __syncthreads_and(ok);  // also publishes posS
     }
-    f32x16 acc[4][2];
-    if (fast) {
-        // fc1 = table[centre] (f32: static features x W1 + b1, x3-accurate) + the occupancy
-        // columns x bits (K = 128 cells; bits exact in bf16: hi and lo weights, 2 MFMAs)
-#pragma unroll
-        for (int mt = 0; mt < 4; mt++)
-#pragma unroll
-            for (int r = 0; r < 16; r++) {
-                const int rl = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                const float* srow = a.stat + (size_t)posS[rl] * HID + w * 32 + (lane & 31);
-                acc[mt][0][r] = srow[0];
-                acc[mt][1][r] = srow[256];
-            }
-        uint32_t occ[4][4];
-#pragma unroll
-        for (int mt = 0; mt < 4; mt++) {
-            const int row = m0 + mt * 32 + (lane & 31);
-            uint4 o = make_uint4(0u, 0u, 0u, 0u);
-            if (row < a.N) o = *reinterpret_cast<const uint4*>(&a.obs[orow(a, row)].occ[0]);
-            occ[mt][0] = o.x;
-            occ[mt][1] = o.y;
-            occ[mt][2] = o.z;
-            occ[mt][3] = o.w;
-        }
-        const uint32_t one = 0x3f80u;
-#pragma unroll 2
-        for (int ks = 0; ks < 8; ks++) {  // k-step: cells 16 ks + 8 h .. + 7 of the 128
-            bf16x8 bh[2], bl[2];
-#pragma unroll
-            for (int nt = 0; nt < 2; nt++) {  // column tiles w and w + 8
-                bh[nt] = *reinterpret_cast<const bf16x8*>(a.w1o + w1o_tile(w + 8 * nt, ks >> 1, ks & 1) + lane * 8);
-                bl[nt] = *reinterpret_cast<const bf16x8*>(a.w1ol + w1o_tile(w + 8 * nt, ks >> 1, ks & 1) + lane * 8);
-            }
-            const int c0 = ks * 16 + 8 * h;  // multiple of 8: the 8 bits sit in one word
-#pragma unroll
-            for (int mt = 0; mt < 4; mt++) {
-                const uint32_t wd = (c0 >> 5) == 0 ? occ[mt][0] : (c0 >> 5) == 1 ? occ[mt][1]
-                                  : (c0 >> 5) == 2 ? occ[mt][2] : occ[mt][3];
-                const uint32_t bits = (wd >> (c0 & 31)) & 0xffu;
-                uint32_t av4[4];
-#pragma unroll
-                for (int j = 0; j < 4; j++)
-                    av4[j] = ((bits >> (2 * j)) & 1u) * one | (((bits >> (2 * j + 1)) & 1u) * one) << 16;
-                const bf16x8 av = __builtin_bit_cast(bf16x8, av4);
-#pragma unroll
-                for (int nt = 0; nt < 2; nt++) {
-                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bh[nt], acc[mt][nt], 0, 0, 0);
-                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bl[nt], acc[mt][nt], 0, 0, 0);
-                }
-            }
-        }
-    } else {
-        fc1_tile<4, 2, 8, true>(a, m0, w * 32, false, dsm, acc, 256);  // ends with a barrier: A buffers free
-    }
     f32x16 acc2[4];
 #pragma unroll
     for (int mt = 0; mt < 4; mt++)
 #pragma unroll
         for (int r = 0; r < 16; r++) acc2[mt][r] = 0.f;
+    // One column half at a time: fc1 of the half (wave w: column tile hh * 8 + w), its H1 slabs
+    // into the LDS planes, fc2 over that half of K. Only one half's fc1 accumulators are ever
+    // live (64 VGPRs; both halves at once spilled ~100 VGPRs to scratch); the full path expands
+    // the observations once per half.
 #pragma unroll
     for (int hh = 0; hh < 2; hh++) {
-        const float bias[1] = {fast ? 0.f : a.b1[hh * 256 + w * 32 + (lane & 31)]};  // the table holds the bias
+        f32x16 acc[4][1];
+        const int col0 = hh * 256 + w * 32;
+        if (fast) {
+            // fc1 = table[centre] (f32: static features x W1 + b1, x3-accurate) + the occupancy
+            // columns x bits (K = 128 cells; bits exact in bf16: hi and lo weights, 2 MFMAs)
+            uint32_t occ[4][4];  // occupancy bits of the wave's 32-row slabs
 #pragma unroll
-        for (int mt = 0; mt < 4; mt++) {
-            const f32x16 one[1] = {acc[mt][hh]};
-            fc1_slab<1, A3_HP, true>(a, one, bias, m0 + mt * 32, hh * 256, w * 32,
-                                     reinterpret_cast<__bf16 (*)[A3_HP]>(&Hh[mt * 32][0]),
-                                     reinterpret_cast<__bf16 (*)[A3_HP]>(&Hl[mt * 32][0]));
+            for (int mt = 0; mt < 4; mt++) {
+                const int row = m0 + mt * 32 + (lane & 31);
+                uint4 o = make_uint4(0u, 0u, 0u, 0u);
+                if (row < a.N) o = *reinterpret_cast<const uint4*>(&a.obs[orow(a, row)].occ[0]);
+                occ[mt][0] = o.x;
+                occ[mt][1] = o.y;
+                occ[mt][2] = o.z;
+                occ[mt][3] = o.w;
+            }
+            // 32-bit offsets from the uniform table base: one VGPR per load address, not two
+            const uint32_t cofs = (uint32_t)(col0 + (lane & 31));
+#pragma unroll
+            for (int mt = 0; mt < 4; mt++)
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    const int rl = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    acc[mt][0][r] = a.stat[(uint32_t)posS[rl] * (uint32_t)HID + cofs];
+                }
+            const uint32_t one = 0x3f80u;
+#pragma unroll 2
+            for (int ks = 0; ks < 8; ks++) {  // k-step: cells 16 ks + 8 h .. + 7 of the 128
+                const bf16x8 bh = *reinterpret_cast<const bf16x8*>(a.w1o + w1o_tile(hh * 8 + w, ks >> 1, ks & 1) + lane * 8);
+                const bf16x8 bl = *reinterpret_cast<const bf16x8*>(a.w1ol + w1o_tile(hh * 8 + w, ks >> 1, ks & 1) + lane * 8);
+                const int c0 = ks * 16 + 8 * h;  // multiple of 8: the 8 bits sit in one word
+#pragma unroll
+                for (int mt = 0; mt < 4; mt++) {
+                    const uint32_t wd = (c0 >> 5) == 0 ? occ[mt][0] : (c0 >> 5) == 1 ? occ[mt][1]
+                                      : (c0 >> 5) == 2 ? occ[mt][2] : occ[mt][3];
+                    const uint32_t bits = (wd >> (c0 & 31)) & 0xffu;
+                    uint32_t av4[4];
+#pragma unroll
+                    for (int j = 0; j < 4; j++)
+                        av4[j] = ((bits >> (2 * j)) & 1u) * one | (((bits >> (2 * j + 1)) & 1u) * one) << 16;
+                    const bf16x8 av = __builtin_bit_cast(bf16x8, av4);
+                    acc[mt][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bh, acc[mt][0], 0, 0, 0);
+                    acc[mt][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bl, acc[mt][0], 0, 0, 0);
+                }
+            }
+        } else {
+            fc1_tile<4, 1, 8, true>(a, m0, col0, false, dsm, acc);  // ends with a barrier: A buffers free
         }
+        const float bias[1] = {fast ? 0.f : a.b1[col0 + (lane & 31)]};  // the table holds the bias
+#pragma unroll
+        for (int mt = 0; mt < 4; mt++)
+            fc1_slab_m<1, A3_HP, true, DM>(a, acc[mt], bias, m0 + mt * 32, hh * 256, w * 32,
+                                           reinterpret_cast<__bf16 (*)[A3_HP]>(&Hh[mt * 32][0]),
+                                           reinterpret_cast<__bf16 (*)[A3_HP]>(&Hl[mt * 32][0]), phS + mt * 16);
         __syncthreads();
         // fc2 over K = [256 hh, 256 hh + 256): wave w -> columns [32w, 32w + 32)
         bf16x8 bc[2], bn[2], lc[2], ln[2];
@@ -802,9 +881,11 @@ __global__ __launch_bounds__(512, 1) void qact3_kernel(Fwd a) {
 
 // ------------------------------------------------------------ fc2 + fc3
 // X3: A = H1 hi / lo planes, B = fc2.weight hi / lo (3 MFMAs per fragment pair)
-template <bool X3 = false>
-__global__ __launch_bounds__(256, 2) void qfc23_kernel(Fwd a0, Fwd a1) {
-    const Fwd& a = blockIdx.z ? a1 : a0;
+template <bool X3 = false, bool GR = false>
+__global__ __launch_bounds__(256, 2) void qfc23_kernel(Fwd a0, Fwd a1, int np) {
+    Fwd ag;
+    if constexpr (GR) ag = fwd_net((int)blockIdx.z % np ? a1 : a0, (int)blockIdx.z / np);
+    const Fwd& a = GR ? ag : (blockIdx.z ? a1 : a0);
     // A stages (row pitch 40 bf16 = 20 words: conflict-free ds_read_b128), then H2 in the same
     // bytes (pitch 4 mod 32 words: fc3_act reads conflict-free)
     constexpr int AP = 40, NPL = X3 ? 2 : 1;
@@ -1026,11 +1107,38 @@ struct Bwd {
     __bf16* dz2l;
     __bf16* dz1l;
 };
+// net g's view of a blocked grouped backward (see fwd_net; x3: two planes per activation)
+__device__ __forceinline__ Bwd bwd_net(const Bwd& a0, int g) {
+    Bwd a = a0;
+    const size_t G = (size_t)g, B = (size_t)a.B;
+    a.dq += G * B * NACT;
+    a.h2 += G * B * HID2;
+    a.h1 += G * 2 * B * HID;
+    a.h1l = a.h1 + B * HID;
+    a.x += G * B * K1X;
+    a.w3 += G * NPAR;
+    a.w2t += G * HID2 * HID;
+    a.w2tl += G * HID2 * HID;
+    a.dz2 += G * 2 * B * HID2;
+    a.dz2l = a.dz2 + B * HID2;
+    a.dz1 += G * 2 * B * HID;
+    a.dz1l = a.dz1 + B * HID;
+    a.gw1 += G * NPAR;
+    a.gb1 += G * NPAR;
+    a.gw2 += G * NPAR;
+    a.gb2 += G * NPAR;
+    a.gw3 += G * NPAR;
+    a.gb3 += G * NPAR;
+    return a;
+}
 
 // fc3 backward: thread n of a 32-row block walks the rows (coalesced over n)
 constexpr int R3 = 32;
-template <bool X3 = false>
-__global__ __launch_bounds__(256) void qbwd3_kernel(Bwd a) {
+template <bool X3 = false, bool GR = false>  // GR: blockIdx.y = net
+__global__ __launch_bounds__(256) void qbwd3_kernel(Bwd a0) {
+    Bwd ag;
+    if constexpr (GR) ag = bwd_net(a0, (int)blockIdx.y);
+    const Bwd& a = GR ? ag : a0;
     __shared__ float dqs[R3][NACT];
     const int n = threadIdx.x, b0 = blockIdx.x * R3;
     for (int i = n; i < R3 * NACT; i += 256) {
@@ -1215,7 +1323,18 @@ struct GemmTN {
     float* part;
     const __bf16 *Al, *Bl;
     int gx, gy, gz;  // grid
+    int64_t gsA, gsB, gsC, gsP;  // grouped: elements between consecutive nets' A (Al), B (Bl), C, part
 };
+__device__ __forceinline__ GemmTN tn_net(const GemmTN& g0, int g) {
+    GemmTN t = g0;
+    t.A += g * t.gsA;
+    t.Al = adv(t.Al, (size_t)(g * t.gsA));
+    t.Bm += g * t.gsB;
+    t.Bl = adv(t.Bl, (size_t)(g * t.gsB));
+    t.C += g * t.gsC;
+    t.part = adv(t.part, (size_t)(g * t.gsP));
+    return t;
+}
 template <int AP, int BP>
 constexpr int gemm_tn_lds_bytes() { return (AP + BP) * TT * TPAD * 2; }
 template <int AP = 1, int BP = 1>
@@ -1336,23 +1455,30 @@ __device__ __forceinline__ void gemm_tn_body(const GemmTN& g, char* smem, int bx
             }
     }
 }
-template <int AP = 1, int BP = 1>
+template <int AP = 1, int BP = 1, bool GR = false>  // GR: blockIdx.z = net * gz + split
 __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(GemmTN g) {
     __shared__ __attribute__((aligned(16))) char smem[gemm_tn_lds_bytes<AP, BP>()];
-    gemm_tn_body<AP, BP>(g, smem, blockIdx.x, blockIdx.y, blockIdx.z);
+    if constexpr (GR) {
+        const int nz = (int)blockIdx.z / g.gz;
+        gemm_tn_body<AP, BP>(tn_net(g, nz), smem, blockIdx.x, blockIdx.y, (int)blockIdx.z - nz * g.gz);
+    } else {
+        gemm_tn_body<AP, BP>(g, smem, blockIdx.x, blockIdx.y, blockIdx.z);
+    }
 }
 // dZ1 (qdz1) and dW2 = dZ2^T H1 (gemm_tn) in one launch: both need only qbwd3's outputs. Blocks
 // [0, ndz) run qdz1 tiles (grid ndzx x HID / 128), the rest the dW2 split-K tiles; the LDS is one
 // dynamic buffer sized for the larger of the two.
-template <bool X3, int AP, int BP>
+template <bool X3, int AP, int BP, bool GR = false>  // GR: blockIdx.y = net
 __global__ __launch_bounds__(256, 2) void bwd_mid_kernel(Bwd a, int ndzx, GemmTN g) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int b = (int)blockIdx.x, ndz = ndzx * (HID / 128);
     if (b < ndz) {
-        qdz1_body<X3>(a, smem, b % ndzx, b / ndzx);
+        if constexpr (GR) qdz1_body<X3>(bwd_net(a, (int)blockIdx.y), smem, b % ndzx, b / ndzx);
+        else qdz1_body<X3>(a, smem, b % ndzx, b / ndzx);
     } else {
         const int t = b - ndz, gxy = g.gx * g.gy;
-        gemm_tn_body<AP, BP>(g, smem, t % g.gx, (t % gxy) / g.gx, t / gxy);
+        if constexpr (GR) gemm_tn_body<AP, BP>(tn_net(g, (int)blockIdx.y), smem, t % g.gx, (t % gxy) / g.gx, t / gxy);
+        else gemm_tn_body<AP, BP>(g, smem, t % g.gx, (t % gxy) / g.gx, t / gxy);
     }
 }
 
@@ -1361,8 +1487,6 @@ __global__ __launch_bounds__(256, 2) void bwd_mid_kernel(Bwd a, int ndzx, GemmTN
 // partials; fixed order). The last workgroup adds the squares of the small gradients the
 // other kernels finished (b1, the centre column of W1, b2, W3, b3); W1's channel-0 and
 // non-centre channel-5 columns stay zero.
-constexpr int NPAR = HID * K1 + HID + HID2 * HID + HID2 + NACT * HID2 + NACT;
-constexpr int OB1 = HID * K1, OW2 = OB1 + HID, OB2 = OW2 + HID2 * HID, OW3 = OB2 + HID2, OB3 = OW3 + NACT * HID2;
 struct Red2 {
     const float* part2;  // dW2 partials [S2][HID2][HID]
     int S2;
@@ -1371,6 +1495,7 @@ struct Red2 {
     float *gw1, *gb1, *gw2, *gb2, *gw3, *gb3;  // gradients
     float* ss;           // [gridDim.x] squared-norm partials, or NULL
     int nb2, nb1;        // workgroups of the two reductions
+    int64_t gsP;         // grouped (blockIdx.y = net): floats between consecutive nets' partials
 };
 __device__ __forceinline__ float red_sum256(float x, float* red) {
     red[threadIdx.x] = x;
@@ -1381,8 +1506,17 @@ __device__ __forceinline__ float red_sum256(float x, float* red) {
     }
     return red[0];
 }
-__global__ __launch_bounds__(256) void reduce2_kernel(Red2 r) {
+__global__ __launch_bounds__(256) void reduce2_kernel(Red2 r0) {
     __shared__ float red[256];
+    Red2 r = r0;
+    if (blockIdx.y) {  // grouped: net blockIdx.y's partials, gradients and norm partials
+        const size_t G = blockIdx.y;
+        r.part2 += G * r.gsP;
+        r.part1 += G * r.gsP;
+        r.gw1 += G * NPAR; r.gb1 += G * NPAR; r.gw2 += G * NPAR;
+        r.gb2 += G * NPAR; r.gw3 += G * NPAR; r.gb3 += G * NPAR;
+        r.ss = adv(r.ss, G * gridDim.x);
+    }
     const int b = (int)blockIdx.x;
     float sq = 0.f;
     if (b < r.nb2) {  // dW2: 4 columns per thread
@@ -1474,8 +1608,20 @@ __device__ __forceinline__ float adam_one(const AdamPack& a, int i, float coef) 
     a.p[i] = pn;
     return pn;
 }
-__global__ __launch_bounds__(256) void adam_pack3_kernel(AdamPack a) {
+__global__ __launch_bounds__(256) void adam_pack3_kernel(AdamPack a0) {
     __shared__ float red[256];
+    AdamPack a = a0;
+    if (blockIdx.y) {  // grouped: net blockIdx.y (clip_grad_norm_ and Adam per net)
+        const size_t G = blockIdx.y;
+        a.p += G * NPAR; a.g += G * NPAR; a.m += G * NPAR; a.v += G * NPAR;
+        a.ss += G * a.nss;
+        a.w1b += G * HID * K1X; a.w1l += G * HID * K1P;
+        a.w2b += G * HID2 * HID; a.w2l += G * HID2 * HID;
+        a.w2t = adv(a.w2t, G * HID2 * HID); a.w2tl = adv(a.w2tl, G * HID2 * HID);
+        a.w1o = adv(a.w1o, G * HID * 128); a.w1ol = adv(a.w1ol, G * HID * 128);
+        a.b1c += G * HID;
+        a.norm_out = adv(a.norm_out, G);
+    }
     float t = 0.f;
     for (int k = (int)threadIdx.x; k < a.nss; k += 256) t += a.ss[k];
     const float norm = sqrtf(red_sum256(t, red));
@@ -1601,6 +1747,18 @@ int evx_qmlp_pack3(const float* w1, const float* b1, const float* w2, uint16_t* 
     return mlaunch("qmlp_pack3");
 }
 
+// the x3 act kernel for the dropout mode of a (fc1_slab_m)
+extern "C++" template <bool GR>
+static void launch_act3(const evxm::Fwd& a, int32_t n, int nets, hipStream_t st) {
+    const dim3 grid((unsigned)((n + 127) / 128), (unsigned)nets);
+    if (a.drop_mask)
+        hipLaunchKernelGGL((evxm::qact3_kernel<GR, 2>), grid, dim3(512), evxm::ACT3_LDS, st, a);
+    else if (a.drop_thresh)
+        hipLaunchKernelGGL((evxm::qact3_kernel<GR, 1>), grid, dim3(512), evxm::ACT3_LDS, st, a);
+    else
+        hipLaunchKernelGGL((evxm::qact3_kernel<GR, 0>), grid, dim3(512), evxm::ACT3_LDS, st, a);
+}
+
 static int make_fwd(const evx_layout* lay, const evx_obs* obs, int32_t n, const evx_qmlp_params* p,
                     const evx_qmlp_dropout* drop, const evx_qmlp_fwd_out* out, evxm::Fwd& a) {
     if (!lay || !obs || !p || !out) return mfail(-22, "qmlp_forward: NULL argument");
@@ -1670,22 +1828,35 @@ static int make_fwd(const evx_layout* lay, const evx_obs* obs, int32_t n, const 
     }
     a.perm = out->perm;
     a.rpe = out->rows_per_env > 0 ? out->rows_per_env : 1;
+    a.gn = 0;
+    a.g = 0;
     if (a.perm && (a.rpe & 1)) return mfail(-22, "qmlp_forward: rows_per_env must be even (dropout row pairs)");
     return 0;
 }
 
 static int launch_fwd(const evxm::Fwd& a0, const evxm::Fwd& a1, int32_t n, int pairs, bool fc23, hipStream_t st,
-                      bool x3 = false) {
+                      bool x3 = false, int nets = 1) {
     const unsigned blocks = (unsigned)((n + evxm::RM - 1) / evxm::RM);
     const unsigned big = (unsigned)((n + 127) / 128);
+    if (nets > 1) {  // grouped (x3 only): blockIdx.z = net * pairs + problem
+        const unsigned z = (unsigned)(pairs * nets);
+        if (big * z >= 384)
+            hipLaunchKernelGGL((evxm::qfc1_kernel<4, 1, 8, true, true>), dim3(big, 2, z), dim3(512), 0, st, a0, a1, pairs);
+        else
+            hipLaunchKernelGGL((evxm::qfc1_kernel<2, 1, 4, true, true>), dim3(blocks, 4, z), dim3(256), 0, st, a0, a1, pairs);
+        int rc = mlaunch("qfc1 grouped");
+        if (rc || !fc23) return rc;
+        hipLaunchKernelGGL((evxm::qfc23_kernel<true, true>), dim3(blocks, 1, z), dim3(256), 0, st, a0, a1, pairs);
+        return mlaunch("qfc23 grouped");
+    }
     if (x3) {  // f32-accurate: 128 x 256 tiles for large batches (register budget), else 64 x 128
         if (big * pairs >= 384)
-            hipLaunchKernelGGL((evxm::qfc1_kernel<4, 1, 8, true>), dim3(big, 2, pairs), dim3(512), 0, st, a0, a1);
+            hipLaunchKernelGGL((evxm::qfc1_kernel<4, 1, 8, true>), dim3(big, 2, pairs), dim3(512), 0, st, a0, a1, pairs);
         else
-            hipLaunchKernelGGL((evxm::qfc1_kernel<2, 1, 4, true>), dim3(blocks, 4, pairs), dim3(256), 0, st, a0, a1);
+            hipLaunchKernelGGL((evxm::qfc1_kernel<2, 1, 4, true>), dim3(blocks, 4, pairs), dim3(256), 0, st, a0, a1, pairs);
         int rc = mlaunch("qfc1");
         if (rc || !fc23) return rc;
-        hipLaunchKernelGGL(evxm::qfc23_kernel<true>, dim3(blocks, 1, pairs), dim3(256), 0, st, a0, a1);
+        hipLaunchKernelGGL(evxm::qfc23_kernel<true>, dim3(blocks, 1, pairs), dim3(256), 0, st, a0, a1, pairs);
         return mlaunch("qfc23");
     }
     static int nwv = -1;  // EVX_FC1_NWV=4: 128 x 256 tiles of 4 waves (tuning)
@@ -1694,14 +1865,14 @@ static int launch_fwd(const evxm::Fwd& a0, const evxm::Fwd& a1, int32_t n, int p
         nwv = v ? atoi(v) : 8;
     }
     if (big * pairs >= 384 && nwv == 4)
-        hipLaunchKernelGGL((evxm::qfc1_kernel<4, 2, 4>), dim3(big, 2, pairs), dim3(256), 0, st, a0, a1);
+        hipLaunchKernelGGL((evxm::qfc1_kernel<4, 2, 4>), dim3(big, 2, pairs), dim3(256), 0, st, a0, a1, pairs);
     else if (big * pairs >= 384)  // enough 128-row tiles (all 512 columns each) to fill the chip
-        hipLaunchKernelGGL((evxm::qfc1_kernel<4, 2, 8>), dim3(big, 1, pairs), dim3(512), 0, st, a0, a1);
+        hipLaunchKernelGGL((evxm::qfc1_kernel<4, 2, 8>), dim3(big, 1, pairs), dim3(512), 0, st, a0, a1, pairs);
     else
-        hipLaunchKernelGGL((evxm::qfc1_kernel<2, 1, 4>), dim3(blocks, 4, pairs), dim3(256), 0, st, a0, a1);
+        hipLaunchKernelGGL((evxm::qfc1_kernel<2, 1, 4>), dim3(blocks, 4, pairs), dim3(256), 0, st, a0, a1, pairs);
     int rc = mlaunch("qfc1");
     if (rc || !fc23) return rc;
-    hipLaunchKernelGGL(evxm::qfc23_kernel<false>, dim3(blocks, 1, pairs), dim3(256), 0, st, a0, a1);
+    hipLaunchKernelGGL(evxm::qfc23_kernel<false>, dim3(blocks, 1, pairs), dim3(256), 0, st, a0, a1, pairs);
     return mlaunch("qfc23");
 }
 
@@ -1732,13 +1903,14 @@ int evx_qmlp_act(const evx_layout* lay, const evx_obs* obs, int32_t n, const evx
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)evxm::qact_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   evxm::ACT_LDS);
-        (void)hipFuncSetAttribute((const void*)evxm::qact3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  evxm::ACT3_LDS);
+        const void* ks[6] = {(const void*)evxm::qact3_kernel<false, 0>, (const void*)evxm::qact3_kernel<false, 1>,
+                             (const void*)evxm::qact3_kernel<false, 2>, (const void*)evxm::qact3_kernel<true, 0>,
+                             (const void*)evxm::qact3_kernel<true, 1>, (const void*)evxm::qact3_kernel<true, 2>};
+        for (const void* k : ks) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, evxm::ACT3_LDS);
         attr = true;
     }
     if (p->x3)
-        hipLaunchKernelGGL(evxm::qact3_kernel, dim3((unsigned)((n + 127) / 128)), dim3(512), evxm::ACT3_LDS,
-                           (hipStream_t)stream, a);
+        launch_act3<false>(a, n, 1, (hipStream_t)stream);
     else
         hipLaunchKernelGGL(evxm::qact_kernel, dim3((unsigned)((n + 127) / 128)), dim3(512), evxm::ACT_LDS,
                            (hipStream_t)stream, a);
@@ -1803,7 +1975,8 @@ int64_t evx_qmlp_nparams(void) { return evxm::NPAR; }
 
 extern "C++" {
 template <bool X3, int AP2, int BP2, int AP1, int BP1>
-static void launch_tail(const evxm::Bwd& a, int32_t B, const evx_qmlp_grads* g, float* ss, hipStream_t st) {
+static void launch_tail(const evxm::Bwd& a, int32_t B, const evx_qmlp_grads* g, float* ss, hipStream_t st,
+                        int nets = 1) {
     // dW2 = dZ2^T H1 (256 x 512); dW1 = dZ1^T X (512 x compact K -> 726); K = B split into S tiles
     evxm::GemmTN g2{a.dz2, evxm::HID2, a.h1, evxm::HID, B, evxm::HID2, evxm::HID, ksplit_kper(B, 8), g->w2, evxm::HID, 0,
                     g->part, X3 ? a.dz2l : nullptr, X3 ? a.h1l : nullptr, evxm::HID / evxm::TT, evxm::HID2 / evxm::TT, 0};
@@ -1814,6 +1987,32 @@ static void launch_tail(const evxm::Bwd& a, int32_t B, const evx_qmlp_grads* g, 
                     X3 ? a.dz1l : nullptr, nullptr, KX / evxm::TT, evxm::HID / evxm::TT, 0};
     g1.gz = (B + g1.kper - 1) / g1.kper;
     const int ndzx = (B + evxm::RM - 1) / evxm::RM;
+    if (nets > 1) {  // grouped (x3, partials): net g's operands, gradients and partials (fwd_net / bwd_net)
+        const int64_t pf = evx_qmlp_backward_part_floats(B);
+        g2.gsA = 2 * (int64_t)B * evxm::HID2;
+        g2.gsB = 2 * (int64_t)B * evxm::HID;
+        g2.gsC = evxm::NPAR;
+        g2.gsP = pf;
+        g1.gsA = 2 * (int64_t)B * evxm::HID;
+        g1.gsB = (int64_t)B * evxm::K1X;
+        g1.gsC = evxm::NPAR;
+        g1.gsP = pf;
+        constexpr int lds = std::max(evxm::qdz1_lds_bytes<X3>(), evxm::gemm_tn_lds_bytes<AP2, BP2>());
+        static bool attr_g = false;
+        if (!attr_g) {
+            (void)hipFuncSetAttribute((const void*)evxm::bwd_mid_kernel<X3, AP2, BP2, true>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+            attr_g = true;
+        }
+        const unsigned nmid = (unsigned)(ndzx * (evxm::HID / 128) + g2.gx * g2.gy * g2.gz);
+        hipLaunchKernelGGL((evxm::bwd_mid_kernel<X3, AP2, BP2, true>), dim3(nmid, nets), dim3(256), lds, st, a, ndzx, g2);
+        hipLaunchKernelGGL((evxm::gemm_tn_kernel<AP1, BP1, true>), dim3(g1.gx, g1.gy, g1.gz * nets), dim3(256), 0, st, g1);
+        evxm::Red2 r{g->part, g2.gz, g1.part, g1.gz, g1.gx * evxm::TT, 4 * evxm::NCELL, X3 ? 3 : 1,
+                     g->w1, g->b1, g->w2, g->b2, g->w3, g->b3, ss,
+                     (evxm::HID2 * evxm::HID / 4 + 255) / 256, (evxm::HID * evxm::NCELL + 255) / 256, pf};
+        hipLaunchKernelGGL(evxm::reduce2_kernel, dim3((unsigned)norm_parts(), nets), dim3(256), 0, st, r);
+        return;
+    }
     if (g->part) {
         // qdz1 and the dW2 tiles in one launch (both read only qbwd3's outputs), then the dW1
         // tiles, then both reductions + the squared-norm partials in one launch
@@ -1843,7 +2042,7 @@ static void launch_tail(const evxm::Bwd& a, int32_t B, const evx_qmlp_grads* g, 
 
 static int qmlp_backward(const evx_qmlp_params* p, int32_t B, const float* dq, const uint16_t* x, const uint16_t* h1,
                          const float* h2, float drop_p, uint16_t* dz2, uint16_t* dz1, const evx_qmlp_grads* g,
-                         int32_t zero_grads, float* ss, void* stream) {
+                         int32_t zero_grads, float* ss, void* stream, int nets = 1) {
     if (!p || !g || !dq || !x || !h1 || !h2 || !dz2 || !dz1) return mfail(-22, "qmlp_backward: NULL argument");
     if (!p->w2t || !p->w3) return mfail(-22, "qmlp_backward: w2t / w3 required");
     if (!g->w1 || !g->b1 || !g->w2 || !g->b2 || !g->w3 || !g->b3) return mfail(-22, "qmlp_backward: missing grad");
@@ -1884,6 +2083,12 @@ static int qmlp_backward(const evx_qmlp_params* p, int32_t B, const float* dq, c
         a.w2tl = reinterpret_cast<const __bf16*>(p->w2tl);
         a.dz2l = a.dz2 + (size_t)B * evxm::HID2;
         a.dz1l = a.dz1 + (size_t)B * evxm::HID;
+        if (nets > 1) {
+            hipLaunchKernelGGL((evxm::qbwd3_kernel<true, true>), dim3((unsigned)((B + evxm::R3 - 1) / evxm::R3), nets),
+                               dim3(256), 0, st, a);
+            launch_tail<true, 2, 2, 2, 1>(a, B, g, ss, st, nets);
+            return mlaunch("qmlp_backward grouped");
+        }
         hipLaunchKernelGGL(evxm::qbwd3_kernel<true>, dim3((unsigned)((B + evxm::R3 - 1) / evxm::R3)), dim3(256), 0, st, a);
         // dW2: both operands split; dW1 over the 640 x3 columns (X exact in bf16): the danger
         // residual column of a cell adds into its danger column
@@ -1914,9 +2119,28 @@ int evx_qmlp_sumsq_parts(const float* g, float* ss, void* stream) {
     return mlaunch("qmlp_sumsq_parts");
 }
 
+static int adam_pack3(float* p, float* g, float* m, float* v, float max_norm, const evx_adam* h, uint16_t* w1b,
+                      uint16_t* w1l, float* b1c, uint16_t* w2b, uint16_t* w2l, uint16_t* w2t, uint16_t* w2tl,
+                      uint16_t* w1o, uint16_t* w1ol, const float* ss, int32_t nss, float* norm_out, void* stream,
+                      int nets);
 int evx_qmlp_adam_pack3(float* p, float* g, float* m, float* v, float max_norm, const evx_adam* h, uint16_t* w1b,
                         uint16_t* w1l, float* b1c, uint16_t* w2b, uint16_t* w2l, uint16_t* w2t, uint16_t* w2tl,
                         uint16_t* w1o, uint16_t* w1ol, const float* ss, int32_t nss, float* norm_out, void* stream) {
+    return adam_pack3(p, g, m, v, max_norm, h, w1b, w1l, b1c, w2b, w2l, w2t, w2tl, w1o, w1ol, ss, nss, norm_out,
+                      stream, 1);
+}
+int evx_qmlp_adam_pack3_g(float* p, float* g, float* m, float* v, float max_norm, const evx_adam* h, uint16_t* w1b,
+                          uint16_t* w1l, float* b1c, uint16_t* w2b, uint16_t* w2l, uint16_t* w2t, uint16_t* w2tl,
+                          uint16_t* w1o, uint16_t* w1ol, const float* ss, int32_t nss, float* norm_out, int32_t nets,
+                          void* stream) {
+    if (nets < 1 || nets > 1024) return mfail(-22, "qmlp_adam_pack3_g: nets must be 1..1024");
+    return adam_pack3(p, g, m, v, max_norm, h, w1b, w1l, b1c, w2b, w2l, w2t, w2tl, w1o, w1ol, ss, nss, norm_out,
+                      stream, nets);
+}
+static int adam_pack3(float* p, float* g, float* m, float* v, float max_norm, const evx_adam* h, uint16_t* w1b,
+                      uint16_t* w1l, float* b1c, uint16_t* w2b, uint16_t* w2l, uint16_t* w2t, uint16_t* w2tl,
+                      uint16_t* w1o, uint16_t* w1ol, const float* ss, int32_t nss, float* norm_out, void* stream,
+                      int nets) {
     if ((w1o == nullptr) != (w1ol == nullptr)) return mfail(-22, "qmlp_adam_pack3: w1o and w1ol go together");
     if (!p || !g || !m || !v || !h || !w1b || !w1l || !b1c || !w2b || !w2l || !ss)
         return mfail(-22, "qmlp_adam_pack3: NULL argument");
@@ -1936,9 +2160,77 @@ int evx_qmlp_adam_pack3(float* p, float* g, float* m, float* v, float max_norm, 
     a.w2t = reinterpret_cast<__bf16*>(w2t); a.w2tl = reinterpret_cast<__bf16*>(w2tl);
     a.b1c = b1c; a.norm_out = norm_out;
     a.w1o = reinterpret_cast<__bf16*>(w1o); a.w1ol = reinterpret_cast<__bf16*>(w1ol);
-    hipLaunchKernelGGL(evxm::adam_pack3_kernel, dim3((unsigned)((evxm::NPAR + 255) / 256)), dim3(256), 0,
+    hipLaunchKernelGGL(evxm::adam_pack3_kernel, dim3((unsigned)((evxm::NPAR + 255) / 256), nets), dim3(256), 0,
                        (hipStream_t)stream, a);
     return mlaunch("qmlp_adam_pack3");
+}
+
+// ------------------------------------------------ grouped nets
+// Every per-net buffer is an array [nets][one net's buffer]: the pointers passed are net 0's.
+static int group_check(int32_t nets, const evx_qmlp_params* p, const char* what) {
+    if (nets < 1 || nets > 1024) return mfail(-22, "grouped qmlp: nets must be 1..1024");
+    if (!p || !p->x3) return mfail(-22, "grouped qmlp: x3 parameters required (the [nets] operand layout is x3's)");
+    (void)what;
+    return 0;
+}
+
+int evx_qmlp_act_g(const evx_layout* lay, const evx_obs* obs, int32_t n, int32_t nets, const evx_qmlp_params* p,
+                   const evx_qmlp_dropout* drop, const evx_qmlp_fwd_out* out, void* stream) {
+    int rc = group_check(nets, p, "act");
+    if (rc) return rc;
+    if (n <= 0) return 0;
+    if (!out || (!out->q && !out->actions)) return mfail(-22, "qmlp_act_g: needs q or actions");
+    if (out->perm) return mfail(-22, "qmlp_act_g: no act permutation with grouped nets");
+    if (p->stat) return mfail(-22, "qmlp_act_g: the act table path is single-net");
+    if (n & 1) return mfail(-22, "qmlp_act_g: rows per net must be even (dropout row pairs)");
+    evx_qmlp_fwd_out o = *out;
+    o.h1 = reinterpret_cast<uint16_t*>(1);
+    o.x = nullptr;
+    o.h2 = nullptr;
+    evxm::Fwd a;
+    rc = make_fwd(lay, obs, n, p, drop, &o, a);
+    if (rc) return rc;
+    a.h1 = nullptr;
+    a.h1l = nullptr;
+    a.gn = nets;
+    static bool attr = false;
+    if (!attr) {
+        const void* ks[3] = {(const void*)evxm::qact3_kernel<true, 0>, (const void*)evxm::qact3_kernel<true, 1>,
+                             (const void*)evxm::qact3_kernel<true, 2>};
+        for (const void* k : ks) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, evxm::ACT3_LDS);
+        attr = true;
+    }
+    launch_act3<true>(a, n, nets, (hipStream_t)stream);
+    return mlaunch("qact_g");
+}
+
+int evx_qmlp_forward2_g(const evx_layout* lay, int32_t n, int32_t nets, const evx_obs* obs0, const evx_qmlp_params* p0,
+                        const evx_qmlp_dropout* drop0, const evx_qmlp_fwd_out* out0, const evx_obs* obs1,
+                        const evx_qmlp_params* p1, const evx_qmlp_dropout* drop1, const evx_qmlp_fwd_out* out1,
+                        void* stream) {
+    int rc = group_check(nets, p0, "forward2");
+    if (!rc) rc = group_check(nets, p1, "forward2");
+    if (rc) return rc;
+    if (n <= 0) return 0;
+    if (n & 1) return mfail(-22, "qmlp_forward2_g: rows per net must be even (dropout row pairs)");
+    evxm::Fwd a0, a1;
+    rc = make_fwd(lay, obs0, n, p0, drop0, out0, a0);
+    if (!rc) rc = make_fwd(lay, obs1, n, p1, drop1, out1, a1);
+    if (rc) return rc;
+    if (a0.stat || a1.stat || a0.perm || a1.perm) return mfail(-22, "qmlp_forward2_g: no table path / permutation");
+    if (!(out0->q || out0->h2) || !(out1->q || out1->h2)) return mfail(-22, "qmlp_forward2_g: needs fc2/fc3 outputs");
+    if ((int64_t)n * nets * 2 > (int64_t)1 << 31) return mfail(-22, "qmlp_forward2_g: too many rows");
+    return launch_fwd(a0, a1, n, 2, true, (hipStream_t)stream, true, nets);
+}
+
+int evx_qmlp_backward_ss_g(const evx_qmlp_params* p, int32_t B, int32_t nets, const float* dq, const uint16_t* x,
+                           const uint16_t* h1, const float* h2, float drop_p, uint16_t* dz2, uint16_t* dz1,
+                           const evx_qmlp_grads* g, float* ss, void* stream) {
+    int rc = group_check(nets, p, "backward");
+    if (rc) return rc;
+    if (!g || !g->part) return mfail(-22, "qmlp_backward_ss_g: split-K partials required ([nets][part floats(B)])");
+    if (!ss) return mfail(-22, "qmlp_backward_ss_g: NULL ss");
+    return qmlp_backward(p, B, dq, x, h1, h2, drop_p, dz2, dz1, g, 0, ss, stream, nets);
 }
 
 }  // extern "C"

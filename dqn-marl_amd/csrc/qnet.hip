@@ -272,7 +272,7 @@ __global__ __launch_bounds__(256) void colsum_finish(const float* __restrict__ p
 // One row per thread over many blocks; the last block to finish sums the block
 // partials in block order (deterministic).
 __device__ float g_td_part[4096];
-__device__ unsigned int g_td_ticket = 0;
+__device__ unsigned int g_td_ticket[64];  // one per net of a grouped launch (blockIdx.y)
 __global__ __launch_bounds__(256) void td_loss_kernel(const float* __restrict__ Q, const float* __restrict__ Qt,
                                                       int A, const int32_t* __restrict__ act,
                                                       const float* __restrict__ rew, const uint8_t* __restrict__ done,
@@ -283,11 +283,26 @@ __global__ __launch_bounds__(256) void td_loss_kernel(const float* __restrict__ 
     __shared__ float red[256];
     __shared__ bool last;
     if (zero && (int)blockIdx.x >= ntd) {  // the extra workgroups clear the gradient buffer for the backward
+        if (blockIdx.y) return;
         const int64_t z0 = ((int64_t)blockIdx.x - ntd) * 256 + threadIdx.x, zs = ((int64_t)gridDim.x - ntd) * 256;
         for (int64_t k = z0; k < nzero; k += zs) zero[k] = 0.f;
         return;
     }
     const unsigned nb = zero ? (unsigned)ntd : gridDim.x;
+    // grouped nets (evx_td_loss_zero_g): net blockIdx.y owns rows [y B, (y + 1) B) and loss_out[y]
+    const unsigned gy = blockIdx.y;
+    if (gy) {
+        const size_t o = (size_t)gy * B;
+        Q += o * A;
+        Qt += o * A;
+        act += o;
+        rew += o;
+        done += o;
+        if (w) w += o;
+        dQ += o * A;
+        if (td_abs) td_abs += o;
+        loss_out += gy;
+    }
     const int i = blockIdx.x * 256 + threadIdx.x;
     float part = 0.f;
     if (i < B) {
@@ -310,17 +325,18 @@ __global__ __launch_bounds__(256) void td_loss_kernel(const float* __restrict__ 
         __syncthreads();
     }
     if (threadIdx.x == 0) {
-        g_td_part[blockIdx.x] = red[0];
+        g_td_part[gy * nb + blockIdx.x] = red[0];
         __threadfence();
-        last = atomicAdd(&g_td_ticket, 1u) == nb - 1;
+        last = atomicAdd(&g_td_ticket[gy], 1u) == nb - 1;
     }
     __syncthreads();
     if (last && threadIdx.x == 0) {
         __threadfence();
         float t = 0.f;
-        for (unsigned k = 0; k < nb; k++) t += __hip_atomic_load(&g_td_part[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (unsigned k = 0; k < nb; k++)
+            t += __hip_atomic_load(&g_td_part[gy * nb + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         loss_out[0] = t / (float)B;
-        g_td_ticket = 0;
+        g_td_ticket[gy] = 0;
     }
 }
 
@@ -607,6 +623,19 @@ int evx_td_loss_zero(const float* Q, const float* Qt, int32_t A, const int32_t* 
     hipLaunchKernelGGL(evxq::td_loss_kernel, dim3(ntd + nz), dim3(256), 0, (hipStream_t)stream, Q, Qt, A, act, rew, done,
                        gamma, B, w, dQ, loss, td_abs, ntd, zero, nzero);
     return qlaunch("td_loss_zero");
+}
+
+int evx_td_loss_zero_g(const float* Q, const float* Qt, int32_t A, const int32_t* act, const float* rew,
+                       const uint8_t* done, float gamma, int32_t B, int32_t nets, const float* w, float* dQ, float* loss,
+                       float* td_abs, float* zero, int64_t nzero, void* stream) {
+    if (B <= 0) return 0;
+    if (nets < 1 || nets > 64) return qfail(-22, "td_loss_g: nets must be 1..64");
+    const int ntd = (B + 255) / 256;
+    if ((int64_t)ntd * nets > 4096) return qfail(-22, "td_loss_g: batch x nets too large");
+    const int nz = zero && nzero > 0 ? (int)std::min<int64_t>((nzero + 256 * 16 - 1) / (256 * 16), 512) : 0;
+    hipLaunchKernelGGL(evxq::td_loss_kernel, dim3(ntd + nz, nets), dim3(256), 0, (hipStream_t)stream, Q, Qt, A, act, rew,
+                       done, gamma, B, w, dQ, loss, td_abs, ntd, nz ? zero : nullptr, nzero);
+    return qlaunch("td_loss_zero_g");
 }
 
 int evx_td_loss(const float* Q, const float* Qt, int32_t A, const int32_t* act, const float* rew, const uint8_t* done,

@@ -426,6 +426,52 @@ int evx_qmlp_adam_pack3(float *p, float *g, float *m, float *v, float max_norm, 
                         uint16_t *w1o, uint16_t *w1ol, const float *ss, int32_t nss, float *norm_out, void *stream);
 const char *evx_qmlp_last_error(void);
 
+/* ---- Grouped independent nets: runners/train_double_dqn.py:35-56 trains one
+ * DQNAgent per robot, runners/train_qmix.py:78-118 one per agent under a mixer. `nets` MLPs in
+ * one launch per kernel: every per-net buffer is an array [nets][one net's buffer] and the
+ * pointers passed are net 0's (x3 parameters: evx_qmlp_pack3 layout per net; flat parameters,
+ * gradients, m, v [nets][evx_qmlp_nparams()]). */
+/* DQNAgent.act of net g for rows i*nets + g of obs / q / actions (robot g of env i uses net g),
+ * n rows per net (even); dropout rows keyed g*n + i, epsilon draws by the data row. No
+ * permutation, no table path (p->stat NULL). */
+int evx_qmlp_act_g(const evx_layout *lay, const evx_obs *obs, int32_t n, int32_t nets, const evx_qmlp_params *p,
+                   const evx_qmlp_dropout *drop, const evx_qmlp_fwd_out *out, void *stream);
+/* evx_qmlp_forward2 for nets blocked problems: net g reads obs rows [g n, (g + 1) n) and writes
+ * its [n]-row blocks of h1 (two planes) / x / h2 / q; dropout rows keyed g*n + row. */
+int evx_qmlp_forward2_g(const evx_layout *lay, int32_t n, int32_t nets, const evx_obs *obs0,
+                        const evx_qmlp_params *p0, const evx_qmlp_dropout *drop0, const evx_qmlp_fwd_out *out0,
+                        const evx_obs *obs1, const evx_qmlp_params *p1, const evx_qmlp_dropout *drop1,
+                        const evx_qmlp_fwd_out *out1, void *stream);
+/* evx_td_loss_zero per net: rows [g B, (g + 1) B) of Q / Qt / act / rew / done / dQ, loss[g]
+ * = mean over the net's rows (nets <= 64, nets * ceil(B / 256) <= 4096). */
+int evx_td_loss_zero_g(const float *Q, const float *Qt, int32_t A, const int32_t *act, const float *rew,
+                       const uint8_t *done, float gamma, int32_t B, int32_t nets, const float *w, float *dQ,
+                       float *loss, float *td_abs, float *zero, int64_t nzero, void *stream);
+/* evx_qmlp_backward_ss for the blocked forward of evx_qmlp_forward2_g (gradients cleared by the
+ * caller); g->part: [nets][evx_qmlp_backward_part_floats(B)], ss [nets][evx_qmlp_norm_parts()]. */
+int evx_qmlp_backward_ss_g(const evx_qmlp_params *p, int32_t B, int32_t nets, const float *dq, const uint16_t *x,
+                           const uint16_t *h1, const float *h2, float drop_p, uint16_t *dz2, uint16_t *dz1,
+                           const evx_qmlp_grads *g, float *ss, void *stream);
+/* evx_qmlp_adam_pack3 per net (clip_grad_norm_ per agent, train_qmix.py:107-109); ss
+ * [nets][nss], norm_out [nets] or NULL. */
+int evx_qmlp_adam_pack3_g(float *p, float *g, float *m, float *v, float max_norm, const evx_adam *h, uint16_t *w1b,
+                          uint16_t *w1l, float *b1c, uint16_t *w2b, uint16_t *w2l, uint16_t *w2t, uint16_t *w2tl,
+                          uint16_t *w1o, uint16_t *w1ol, const float *ss, int32_t nss, float *norm_out, int32_t nets,
+                          void *stream);
+
+/* ---- QMIX mixer (runners/train_qmix.py:39-54 MixingNetwork, loss :78-104) for n <= 16 agents:
+ * Q / Qt [n][B][A] (evx_qmlp_forward2_g), act [n][B], rew / done [B]; mix / mix_t the online /
+ * target mixer flat in state_dict order (fc1_weight [n][32], fc1_bias [32], fc2_weight [32][1],
+ * fc2_bias [1]: evx_qmix_nparams(n)). Writes dQ [n][B][A] (d loss / d Q at the taken actions),
+ * the online mixer's gradient and loss[0] = mse; part: evx_qmix_part_floats(B, n) floats of
+ * scratch; zero[0..nzero) (the agents' gradients) is cleared in the same launch. */
+int32_t evx_qmix_nparams(int32_t n);
+int64_t evx_qmix_part_floats(int32_t B, int32_t n);
+int evx_qmix_loss(const float *Q, const float *Qt, int32_t A, const int32_t *act, const float *rew,
+                  const uint8_t *done, float gamma, int32_t B, int32_t n, const float *mix, const float *mix_t,
+                  float *dQ, float *mix_grad, float *loss, float *part, float *zero, int64_t nzero, void *stream);
+const char *evx_qmix_last_error(void);
+
 #ifdef __cplusplus
 }
 #endif
