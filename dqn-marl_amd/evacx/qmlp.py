@@ -86,6 +86,25 @@ def mlib():
         L.evx_qmlp_backward.argtypes = [C.POINTER(evx_qmlp_params), C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
                                         C.c_void_p, C.c_float, C.c_void_p, C.c_void_p, C.POINTER(evx_qmlp_grads),
                                         C.c_int32, C.c_void_p]
+        # grouped nets (evacx.qgroup)
+        L.evx_qmlp_act_g.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.POINTER(evx_qmlp_params),
+                                     C.POINTER(evx_qmlp_dropout), C.POINTER(evx_qmlp_fwd_out), C.c_void_p]
+        L.evx_qmlp_forward2_g.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.POINTER(evx_qmlp_params),
+                                          C.POINTER(evx_qmlp_dropout), C.POINTER(evx_qmlp_fwd_out), C.c_void_p,
+                                          C.POINTER(evx_qmlp_params), C.POINTER(evx_qmlp_dropout),
+                                          C.POINTER(evx_qmlp_fwd_out), C.c_void_p]
+        L.evx_qmlp_backward_ss_g.argtypes = [C.POINTER(evx_qmlp_params), C.c_int32, C.c_int32, C.c_void_p, C.c_void_p,
+                                             C.c_void_p, C.c_void_p, C.c_float, C.c_void_p, C.c_void_p,
+                                             C.POINTER(evx_qmlp_grads), C.c_void_p, C.c_void_p]
+        L.evx_qmlp_adam_pack3_g.argtypes = [C.c_void_p] * 4 + [C.c_float, C.c_void_p] + [C.c_void_p] * 10 + \
+            [C.c_int32, C.c_void_p, C.c_int32, C.c_void_p]
+        L.evx_qmix_last_error.restype = C.c_char_p
+        L.evx_qmix_nparams.restype = C.c_int32
+        L.evx_qmix_part_floats.restype = C.c_int64
+        L.evx_qmix_part_floats.argtypes = [C.c_int32, C.c_int32]
+        L.evx_qmix_loss.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_float,
+                                    C.c_int32, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                    C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]
         _inited = True
     return L
 
@@ -109,25 +128,47 @@ class MLPFast:
     """bf16 operand copies of one MLP parameter set (evacx.qnet.FlatParams) + forward.
     x3=True: the f32-accurate mode (hi + lo operand pairs; evx_qmlp_pack3)."""
 
-    def __init__(self, params, device, x3: bool = False):
+    # operand buffers: name -> (elements, dtype); x3 adds the lo copies
+    @staticmethod
+    def buffer_sizes(x3: bool):
+        kx = K1X if x3 else K1P
+        d = {"w1b": (HID * kx, torch.int16), "w2b": (HID2 * HID, torch.int16), "w2t": (HID * HID2, torch.int16),
+             "b1c": (HID, torch.float32), "w1o": (HID * 128, torch.int16)}
+        if x3:
+            d.update(w1ol=(HID * 128, torch.int16), w1l=(HID * K1P, torch.int16), w2l=(HID2 * HID, torch.int16),
+                     w2tl=(HID * HID2, torch.int16))
+        return d
+
+    def __init__(self, params, device, x3: bool = False, store=None):
+        """store: optional name -> preallocated tensor of buffer_sizes(x3) (evacx.qgroup: every net's
+        operands one slice of a [nets][...] array, as the grouped kernels address them)."""
         self.P = params
         self.device = torch.device(device)
         self.x3 = bool(x3)
-        i16 = dict(dtype=torch.int16, device=self.device)
         self.kx = K1X if self.x3 else K1P  # width of fc1's expanded input (the learner's saved X)
-        self.w1b = torch.zeros(HID * self.kx, **i16)
-        self.w2b = torch.zeros(HID2 * HID, **i16)
-        self.w2t = torch.zeros(HID * HID2, **i16)
-        self.b1c = torch.zeros(HID, dtype=torch.float32, device=self.device)
-        self.w1o = torch.zeros(HID * 128, **i16)  # fc1's occupancy columns (act fast path; x3: hi)
-        self.w1ol = torch.zeros(HID * 128, **i16) if self.x3 else None  # x3: their lo part
+        sizes = self.buffer_sizes(self.x3)
+
+        def buf(name):
+            n, dt = sizes[name]
+            if store is not None:
+                t = store[name]
+                if t.numel() != n or t.dtype != dt or not t.is_contiguous():
+                    raise ValueError(f"MLPFast store[{name}]: needs {n} contiguous {dt}")
+                return t
+            return torch.zeros(n, dtype=dt, device=self.device)
+        self.w1b = buf("w1b")
+        self.w2b = buf("w2b")
+        self.w2t = buf("w2t")
+        self.b1c = buf("b1c")
+        self.w1o = buf("w1o")  # fc1's occupancy columns (act fast path; x3: hi)
+        self.w1ol = buf("w1ol") if self.x3 else None  # x3: their lo part
         self.c = evx_qmlp_params(w1=self.w1b.data_ptr(), b1c=self.b1c.data_ptr(), w2=self.w2b.data_ptr(),
                                  w2t=self.w2t.data_ptr(), b2=params["fc2.bias"].data_ptr(),
                                  w3=params["fc3.weight"].data_ptr(), b3=params["fc3.bias"].data_ptr())
         if self.x3:
-            self.w1l = torch.zeros(HID * K1P, **i16)
-            self.w2l = torch.zeros(HID2 * HID, **i16)
-            self.w2tl = torch.zeros(HID * HID2, **i16)
+            self.w1l = buf("w1l")
+            self.w2l = buf("w2l")
+            self.w2tl = buf("w2tl")
             self.c.x3 = 1
             self.c.w1l, self.c.w2l, self.c.w2tl = self.w1l.data_ptr(), self.w2l.data_ptr(), self.w2tl.data_ptr()
             self.c.w1ol = self.w1ol.data_ptr()

@@ -64,6 +64,9 @@ def qlib():
         L.evx_td_loss_zero.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
                                        C.c_float, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                        C.c_void_p, C.c_int64, C.c_void_p]
+        L.evx_td_loss_zero_g.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                         C.c_float, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                         C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]
         L.evx_sumsq_norm.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
         L.evx_clip_adam.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p,
                                     C.c_float, C.POINTER(evx_adam), C.c_void_p]
@@ -372,7 +375,7 @@ class Learner:
         return self.loss
 
     def learn_obs(self, lay_c, s_obs, a, r, done, s2_obs, B, update: bool = True, weights=None, td_abs=None,
-                  mask_online=None, mask_target=None):
+                  mask_online=None, mask_target=None, drop_row0: int = 0):
         """DQNAgent.learn on compact observations with the fused kernels (x3 = f32-accurate,
         or bf16): online forward (saves X, H1, H2), target forward, TD loss, backward,
         clip+Adam. update=False stops after the gradients (the caller runs step_optimizer
@@ -394,8 +397,9 @@ class Learner:
         dz2 = ws.get("fdz2", (pl * B * HID2,), torch.int16, dev)
         dz1 = ws.get("fdz1", (pl * B * HID,), torch.int16, dev)
         self.drop_stream += 2
-        d_on = (self.seed, self.drop_stream, DROPOUT_P) + ((mask_online,) if mask_online is not None else ())
-        d_tg = (self.seed, self.drop_stream + 1, DROPOUT_P) + ((mask_target,) if mask_target is not None else ())
+        # drop_row0 (even): the dropout hash rows start there (evacx.qgroup keys net g's batch rows g * B + i)
+        d_on = (self.seed, self.drop_stream, DROPOUT_P, mask_online, drop_row0)
+        d_tg = (self.seed, self.drop_stream + 1, DROPOUT_P, mask_target, drop_row0)
         type(self.fast).forward_pair(lay_c, B, self.fast, s_obs, d_on, dict(h1=H1, x=X, h2=H2, q=Q), self.fast_t,
                                      s2_obs, d_tg, dict(h1=H1t, q=Qt))
         L = qlib()
