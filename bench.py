@@ -121,6 +121,9 @@ def parse():
                     help="prioritized: GPU sum/min-tree proportional replay (cfg5; evacx.prio)")
     ap.add_argument("--replay-capacity", type=int, default=0,
                     help="transitions per GPU (0: the power of two >= 16 steps of pushes, envs x robots x 16)")
+    ap.add_argument("--nets", choices=["shared", "per_robot"], default="shared",
+                    help="per_robot: every robot index has its own Q-network, memory and optimizer (SURVEY F3; "
+                         "grouped launches, batch / robots transitions per net)")
     ap.add_argument("--groups", type=int, default=1,
                     help="env groups per GPU, each with its own act -> env.step -> push stream chain "
                          "(evacx.trainer._Group): one group's env.step tail overlaps the others' work")
@@ -195,7 +198,7 @@ def main():
                     grad_hook=hook,
                     lagged_learn=args.schedule == "lagged", replay=args.replay,
                     replay_capacity=args.replay_capacity, groups=args.groups if args.mode == "train" else 1,
-                    layout_of=layout_of, world_envs=E * world)
+                    layout_of=layout_of, world_envs=E * world, nets=args.nets)
     env = tr.env
     lagged_ok = tr.fast is not None  # the lagged schedule needs the fused MLP path
     schedule = args.schedule if lagged_ok else "strict"
@@ -273,7 +276,7 @@ def main():
     env.check_err()
     kern_ms = ev_mean(ev_env, args.steps)
     learn_ms = ev_mean(ev_learn, args.steps) if args.mode == "train" else None
-    loss = float(tr.last_loss.item()) if tr.last_loss is not None else None
+    loss = float(tr.last_loss.float().mean().item()) if tr.last_loss is not None else None
     value = E * world * args.steps / elapsed
 
     # ------------------------------- the other schedule on the same state (extra)
@@ -359,7 +362,7 @@ def main():
                 "batch": args.batch, "replay_capacity": args.replay_capacity, "schedule": schedule, "precision": prec,
                 "qnet": ("MLP 726-512-256-5" if args.qnet == "mlp"
                          else "DQNNetwork conv 6-32-64-128 + 15488-512-256-5"),
-                "replay": args.replay, "groups": args.groups if args.mode == "train" else 1,
+                "replay": args.replay, "groups": args.groups if args.mode == "train" else 1, "nets": args.nets,
                 "parallelism": f"data-parallel over {world} GPU(s): envs sharded, grad all-reduce (RCCL) per learn",
             },
             "other_schedule": other,

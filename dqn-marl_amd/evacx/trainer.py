@@ -128,7 +128,8 @@ class VecTrainer:
                  epsilon_decay: float = 0.9995, target_every: int = 1000, learner_seed: int = 0,
                  grad_hook=None, learn_every: int = 1, lagged_learn: bool = False, replay: str = "uniform",
                  prio_alpha: float = 0.6, prio_beta0: float = 0.4, prio_beta_steps: int = 100000,
-                 prio_eps: float = 1e-6, groups: int = 1, layout_of=None, world_envs: Optional[int] = None):
+                 prio_eps: float = 1e-6, groups: int = 1, layout_of=None, world_envs: Optional[int] = None,
+                 nets: str = "shared"):
         """groups: the envs are split into this many parts, each stepping on its own
         stream chain (see _Group); the env results do not depend on it (every env is
         still stepped once per step with its own streams), the act's dropout masks do.
@@ -137,7 +138,11 @@ class VecTrainer:
         world_envs: envs over all ranks (default E). This rank's envs are global ids
         env_offset .. env_offset + E - 1; the act's epsilon draws and dropout rows are keyed
         by global agent id, so every env's trajectory is the same at any GPU count as long
-        as the actions do not depend on the (rank-shared) weights' history."""
+        as the actions do not depend on the (rank-shared) weights' history.
+        nets: "shared" (one Q-network for every robot) or "per_robot" (robot r of every env has
+        its own network, memory and optimizer, as runners/train_double_dqn.py:35-56 gives each
+        robot its own DQNAgent: evacx.qgroup.GroupedLearner, batch / R transitions per net per
+        learn step, strict schedule, one GPU)."""
         self.lay, self.E, self.R = layout, E, layout.R
         self.device = layout.device
         # the push reads env.obs_prev: no copy per step
@@ -146,9 +151,22 @@ class VecTrainer:
         self.env.reset()
         parts = self.env.split(groups) if groups > 1 else [self.env]
         self.env.compute_order()
+        self.per_robot = nets == "per_robot"
+        if nets not in ("shared", "per_robot"):
+            raise ValueError(f"nets must be 'shared' or 'per_robot', not {nets!r}")
+        if self.per_robot:
+            if kind != "mlp" or precision != "f32" or groups != 1 or lagged_learn or replay != "uniform" or \
+                    layout_of is not None or grad_hook is not None:
+                raise ValueError("per_robot nets: MLP, f32, one group, strict schedule, uniform replay, one layout, "
+                                 "one GPU")
+            if batch % (2 * self.R) or replay_capacity % self.R:
+                raise ValueError("per_robot nets: batch a multiple of 2 R, replay capacity a multiple of R")
+            from .qgroup import GroupedLearner
+            self.glearner = GroupedLearner(self.R, self.device, lr=lr, gamma=gamma, seed=learner_seed)
         self.learner = Learner(kind=kind, device=self.device, lr=lr, gamma=gamma, precision=precision,
-                               seed=learner_seed)
-        self.learner.grad_hook = grad_hook
+                               seed=learner_seed) if not self.per_robot else None
+        if self.learner is not None:
+            self.learner.grad_hook = grad_hook
         # replay: "uniform" (DQNAgent.memory's random.sample) or "prioritized" (evacx.prio:
         # device sum/min trees, importance-weighted loss, beta annealed to 1)
         self.prio = replay == "prioritized"
@@ -202,7 +220,7 @@ class VecTrainer:
         self.ev_learned.record(cur)
         self.last_loss: Optional[torch.Tensor] = None
         # bf16 MLP: act and learn straight from compact observations (csrc/qmlp.hip)
-        self.fast = self.learner.fast
+        self.fast = self.learner.fast if self.learner is not None else None
         if self.fast is None:
             self.lagged = False  # the split learn step needs the fused bf16 MLP path
         self._perm = None
@@ -223,6 +241,10 @@ class VecTrainer:
         over argmax Q; the epsilon draws are counted over all E*R robots of the step."""
         g0 = self.agent0 + grp.row0  # global agent id of the group's first robot
         off = self.t * self.n_world + g0
+        if self.per_robot:  # robot r of every env through net r, one launch
+            self.glearner.act(self.lay.c, grp.env.obs, grp.env.E, actions=grp.actions, epsilon=float(self.epsilon),
+                              act_seed=self.act_seed, act_offset=off)
+            return
         if self.fast is not None:
             self.learner.drop_stream += 1
             self.fast.act(self.lay.c, grp.env.obs, grp.n,
@@ -244,6 +266,25 @@ class VecTrainer:
         """window: (base, count) of the replay ring to sample from (default: all of it).
         phase: "all", or "grads" (sample .. backward) then "update" (clip+Adam, bf16
         repack, epsilon, target sync) -- the update may wait for readers of the weights."""
+        if self.per_robot:  # every robot's net on batch / R of its own transitions
+            Bn = self.batch // self.R
+            if self.replay.size < self.batch:
+                return None
+            L = _lib.lib()
+            L.evx_replay_sample_agents.argtypes = [C.POINTER(evx_replay), C.c_int64, C.c_int32, C.c_int32, C.c_uint64,
+                                                   C.c_uint64] + [C.c_void_p] * 6
+            sp = self.samp
+            qcheck(L.evx_replay_sample_agents(C.byref(self.replay.c), self.replay.size, Bn, self.R, self.seed + 1,
+                                              self.learn_steps * self.batch, sp["s"].data_ptr(), sp["s2"].data_ptr(),
+                                              sp["a"].data_ptr(), sp["r"].data_ptr(), sp["done"].data_ptr(),
+                                              _stream()), "replay_sample_agents")
+            loss = self.glearner.learn_obs(self.lay.c, sp["s"], sp["a"], sp["r"], sp["done"], sp["s2"], Bn)
+            self.learn_steps += 1
+            if self.epsilon > self.epsilon_min:
+                self.epsilon *= self.epsilon_decay
+            if self.learn_steps % self.target_every == 0:
+                self.glearner.sync_target()
+            return loss
         if phase != "update":
             if (self.replay.size if window is None else window[1]) < self.batch:
                 return None

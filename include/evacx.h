@@ -241,6 +241,13 @@ int evx_replay_sample(const evx_replay *rp, int64_t size, int32_t B, uint64_t se
 int evx_replay_sample_window(const evx_replay *rp, int64_t base, int64_t count, int32_t B, uint64_t seed,
                              uint64_t offset, evx_obs *s, evx_obs *s2, int32_t *a, float *r, uint8_t *done,
                              int64_t *idx_out, void *stream);
+/* One memory per agent (runners/train_double_dqn.py:50-51: agent_i.remember / learn on its own
+ * transitions): with pushes of whole envs (rows env * nets + agent, capacity % nets == 0) the
+ * agent's transitions are the ring slots == agent (mod nets); B uniform draws among them
+ * (among the first size slots) for every agent, into rows [agent B, (agent + 1) B). */
+int evx_replay_sample_agents(const evx_replay *rp, int64_t size, int32_t B, int32_t nets, uint64_t seed,
+                             uint64_t offset, evx_obs *s, evx_obs *s2, int32_t *a, float *r, uint8_t *done,
+                             void *stream);
 /* ------------------------------------------- prioritized replay
  * Proportional prioritized replay (Schaul et al. 2016) over the slots of an evx_replay
  * ring; the reference samples uniformly (random.sample, agents/dqn_agent.py:132), so

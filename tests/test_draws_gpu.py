@@ -99,6 +99,41 @@ def test_replay_sampling_matches_restatement(window):
     assert torch.equal(out["s2"].view(B, OBS_WORDS), rp.s2.view(cap, OBS_WORDS)[j])
 
 
+def test_per_agent_replay_sampling_matches_restatement():
+    """evx_replay_sample_agents (one memory per robot): agent g's draws are the uniform
+    sampler's restated draws (counters offset + g B + i) over its own slots (== g mod nets)."""
+    _need_gpu()
+    from evacx.env import OBS_WORDS
+    from evacx.qnet import qcheck
+    from evacx.trainer import Replay
+    import ctypes as C
+    from evacx import _lib
+    cap, nets, B, size = 4096, 8, 600, 3000 // 8 * 8
+    rp = Replay(cap, "cuda")
+    rp.a.copy_(torch.arange(cap, device="cuda", dtype=torch.int32))
+    rp.s.copy_(torch.arange(cap * OBS_WORDS, device="cuda", dtype=torch.int32))
+    out = dict(s=torch.empty(nets * B * OBS_WORDS, dtype=torch.int32, device="cuda"),
+               s2=torch.empty(nets * B * OBS_WORDS, dtype=torch.int32, device="cuda"),
+               a=torch.empty(nets * B, dtype=torch.int32, device="cuda"), r=torch.empty(nets * B, device="cuda"),
+               done=torch.empty(nets * B, dtype=torch.uint8, device="cuda"))
+    L = _lib.lib()
+    L.evx_replay_sample_agents.argtypes = [C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_uint64,
+                                           C.c_uint64] + [C.c_void_p] * 6
+    qcheck(L.evx_replay_sample_agents(C.byref(rp.c), size, B, nets, 17, 4096, out["s"].data_ptr(), out["s2"].data_ptr(),
+                                      out["a"].data_ptr(), out["r"].data_ptr(), out["done"].data_ptr(), None),
+           "sample_agents")
+    torch.cuda.synchronize()
+    a = out["a"].cpu().numpy().reshape(nets, B)
+    for g in range(nets):
+        ref = orc.replay_indices(0, size // nets, 1 << 40, B, 17, 4096 + g * B) * nets + g
+        assert np.array_equal(a[g], ref), g
+    assert torch.equal(out["s"].view(nets * B, OBS_WORDS), rp.s.view(cap, OBS_WORDS)[out["a"].long()])
+    assert a.max() < size
+    assert L.evx_replay_sample_agents(C.byref(rp.c), size + 1, B, nets, 17, 0, out["s"].data_ptr(),
+                                      out["s2"].data_ptr(), out["a"].data_ptr(), out["r"].data_ptr(),
+                                      out["done"].data_ptr(), None) != 0  # size not a multiple of nets
+
+
 @pytest.mark.parametrize("lagged", [False, True])
 def test_trainer_step_composition(lagged):
     _need_gpu()

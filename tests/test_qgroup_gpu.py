@@ -228,3 +228,33 @@ def test_grouped_qmix_step_matches_torch_autograd():
         assert abs(qm.mix_norm.item() - mnorm.item()) <= 2e-4 * mnorm.item() + 1e-6
         mref = torch.cat([p.detach().reshape(-1) for p in mixing.state_dict().values()])
         torch.testing.assert_close(qm.mix, mref, rtol=1e-4, atol=1e-5)
+
+
+def test_vec_trainer_per_robot_nets():
+    """VecTrainer(nets="per_robot"): robot r of every env acts through net r (== the grouped act
+    on the same observations and weights), every net learns from its own robot's transitions
+    (the per-agent sampler) and moves; the shared-net parameters are untouched by construction."""
+    _need_gpu()
+    from evacx.env import DeviceLayout
+    from evacx.layout import build_tables, synthetic
+    from evacx.trainer import VecTrainer
+    R, E = 4, 64
+    lay = DeviceLayout(build_tables(synthetic(48, 48, R)), 300)
+    tr = VecTrainer(lay, E, batch=8 * R * 2, replay_capacity=1 << 12, nets="per_robot", epsilon=0.3, learner_seed=3)
+    p0 = tr.glearner.flat.clone()
+    for _ in range(6):
+        tr.step()
+    tr.sync()
+    torch.cuda.synchronize()
+    assert tr.last_loss is not None and tr.last_loss.shape == (R,) and torch.isfinite(tr.last_loss).all()
+    moved = (tr.glearner.flat != p0).any(dim=1)
+    assert bool(moved.all())
+    # the next act == a grouped act with the trainer's draws
+    a_ref = torch.empty(E * R, dtype=torch.int32, device="cuda")
+    off = tr.t * tr.n_world + tr.agent0
+    stream = 0x40000000 + tr.glearner._act_calls + 1
+    tr.glearner.act(lay.c, tr.env.obs, E, actions=a_ref, epsilon=float(tr.epsilon), act_seed=tr.act_seed,
+                    act_offset=off, drop_stream=stream)
+    a = tr.act()
+    torch.cuda.synchronize()
+    assert torch.equal(a, a_ref)
