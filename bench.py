@@ -121,9 +121,10 @@ def parse():
                     help="prioritized: GPU sum/min-tree proportional replay (cfg5; evacx.prio)")
     ap.add_argument("--replay-capacity", type=int, default=0,
                     help="transitions per GPU (0: the power of two >= 16 steps of pushes, envs x robots x 16)")
-    ap.add_argument("--nets", choices=["shared", "per_robot"], default="shared",
+    ap.add_argument("--nets", choices=["shared", "per_robot", "qmix"], default="shared",
                     help="per_robot: every robot index has its own Q-network, memory and optimizer (SURVEY F3; "
-                         "grouped launches, batch / robots transitions per net)")
+                         "grouped launches, batch / robots transitions per net); qmix: those nets under a QMIX mixer "
+                         "(batch / robots joint env-steps)")
     ap.add_argument("--groups", type=int, default=1,
                     help="env groups per GPU, each with its own act -> env.step -> push stream chain "
                          "(evacx.trainer._Group): one group's env.step tail overlaps the others' work")

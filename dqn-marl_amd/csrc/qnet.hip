@@ -451,14 +451,16 @@ __global__ __launch_bounds__(256) void replay_sample_kernel(evx_replay rp, int64
                                                             uint64_t offset, evx_obs* __restrict__ s,
                                                             evx_obs* __restrict__ s2, int32_t* __restrict__ a,
                                                             float* __restrict__ r, uint8_t* __restrict__ done,
-                                                            int64_t* __restrict__ idx_out, int nets = 1) {
+                                                            int64_t* __restrict__ idx_out, int nets = 1,
+                                                            int joint = 0) {
     const int i0 = blockIdx.x * 256 + threadIdx.x;
     if (i0 >= B) return;
     // nets > 1 (evx_replay_sample_agents): agent blockIdx.y's own transitions -- the ring slots
-    // == agent (mod nets) -- into rows [agent B, (agent + 1) B), draws counted agent B + i
+    // == agent (mod nets) -- into rows [agent B, (agent + 1) B), draws counted agent B + i;
+    // joint (evx_replay_sample_joint): draw i is shared by every agent (the same env-steps)
     const int g = (int)blockIdx.y;
     const int i = g * B + i0;
-    const uint64_t c = (uint64_t)i + offset;
+    const uint64_t c = (uint64_t)(joint ? i0 : i) + offset;
     const u4 q = philox((uint32_t)c, (uint32_t)(c >> 32), 0x5a3b1eu, 0u, (uint32_t)seed, (uint32_t)(seed >> 32));
     const uint64_t r64 = ((uint64_t)q.x << 32) | q.y;
     int64_t j;
@@ -733,6 +735,20 @@ int evx_replay_sample_agents(const evx_replay* rp, int64_t size, int32_t B, int3
     hipLaunchKernelGGL(evxq::replay_sample_kernel, dim3(nblk(B), nets), dim3(256), 0, (hipStream_t)stream, *rp, (int64_t)0,
                        size, B, seed, offset, s, s2, a, r, done, nullptr, (int)nets);
     return qlaunch("replay_sample_agents");
+}
+
+int evx_replay_sample_joint(const evx_replay* rp, int64_t size, int32_t B, int32_t nets, uint64_t seed,
+                            uint64_t offset, evx_obs* s, evx_obs* s2, int32_t* a, float* r, uint8_t* done,
+                            void* stream) {
+    if (!rp || !s || !s2 || !a || !r || !done) return qfail(-22, "replay_sample_joint: NULL argument");
+    if (B <= 0) return 0;
+    if (nets < 1 || nets > 65535) return qfail(-22, "replay_sample_joint: nets must be 1..65535");
+    if (rp->capacity % nets) return qfail(-22, "replay_sample_joint: capacity must be a multiple of nets");
+    if (size < nets || size > rp->capacity || size % nets)
+        return qfail(-22, "replay_sample_joint: size must be a positive multiple of nets within the capacity");
+    hipLaunchKernelGGL(evxq::replay_sample_kernel, dim3(nblk(B), nets), dim3(256), 0, (hipStream_t)stream, *rp, (int64_t)0,
+                       size, B, seed, offset, s, s2, a, r, done, nullptr, (int)nets, 1);
+    return qlaunch("replay_sample_joint");
 }
 
 int evx_replay_sample_window(const evx_replay* rp, int64_t base, int64_t count, int32_t B, uint64_t seed,

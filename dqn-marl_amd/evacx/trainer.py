@@ -142,7 +142,8 @@ class VecTrainer:
         nets: "shared" (one Q-network for every robot) or "per_robot" (robot r of every env has
         its own network, memory and optimizer, as runners/train_double_dqn.py:35-56 gives each
         robot its own DQNAgent: evacx.qgroup.GroupedLearner, batch / R transitions per net per
-        learn step, strict schedule, one GPU)."""
+        learn step, strict schedule, one GPU) or "qmix" (per-robot nets under a QMIX mixer,
+        runners/train_qmix.py: batch / R joint env-steps per learn step, evacx.qgroup.GroupedQMix)."""
         self.lay, self.E, self.R = layout, E, layout.R
         self.device = layout.device
         # the push reads env.obs_prev: no copy per step
@@ -151,9 +152,9 @@ class VecTrainer:
         self.env.reset()
         parts = self.env.split(groups) if groups > 1 else [self.env]
         self.env.compute_order()
-        self.per_robot = nets == "per_robot"
-        if nets not in ("shared", "per_robot"):
-            raise ValueError(f"nets must be 'shared' or 'per_robot', not {nets!r}")
+        self.per_robot = nets in ("per_robot", "qmix")
+        if nets not in ("shared", "per_robot", "qmix"):
+            raise ValueError(f"nets must be 'shared', 'per_robot' or 'qmix', not {nets!r}")
         if self.per_robot:
             if kind != "mlp" or precision != "f32" or groups != 1 or lagged_learn or replay != "uniform" or \
                     layout_of is not None or grad_hook is not None:
@@ -161,8 +162,11 @@ class VecTrainer:
                                  "one GPU")
             if batch % (2 * self.R) or replay_capacity % self.R:
                 raise ValueError("per_robot nets: batch a multiple of 2 R, replay capacity a multiple of R")
-            from .qgroup import GroupedLearner
+            from .qgroup import GroupedLearner, GroupedQMix
             self.glearner = GroupedLearner(self.R, self.device, lr=lr, gamma=gamma, seed=learner_seed)
+            # qmix: the R robots of an env are the agents of runners/train_qmix.py -- joint samples
+            # (the same env-steps for every agent), the mixer's loss over the team reward
+            self.qmix = GroupedQMix(self.glearner, seed=learner_seed) if nets == "qmix" else None
         self.learner = Learner(kind=kind, device=self.device, lr=lr, gamma=gamma, precision=precision,
                                seed=learner_seed) if not self.per_robot else None
         if self.learner is not None:
@@ -274,16 +278,23 @@ class VecTrainer:
             L.evx_replay_sample_agents.argtypes = [C.POINTER(evx_replay), C.c_int64, C.c_int32, C.c_int32, C.c_uint64,
                                                    C.c_uint64] + [C.c_void_p] * 6
             sp = self.samp
-            qcheck(L.evx_replay_sample_agents(C.byref(self.replay.c), self.replay.size, Bn, self.R, self.seed + 1,
-                                              self.learn_steps * self.batch, sp["s"].data_ptr(), sp["s2"].data_ptr(),
-                                              sp["a"].data_ptr(), sp["r"].data_ptr(), sp["done"].data_ptr(),
-                                              _stream()), "replay_sample_agents")
-            loss = self.glearner.learn_obs(self.lay.c, sp["s"], sp["a"], sp["r"], sp["done"], sp["s2"], Bn)
+            fn = L.evx_replay_sample_joint if self.qmix is not None else L.evx_replay_sample_agents
+            fn.argtypes = L.evx_replay_sample_agents.argtypes
+            qcheck(fn(C.byref(self.replay.c), self.replay.size, Bn, self.R, self.seed + 1, self.learn_steps * self.batch,
+                      sp["s"].data_ptr(), sp["s2"].data_ptr(), sp["a"].data_ptr(), sp["r"].data_ptr(),
+                      sp["done"].data_ptr(), _stream()), "replay_sample_agents/joint")
+            if self.qmix is not None:  # agent 0's rows carry the team reward / done of the sampled env-steps
+                loss = self.qmix(self.lay.c, sp["s"], sp["a"], sp["r"], sp["done"], sp["s2"], Bn)
+            else:
+                loss = self.glearner.learn_obs(self.lay.c, sp["s"], sp["a"], sp["r"], sp["done"], sp["s2"], Bn)
             self.learn_steps += 1
             if self.epsilon > self.epsilon_min:
                 self.epsilon *= self.epsilon_decay
             if self.learn_steps % self.target_every == 0:
-                self.glearner.sync_target()
+                if self.qmix is not None:
+                    self.qmix.sync_targets()
+                else:
+                    self.glearner.sync_target()
             return loss
         if phase != "update":
             if (self.replay.size if window is None else window[1]) < self.batch:

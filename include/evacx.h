@@ -248,6 +248,12 @@ int evx_replay_sample_window(const evx_replay *rp, int64_t base, int64_t count, 
 int evx_replay_sample_agents(const evx_replay *rp, int64_t size, int32_t B, int32_t nets, uint64_t seed,
                              uint64_t offset, evx_obs *s, evx_obs *s2, int32_t *a, float *r, uint8_t *done,
                              void *stream);
+/* The joint memory of runners/train_qmix.py:36,78-96 (one entry per env-step, all agents'
+ * observations and actions): draw i picks the same env-step for every agent (rows agent B + i
+ * hold that agent's slot); counters offset + i. */
+int evx_replay_sample_joint(const evx_replay *rp, int64_t size, int32_t B, int32_t nets, uint64_t seed,
+                            uint64_t offset, evx_obs *s, evx_obs *s2, int32_t *a, float *r, uint8_t *done,
+                            void *stream);
 /* ------------------------------------------- prioritized replay
  * Proportional prioritized replay (Schaul et al. 2016) over the slots of an evx_replay
  * ring; the reference samples uniformly (random.sample, agents/dqn_agent.py:132), so

@@ -129,6 +129,16 @@ def test_per_agent_replay_sampling_matches_restatement():
         assert np.array_equal(a[g], ref), g
     assert torch.equal(out["s"].view(nets * B, OBS_WORDS), rp.s.view(cap, OBS_WORDS)[out["a"].long()])
     assert a.max() < size
+    # joint draws (QMIX's memory of env-steps): draw i picks the same env-step for every agent
+    L.evx_replay_sample_joint.argtypes = L.evx_replay_sample_agents.argtypes
+    qcheck(L.evx_replay_sample_joint(C.byref(rp.c), size, B, nets, 17, 4096, out["s"].data_ptr(), out["s2"].data_ptr(),
+                                     out["a"].data_ptr(), out["r"].data_ptr(), out["done"].data_ptr(), None),
+           "sample_joint")
+    torch.cuda.synchronize()
+    aj = out["a"].cpu().numpy().reshape(nets, B)
+    step = orc.replay_indices(0, size // nets, 1 << 40, B, 17, 4096)
+    for g in range(nets):
+        assert np.array_equal(aj[g], step * nets + g), g
     assert L.evx_replay_sample_agents(C.byref(rp.c), size + 1, B, nets, 17, 0, out["s"].data_ptr(),
                                       out["s2"].data_ptr(), out["a"].data_ptr(), out["r"].data_ptr(),
                                       out["done"].data_ptr(), None) != 0  # size not a multiple of nets

@@ -258,3 +258,24 @@ def test_vec_trainer_per_robot_nets():
     a = tr.act()
     torch.cuda.synchronize()
     assert torch.equal(a, a_ref)
+
+
+def test_vec_trainer_qmix_nets():
+    """VecTrainer(nets="qmix"): the robots of an env as the agents of runners/train_qmix.py --
+    joint samples, GroupedQMix learn steps (mixer kernel), every agent and the mixer move."""
+    _need_gpu()
+    from evacx.env import DeviceLayout
+    from evacx.layout import build_tables, synthetic
+    from evacx.trainer import VecTrainer
+    R, E = 4, 64
+    lay = DeviceLayout(build_tables(synthetic(48, 48, R)), 300)
+    tr = VecTrainer(lay, E, batch=8 * R * 2, replay_capacity=1 << 12, nets="qmix", epsilon=0.3, learner_seed=5,
+                    target_every=3)
+    p0, m0 = tr.glearner.flat.clone(), tr.qmix.mix.clone()
+    for _ in range(8):
+        tr.step()
+    tr.sync()
+    torch.cuda.synchronize()
+    assert tr.last_loss is not None and torch.isfinite(tr.last_loss).all()
+    assert bool((tr.glearner.flat != p0).any(dim=1).all()) and not torch.equal(tr.qmix.mix, m0)
+    assert torch.equal(tr.qmix.mix_t, tr.qmix.mix) or tr.learn_steps % 3 != 0
