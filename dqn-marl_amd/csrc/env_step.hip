@@ -49,8 +49,9 @@ constexpr int WR = 1024;             // MT ring words per stream (>= 624 + 227)
 constexpr int WRM = WR - 1;
 constexpr int WWIN = WR - 64 - 16;   // scoring words made readable per ensure
 constexpr int SHUF_WORDS = 384;      // words per lane-0 shuffle round (keeps mt_store_w's window valid)
-constexpr int CL_CAP = 510;          // contested movers sorted in LDS (more: global scratch); the np
-                                     // ring holds list (512 with sort padding) | heads 256 | starts 256
+constexpr int CL_CAP = 510;          // contested movers sorted in LDS (more: global scratch): the list
+                                     // (512 with sort padding) in the numpy ring, heads 256 | starts 256
+                                     // in the planner queue (both dead after the rows)
 constexpr int EV_CAP = 256;          // order-sensitive occupancy events
 constexpr int LEAF_CAP = 256;        // numpy pairwise leaves (n <= 16383 needs <= 128)
 constexpr int GRP_MAX = 128;         // movers of one contested target
@@ -193,6 +194,50 @@ __device__ __forceinline__ void mt_store_w(uint32_t* ring, int& front, int head,
     const int b = MT_N * ((head - 1) / MT_N);
     mt_ensure_w(ring, front, b + MT_N);
     for (int i = lane; i < MT_N; i += 64) gst[i] = ring[(b + i) & WRM];
+    if (lane == 0) gst[MT_N] = (uint32_t)(head - b);
+}
+
+// The numpy stream's ring: exactly the 624-word MT state, word n in slot n % 624 (the stream is
+// read in order, at most 128 words ahead of the last word read, so the in-place twist -- every
+// operand of a round loaded before any word of it is written -- never overwrites an unread
+// word). 400 words less LDS per env than a 1024-word ring.
+__device__ __forceinline__ int np_slot(int n) { return n - MT_N * (int)((uint32_t)n / (uint32_t)MT_N); }
+__device__ __forceinline__ void np_ensure(uint32_t* ring, int& front, int upto) {
+    const int lane = (int)(threadIdx.x & 63);
+    while (front < upto) {
+        const int cnt = min(MT_LAG, upto - front);
+        uint32_t lag[4], a[4], b[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int n = front + lane + 64 * j;
+            lag[j] = ring[np_slot(n - MT_LAG)];
+            a[j] = ring[np_slot(n - 624)];
+            b[j] = ring[np_slot(n - 623)];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int n = front + lane + 64 * j;
+            if (lane + 64 * j < cnt) ring[np_slot(n)] = mt_twist1(lag[j], a[j], b[j]);
+        }
+        front += cnt;
+        wave_fence();
+    }
+}
+__device__ __forceinline__ double np_double(const uint32_t* ring, int idx) {
+    const uint32_t a = mt_temper(ring[np_slot(idx)]) >> 5, b = mt_temper(ring[np_slot(idx + 1)]) >> 6;
+    return ((double)a * 67108864.0 + (double)b) * (1.0 / 9007199254740992.0);
+}
+// mt_store_w for the numpy ring: the stream is consumed exactly up to front, so the block
+// [b, b + 624) holding head - 1 completes in place
+__device__ __forceinline__ void np_store(uint32_t* ring, int& front, int head, uint32_t* gst) {
+    const int lane = (int)(threadIdx.x & 63);
+    if (head <= MT_N) {
+        if (lane == 0) gst[MT_N] = (uint32_t)head;
+        return;
+    }
+    const int b = MT_N * ((head - 1) / MT_N);
+    np_ensure(ring, front, b + MT_N);
+    for (int i = lane; i < MT_N; i += 64) gst[i] = ring[i];
     if (lane == 0) gst[MT_N] = (uint32_t)(head - b);
 }
 
@@ -551,7 +596,7 @@ __host__ __device__ inline WaveLds wave_lds(int L, int W, int P, int R) {
     const int NCW = (((L + 2 + 3) >> 2) * ((W + 2 + 3) >> 2) + 31) / 32;
     int o = 0;
     s.pyring = o; o += WR;                 // after the shuffles: vacated-cell bitmap; reward: leaf sums | leaf buffer
-    s.npring = o; o += WR;                 // after the rows: contested list | group heads | group starts
+    s.npring = o; o += MT_N;               // the numpy ring (np_ensure); after the rows: contested list
     s.aux = o; o += 512 + 16;              // planner queue + health group; events; leaf table
     s.rmapb = o; o += RW;
     s.tbits = o; o += RW;
@@ -746,22 +791,23 @@ struct WideCtl {
 };
 // Workgroup LDS (WNW waves): WNW env regions of step_lds_words, then WideCtl. A heavy
 // env keeps wave 0's region; the rows buffers overlay regions 1.. (dead once the
-// rows are done, when waves 1.. go on with other envs).
+// rows are done, when waves 1.. go on with other envs) and may run past them; WideCtl
+// follows whichever ends later.
 struct WideLds {
     int ctl, grp, NGmax, lin, LINW, lists, CHmax, end, total;
 };
 __host__ __device__ inline WideLds wide_lds(const evx_layout& l) {
     WideLds s;
     const int LW = step_lds_words(l);
-    s.ctl = WNW * LW;
-    s.total = s.ctl + 32;
     s.NGmax = (l.P + 63) / 64;
     s.grp = LW;                 // per group: numpy words | Python words | movers | Python offset
     s.lin = s.grp + ((4 * s.NGmax + 3) & ~3);
     s.LINW = ((2 * l.P + 1280) + 3) & ~3;  // numpy words of the step + MT history + slack
     s.lists = s.lin + s.LINW;
     s.CHmax = ((s.NGmax + WNW - 1) / WNW) * 64;  // planners per wave
-    s.end = s.lists + WNW * s.CHmax * 3;          // must be <= ctl
+    s.end = s.lists + WNW * s.CHmax * 3;
+    s.ctl = ((WNW * LW > s.end ? WNW * LW : s.end) + 3) & ~3;
+    s.total = s.ctl + 32;
     return s;
 }
 
@@ -1426,9 +1472,9 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
         const int tot = 2 * __popcll(nm);
         bool alive = act, died = false;
         if (tot) {
-            mt_ensure_w(npring, np_front, np_head + tot);
+            np_ensure(npring, np_front, np_head + tot);
             if (need) {
-                const double u = mt_double(npring, WRM, np_head + 2 * lanes_below(nm));
+                const double u = np_double(npring, np_head + 2 * lanes_below(nm));
                 if (update_health(hh, dg, u)) {
                     died = true;
                     alive = false;
@@ -1613,7 +1659,7 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
         PT_END(top);
     }
     // the numpy stream is finished for this step
-    mt_store_w(npring, np_front, np_head, st.np_mt + (size_t)e * EVX_MT_WORDS);
+    np_store(npring, np_front, np_head, st.np_mt + (size_t)e * EVX_MT_WORDS);
     EVX_COUNT(13, np_head);
     EVX_COUNT(11, nplan);
     }  // !WIDE
@@ -1661,7 +1707,7 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
         PT_END(lp);
         PT_BEGIN(grp);
         if (ncont <= CL_CAP) {
-            contested_groups(Lp, npring + 512, npring + 768, ncont, pb, pyring, py_front, py_head, lost, misc, err, cgp);
+            contested_groups(Lp, aux, aux + 256, ncont, pb, pyring, py_front, py_head, lost, misc, err, cgp);
         } else {  // rare: sort in this env's global scratch
             Lp = Lg;
             int k = 0;

@@ -158,6 +158,7 @@ struct Fwd {
     const float* stat;
     const __bf16* w1o;
     int stat_fs;
+    int stat_x0, stat_nx;  // the table's centres: x in [stat_x0, stat_x0 + stat_nx), every y
     // qfc1_kernel raw mode: f32 pre-activation (acc + bias, no ReLU / dropout) [N][512]
     float* raw;
     // X3 mode: danger residual features (evx_layout.obs_feat_lo / obs_feats_lo), lo weight
@@ -268,7 +269,9 @@ __device__ __forceinline__ uint2 cell_feat(const evx_obs& ob, int c, uint32_t v)
 // compact chunk's fragments meet the lo weights too (the features are exact in bf16
 // except the danger, whose lo rides in the extra chunks).
 // Column tile nt of a wave starts at ncol0 + nt * nstride.
-template <int MT, int NTW, int NWV, bool X3 = false>
+// KU: K-loop unroll (0: the compiler's choice; the x3 act passes 2 -- fully unrolled, the
+// per-chunk feature offsets were hoisted into ~70 live VGPRs and spilled)
+template <int MT, int NTW, int NWV, bool X3 = false, int KU = 0>
 __device__ __forceinline__ void fc1_tile(const Fwd& a, int m0, int ncol0, bool want_x, char* smem,
                                          f32x16 (&acc)[MT][NTW], int nstride = 32) {
     constexpr int NT = 64 * NWV, RT = 32 * MT;
@@ -367,8 +370,7 @@ __device__ __forceinline__ void fc1_tile(const Fwd& a, int m0, int ncol0, bool w
     if constexpr (AH == 2) loadB(1, bn);
     loadL(0, lc);
     __syncthreads();
-#pragma unroll 2
-    for (int kc = 0; kc < NKC; kc++) {
+    auto kstep = [&](int kc) {
         const int buf = kc & 1;
         if (kc + AH < NKC) loadB(kc + AH, AH == 2 ? bf : bn);
         if (kc + 1 < NKC) loadL(kc + 1, ln);
@@ -404,6 +406,12 @@ __device__ __forceinline__ void fc1_tile(const Fwd& a, int m0, int ncol0, bool w
             }
         }
         __syncthreads();
+    };
+    if constexpr (KU == 2) {
+#pragma unroll 2
+        for (int kc = 0; kc < NKC; kc++) kstep(kc);
+    } else {
+        for (int kc = 0; kc < NKC; kc++) kstep(kc);
     }
 }
 
@@ -607,8 +615,9 @@ __global__ __launch_bounds__(512, 1) void qact_kernel(Fwd a) {
             int pos = 0;
             if (m0 + tid < a.N) {
                 const evx_obs ob = a.obs[orow(a, m0 + tid)];
-                ok = min(max(ob.fire_step, 0), a.t_max) == a.stat_fs && ob.cx >= 0 && ob.cx <= a.L + 1 && ob.cy >= 0 && ob.cy <= a.W + 1;
-                pos = ok ? ob.cx * (a.W + 2) + ob.cy : 0;
+                ok = min(max(ob.fire_step, 0), a.t_max) == a.stat_fs && ob.cx >= a.stat_x0 &&
+                     ob.cx < a.stat_x0 + a.stat_nx && ob.cy >= 0 && ob.cy <= a.W + 1;
+                pos = ok ? (ob.cx - a.stat_x0) * (a.W + 2) + ob.cy : 0;
             }
             posS[tid] = pos;
         }
@@ -758,9 +767,9 @@ __global__ __launch_bounds__(512, 1) void qact3_kernel(Fwd a0) {
             int pos = 0;
             if (m0 + tid < a.N) {
                 const evx_obs ob = a.obs[orow(a, m0 + tid)];
-                ok = min(max(ob.fire_step, 0), a.t_max) == a.stat_fs && ob.cx >= 0 && ob.cx <= a.L + 1 && ob.cy >= 0 &&
-                     ob.cy <= a.W + 1;
-                pos = ok ? ob.cx * (a.W + 2) + ob.cy : 0;
+                ok = min(max(ob.fire_step, 0), a.t_max) == a.stat_fs && ob.cx >= a.stat_x0 &&
+                     ob.cx < a.stat_x0 + a.stat_nx && ob.cy >= 0 && ob.cy <= a.W + 1;
+                pos = ok ? (ob.cx - a.stat_x0) * (a.W + 2) + ob.cy : 0;
             }
             posS[tid] = pos;
         }
@@ -823,7 +832,7 @@ __global__ __launch_bounds__(512, 1) void qact3_kernel(Fwd a0) {
                 }
             }
         } else {
-            fc1_tile<4, 1, 8, true>(a, m0, col0, false, dsm, acc);  // ends with a barrier: A buffers free
+            fc1_tile<4, 1, 8, true, 2>(a, m0, col0, false, dsm, acc);  // ends with a barrier: A buffers free
         }
         const float bias[1] = {fast ? 0.f : a.b1[col0 + (lane & 31)]};  // the table holds the bias
 #pragma unroll
@@ -1806,6 +1815,10 @@ static int make_fwd(const evx_layout* lay, const evx_obs* obs, int32_t n, const 
     a.w1o = reinterpret_cast<const __bf16*>(p->w1o);
     a.stat = (p->w1o && !a.feats) ? p->stat : nullptr;  // the table is per layout: single layout only
     a.stat_fs = p->stat_fs;
+    a.stat_x0 = p->stat_nx > 0 ? p->stat_x0 : 0;
+    a.stat_nx = p->stat_nx > 0 ? p->stat_nx : lay->L + 2;
+    if (a.stat && (a.stat_x0 < 0 || a.stat_x0 + a.stat_nx > lay->L + 2))
+        return mfail(-22, "qmlp: the table's centre range must lie in [0, L + 2)");
     a.raw = nullptr;
     a.drop_mask = drop ? drop->mask : nullptr;
     if (a.drop_mask && !(dp > 0.f)) return mfail(-22, "qmlp_forward: an explicit dropout mask needs p > 0 (its scale)");

@@ -33,7 +33,8 @@ def compact_ref_cols() -> np.ndarray:
 
 class evx_qmlp_params(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in ["w1", "b1c", "w2", "w2t", "b2", "w3", "b3", "w1o", "stat"]] + \
-        [("stat_fs", C.c_int32), ("x3", C.c_int32)] + [(n, C.c_void_p) for n in ["w1l", "w2l", "w2tl", "w1ol"]]
+        [("stat_fs", C.c_int32), ("x3", C.c_int32)] + [(n, C.c_void_p) for n in ["w1l", "w2l", "w2tl", "w1ol"]] + \
+        [("stat_x0", C.c_int32), ("stat_nx", C.c_int32)]
 
 
 class evx_qmlp_dropout(C.Structure):
@@ -219,22 +220,29 @@ class MLPFast:
         """The squared-norm partials of a flat gradient buffer (evx_qmlp_sumsq_parts)."""
         mcheck(mlib().evx_qmlp_sumsq_parts(g.data_ptr(), ss.data_ptr(), _stream()), "qmlp_sumsq_parts")
 
-    def attach_static(self, lay_c, L: int, W: int, t_max: int):
+    def attach_static(self, lay_c, L: int, W: int, t_max: int, x_range=None):
         """Enable act()'s fast path for observations at fire step >= t_max (the fire has
         stopped spreading): fc1's pre-activation at zero occupancy for every window centre
-        of the layout, [(L+2)(W+2)][512] f32 (x3: f32-accurate), rebuilt with every repack and
-        every optimizer step (adam_step)."""
-        cx, cy = np.meshgrid(np.arange(L + 2), np.arange(W + 2), indexing="ij")
-        ob = np.zeros(((L + 2) * (W + 2), 8), np.int32)
+        of the layout, [nx (W+2)][512] f32 (x3: f32-accurate), rebuilt with every repack and
+        every optimizer step (adam_step). x_range = (x0, x1): only centres with x0 <= x <= x1
+        (Map.robot_range, envs/map.py:75: a robot never leaves it), default every x."""
+        x0, x1 = (0, L + 1) if x_range is None else (int(x_range[0]), int(x_range[1]))
+        if not 0 <= x0 <= x1 <= L + 1:
+            raise ValueError("attach_static: x_range must lie in [0, L + 1]")
+        nx = x1 - x0 + 1
+        cx, cy = np.meshgrid(np.arange(x0, x1 + 1), np.arange(W + 2), indexing="ij")
+        ob = np.zeros((nx * (W + 2), 8), np.int32)
         ob[:, 4], ob[:, 5], ob[:, 6] = cx.ravel(), cy.ravel(), t_max
         self._static = (lay_c, torch.from_numpy(ob).to(self.device),
-                        torch.empty((L + 2) * (W + 2), HID, dtype=torch.float32, device=self.device))
+                        torch.empty(nx * (W + 2), HID, dtype=torch.float32, device=self.device))
         self._rebuild_static()
         self.c.w1o, self.c.stat, self.c.stat_fs = self.w1o.data_ptr(), self._static[2].data_ptr(), int(t_max)
+        self.c.stat_x0, self.c.stat_nx = x0, nx
 
     def detach_static(self):
         self._static = None
         self.c.w1o = self.c.stat = None
+        self.c.stat_x0 = self.c.stat_nx = 0
 
     def _rebuild_static(self):
         lay_c, ob, T = self._static

@@ -235,8 +235,8 @@ class VecTrainer:
             # occupancy columns; the act visits those envs first (VecEnv.act_perm) so its row tiles
             # are uniform. x3: on by default (the table replaces ~3/4 of fc1's products); bf16: off
             # by default (the rebuild costs what the act saves, tools/gpu_ab_static.sh)
-            lc = self.lay.c
-            self.fast.attach_static(lc, lc.L, lc.W, lc.t_max)
+            lc = self.lay.c  # centres only where robots can be (Map.robot_range): 55 of 130 columns at cfg3
+            self.fast.attach_static(lc, lc.L, lc.W, lc.t_max, x_range=(max(lc.rx_lo, 0), min(lc.rx_hi, lc.L + 1)))
             self._perm = torch.zeros(E, dtype=torch.int32, device=self.device)
             self.env.act_perm(self._perm)
 

@@ -340,6 +340,9 @@ typedef struct {
     const uint16_t *w1l, *w2l, *w2tl;
     /* x3 act fast path: the lo part of w1o (w1o then holds the hi part; evx_qmlp_pack3 / _adam_pack3) */
     const uint16_t *w1ol;
+    /* the table's window centres: x in [stat_x0, stat_x0 + stat_nx) (Map.robot_range: robots never
+     * leave it), every y in [0, W + 1], row (x - stat_x0) * (W + 2) + y; stat_nx = 0: all L + 2 */
+    int32_t stat_x0, stat_nx;
 } evx_qmlp_params;
 
 typedef struct {

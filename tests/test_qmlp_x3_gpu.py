@@ -267,14 +267,16 @@ def test_fused_learn_chain_matches_separate_launches(hook):
         assert torch.equal(got, want)
 
 
-def test_x3_act_static_table_and_env_order():
+@pytest.mark.parametrize("xr", ["all", "robot_range"])
+def test_x3_act_static_table_and_env_order(xr):
     """x3 act fast path: rows whose fire has reached the layout's last step start fc1 from the
     per-centre table of the static features (evx_qmlp_stat, x3) and add the occupancy columns
     (hi + lo weights); VecEnv.act_perm visits those envs first so act tiles are uniform.
     Against the plain x3 act on the same observations: Q within f32 reassociation (and not
     bit-identical on the table rows: the table path ran), greedy actions equal, epsilon draws
     and dropout rows keyed by the original row (epsilon = 1: identical actions); act_perm is
-    the stable partition of the envs by fire step >= t_max."""
+    the stable partition of the envs by fire step >= t_max. robot_range: the table covers only
+    the centres of Map.robot_range's columns (the trainer's table)."""
     _need_gpu()
     from evacx.qnet import DROPOUT_P, Learner
     lay, env = _env_obs(E=256, R=4)
@@ -298,7 +300,10 @@ def test_x3_act_static_table_and_env_order():
     res = {}
     for mode in ("plain", "table"):
         if mode == "table":
-            fast.attach_static(lay.c, int(lay.c.L), int(lay.c.W), t_max)
+            x_range = (int(lay.c.rx_lo), int(lay.c.rx_hi)) if xr == "robot_range" else None
+            fast.attach_static(lay.c, int(lay.c.L), int(lay.c.W), t_max, x_range=x_range)
+            if x_range is not None:
+                assert fast._static[2].shape[0] == (x_range[1] - x_range[0] + 1) * (int(lay.c.W) + 2)
         kw = dict(perm=perm, rows_per_env=R) if mode == "table" else {}
         q = torch.empty(n, 5, device="cuda")
         a0 = torch.empty(n, dtype=torch.int32, device="cuda")
