@@ -119,6 +119,42 @@ __device__ __forceinline__ bool in_map(const Geo& g, const uint32_t* validb, int
     return x >= 1 && x <= g.L && y >= 1 && y <= g.W;
 }
 
+// Compact observations of robots r0 .. r0 + 3 (< R) built by one wave in one pass: the 8 LDS
+// bit reads per lane issue together, lane k stores robot r0 + k's record.
+__device__ __forceinline__ void write_obs4(const Geo& g, const uint32_t* rmapb, const uint32_t* cen, int r0, int R,
+                                           int fs, uint32_t lid, evx_obs* dst) {
+    const int lane = threadIdx.x & 63;
+    const int i0 = lane / 11, j0 = lane - 11 * (lane / 11);
+    const int c1 = lane + 64, i1 = c1 / 11, j1 = c1 - 11 * (c1 / 11);
+    unsigned long long m[4][2];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int r = r0 + k < R ? r0 + k : r0;
+        const int cx = rp_x(cen[r]), cy = rp_y(cen[r]);
+        bool b0 = false, b1 = false;
+        {
+            const int mx = cx + i0 - 5, my = cy + j0 - 5;
+            if (in_map(g, nullptr, mx, my)) b0 = bit_get(rmapb, mx * g.GY + my);
+        }
+        {
+            const int mx = cx + i1 - 5, my = cy + j1 - 5;
+            if (c1 < 121 && in_map(g, nullptr, mx, my)) b1 = bit_get(rmapb, mx * g.GY + my);
+        }
+        m[k][0] = __ballot(b0);
+        m[k][1] = __ballot(b1);
+    }
+    if (lane < 4 && r0 + lane < R) {
+        const int k = lane;
+        const unsigned long long a0 = k == 0 ? m[0][0] : k == 1 ? m[1][0] : k == 2 ? m[2][0] : m[3][0];
+        const unsigned long long a1 = k == 0 ? m[0][1] : k == 1 ? m[1][1] : k == 2 ? m[2][1] : m[3][1];
+        const uint32_t c = cen[r0 + k];
+        uint4 a = make_uint4((uint32_t)a0, (uint32_t)(a0 >> 32), (uint32_t)a1, (uint32_t)(a1 >> 32));
+        uint4 b = make_uint4((uint32_t)rp_x(c), (uint32_t)rp_y(c), (uint32_t)fs, lid);
+        reinterpret_cast<uint4*>(dst + r0 + k)[0] = a;
+        reinterpret_cast<uint4*>(dst + r0 + k)[1] = b;
+    }
+}
+
 // Compact observation of one robot built by one wave (bits by ballot).
 __device__ __forceinline__ void write_obs(const Geo& g, const uint32_t* validb, const uint32_t* rmapb, int cx,
                                           int cy, int fs, uint32_t lid, evx_obs* dst) {
@@ -1370,6 +1406,10 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     for (int d = 0; d < 8; d++) doff[d] = move_dx(d) * GY + move_dy(d);
 
     int nplan = 0, n_died = 0;
+    // the persons in play that survive update_health, compacted in list order over the
+    // not-dead list's consumed entries: the reward pass walks them instead of the whole
+    // not-dead list (a light path; the wide rows keep nrl = nnd)
+    int nrl = nnd;
     bool any_cont = false;
     PT_DECL(np);
     PT_DECL(hsum);
@@ -1411,6 +1451,7 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     int* qc = reinterpret_cast<int*>(aux + 256);        // first Python-stream word
     double* hc = reinterpret_cast<double*>(aux + 384);  // one group of not-dead healths (lane 0 sums them)
     int qn = 0;
+    int nal = 0;  // alive persons in play so far (see nrl)
     auto score_batch = [&](int n) {  // People.find_best_direction for queue entries [0, n)
         PT_BEGIN(sbl);
         const bool has = lane < n;
@@ -1483,6 +1524,13 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
             np_head += tot;
         }
         n_died += __popcll(__ballot(died));
+        {
+            // entry i of the not-dead list was read two iterations ago: the compacted alive list
+            // (index <= i) overwrites only consumed entries
+            const unsigned long long am = __ballot(alive);
+            if (alive) ndl[nal + lanes_below(am)] = make_uint2((uint32_t)p, v);
+            nal += __popcll(am);
+        }
         PT_END(np);
         PT_BEGIN(hsum);
         {  // health total over the still-not-dead, in person order (lane 0). The
@@ -1660,6 +1708,7 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     }
     // the numpy stream is finished for this step
     np_store(npring, np_front, np_head, st.np_mt + (size_t)e * EVX_MT_WORDS);
+    nrl = nal;
     EVX_COUNT(13, np_head);
     EVX_COUNT(11, nplan);
     }  // !WIDE
@@ -1863,10 +1912,11 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     const int vx = rp_x(view), vy = rp_y(view);
     double gq_t = 0.0;
     int q = 0;
-    // remaining persons = the not-dead list minus this step's deaths and evacuations
+    // remaining persons = the list nrl (the alive persons in play, or the whole not-dead list)
+    // minus this step's deaths and evacuations
     auto reward_half = [&](int i, uint32_t v, double hv) {
         PT_BEGIN(rew);
-        const bool rem = i < nnd && !pk_safe(v) && !pk_dead(v);
+        const bool rem = i < nrl && !pk_safe(v) && !pk_dead(v);
         const long long x2 = 2 * pk_x(v) + 1, y2 = 2 * pk_y(v) + 1;
         const long long dxr = x2 - 2LL * vx, dyr = y2 - 2LL * vy;
         const long long n4 = dxr * dxr + dyr * dyr;  // (2*distance)^2, exact
@@ -1885,13 +1935,13 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     };
     auto load_idx = [&](int i) -> uint32_t {
         uint32_t p = 0u;
-        if (i < nnd) p = ndl[i].x;
+        if (i < nrl) p = ndl[i].x;
         return p;
     };
     auto load_pw = [&](int i, uint32_t p, uint32_t& w, double& h) {
         w = DONEPK;
         h = 0.0;
-        if (i < nnd) {
+        if (i < nrl) {
             w = pk_g[p];
             h = h_g[p];
         }
@@ -1905,7 +1955,7 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     }
 #pragma unroll
     for (int k = 0; k < GQ; k++) load_pw(64 * k + lane, nxj[k], nxw[k], nxhv[k]);
-    const int NITR = (nnd + 64 * GQ - 1) / (64 * GQ);
+    const int NITR = (nrl + 64 * GQ - 1) / (64 * GQ);
     for (int it = 0; it < NITR; it++) {
         PT_BEGIN(rtop);
         const int i0 = it * 64 * GQ + lane;
@@ -2054,11 +2104,16 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     const bool fin = __builtin_amdgcn_readfirstlane((int)((evac + dead == P) || (0.5 * (double)(cur_step + 1) >= 600.0)));
     const bool ar = out.obs_term != nullptr && fin;
     evx_obs* obs_dst = ar ? out.obs_term : out.obs;
-    for (int r = 0; r < R; r++) {
-        const uint32_t c = (r == 0) ? view : robots[r];
-        write_obs(g, nullptr, rmapb, rp_x(c), rp_y(c), fs1, st.layout_idx ? (uint32_t)st.layout_idx[e] : 0u,
-                  obs_dst + (size_t)e * R + r);
-    }
+    // robot 0's observation is centred on Map.robot_position (view), the others on their own
+    // positions: the centres go to the robots table's slot 0 for the pass (wave-private LDS)
+    const uint32_t rob0 = robots[0];
+    if (lane == 0) robots[0] = view;
+    wave_fence();
+    const uint32_t lid = st.layout_idx ? (uint32_t)st.layout_idx[e] : 0u;
+    for (int r0 = 0; r0 < R; r0 += 4) write_obs4(g, rmapb, robots, r0, R, fs1, lid, obs_dst + (size_t)e * R);
+    wave_fence();
+    if (lane == 0) robots[0] = rob0;
+    wave_fence();
     EVX_STAMP(8);
     if (ar) {
         __threadfence();  // this wave's state writes complete and visible before the reset reads them
