@@ -1264,6 +1264,11 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     uint32_t* scr = st.scratch + (size_t)e * SW;
     uint2* plan = reinterpret_cast<uint2*>(scr);           // (person, cell | dir << 24) of every mover
     uint2* ndl = reinterpret_cast<uint2*>(scr + 2 * P);    // (person, person word) of the not-dead
+    // light path: the persons in play (not safe, not dead) as (person | not-dead index << 16, word)
+    // in the wide path's health region, and every not-dead person's health in list order
+    // (frozen for the safe ones, updated by the rows for those in play) in the spill region
+    uint2* ipl = reinterpret_cast<uint2*>(scr + wave_hv_offset(P));
+    double* hl = reinterpret_cast<double*>(scr + 4 * P);
     const int n2P = pow2_ceil(P < 64 ? 64 : P);
     uint32_t* Lg = scr + 4 * P;                             // spill: contested list
     uint32_t* Hg = Lg + n2P;                                // spill: group heads
@@ -1289,6 +1294,19 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
             wpy[j] = gpy[lane + 64 * j];
             wnp[j] = gnp[lane + 64 * j];
         }
+    }
+    // the first rows of person words, in flight with the MT and rmap loads (the not-dead scan
+    // below prefetches each next batch while it processes one)
+    // light path: the rows' healths too (contiguous, all persons: no dependence on the words)
+    constexpr int PKB = WIDE ? 12 : 8;
+    uint32_t vv[PKB];
+    double hr[WIDE ? 1 : PKB];
+#pragma unroll
+    for (int j = 0; j < PKB; j++) {
+        const int p = j * 64 + lane;
+        vv[j] = 2u << 24;
+        if (p < P) vv[j] = pk_g[p];
+        if constexpr (!WIDE) hr[j] = p < P ? h_g[p] : 0.0;
     }
     const uint32_t* grm = st.rmap + (size_t)e * g.RW;
     for (int i0 = 0; i0 < g.RW; i0 += 16 * 64) {
@@ -1345,23 +1363,39 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     PT_BEGIN(ld2);
     // the not-dead persons in person order (sum(... if not p.dead) and the movers
     // never look at anyone else)
-    int nnd = 0, n_safe = 0;
-    for (int r0 = 0; r0 < NR; r0 += 12) {  // 12 rows of loads in flight
-        uint32_t vv[12];
+    int nnd = 0, n_safe = 0, nip = 0;
+    for (int r0 = 0; r0 < NR; r0 += PKB) {  // PKB rows processed while the next PKB are in flight
+        uint32_t nx[PKB];
+        double hn[WIDE ? 1 : PKB];
 #pragma unroll
-        for (int j = 0; j < 12; j++) {
-            const int p = (r0 + j) * 64 + lane;
-            vv[j] = 2u << 24;
-            if (p < P) vv[j] = pk_g[p];
+        for (int j = 0; j < PKB; j++) {
+            const int p = (r0 + PKB + j) * 64 + lane;
+            nx[j] = 2u << 24;
+            if (p < P) nx[j] = pk_g[p];
+            if constexpr (!WIDE) hn[j] = p < P ? h_g[p] : 0.0;
         }
 #pragma unroll
-        for (int j = 0; j < 12; j++) {
+        for (int j = 0; j < PKB; j++) {
+            pin(vv[j]);
             const int p = (r0 + j) * 64 + lane;
             const bool nd = !pk_dead(vv[j]);
             const unsigned long long m = __ballot(nd);
-            if (nd) ndl[nnd + lanes_below(m)] = make_uint2((uint32_t)p, vv[j]);
+            const int k = nnd + lanes_below(m);
+            if (nd) ndl[k] = make_uint2((uint32_t)p, vv[j]);
+            if constexpr (!WIDE) {
+                if (nd) hl[k] = hr[j];
+                const bool ip = nd && !pk_safe(vv[j]);
+                const unsigned long long mi = __ballot(ip);
+                if (ip) ipl[nip + lanes_below(mi)] = make_uint2((uint32_t)p | ((uint32_t)k << 16), vv[j]);
+                nip += __popcll(mi);
+            }
             nnd += __popcll(m);
             n_safe += __popcll(__ballot(nd && pk_safe(vv[j])));
+        }
+#pragma unroll
+        for (int j = 0; j < PKB; j++) {
+            vv[j] = nx[j];
+            if constexpr (!WIDE) hr[j] = hn[j];
         }
     }
     wave_fence();
@@ -1406,10 +1440,11 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     for (int d = 0; d < 8; d++) doff[d] = move_dx(d) * GY + move_dy(d);
 
     int nplan = 0, n_died = 0;
-    // the persons in play that survive update_health, compacted in list order over the
-    // not-dead list's consumed entries: the reward pass walks them instead of the whole
-    // not-dead list (a light path; the wide rows keep nrl = nnd)
+    // the persons in play that survive update_health, compacted in list order over the in-play
+    // list's consumed entries: the reward pass walks them (light path; the wide rows: the
+    // not-dead list, nrl = nnd)
     int nrl = nnd;
+    const uint2* rl = ndl;
     bool any_cont = false;
     PT_DECL(np);
     PT_DECL(hsum);
@@ -1449,7 +1484,6 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     uint32_t* qa = aux;        // person | candidate mask << 16   (<= 127 queued)
     uint32_t* qb = aux + 128;  // x | y << 12
     int* qc = reinterpret_cast<int*>(aux + 256);        // first Python-stream word
-    double* hc = reinterpret_cast<double*>(aux + 384);  // one group of not-dead healths (lane 0 sums them)
     int qn = 0;
     int nal = 0;  // alive persons in play so far (see nrl)
     auto score_batch = [&](int n) {  // People.find_best_direction for queue entries [0, n)
@@ -1500,12 +1534,13 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
         PT_END(sbt);
     };
     // one group (64 list entries, in person order) of People.run phases 1+2
+    // one group (64 entries of the in-play list, in person order) of People.run phases 1+2
     auto person_half = [&](int i, uint2 en, double hh, double ac, double dg, uint32_t nv) {
         PT_BEGIN(np);
-        const bool inr = i < nnd;
-        const int p = (int)en.x;
+        const bool inr = i < nip;
+        const int p = (int)(en.x & 0xffffu);
         const uint32_t v = en.y;
-        const bool act = inr && !((v >> 24) & 3u);
+        const bool act = inr;
         const int x = pk_x(v), y = pk_y(v), cold = x * GY + y;
         // phase 1: Person.update_state -> update_health (numpy stream)
         const bool need = act && dg > 0;
@@ -1528,41 +1563,11 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
             // entry i of the not-dead list was read two iterations ago: the compacted alive list
             // (index <= i) overwrites only consumed entries
             const unsigned long long am = __ballot(alive);
-            if (alive) ndl[nal + lanes_below(am)] = make_uint2((uint32_t)p, v);
+            if (alive) ipl[nal + lanes_below(am)] = make_uint2((uint32_t)p, v);
             nal += __popcll(am);
         }
         PT_END(np);
-        PT_BEGIN(hsum);
-        {  // health total over the still-not-dead, in person order (lane 0). The
-           // group's values are compacted to the front of 64 slots, the rest +0.0
-           // (healths are >= +0, so adding +0.0 leaves the running sum unchanged),
-           // and folded with 16 values in flight.
-            const bool hv = inr && !died;
-            const unsigned long long hm = __ballot(hv);
-            hc[hv ? lanes_below(hm) : __popcll(hm) + lanes_below(~hm)] = hv ? hh : 0.0;
-            wave_fence();
-            if (lane == 0) {
-                const double2* h2 = reinterpret_cast<const double2*>(hc);
-                double2 q0 = h2[0], q1 = h2[1], q2 = h2[2], q3 = h2[3];
-                double2 r0 = h2[4], r1 = h2[5], r2 = h2[6], r3 = h2[7];
-#pragma unroll
-                for (int c = 0; c < 8; c++) {
-                    double2 s0 = q0, s1 = q1, s2 = q2, s3 = q3;
-                    if (c + 2 < 8) {
-                        s0 = h2[4 * (c + 2)];
-                        s1 = h2[4 * (c + 2) + 1];
-                        s2 = h2[4 * (c + 2) + 2];
-                        s3 = h2[4 * (c + 2) + 3];
-                    }
-                    total += q0.x; total += q0.y; total += q1.x; total += q1.y;
-                    total += q2.x; total += q2.y; total += q3.x; total += q3.y;
-                    q0 = r0; q1 = r1; q2 = r2; q3 = r3;
-                    r0 = s0; r1 = s1; r2 = s2; r3 = s3;
-                }
-            }
-            wave_fence();
-        }
-        PT_END(hsum);
+        if (inr) hl[en.x >> 16] = died ? 0.0 : hh;  // the list-order health the fold reads (dead: +0.0)
         PT_BEGIN(plan);
         // phase 2: accumulate; candidates of find_best_direction
         bool planner = false;
@@ -1610,19 +1615,18 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     const uint2 NOONE = make_uint2(0u, DONEPK);
     auto load_entry = [&](int i) -> uint2 {
         uint2 en = NOONE;
-        if (i < nnd) en = ndl[i];
+        if (i < nip) en = ipl[i];
         return en;
     };
     auto load_data = [&](int i, uint2 en, double& h, double& a, double& dg, uint32_t& nv) {
         h = 0.0; a = 0.0; dg = 0.0; nv = 0u;
-        if (i < nnd) {
-            h = h_g[en.x];
-            if (!((en.y >> 24) & 3u)) {
-                const int c = pk_x(en.y) * GY + pk_y(en.y);
-                a = a_g[en.x];
-                dg = dpt[c];
-                nv = nbv[c];
-            }
+        if (i < nip) {
+            const uint32_t pe = en.x & 0xffffu;
+            const int c = pk_x(en.y) * GY + pk_y(en.y);
+            h = h_g[pe];
+            a = a_g[pe];
+            dg = dpt[c];
+            nv = nbv[c];
         }
     };
     uint2 nxe[GQ], nne[GQ];
@@ -1635,7 +1639,7 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     }
 #pragma unroll
     for (int k = 0; k < GQ; k++) load_data(64 * k + lane, nxe[k], nxh[k], nxa[k], nxg[k], nxv[k]);
-    const int NIT = (nnd + 64 * GQ - 1) / (64 * GQ);
+    const int NIT = (nip + 64 * GQ - 1) / (64 * GQ);
     for (int it = 0; it <= NIT; it++) {  // the extra iteration only drains the planner queue
         PT_BEGIN(top);
         const int i0 = it * 64 * GQ + lane;
@@ -1709,11 +1713,62 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     // the numpy stream is finished for this step
     np_store(npring, np_front, np_head, st.np_mt + (size_t)e * EVX_MT_WORDS);
     nrl = nal;
+    rl = ipl;
     EVX_COUNT(13, np_head);
     EVX_COUNT(11, nplan);
     }  // !WIDE
     any_cont = __ballot(any_cont) != 0;
     wave_sync();  // plan[] and the person writes are visible to every lane
+    if constexpr (!WIDE) {
+        // CPython's sum(p.health for p in self.people.list if not p.dead): lane 0 folds the
+        // not-dead list's healths (after update_health; +0.0 for this step's deaths, which leaves
+        // the running sum unchanged) in list order, staged 64 at a time through LDS; the loads of
+        // the next 4 groups are in flight while a group is folded
+        PT_BEGIN(hsum);
+        double* hc = reinterpret_cast<double*>(aux + 384);
+        constexpr int FB = 4;
+        double fv[FB];
+#pragma unroll
+        for (int k = 0; k < FB; k++) fv[k] = 64 * k + lane < nnd ? hl[64 * k + lane] : 0.0;
+        for (int i0 = 0; i0 < nnd; i0 += 64 * FB) {
+            double fn[FB];
+#pragma unroll
+            for (int k = 0; k < FB; k++) {
+                const int i = i0 + 64 * (FB + k) + lane;
+                fn[k] = i < nnd ? hl[i] : 0.0;
+            }
+#pragma unroll
+            for (int k = 0; k < FB; k++) {
+                if (i0 + 64 * k >= nnd) break;
+                pin(fv[k]);
+                hc[lane] = fv[k];
+                wave_fence();
+                if (lane == 0) {
+                    const double2* h2 = reinterpret_cast<const double2*>(hc);
+                    double2 q0 = h2[0], q1 = h2[1], q2 = h2[2], q3 = h2[3];
+                    double2 r0 = h2[4], r1 = h2[5], r2 = h2[6], r3 = h2[7];
+#pragma unroll
+                    for (int c = 0; c < 8; c++) {
+                        double2 s0 = q0, s1 = q1, s2 = q2, s3 = q3;
+                        if (c + 2 < 8) {
+                            s0 = h2[4 * (c + 2)];
+                            s1 = h2[4 * (c + 2) + 1];
+                            s2 = h2[4 * (c + 2) + 2];
+                            s3 = h2[4 * (c + 2) + 3];
+                        }
+                        total += q0.x; total += q0.y; total += q1.x; total += q1.y;
+                        total += q2.x; total += q2.y; total += q3.x; total += q3.y;
+                        q0 = r0; q1 = r1; q2 = r2; q3 = r3;
+                        r0 = s0; r1 = s1; r2 = s2; r3 = s3;
+                    }
+                }
+                wave_fence();
+            }
+#pragma unroll
+            for (int k = 0; k < FB; k++) fv[k] = fn[k];
+        }
+        PT_END(hsum);
+    }
     EVX_STAMP(2);
 
     // The move plan in HBM is walked 4 x 64 entries at a time, loads first.
@@ -1935,7 +1990,7 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     };
     auto load_idx = [&](int i) -> uint32_t {
         uint32_t p = 0u;
-        if (i < nrl) p = ndl[i].x;
+        if (i < nrl) p = rl[i].x & 0xffffu;
         return p;
     };
     auto load_pw = [&](int i, uint32_t p, uint32_t& w, double& h) {
