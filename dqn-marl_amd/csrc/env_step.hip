@@ -1283,6 +1283,12 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     PT_DECL(ld3);
     PT_BEGIN(ld1);
     // every global read of this phase is issued before any of it is used
+    uint32_t rp_pre = 0u;  // this lane's robot (Map.move_robot below)
+    int a_pre = -1;
+    if (lane < R) {
+        rp_pre = st.robots[(size_t)e * R + lane];
+        a_pre = actions[(size_t)e * R + lane];
+    }
     const uint32_t* gpy = st.py_mt + (size_t)e * EVX_MT_WORDS;
     const uint32_t* gnp = st.np_mt + (size_t)e * EVX_MT_WORDS;
     uint32_t wpy[10], wnp[10];
@@ -1341,8 +1347,8 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     // Map.move_robot for every robot (envs/map.py:160-201); robots never interact.
     bool valid_a0 = false;
     for (int r = lane; r < R; r += 64) {
-        uint32_t rp = st.robots[(size_t)e * R + r];
-        const int a = actions[(size_t)e * R + r];
+        uint32_t rp = r == lane ? rp_pre : st.robots[(size_t)e * R + r];
+        const int a = r == lane ? a_pre : actions[(size_t)e * R + r];
         if (a >= 0 && a <= 4) {
             const int x = rp_x(rp), y = rp_y(rp);
             int nx = x, ny = y;
@@ -1409,18 +1415,22 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     int rr = 0;
     while ((rr + 1) * (rr + 1) < rd2) rr++;
     const int rb = rr + 1;  // a neighbour within range of a robot lies within rb of it in x and y
-    if (rd2 > 0) {
-        for (int r = 0; r < R; r++) {
-            const uint32_t rp = robots[r];
-            const int bx0 = max(rp_x(rp) - rr, 0) >> 2, bx1 = min(rp_x(rp) + rr, g.L + 1) >> 2;
-            const int by0 = max(rp_y(rp) - rr, 0) >> 2, by1 = min(rp_y(rp) + rr, g.W + 1) >> 2;
-            if (bx1 < bx0 || by1 < by0) continue;
-            const int nby = by1 - by0 + 1;
-            const float inv = 1.0f / (float)nby;
-            for (int c = lane; c < (bx1 - bx0 + 1) * nby; c += 64) {
-                const int q = (int)(((float)c + 0.5f) * inv);  // c / nby, exact for c < 2^20
-                const int b = (bx0 + q) * BY + by0 + (c - q * nby);
-                atomicOr(&nearc[b >> 5], 1u << (b & 31));
+    if (rd2 > 0) {  // 16 robots per pass, 4 lanes each (a robot's range spans few blocks)
+        for (int r0 = 0; r0 < R; r0 += 16) {
+            const int r = r0 + (lane >> 2), sub = lane & 3;
+            if (r < R) {
+                const uint32_t rp = robots[r];
+                const int bx0 = max(rp_x(rp) - rr, 0) >> 2, bx1 = min(rp_x(rp) + rr, g.L + 1) >> 2;
+                const int by0 = max(rp_y(rp) - rr, 0) >> 2, by1 = min(rp_y(rp) + rr, g.W + 1) >> 2;
+                if (bx1 >= bx0 && by1 >= by0) {
+                    const int nby = by1 - by0 + 1;
+                    const float inv = 1.0f / (float)nby;
+                    for (int c = sub; c < (bx1 - bx0 + 1) * nby; c += 4) {
+                        const int q = (int)(((float)c + 0.5f) * inv);  // c / nby, exact for c < 2^20
+                        const int b = (bx0 + q) * BY + by0 + (c - q * nby);
+                        atomicOr(&nearc[b >> 5], 1u << (b & 31));
+                    }
+                }
             }
         }
     }
