@@ -1387,8 +1387,10 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
             const bool nd = !pk_dead(vv[j]);
             const unsigned long long m = __ballot(nd);
             const int k = nnd + lanes_below(m);
-            if (nd) ndl[k] = make_uint2((uint32_t)p, vv[j]);
-            if constexpr (!WIDE) {
+            if constexpr (WIDE) {
+                if (nd) ndl[k] = make_uint2((uint32_t)p, vv[j]);
+                n_safe += __popcll(__ballot(nd && pk_safe(vv[j])));
+            } else {  // the light path needs only the in-play list and the list-order healths
                 if (nd) hl[k] = hr[j];
                 const bool ip = nd && !pk_safe(vv[j]);
                 const unsigned long long mi = __ballot(ip);
@@ -1396,7 +1398,6 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
                 nip += __popcll(mi);
             }
             nnd += __popcll(m);
-            n_safe += __popcll(__ballot(nd && pk_safe(vv[j])));
         }
 #pragma unroll
         for (int j = 0; j < PKB; j++) {
@@ -1404,6 +1405,7 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
             if constexpr (!WIDE) hr[j] = hn[j];
         }
     }
+    if constexpr (!WIDE) n_safe = nnd - nip;
     wave_fence();
     PT_END(ld2);
     PT_BEGIN(ld3);
