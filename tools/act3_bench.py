@@ -16,6 +16,9 @@ from evacx.qnet import DROPOUT_P, Learner  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--rows", type=int, default=1 << 19)
 ap.add_argument("--iters", type=int, default=20)
+ap.add_argument("--table-frac", type=float, default=0.0,
+                help="fraction of rows (the first ones) at the fire's last step, through the act table "
+                     "(attach_static over Map.robot_range, as the trainer)")
 args = ap.parse_args()
 E, R = 4096, 16
 lay = DeviceLayout(build_tables(synthetic(128, 128, R)), 2276)
@@ -28,6 +31,11 @@ obs = env.obs.view(-1, 8)
 reps = (args.rows + obs.shape[0] - 1) // obs.shape[0]
 obs = obs.repeat(reps, 1)[:args.rows].contiguous()
 lr = Learner(kind="mlp", precision="f32", seed=1)
+if args.table_frac > 0:
+    c = lay.c
+    lr.fast.attach_static(c, c.L, c.W, c.t_max, x_range=(c.rx_lo, c.rx_hi))
+    nt = int(args.rows * args.table_frac) // 128 * 128
+    obs[:nt, 6] = int(c.t_max)
 act = torch.empty(args.rows, dtype=torch.int32, device="cuda")
 for i in range(3):
     lr.fast.act(lay.c, obs.view(-1), args.rows, drop=(1, i, DROPOUT_P), actions=act, epsilon=0.1)
