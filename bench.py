@@ -330,7 +330,8 @@ def main():
         cpu = cpu_baseline(cpu_snap, env.lay.R, lay_tables, P, args, E)
     if rank == 0:
         prec = args.precision
-        qdesc = ("f32 Q-net (bf16x3-split MFMA operands)" if prec == "f32" and tr.fast is not None
+        lp = tr.learner.precision if tr.learner is not None else prec
+        qdesc = ("f32 Q-net (bf16x3-split MFMA operands)" if prec == "f32" and (tr.fast is not None or lp == "x3")
                  else f"{prec} Q-net")
         line = {
             "metric": METRIC,

@@ -235,6 +235,121 @@ __global__ __launch_bounds__(256) void gemm128_kernel(evx_gemm_desc g, int kspli
     }
 }
 
+// gemm128 in the f32-accurate x3 mode (EVX_PREC_X3, as the fused MLP's): every f32 operand is
+// staged in LDS as bf16 hi = bf16(v) and lo = bf16(v - hi), a product as hi*hi + hi*lo + lo*hi
+// on v_mfma_f32_32x32x16_bf16 (relative error ~2^-16 per product, f32 accumulation): 3 bf16
+// MFMAs per 16-deep step instead of 8 f32 32x32x2 ones, and 16-B LDS reads instead of 4-B.
+__global__ __launch_bounds__(256) void gemm128x3_kernel(evx_gemm_desc g, int ksplit_len) {
+    constexpr int PK = BK + 8;  // row pitch (bf16): 20 words, conflict-free 16-B reads
+    __shared__ __attribute__((aligned(16))) __bf16 As[2][TB][PK];
+    __shared__ __attribute__((aligned(16))) __bf16 Bs[2][TB][PK];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = w >> 1, wn = w & 1;
+    const int m0 = blockIdx.y * TB, n0 = blockIdx.x * TB;
+    const int kb = blockIdx.z * ksplit_len, ke = min(g.K, kb + ksplit_len);
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int j = 0; j < 2; j++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc[i][j][r] = 0.f;
+    const bool a_kc = g.sak == 1, b_nc = g.sbn == 1;
+    float ra[16], rb[16];
+    auto fetch = [&](int k0) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const int idx = tid + 256 * i;
+            int mm, kk;
+            if (a_kc) { mm = idx >> 5; kk = idx & 31; } else { kk = idx >> 7; mm = idx & 127; }
+            const int gm = m0 + mm, gk = k0 + kk;
+            ra[i] = (gm < g.M && gk < ke) ? g.A[(int64_t)gm * g.sam + (int64_t)gk * g.sak] : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const int idx = tid + 256 * i;
+            int nn, kk;
+            if (b_nc) { kk = idx >> 7; nn = idx & 127; } else { nn = idx >> 5; kk = idx & 31; }
+            const int gn = n0 + nn, gk = k0 + kk;
+            rb[i] = (gn < g.N && gk < ke) ? g.B[(int64_t)gk * g.sbk + (int64_t)gn * g.sbn] : 0.f;
+        }
+    };
+    auto stash = [&]() {
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const int idx = tid + 256 * i;
+            int mm, kk;
+            if (a_kc) { mm = idx >> 5; kk = idx & 31; } else { kk = idx >> 7; mm = idx & 127; }
+            const __bf16 hi = (__bf16)ra[i];
+            As[0][mm][kk] = hi;
+            As[1][mm][kk] = (__bf16)(ra[i] - (float)hi);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const int idx = tid + 256 * i;
+            int nn, kk;
+            if (b_nc) { kk = idx >> 7; nn = idx & 127; } else { nn = idx >> 5; kk = idx & 31; }
+            const __bf16 hi = (__bf16)rb[i];
+            Bs[0][nn][kk] = hi;
+            Bs[1][nn][kk] = (__bf16)(rb[i] - (float)hi);
+        }
+    };
+    if (kb < ke) fetch(kb);
+    for (int k0 = kb; k0 < ke; k0 += BK) {
+        stash();
+        __syncthreads();
+        if (k0 + BK < ke) fetch(k0 + BK);  // in flight during the MFMAs below
+        const int h = lane >> 5;
+#pragma unroll
+        for (int s = 0; s < BK / 16; s++) {
+            bf16x8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+                const int ar = wm * 64 + i * 32 + (lane & 31), br = wn * 64 + i * 32 + (lane & 31);
+                ah[i] = *reinterpret_cast<const bf16x8*>(&As[0][ar][16 * s + 8 * h]);
+                al[i] = *reinterpret_cast<const bf16x8*>(&As[1][ar][16 * s + 8 * h]);
+                bh[i] = *reinterpret_cast<const bf16x8*>(&Bs[0][br][16 * s + 8 * h]);
+                bl[i] = *reinterpret_cast<const bf16x8*>(&Bs[1][br][16 * s + 8 * h]);
+            }
+#pragma unroll
+            for (int mi = 0; mi < 2; mi++)
+#pragma unroll
+                for (int ni = 0; ni < 2; ni++) {
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[mi], bh[ni], acc[mi][ni], 0, 0, 0);
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[mi], bl[ni], acc[mi][ni], 0, 0, 0);
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[mi], bh[ni], acc[mi][ni], 0, 0, 0);
+                }
+        }
+        __syncthreads();
+    }
+    const bool split = gridDim.z > 1;
+#pragma unroll
+    for (int ni = 0; ni < 2; ni++) {
+        const int gn = n0 + wn * 64 + ni * 32 + (lane & 31);
+        if (gn >= g.N) continue;
+        const float bias = g.bias ? g.bias[gn] : 0.f;
+#pragma unroll
+        for (int mi = 0; mi < 2; mi++) {
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int gm = m0 + wm * 64 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                if (gm >= g.M) continue;
+                float* cp = g.C + (int64_t)gm * g.ldc + gn;
+                if (split) {
+                    atomicAdd(cp, g.alpha * acc[mi][ni][r]);
+                    continue;
+                }
+                float v = g.alpha * acc[mi][ni][r] + bias;
+                if (g.flags & EVX_GEMM_RELU) v = v > 0.f ? v : 0.f;
+                if (g.mask) v = g.mask[(int64_t)gm * g.ldm + gn] ? v * g.mask_scale : 0.f;
+                if (g.gate) v = g.gate[(int64_t)gm * g.ldg + gn] > 0.f ? v : 0.f;
+                if (g.flags & EVX_GEMM_ACCUM) v += *cp;
+                *cp = v;
+            }
+        }
+    }
+}
+
 // zero an f32 matrix C[M][ldc] (split-K target)
 __global__ __launch_bounds__(256) void zero_rows_kernel(float* __restrict__ C, int M, int N, int64_t ldc) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -579,8 +694,9 @@ int evx_gemm(const evx_gemm_desc* g, void* stream) {
     const int tiles = ((g->M + TB - 1) / TB) * ((g->N + TB - 1) / TB);
     const bool epi = g->bias || g->mask || g->gate || (g->flags & EVX_GEMM_RELU);
     int S = 1;
-    // split K only on the bf16 path (f32 atomics reorder the sum; the f32 path stays deterministic)
-    if (!epi && g->precision == EVX_PREC_BF16 && tiles < 256 && g->K >= 512) {
+    // split K only on the bf16 / x3 paths (f32 atomics reorder the sum; the exact-f32 path stays
+    // deterministic)
+    if (!epi && g->precision != EVX_PREC_F32 && tiles < 256 && g->K >= 512) {
         S = (512 + tiles - 1) / tiles;
         if (S > g->K / 256) S = g->K / 256;
         if (S < 1) S = 1;
@@ -595,6 +711,8 @@ int evx_gemm(const evx_gemm_desc* g, void* stream) {
                            (hipStream_t)stream, g->C, g->M, g->N, g->ldc);
     if (g->precision == EVX_PREC_BF16)
         hipLaunchKernelGGL(evxq::gemm128_kernel<__bf16>, grid, dim3(256), 0, (hipStream_t)stream, *g, klen);
+    else if (g->precision == EVX_PREC_X3)
+        hipLaunchKernelGGL(evxq::gemm128x3_kernel, grid, dim3(256), 0, (hipStream_t)stream, *g, klen);
     else
         hipLaunchKernelGGL(evxq::gemm128_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, *g, klen);
     return qlaunch("gemm");

@@ -25,7 +25,7 @@ import torch
 from . import _lib
 from .env import _stream
 
-PREC = {"f32": 0, "bf16": 1}
+PREC = {"f32": 0, "bf16": 1, "x3": 2}
 RELU, ACCUM = 1, 2
 DROPOUT_P = 0.2
 
@@ -324,10 +324,10 @@ class Learner:
         # them in the x3 (f32-accurate) mode, bf16 with bf16 operands. The dense-tensor path
         # (forward / learn on expanded observations) keeps evx_gemm at `precision`.
         self.fast = self.fast_t = None
-        if kind == "mlp" and precision in ("bf16", "f32") and hidden == 512 and actions == 5:
+        if kind == "mlp" and precision in ("bf16", "f32", "x3") and hidden == 512 and actions == 5:
             from .qmlp import MLPFast
-            self.fast = MLPFast(self.online, self.device, x3=precision == "f32")
-            self.fast_t = MLPFast(self.target, self.device, x3=precision == "f32")
+            self.fast = MLPFast(self.online, self.device, x3=precision != "bf16")
+            self.fast_t = MLPFast(self.target, self.device, x3=precision != "bf16")
         self.drop_stream = 0
         # x3 MLP: TD + gradient clear in one launch, the norm partials out of the backward's
         # reductions, clip + Adam + operand repack in one launch (EVX_FUSED_OPT=0: the separate

@@ -167,7 +167,12 @@ class VecTrainer:
             # qmix: the R robots of an env are the agents of runners/train_qmix.py -- joint samples
             # (the same env-steps for every agent), the mixer's loss over the team reward
             self.qmix = GroupedQMix(self.glearner, seed=learner_seed) if nets == "qmix" else None
-        self.learner = Learner(kind=kind, device=self.device, lr=lr, gamma=gamma, precision=precision,
+        # conv + f32: the im2col GEMMs in the f32-accurate x3 mode (bf16 hi/lo operand pairs, as
+        # the fused MLP's f32); EVX_CONV_EXACT=1 keeps the exact-f32 MFMA (the golden-test path)
+        lprec = precision
+        if kind == "conv" and precision == "f32" and os.environ.get("EVX_CONV_EXACT", "0") != "1":
+            lprec = "x3"
+        self.learner = Learner(kind=kind, device=self.device, lr=lr, gamma=gamma, precision=lprec,
                                seed=learner_seed) if not self.per_robot else None
         if self.learner is not None:
             self.learner.grad_hook = grad_hook

@@ -161,6 +161,7 @@ const char *evx_last_error(void);
 
 #define EVX_PREC_F32 0   /* exact f32 MFMA (v_mfma_f32_32x32x2_f32), parity path */
 #define EVX_PREC_BF16 1  /* bf16 inputs, f32 accumulate (v_mfma_f32_32x32x16_bf16) */
+#define EVX_PREC_X3 2    /* f32-accurate: bf16 hi + lo operand pairs, hi*hi + hi*lo + lo*hi on the bf16 MFMA */
 #define EVX_GEMM_RELU 1
 #define EVX_GEMM_ACCUM 2
 
