@@ -237,9 +237,23 @@ __global__ __launch_bounds__(256) void gemm128_kernel(evx_gemm_desc g, int kspli
 
 // gemm128 in the f32-accurate x3 mode (EVX_PREC_X3, as the fused MLP's): every f32 operand is
 // staged in LDS as bf16 hi = bf16(v) and lo = bf16(v - hi), a product as hi*hi + hi*lo + lo*hi
-// on v_mfma_f32_32x32x16_bf16 (relative error ~2^-16 per product, f32 accumulation): 3 bf16
+// on v_mfma_f32_32x32x16_bf16 (relative error ~2^-17 per product, f32 accumulation): 3 bf16
 // MFMAs per 16-deep step instead of 8 f32 32x32x2 ones, and 16-B LDS reads instead of 4-B.
-__global__ __launch_bounds__(256) void gemm128x3_kernel(evx_gemm_desc g, int ksplit_len) {
+//
+// CM selects an implicit-GEMM 3x3 convolution (padding 1, 11x11 maps, pixel-major [B*121][C]
+// activations, agents/dqn_agent.py:22-24,48-50) in place of im2col + GEMM: the operand is
+// gathered from the activations during the tile fetch (cs = the gathered tensor's channels).
+//   CV_FWD: Y = X (*) W. A(m, k) = X[pixel m shifted by tap][c], k = tap*cs + c (one tap
+//           per K-tile when cs >= 32: contiguous channel runs); B(k, n) = W[c*sbk + n*sbn + tap].
+//   CV_DX:  dX = dY (*) flip(W): A(m, k) = dY[pixel m shifted by -tap][o], k = tap*cs + o;
+//           B the same gather of W (c*sbk -> o*9N, n*sbn -> n*9); the ReLU-backward gate
+//           of the layer below rides the epilogue (no col2im / relu_grad pass).
+//   CV_DW:  dW[o][c*9+tap] = sum_m dY[m][o] X[pixel m shifted by tap][c]: B(k = m, n) gathered.
+enum { CV_NONE = 0, CV_FWD = 1, CV_DX = 2, CV_DW = 3 };
+__device__ __forceinline__ uint32_t div121(uint32_t m) { return __umulhi(m, 35495598u); }  // m < 2^26
+__device__ __forceinline__ int div11(int p) { return (p * 187) >> 11; }                     // p < 121
+template <int CM>
+__global__ __launch_bounds__(256) void gemm128x3_kernel(evx_gemm_desc g, int ksplit_len, int cs) {
     constexpr int PK = BK + 8;  // row pitch (bf16): 20 words, conflict-free 16-B reads
     __shared__ __attribute__((aligned(16))) __bf16 As[2][TB][PK];
     __shared__ __attribute__((aligned(16))) __bf16 Bs[2][TB][PK];
@@ -254,24 +268,75 @@ __global__ __launch_bounds__(256) void gemm128x3_kernel(evx_gemm_desc g, int ksp
         for (int j = 0; j < 2; j++)
 #pragma unroll
             for (int r = 0; r < 16; r++) acc[i][j][r] = 0.f;
-    const bool a_kc = g.sak == 1, b_nc = g.sbn == 1;
+    const bool a_kc = CM == CV_FWD || CM == CV_DX || g.sak == 1;
+    const bool b_nc = CM == CV_DW || (CM == CV_NONE && g.sbn == 1);
     float ra[16], rb[16];
+    // CV_FWD / CV_DX: this thread's rows are m0 + (tid >> 5) + 8 i; their pixel index p0 (i = 0)
+    // steps by 8 (mod 121). CV_DW: this thread's column n = n0 + (tid & 127) is fixed.
+    const int pa0 = (int)((uint32_t)(m0 + (tid >> 5)) - div121((uint32_t)(m0 + (tid >> 5))) * 121u);
+    int dw_c = 0, dw_dy = 0, dw_dx = 0;
+    if constexpr (CM == CV_DW) {
+        const int n = n0 + (tid & 127);
+        dw_c = n / 9;
+        const int tap = n - dw_c * 9;
+        dw_dy = tap / 3 - 1;
+        dw_dx = tap - (tap / 3) * 3 - 1;
+    }
     auto fetch = [&](int k0) {
+        if constexpr (CM == CV_FWD || CM == CV_DX) {
+            const int k = k0 + (tid & 31);
+            const int tap = k / cs, c = k - tap * cs;
+            int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
+            if (CM == CV_DX) { dy = -dy; dx = -dx; }
+            const int64_t toff = (int64_t)(dy * 11 + dx) * cs + c;
+            int p = pa0;
 #pragma unroll
-        for (int i = 0; i < 16; i++) {
-            const int idx = tid + 256 * i;
-            int mm, kk;
-            if (a_kc) { mm = idx >> 5; kk = idx & 31; } else { kk = idx >> 7; mm = idx & 127; }
-            const int gm = m0 + mm, gk = k0 + kk;
-            ra[i] = (gm < g.M && gk < ke) ? g.A[(int64_t)gm * g.sam + (int64_t)gk * g.sak] : 0.f;
-        }
+            for (int i = 0; i < 16; i++) {
+                const int gm = m0 + (tid >> 5) + 8 * i;
+                const int y = div11(p), x = p - 11 * y;
+                const bool ok = gm < g.M && k < ke && (unsigned)(y + dy) < 11u && (unsigned)(x + dx) < 11u;
+                ra[i] = ok ? g.A[(int64_t)gm * cs + toff] : 0.f;
+                p += 8;
+                if (p >= 121) p -= 121;
+            }
 #pragma unroll
-        for (int i = 0; i < 16; i++) {
-            const int idx = tid + 256 * i;
-            int nn, kk;
-            if (b_nc) { kk = idx >> 7; nn = idx & 127; } else { nn = idx >> 5; kk = idx & 31; }
-            const int gn = n0 + nn, gk = k0 + kk;
-            rb[i] = (gn < g.N && gk < ke) ? g.B[(int64_t)gk * g.sbk + (int64_t)gn * g.sbn] : 0.f;
+            for (int i = 0; i < 16; i++) {
+                const int gn = n0 + (tid >> 5) + 8 * i;
+                rb[i] = (gn < g.N && k < ke) ? g.B[(int64_t)c * g.sbk + (int64_t)gn * g.sbn + tap] : 0.f;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                const int idx = tid + 256 * i;
+                int mm, kk;
+                if (a_kc) { mm = idx >> 5; kk = idx & 31; } else { kk = idx >> 7; mm = idx & 127; }
+                const int gm = m0 + mm, gk = k0 + kk;
+                ra[i] = (gm < g.M && gk < ke) ? g.A[(int64_t)gm * g.sam + (int64_t)gk * g.sak] : 0.f;
+            }
+            if constexpr (CM == CV_DW) {
+                const int gn = n0 + (tid & 127);
+                const int m1 = k0 + (tid >> 7);
+                int p = (int)((uint32_t)m1 - div121((uint32_t)m1) * 121u);
+                const int64_t toff = (int64_t)(dw_dy * 11 + dw_dx) * cs + dw_c;
+#pragma unroll
+                for (int i = 0; i < 16; i++) {
+                    const int gk = m1 + 2 * i;
+                    const int y = div11(p), x = p - 11 * y;
+                    const bool ok = gn < g.N && gk < ke && (unsigned)(y + dw_dy) < 11u && (unsigned)(x + dw_dx) < 11u;
+                    rb[i] = ok ? g.B[(int64_t)gk * cs + toff] : 0.f;
+                    p += 2;
+                    if (p >= 121) p -= 121;
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < 16; i++) {
+                    const int idx = tid + 256 * i;
+                    int nn, kk;
+                    if (b_nc) { kk = idx >> 7; nn = idx & 127; } else { nn = idx >> 5; kk = idx & 31; }
+                    const int gn = n0 + nn, gk = k0 + kk;
+                    rb[i] = (gn < g.N && gk < ke) ? g.B[(int64_t)gk * g.sbk + (int64_t)gn * g.sbn] : 0.f;
+                }
+            }
         }
     };
     auto stash = [&]() {
@@ -687,7 +752,10 @@ extern "C" {
 
 const char* evx_q_last_error(void) { return q_err; }
 
-int evx_gemm(const evx_gemm_desc* g, void* stream) {
+}  // extern "C"
+
+namespace {
+int gemm_launch(const evx_gemm_desc* g, int cm, int cs, void* stream) {
     if (!g || !g->A || !g->B || !g->C) return qfail(-22, "gemm: NULL operand");
     if (g->M <= 0 || g->N <= 0 || g->K <= 0) return 0;
     const int TB = evxq::TB;
@@ -709,13 +777,38 @@ int evx_gemm(const evx_gemm_desc* g, void* stream) {
     if (S > 1 && !(g->flags & EVX_GEMM_ACCUM))
         hipLaunchKernelGGL(evxq::zero_rows_kernel, dim3(nblk((int64_t)g->M * g->N)), dim3(256), 0,
                            (hipStream_t)stream, g->C, g->M, g->N, g->ldc);
-    if (g->precision == EVX_PREC_BF16)
-        hipLaunchKernelGGL(evxq::gemm128_kernel<__bf16>, grid, dim3(256), 0, (hipStream_t)stream, *g, klen);
+    hipStream_t st = (hipStream_t)stream;
+    if (cm == evxq::CV_FWD)
+        hipLaunchKernelGGL(evxq::gemm128x3_kernel<evxq::CV_FWD>, grid, dim3(256), 0, st, *g, klen, cs);
+    else if (cm == evxq::CV_DX)
+        hipLaunchKernelGGL(evxq::gemm128x3_kernel<evxq::CV_DX>, grid, dim3(256), 0, st, *g, klen, cs);
+    else if (cm == evxq::CV_DW)
+        hipLaunchKernelGGL(evxq::gemm128x3_kernel<evxq::CV_DW>, grid, dim3(256), 0, st, *g, klen, cs);
+    else if (g->precision == EVX_PREC_BF16)
+        hipLaunchKernelGGL(evxq::gemm128_kernel<__bf16>, grid, dim3(256), 0, st, *g, klen);
     else if (g->precision == EVX_PREC_X3)
-        hipLaunchKernelGGL(evxq::gemm128x3_kernel, grid, dim3(256), 0, (hipStream_t)stream, *g, klen);
+        hipLaunchKernelGGL(evxq::gemm128x3_kernel<evxq::CV_NONE>, grid, dim3(256), 0, st, *g, klen, 0);
     else
-        hipLaunchKernelGGL(evxq::gemm128_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, *g, klen);
+        hipLaunchKernelGGL(evxq::gemm128_kernel<float>, grid, dim3(256), 0, st, *g, klen);
     return qlaunch("gemm");
+}
+}  // namespace
+
+extern "C" {
+
+int evx_gemm(const evx_gemm_desc* g, void* stream) { return gemm_launch(g, evxq::CV_NONE, 0, stream); }
+
+int evx_conv3x3_gemm(const evx_gemm_desc* g, int32_t mode, int32_t cs, void* stream) {
+    if (!g) return qfail(-22, "conv3x3: NULL descriptor");
+    if (g->precision != EVX_PREC_X3) return qfail(-22, "conv3x3: implicit-GEMM convolution is x3 only");
+    if (mode < EVX_CONV_FWD || mode > EVX_CONV_DW) return qfail(-22, "conv3x3: bad mode");
+    if (cs <= 0) return qfail(-22, "conv3x3: channels <= 0");
+    const int64_t pix = mode == EVX_CONV_DW ? g->K : g->M;  // rows of the pixel-major activations
+    if (pix % 121 || pix >= (1LL << 26)) return qfail(-22, "conv3x3: pixel count not 121*B (< 2^26)");
+    if ((mode == EVX_CONV_DW ? g->N : g->K) != 9 * cs) return qfail(-22, "conv3x3: 3x3 taps x channels mismatch");
+    if (mode == EVX_CONV_DW && (g->sam != 1 || g->sak != g->M))
+        return qfail(-22, "conv3x3 dW: A must be dY [pixels][M]");
+    return gemm_launch(g, mode, cs, stream);
 }
 
 int evx_colsum(const float* X, int64_t ld, int32_t M, int32_t N, float* out, int32_t accum, float* scratch,

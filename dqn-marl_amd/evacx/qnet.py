@@ -77,6 +77,7 @@ def qlib():
         L.evx_col2im3x3.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]
         L.evx_pix_nchw.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]
         L.evx_relu_grad.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]
+        L.evx_conv3x3_gemm.argtypes = [C.POINTER(evx_gemm_desc), C.c_int32, C.c_int32, C.c_void_p]
         _q_inited = True
     return L
 
@@ -96,6 +97,18 @@ def gemm(M, N, K, A, sam, sak, B, sbk, sbn, Cm, ldc, precision="f32", bias=None,
                       alpha=alpha, A=_p(A), sam=sam, sak=sak, B=_p(B), sbk=sbk, sbn=sbn, C=_p(Cm), ldc=ldc,
                       bias=_p(bias), mask=_p(mask), ldm=ldm, mask_scale=mask_scale, gate=_p(gate), ldg=ldg)
     qcheck(qlib().evx_gemm(C.byref(d), _stream()), "evx_gemm")
+
+
+CONV_FWD, CONV_DX, CONV_DW = 1, 2, 3
+
+
+def conv_gemm(mode, M, N, K, A, B, Cm, cs, sam=0, sak=0, sbk=0, sbn=0, bias=None, relu=False, gate=None,
+              ldg=0):
+    """evx_conv3x3_gemm (x3): implicit-GEMM 3x3 conv forward / dX / dW on pixel-major activations."""
+    d = evx_gemm_desc(M=M, N=N, K=K, precision=PREC["x3"], flags=RELU if relu else 0, alpha=1.0, A=_p(A),
+                      sam=sam, sak=sak, B=_p(B), sbk=sbk, sbn=sbn, C=_p(Cm), ldc=N, bias=_p(bias), mask=None,
+                      ldm=0, mask_scale=1.0, gate=_p(gate), ldg=ldg)
+    qcheck(qlib().evx_conv3x3_gemm(C.byref(d), mode, cs, _stream()), "evx_conv3x3_gemm")
 
 
 def colsum(X, M, N, out, scratch):
@@ -200,6 +213,8 @@ class QNet:
     def __init__(self, kind: str, params: FlatParams, precision="f32", hidden=512, actions=5):
         self.kind, self.P, self.prec = kind, params, precision
         self.hidden, self.actions = hidden, actions
+        # x3 conv layers as implicit GEMMs (EVX_CONV_IM2COL=1: im2col + GEMM, for A/B checks)
+        self.implicit = kind == "conv" and precision == "x3" and os.environ.get("EVX_CONV_IM2COL", "0") != "1"
         self.device = params.flat.device
         self.ws = _Workspace()
         self.saved = None
@@ -232,6 +247,14 @@ class QNet:
         cur, C_in = x, 6
         for li, (cname, cout) in enumerate([("conv1", 32), ("conv2", 64), ("conv3", 128)]):
             K9 = C_in * 9
+            if self.implicit:  # x3: the taps gathered in the GEMM's tile fetch (no im2col buffer)
+                Y = ws.get(tag + f"y{li}", (Mp, cout), torch.float32, dev)
+                conv_gemm(CONV_FWD, Mp, cout, K9, cur, P[cname + ".weight"], Y, C_in, sbk=9, sbn=K9,
+                          bias=P[cname + ".bias"], relu=True)
+                cols.append(cur)  # the layer input, gathered again by the dW GEMM
+                ys.append(Y)
+                cur, C_in = Y, cout
+                continue
             col = ws.get(tag + f"col{li}", (Mp, K9), torch.float32, dev)
             qcheck(L.evx_im2col3x3(_p(cur), B, C_in, 1, _p(col), _stream()), "im2col")
             Y = ws.get(tag + f"y{li}", (Mp, cout), torch.float32, dev)
@@ -281,6 +304,16 @@ class QNet:
         for li, (cname, cin, cout) in reversed(list(enumerate([("conv1", 6, 32), ("conv2", 32, 64),
                                                                 ("conv3", 64, 128)]))):
             K9 = cin * 9
+            if self.implicit:  # cols[li] is the layer input [Mp][cin]
+                conv_gemm(CONV_DW, cout, K9, Mp, dY, cols[li], grads[cname + ".weight"], cin, sam=1, sak=cout)
+                colsum(dY, Mp, cout, grads[cname + ".bias"], scratch)
+                if li == 0:
+                    break
+                dYp = ws.get(f"dyp{li}", (Mp, cin), torch.float32, dev)
+                conv_gemm(CONV_DX, Mp, cin, cout * 9, dY, P[cname + ".weight"], dYp, cout, sbk=K9, sbn=9,
+                          gate=ys[li - 1], ldg=cin)
+                dY = dYp
+                continue
             gemm(cout, K9, Mp, dY, 1, cout, cols[li], K9, 1, grads[cname + ".weight"], K9, pr)
             colsum(dY, Mp, cout, grads[cname + ".bias"], scratch)
             if li == 0:

@@ -197,6 +197,21 @@ typedef struct {
 } evx_replay;
 
 int evx_gemm(const evx_gemm_desc *g, void *stream);
+/* Implicit-GEMM 3x3 convolution, padding 1, on 11x11 maps (DQNNetwork conv1-3,
+ * agents/dqn_agent.py:22-24,48-50, in place of im2col + evx_gemm; x3 precision only). The
+ * activations are pixel-major [B*121][cs]; the operand they feed is gathered in the tile fetch:
+ *   EVX_CONV_FWD: C[m][n] = sum_{tap,c} A[m shifted by tap][c] W[n][c][tap]; M = B*121, K = 9 cs,
+ *                 B = W with sbk = 9 (c stride), sbn = 9 cs (n stride). Epilogue as evx_gemm.
+ *   EVX_CONV_DX:  C[m][n] = sum_{tap,o} A[m shifted by -tap][o] W[o][n][tap] (dX of the layer,
+ *                 A = dY [B*121][cs]); K = 9 cs, B = W with sbk = 9 N, sbn = 9; gate = the
+ *                 layer input (ReLU backward of the layer below).
+ *   EVX_CONV_DW:  C[o][c*9+tap] = sum_m A[m][o] B[m shifted by tap][c] (dW, A = dY with sam = 1,
+ *                 sak = M; B = the layer input [B*121][cs]); N = 9 cs, K = B*121.
+ * Out-of-map taps read 0. */
+#define EVX_CONV_FWD 1
+#define EVX_CONV_DX 2
+#define EVX_CONV_DW 3
+int evx_conv3x3_gemm(const evx_gemm_desc *g, int32_t mode, int32_t cs, void *stream);
 /* out[n] (+)= sum_m X[m*ld+n] (bias gradients), fixed summation order */
 int evx_colsum(const float *X, int64_t ld, int32_t M, int32_t N, float *out, int32_t accum, float *scratch,
                int32_t scratch_elems, void *stream);

@@ -120,7 +120,9 @@ def test_learn_steps_match_torch_adam(kind, prec):
             bar = 2e-3 if prec == "x3" else 1e-4
             if k.split(".")[0] not in flipped:
                 assert (diff > 1e-5).float().mean().item() <= bar, (k, diff.max().item())
-            assert diff.max().item() <= 1e-3, (k, diff.max().item())
+            # one Adam step moves an element by at most lr (1-b1)/sqrt(1-b2) ~ 3.2 lr: below a relu
+            # flip a near-zero gradient may change sign, so there the bar is two such steps
+            assert diff.max().item() <= (6.4e-3 if k.split(".")[0] in flipped else 1e-3), (k, diff.max().item())
 
 
 def _relu_flips(lr, params, x):
@@ -163,3 +165,36 @@ def test_dropout_mask_rate():
     m = torch.zeros(1 << 20, dtype=torch.uint8, device="cuda")
     qnet.qcheck(qnet.qlib().evx_dropout_mask(m.data_ptr(), m.numel(), 0.2, 11, 0, qnet._stream()), "mask")
     assert abs(m.float().mean().item() - 0.8) < 0.003
+
+
+@pytest.mark.parametrize("cin,cout,B", [(6, 32, 5), (32, 64, 3), (64, 128, 2), (5, 7, 4)])
+def test_conv3x3_implicit_gemm_vs_torch(cin, cout, B):
+    """evx_conv3x3_gemm forward / dX (with the ReLU gate of the layer below) / dW against torch's
+    conv2d and autograd in float64 (the same 3x3 padding-1 conv as DQNNetwork's, dqn_agent.py:22-24).
+    x3 precision: error ~2^-17 of the sum of |products| -> atol scales with the tensor."""
+    _need_gpu()
+    from evacx import qnet
+    g = torch.Generator().manual_seed(cin * 100 + cout)
+    x = torch.randn(B, 11, 11, cin, generator=g)           # pixel-major = NHWC
+    w = torch.randn(cout, cin, 3, 3, generator=g) * 0.2
+    bias = torch.randn(cout, generator=g) * 0.1
+    dy = torch.randn(B, 11, 11, cout, generator=g)
+    below = torch.randn(B, 11, 11, cin, generator=g)        # the layer below's relu output (gate)
+    Mp, K9 = B * 121, cin * 9
+    xd, wd, bd, dyd, gd = (t.cuda().contiguous() for t in (x, w, bias, dy, below))
+    y = torch.zeros(Mp, cout, device="cuda")
+    qnet.conv_gemm(qnet.CONV_FWD, Mp, cout, K9, xd, wd, y, cin, sbk=9, sbn=K9, bias=bd, relu=True)
+    dx = torch.zeros(Mp, cin, device="cuda")
+    qnet.conv_gemm(qnet.CONV_DX, Mp, cin, cout * 9, dyd, wd, dx, cout, sbk=K9, sbn=9, gate=gd, ldg=cin)
+    dw = torch.full((cout, K9), 7.0, device="cuda")        # overwritten (split-K zeroes it first)
+    qnet.conv_gemm(qnet.CONV_DW, cout, K9, Mp, dyd, xd, dw, cin, sam=1, sak=cout)
+    xr = x.double().permute(0, 3, 1, 2).requires_grad_(True)
+    wr = w.double().requires_grad_(True)
+    z = F.conv2d(xr, wr, bias.double(), padding=1)
+    yref = F.relu(z).permute(0, 2, 3, 1).reshape(Mp, cout)
+    z.backward(dy.double().permute(0, 3, 1, 2))
+    dxref = (xr.grad.permute(0, 2, 3, 1) * (below.double() > 0)).reshape(Mp, cin)
+    dwref = wr.grad.reshape(cout, K9)
+    for got, ref in ((y, yref), (dx, dxref), (dw, dwref)):
+        ref = ref.detach().float()
+        torch.testing.assert_close(got.cpu(), ref, rtol=1e-4, atol=2e-5 * ref.abs().max().item())
