@@ -625,7 +625,13 @@ struct WaveLds {  // word offsets into dynamic LDS
     int pyring, npring, aux, rmapb, tbits, cbits, vac, nearc, lost, robots, misc, total;
 };
 
-__host__ __device__ inline WaveLds wave_lds(int L, int W, int P, int R) {
+// Big grids (bitmaps of more than WR words: beyond ~181x181 cells, e.g. cfg4's 256x256): the
+// target / contested / vacated bitmaps live in the env's global step scratch (L2) instead of LDS,
+// which leaves the occupancy map as the only grid-sized LDS table (44 -> 21 KB per env at 256x256:
+// 3 -> 7 envs per CU).
+__host__ __device__ inline bool big_grid(int L, int W) { return ((L + 2) * (W + 2) + 31) / 32 > WR; }
+
+__host__ __device__ inline WaveLds wave_lds(int L, int W, int P, int R, bool bigg = false) {
     WaveLds s;
     const int G = (L + 2) * (W + 2);
     const int RW = (G + 31) / 32;
@@ -635,12 +641,16 @@ __host__ __device__ inline WaveLds wave_lds(int L, int W, int P, int R) {
     s.npring = o; o += MT_N;               // the numpy ring (np_ensure); after the rows: contested list
     s.aux = o; o += 512 + 16;              // planner queue + health group; events; leaf table
     s.rmapb = o; o += RW;
-    s.tbits = o; o += RW;
-    s.cbits = o; o += RW;
-    if (RW <= WR) {
-        s.vac = s.pyring;
+    if (bigg) {
+        s.tbits = s.cbits = s.vac = -1;  // global scratch (env_scratch_words)
     } else {
-        s.vac = o; o += RW;
+        s.tbits = o; o += RW;
+        s.cbits = o; o += RW;
+        if (RW <= WR) {
+            s.vac = s.pyring;
+        } else {
+            s.vac = o; o += RW;
+        }
     }
     s.nearc = o; o += NCW;
     s.lost = o; o += (P + 31) / 32;
@@ -660,6 +670,11 @@ __host__ __device__ inline int64_t wave_hv_offset(int P) {
 }
 // ... | health of every not-dead person after update_health, list order (wide rows)
 __host__ __device__ inline int64_t wave_scratch_words(int P) { return wave_hv_offset(P) + 2 * (int64_t)P; }
+// ... | big grids: target, contested and vacated bitmaps [3][RW] (the per-env stride)
+__host__ __device__ inline int64_t env_scratch_words(const evx_layout& l) {
+    const int RW = ((l.L + 2) * (l.W + 2) + 31) / 32;
+    return wave_scratch_words(l.P) + (big_grid(l.L, l.W) ? 3 * (int64_t)RW : 0);
+}
 
 __device__ __forceinline__ int pb_bits(int P) { return P > 1 ? bit_length((uint32_t)(P - 1)) : 1; }
 
@@ -724,9 +739,9 @@ __host__ __device__ inline ResetLds reset_lds(int G, int P) {
 }
 
 // dynamic LDS words of one env's wave: the step's layout, which also hosts a fused reset
-__host__ __device__ inline int step_lds_words(const evx_layout& l) {
+__host__ __device__ inline int step_lds_words(const evx_layout& l, bool bigg = false) {
     const int G = (l.L + 2) * (l.W + 2);
-    const int a = wave_lds(l.L, l.W, l.P, l.R).total, b = reset_lds(G, l.P).total;
+    const int a = wave_lds(l.L, l.W, l.P, l.R, bigg).total, b = reset_lds(G, l.P).total;
     return ((a > b ? a : b) + 3) & ~3;
 }
 
@@ -911,7 +926,7 @@ __device__ __forceinline__ void rows_wide(const evx_layout& lay, const evx_state
     uint32_t* pk_g = st.pk + (size_t)e * P;
     double* h_g = st.health + (size_t)e * P;
     double* a_g = st.acc + (size_t)e * P;
-    uint32_t* scr = st.scratch + (size_t)e * wave_scratch_words(P);
+    uint32_t* scr = st.scratch + (size_t)e * env_scratch_words(lay);
     uint2* plan = reinterpret_cast<uint2*>(scr);
     const uint2* ndl = reinterpret_cast<const uint2*>(scr + 2 * P);
     double* hv = reinterpret_cast<double*>(scr + wave_hv_offset(P));
@@ -1213,7 +1228,7 @@ __device__ __forceinline__ void wide_health_sum(const evx_layout& lay, const evx
     const int P = lay.P;
     WideCtl* ctl = reinterpret_cast<WideCtl*>(smem + wide_lds(lay).ctl);
     const int nnd = ctl->nnd;
-    const double* hv = reinterpret_cast<const double*>(st.scratch + (size_t)e * wave_scratch_words(P) + wave_hv_offset(P));
+    const double* hv = reinterpret_cast<const double*>(st.scratch + (size_t)e * env_scratch_words(lay) + wave_hv_offset(P));
     double total = 0.0;
     double cur = lane < nnd ? hv[lane] : 0.0;
     for (int i0 = 0; i0 < nnd; i0 += 64) {
@@ -1230,7 +1245,7 @@ __device__ __forceinline__ void wide_health_sum(const evx_layout& lay, const evx
 
 // One env-step of env e by the calling wave (smem: its wave_lds region).
 // WIDE: wave 0 of a heavy env's workgroup; the rows phase runs on all its waves.
-template <bool WIDE>
+template <bool WIDE, bool BIGG = false>
 __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state& st, const int32_t* __restrict__ actions,
                                          const evx_step_out& out, const int e, uint32_t* smem) {
     const int lane = (int)(threadIdx.x & 63);
@@ -1242,14 +1257,29 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     const int P = g.P, R = g.R, GY = g.GY;
     const int NR = (P + 63) >> 6;
     const int pb = pb_bits(P);
-    const WaveLds S = wave_lds(g.L, g.W, P, R);
+    const WaveLds S = wave_lds(g.L, g.W, P, R, BIGG);
     uint32_t* pyring = smem + S.pyring;
     uint32_t* npring = smem + S.npring;
     uint32_t* aux = smem + S.aux;
     uint32_t* rmapb = smem + S.rmapb;
-    uint32_t* tbits = smem + S.tbits;
-    uint32_t* cbits = smem + S.cbits;
-    uint32_t* vac = smem + S.vac;
+    const int64_t SW = env_scratch_words(lay);
+    uint32_t* scr = st.scratch + (size_t)e * SW;
+    uint32_t *tbits, *cbits, *vac;
+    if constexpr (BIGG) {  // global (L2): read with agent-scope atomic loads, past the L1
+        tbits = scr + wave_scratch_words(P);
+        cbits = tbits + g.RW;
+        vac = cbits + g.RW;
+    } else {
+        tbits = smem + S.tbits;
+        cbits = smem + S.cbits;
+        vac = smem + S.vac;
+    }
+    auto tc_get = [&](const uint32_t* b, int i) -> bool {
+        if constexpr (BIGG)
+            return (__hip_atomic_load(b + (i >> 5), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (i & 31)) & 1u;
+        else
+            return bit_get(b, i);
+    };
     uint32_t* nearc = smem + S.nearc;
     const int NCW = (((g.L + 2 + 3) >> 2) * ((GY + 3) >> 2) + 31) / 32;
     uint32_t* lost = smem + S.lost;
@@ -1260,8 +1290,6 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     uint32_t* pk_g = st.pk + (size_t)e * P;
     double* h_g = st.health + (size_t)e * P;
     double* a_g = st.acc + (size_t)e * P;
-    const int64_t SW = wave_scratch_words(P);
-    uint32_t* scr = st.scratch + (size_t)e * SW;
     uint2* plan = reinterpret_cast<uint2*>(scr);           // (person, cell | dir << 24) of every mover
     uint2* ndl = reinterpret_cast<uint2*>(scr + 2 * P);    // (person, person word) of the not-dead
     // light path: the persons in play (not safe, not dead) as (person | not-dead index << 16, word)
@@ -1812,7 +1840,7 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
             uint32_t key = 0;
             if (ok) {
                 const int t = (int)(en.y & 0xffffffu) + doff_of(en.y >> 24, GY);
-                c = bit_get(cbits, t);
+                c = tc_get(cbits, t);
                 key = ((uint32_t)t << pb) | en.x;
             }
             const unsigned long long m = __ballot(c);
@@ -1832,7 +1860,7 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
                 uint32_t key = 0;
                 if (ok) {
                     const int t = (int)(en.y & 0xffffffu) + doff_of(en.y >> 24, GY);
-                    c = bit_get(cbits, t);
+                    c = tc_get(cbits, t);
                     key = ((uint32_t)t << pb) | en.x;
                 }
                 const unsigned long long m = __ballot(c);
@@ -1870,7 +1898,7 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
         if (ok) {
             const int cold = (int)(en.y & 0xffffffu);
             const int t = cold + doff_of(en.y >> 24, GY);
-            const bool win = !bit_get(cbits, t) || !bit_get(lost, (int)en.x);
+            const bool win = !tc_get(cbits, t) || !bit_get(lost, (int)en.x);
             if (win) atomicOr(&vac[cold >> 5], 1u << (cold & 31));
             if (st.thmap) atomicAdd(&st.thmap[(size_t)e * g.G + (win ? t : cold)], 1);
         }
@@ -1902,11 +1930,11 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
             const int cold = (int)(en.y & 0xffffffu);
             const int dd = (int)(en.y >> 24);
             const int t = cold + doff_of((uint32_t)dd, GY);
-            const bool cont = bit_get(cbits, t);
+            const bool cont = tc_get(cbits, t);
             if (!cont || !bit_get(lost, p)) {
                 const bool ex = (ci4[j] >> 1) & 1u;
                 exw = ex;
-                const bool ev_old = bit_get(tbits, cold), ev_new = bit_get(vac, t);
+                const bool ev_old = tc_get(tbits, cold), ev_new = tc_get(vac, t);
                 int pf = p;
                 if ((ev_old || ev_new) && cont) pf = find_pf(Lp, ncont, t, pb);
                 if (ev_old) {
@@ -2407,22 +2435,25 @@ __global__ __launch_bounds__(64) void env_reset_kernel(evx_layout lay, evx_state
 #ifndef EVX_ENV_MINW
 #define EVX_ENV_MINW 3
 #endif
-template <int NWB, bool MULTI>
+// BIGG: big_grid layouts (target / contested / vacated bitmaps in global scratch, no heavy
+// workgroups).
+template <int NWB, bool MULTI, bool BIGG = false>
 __global__ __launch_bounds__(64 * NWB, EVX_ENV_MINW) void env_step_kernel(evx_layout lay, evx_state st,
                                                             const int32_t* __restrict__ actions, evx_step_out out,
                                                             int hcap, int pslots, int part) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const int w = (int)(threadIdx.x >> 6);
-    const int words = step_lds_words(lay);
+    const int words = step_lds_words(lay, BIGG);
     const int H = (NWB == WNW && st.order && hcap > 0) ? min(hcap, st.order[st.E]) : 0;
     // light envs order[H, E): the last nt of them go to the heavy workgroups' spare waves
     // (only when one launch steps them all: part 0). Each step_env variant has ONE call site:
     // every inlined copy of its body costs instruction-cache space.
     const int nt = part == 0 ? min((NWB - 1) * H, st.E - H) : 0;
-    const bool heavy = part != 2 && (int)blockIdx.x < H;
+    const bool heavy = !BIGG && part != 2 && (int)blockIdx.x < H;
     if (part == 1 && !heavy) return;  // heavy envs only
     int slot = -1;                    // this wave's light env slot in the order
-    if (heavy) {
+    if constexpr (BIGG) {
+    } else if (heavy) {
         const int e = st.order[blockIdx.x];
         if (pslots > 0) __builtin_amdgcn_s_setprio(2);
         if (w == 0) {
@@ -2435,7 +2466,8 @@ __global__ __launch_bounds__(64 * NWB, EVX_ENV_MINW) void env_step_kernel(evx_la
             if (t < nt) slot = st.E - nt + t;
         }
         if (pslots > 0) __builtin_amdgcn_s_setprio(0);
-    } else {
+    }
+    if (!heavy) {
         slot = part == 2 ? H + (int)blockIdx.x * NWB + w : H + ((int)blockIdx.x - H) * NWB + w;
         if (slot >= (part == 2 ? st.E : st.E - nt)) {
             slot = -1;
@@ -2446,7 +2478,7 @@ __global__ __launch_bounds__(64 * NWB, EVX_ENV_MINW) void env_step_kernel(evx_la
     }
     if (slot < 0) return;
     const int e = st.order ? st.order[slot] : slot;
-    step_env<false>(lay_of<MULTI>(lay, st, e), st, actions, out, e, smem + (size_t)w * words);
+    step_env<false, BIGG>(lay_of<MULTI>(lay, st, e), st, actions, out, e, smem + (size_t)w * words);
 }
 
 // ------------------------------------------------------- dispatch order
@@ -2604,10 +2636,12 @@ __global__ __launch_bounds__(256) void obs_expand_kernel(evx_layout lay0, const 
 
 // ===================================================================== C-ABI
 // the step kernel's dynamic LDS also hosts a fused auto-reset
-static size_t step_lds_bytes(const evx_layout& l) { return (size_t)evx::step_lds_words(l) * 4; }
+static size_t step_lds_bytes(const evx_layout& l, bool bigg = false) {
+    return (size_t)evx::step_lds_words(l, bigg) * 4;
+}
 // dynamic LDS of a step workgroup of nwb waves: nwb envs, or (nwb == 4) one heavy env
-static size_t step_launch_lds(const evx_layout& l, int nwb) {
-    if (nwb != evx::WNW) return step_lds_bytes(l) * nwb;
+static size_t step_launch_lds(const evx_layout& l, int nwb, bool bigg = false) {
+    if (bigg || nwb != evx::WNW) return step_lds_bytes(l, bigg) * nwb;
     return (size_t)evx::wide_lds(l).total * 4;  // WNW env regions + WideCtl
 }
 // Heavy envs per step (rows_wide workgroups): at most the cap, each with >= *hmin
@@ -2625,6 +2659,7 @@ static int heavy_cap(const evx_layout& l, int* hmin) {
         min_env = m ? atoi(m) : -1;
     }
     *hmin = std::max(1, min_env >= 0 ? min_env : l.P / 4);
+    if (evx::big_grid(l.L, l.W)) return 0;  // BIGG kernels: no heavy workgroups
     const evx::WideLds wl = evx::wide_lds(l);
     if (step_launch_lds(l, evx::WNW) > 160 * 1024 || wl.end > wl.ctl) return 0;
     return cap_env >= 0 ? cap_env : 176;
@@ -2656,13 +2691,12 @@ const char* evx_last_error(void) { return g_err; }
 
 int64_t evx_step_lds_bytes(const evx_layout* l) {
     if (check_layout(l)) return -1;
-    const int G = (l->L + 2) * (l->W + 2);
-    return (int64_t)step_lds_bytes(*l);
+    return (int64_t)step_lds_bytes(*l, evx::big_grid(l->L, l->W));
 }
 
 int64_t evx_step_scratch_words(const evx_layout* l) {
     if (check_layout(l)) return -1;
-    return evx::wave_scratch_words(l->P);
+    return evx::env_scratch_words(*l);
 }
 
 int evx_env_step(const evx_layout* l, const evx_state* s, const int32_t* actions, const evx_step_out* o, void* stream) {
@@ -2685,14 +2719,19 @@ int evx_env_step_part(const evx_layout* l, const evx_state* s, const int32_t* ac
         while ((1LL << gb) < (long long)G) gb++;
         if (pb + gb > 32) return fail(-22, "grid cells x people too large for 32-bit move keys");
     }
-    const size_t lds = step_lds_bytes(*l);
+    const bool bigg = evx::big_grid(l->L, l->W);
+    const size_t lds = step_lds_bytes(*l, bigg);
     if (lds > 160 * 1024) return fail(-7, "layout needs more than 160 KiB of LDS");
     const bool multi = l->layout_set && s->layout_idx;
     static bool attr_set = false;
     if (!attr_set) {
-        const void* ks[6] = {(const void*)evx::env_step_kernel<1, false>, (const void*)evx::env_step_kernel<2, false>,
-                             (const void*)evx::env_step_kernel<4, false>, (const void*)evx::env_step_kernel<1, true>,
-                             (const void*)evx::env_step_kernel<2, true>, (const void*)evx::env_step_kernel<4, true>};
+        const void* ks[10] = {(const void*)evx::env_step_kernel<1, false>, (const void*)evx::env_step_kernel<2, false>,
+                              (const void*)evx::env_step_kernel<4, false>, (const void*)evx::env_step_kernel<1, true>,
+                              (const void*)evx::env_step_kernel<2, true>, (const void*)evx::env_step_kernel<4, true>,
+                              (const void*)evx::env_step_kernel<1, false, true>,
+                              (const void*)evx::env_step_kernel<2, false, true>,
+                              (const void*)evx::env_step_kernel<1, true, true>,
+                              (const void*)evx::env_step_kernel<2, true, true>};
         for (const void* k : ks) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_set = true;
     }
@@ -2714,7 +2753,8 @@ int evx_env_step_part(const evx_layout* l, const evx_state* s, const int32_t* ac
             ncu = 256;
     }
     int nwb = nwb_env == 1 || nwb_env == 2 || nwb_env == 4 ? nwb_env : (s->E >= 32 * ncu ? 1 : 4);
-    while (nwb > 1 && step_launch_lds(*l, nwb) > 160 * 1024) nwb >>= 1;
+    if (bigg && nwb > 2) nwb = 2;  // BIGG kernels: 1 or 2 envs per workgroup
+    while (nwb > 1 && step_launch_lds(*l, nwb, bigg) > 160 * 1024) nwb >>= 1;
     int hmin = 0;
     const int hcap = (nwb == evx::WNW && s->order) ? heavy_cap(*l, &hmin) : 0;
     // EVX_PRIO_SLOTS: single-wave envs at order slots < H + this run at raised priority
@@ -2725,12 +2765,25 @@ int evx_env_step_part(const evx_layout* l, const evx_state* s, const int32_t* ac
         pslots_env = v ? atoi(v) : -1;
     }
     const int pslots = s->order ? (pslots_env >= 0 ? pslots_env : 0) : 0;
-    const size_t blds = step_launch_lds(*l, nwb);
+    const size_t blds = step_launch_lds(*l, nwb, bigg);
     // heavy envs take a workgroup each; part 1: only those, part 2: only the rest
     if (part == 1 && hcap == 0) return 0;  // no heavy workgroups for this layout: part 2 steps every env
     const int nblk = part == 1 ? hcap : (s->E + nwb - 1) / nwb + (part == 0 ? hcap : 0);
     hipStream_t hs = (hipStream_t)stream;
-    if (nwb == 4 && multi)
+    if (bigg) {
+        if (nwb == 2 && multi)
+            hipLaunchKernelGGL((evx::env_step_kernel<2, true, true>), dim3(nblk), dim3(128), blds, hs, *l, *s, actions,
+                               *o, 0, 0, (int)part);
+        else if (nwb == 2)
+            hipLaunchKernelGGL((evx::env_step_kernel<2, false, true>), dim3(nblk), dim3(128), blds, hs, *l, *s, actions,
+                               *o, 0, 0, (int)part);
+        else if (multi)
+            hipLaunchKernelGGL((evx::env_step_kernel<1, true, true>), dim3(nblk), dim3(64), blds, hs, *l, *s, actions,
+                               *o, 0, 0, (int)part);
+        else
+            hipLaunchKernelGGL((evx::env_step_kernel<1, false, true>), dim3(nblk), dim3(64), blds, hs, *l, *s, actions,
+                               *o, 0, 0, (int)part);
+    } else if (nwb == 4 && multi)
         hipLaunchKernelGGL((evx::env_step_kernel<4, true>), dim3(nblk), dim3(256), blds, hs, *l, *s, actions, *o, hcap,
                            pslots, (int)part);
     else if (nwb == 4)
