@@ -629,7 +629,10 @@ struct WaveLds {  // word offsets into dynamic LDS
 // target / contested / vacated bitmaps live in the env's global step scratch (L2) instead of LDS,
 // which leaves the occupancy map as the only grid-sized LDS table (44 -> 21 KB per env at 256x256:
 // 3 -> 7 envs per CU).
-__host__ __device__ inline bool big_grid(int L, int W) { return ((L + 2) * (W + 2) + 31) / 32 > WR; }
+#ifndef EVX_BIGG_RW
+#define EVX_BIGG_RW WR  // experiment builds: -DEVX_BIGG_RW=0 puts every grid's bitmaps in global scratch
+#endif
+__host__ __device__ inline bool big_grid(int L, int W) { return ((L + 2) * (W + 2) + 31) / 32 > EVX_BIGG_RW; }
 
 __host__ __device__ inline WaveLds wave_lds(int L, int W, int P, int R, bool bigg = false) {
     WaveLds s;
