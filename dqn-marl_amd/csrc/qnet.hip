@@ -124,7 +124,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(evx_gemm_desc g) {
 // accumulators per lane). The next K-tile is fetched into registers while the current
 // one is multiplied (register double buffering, one barrier pair per K-step). gridDim.z
 // splits K: partial sums are atomically added into a zeroed C (used for dW = dY^T X,
-// whose M x N grid alone cannot fill 256 CUs); epilogue ops require gridDim.z == 1.
+// whose M x N grid alone cannot fill 256 CUs); with epilogue ops the slices sum raw products
+// and gemm_epilogue_kernel applies them afterwards.
 constexpr int TB = 128;
 template <typename TIn>
 __global__ __launch_bounds__(256) void gemm128_kernel(evx_gemm_desc g, int ksplit_len) {
@@ -415,6 +416,21 @@ __global__ __launch_bounds__(256) void gemm128x3_kernel(evx_gemm_desc g, int ksp
     }
 }
 
+// Epilogue of a split-K GEMM whose partials were atomically summed into a zeroed C (C holds
+// alpha * A B): bias, ReLU, dropout mask, gate -- the same sequence as the one-pass epilogue.
+__global__ __launch_bounds__(256) void gemm_epilogue_kernel(evx_gemm_desc g) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)g.M * g.N) return;
+    const int64_t gm = i / g.N;
+    const int gn = (int)(i - gm * g.N);
+    float* cp = g.C + gm * g.ldc + gn;
+    float v = *cp + (g.bias ? g.bias[gn] : 0.f);
+    if (g.flags & EVX_GEMM_RELU) v = v > 0.f ? v : 0.f;
+    if (g.mask) v = g.mask[gm * g.ldm + gn] ? v * g.mask_scale : 0.f;
+    if (g.gate) v = g.gate[gm * g.ldg + gn] > 0.f ? v : 0.f;
+    *cp = v;
+}
+
 // zero an f32 matrix C[M][ldc] (split-K target)
 __global__ __launch_bounds__(256) void zero_rows_kernel(float* __restrict__ C, int M, int N, int64_t ldc) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -425,11 +441,16 @@ __global__ __launch_bounds__(256) void zero_rows_kernel(float* __restrict__ C, i
 
 // ------------------------------------------------------------- column sums
 // out[n] (+)= sum_m X[m*ld + n], deterministic: fixed-order partials then a fixed-order total.
+// Partials: COLSUM_ROWS rows per chunk; a block covers 64 columns x 4 chunks (the 4 waves), so a
+// narrow matrix (a conv layer's 32 channels) still fills its lanes. The total: one block per
+// column, strided partial sums then a fixed LDS tree (was one thread per column walking every
+// chunk: ~110 us for the 968 chunks of a 123 904-pixel conv layer).
+constexpr int COLSUM_ROWS = 64;
 __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ X, int64_t ld, int M, int N,
                                                      float* __restrict__ part, int chunks) {
-    const int n = blockIdx.x * 256 + threadIdx.x;
-    const int c = blockIdx.y;
-    if (n >= N) return;
+    const int n = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int c = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (n >= N || c >= chunks) return;
     const int rows = (M + chunks - 1) / chunks;
     const int r0 = c * rows, r1 = min(M, r0 + rows);
     float s = 0.f;
@@ -438,11 +459,17 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ X
 }
 __global__ __launch_bounds__(256) void colsum_finish(const float* __restrict__ part, int N, int chunks,
                                                      float* __restrict__ out, int accum) {
-    const int n = blockIdx.x * 256 + threadIdx.x;
-    if (n >= N) return;
+    __shared__ float red[256];
+    const int n = blockIdx.x, t = threadIdx.x;
     float s = 0.f;
-    for (int c = 0; c < chunks; c++) s += part[(int64_t)c * N + n];
-    out[n] = accum ? out[n] + s : s;
+    for (int c = t; c < chunks; c += 256) s += part[(int64_t)c * N + n];
+    red[t] = s;
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+        if (t < h) red[t] += red[t + h];
+        __syncthreads();
+    }
+    if (t == 0) out[n] = accum ? out[n] + red[0] : red[0];
 }
 
 // --------------------------------------------------------------- TD loss
@@ -756,6 +783,7 @@ const char* evx_q_last_error(void) { return q_err; }
 
 namespace {
 int gemm_launch(const evx_gemm_desc* g, int cm, int cs, void* stream) {
+    const evx_gemm_desc* orig = g;
     if (!g || !g->A || !g->B || !g->C) return qfail(-22, "gemm: NULL operand");
     if (g->M <= 0 || g->N <= 0 || g->K <= 0) return 0;
     const int TB = evxq::TB;
@@ -763,10 +791,15 @@ int gemm_launch(const evx_gemm_desc* g, int cm, int cs, void* stream) {
     const bool epi = g->bias || g->mask || g->gate || (g->flags & EVX_GEMM_RELU);
     int S = 1;
     // split K only on the bf16 / x3 paths (f32 atomics reorder the sum; the exact-f32 path stays
-    // deterministic)
-    if (!epi && g->precision != EVX_PREC_F32 && tiles < 256 && g->K >= 512) {
-        S = (512 + tiles - 1) / tiles;
-        if (S > g->K / 256) S = g->K / 256;
+    // deterministic). Without an epilogue: grids under 256 tiles with K >= 512 (dW = dY^T X). With
+    // one (bias / ReLU / mask / gate), when the contraction is long enough to pay for a separate
+    // epilogue pass over C: the conv net's fc1 (K = 15 488) at a learn batch of 1024 is 32 tiles,
+    // 1.19 ms unsplit. Each K slice keeps >= 256 (>= 1024 with an epilogue) of the contraction.
+    const bool accum = (g->flags & EVX_GEMM_ACCUM) != 0;
+    if (g->precision != EVX_PREC_F32 && tiles < 256 && !(epi && accum) && g->K >= (epi ? 4096 : 512)) {
+        S = ((epi ? 1024 : 512) + tiles - 1) / tiles;
+        const int kmin = epi ? 1024 : 256;
+        if (S > g->K / kmin) S = g->K / kmin;
         if (S < 1) S = 1;
     }
     int klen = (g->K + S - 1) / S;
@@ -774,10 +807,19 @@ int gemm_launch(const evx_gemm_desc* g, int cm, int cs, void* stream) {
     S = (g->K + klen - 1) / klen;
     dim3 grid((unsigned)((g->N + TB - 1) / TB), (unsigned)((g->M + TB - 1) / TB), (unsigned)S);
     if (grid.y > 65535u) return qfail(-22, "gemm: M too large for one launch");
-    if (S > 1 && !(g->flags & EVX_GEMM_ACCUM))
+    if (S > 1 && !accum)
         hipLaunchKernelGGL(evxq::zero_rows_kernel, dim3(nblk((int64_t)g->M * g->N)), dim3(256), 0,
                            (hipStream_t)stream, g->C, g->M, g->N, g->ldc);
     hipStream_t st = (hipStream_t)stream;
+    // the K slices sum raw products (alpha applied); bias / ReLU / mask / gate follow in one pass
+    evx_gemm_desc gs = *g;
+    if (S > 1 && epi) {
+        gs.bias = nullptr;
+        gs.mask = nullptr;
+        gs.gate = nullptr;
+        gs.flags &= ~EVX_GEMM_RELU;
+    }
+    g = &gs;
     if (cm == evxq::CV_FWD)
         hipLaunchKernelGGL(evxq::gemm128x3_kernel<evxq::CV_FWD>, grid, dim3(256), 0, st, *g, klen, cs);
     else if (cm == evxq::CV_DX)
@@ -790,6 +832,11 @@ int gemm_launch(const evx_gemm_desc* g, int cm, int cs, void* stream) {
         hipLaunchKernelGGL(evxq::gemm128x3_kernel<evxq::CV_NONE>, grid, dim3(256), 0, st, *g, klen, 0);
     else
         hipLaunchKernelGGL(evxq::gemm128_kernel<float>, grid, dim3(256), 0, st, *g, klen);
+    if (S > 1 && epi) {
+        const int e = qlaunch("gemm");
+        if (e) return e;
+        hipLaunchKernelGGL(evxq::gemm_epilogue_kernel, dim3(nblk((int64_t)g->M * g->N)), dim3(256), 0, st, *orig);
+    }
     return qlaunch("gemm");
 }
 }  // namespace
@@ -814,13 +861,13 @@ int evx_conv3x3_gemm(const evx_gemm_desc* g, int32_t mode, int32_t cs, void* str
 int evx_colsum(const float* X, int64_t ld, int32_t M, int32_t N, float* out, int32_t accum, float* scratch,
                int32_t scratch_elems, void* stream) {
     if (M <= 0 || N <= 0) return 0;
-    int chunks = (M + 255) / 256;
+    int chunks = (M + evxq::COLSUM_ROWS - 1) / evxq::COLSUM_ROWS;
     if ((int64_t)chunks * N > scratch_elems) chunks = scratch_elems / N;
     if (chunks < 1) return qfail(-22, "colsum: scratch too small");
-    hipLaunchKernelGGL(evxq::colsum_kernel, dim3(nblk(N), chunks), dim3(256), 0, (hipStream_t)stream, X, ld, M, N,
-                       scratch, chunks);
-    hipLaunchKernelGGL(evxq::colsum_finish, dim3(nblk(N)), dim3(256), 0, (hipStream_t)stream, scratch, N, chunks, out,
-                       accum);
+    hipLaunchKernelGGL(evxq::colsum_kernel, dim3((unsigned)((N + 63) / 64), (unsigned)((chunks + 3) / 4)), dim3(256), 0,
+                       (hipStream_t)stream, X, ld, M, N, scratch, chunks);
+    hipLaunchKernelGGL(evxq::colsum_finish, dim3((unsigned)N), dim3(256), 0, (hipStream_t)stream, scratch, N, chunks,
+                       out, accum);
     return qlaunch("colsum");
 }
 
