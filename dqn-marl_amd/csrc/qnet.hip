@@ -794,9 +794,9 @@ int gemm_launch(const evx_gemm_desc* g, int cm, int cs, void* stream) {
     // deterministic). Without an epilogue: grids under 256 tiles with K >= 512 (dW = dY^T X). With
     // one (bias / ReLU / mask / gate), when the contraction is long enough to pay for a separate
     // epilogue pass over C: the conv net's fc1 (K = 15 488) at a learn batch of 1024 is 32 tiles,
-    // 1.19 ms unsplit. Each K slice keeps >= 256 (>= 1024 with an epilogue) of the contraction.
+    // 1.19 ms unsplit; at the act's 8192 rows 256 tiles, one 4-wave workgroup per CU. Each K slice keeps >= 256 (>= 1024 with an epilogue) of the contraction.
     const bool accum = (g->flags & EVX_GEMM_ACCUM) != 0;
-    if (g->precision != EVX_PREC_F32 && tiles < 256 && !(epi && accum) && g->K >= (epi ? 4096 : 512)) {
+    if (g->precision != EVX_PREC_F32 && tiles < (epi ? 257 : 256) && !(epi && accum) && g->K >= (epi ? 4096 : 512)) {
         S = ((epi ? 1024 : 512) + tiles - 1) / tiles;
         const int kmin = epi ? 1024 : 256;
         if (S > g->K / kmin) S = g->K / kmin;

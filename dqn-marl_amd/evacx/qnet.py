@@ -220,10 +220,11 @@ class QNet:
         self.saved = None
 
     # ------------------------------------------------------------ fc stack
-    def _fc_forward(self, X, B, K0, mask, tag):
+    def _fc_forward(self, X, B, K0, mask, tag, w1=None):
         P, ws, dev, H, A = self.P, self.ws, self.device, self.hidden, self.actions
         H1 = ws.get(tag + "h1", (B, H), torch.float32, dev)
-        gemm(B, H, K0, X, K0, 1, P["fc1.weight"], 1, K0, H1, H, self.prec, bias=P["fc1.bias"], relu=True,
+        gemm(B, H, K0, X, K0, 1, P["fc1.weight"] if w1 is None else w1, 1, K0, H1, H, self.prec, bias=P["fc1.bias"],
+             relu=True,
              mask=mask, ldm=H, mask_scale=1.0 / (1.0 - DROPOUT_P))
         H2 = ws.get(tag + "h2", (B, H // 2), torch.float32, dev)
         gemm(B, H // 2, H, H1, H, 1, P["fc2.weight"], 1, H, H2, H // 2, self.prec, bias=P["fc2.bias"], relu=True)
@@ -263,6 +264,18 @@ class QNet:
             cols.append(col)
             ys.append(Y)
             cur, C_in = Y, cout
+        if self.implicit:
+            # fc1 reads conv3's pixel-major output as it lies ([B][121 * 128], column p * 128 + c)
+            # against a copy of fc1.weight with its columns in that order (the reference flattens
+            # NCHW: column c * 121 + p). The copy is made per forward (31.7 MB, ~20 us) instead of
+            # transposing the activations (8192 rows: 507 MB, 0.57 ms).
+            W1p = ws.get(tag + "w1p", (self.hidden, 128 * 121), torch.float32, dev)
+            qcheck(L.evx_pix_nchw(_p(P["fc1.weight"]), self.hidden, 128, 0, _p(W1p), _stream()), "pix_nchw")
+            F = cur.view(B, 128 * 121)
+            H1, H2, Q = self._fc_forward(F, B, 128 * 121, mask, tag, w1=W1p)
+            if save:
+                self.saved = dict(B=B, x=F, H1=H1, H2=H2, mask=mask, cols=cols, ys=ys, w1p=W1p)
+            return Q
         F = ws.get(tag + "flat", (B, 128 * 121), torch.float32, dev)
         qcheck(L.evx_pix_nchw(_p(cur), B, 128, 1, _p(F), _stream()), "pix_nchw")  # torch reshape of NCHW
         H1, H2, Q = self._fc_forward(F, B, 128 * 121, mask, tag)
@@ -277,7 +290,8 @@ class QNet:
         B, X, H1, H2, mask = s["B"], s["x"], s["H1"], s["H2"], s["mask"]
         P, ws, dev, H, A, pr = self.P, self.ws, self.device, self.hidden, self.actions, self.prec
         K0 = X.shape[1]
-        scratch = ws.get("colsum", (max(1, (max(B * 121, B) + 255) // 256) * max(H, 128),), torch.float32, dev)
+        # colsum partials: one per 64 rows and column (evx_colsum)
+        scratch = ws.get("colsum", (max(1, (max(B * 121, B) + 63) // 64) * max(H, 128),), torch.float32, dev)
         # fc3
         gemm(A, H // 2, B, dQ, 1, A, H2, H // 2, 1, grads["fc3.weight"], H // 2, pr)
         colsum(dQ, B, A, grads["fc3.bias"], scratch)
@@ -290,16 +304,25 @@ class QNet:
         gemm(B, H, H // 2, dZ2, H // 2, 1, P["fc2.weight"], H, 1, dZ1, H, pr, mask=mask, ldm=H,
              mask_scale=1.0 / (1.0 - DROPOUT_P), gate=H1, ldg=H)
         # fc1
-        gemm(H, K0, B, dZ1, 1, H, X, K0, 1, grads["fc1.weight"], K0, pr)
+        L = qlib()
+        W1p = s.get("w1p")
+        if W1p is None:
+            gemm(H, K0, B, dZ1, 1, H, X, K0, 1, grads["fc1.weight"], K0, pr)
+        else:  # X is pixel-major: dW1 in that column order, then back to the reference's
+            dW1p = ws.get("dw1p", (H, K0), torch.float32, dev)
+            gemm(H, K0, B, dZ1, 1, H, X, K0, 1, dW1p, K0, pr)
+            qcheck(L.evx_pix_nchw(_p(dW1p), H, 128, 1, _p(grads["fc1.weight"]), _stream()), "pix_nchw")
         colsum(dZ1, B, H, grads["fc1.bias"], scratch)
         if self.kind == "mlp":
             return
-        L = qlib()
-        dF = ws.get("dflat", (B, K0), torch.float32, dev)
-        gemm(B, K0, H, dZ1, H, 1, P["fc1.weight"], K0, 1, dF, K0, pr, gate=X, ldg=K0)  # gate: relu(conv3) > 0
         Mp = B * 121
         dY = ws.get("dy2", (Mp, 128), torch.float32, dev)
-        qcheck(L.evx_pix_nchw(_p(dF), B, 128, 0, _p(dY), _stream()), "pix_nchw")
+        if W1p is not None:  # dF in pixel order is conv3's dY
+            gemm(B, K0, H, dZ1, H, 1, W1p, K0, 1, dY.view(B, K0), K0, pr, gate=X, ldg=K0)
+        else:
+            dF = ws.get("dflat", (B, K0), torch.float32, dev)
+            gemm(B, K0, H, dZ1, H, 1, P["fc1.weight"], K0, 1, dF, K0, pr, gate=X, ldg=K0)  # gate: relu(conv3) > 0
+            qcheck(L.evx_pix_nchw(_p(dF), B, 128, 0, _p(dY), _stream()), "pix_nchw")
         cols, ys = s["cols"], s["ys"]
         for li, (cname, cin, cout) in reversed(list(enumerate([("conv1", 6, 32), ("conv2", 32, 64),
                                                                 ("conv3", 64, 128)]))):
