@@ -600,7 +600,7 @@ __device__ __forceinline__ void contested_groups(T* Lp, T* heads, T* gstart, int
                     grp[i] = grp[r];
                     grp[r] = t;
                 }
-                for (int q = 1; q < cnt; q++) lost[grp[q] >> 5] |= 1u << (grp[q] & 31);
+                for (int q = 1; q < cnt; q++) atomicOr(&lost[grp[q] >> 5], 1u << (grp[q] & 31));
             }
         }
         wave_sync();
@@ -656,7 +656,11 @@ __host__ __device__ inline WaveLds wave_lds(int L, int W, int P, int R, bool big
         }
     }
     s.nearc = o; o += NCW;
-    s.lost = o; o += (P + 31) / 32;
+    if (bigg) {
+        s.lost = -1;  // global scratch, after the three bitmaps
+    } else {
+        s.lost = o; o += (P + 31) / 32;
+    }
     o = (o + 3) & ~3;
     s.robots = o; o += (R + 3) & ~3;  // 16-B aligned: read 4 robots at a time
     o = (o + 1) & ~1;
@@ -673,10 +677,11 @@ __host__ __device__ inline int64_t wave_hv_offset(int P) {
 }
 // ... | health of every not-dead person after update_health, list order (wide rows)
 __host__ __device__ inline int64_t wave_scratch_words(int P) { return wave_hv_offset(P) + 2 * (int64_t)P; }
-// ... | big grids: target, contested and vacated bitmaps [3][RW] (the per-env stride)
+// ... | big grids: target, contested and vacated bitmaps [3][RW], contest losers [P/32] (the
+// per-env stride)
 __host__ __device__ inline int64_t env_scratch_words(const evx_layout& l) {
     const int RW = ((l.L + 2) * (l.W + 2) + 31) / 32;
-    return wave_scratch_words(l.P) + (big_grid(l.L, l.W) ? 3 * (int64_t)RW : 0);
+    return wave_scratch_words(l.P) + (big_grid(l.L, l.W) ? 3 * (int64_t)RW + (l.P + 31) / 32 : 0);
 }
 
 __device__ __forceinline__ int pb_bits(int P) { return P > 1 ? bit_length((uint32_t)(P - 1)) : 1; }
@@ -724,18 +729,25 @@ __device__ __forceinline__ double readlane_d(double v, int k) {
     return __hiloint2double(hi, lo);
 }
 
+template <bool BIGG = false>
 __device__ __forceinline__ void reset_one(const evx_layout& lay, const evx_state& st, const int e, uint32_t* smem,
                                           evx_obs* obs, int32_t* err);
 
 struct ResetLds {
     int pyring, validb, rmapb, total;
 };
-__host__ __device__ inline ResetLds reset_lds(int G, int P) {
+// bigg: the validity bitmap is read from the layout's table (L2) instead of an LDS copy, so a
+// big grid's fused reset needs no more LDS than its step (cfg4: 20.7 -> 19.3 KB per env)
+__host__ __device__ inline ResetLds reset_lds(int G, int P, bool bigg = false) {
     ResetLds s;
     const int RW = (G + 31) / 32;
     int o = 0;
     s.pyring = o; o += WR;
-    s.validb = o; o += RW;
+    if (bigg) {
+        s.validb = -1;
+    } else {
+        s.validb = o; o += RW;
+    }
     s.rmapb = o; o += RW;
     s.total = (o + 3) & ~3;
     return s;
@@ -744,7 +756,7 @@ __host__ __device__ inline ResetLds reset_lds(int G, int P) {
 // dynamic LDS words of one env's wave: the step's layout, which also hosts a fused reset
 __host__ __device__ inline int step_lds_words(const evx_layout& l, bool bigg = false) {
     const int G = (l.L + 2) * (l.W + 2);
-    const int a = wave_lds(l.L, l.W, l.P, l.R, bigg).total, b = reset_lds(G, l.P).total;
+    const int a = wave_lds(l.L, l.W, l.P, l.R, bigg).total, b = reset_lds(G, l.P, bigg).total;
     return ((a > b ? a : b) + 3) & ~3;
 }
 
@@ -1285,7 +1297,7 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     };
     uint32_t* nearc = smem + S.nearc;
     const int NCW = (((g.L + 2 + 3) >> 2) * ((GY + 3) >> 2) + 31) / 32;
-    uint32_t* lost = smem + S.lost;
+    uint32_t* lost = BIGG ? vac + g.RW : smem + S.lost;  // BIGG: set by atomics, read by tc_get
     uint32_t* robots = smem + S.robots;
     uint32_t* misc = smem + S.misc;
     const uint32_t* __restrict__ validg = lay.valid_bits;
@@ -1901,7 +1913,7 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
         if (ok) {
             const int cold = (int)(en.y & 0xffffffu);
             const int t = cold + doff_of(en.y >> 24, GY);
-            const bool win = !tc_get(cbits, t) || !bit_get(lost, (int)en.x);
+            const bool win = !tc_get(cbits, t) || !tc_get(lost, (int)en.x);
             if (win) atomicOr(&vac[cold >> 5], 1u << (cold & 31));
             if (st.thmap) atomicAdd(&st.thmap[(size_t)e * g.G + (win ? t : cold)], 1);
         }
@@ -1934,7 +1946,7 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
             const int dd = (int)(en.y >> 24);
             const int t = cold + doff_of((uint32_t)dd, GY);
             const bool cont = tc_get(cbits, t);
-            if (!cont || !bit_get(lost, p)) {
+            if (!cont || !tc_get(lost, p)) {
                 const bool ex = (ci4[j] >> 1) & 1u;
                 exw = ex;
                 const bool ev_old = tc_get(tbits, cold), ev_new = tc_get(vac, t);
@@ -2216,7 +2228,7 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     if (ar) {
         __threadfence();  // this wave's state writes complete and visible before the reset reads them
         wave_sync();
-        reset_one(lay, st, e, smem, out.obs, out.err);
+        reset_one<BIGG>(lay, st, e, smem, out.obs, out.err);
     }
     EVX_RSTAMP(10);
 }
@@ -2231,7 +2243,8 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
 // from the bitmap) -> (end, success, cell). The wave then follows the chain of
 // attempts from the stream head with readlanes: a few scalar ops per attempt.
 
-// Reset of env e by the calling wave; smem: >= reset_lds(G, P).total words.
+// Reset of env e by the calling wave; smem: >= reset_lds(G, P, BIGG).total words.
+template <bool BIGG>
 __device__ __forceinline__ void reset_one(const evx_layout& lay, const evx_state& st, const int e, uint32_t* smem,
                                           evx_obs* obs, int32_t* err) {
     const int lane = (int)(threadIdx.x & 63);
@@ -2239,13 +2252,20 @@ __device__ __forceinline__ void reset_one(const evx_layout& lay, const evx_state
     g.L = lay.L; g.W = lay.W; g.GY = lay.W + 2; g.G = (lay.L + 2) * (lay.W + 2);
     g.RW = (g.G + 31) / 32; g.P = lay.P; g.R = lay.R;
     const int P = g.P, R = g.R;
-    const ResetLds S = reset_lds(g.G, P);
+    const ResetLds S = reset_lds(g.G, P, BIGG);
     uint32_t* pyring = smem + S.pyring;
-    uint32_t* validb = smem + S.validb;
+    const uint32_t* validb;
     uint32_t* rmapb = smem + S.rmapb;
-    for (int i = lane; i < g.RW; i += 64) {
-        validb[i] = lay.valid_bits[i];
-        rmapb[i] = 0;
+    if constexpr (BIGG) {
+        validb = lay.valid_bits;
+        for (int i = lane; i < g.RW; i += 64) rmapb[i] = 0;
+    } else {
+        uint32_t* vb = smem + S.validb;
+        for (int i = lane; i < g.RW; i += 64) {
+            vb[i] = lay.valid_bits[i];
+            rmapb[i] = 0;
+        }
+        validb = vb;
     }
     const uint32_t* gpy = st.py_mt + (size_t)e * EVX_MT_WORDS;
     for (int i = lane; i < MT_N; i += 64) pyring[i] = gpy[i];
