@@ -537,13 +537,22 @@ __global__ __launch_bounds__(256) void td_loss_kernel(const float* __restrict__ 
         last = atomicAdd(&g_td_ticket[gy], 1u) == nb - 1;
     }
     __syncthreads();
-    if (last && threadIdx.x == 0) {
+    if (last) {  // the whole last block: strided partial sums, then a fixed LDS tree (deterministic;
+                 // one thread walking the 128 partials of a 32768-row batch took ~20 us)
         __threadfence();
         float t = 0.f;
-        for (unsigned k = 0; k < nb; k++)
+        for (unsigned k = threadIdx.x; k < nb; k += 256)
             t += __hip_atomic_load(&g_td_part[gy * nb + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        loss_out[0] = t / (float)B;
-        g_td_ticket[gy] = 0;
+        red[threadIdx.x] = t;
+        __syncthreads();
+        for (int s = 128; s > 0; s >>= 1) {
+            if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) {
+            loss_out[0] = red[0] / (float)B;
+            g_td_ticket[gy] = 0;
+        }
     }
 }
 
