@@ -272,9 +272,14 @@ __global__ __launch_bounds__(256) void gemm128x3_kernel(evx_gemm_desc g, int ksp
     const bool a_kc = CM == CV_FWD || CM == CV_DX || g.sak == 1;
     const bool b_nc = CM == CV_DW || (CM == CV_NONE && g.sbn == 1);
     float ra[16], rb[16];
-    // CV_FWD / CV_DX: this thread's rows are m0 + (tid >> 5) + 8 i; their pixel index p0 (i = 0)
-    // steps by 8 (mod 121). CV_DW: this thread's column n = n0 + (tid & 127) is fixed.
-    const int pa0 = (int)((uint32_t)(m0 + (tid >> 5)) - div121((uint32_t)(m0 + (tid >> 5))) * 121u);
+    // Staging: a k-contiguous operand (A with a_kc, B with !b_nc -- every conv forward / dX operand
+    // and the fc layers') is held as k pairs: thread t takes rows (t >> 4) + 16 i (i < 8) at
+    // k = 2 (t & 15) + {0, 1} and stages each pair's hi and lo as one 4-byte LDS store (was 64
+    // 2-byte stores per thread per K-tile, lane pairs sharing a word). The transposed layouts keep
+    // one k per thread (rows t & 127, k = (t >> 7) + 2 i).
+    // CV_FWD / CV_DX: this thread's A rows are m0 + (t >> 4) + 16 i; their pixel index p0 (i = 0)
+    // steps by 16 (mod 121). CV_DW: this thread's column n = n0 + (tid & 127) is fixed.
+    const int pa0 = (int)((uint32_t)(m0 + (tid >> 4)) - div121((uint32_t)(m0 + (tid >> 4))) * 121u);
     int dw_c = 0, dw_dy = 0, dw_dx = 0;
     if constexpr (CM == CV_DW) {
         const int n = n0 + (tid & 127);
@@ -283,36 +288,63 @@ __global__ __launch_bounds__(256) void gemm128x3_kernel(evx_gemm_desc g, int ksp
         dw_dy = tap / 3 - 1;
         dw_dx = tap - (tap / 3) * 3 - 1;
     }
+    const int kp = 2 * (tid & 15), rp = tid >> 4;  // pair layout: k offset, first row
     auto fetch = [&](int k0) {
         if constexpr (CM == CV_FWD || CM == CV_DX) {
-            const int k = k0 + (tid & 31);
-            const int tap = k / cs, c = k - tap * cs;
-            int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
-            if (CM == CV_DX) { dy = -dy; dx = -dx; }
-            const int64_t toff = (int64_t)(dy * 11 + dx) * cs + c;
+            int64_t toff[2], boff[2];
+            int dyq[2], dxq[2];
+            bool kin[2];
+#pragma unroll
+            for (int q = 0; q < 2; q++) {
+                const int k = k0 + kp + q;
+                const int tap = k / cs, c = k - tap * cs;
+                int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
+                boff[q] = (int64_t)c * g.sbk + tap;
+                if (CM == CV_DX) { dy = -dy; dx = -dx; }
+                dyq[q] = dy;
+                dxq[q] = dx;
+                toff[q] = (int64_t)(dy * 11 + dx) * cs + c;
+                kin[q] = k < ke;
+            }
             int p = pa0;
 #pragma unroll
-            for (int i = 0; i < 16; i++) {
-                const int gm = m0 + (tid >> 5) + 8 * i;
+            for (int i = 0; i < 8; i++) {
+                const int gm = m0 + rp + 16 * i;
                 const int y = div11(p), x = p - 11 * y;
-                const bool ok = gm < g.M && k < ke && (unsigned)(y + dy) < 11u && (unsigned)(x + dx) < 11u;
-                ra[i] = ok ? g.A[(int64_t)gm * cs + toff] : 0.f;
-                p += 8;
+#pragma unroll
+                for (int q = 0; q < 2; q++) {
+                    const bool ok = gm < g.M && kin[q] && (unsigned)(y + dyq[q]) < 11u && (unsigned)(x + dxq[q]) < 11u;
+                    ra[2 * i + q] = ok ? g.A[(int64_t)gm * cs + toff[q]] : 0.f;
+                }
+                p += 16;
                 if (p >= 121) p -= 121;
             }
 #pragma unroll
-            for (int i = 0; i < 16; i++) {
-                const int gn = n0 + (tid >> 5) + 8 * i;
-                rb[i] = (gn < g.N && k < ke) ? g.B[(int64_t)c * g.sbk + (int64_t)gn * g.sbn + tap] : 0.f;
+            for (int i = 0; i < 8; i++) {
+                const int gn = n0 + rp + 16 * i;
+#pragma unroll
+                for (int q = 0; q < 2; q++)
+                    rb[2 * i + q] = (gn < g.N && kin[q]) ? g.B[boff[q] + (int64_t)gn * g.sbn] : 0.f;
             }
         } else {
+            if (a_kc) {
 #pragma unroll
-            for (int i = 0; i < 16; i++) {
-                const int idx = tid + 256 * i;
-                int mm, kk;
-                if (a_kc) { mm = idx >> 5; kk = idx & 31; } else { kk = idx >> 7; mm = idx & 127; }
-                const int gm = m0 + mm, gk = k0 + kk;
-                ra[i] = (gm < g.M && gk < ke) ? g.A[(int64_t)gm * g.sam + (int64_t)gk * g.sak] : 0.f;
+                for (int i = 0; i < 8; i++) {
+                    const int gm = m0 + rp + 16 * i;
+#pragma unroll
+                    for (int q = 0; q < 2; q++) {
+                        const int gk = k0 + kp + q;
+                        ra[2 * i + q] = (gm < g.M && gk < ke) ? g.A[(int64_t)gm * g.sam + (int64_t)gk * g.sak] : 0.f;
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < 16; i++) {
+                    const int idx = tid + 256 * i;
+                    const int kk = idx >> 7, mm = idx & 127;
+                    const int gm = m0 + mm, gk = k0 + kk;
+                    ra[i] = (gm < g.M && gk < ke) ? g.A[(int64_t)gm * g.sam + (int64_t)gk * g.sak] : 0.f;
+                }
             }
             if constexpr (CM == CV_DW) {
                 const int gn = n0 + (tid & 127);
@@ -328,36 +360,62 @@ __global__ __launch_bounds__(256) void gemm128x3_kernel(evx_gemm_desc g, int ksp
                     p += 2;
                     if (p >= 121) p -= 121;
                 }
-            } else {
+            } else if (b_nc) {
 #pragma unroll
                 for (int i = 0; i < 16; i++) {
                     const int idx = tid + 256 * i;
-                    int nn, kk;
-                    if (b_nc) { kk = idx >> 7; nn = idx & 127; } else { nn = idx >> 5; kk = idx & 31; }
+                    const int kk = idx >> 7, nn = idx & 127;
                     const int gn = n0 + nn, gk = k0 + kk;
                     rb[i] = (gn < g.N && gk < ke) ? g.B[(int64_t)gk * g.sbk + (int64_t)gn * g.sbn] : 0.f;
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < 8; i++) {
+                    const int gn = n0 + rp + 16 * i;
+#pragma unroll
+                    for (int q = 0; q < 2; q++) {
+                        const int gk = k0 + kp + q;
+                        rb[2 * i + q] = (gn < g.N && gk < ke) ? g.B[(int64_t)gk * g.sbk + (int64_t)gn * g.sbn] : 0.f;
+                    }
                 }
             }
         }
     };
+    // one k pair -> hi pair and lo pair, each a 4-byte LDS store
+    auto put2 = [&](__bf16 (*S)[TB][PK], int row, int kk, float v0, float v1) {
+        const __bf16 h0 = (__bf16)v0, h1 = (__bf16)v1;
+        const __bf16 l0 = (__bf16)(v0 - (float)h0), l1 = (__bf16)(v1 - (float)h1);
+        *reinterpret_cast<uint32_t*>(&S[0][row][kk]) =
+            (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
+        *reinterpret_cast<uint32_t*>(&S[1][row][kk]) =
+            (uint32_t)__builtin_bit_cast(uint16_t, l0) | ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
+    };
     auto stash = [&]() {
+        if (a_kc) {
 #pragma unroll
-        for (int i = 0; i < 16; i++) {
-            const int idx = tid + 256 * i;
-            int mm, kk;
-            if (a_kc) { mm = idx >> 5; kk = idx & 31; } else { kk = idx >> 7; mm = idx & 127; }
-            const __bf16 hi = (__bf16)ra[i];
-            As[0][mm][kk] = hi;
-            As[1][mm][kk] = (__bf16)(ra[i] - (float)hi);
+            for (int i = 0; i < 8; i++) put2(As, rp + 16 * i, kp, ra[2 * i], ra[2 * i + 1]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                const int idx = tid + 256 * i;
+                const int kk = idx >> 7, mm = idx & 127;
+                const __bf16 hi = (__bf16)ra[i];
+                As[0][mm][kk] = hi;
+                As[1][mm][kk] = (__bf16)(ra[i] - (float)hi);
+            }
         }
+        if (!b_nc) {
 #pragma unroll
-        for (int i = 0; i < 16; i++) {
-            const int idx = tid + 256 * i;
-            int nn, kk;
-            if (b_nc) { kk = idx >> 7; nn = idx & 127; } else { nn = idx >> 5; kk = idx & 31; }
-            const __bf16 hi = (__bf16)rb[i];
-            Bs[0][nn][kk] = hi;
-            Bs[1][nn][kk] = (__bf16)(rb[i] - (float)hi);
+            for (int i = 0; i < 8; i++) put2(Bs, rp + 16 * i, kp, rb[2 * i], rb[2 * i + 1]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                const int idx = tid + 256 * i;
+                const int kk = idx >> 7, nn = idx & 127;
+                const __bf16 hi = (__bf16)rb[i];
+                Bs[0][nn][kk] = hi;
+                Bs[1][nn][kk] = (__bf16)(rb[i] - (float)hi);
+            }
         }
     };
     if (kb < ke) fetch(kb);
