@@ -1208,12 +1208,34 @@ __global__ __launch_bounds__(256) void qbwd3_kernel(Bwd a0) {
 // 32 columns), K = 256 in chunks of 32; dZ2 staged through LDS, W2^T operand-tiled.
 template <bool X3>
 constexpr int qdz1_lds_bytes() { return 2 * (X3 ? 2 : 1) * RM * 40 * 2; }
+// Row tiles per qdz1 workgroup: the tile's column sums (db1 and the centre column of dW1) leave by
+// one f32 atomic per column; with one 64-row tile per workgroup every such word took B / 64
+// same-address atomics, which the L2 serialises.
+constexpr int QZ_RT = 2;
+template <bool X3 = false>
+__device__ __forceinline__ void qdz1_tile(const Bwd& a, char* smem, int m0, int by, float& cs);
 template <bool X3 = false>
 __device__ __forceinline__ void qdz1_body(const Bwd& a, char* smem, int bx, int by) {
+    float cs = 0.f;
+    for (int rt = 0; rt < QZ_RT; rt++) {
+        const int m0 = (bx * QZ_RT + rt) * RM;
+        if (m0 >= a.B) break;
+        qdz1_tile<X3>(a, smem, m0, by, cs);
+    }
+    const int lane = threadIdx.x & 63, h = lane >> 5;
+    const int col = by * 128 + (threadIdx.x >> 6) * 32 + (lane & 31);
+    cs += __shfl_xor(cs, 32, 64);  // the two row halves of the column
+    if (h == 0) {
+        atomicAdd(&a.gb1[col], cs);
+        atomicAdd(&a.gw1[(size_t)col * K1 + CENTRE_COL], cs);  // d/dW1 of the constant centre input
+    }
+}
+template <bool X3>
+__device__ __forceinline__ void qdz1_tile(const Bwd& a, char* smem, int m0, int by, float& cs) {
     constexpr int NPL = X3 ? 2 : 1;
     auto As = reinterpret_cast<__bf16 (*)[NPL][RM][40]>(smem);  // [2][NPL][RM][40], pitch 20 words: conflict-free b128 reads
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
-    const int m0 = bx * RM, n0 = by * 128 + w * 32;
+    const int n0 = by * 128 + w * 32;
     const int gr = tid >> 2, go = (tid & 3) * 8;
     const bool rowok = m0 + gr < a.B;
     f32x16 acc[2];
@@ -1276,7 +1298,6 @@ __device__ __forceinline__ void qdz1_body(const Bwd& a, char* smem, int bx, int 
         __syncthreads();
     }
     const int col = n0 + (lane & 31);
-    float cs = 0.f;
 #pragma unroll
     for (int mt = 0; mt < 2; mt++)
 #pragma unroll
@@ -1292,11 +1313,6 @@ __device__ __forceinline__ void qdz1_body(const Bwd& a, char* smem, int bx, int 
             }
             cs += v;
         }
-    cs += __shfl_xor(cs, 32, 64);  // the two row halves of the column
-    if (h == 0) {
-        atomicAdd(&a.gb1[col], cs);
-        atomicAdd(&a.gw1[(size_t)col * K1 + CENTRE_COL], cs);  // d/dW1 of the constant centre input
-    }
 }
 template <bool X3 = false>
 __global__ __launch_bounds__(256, 2) void qdz1_kernel(Bwd a) {
@@ -2015,7 +2031,7 @@ static void launch_tail(const evxm::Bwd& a, int32_t B, const evx_qmlp_grads* g, 
                     ksplit_kper(B, X3 ? 20 : 24), g->w1, evxm::K1, X3 ? 3 : 1, g->part ? g->part + part2_floats(B) : nullptr,
                     X3 ? a.dz1l : nullptr, nullptr, KX / evxm::TT, evxm::HID / evxm::TT, 0};
     g1.gz = (B + g1.kper - 1) / g1.kper;
-    const int ndzx = (B + evxm::RM - 1) / evxm::RM;
+    const int ndzx = (B + evxm::RM * evxm::QZ_RT - 1) / (evxm::RM * evxm::QZ_RT);
     if (nets > 1) {  // grouped (x3, partials): net g's operands, gradients and partials (fwd_net / bwd_net)
         const int64_t pf = evx_qmlp_backward_part_floats(B);
         g2.gsA = 2 * (int64_t)B * evxm::HID2;
