@@ -1211,7 +1211,7 @@ constexpr int qdz1_lds_bytes() { return 2 * (X3 ? 2 : 1) * RM * 40 * 2; }
 // Row tiles per qdz1 workgroup: the tile's column sums (db1 and the centre column of dW1) leave by
 // one f32 atomic per column; with one 64-row tile per workgroup every such word took B / 64
 // same-address atomics, which the L2 serialises.
-constexpr int QZ_RT = 4;
+constexpr int QZ_RT = 8;
 template <bool X3 = false>
 __device__ __forceinline__ void qdz1_tile(const Bwd& a, char* smem, int m0, int by, float& cs);
 template <bool X3 = false>
