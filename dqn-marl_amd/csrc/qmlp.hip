@@ -1210,15 +1210,18 @@ template <bool X3>
 constexpr int qdz1_lds_bytes() { return 2 * (X3 ? 2 : 1) * RM * 40 * 2; }
 // Row tiles per qdz1 workgroup: the tile's column sums (db1 and the centre column of dW1) leave by
 // one f32 atomic per column; with one 64-row tile per workgroup every such word took B / 64
-// same-address atomics, which the L2 serialises.
+// same-address atomics, which the L2 serialises. Up to QZ_RT tiles per workgroup while the grid
+// keeps >= 256 qdz1 workgroups (qdz1_tiles_per_wg; B = 32768: 8, 8192: 2, 4096: 1).
 constexpr int QZ_RT = 8;
+inline int qdz1_tiles_per_wg(int B) { return B / 4096 < 1 ? 1 : (B / 4096 > QZ_RT ? QZ_RT : B / 4096); }
 template <bool X3 = false>
 __device__ __forceinline__ void qdz1_tile(const Bwd& a, char* smem, int m0, int by, float& cs);
 template <bool X3 = false>
-__device__ __forceinline__ void qdz1_body(const Bwd& a, char* smem, int bx, int by) {
+__device__ __forceinline__ void qdz1_body(const Bwd& a, char* smem, int bx, int by, int ndzx) {
     float cs = 0.f;
-    for (int rt = 0; rt < QZ_RT; rt++) {
-        const int m0 = (bx * QZ_RT + rt) * RM;
+    const int nrt = (a.B + RM * ndzx - 1) / (RM * ndzx);  // row tiles per workgroup
+    for (int rt = 0; rt < nrt; rt++) {
+        const int m0 = (bx * nrt + rt) * RM;
         if (m0 >= a.B) break;
         qdz1_tile<X3>(a, smem, m0, by, cs);
     }
@@ -1317,7 +1320,7 @@ __device__ __forceinline__ void qdz1_tile(const Bwd& a, char* smem, int m0, int 
 template <bool X3 = false>
 __global__ __launch_bounds__(256, 2) void qdz1_kernel(Bwd a) {
     __shared__ __attribute__((aligned(16))) char smem[qdz1_lds_bytes<X3>()];
-    qdz1_body<X3>(a, smem, blockIdx.x, blockIdx.y);
+    qdz1_body<X3>(a, smem, blockIdx.x, blockIdx.y, gridDim.x);
 }
 
 // C[m][n] += sum_k A[k][m] B[k][n] (both operands K-major bf16), 128x128 tiles of
@@ -1514,8 +1517,8 @@ __global__ __launch_bounds__(256, 2) void bwd_mid_kernel(Bwd a, int ndzx, GemmTN
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int b = (int)blockIdx.x, ndz = ndzx * (HID / 128);
     if (b < ndz) {
-        if constexpr (GR) qdz1_body<X3>(bwd_net(a, (int)blockIdx.y), smem, b % ndzx, b / ndzx);
-        else qdz1_body<X3>(a, smem, b % ndzx, b / ndzx);
+        if constexpr (GR) qdz1_body<X3>(bwd_net(a, (int)blockIdx.y), smem, b % ndzx, b / ndzx, ndzx);
+        else qdz1_body<X3>(a, smem, b % ndzx, b / ndzx, ndzx);
     } else {
         const int t = b - ndz, gxy = g.gx * g.gy;
         if constexpr (GR) gemm_tn_body<AP, BP>(tn_net(g, (int)blockIdx.y), smem, t % g.gx, (t % gxy) / g.gx, t / gxy);
@@ -2031,7 +2034,8 @@ static void launch_tail(const evxm::Bwd& a, int32_t B, const evx_qmlp_grads* g, 
                     ksplit_kper(B, X3 ? 20 : 24), g->w1, evxm::K1, X3 ? 3 : 1, g->part ? g->part + part2_floats(B) : nullptr,
                     X3 ? a.dz1l : nullptr, nullptr, KX / evxm::TT, evxm::HID / evxm::TT, 0};
     g1.gz = (B + g1.kper - 1) / g1.kper;
-    const int ndzx = (B + evxm::RM * evxm::QZ_RT - 1) / (evxm::RM * evxm::QZ_RT);
+    const int qrt = evxm::qdz1_tiles_per_wg(B);
+    const int ndzx = (B + evxm::RM * qrt - 1) / (evxm::RM * qrt);
     if (nets > 1) {  // grouped (x3, partials): net g's operands, gradients and partials (fwd_net / bwd_net)
         const int64_t pf = evx_qmlp_backward_part_floats(B);
         g2.gsA = 2 * (int64_t)B * evxm::HID2;
