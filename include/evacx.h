@@ -168,7 +168,11 @@ const char *evx_last_error(void);
 /* C[m][n] = epi(alpha * sum_k A(m,k) B(k,n) + bias[n]) with A(m,k) = A[m*sam + k*sak],
  * B(k,n) = B[k*sbk + n*sbn], C[m*ldc + n]; epilogue order: bias, ReLU, dropout mask
  * (mask[m*ldm+n] ? v*mask_scale : 0), ReLU-backward gate (gate[m*ldg+n] > 0 ? v : 0),
- * accumulate. Covers nn.Linear forward (A x W^T), its dX (dY W) and dW (dY^T X). */
+ * accumulate. Covers nn.Linear forward (A x W^T), its dX (dY W) and dW (dY^T X).
+ * BF16 / X3 GEMMs with fewer than 256 128x128 tiles and a long K are split over K: the slices
+ * add into C with f32 atomics (summation order not fixed between calls; EVX_PREC_F32 never
+ * splits), and with an epilogue C is first the raw sum, then rewritten by an epilogue pass on
+ * the same stream. ACCUM with an epilogue is never split. */
 typedef struct {
     int32_t M, N, K;
     int32_t precision;         /* EVX_PREC_* */
