@@ -92,7 +92,17 @@ def parse():
                     help="env-only preparation steps that spread env ages over an episode (before --warmup)")
     ap.add_argument("--stagger", type=int, default=1200,
                     help="preparation step w force-resets envs with global id %% stagger == w (0 = no stagger)")
-    ap.add_argument("--envs", type=int, default=32768, help="envs per GPU")
+    ap.add_argument("--envs", type=int, default=32768,
+                    help="envs PER GPU (weak scaling: N GPUs step N x envs); see --envs-total")
+    ap.add_argument("--envs-total", type=int, default=0,
+                    help="envs of the WHOLE job, split evenly over the ranks (overrides --envs; strong-scaling "
+                         "reading)")
+    ap.add_argument("--total-reading", type=int, default=32768,
+                    help="extra (N > 1 only): also time the training step with this many envs for the whole job "
+                         "(BASELINE.json configs[2] read as 32768 envs over all GPUs: 32768 / N per GPU); 0 = skip")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="torch.distributed backend when WORLD_SIZE > 1 (nccl = RCCL over xGMI; gloo: CPU tests, "
+                         "several ranks on one GPU)")
     ap.add_argument("--grid", type=int, default=128)
     ap.add_argument("--layouts", type=int, default=1,
                     help="K > 1: per-env layouts, K random variants of the synthetic layout (env e runs e %% K)")
@@ -132,6 +142,11 @@ def parse():
                     help="PMC traffic record of env_step_kernel on this workload and phase (tools/parse_prof.py); "
                          "default profiles/r2/env_traffic_<phase>.json")
     args = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.envs_total > 0:
+        if args.envs_total % world:
+            ap.error("--envs-total must be a multiple of the world size")
+        args.envs = args.envs_total // world
     if args.batch <= 0:
         args.batch = args.envs
     if args.replay_capacity <= 0:
@@ -170,11 +185,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    # one rank per GPU; with gloo, ranks beyond the visible GPUs share them (tests on one GPU)
+    dev = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev)
     dist = None
     if world > 1:
         import torch.distributed as dist  # noqa: F811
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group("gloo")
 
     from evacx.env import DeviceLayout
     from evacx.layout import build_tables_device, synthetic
@@ -195,14 +215,6 @@ def main():
         lay_tables = build_tables_device([spec])
         lay = DeviceLayout(lay_tables[0], P)
     hook = make_allreduce_hook(dist, world) if dist is not None else None
-    tr = VecTrainer(lay, E, env_offset=rank * E, kind=args.qnet, precision=args.precision, batch=args.batch,
-                    grad_hook=hook,
-                    lagged_learn=args.schedule == "lagged", replay=args.replay,
-                    replay_capacity=args.replay_capacity, groups=args.groups if args.mode == "train" else 1,
-                    layout_of=layout_of, world_envs=E * world, nets=args.nets)
-    env = tr.env
-    lagged_ok = tr.fast is not None  # the lagged schedule needs the fused MLP path
-    schedule = args.schedule if lagged_ok else "strict"
 
     def barrier():
         if dist is not None:
@@ -216,24 +228,37 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    # --------------------------------------------------- episode-phase preparation
-    # env-only steps (uniform random actions): preparation step w force-resets the envs
-    # with global id % stagger == w, spreading env ages over one episode length
-    gid = torch.arange(E, device="cuda") + rank * E
+    def build(E, batch):
+        """The trainer for E envs per rank (global env ids rank * E + e), prepared to the episode
+        phase: env-only steps (uniform random actions) where preparation step w force-resets the
+        envs with global id % stagger == w, spreading env ages over one episode length."""
+        tr = VecTrainer(lay, E, env_offset=rank * E, kind=args.qnet, precision=args.precision, batch=batch,
+                        grad_hook=hook,
+                        lagged_learn=args.schedule == "lagged", replay=args.replay,
+                        replay_capacity=args.replay_capacity, groups=args.groups if args.mode == "train" else 1,
+                        layout_of=layout_of, world_envs=E * world, nets=args.nets)
+        env = tr.env
+        gid = torch.arange(E, device="cuda") + rank * E
+        S = args.stagger
+        prep_acts = torch.empty(E * R, device="cuda", dtype=torch.int32)
+        g = torch.Generator(device="cuda").manual_seed(4321 + rank)
+        for w in range(args.age_steps):
+            if rank == 0 and w % 200 == 0:  # progress on stderr (long profiled runs)
+                print(f"preparation step {w}/{args.age_steps} ({E} envs per rank)", file=sys.stderr, flush=True)
+            torch.randint(0, 5, (E * R,), device="cuda", dtype=torch.int32, generator=g, out=prep_acts)
+            env.step(prep_acts, auto_reset=True)
+            if 0 < S and w < S:
+                force = (gid % S == w) & ~env.done.bool()
+                env.reset(mask=force)
+        if args.phase == "start":
+            env.reset()  # every env at the start of an episode (people fresh, fire kept)
+        barrier()
+        return tr, env
+
     S = args.stagger
-    prep_acts = torch.empty(E * R, device="cuda", dtype=torch.int32)
-    g = torch.Generator(device="cuda").manual_seed(4321 + rank)
-    for w in range(args.age_steps):
-        if rank == 0 and w % 200 == 0:  # progress on stderr (long profiled runs)
-            print(f"preparation step {w}/{args.age_steps}", file=sys.stderr, flush=True)
-        torch.randint(0, 5, (E * R,), device="cuda", dtype=torch.int32, generator=g, out=prep_acts)
-        env.step(prep_acts, auto_reset=True)
-        if 0 < S and w < S:
-            force = (gid % S == w) & ~env.done.bool()
-            env.reset(mask=force)
-    if args.phase == "start":
-        env.reset()  # every env at the start of an episode (people fresh, fire kept)
-    barrier()
+    tr, env = build(E, args.batch)
+    lagged_ok = tr.fast is not None  # the lagged schedule needs the fused MLP path
+    schedule = args.schedule if lagged_ok else "strict"
 
     def timed_train(n, ev_env=None, ev_learn=None):
         barrier()
@@ -312,6 +337,23 @@ def main():
                  "steps": args.start_steps,
                  "what": "every env reset (all persons in play), then the timed training steps"}
 
+    # ---------- BASELINE configs[2] read as envs for the whole job (extra, N > 1 only)
+    total = None
+    Et = args.total_reading // world if args.total_reading > 0 and args.total_reading % world == 0 else 0
+    if args.mode == "train" and world > 1 and Et > 0 and Et != E and args.envs_total == 0:
+        tr.sync()
+        tr = env = None  # free the headline's state first
+        torch.cuda.empty_cache()
+        tr, env = build(Et, Et)
+        timed_train(max(args.warmup, 3))
+        n_t = max(5, args.steps // 2)
+        dt = timed_train(n_t)
+        total = {"envs_total": Et * world, "envs_per_gpu": Et, "batch_per_gpu": Et, "steps": n_t,
+                 "steps_per_s": Et * world * n_t / dt, "agent_transitions_per_s": Et * world * n_t / dt * R,
+                 "ms_per_step": 1e3 * dt / n_t,
+                 "what": f"BASELINE.json configs[2] read as {Et * world} envs for the whole {world}-GPU job "
+                         f"({Et} per GPU, learn batch {Et} per GPU), same phase preparation and schedule"}
+
     G = (L + 2) * (W + 2)
     bpe = bytes_per_env_step(P, R, G)
     per_launch = E // args.groups if args.mode == "train" else E  # env.step launches of group 0 are timed
@@ -360,13 +402,21 @@ def main():
                                 if args.phase == "stationary" else
                                 "; episode phase: start (every env freshly reset before the timed steps)")),
                 "episode_phase": args.phase, "age_steps": args.age_steps, "stagger": S,
-                "envs_per_gpu": E, "grid": f"{L}x{W}", "people": P, "robots": R, "mode": args.mode,
+                "envs_per_gpu": E, "envs_total": E * world,
+                "baseline_mapping": ("BASELINE.json configs[2] (32768 envs x 16 agents, 128x128) is run as "
+                                     f"{E} envs PER GPU (weak scaling: {E * world} envs over {world} GPU(s)), learn "
+                                     f"batch {args.batch} per GPU; the whole-job-32768 reading is "
+                                     "total_envs_reading (N > 1)") if (L, R) == (128, 16) else None, "grid": f"{L}x{W}", "people": P, "robots": R, "mode": args.mode,
                 "batch": args.batch, "replay_capacity": args.replay_capacity, "schedule": schedule, "precision": prec,
                 "qnet": ("MLP 726-512-256-5" if args.qnet == "mlp"
                          else "DQNNetwork conv 6-32-64-128 + 15488-512-256-5"),
                 "replay": args.replay, "groups": args.groups if args.mode == "train" else 1, "nets": args.nets,
-                "parallelism": f"data-parallel over {world} GPU(s): envs sharded, grad all-reduce (RCCL) per learn",
+                "parallelism": (f"data-parallel over {world} GPU(s): envs sharded by global id, grad all-reduce "
+                                f"({'RCCL' if args.dist_backend == 'nccl' else 'gloo'}) per learn"
+                                if world > 1 else "1 GPU"),
+                "dist_backend": args.dist_backend if world > 1 else None,
             },
+            "total_envs_reading": total,
             "other_schedule": other,
             "env_only_steps_per_s": env_only,
             "start_phase": start,

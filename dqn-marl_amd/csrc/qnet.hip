@@ -123,9 +123,9 @@ __global__ __launch_bounds__(256) void gemm_kernel(evx_gemm_desc g) {
 // 128x128x32 block tile, 4 waves as 2x2, each wave 64x64 = 2x2 MFMA 32x32 tiles (64 f32
 // accumulators per lane). The next K-tile is fetched into registers while the current
 // one is multiplied (register double buffering, one barrier pair per K-step). gridDim.z
-// splits K: partial sums are atomically added into a zeroed C (used for dW = dY^T X,
-// whose M x N grid alone cannot fill 256 CUs); with epilogue ops the slices sum raw products
-// and gemm_epilogue_kernel applies them afterwards.
+// splits K: each slice stores its raw partial into the workspace ws[z][M][N] (used for dW =
+// dY^T X, whose M x N grid alone cannot fill 256 CUs, and long-K GEMMs with an epilogue);
+// splitk_reduce_kernel adds the slices in slice order and applies the epilogue.
 constexpr int TB = 128;
 template <typename TIn>
 __global__ __launch_bounds__(256) void gemm128_kernel(evx_gemm_desc g, int ksplit_len) {
@@ -221,8 +221,8 @@ __global__ __launch_bounds__(256) void gemm128_kernel(evx_gemm_desc g, int kspli
                 const int gm = m0 + wm * 64 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
                 if (gm >= g.M) continue;
                 float* cp = g.C + (int64_t)gm * g.ldc + gn;
-                if (split) {
-                    atomicAdd(cp, g.alpha * acc[mi][ni][r]);
+                if (split) {  // this K slice's partial, summed in slice order by splitk_reduce_kernel
+                    g.ws[((int64_t)blockIdx.z * g.M + gm) * g.N + gn] = g.alpha * acc[mi][ni][r];
                     continue;
                 }
                 float v = g.alpha * acc[mi][ni][r] + bias;
@@ -459,8 +459,8 @@ __global__ __launch_bounds__(256) void gemm128x3_kernel(evx_gemm_desc g, int ksp
                 const int gm = m0 + wm * 64 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
                 if (gm >= g.M) continue;
                 float* cp = g.C + (int64_t)gm * g.ldc + gn;
-                if (split) {
-                    atomicAdd(cp, g.alpha * acc[mi][ni][r]);
+                if (split) {  // this K slice's partial, summed in slice order by splitk_reduce_kernel
+                    g.ws[((int64_t)blockIdx.z * g.M + gm) * g.N + gn] = g.alpha * acc[mi][ni][r];
                     continue;
                 }
                 float v = g.alpha * acc[mi][ni][r] + bias;
@@ -474,27 +474,44 @@ __global__ __launch_bounds__(256) void gemm128x3_kernel(evx_gemm_desc g, int ksp
     }
 }
 
-// Epilogue of a split-K GEMM whose partials were atomically summed into a zeroed C (C holds
-// alpha * A B): bias, ReLU, dropout mask, gate -- the same sequence as the one-pass epilogue.
-__global__ __launch_bounds__(256) void gemm_epilogue_kernel(evx_gemm_desc g) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= (int64_t)g.M * g.N) return;
-    const int64_t gm = i / g.N;
-    const int gn = (int)(i - gm * g.N);
-    float* cp = g.C + gm * g.ldc + gn;
-    float v = *cp + (g.bias ? g.bias[gn] : 0.f);
-    if (g.flags & EVX_GEMM_RELU) v = v > 0.f ? v : 0.f;
-    if (g.mask) v = g.mask[gm * g.ldm + gn] ? v * g.mask_scale : 0.f;
-    if (g.gate) v = g.gate[gm * g.ldg + gn] > 0.f ? v : 0.f;
-    *cp = v;
-}
-
-// zero an f32 matrix C[M][ldc] (split-K target)
-__global__ __launch_bounds__(256) void zero_rows_kernel(float* __restrict__ C, int M, int N, int64_t ldc) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= (int64_t)M * N) return;
-    const int64_t m = i / N, n = i - m * N;
-    C[m * ldc + n] = 0.f;
+// Split-K reduction + epilogue: C = epi(sum_z ws[z][m][n]) with the slices added in slice order
+// (deterministic: the same bits on every call), then bias, ReLU, dropout mask, gate, accumulate --
+// the same sequence as the one-pass epilogue. Four consecutive columns per thread (16-B loads).
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(evx_gemm_desc g, int S) {
+    const int64_t MN = (int64_t)g.M * g.N;
+    const int64_t i0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+    if (i0 >= MN) return;
+    float v[4];
+    const bool vec = (i0 + 4 <= MN) && ((MN & 3) == 0);
+    if (vec) {
+        float4 a = *reinterpret_cast<const float4*>(g.ws + i0);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+        for (int z = 1; z < S; z++) {
+            const float4 b = *reinterpret_cast<const float4*>(g.ws + (int64_t)z * MN + i0);
+            v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+        }
+    } else {
+        for (int j = 0; j < 4; j++) {
+            v[j] = 0.f;
+            if (i0 + j < MN) {
+                v[j] = g.ws[i0 + j];
+                for (int z = 1; z < S; z++) v[j] += g.ws[(int64_t)z * MN + i0 + j];
+            }
+        }
+    }
+    for (int j = 0; j < 4; j++) {
+        const int64_t i = i0 + j;
+        if (i >= MN) break;
+        const int64_t gm = i / g.N;
+        const int gn = (int)(i - gm * g.N);
+        float* cp = g.C + gm * g.ldc + gn;
+        float x = v[j] + (g.bias ? g.bias[gn] : 0.f);
+        if (g.flags & EVX_GEMM_RELU) x = x > 0.f ? x : 0.f;
+        if (g.mask) x = g.mask[gm * g.ldm + gn] ? x * g.mask_scale : 0.f;
+        if (g.gate) x = g.gate[gm * g.ldg + gn] > 0.f ? x : 0.f;
+        if (g.flags & EVX_GEMM_ACCUM) x += *cp;
+        *cp = x;
+    }
 }
 
 // ------------------------------------------------------------- column sums
@@ -721,6 +738,54 @@ __global__ __launch_bounds__(256) void replay_push_kernel(evx_replay rp, const e
     rp.done[slot] = done_env[e];
 }
 
+// Sampling WITHOUT replacement, as DQNAgent.learn's random.sample(memory, B)
+// (agents/dqn_agent.py:132): draw i of a batch is perm(i) for a keyed pseudo-random permutation
+// perm of [0, n) -- a 6-round balanced Feistel network on the smallest even-width domain 2^w >= n,
+// cycle-walked back into [0, n) (terminates: i's cycle under the domain permutation contains i
+// itself; expected < 4 rounds of walking since 2^w < 4n). Round keys from Philox4x32-10 of the
+// draw's (offset, stream) under the seed, so each learn step's batch is a fresh permutation and
+// the B draws are distinct (B <= n). oracle/draw_oracle.c orc_replay_indices restates it.
+struct perm_key {
+    uint32_t k[6];
+    int half;       // bits per Feistel half
+    uint64_t hmask; // (1 << half) - 1
+};
+__device__ __forceinline__ uint32_t fmix32(uint32_t h) {
+    h ^= h >> 16;
+    h *= 0x85ebca6bu;
+    h ^= h >> 13;
+    h *= 0xc2b2ae35u;
+    h ^= h >> 16;
+    return h;
+}
+__device__ __forceinline__ perm_key make_perm_key(uint64_t n, uint64_t seed, uint64_t offset, uint32_t stream) {
+    perm_key pk;
+    const u4 q = philox((uint32_t)offset, (uint32_t)(offset >> 32), 0x5a3b1eu, stream, (uint32_t)seed,
+                        (uint32_t)(seed >> 32));
+    const uint32_t qq[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int r = 0; r < 6; r++) pk.k[r] = fmix32(qq[r & 3] + (uint32_t)r * 0x9e3779b9u);
+    int w = 2;
+    while (w < 62 && (1ull << w) < n) w += 2;
+    pk.half = w / 2;
+    pk.hmask = (1ull << pk.half) - 1;
+    return pk;
+}
+__device__ __forceinline__ uint64_t perm_apply(const perm_key& pk, uint64_t x, uint64_t n) {
+    do {
+        uint64_t L = x >> pk.half, R = x & pk.hmask;
+#pragma unroll
+        for (int r = 0; r < 6; r++) {
+            const uint64_t F = (uint64_t)fmix32((uint32_t)R ^ pk.k[r]) & pk.hmask;  // R < 2^31
+            const uint64_t t = R;
+            R = L ^ F;
+            L = t;
+        }
+        x = (L << pk.half) | R;
+    } while (x >= n);
+    return x;
+}
+
 __global__ __launch_bounds__(256) void replay_sample_kernel(evx_replay rp, int64_t base, int64_t size, int B, uint64_t seed,
                                                             uint64_t offset, evx_obs* __restrict__ s,
                                                             evx_obs* __restrict__ s2, int32_t* __restrict__ a,
@@ -730,18 +795,18 @@ __global__ __launch_bounds__(256) void replay_sample_kernel(evx_replay rp, int64
     const int i0 = blockIdx.x * 256 + threadIdx.x;
     if (i0 >= B) return;
     // nets > 1 (evx_replay_sample_agents): agent blockIdx.y's own transitions -- the ring slots
-    // == agent (mod nets) -- into rows [agent B, (agent + 1) B), draws counted agent B + i;
+    // == agent (mod nets) -- into rows [agent B, (agent + 1) B), a permutation keyed by the agent;
     // joint (evx_replay_sample_joint): draw i is shared by every agent (the same env-steps)
     const int g = (int)blockIdx.y;
     const int i = g * B + i0;
-    const uint64_t c = (uint64_t)(joint ? i0 : i) + offset;
-    const u4 q = philox((uint32_t)c, (uint32_t)(c >> 32), 0x5a3b1eu, 0u, (uint32_t)seed, (uint32_t)(seed >> 32));
-    const uint64_t r64 = ((uint64_t)q.x << 32) | q.y;
+    const uint64_t n = nets > 1 ? (uint64_t)(size / nets) : (uint64_t)size;
+    const perm_key pk = make_perm_key(n, seed, offset, joint ? 0u : (uint32_t)g);
+    const uint64_t d = perm_apply(pk, (uint64_t)i0, n);
     int64_t j;
     if (nets > 1) {
-        j = (int64_t)(r64 % (uint64_t)(size / nets)) * nets + g;
+        j = (int64_t)d * nets + g;
     } else {
-        j = base + (int64_t)(r64 % (uint64_t)size);
+        j = base + (int64_t)d;
         if (j >= rp.capacity) j -= rp.capacity;
     }
     s[i] = rp.s[j];
@@ -849,44 +914,47 @@ const char* evx_q_last_error(void) { return q_err; }
 }  // extern "C"
 
 namespace {
-int gemm_launch(const evx_gemm_desc* g, int cm, int cs, void* stream) {
-    const evx_gemm_desc* orig = g;
-    if (!g || !g->A || !g->B || !g->C) return qfail(-22, "gemm: NULL operand");
-    if (g->M <= 0 || g->N <= 0 || g->K <= 0) return 0;
+// K slices of a GEMM (1: no split). Split K only on the bf16 / x3 paths (the exact-f32 path is
+// the parity path and stays one pass). Without an epilogue: grids under 256 tiles with K >= 512
+// (dW = dY^T X). With one (bias / ReLU / mask / gate), when the contraction is long enough to pay
+// for the reduction pass: the conv net's fc1 (K = 15 488) at a learn batch of 1024 is 32 tiles,
+// 1.19 ms unsplit; at the act's 8192 rows 256 tiles, one 4-wave workgroup per CU. Each K slice
+// keeps >= 256 (>= 1024 with an epilogue) of the contraction. The slices' partials go to the
+// caller's workspace (ws, [S][M][N] f32), so S is also capped by ws_elems / (M N).
+int gemm_slices(const evx_gemm_desc* g, int64_t ws_cap, int* klen_out) {
     const int TB = evxq::TB;
     const int tiles = ((g->M + TB - 1) / TB) * ((g->N + TB - 1) / TB);
     const bool epi = g->bias || g->mask || g->gate || (g->flags & EVX_GEMM_RELU);
     int S = 1;
-    // split K only on the bf16 / x3 paths (f32 atomics reorder the sum; the exact-f32 path stays
-    // deterministic). Without an epilogue: grids under 256 tiles with K >= 512 (dW = dY^T X). With
-    // one (bias / ReLU / mask / gate), when the contraction is long enough to pay for a separate
-    // epilogue pass over C: the conv net's fc1 (K = 15 488) at a learn batch of 1024 is 32 tiles,
-    // 1.19 ms unsplit; at the act's 8192 rows 256 tiles, one 4-wave workgroup per CU. Each K slice keeps >= 256 (>= 1024 with an epilogue) of the contraction.
-    const bool accum = (g->flags & EVX_GEMM_ACCUM) != 0;
-    if (g->precision != EVX_PREC_F32 && tiles < (epi ? 257 : 256) && !(epi && accum) && g->K >= (epi ? 4096 : 512)) {
+    if (g->precision != EVX_PREC_F32 && tiles < (epi ? 257 : 256) && g->K >= (epi ? 4096 : 512)) {
         S = ((epi ? 1024 : 512) + tiles - 1) / tiles;
         const int kmin = epi ? 1024 : 256;
         if (S > g->K / kmin) S = g->K / kmin;
         if (S < 1) S = 1;
     }
+    if (S > 1) {
+        const int64_t mn = (int64_t)g->M * g->N;
+        const int64_t fit = ws_cap / mn;
+        if (S > fit) S = (int)fit;
+        if (S < 2) S = 1;
+    }
     int klen = (g->K + S - 1) / S;
     klen = (klen + evxq::BK - 1) / evxq::BK * evxq::BK;
     S = (g->K + klen - 1) / klen;
+    if (klen_out) *klen_out = klen;
+    return S;
+}
+
+int gemm_launch(const evx_gemm_desc* g, int cm, int cs, void* stream) {
+    if (!g || !g->A || !g->B || !g->C) return qfail(-22, "gemm: NULL operand");
+    if (g->M <= 0 || g->N <= 0 || g->K <= 0) return 0;
+    if (g->ws_elems < 0) return qfail(-22, "gemm: ws_elems < 0");
+    const int TB = evxq::TB;
+    int klen = 0;
+    const int S = gemm_slices(g, g->ws ? g->ws_elems : 0, &klen);
     dim3 grid((unsigned)((g->N + TB - 1) / TB), (unsigned)((g->M + TB - 1) / TB), (unsigned)S);
     if (grid.y > 65535u) return qfail(-22, "gemm: M too large for one launch");
-    if (S > 1 && !accum)
-        hipLaunchKernelGGL(evxq::zero_rows_kernel, dim3(nblk((int64_t)g->M * g->N)), dim3(256), 0,
-                           (hipStream_t)stream, g->C, g->M, g->N, g->ldc);
     hipStream_t st = (hipStream_t)stream;
-    // the K slices sum raw products (alpha applied); bias / ReLU / mask / gate follow in one pass
-    evx_gemm_desc gs = *g;
-    if (S > 1 && epi) {
-        gs.bias = nullptr;
-        gs.mask = nullptr;
-        gs.gate = nullptr;
-        gs.flags &= ~EVX_GEMM_RELU;
-    }
-    g = &gs;
     if (cm == evxq::CV_FWD)
         hipLaunchKernelGGL(evxq::gemm128x3_kernel<evxq::CV_FWD>, grid, dim3(256), 0, st, *g, klen, cs);
     else if (cm == evxq::CV_DX)
@@ -899,10 +967,11 @@ int gemm_launch(const evx_gemm_desc* g, int cm, int cs, void* stream) {
         hipLaunchKernelGGL(evxq::gemm128x3_kernel<evxq::CV_NONE>, grid, dim3(256), 0, st, *g, klen, 0);
     else
         hipLaunchKernelGGL(evxq::gemm128_kernel<float>, grid, dim3(256), 0, st, *g, klen);
-    if (S > 1 && epi) {
+    if (S > 1) {  // the slices' partials summed in slice order, then the epilogue
         const int e = qlaunch("gemm");
         if (e) return e;
-        hipLaunchKernelGGL(evxq::gemm_epilogue_kernel, dim3(nblk((int64_t)g->M * g->N)), dim3(256), 0, st, *orig);
+        hipLaunchKernelGGL(evxq::splitk_reduce_kernel, dim3(nblk(((int64_t)g->M * g->N + 3) / 4)), dim3(256), 0, st,
+                           *g, S);
     }
     return qlaunch("gemm");
 }
@@ -911,6 +980,12 @@ int gemm_launch(const evx_gemm_desc* g, int cm, int cs, void* stream) {
 extern "C" {
 
 int evx_gemm(const evx_gemm_desc* g, void* stream) { return gemm_launch(g, evxq::CV_NONE, 0, stream); }
+
+int64_t evx_gemm_ws_elems(const evx_gemm_desc* g) {
+    if (!g || g->M <= 0 || g->N <= 0 || g->K <= 0) return 0;
+    const int S = gemm_slices(g, INT64_MAX, nullptr);
+    return S > 1 ? (int64_t)S * g->M * g->N : 0;
+}
 
 int evx_conv3x3_gemm(const evx_gemm_desc* g, int32_t mode, int32_t cs, void* stream) {
     if (!g) return qfail(-22, "conv3x3: NULL descriptor");
@@ -1043,6 +1118,7 @@ int evx_replay_sample(const evx_replay* rp, int64_t size, int32_t B, uint64_t se
     if (!rp || size <= 0) return qfail(-22, "replay: empty");
     if (B <= 0) return 0;
     if (size > rp->capacity) return qfail(-22, "replay: size > capacity");
+    if (B > size) return qfail(-22, "replay: sample larger than population (random.sample)");
     hipLaunchKernelGGL(evxq::replay_sample_kernel, dim3(nblk(B)), dim3(256), 0, (hipStream_t)stream, *rp, (int64_t)0,
                        size, B, seed, offset, s, s2, a, r, done, idx_out);
     return qlaunch("replay_sample");
@@ -1057,6 +1133,7 @@ int evx_replay_sample_agents(const evx_replay* rp, int64_t size, int32_t B, int3
     if (rp->capacity % nets) return qfail(-22, "replay_sample_agents: capacity must be a multiple of nets");
     if (size < nets || size > rp->capacity || size % nets)
         return qfail(-22, "replay_sample_agents: size must be a positive multiple of nets within the capacity");
+    if (B > size / nets) return qfail(-22, "replay_sample_agents: sample larger than an agent's population");
     hipLaunchKernelGGL(evxq::replay_sample_kernel, dim3(nblk(B), nets), dim3(256), 0, (hipStream_t)stream, *rp, (int64_t)0,
                        size, B, seed, offset, s, s2, a, r, done, nullptr, (int)nets);
     return qlaunch("replay_sample_agents");
@@ -1071,6 +1148,7 @@ int evx_replay_sample_joint(const evx_replay* rp, int64_t size, int32_t B, int32
     if (rp->capacity % nets) return qfail(-22, "replay_sample_joint: capacity must be a multiple of nets");
     if (size < nets || size > rp->capacity || size % nets)
         return qfail(-22, "replay_sample_joint: size must be a positive multiple of nets within the capacity");
+    if (B > size / nets) return qfail(-22, "replay_sample_joint: sample larger than the population");
     hipLaunchKernelGGL(evxq::replay_sample_kernel, dim3(nblk(B), nets), dim3(256), 0, (hipStream_t)stream, *rp, (int64_t)0,
                        size, B, seed, offset, s, s2, a, r, done, nullptr, (int)nets, 1);
     return qlaunch("replay_sample_joint");
@@ -1082,6 +1160,7 @@ int evx_replay_sample_window(const evx_replay* rp, int64_t base, int64_t count, 
     if (!rp || count <= 0) return qfail(-22, "replay: empty window");
     if (count > rp->capacity || base < 0 || base >= rp->capacity) return qfail(-22, "replay: bad window");
     if (B <= 0) return 0;
+    if (B > count) return qfail(-22, "replay: sample larger than the window (random.sample)");
     hipLaunchKernelGGL(evxq::replay_sample_kernel, dim3(nblk(B)), dim3(256), 0, (hipStream_t)stream, *rp, base, count,
                        B, seed, offset, s, s2, a, r, done, idx_out);
     return qlaunch("replay_sample_window");

@@ -37,7 +37,7 @@ class evx_gemm_desc(C.Structure):
                 ("B", C.c_void_p), ("sbk", C.c_int64), ("sbn", C.c_int64),
                 ("C", C.c_void_p), ("ldc", C.c_int64), ("bias", C.c_void_p),
                 ("mask", C.c_void_p), ("ldm", C.c_int64), ("mask_scale", C.c_float),
-                ("gate", C.c_void_p), ("ldg", C.c_int64)]
+                ("gate", C.c_void_p), ("ldg", C.c_int64), ("ws", C.c_void_p), ("ws_elems", C.c_int64)]
 
 
 class evx_adam(C.Structure):
@@ -54,6 +54,8 @@ def qlib():
     if not _q_inited:
         L.evx_q_last_error.restype = C.c_char_p
         L.evx_gemm.argtypes = [C.POINTER(evx_gemm_desc), C.c_void_p]
+        L.evx_gemm_ws_elems.argtypes = [C.POINTER(evx_gemm_desc)]
+        L.evx_gemm_ws_elems.restype = C.c_int64
         L.evx_colsum.argtypes = [C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p,
                                  C.c_int32, C.c_void_p]
         L.evx_td_loss.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_float,
@@ -91,11 +93,36 @@ def _p(t):
     return None if t is None else t.data_ptr()
 
 
+_WS_NEED: Dict[Tuple, int] = {}
+
+
+def _attach_ws(d, ws, tag, device):
+    """Split-K workspace of a descriptor (evx_gemm_ws_elems): ws is a _Workspace (a buffer per
+    tag and size, kept for the pool's life, so a stream never sees another stream's scratch
+    freed under it), a f32 tensor, or None (the GEMM runs in one pass)."""
+    if ws is None:
+        return
+    key = (d.M, d.N, d.K, d.precision, d.flags, bool(d.bias), bool(d.mask), bool(d.gate))
+    need = _WS_NEED.get(key)
+    if need is None:
+        need = _WS_NEED[key] = int(qlib().evx_gemm_ws_elems(C.byref(d)))
+    if need <= 0:
+        return
+    if isinstance(ws, torch.Tensor):
+        if ws.dtype != torch.float32:
+            raise ValueError("gemm workspace must be float32")
+        d.ws, d.ws_elems = ws.data_ptr(), ws.numel()
+        return
+    buf = ws.get(tag + "splitk", (need,), torch.float32, device)
+    d.ws, d.ws_elems = buf.data_ptr(), need
+
+
 def gemm(M, N, K, A, sam, sak, B, sbk, sbn, Cm, ldc, precision="f32", bias=None, relu=False, mask=None,
-         ldm=0, mask_scale=1.0, gate=None, ldg=0, accumulate=False, alpha=1.0):
+         ldm=0, mask_scale=1.0, gate=None, ldg=0, accumulate=False, alpha=1.0, ws=None, tag=""):
     d = evx_gemm_desc(M=M, N=N, K=K, precision=PREC[precision], flags=(RELU if relu else 0) | (ACCUM if accumulate else 0),
                       alpha=alpha, A=_p(A), sam=sam, sak=sak, B=_p(B), sbk=sbk, sbn=sbn, C=_p(Cm), ldc=ldc,
                       bias=_p(bias), mask=_p(mask), ldm=ldm, mask_scale=mask_scale, gate=_p(gate), ldg=ldg)
+    _attach_ws(d, ws, tag, Cm.device)
     qcheck(qlib().evx_gemm(C.byref(d), _stream()), "evx_gemm")
 
 
@@ -103,11 +130,12 @@ CONV_FWD, CONV_DX, CONV_DW = 1, 2, 3
 
 
 def conv_gemm(mode, M, N, K, A, B, Cm, cs, sam=0, sak=0, sbk=0, sbn=0, bias=None, relu=False, gate=None,
-              ldg=0):
+              ldg=0, ws=None, tag=""):
     """evx_conv3x3_gemm (x3): implicit-GEMM 3x3 conv forward / dX / dW on pixel-major activations."""
     d = evx_gemm_desc(M=M, N=N, K=K, precision=PREC["x3"], flags=RELU if relu else 0, alpha=1.0, A=_p(A),
                       sam=sam, sak=sak, B=_p(B), sbk=sbk, sbn=sbn, C=_p(Cm), ldc=N, bias=_p(bias), mask=None,
                       ldm=0, mask_scale=1.0, gate=_p(gate), ldg=ldg)
+    _attach_ws(d, ws, tag, Cm.device)
     qcheck(qlib().evx_conv3x3_gemm(C.byref(d), mode, cs, _stream()), "evx_conv3x3_gemm")
 
 
@@ -225,11 +253,11 @@ class QNet:
         H1 = ws.get(tag + "h1", (B, H), torch.float32, dev)
         gemm(B, H, K0, X, K0, 1, P["fc1.weight"] if w1 is None else w1, 1, K0, H1, H, self.prec, bias=P["fc1.bias"],
              relu=True,
-             mask=mask, ldm=H, mask_scale=1.0 / (1.0 - DROPOUT_P))
+             mask=mask, ldm=H, mask_scale=1.0 / (1.0 - DROPOUT_P), ws=self.ws, tag=tag)
         H2 = ws.get(tag + "h2", (B, H // 2), torch.float32, dev)
-        gemm(B, H // 2, H, H1, H, 1, P["fc2.weight"], 1, H, H2, H // 2, self.prec, bias=P["fc2.bias"], relu=True)
+        gemm(B, H // 2, H, H1, H, 1, P["fc2.weight"], 1, H, H2, H // 2, self.prec, bias=P["fc2.bias"], relu=True, ws=self.ws, tag=tag)
         Q = ws.get(tag + "q", (B, A), torch.float32, dev)
-        gemm(B, A, H // 2, H2, H // 2, 1, P["fc3.weight"], 1, H // 2, Q, A, self.prec, bias=P["fc3.bias"])
+        gemm(B, A, H // 2, H2, H // 2, 1, P["fc3.weight"], 1, H // 2, Q, A, self.prec, bias=P["fc3.bias"], ws=self.ws, tag=tag)
         return H1, H2, Q
 
     def forward(self, x: torch.Tensor, mask: Optional[torch.Tensor], save=True, tag="") -> torch.Tensor:
@@ -251,7 +279,7 @@ class QNet:
             if self.implicit:  # x3: the taps gathered in the GEMM's tile fetch (no im2col buffer)
                 Y = ws.get(tag + f"y{li}", (Mp, cout), torch.float32, dev)
                 conv_gemm(CONV_FWD, Mp, cout, K9, cur, P[cname + ".weight"], Y, C_in, sbk=9, sbn=K9,
-                          bias=P[cname + ".bias"], relu=True)
+                          bias=P[cname + ".bias"], relu=True, ws=self.ws, tag=tag)
                 cols.append(cur)  # the layer input, gathered again by the dW GEMM
                 ys.append(Y)
                 cur, C_in = Y, cout
@@ -260,7 +288,7 @@ class QNet:
             qcheck(L.evx_im2col3x3(_p(cur), B, C_in, 1, _p(col), _stream()), "im2col")
             Y = ws.get(tag + f"y{li}", (Mp, cout), torch.float32, dev)
             gemm(Mp, cout, K9, col, K9, 1, P[cname + ".weight"], 1, K9, Y, cout, self.prec, bias=P[cname + ".bias"],
-                 relu=True)
+                 relu=True, ws=self.ws, tag=tag)
             cols.append(col)
             ys.append(Y)
             cur, C_in = Y, cout
@@ -293,24 +321,24 @@ class QNet:
         # colsum partials: one per 64 rows and column (evx_colsum)
         scratch = ws.get("colsum", (max(1, (max(B * 121, B) + 63) // 64) * max(H, 128),), torch.float32, dev)
         # fc3
-        gemm(A, H // 2, B, dQ, 1, A, H2, H // 2, 1, grads["fc3.weight"], H // 2, pr)
+        gemm(A, H // 2, B, dQ, 1, A, H2, H // 2, 1, grads["fc3.weight"], H // 2, pr, ws=self.ws, tag="bw_")
         colsum(dQ, B, A, grads["fc3.bias"], scratch)
         dZ2 = ws.get("dz2", (B, H // 2), torch.float32, dev)
-        gemm(B, H // 2, A, dQ, A, 1, P["fc3.weight"], H // 2, 1, dZ2, H // 2, pr, gate=H2, ldg=H // 2)
+        gemm(B, H // 2, A, dQ, A, 1, P["fc3.weight"], H // 2, 1, dZ2, H // 2, pr, gate=H2, ldg=H // 2, ws=self.ws, tag="bw_")
         # fc2
-        gemm(H // 2, H, B, dZ2, 1, H // 2, H1, H, 1, grads["fc2.weight"], H, pr)
+        gemm(H // 2, H, B, dZ2, 1, H // 2, H1, H, 1, grads["fc2.weight"], H, pr, ws=self.ws, tag="bw_")
         colsum(dZ2, B, H // 2, grads["fc2.bias"], scratch)
         dZ1 = ws.get("dz1", (B, H), torch.float32, dev)
         gemm(B, H, H // 2, dZ2, H // 2, 1, P["fc2.weight"], H, 1, dZ1, H, pr, mask=mask, ldm=H,
-             mask_scale=1.0 / (1.0 - DROPOUT_P), gate=H1, ldg=H)
+             mask_scale=1.0 / (1.0 - DROPOUT_P), gate=H1, ldg=H, ws=self.ws, tag="bw_")
         # fc1
         L = qlib()
         W1p = s.get("w1p")
         if W1p is None:
-            gemm(H, K0, B, dZ1, 1, H, X, K0, 1, grads["fc1.weight"], K0, pr)
+            gemm(H, K0, B, dZ1, 1, H, X, K0, 1, grads["fc1.weight"], K0, pr, ws=self.ws, tag="bw_")
         else:  # X is pixel-major: dW1 in that column order, then back to the reference's
             dW1p = ws.get("dw1p", (H, K0), torch.float32, dev)
-            gemm(H, K0, B, dZ1, 1, H, X, K0, 1, dW1p, K0, pr)
+            gemm(H, K0, B, dZ1, 1, H, X, K0, 1, dW1p, K0, pr, ws=self.ws, tag="bw_")
             qcheck(L.evx_pix_nchw(_p(dW1p), H, 128, 1, _p(grads["fc1.weight"]), _stream()), "pix_nchw")
         colsum(dZ1, B, H, grads["fc1.bias"], scratch)
         if self.kind == "mlp":
@@ -318,31 +346,31 @@ class QNet:
         Mp = B * 121
         dY = ws.get("dy2", (Mp, 128), torch.float32, dev)
         if W1p is not None:  # dF in pixel order is conv3's dY
-            gemm(B, K0, H, dZ1, H, 1, W1p, K0, 1, dY.view(B, K0), K0, pr, gate=X, ldg=K0)
+            gemm(B, K0, H, dZ1, H, 1, W1p, K0, 1, dY.view(B, K0), K0, pr, gate=X, ldg=K0, ws=self.ws, tag="bw_")
         else:
             dF = ws.get("dflat", (B, K0), torch.float32, dev)
-            gemm(B, K0, H, dZ1, H, 1, P["fc1.weight"], K0, 1, dF, K0, pr, gate=X, ldg=K0)  # gate: relu(conv3) > 0
+            gemm(B, K0, H, dZ1, H, 1, P["fc1.weight"], K0, 1, dF, K0, pr, gate=X, ldg=K0, ws=self.ws, tag="bw_")  # gate: relu(conv3) > 0
             qcheck(L.evx_pix_nchw(_p(dF), B, 128, 0, _p(dY), _stream()), "pix_nchw")
         cols, ys = s["cols"], s["ys"]
         for li, (cname, cin, cout) in reversed(list(enumerate([("conv1", 6, 32), ("conv2", 32, 64),
                                                                 ("conv3", 64, 128)]))):
             K9 = cin * 9
             if self.implicit:  # cols[li] is the layer input [Mp][cin]
-                conv_gemm(CONV_DW, cout, K9, Mp, dY, cols[li], grads[cname + ".weight"], cin, sam=1, sak=cout)
+                conv_gemm(CONV_DW, cout, K9, Mp, dY, cols[li], grads[cname + ".weight"], cin, sam=1, sak=cout, ws=self.ws, tag="bw_")
                 colsum(dY, Mp, cout, grads[cname + ".bias"], scratch)
                 if li == 0:
                     break
                 dYp = ws.get(f"dyp{li}", (Mp, cin), torch.float32, dev)
                 conv_gemm(CONV_DX, Mp, cin, cout * 9, dY, P[cname + ".weight"], dYp, cout, sbk=K9, sbn=9,
-                          gate=ys[li - 1], ldg=cin)
+                          gate=ys[li - 1], ldg=cin, ws=self.ws, tag="bw_")
                 dY = dYp
                 continue
-            gemm(cout, K9, Mp, dY, 1, cout, cols[li], K9, 1, grads[cname + ".weight"], K9, pr)
+            gemm(cout, K9, Mp, dY, 1, cout, cols[li], K9, 1, grads[cname + ".weight"], K9, pr, ws=self.ws, tag="bw_")
             colsum(dY, Mp, cout, grads[cname + ".bias"], scratch)
             if li == 0:
                 break
             dcol = ws.get(f"dcol{li}", (Mp, K9), torch.float32, dev)
-            gemm(Mp, K9, cout, dY, cout, 1, P[cname + ".weight"], K9, 1, dcol, K9, pr)
+            gemm(Mp, K9, cout, dY, cout, 1, P[cname + ".weight"], K9, 1, dcol, K9, pr, ws=self.ws, tag="bw_")
             dx = ws.get(f"dx{li}", (B, cin * 121), torch.float32, dev)
             qcheck(L.evx_col2im3x3(_p(dcol), B, cin, _p(dx), _stream()), "col2im")
             dYp = ws.get(f"dyp{li}", (Mp, cin), torch.float32, dev)

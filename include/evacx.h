@@ -169,10 +169,13 @@ const char *evx_last_error(void);
  * B(k,n) = B[k*sbk + n*sbn], C[m*ldc + n]; epilogue order: bias, ReLU, dropout mask
  * (mask[m*ldm+n] ? v*mask_scale : 0), ReLU-backward gate (gate[m*ldg+n] > 0 ? v : 0),
  * accumulate. Covers nn.Linear forward (A x W^T), its dX (dY W) and dW (dY^T X).
- * BF16 / X3 GEMMs with fewer than 256 128x128 tiles and a long K are split over K: the slices
- * add into C with f32 atomics (summation order not fixed between calls; EVX_PREC_F32 never
- * splits), and with an epilogue C is first the raw sum, then rewritten by an epilogue pass on
- * the same stream. ACCUM with an epilogue is never split. */
+ * BF16 / X3 GEMMs with a long K and few 128x128 tiles (fewer than 256 without an epilogue, at
+ * most 256 with one) may be split over K when the caller passes a workspace: each K slice
+ * stores its raw partial into ws[z][M][N] and a second launch on the same stream adds the
+ * slices in slice order and applies the epilogue (deterministic: the same bits on every call).
+ * The slice count is capped by ws_elems / (M*N); ws = NULL runs the GEMM in one pass.
+ * evx_gemm_ws_elems gives the workspace a descriptor's full split uses (0: never split).
+ * EVX_PREC_F32 never splits. */
 typedef struct {
     int32_t M, N, K;
     int32_t precision;         /* EVX_PREC_* */
@@ -184,6 +187,7 @@ typedef struct {
     const float *bias;         /* [N] or NULL */
     const uint8_t *mask; int64_t ldm; float mask_scale;  /* or NULL */
     const float *gate; int64_t ldg;                        /* or NULL */
+    float *ws; int64_t ws_elems;  /* split-K workspace (f32 elements) or NULL */
 } evx_gemm_desc;
 
 typedef struct {
@@ -201,6 +205,7 @@ typedef struct {
 } evx_replay;
 
 int evx_gemm(const evx_gemm_desc *g, void *stream);
+int64_t evx_gemm_ws_elems(const evx_gemm_desc *g);
 /* Implicit-GEMM 3x3 convolution, padding 1, on 11x11 maps (DQNNetwork conv1-3,
  * agents/dqn_agent.py:22-24,48-50, in place of im2col + evx_gemm; x3 precision only). The
  * activations are pixel-major [B*121][cs]; the operand they feed is gathered in the tile fetch:

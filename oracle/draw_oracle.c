@@ -38,23 +38,6 @@ void orc_epsilon_greedy(const float *Q, int n, int A, float epsilon, uint64_t se
     }
 }
 
-/* sample i: ring slot base + (x << 32 | y) mod size (wrapped at capacity), Philox(ctr = (i + offset)
- * lo, hi, 0x5a3b1e, 0; key = seed) -- uniform with replacement over the window [base, base + size) */
-void orc_replay_indices(int64_t base, int64_t size, int64_t capacity, int B, uint64_t seed, uint64_t offset,
-                        int64_t *idx) {
-    for (int i = 0; i < B; i++) {
-        const uint64_t c = (uint64_t)i + offset;
-        const uint32_t ctr[4] = {(uint32_t)c, (uint32_t)(c >> 32), 0x5a3b1eu, 0u};
-        const uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
-        uint32_t q[4];
-        orc_philox4x32_10(ctr, key, q);
-        const uint64_t r64 = ((uint64_t)q[0] << 32) | q[1];
-        int64_t j = base + (int64_t)(r64 % (uint64_t)size);
-        if (j >= capacity) j -= capacity;
-        idx[i] = j;
-    }
-}
-
 static uint32_t fmix32(uint32_t h) {
     h ^= h >> 16;
     h *= 0x85ebca6bu;
@@ -62,6 +45,41 @@ static uint32_t fmix32(uint32_t h) {
     h *= 0xc2b2ae35u;
     h ^= h >> 16;
     return h;
+}
+
+/* sample i WITHOUT replacement (DQNAgent.learn's random.sample, agents/dqn_agent.py:132): ring slot
+ * base + perm(i) (wrapped at capacity) for a keyed permutation perm of [0, size): a 6-round balanced
+ * Feistel network on the smallest even width 2^w >= size, cycle-walked into [0, size). Round keys
+ * k[r] = fmix32(q[r & 3] + r * 0x9e3779b9) from q = Philox(ctr = offset lo, hi, 0x5a3b1e, stream;
+ * key = seed); round: (L, R) -> (R, L ^ (fmix32(R ^ k[r]) & mask)). stream: the agent of a
+ * per-agent memory (evx_replay_sample_agents), else 0. */
+void orc_replay_indices(int64_t base, int64_t size, int64_t capacity, int B, uint64_t seed, uint64_t offset,
+                        uint32_t stream, int64_t *idx) {
+    const uint32_t ctr[4] = {(uint32_t)offset, (uint32_t)(offset >> 32), 0x5a3b1eu, stream};
+    const uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    uint32_t q[4], k[6];
+    orc_philox4x32_10(ctr, key, q);
+    for (int r = 0; r < 6; r++) k[r] = fmix32(q[r & 3] + (uint32_t)r * 0x9e3779b9u);
+    int w = 2;
+    while (w < 62 && (1ull << w) < (uint64_t)size) w += 2;
+    const int half = w / 2;
+    const uint64_t hmask = (1ull << half) - 1;
+    for (int i = 0; i < B; i++) {
+        uint64_t x = (uint64_t)i;
+        do {
+            uint64_t L = x >> half, R = x & hmask;
+            for (int r = 0; r < 6; r++) {
+                const uint64_t F = (uint64_t)fmix32((uint32_t)R ^ k[r]) & hmask;
+                const uint64_t t = R;
+                R = L ^ F;
+                L = t;
+            }
+            x = (L << half) | R;
+        } while (x >= (uint64_t)size);
+        int64_t j = base + (int64_t)x;
+        if (j >= capacity) j -= capacity;
+        idx[i] = j;
+    }
 }
 
 /* keep[r][c] of the fused MLP's dropout: one fmix32 hash per (row pair, column), low 16 bits

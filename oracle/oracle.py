@@ -267,13 +267,14 @@ def epsilon_greedy(Q, epsilon, seed, offset):
     return out
 
 
-def replay_indices(base, size, capacity, B, seed, offset):
-    """evx_replay_sample(_window)'s ring slots restated: int64 [B]."""
+def replay_indices(base, size, capacity, B, seed, offset, stream=0):
+    """evx_replay_sample(_window / _agents)'s ring slots restated (without replacement): int64 [B]."""
     idx = np.zeros(B, np.int64)
     L = lib()
-    L.orc_replay_indices.argtypes = [C.c_int64, C.c_int64, C.c_int64, C.c_int, C.c_uint64, C.c_uint64, C.c_void_p]
+    L.orc_replay_indices.argtypes = [C.c_int64, C.c_int64, C.c_int64, C.c_int, C.c_uint64, C.c_uint64, C.c_uint32,
+                                     C.c_void_p]
     L.orc_replay_indices(int(base), int(size), int(capacity), int(B), int(seed) & (2**64 - 1),
-                         int(offset) & (2**64 - 1), _p(idx))
+                         int(offset) & (2**64 - 1), int(stream) & 0xFFFFFFFF, _p(idx))
     return idx
 
 

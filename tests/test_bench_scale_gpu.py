@@ -1,0 +1,194 @@
+"""Parity of the kernels at the sizes bench.py times them (VERDICT r2 "Next round" 1).
+
+The kernel variant a launch picks depends on its size, so parity at small E / small B
+says nothing about the variant the bench runs:
+
+* env.step: at E >= 32 x CUs (8192 on MI355X) evx_env_step picks one-wave workgroups
+  (env_step_kernel<1, ...>, csrc/env_step.hip: evx_env_step_part), for cfg4's 256x256
+  grid the big-grid instantiation <1, false, true>. cfg4 (256x256, P 9102, R 1, 8192 envs)
+  and cfg5 (128x128, P 2276, R 32, 8192 envs) are prepared as bench.py prepares them
+  (env-only steps, env g force-reset at step g % stagger: ages spread over an episode,
+  fused auto-resets), then envs spread over the age mix are snapshotted into the oracle
+  (oracle/evac_oracle.c, pinned by the reference's trajectories) and both step with the
+  same actions: every state field, both MT19937 streams, reward, done and observation
+  (terminal ones through obs_term) bit-exact on every step.
+  Reference: envs/people.py:196-314, envs/evacuation_env.py:84-288.
+
+* learn: the x3 learn chain at the bench's batches picks qfc1_kernel<4,1,8,true> (B >=
+  24576) and multi-tile qdz1 workgroups (8 tiles at B = 32768, 2 at 8192;
+  csrc/qmlp.hip: qdz1_tiles_per_wg, launch_fwd). One DQNAgent.learn step
+  (agents/dqn_agent.py:126-168) from compact observations of a 128x128 R16 env, explicit
+  dropout keep masks, against torch fp32 autograd + clip_grad_norm_ + Adam on the expanded
+  observations -- the same restatement tests/test_dqn_golden_cpu.py pins to the reference's
+  own dqn_learn.npz. Tolerances are the x3 path's (tests/test_qmlp_x3_gpu.py): loss and
+  norm rtol 2e-4, gradients rtol 2e-3 with atol 1e-5 of the tensor's max, Adam parameters
+  within 2e-3 of lr-scale and at most 0.1 % beyond 1e-5.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _prepare_like_bench(env, E, R, age_steps, stagger, seed=4321):
+    """bench.py's --phase stationary preparation (uniform random actions, staggered resets)."""
+    gid = torch.arange(E, device="cuda")
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    acts = torch.empty(E * R, device="cuda", dtype=torch.int32)
+    for w in range(age_steps):
+        torch.randint(0, 5, (E * R,), device="cuda", dtype=torch.int32, generator=g, out=acts)
+        env.step(acts, auto_reset=True)
+        if w < stagger:
+            env.reset(mask=(gid % stagger == w) & ~env.done.bool())
+
+
+def _bench_mix_parity(L, P, R, E, age_steps, stagger, n_snap, steps, min_age_span):
+    from evacx.env import DeviceLayout, VecEnv
+    from evacx.layout import build_tables, synthetic
+    from oracle import oracle as orc
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    assert E >= 32 * ncu, "the test must reach the one-wave-workgroup launch the bench runs"
+    tables = build_tables(synthetic(L, L, R))
+    lay = DeviceLayout(tables, P)
+    env = VecEnv(lay, E)
+    env.seed([1234 + i for i in range(E)])
+    env.reset()
+    _prepare_like_bench(env, E, R, age_steps, stagger)
+    ids = list(range(0, E, E // n_snap))[:n_snap]
+    olay = orc.Layout.from_tables(tables, P)
+    oenvs = []
+    for st in env.host_states(ids):
+        oe = orc.Env(olay, thmap=False)
+        oe.load_state(st)
+        oenvs.append(oe)
+    ages = np.array([oe.scal[1] for oe in oenvs])
+    assert ages.max() - ages.min() >= min_age_span, ages  # the sample spans the episode-age mix
+    rng = np.random.RandomState(11)
+    n_done = 0
+    idt = torch.tensor(ids, device="cuda")
+    for s in range(steps):
+        a = rng.randint(0, 5, size=(E, R)).astype(np.int32)
+        a[rng.rand(E, R) < 0.02] = 7  # invalid actions: silent no-ops (envs/map.py:180-181)
+        env.step(torch.from_numpy(a.reshape(-1)).cuda(), auto_reset=True)
+        rew = env.reward[ids].cpu().numpy()
+        dn = env.done[ids].cpu().numpy()
+        ob = env.expand_obs(torch.float64, env.obs.view(E, -1)[idt].reshape(-1)).cpu().numpy()
+        term = env.expand_obs(torch.float64, env.obs_term.view(E, -1)[idt].reshape(-1)).cpu().numpy() \
+            if dn.any() else None
+        sts = env.host_states(ids)
+        for j, (e, oe) in enumerate(zip(ids, oenvs)):
+            oobs, r, d = oe.step(a[e])
+            assert rew[j] == r and bool(dn[j]) == d, (s, e, rew[j], r)
+            if d:
+                assert np.array_equal(term[j], oobs), (s, e, "terminal obs")
+                oobs = oe.reset()
+                n_done += 1
+            assert np.array_equal(ob[j], oobs), (s, e, "obs")
+            st = sts[j]
+            for k in ["pos", "flags", "health", "acc", "rmap", "robots", "view", "scal", "py_mt", "np_mt"]:
+                assert np.array_equal(st[k], getattr(oe, k)), (s, e, k)
+    env.check_err()
+    return ages, n_done
+
+
+def test_cfg4_env_at_bench_scale():
+    """cfg4: 256x256, P 9102, R 1, 8192 envs (env_step_kernel<1, false, true>), prepared as the
+    cfg4 bench line (--age-steps 300 --stagger 300); 32 envs x 40 steps vs the oracle."""
+    _need_gpu()
+    ages, _ = _bench_mix_parity(L=256, P=9102, R=1, E=8192, age_steps=300, stagger=300, n_snap=32, steps=40,
+                                min_age_span=200)
+    print(f"cfg4 bench mix: ages {ages.min()}..{ages.max()}")
+
+
+def test_cfg5_env_at_bench_scale():
+    """cfg5: 128x128, P 2276, R 32, 8192 envs (env_step_kernel<1, false>), prepared as the bench
+    (--age-steps 1300 --stagger 1200); 48 envs x 50 steps vs the oracle."""
+    _need_gpu()
+    ages, n_done = _bench_mix_parity(L=128, P=2276, R=32, E=8192, age_steps=1300, stagger=1200, n_snap=48,
+                                     steps=50, min_age_span=600)
+    print(f"cfg5 bench mix: ages {ages.min()}..{ages.max()}, resets {n_done}")
+
+
+# ------------------------------------------------------------------------- learn
+def _torch_q(sd, X, mask):
+    h = F.relu(F.linear(X, sd["fc1.weight"], sd["fc1.bias"]))
+    if mask is not None:
+        h = h * mask.float() / 0.8
+    h = F.relu(F.linear(h, sd["fc2.weight"], sd["fc2.bias"]))
+    return F.linear(h, sd["fc3.weight"], sd["fc3.bias"])
+
+
+@pytest.mark.parametrize("B", [8192, 32768])
+def test_x3_learn_at_bench_batch(B):
+    """Two learn steps (each from the same parameters and Adam moments on both sides) at the
+    bench's learn batch: cfg5's 8192 (2-tile qdz1) and cfg3's 32768 (qfc1<4,1,8,true>, 8-tile
+    qdz1). Observations: a 128x128 R16 env 40 steps into its episode (fire spreading, people
+    moving), sampled without replacement into s and s'."""
+    _need_gpu()
+    from evacx.env import DeviceLayout, VecEnv
+    from evacx.layout import build_tables, synthetic
+    from evacx.qmlp import HID, K1
+    from evacx.qnet import Learner
+    R, P = 16, 2276
+    E = 2 * B // R
+    lay = DeviceLayout(build_tables(synthetic(128, 128, R)), P)
+    env = VecEnv(lay, E)
+    env.seed([500 + i for i in range(E)])
+    env.reset()
+    g = torch.Generator(device="cuda").manual_seed(1)
+    for _ in range(40):
+        env.step(torch.randint(0, 5, (E * R,), device="cuda", dtype=torch.int32, generator=g), auto_reset=True)
+    torch.cuda.synchronize()
+    dev = "cuda"
+    lr = Learner(kind="mlp", precision="f32", seed=41, lr=1e-3)
+    assert lr.fast is not None and lr.fast.x3 and lr.fused_opt  # the trainer's chain
+    sd0 = {k: v.clone() for k, v in lr.online.state_dict().items()}
+    params = {k: torch.nn.Parameter(v.clone()) for k, v in sd0.items()}
+    tgt = {k: v.clone() for k, v in sd0.items()}
+    opt = torch.optim.Adam(params.values(), lr=1e-3)
+    gh = torch.Generator().manual_seed(B)
+    obs = env.obs.view(-1, 8)
+    for it in range(2):
+        if it > 0:
+            lr.online.load_state_dict({k: p.detach() for k, p in params.items()})
+            lr.fast.repack()
+            for key, buf in (("exp_avg", lr.m), ("exp_avg_sq", lr.v)):
+                buf.copy_(torch.cat([opt.state[p][key].reshape(-1) for p in params.values()]))
+        perm = torch.randperm(E * R, generator=gh)
+        s_obs = obs[perm[:B].to(dev)].contiguous().view(-1)
+        s2_obs = obs[perm[B:2 * B].to(dev)].contiguous().view(-1)
+        a = torch.randint(0, 5, (B,), generator=gh, dtype=torch.int32).to(dev)
+        r = (torch.randn(B, generator=gh) * 30).to(dev)
+        d = (torch.rand(B, generator=gh) < 0.05).to(torch.uint8).to(dev)
+        m1 = (torch.rand(B, HID, generator=gh) >= 0.2).to(torch.uint8).to(dev)
+        m2 = (torch.rand(B, HID, generator=gh) >= 0.2).to(torch.uint8).to(dev)
+        loss = lr.learn_obs(lay.c, s_obs, a, r, d, s2_obs, B, mask_online=m1, mask_target=m2)
+        X = env.expand_obs(torch.float32, s_obs).reshape(B, K1)
+        X2 = env.expand_obs(torch.float32, s2_obs).reshape(B, K1)
+        q = _torch_q(params, X, m1).gather(1, a.long().unsqueeze(1))
+        with torch.no_grad():
+            y = r + 0.99 * _torch_q(tgt, X2, m2).max(1)[0] * (~d.bool())
+        ref_loss = F.mse_loss(q.squeeze(), y)
+        opt.zero_grad()
+        ref_loss.backward()
+        gnorm = torch.nn.utils.clip_grad_norm_(params.values(), 1.0)
+        grads_ref = {k: p.grad.clone() for k, p in params.items()}
+        opt.step()
+        torch.cuda.synchronize()
+        assert abs(loss.item() - ref_loss.item()) <= 2e-4 * abs(ref_loss.item()) + 1e-5, (it, loss.item(),
+                                                                                         ref_loss.item())
+        assert abs(lr.norm.item() - gnorm.item()) <= 2e-4 * gnorm.item() + 1e-6, (it, lr.norm.item(), gnorm.item())
+        for k in params:
+            ref = grads_ref[k]
+            torch.testing.assert_close(lr.grads[k], ref, rtol=2e-3, atol=1e-5 * ref.abs().max().item() + 1e-9,
+                                       msg=lambda m: f"B={B} step {it} grad {k}: {m}")
+            diff = (lr.online[k] - params[k].detach()).abs()
+            assert (diff > 1e-5).float().mean().item() <= 1e-3, (it, k, diff.max().item())
+            assert diff.max().item() <= 2e-3, (it, k, diff.max().item())

@@ -62,7 +62,8 @@ def test_replay_sampling_matches_restatement(window):
     from evacx.trainer import Replay
     import ctypes as C
     from evacx import _lib
-    cap, B = 4096, 5000
+    cap = 4096
+    B = 4096 if window is None else min(1500, window[1])  # random.sample: B <= population
     rp = Replay(cap, "cuda")
     g = torch.Generator(device="cuda").manual_seed(2)
     rp.s.copy_(torch.randint(-2**31, 2**31 - 1, rp.s.shape, device="cuda", generator=g, dtype=torch.int32))
@@ -93,22 +94,27 @@ def test_replay_sampling_matches_restatement(window):
     torch.cuda.synchronize()
     ref = orc.replay_indices(base, size, cap, B, 17, 4096)
     assert np.array_equal(idx.cpu().numpy(), ref)
+    assert len(np.unique(ref)) == B  # without replacement
     j = torch.from_numpy(ref).cuda()
     assert torch.equal(out["a"], rp.a[j]) and torch.equal(out["r"], rp.r[j]) and torch.equal(out["done"], rp.done[j])
     assert torch.equal(out["s"].view(B, OBS_WORDS), rp.s.view(cap, OBS_WORDS)[j])
     assert torch.equal(out["s2"].view(B, OBS_WORDS), rp.s2.view(cap, OBS_WORDS)[j])
+    if window is None:  # random.sample raises for a sample larger than the population
+        assert L.evx_replay_sample(C.byref(rp.c), cap, cap + 1, 17, 0, out["s"].data_ptr(), out["s2"].data_ptr(),
+                                   out["a"].data_ptr(), out["r"].data_ptr(), out["done"].data_ptr(), None,
+                                   None) != 0
 
 
 def test_per_agent_replay_sampling_matches_restatement():
     """evx_replay_sample_agents (one memory per robot): agent g's draws are the uniform
-    sampler's restated draws (counters offset + g B + i) over its own slots (== g mod nets)."""
+    sampler's restated draws (the permutation keyed by stream g) over its own slots (== g mod nets)."""
     _need_gpu()
     from evacx.env import OBS_WORDS
     from evacx.qnet import qcheck
     from evacx.trainer import Replay
     import ctypes as C
     from evacx import _lib
-    cap, nets, B, size = 4096, 8, 600, 3000 // 8 * 8
+    cap, nets, B, size = 4096, 8, 300, 3000 // 8 * 8
     rp = Replay(cap, "cuda")
     rp.a.copy_(torch.arange(cap, device="cuda", dtype=torch.int32))
     rp.s.copy_(torch.arange(cap * OBS_WORDS, device="cuda", dtype=torch.int32))
@@ -125,7 +131,7 @@ def test_per_agent_replay_sampling_matches_restatement():
     torch.cuda.synchronize()
     a = out["a"].cpu().numpy().reshape(nets, B)
     for g in range(nets):
-        ref = orc.replay_indices(0, size // nets, 1 << 40, B, 17, 4096 + g * B) * nets + g
+        ref = orc.replay_indices(0, size // nets, 1 << 40, B, 17, 4096, stream=g) * nets + g
         assert np.array_equal(a[g], ref), g
     assert torch.equal(out["s"].view(nets * B, OBS_WORDS), rp.s.view(cap, OBS_WORDS)[out["a"].long()])
     assert a.max() < size

@@ -198,3 +198,36 @@ def test_conv3x3_implicit_gemm_vs_torch(cin, cout, B):
     for got, ref in ((y, yref), (dx, dxref), (dw, dwref)):
         ref = ref.detach().float()
         torch.testing.assert_close(got.cpu(), ref, rtol=1e-4, atol=2e-5 * ref.abs().max().item())
+
+
+def test_conv_x3_act_and_learn_are_deterministic():
+    """The conv Q-net in x3 at the cfg4 act's 8192 rows splits fc1 over K (256 tiles) and its
+    learn splits the weight gradients: the K slices are summed in slice order (evx_gemm's
+    workspace, splitk_reduce_kernel), so two act calls give the same Q bits, and two learners
+    from the same state on the same batch give the same gradients and parameters (ADVICE r2:
+    f32 atomics made cfg4's act -- and so its trajectories -- vary between same-seed runs).
+    Also against torch fp32 (rtol 2e-4 / atol 2e-5 as test_forward_f32_matches_torch)."""
+    _need_gpu()
+    from evacx.qnet import Learner
+    B = 8192
+    g = torch.Generator(device="cuda").manual_seed(8)
+    x = (torch.rand(B, 11, 11, 6, device="cuda", generator=g) < 0.3).float()
+    x[..., 2] = torch.rand(B, 11, 11, device="cuda", generator=g) * 0.8
+    mask = (torch.rand(B, 512, device="cuda", generator=g) >= 0.2).to(torch.uint8)
+    lr = Learner(kind="conv", precision="x3", seed=5)
+    q1 = lr.q_values(x, train=True, mask=mask).clone()
+    q2 = lr.q_values(x, train=True, mask=mask).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(q1, q2)
+    sd = lr.online.state_dict()
+    ref = torch_forward("conv", sd, x, mask)
+    torch.testing.assert_close(q1, ref, rtol=2e-4, atol=2e-5)
+    xb, x2b, a, r, d, m1, m2 = [t.cuda() for t in make_batch(1024, 4)]
+    runs = []
+    for _ in range(2):
+        lrn = Learner(kind="conv", precision="x3", seed=5)
+        loss = lrn.learn(xb, a, r, d, x2b, mask_online=m1, mask_target=m2)
+        torch.cuda.synchronize()
+        runs.append((loss.item(), lrn.grads.flat.clone(), lrn.online.flat.clone()))
+    assert runs[0][0] == runs[1][0]
+    assert torch.equal(runs[0][1], runs[1][1]) and torch.equal(runs[0][2], runs[1][2])
