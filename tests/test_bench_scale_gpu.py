@@ -125,16 +125,36 @@ def _torch_q(sd, X, mask):
     return F.linear(h, sd["fc3.weight"], sd["fc3.bias"])
 
 
+def _torch_q_gated(sd, X, g1, g2):
+    """The same network with the ReLU/dropout pattern given (g1: keep AND fc1 > 0, g2: fc2 > 0) --
+    the device's own pattern, so autograd walks the branches the device's backward walked."""
+    z1 = F.linear(X, sd["fc1.weight"], sd["fc1.bias"])
+    h1 = z1 * g1 / 0.8
+    z2 = F.linear(h1, sd["fc2.weight"], sd["fc2.bias"])
+    return F.linear(z2 * g2, sd["fc3.weight"], sd["fc3.bias"]), z1, z2
+
+
 @pytest.mark.parametrize("B", [8192, 32768])
 def test_x3_learn_at_bench_batch(B):
     """Two learn steps (each from the same parameters and Adam moments on both sides) at the
     bench's learn batch: cfg5's 8192 (2-tile qdz1) and cfg3's 32768 (qfc1<4,1,8,true>, 8-tile
     qdz1). Observations: a 128x128 R16 env 40 steps into its episode (fire spreading, people
-    moving), sampled without replacement into s and s'."""
+    moving), sampled without replacement into s and s'.
+
+    ReLU branches. x3 products are ~2^-17 off, so a pre-activation within that of 0 can take
+    the other ReLU branch than fp32 torch; at these batches (16.8 M fc1 and 8.4 M fc2
+    activations at B = 32768) a few do, and each moves its row's whole contribution to the
+    gradients (tools/learn_diag.py: up to 1e-2 of max |grad| in db1 and the occupancy columns).
+    So (1) every activation whose branch differs from torch's must have a torch pre-activation
+    within 1e-4 of the layer's max |z| (the x3 rounding of 0), and at most 1e-5 of them may
+    differ; (2) the gradients, norm and Adam update are compared with the tests' x3 tolerances
+    against torch autograd through the DEVICE's branch pattern (read from the saved H1 / H2), so
+    the arithmetic is checked to 2e-3 / 1e-5 of max |grad|; (3) against plain torch the loss
+    (rtol 2e-4) and the norm (rtol 1e-3)."""
     _need_gpu()
     from evacx.env import DeviceLayout, VecEnv
     from evacx.layout import build_tables, synthetic
-    from evacx.qmlp import HID, K1
+    from evacx.qmlp import HID, HID2, K1
     from evacx.qnet import Learner
     R, P = 16, 2276
     E = 2 * B // R
@@ -155,6 +175,7 @@ def test_x3_learn_at_bench_batch(B):
     opt = torch.optim.Adam(params.values(), lr=1e-3)
     gh = torch.Generator().manual_seed(B)
     obs = env.obs.view(-1, 8)
+    n_flips = 0
     for it in range(2):
         if it > 0:
             lr.online.load_state_dict({k: p.detach() for k, p in params.items()})
@@ -170,12 +191,35 @@ def test_x3_learn_at_bench_batch(B):
         m1 = (torch.rand(B, HID, generator=gh) >= 0.2).to(torch.uint8).to(dev)
         m2 = (torch.rand(B, HID, generator=gh) >= 0.2).to(torch.uint8).to(dev)
         loss = lr.learn_obs(lay.c, s_obs, a, r, d, s2_obs, B, mask_online=m1, mask_target=m2)
+        torch.cuda.synchronize()
+        # the device's branch pattern, from the forward it saved for the backward
+        h1 = lr.net.ws.get("fh1", (2 * B * HID,), torch.int16, torch.device(dev)).view(torch.bfloat16)
+        h1 = h1.view(2, B, HID).float().sum(0)
+        h2 = lr.net.ws.get("fh2", (B, HID2), torch.float32, torch.device(dev))
+        g1, g2 = (h1 > 0).float(), (h2 > 0).float()
         X = env.expand_obs(torch.float32, s_obs).reshape(B, K1)
         X2 = env.expand_obs(torch.float32, s2_obs).reshape(B, K1)
-        q = _torch_q(params, X, m1).gather(1, a.long().unsqueeze(1))
         with torch.no_grad():
             y = r + 0.99 * _torch_q(tgt, X2, m2).max(1)[0] * (~d.bool())
-        ref_loss = F.mse_loss(q.squeeze(), y)
+            # (3) plain torch: loss and norm
+            plain = {k: p.detach().clone().requires_grad_(True) for k, p in params.items()}
+        q_plain = _torch_q(plain, X, m1).gather(1, a.long().unsqueeze(1))
+        F.mse_loss(q_plain.squeeze(), y).backward()
+        plain_norm = torch.sqrt(sum((p.grad.double() ** 2).sum() for p in plain.values())).item()
+        # (1) the branches that differ are x3 roundings of 0
+        qg, z1, _ = _torch_q_gated(params, X, g1, g2)
+        with torch.no_grad():
+            z2p = F.linear(F.relu(z1) * m1.float() / 0.8, params["fc2.weight"], params["fc2.bias"])  # torch's fc2
+            f1, f2 = ((z1 > 0) & m1.bool()) != g1.bool(), (z2p > 0) != g2.bool()
+            n_flips += int(f1.sum()) + int(f2.sum())
+            assert int(f1.sum()) <= 1e-5 * f1.numel() and int(f2.sum()) <= 1e-5 * f2.numel(), (int(f1.sum()),
+                                                                                              int(f2.sum()))
+            if f1.any():
+                assert z1[f1].abs().max().item() <= 1e-4 * z1.abs().max().item()
+            if f2.any():
+                assert z2p[f2].abs().max().item() <= 1e-4 * z2p.abs().max().item()
+        # (2) gradients / norm / Adam through the device's branches
+        ref_loss = F.mse_loss(qg.gather(1, a.long().unsqueeze(1)).squeeze(), y)
         opt.zero_grad()
         ref_loss.backward()
         gnorm = torch.nn.utils.clip_grad_norm_(params.values(), 1.0)
@@ -184,7 +228,9 @@ def test_x3_learn_at_bench_batch(B):
         torch.cuda.synchronize()
         assert abs(loss.item() - ref_loss.item()) <= 2e-4 * abs(ref_loss.item()) + 1e-5, (it, loss.item(),
                                                                                          ref_loss.item())
+        assert abs(loss.item() - F.mse_loss(q_plain.squeeze(), y).item()) <= 2e-4 * abs(loss.item())
         assert abs(lr.norm.item() - gnorm.item()) <= 2e-4 * gnorm.item() + 1e-6, (it, lr.norm.item(), gnorm.item())
+        assert abs(lr.norm.item() - plain_norm) <= 1e-3 * plain_norm, (it, lr.norm.item(), plain_norm)
         for k in params:
             ref = grads_ref[k]
             torch.testing.assert_close(lr.grads[k], ref, rtol=2e-3, atol=1e-5 * ref.abs().max().item() + 1e-9,
@@ -192,3 +238,4 @@ def test_x3_learn_at_bench_batch(B):
             diff = (lr.online[k] - params[k].detach()).abs()
             assert (diff > 1e-5).float().mean().item() <= 1e-3, (it, k, diff.max().item())
             assert diff.max().item() <= 2e-3, (it, k, diff.max().item())
+    print(f"B={B}: {n_flips} activations on the other ReLU branch than fp32 torch (x3 roundings of 0)")

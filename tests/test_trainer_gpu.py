@@ -85,15 +85,17 @@ def test_replay_sample_window_stays_inside():
                a=torch.zeros(4096, dtype=torch.int32, device="cuda"),
                r=torch.zeros(4096, dtype=torch.float32, device="cuda"),
                done=torch.zeros(4096, dtype=torch.uint8, device="cuda"))
-    rp.sample_window(base, count, 4096, 9, 0, out)
-    got = out["s"].view(4096, 8)[:, 0].cpu().numpy()
-    # slot k of the ring holds push (k + 4*30 - 20 ...): recover the slot from the stored values
     ring = rp.s.view(100, 8)[:, 0].cpu().numpy()
     slot = {int(v): k for k, v in enumerate(ring)}
-    slots = np.array([slot[int(v)] for v in got])
-    inside = (slots - base) % 100 < count
-    assert inside.all()
-    assert len(np.unique(slots)) == count  # every slot of the window is reachable
+    # slot k of the ring holds push (k + 4*30 - 20 ...): recover the slots from the stored values
+    for off, B in ((0, count), (70, 40), (110, 1)):  # without replacement: B <= count distinct slots
+        rp.sample_window(base, count, B, 9, off, out)
+        got = out["s"].view(4096, 8)[:B, 0].cpu().numpy()
+        slots = np.array([slot[int(v)] for v in got])
+        assert ((slots - base) % 100 < count).all()
+        assert len(np.unique(slots)) == B  # B = count: every slot of the window exactly once
+    with pytest.raises(Exception, match="larger than the window"):
+        rp.sample_window(base, count, count + 1, 9, 0, out)
 
 
 @pytest.mark.parametrize("lagged", [False, True])
