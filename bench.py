@@ -372,9 +372,8 @@ def main():
         cpu = cpu_baseline(cpu_snap, env.lay.R, lay_tables, P, args, E)
     if rank == 0:
         prec = args.precision
-        lp = tr.learner.precision if tr.learner is not None else prec
-        qdesc = ("f32 Q-net (bf16x3-split MFMA operands)" if prec == "f32" and (tr.fast is not None or lp == "x3")
-                 else f"{prec} Q-net")
+        qdesc = ("f32-accurate Q-net: x3 (bf16 hi+lo operand pairs on the bf16 MFMA, f32 accumulation; "
+                 "Q and loss within rtol 2e-4 of torch fp32)" if tr.q_arith == "x3" else f"{tr.q_arith} Q-net")
         line = {
             "metric": METRIC,
             "value": value,
@@ -408,6 +407,9 @@ def main():
                                      f"batch {args.batch} per GPU; the whole-job-32768 reading is "
                                      "total_envs_reading (N > 1)") if (L, R) == (128, 16) else None, "grid": f"{L}x{W}", "people": P, "robots": R, "mode": args.mode,
                 "batch": args.batch, "replay_capacity": args.replay_capacity, "schedule": schedule, "precision": prec,
+                "q_arithmetic": tr.q_arith,
+                "replay_sampling": ("uniform without replacement (random.sample semantics: keyed Feistel permutation "
+                                    "per learn step)") if args.replay == "uniform" else "proportional prioritized",
                 "qnet": ("MLP 726-512-256-5" if args.qnet == "mlp"
                          else "DQNNetwork conv 6-32-64-128 + 15488-512-256-5"),
                 "replay": args.replay, "groups": args.groups if args.mode == "train" else 1, "nets": args.nets,

@@ -231,9 +231,11 @@ class LayoutSet:
             self._feats = feats.to(self.device)
             self._feats_lo = feats_lo.to(self.device)
         else:
-            # set_params: new coefficients go into the SAME device buffers (stream-ordered copies):
-            # kernels already queued on other streams may still read them, so they are never freed
-            # and recycled under a running launch
+            # set_params: new coefficients go into the SAME device buffers. Kernels queued on other
+            # streams (a trainer's env / act streams) may still read the old ones, so the device is
+            # drained first: no launch ever sees a mix of old and new coefficients (set_params is a
+            # rare host call -- the reference's class attributes -- not part of a step)
+            torch.cuda.synchronize(self.device)
             self._set.copy_(raw, non_blocking=False)
             self._feats.copy_(feats)
             self._feats_lo.copy_(feats_lo)

@@ -174,6 +174,13 @@ class VecTrainer:
             lprec = "x3"
         self.learner = Learner(kind=kind, device=self.device, lr=lr, gamma=gamma, precision=lprec,
                                seed=learner_seed) if not self.per_robot else None
+        # the arithmetic the Q-network actually runs: "x3" (f32 operands as bf16 hi + lo pairs on the
+        # bf16 MFMA, f32 accumulation: f32 within the tests' stated tolerances), "f32" (exact f32
+        # MFMA) or "bf16"; the fused MLP kernels run x3 for precision "f32"
+        if self.per_robot or (kind == "mlp" and precision == "f32"):
+            self.q_arith = "x3"
+        else:
+            self.q_arith = lprec
         if self.learner is not None:
             self.learner.grad_hook = grad_hook
         # replay: "uniform" (DQNAgent.memory's random.sample) or "prioritized" (evacx.prio:

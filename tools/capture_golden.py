@@ -24,12 +24,14 @@ outputs are small ``.npz`` files under ``tests/golden/`` that pin
   steps of each with the sampled batch indices, the dropout masks (forward hooks on
   the ``Dropout`` modules), the loss, the total gradient norm, the gradients and the
   parameters / Adam moments after every step,
+* the QMIX mixer's learn step with the reference's own ``MixingNetwork``
+  (``runners/train_qmix.py:39-113``; ``qmix_mixer.npz``, ``qmix_fixtures``),
 * a long 128x128 R16 trajectory (``g128_long_traj.npz``: past the fire's last step,
   with a reset) and the per-step digests of the 128x128 danger tables for all 181
   fire steps (``g128_danger_digests.npz``).
 
 Usage:  PYTHONPATH=/root/reference PYTHONDONTWRITEBYTECODE=1 python tools/capture_golden.py [part ...]
-  parts: base (the round-1 fixtures), dqn, g128long, g128danger, dropin, ckpt; default: all
+  parts: base (the round-1 fixtures), dqn, g128long, g128danger, dropin, ckpt, qmix; default: all
 """
 import hashlib
 import os
@@ -607,9 +609,88 @@ def ref_checkpoint():
         init.__defaults__ = (512,)
 
 
+def reference_mixing_class():
+    """The reference's MixingNetwork. It is defined inside train_qmix()
+    (runners/train_qmix.py:39-54), so it cannot be imported: its class statement is taken out
+    of the file's syntax tree and executed here -- the reference's own code, run in this
+    container; nothing of it is written out."""
+    import ast
+    import torch
+    path = os.path.join(REF, "Louvre_Evacuation", "runners", "train_qmix.py")
+    tree = ast.parse(open(path, encoding="utf-8").read())
+    fn = next(n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name == "train_qmix")
+    cls = next(n for n in ast.walk(fn) if isinstance(n, ast.ClassDef) and n.name == "MixingNetwork")
+    ns = {"torch": torch}
+    exec(compile(ast.Module(body=[cls], type_ignores=[]), path, "exec"), ns)
+    return ns["MixingNetwork"]
+
+
+def qmix_fixtures():
+    """The mixer side of three QMIX learn steps (runners/train_qmix.py:78-113) with the
+    reference's own MixingNetwork (n_agents = 2, embed 32, torch.randn init under a fixed seed,
+    target mixer loaded from the online one as at :57-58), Adam(lr = 1e-3): the agents' chosen
+    Q-values and target max-Q values are the step's inputs (leaf tensors in place of
+    agent{1,2}.q_network(...).gather / target_network(...).max, which dqn_learn.npz pins), then
+    the reference's exact sequence -- stack, mixing, target_mixing under no_grad, y_tot =
+    r + gamma * Q_tot' * ~done, mse_loss, zero_grad, backward, clip_grad_norm_(mixing, 1.0),
+    step. Recorded per step: inputs, loss, d loss / d q (what flows into each agent's
+    backward), the mixer's raw and clipped gradients, its total norm, parameters and Adam
+    moments after the step. Batch 32 (configs/dqn.yaml batch_size), gamma 0.99."""
+    import torch
+    MixingNetwork = reference_mixing_class()
+    torch.manual_seed(5)
+    mixing = MixingNetwork(n_agents=2)
+    target_mixing = MixingNetwork(n_agents=2)
+    target_mixing.load_state_dict(mixing.state_dict())
+    mix_optimizer = torch.optim.Adam(mixing.parameters(), lr=1e-3)
+    out = {f"init_{k}": v.detach().numpy().copy() for k, v in mixing.state_dict().items()}
+    out["names"] = np.array(list(mixing.state_dict().keys()))
+    g = torch.Generator().manual_seed(7)
+    B, gamma = 32, 0.99
+    for step in range(3):
+        q = (torch.randn(B, 2, generator=g) * 6.0 + 1.0).requires_grad_(True)
+        tq = torch.randn(B, 2, generator=g) * 6.0 + 1.0
+        r_b = torch.randn(B, generator=g) * 20.0
+        d_b = torch.rand(B, generator=g) < 0.15
+        q1, q2 = q[:, 0], q[:, 1]
+        q_cat = torch.stack([q1, q2], dim=1)
+        q_tot = mixing(q_cat)
+        with torch.no_grad():
+            target_q_cat = torch.stack([tq[:, 0], tq[:, 1]], dim=1)
+            target_q_tot = target_mixing(target_q_cat)
+            y_tot = r_b + gamma * target_q_tot * (~d_b)
+        loss = torch.nn.functional.mse_loss(q_tot, y_tot)
+        mix_optimizer.zero_grad()
+        loss.backward()
+        raw = {k: p.grad.detach().clone() for k, p in mixing.named_parameters()}
+        norm = torch.nn.utils.clip_grad_norm_(mixing.parameters(), 1.0)
+        mix_optimizer.step()
+        pre = f"s{step}_"
+        out[pre + "q"] = q.detach().numpy().copy()
+        out[pre + "tq"] = tq.numpy().copy()
+        out[pre + "r"] = r_b.numpy().copy()
+        out[pre + "d"] = d_b.numpy().astype(np.uint8)
+        out[pre + "loss"] = np.float32(loss.item())
+        out[pre + "dq"] = q.grad.detach().numpy().copy()
+        out[pre + "norm"] = np.float32(norm.item())
+        out[pre + "hidden_active"] = ((q_cat.detach() @ mixing.fc1_weight.detach().abs()) > 0).numpy()
+        for k, p in mixing.named_parameters():
+            st = mix_optimizer.state[p]
+            out[pre + "raw_" + k] = raw[k].numpy()
+            out[pre + "grad_" + k] = p.grad.detach().numpy().copy()
+            out[pre + "param_" + k] = p.detach().numpy().copy()
+            out[pre + "m_" + k] = st["exp_avg"].numpy().copy()
+            out[pre + "v_" + k] = st["exp_avg_sq"].numpy().copy()
+        print(f"  step {step}: loss {loss.item():.6g} norm {norm.item():.6g}")
+    np.savez_compressed(os.path.join(OUT, "qmix_mixer.npz"), **out)
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
-    parts = sys.argv[1:] or ["base", "dqn", "g128long", "g128danger", "dropin", "ckpt"]
+    parts = sys.argv[1:] or ["base", "dqn", "g128long", "g128danger", "dropin", "ckpt", "qmix"]
+    if "qmix" in parts:
+        print("qmix mixer")
+        qmix_fixtures()
     if "ckpt" in parts:
         print("reference checkpoint")
         ref_checkpoint()
