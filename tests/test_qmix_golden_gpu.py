@@ -43,7 +43,8 @@ def test_device_mixer_matches_reference_steps():
         Qt.scatter_(2, torch.randint(0, A, (n, B, 1), generator=g), tq.t().unsqueeze(2))  # ... which one action holds
         rew = torch.from_numpy(fx[p + "r"])
         done = torch.from_numpy(fx[p + "d"])
-        Q, Qt, act, rew, done = Q.to(dev), Qt.to(dev), act.to(dev), rew.to(dev), done.to(dev)
+        # raw pointers below: [n][B][A] contiguous (the broadcast above may leave Qt's strides permuted)
+        Q, Qt, act, rew, done = [t.contiguous().to(dev) for t in (Q, Qt, act, rew, done)]
         dQ = torch.full((n, B, A), 7.0, device=dev)
         part = torch.empty(int(mlib().evx_qmix_part_floats(B, n)), device=dev)
         zero = torch.ones(64, device=dev)
