@@ -679,10 +679,16 @@ __host__ __device__ inline int64_t wave_hv_offset(int P) {
 __host__ __device__ inline int64_t wave_scratch_words(int P) { return wave_hv_offset(P) + 2 * (int64_t)P; }
 // ... | big grids: target, contested and vacated bitmaps [3][RW], contest losers [P/32] (the
 // per-env stride)
-__host__ __device__ inline int64_t env_scratch_words(const evx_layout& l) {
+// ... | the light path's lists, kept from one step to the next: header [4] (LISTS_VALID, not-dead
+// count, in-play count) | the not-dead persons' healths in list order [P] double (the in-play list
+// itself stays in the wide path's health region, which a light step does not otherwise use)
+__host__ __device__ inline int64_t persist_offset(const evx_layout& l) {
     const int RW = ((l.L + 2) * (l.W + 2) + 31) / 32;
-    return wave_scratch_words(l.P) + (big_grid(l.L, l.W) ? 3 * (int64_t)RW + (l.P + 31) / 32 : 0);
+    const int64_t o = wave_scratch_words(l.P) + (big_grid(l.L, l.W) ? 3 * (int64_t)RW + (l.P + 31) / 32 : 0);
+    return (o + 1) & ~(int64_t)1;
 }
+__host__ __device__ inline int64_t env_scratch_words(const evx_layout& l) { return persist_offset(l) + 4 + 2 * (int64_t)l.P; }
+constexpr uint32_t LISTS_VALID = 0x4c495354u;
 
 __device__ __forceinline__ int pb_bits(int P) { return P > 1 ? bit_length((uint32_t)(P - 1)) : 1; }
 
@@ -1311,7 +1317,9 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     // in the wide path's health region, and every not-dead person's health in list order
     // (frozen for the safe ones, updated by the rows for those in play) in the spill region
     uint2* ipl = reinterpret_cast<uint2*>(scr + wave_hv_offset(P));
-    double* hl = reinterpret_cast<double*>(scr + 4 * P);
+    // kept between light steps (persist_offset): the lists' header and the list-order healths
+    uint32_t* lhdr = scr + persist_offset(lay);
+    double* hl = reinterpret_cast<double*>(lhdr + 4);
     const int n2P = pow2_ceil(P < 64 ? 64 : P);
     uint32_t* Lg = scr + 4 * P;                             // spill: contested list
     uint32_t* Hg = Lg + n2P;                                // spill: group heads
@@ -1320,6 +1328,10 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     // ---------------------------------------------------------------- load
     const int* scal_g = st.scal + (size_t)e * 4;
     const int fs = scal_g[0], cur_step = scal_g[1], prev_evac = scal_g[2], prev_dead = scal_g[3];
+    // light path: the in-play list and the list-order healths left by this env's previous (light)
+    // step replace the scan of every person word and health (reset or a wide step invalidate them)
+    const uint32_t lh_valid = lhdr[0], lh_nnd = lhdr[1], lh_nip = lhdr[2];  // (8-byte aligned only)
+    const bool kept = !WIDE && __builtin_amdgcn_readfirstlane((int)(lh_valid == LISTS_VALID));
     uint32_t view = st.view[e];
     PT_DECL(ld1);
     PT_DECL(ld2);
@@ -1354,8 +1366,8 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     for (int j = 0; j < PKB; j++) {
         const int p = j * 64 + lane;
         vv[j] = 2u << 24;
-        if (p < P) vv[j] = pk_g[p];
-        if constexpr (!WIDE) hr[j] = p < P ? h_g[p] : 0.0;
+        if (!kept && p < P) vv[j] = pk_g[p];
+        if constexpr (!WIDE) hr[j] = !kept && p < P ? h_g[p] : 0.0;
     }
     const uint32_t* grm = st.rmap + (size_t)e * g.RW;
     for (int i0 = 0; i0 < g.RW; i0 += 16 * 64) {
@@ -1413,7 +1425,11 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     // the not-dead persons in person order (sum(... if not p.dead) and the movers
     // never look at anyone else)
     int nnd = 0, n_safe = 0, nip = 0;
-    for (int r0 = 0; r0 < NR; r0 += PKB) {  // PKB rows processed while the next PKB are in flight
+    if (kept) {
+        nnd = __builtin_amdgcn_readfirstlane((int)lh_nnd);
+        nip = __builtin_amdgcn_readfirstlane((int)lh_nip);
+    }
+    for (int r0 = 0; r0 < (kept ? 0 : NR); r0 += PKB) {  // PKB rows processed while the next PKB are in flight
         uint32_t nx[PKB];
         double hn[WIDE ? 1 : PKB];
 #pragma unroll
@@ -1514,6 +1530,7 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     PT_DECL(sbs);
     PT_DECL(sbt);
     double total = 0.0;  // CPython sum(p.health for p in self.people.list if not p.dead): sequential
+    int fold_kept = 0;   // light path: entries of the kept list-order healths after this step
     if constexpr (WIDE) {
         WideCtl* ctl = reinterpret_cast<WideCtl*>(smem + wide_lds(lay).ctl);
         if (lane == 0) {
@@ -1613,16 +1630,22 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
             }
             np_head += tot;
         }
-        n_died += __popcll(__ballot(died));
+        const unsigned long long dm = __ballot(died);
+        n_died += __popcll(dm);
         {
             // entry i of the not-dead list was read two iterations ago: the compacted alive list
-            // (index <= i) overwrites only consumed entries
+            // (index <= i) overwrites only consumed entries. Each keeps its index in the not-dead
+            // list as it will stand after this step's deaths are dropped (deaths only happen among
+            // the persons in play, so those before it are the deaths earlier in this list)
             const unsigned long long am = __ballot(alive);
-            if (alive) ipl[nal + lanes_below(am)] = make_uint2((uint32_t)p, v);
+            const uint32_t knew = (en.x >> 16) - (uint32_t)(n_died - __popcll(dm) + lanes_below(dm));
+            if (alive) ipl[nal + lanes_below(am)] = make_uint2((uint32_t)p | (knew << 16), v);
             nal += __popcll(am);
         }
         PT_END(np);
-        if (inr) hl[en.x >> 16] = died ? 0.0 : hh;  // the list-order health the fold reads (dead: +0.0)
+        // the list-order health the fold reads; a death leaves -0.0 (adds nothing to the running
+        // sum, which is >= +0.0) and marks the slot the fold drops from the kept list
+        if (inr) hl[en.x >> 16] = died ? -0.0 : hh;
         PT_BEGIN(plan);
         // phase 2: accumulate; candidates of find_best_direction
         bool planner = false;
@@ -1782,6 +1805,7 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
         PT_BEGIN(hsum);
         double* hc = reinterpret_cast<double*>(aux + 384);
         constexpr int FB = 4;
+        int nkeep = 0;  // the kept list for the next step: this step's deaths (-0.0) dropped, in place
         double fv[FB];
 #pragma unroll
         for (int k = 0; k < FB; k++) fv[k] = 64 * k + lane < nnd ? hl[64 * k + lane] : 0.0;
@@ -1797,6 +1821,12 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
                 if (i0 + 64 * k >= nnd) break;
                 pin(fv[k]);
                 hc[lane] = fv[k];
+                {
+                    const bool keep = i0 + 64 * k + lane < nnd && !signbit(fv[k]);
+                    const unsigned long long km = __ballot(keep);
+                    if (keep) hl[nkeep + lanes_below(km)] = fv[k];  // index <= read index: consumed
+                    nkeep += __popcll(km);
+                }
                 wave_fence();
                 if (lane == 0) {
                     const double2* h2 = reinterpret_cast<const double2*>(hc);
@@ -1822,6 +1852,7 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
 #pragma unroll
             for (int k = 0; k < FB; k++) fv[k] = fn[k];
         }
+        fold_kept = nkeep;
         PT_END(hsum);
     }
     EVX_STAMP(2);
@@ -1842,6 +1873,7 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
 
     // ------------------------- contested targets: groups, shuffle, losers
     int err = 0;
+    if (!WIDE && fold_kept != nnd - n_died) err |= 32;  // kept list out of step with the counts
     int ncont = 0;
     PT_DECL(lp);
     PT_DECL(grp);
@@ -2024,7 +2056,7 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     int q = 0;
     // remaining persons = the list nrl (the alive persons in play, or the whole not-dead list)
     // minus this step's deaths and evacuations
-    auto reward_half = [&](int i, uint32_t v, double hv) {
+    auto reward_half = [&](int i, uint32_t v, double hv, uint32_t px) {
         PT_BEGIN(rew);
         const bool rem = i < nrl && !pk_safe(v) && !pk_dead(v);
         const long long x2 = 2 * pk_x(v) + 1, y2 = 2 * pk_y(v) + 1;
@@ -2040,18 +2072,22 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
         }
         const unsigned long long rm = __ballot(rem);
         if (rem) dist[q + lanes_below(rm)] = 0.5 * sqrt((double)n4);
+        // light path: the persons still in play are the next step's in-play list (entry i was
+        // read two groups ago: index <= i overwrites only consumed entries)
+        if (!WIDE && rem) ipl[q + lanes_below(rm)] = make_uint2(px, v);
         q += __popcll(rm);
         PT_END(rew);
     };
-    auto load_idx = [&](int i) -> uint32_t {
+    auto load_idx = [&](int i) -> uint32_t {  // person | (list index << 16)
         uint32_t p = 0u;
-        if (i < nrl) p = rl[i].x & 0xffffu;
+        if (i < nrl) p = rl[i].x;
         return p;
     };
-    auto load_pw = [&](int i, uint32_t p, uint32_t& w, double& h) {
+    auto load_pw = [&](int i, uint32_t px, uint32_t& w, double& h) {
         w = DONEPK;
         h = 0.0;
         if (i < nrl) {
+            const uint32_t p = px & 0xffffu;
             w = pk_g[p];
             h = h_g[p];
         }
@@ -2071,10 +2107,12 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
         const int i0 = it * 64 * GQ + lane;
         uint32_t cw[GQ];
         double ch[GQ];
+        uint32_t cj[GQ];
 #pragma unroll
         for (int k = 0; k < GQ; k++) {
             cw[k] = nxw[k];
             ch[k] = nxhv[k];
+            cj[k] = nxj[k];
             nxj[k] = nnj[k];
             pin(cw[k]);
             pin(ch[k]);
@@ -2086,17 +2124,18 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
         for (int k = 0; k < GQ; k++) nnj[k] = load_idx(i0 + 64 * (2 * GQ + k));
 #pragma clang loop unroll(disable)
         for (int k = 0; k < GQ; k++) {
-            uint32_t w = cw[0];
+            uint32_t w = cw[0], px = cj[0];
             double h = ch[0];
 #pragma unroll
             for (int j = 1; j < GQ; j++) {
                 if (k == j) {
                     w = cw[j];
                     h = ch[j];
+                    px = cj[j];
                 }
             }
             PT_END(rtop);
-            reward_half(i0 + 64 * k, w, h);
+            reward_half(i0 + 64 * k, w, h, px);
             PT_BEGIN(rtop);
         }
         PT_END(rtop);
@@ -2204,6 +2243,11 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
         sg[3] = dead;
         st.view[e] = view;
         if (err && out.err) atomicOr(out.err, err);
+        // the lists the next light step starts from (a wide step's are not kept; a fused reset
+        // below invalidates them again)
+        lhdr[0] = WIDE ? 0u : LISTS_VALID;
+        lhdr[1] = (uint32_t)(nnd - n_died);
+        lhdr[2] = (uint32_t)q;
     }
 
     // ------------------------------------------------- observations
@@ -2252,6 +2296,8 @@ __device__ __forceinline__ void reset_one(const evx_layout& lay, const evx_state
     g.L = lay.L; g.W = lay.W; g.GY = lay.W + 2; g.G = (lay.L + 2) * (lay.W + 2);
     g.RW = (g.G + 31) / 32; g.P = lay.P; g.R = lay.R;
     const int P = g.P, R = g.R;
+    // fresh people: the light path's kept lists no longer describe this env
+    if (lane == 0) st.scratch[(size_t)e * env_scratch_words(lay) + persist_offset(lay)] = 0u;
     const ResetLds S = reset_lds(g.G, P, BIGG);
     uint32_t* pyring = smem + S.pyring;
     const uint32_t* validb;
