@@ -155,6 +155,58 @@ __device__ __forceinline__ void write_obs4(const Geo& g, const uint32_t* rmapb, 
     }
 }
 
+// Compact observations of robots r0 .. r0 + 15 (< R) in one pass: 4 lanes per robot, lane part q
+// of robot r builds the window rows i = q, q + 4, q + 8 (< 11) -- two LDS words of the occupancy
+// bitmap per row, funnel-shifted to the row's 11 cells (y = cy - 5 .. cy + 5), cells off the map
+// interior masked (People.rmap is only set on valid cells, so Check_Valid reduces to the range
+// test) -- into bits 11 i .. 11 i + 10 of the 121-bit occupancy word (cell c = 11 i + j, as
+// _get_state's [i][j] flattening); the 4 lanes' words meet by xor-shuffles. Robot 0's window is
+// centred on `view0` (Map.robot_position), the others on their own positions.
+__device__ __forceinline__ void write_obs16(const Geo& g, const uint32_t* rmapb, const uint32_t* cen, uint32_t view0,
+                                            int r0, int R, int fs, uint32_t lid, evx_obs* dst) {
+    const int lane = threadIdx.x & 63;
+    const int r = r0 + (lane >> 2), q = lane & 3;
+    const uint32_t c = r < R ? (r == 0 ? view0 : cen[r]) : 0u;
+    const int cx = rp_x(c), cy = rp_y(c), ylo = cy - 5;
+    // columns j with 1 <= ylo + j <= W
+    const int jlo = max(0, 1 - ylo), jhi = min(10, g.W - ylo);
+    const uint32_t cmask = jhi >= jlo ? ((2u << jhi) - 1u) & ~((1u << jlo) - 1u) : 0u;
+    uint32_t rw[3], w0[3], w1[3];
+#pragma unroll
+    for (int t = 0; t < 3; t++) {  // the row words, all reads issued together
+        const int i = q + 4 * t, mx = cx + i - 5;
+        const bool ok = r < R && i < 11 && mx >= 1 && mx <= g.L;
+        const int base = ok ? mx * g.GY + ylo : 0;
+        rw[t] = (uint32_t)base;
+        w0[t] = ok ? rmapb[base >> 5] : 0u;
+        w1[t] = ok ? rmapb[(base >> 5) + 1] : 0u;
+    }
+    uint32_t o0 = 0, o1 = 0, o2 = 0, o3 = 0;
+#pragma unroll
+    for (int t = 0; t < 3; t++) {
+        const int i = q + 4 * t;
+        const uint64_t two = ((uint64_t)w1[t] << 32) | w0[t];
+        const uint64_t row = (uint64_t)((uint32_t)(two >> (rw[t] & 31u)) & cmask) << (11 * i & 31);
+        const int wd = (11 * i) >> 5;  // the row's first word (bits may run into the next)
+        const uint32_t lo = (uint32_t)row, hi = (uint32_t)(row >> 32);
+        o0 |= wd == 0 ? lo : 0u;
+        o1 |= wd == 1 ? lo : (wd == 0 ? hi : 0u);
+        o2 |= wd == 2 ? lo : (wd == 1 ? hi : 0u);
+        o3 |= wd == 3 ? lo : (wd == 2 ? hi : 0u);
+    }
+#pragma unroll
+    for (int m = 1; m <= 2; m <<= 1) {
+        o0 |= (uint32_t)__shfl_xor((int)o0, m, 64);
+        o1 |= (uint32_t)__shfl_xor((int)o1, m, 64);
+        o2 |= (uint32_t)__shfl_xor((int)o2, m, 64);
+        o3 |= (uint32_t)__shfl_xor((int)o3, m, 64);
+    }
+    if (q == 0 && r < R) {
+        reinterpret_cast<uint4*>(dst + r)[0] = make_uint4(o0, o1, o2, o3);
+        reinterpret_cast<uint4*>(dst + r)[1] = make_uint4((uint32_t)cx, (uint32_t)cy, (uint32_t)fs, lid);
+    }
+}
+
 // Compact observation of one robot built by one wave (bits by ballot).
 __device__ __forceinline__ void write_obs(const Geo& g, const uint32_t* validb, const uint32_t* rmapb, int cx,
                                           int cy, int fs, uint32_t lid, evx_obs* dst) {
@@ -2250,6 +2302,7 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
         lhdr[2] = (uint32_t)q;
     }
 
+    EVX_STAMP(6);
     // ------------------------------------------------- observations
     // People.rmap is only ever set on valid cells, so Check_Valid reduces to the
     // interior range test here (no table reads).
@@ -2258,16 +2311,15 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     const bool fin = __builtin_amdgcn_readfirstlane((int)((evac + dead == P) || (0.5 * (double)(cur_step + 1) >= 600.0)));
     const bool ar = out.obs_term != nullptr && fin;
     evx_obs* obs_dst = ar ? out.obs_term : out.obs;
-    // robot 0's observation is centred on Map.robot_position (view), the others on their own
-    // positions: the centres go to the robots table's slot 0 for the pass (wave-private LDS)
-    const uint32_t rob0 = robots[0];
-    if (lane == 0) robots[0] = view;
-    wave_fence();
+    // robot 0's observation is centred on Map.robot_position (view), the others on their own positions
     const uint32_t lid = st.layout_idx ? (uint32_t)st.layout_idx[e] : 0u;
-    for (int r0 = 0; r0 < R; r0 += 4) write_obs4(g, rmapb, robots, r0, R, fs1, lid, obs_dst + (size_t)e * R);
-    wave_fence();
-    if (lane == 0) robots[0] = rob0;
-    wave_fence();
+#ifndef EVX_PROFILE
+    EVX_STAMP(15);
+#endif
+    for (int r0 = 0; r0 < R; r0 += 16) write_obs16(g, rmapb, robots, view, r0, R, fs1, lid, obs_dst + (size_t)e * R);
+#ifndef EVX_PROFILE
+    EVX_STAMP(7);
+#endif
     EVX_STAMP(8);
     if (ar) {
         __threadfence();  // this wave's state writes complete and visible before the reset reads them

@@ -16,7 +16,7 @@ from evacx.layout import build_tables, synthetic  # noqa: E402
 
 # stamp slots written by env_step_kernel (one wave per env)
 SLOTS = [(0, "start"), (1, "load+robots+near"), (2, "rows(health+plan)"), (3, "contested+mt_store"),
-         (4, "execute+rmap"), (5, "reward rows"), (8, "reward+obs")]
+         (4, "execute+rmap"), (5, "reward rows"), (6, "reward formula"), (8, "obs")]
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--envs", type=int, default=4096)
@@ -62,6 +62,9 @@ print(f"  {'phase':28s} {'median':>9s} {'mean':>9s} {'share':>7s} {'slowest1%':>
 for i, (_, n) in enumerate(SLOTS[1:]):
     print(f"  {n:28s} {np.median(d[:, i]):9.0f} {d[:, i].mean():9.0f} {d[:, i].sum() / tot.sum():7.1%}"
           f" {d[top, i].mean():10.0f}")
+if not s[:, 16:30].any() and s[:, 15].any():  # normal build: stamps around the observation writes
+    o1, o2 = s[:, 15] - s[:, 6], s[:, 7] - s[:, 15]
+    print(f"  obs: before the writes median {np.median(o1):.0f}, writes {np.median(o2):.0f}, after {np.median(s[:, 8] - s[:, 7]):.0f}")
 print("py words/step median", np.median(s[:, 12]), " np words/step median", np.median(s[:, 13]),
       " contested movers median/max", np.median(s[:, 14]), s[:, 14].max(), " planners median/max",
       np.median(s[:, 11]), s[:, 11].max())
