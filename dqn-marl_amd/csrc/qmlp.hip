@@ -739,7 +739,23 @@ constexpr int A3_HP = 256 + 8;                     // H1 half-plane row pitch (b
 constexpr int A3_HBYTES = 2 * 128 * A3_HP * 2;     // 135,168: both planes
 static_assert(A3_HBYTES >= 128 * ACT_H2P * 4, "H2 overlays the H1 planes");
 static_assert(A3_HBYTES >= 2 * 128 * (KC1 + 8) * 2, "fc1 A staging overlays the H1 planes");
-constexpr int ACT3_LDS = A3_HBYTES + NACT * HID2 * 4 + 128 * 4 + 64 * 4;  // + W3 + window centres + pair hashes
+// + W3 + window centres + pair hashes + the occupancy-fragment table (table path: byte of 8 cell
+// bits -> the 8 bf16 A values, 0 or 1.0, of one MFMA k-step; one ds_read_b128 instead of ~25 VALU)
+constexpr int ACT3_OCC = 256 * 16;
+constexpr int ACT3_LDS = A3_HBYTES + NACT * HID2 * 4 + 128 * 4 + 64 * 4 + ACT3_OCC;
+// diagnostic build (-DEVX_ACT_STAMPS, tools/act_stamps.py): wave 0's s_memtime at the phase
+// boundaries of every workgroup (evx_diag_act_stamps)
+#ifdef EVX_ACT_STAMPS
+constexpr int ACT_NST = 12;
+__device__ long long g_act_st[8192 * ACT_NST];
+#define ACT_ST(i)                                                                                   \
+    do {                                                                                            \
+        if (threadIdx.x == 0 && blockIdx.x < 8192)                                                  \
+            g_act_st[blockIdx.x * ACT_NST + (i)] = (long long)__builtin_amdgcn_s_memtime();         \
+    } while (0)
+#else
+#define ACT_ST(i)
+#endif
 // GR: grouped act, blockIdx.y = net (interleaved rows); DM: the dropout mode (fc1_slab_m)
 template <bool GR = false, int DM = 1>
 __global__ __launch_bounds__(512, 1) void qact3_kernel(Fwd a0) {
@@ -753,8 +769,10 @@ __global__ __launch_bounds__(512, 1) void qact3_kernel(Fwd a0) {
     auto W3s = reinterpret_cast<float (*)[HID2]>(dsm + A3_HBYTES);
     int* posS = reinterpret_cast<int*>(dsm + A3_HBYTES + NACT * HID2 * 4);
     uint32_t* phS = reinterpret_cast<uint32_t*>(dsm + A3_HBYTES + NACT * HID2 * 4 + 128 * 4);
+    uint4* occT = reinterpret_cast<uint4*>(dsm + A3_HBYTES + NACT * HID2 * 4 + 128 * 4 + 64 * 4);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
     const int m0 = blockIdx.x * 128;
+    ACT_ST(0);
     for (int i = tid; i < NACT * HID2; i += 512) W3s[i / HID2][i % HID2] = a.w3[i];
     if (DM == 1 && tid >= 448) {  // the tile's 64 row-pair dropout hashes (published by the barriers below)
         const int r2 = m0 + 2 * (tid - 448);
@@ -773,8 +791,16 @@ __global__ __launch_bounds__(512, 1) void qact3_kernel(Fwd a0) {
             }
             posS[tid] = pos;
         }
+        if (tid >= 256) {  // the occupancy-fragment table (published by the same barrier)
+            const uint32_t bits = (uint32_t)(tid - 256), one = 0x3f80u;
+            uint32_t v[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) v[j] = ((bits >> (2 * j)) & 1u) * one | (((bits >> (2 * j + 1)) & 1u) * one) << 16;
+            occT[bits] = make_uint4(v[0], v[1], v[2], v[3]);
+        }
         fast = __syncthreads_and(ok);  // also publishes posS
     }
+    ACT_ST(1);
     f32x16 acc2[4];
 #pragma unroll
     for (int mt = 0; mt < 4; mt++)
@@ -811,7 +837,6 @@ __global__ __launch_bounds__(512, 1) void qact3_kernel(Fwd a0) {
                     const int rl = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
                     acc[mt][0][r] = a.stat[(uint32_t)posS[rl] * (uint32_t)HID + cofs];
                 }
-            const uint32_t one = 0x3f80u;
 #pragma unroll 2
             for (int ks = 0; ks < 8; ks++) {  // k-step: cells 16 ks + 8 h .. + 7 of the 128
                 const bf16x8 bh = *reinterpret_cast<const bf16x8*>(a.w1o + w1o_tile(hh * 8 + w, ks >> 1, ks & 1) + lane * 8);
@@ -822,11 +847,7 @@ __global__ __launch_bounds__(512, 1) void qact3_kernel(Fwd a0) {
                     const uint32_t wd = (c0 >> 5) == 0 ? occ[mt][0] : (c0 >> 5) == 1 ? occ[mt][1]
                                       : (c0 >> 5) == 2 ? occ[mt][2] : occ[mt][3];
                     const uint32_t bits = (wd >> (c0 & 31)) & 0xffu;
-                    uint32_t av4[4];
-#pragma unroll
-                    for (int j = 0; j < 4; j++)
-                        av4[j] = ((bits >> (2 * j)) & 1u) * one | (((bits >> (2 * j + 1)) & 1u) * one) << 16;
-                    const bf16x8 av = __builtin_bit_cast(bf16x8, av4);
+                    const bf16x8 av = __builtin_bit_cast(bf16x8, occT[bits]);
                     acc[mt][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bh, acc[mt][0], 0, 0, 0);
                     acc[mt][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bl, acc[mt][0], 0, 0, 0);
                 }
@@ -834,13 +855,16 @@ __global__ __launch_bounds__(512, 1) void qact3_kernel(Fwd a0) {
         } else {
             fc1_tile<4, 1, 8, true, 2>(a, m0, col0, false, dsm, acc);  // ends with a barrier: A buffers free
         }
+        ACT_ST(2 + 4 * hh);
         const float bias[1] = {fast ? 0.f : a.b1[col0 + (lane & 31)]};  // the table holds the bias
 #pragma unroll
         for (int mt = 0; mt < 4; mt++)
             fc1_slab_m<1, A3_HP, true, DM>(a, acc[mt], bias, m0 + mt * 32, hh * 256, w * 32,
                                            reinterpret_cast<__bf16 (*)[A3_HP]>(&Hh[mt * 32][0]),
                                            reinterpret_cast<__bf16 (*)[A3_HP]>(&Hl[mt * 32][0]), phS + mt * 16);
+        ACT_ST(3 + 4 * hh);
         __syncthreads();
+        ACT_ST(4 + 4 * hh);
         // fc2 over K = [256 hh, 256 hh + 256): wave w -> columns [32w, 32w + 32)
         bf16x8 bc[2], bn[2], lc[2], ln[2];
         auto loadB = [&](int kc, bf16x8 (&b)[2], bf16x8 (&l)[2]) {
@@ -870,6 +894,7 @@ __global__ __launch_bounds__(512, 1) void qact3_kernel(Fwd a0) {
                 lc[s] = ln[s];
             }
         }
+        ACT_ST(5 + 4 * hh);
         __syncthreads();  // every wave is done with this half: the next half / H2 reuse the planes
     }
     {
@@ -884,8 +909,10 @@ __global__ __launch_bounds__(512, 1) void qact3_kernel(Fwd a0) {
             }
     }
     __syncthreads();
+    ACT_ST(10);
     const int row = tid >> 2;
     fc3_act(a, &H2s[row][0], W3s, orow(a, m0 + row), m0 + row < a.N);
+    ACT_ST(11);
 }
 
 // ------------------------------------------------------------ fc2 + fc3
@@ -1931,6 +1958,18 @@ int evx_qmlp_forward(const evx_layout* lay, const evx_obs* obs, int32_t n, const
     int rc = make_fwd(lay, obs, n, p, drop, out, a);
     if (rc) return rc;
     return launch_fwd(a, a, n, 1, out->q || out->actions || out->h2, (hipStream_t)stream, p->x3 != 0);
+}
+
+// diagnostic builds only: copy the act stamps out (-1 when the build has none)
+int evx_diag_act_stamps(long long* host, int32_t n) {
+#ifdef EVX_ACT_STAMPS
+    if (n > 8192 * evxm::ACT_NST) n = 8192 * evxm::ACT_NST;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(evxm::g_act_st), (size_t)n * 8) == hipSuccess ? n : -5;
+#else
+    (void)host;
+    (void)n;
+    return -1;
+#endif
 }
 
 int evx_qmlp_act(const evx_layout* lay, const evx_obs* obs, int32_t n, const evx_qmlp_params* p,
