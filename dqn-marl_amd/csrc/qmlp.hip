@@ -1231,10 +1231,16 @@ __global__ __launch_bounds__(256) void qbwd3_kernel(Bwd a0) {
     }
 }
 
-// dZ1 = (dZ2 W2) * scale * [H1 > 0]: 64 rows x 128 columns per workgroup (4 waves x
-// 32 columns), K = 256 in chunks of 32; dZ2 staged through LDS, W2^T operand-tiled.
+// dZ1 = (dZ2 W2) * scale * [H1 > 0]: 64-row tiles x 128 columns per workgroup (4 waves x
+// 32 columns), K = 256. A tile's whole dZ2 block (64 x 256, x3: both planes) is staged in LDS
+// at once and the next tile's is fetched into registers while this one's MFMAs run; the W2^T
+// fragments stream from L2 four k-steps ahead. (Chunks of 32 k with one barrier each left
+// every chunk waiting out a memory latency with one wave per SIMD: 120 us at B = 32768.)
+constexpr int QZ_P = HID2 + 8;  // LDS row pitch (bf16): 528 B, conflict-free ds_read_b128 rows
+constexpr int QZ_CP = 128 + 8;  // the dZ1 tile's row pitch (bf16)
+static_assert(QZ_CP <= QZ_P, "each dZ1 plane overlays a dZ2 plane");
 template <bool X3>
-constexpr int qdz1_lds_bytes() { return 2 * (X3 ? 2 : 1) * RM * 40 * 2; }
+constexpr int qdz1_lds_bytes() { return (X3 ? 2 : 1) * RM * QZ_P * 2 + 2 * RM * 16; }  // + 2 tiles of [H1 > 0] bits
 // Row tiles per qdz1 workgroup: the tile's column sums (db1 and the centre column of dW1) leave by
 // one f32 atomic per column; with one 64-row tile per workgroup every such word took B / 64
 // same-address atomics, which the L2 serialises. Up to QZ_RT tiles per workgroup while the grid
@@ -1242,107 +1248,130 @@ constexpr int qdz1_lds_bytes() { return 2 * (X3 ? 2 : 1) * RM * 40 * 2; }
 constexpr int QZ_RT = 8;
 inline int qdz1_tiles_per_wg(int B) { return B / 4096 < 1 ? 1 : (B / 4096 > QZ_RT ? QZ_RT : B / 4096); }
 template <bool X3 = false>
-__device__ __forceinline__ void qdz1_tile(const Bwd& a, char* smem, int m0, int by, float& cs);
-template <bool X3 = false>
 __device__ __forceinline__ void qdz1_body(const Bwd& a, char* smem, int bx, int by, int ndzx) {
-    float cs = 0.f;
+    constexpr int NPL = X3 ? 2 : 1;
+    auto As = reinterpret_cast<__bf16 (*)[RM][QZ_P]>(smem);  // [NPL][RM][QZ_P]
+    // [H1 > 0] of the tile's 64 rows x 128 columns as bits (byte b of a row: columns 8b .. 8b + 7),
+    // double-buffered by tile parity: H1 arrives with dZ2 in 16-B row pieces instead of the
+    // 2-B loads of the accumulator layout (which cost 75 us at B = 32768)
+    auto Ms = reinterpret_cast<uint32_t (*)[RM][4]>(smem + NPL * RM * QZ_P * 2);  // [2][RM][4]
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+    const int n0 = by * 128 + w * 32, col = n0 + (lane & 31);
     const int nrt = (a.B + RM * ndzx - 1) / (RM * ndzx);  // row tiles per workgroup
-    for (int rt = 0; rt < nrt; rt++) {
-        const int m0 = (bx * nrt + rt) * RM;
-        if (m0 >= a.B) break;
-        qdz1_tile<X3>(a, smem, m0, by, cs);
+    const int t0 = bx * nrt, nt = min(nrt, (a.B + RM - 1) / RM - t0);
+    // staging: 16-B piece j of thread t = (row c >> 5, k 8 (c & 31)) for c = t + 256 j: a wave
+    // reads two whole 512-B rows per plane and piece
+    uint4 pre[NPL][8], hpre[4];
+    auto fetch = [&](int m0) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {  // H1 piece j: row (c >> 4), columns 128 by + 8 (c & 15), c = t + 256 j
+            const int c = tid + 256 * j, row = m0 + (c >> 4);
+            hpre[j] = make_uint4(0u, 0u, 0u, 0u);
+#ifndef QZ_NOH1
+            if (row < a.B) hpre[j] = *reinterpret_cast<const uint4*>(a.h1 + (size_t)row * HID + by * 128 + (c & 15) * 8);
+#endif
+        }
+#pragma unroll
+        for (int p = 0; p < NPL; p++)
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const int c = tid + 256 * j, row = m0 + (c >> 5);
+                pre[p][j] = make_uint4(0u, 0u, 0u, 0u);
+#ifndef QZ_NOFETCH
+                if (row < a.B) pre[p][j] = *reinterpret_cast<const uint4*>((p ? a.dz2l : a.dz2) + (size_t)row * HID2 + (c & 31) * 8);
+#endif
+            }
+    };
+    auto loadB = [&](int ks, bf16x8 (&b)[NPL]) {  // k-step ks (16 k) of the wave's 32 columns
+        b[0] = *reinterpret_cast<const bf16x8*>(a.w2t + w2t_tile(n0 >> 5, ks >> 1, ks & 1) + lane * 8);
+        if constexpr (X3) b[NPL - 1] = *reinterpret_cast<const bf16x8*>(a.w2tl + w2t_tile(n0 >> 5, ks >> 1, ks & 1) + lane * 8);
+    };
+    constexpr int NKS = HID2 / 16, RING = 4;
+    float cs = 0.f;
+    if (nt > 0) fetch(t0 * RM);
+    for (int t = 0; t < nt; t++) {
+        const int m0 = (t0 + t) * RM;
+#pragma unroll
+        for (int p = 0; p < NPL; p++)
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const int c = tid + 256 * j;
+                *reinterpret_cast<uint4*>(&As[p][c >> 5][(c & 31) * 8]) = pre[p][j];
+            }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int c = tid + 256 * j;
+            const uint32_t wv[4] = {hpre[j].x, hpre[j].y, hpre[j].z, hpre[j].w};
+            uint32_t bits = 0u;
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                bits |= (__builtin_bit_cast(float, wv[e] << 16) > 0.f ? 1u : 0u) << (2 * e);
+                bits |= (__builtin_bit_cast(float, wv[e] & 0xffff0000u) > 0.f ? 1u : 0u) << (2 * e + 1);
+            }
+            reinterpret_cast<uint8_t*>(&Ms[t & 1][c >> 4][0])[c & 15] = (uint8_t)bits;
+        }
+        bf16x8 bq[RING][NPL];
+#pragma unroll
+        for (int i = 0; i < RING; i++) loadB(i, bq[i]);
+        __syncthreads();
+        if (t + 1 < nt) fetch(m0 + RM);
+        f32x16 acc[2];
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc[i][r] = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < NKS; ks++) {
+            bf16x8 bc[NPL];
+#pragma unroll
+            for (int p = 0; p < NPL; p++) bc[p] = bq[ks % RING][p];
+            if (ks + RING < NKS) loadB(ks + RING, bq[ks % RING]);
+#pragma unroll
+            for (int mt = 0; mt < 2; mt++) {
+                const bf16x8 av = *reinterpret_cast<const bf16x8*>(&As[0][mt * 32 + (lane & 31)][ks * 16 + 8 * h]);
+                acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bc[0], acc[mt], 0, 0, 0);
+                if constexpr (X3) {
+                    const bf16x8 al = *reinterpret_cast<const bf16x8*>(&As[NPL - 1][mt * 32 + (lane & 31)][ks * 16 + 8 * h]);
+                    acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bc[NPL - 1], acc[mt], 0, 0, 0);
+                    acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bc[0], acc[mt], 0, 0, 0);
+                }
+            }
+        }
+        __syncthreads();  // every wave is done with the tile's dZ2: its LDS takes the dZ1 tile
+        // dZ1 (hi / lo planes) through LDS over the dZ2 image, so that it leaves in 16-B row
+        // pieces rather than 2-B stores of the accumulator layout
+        auto Cs = reinterpret_cast<__bf16 (*)[RM][QZ_CP]>(smem);  // [NPL][RM][QZ_CP]
+#pragma unroll
+        for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int rl = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const bool pos = (Ms[t & 1][rl][w] >> (lane & 31)) & 1u;
+                const float v = pos && m0 + rl < a.B ? acc[mt][r] * a.scale : 0.f;
+                if constexpr (X3) {
+                    split2(v, Cs[0][rl][w * 32 + (lane & 31)], Cs[NPL - 1][rl][w * 32 + (lane & 31)]);
+                } else {
+                    Cs[0][rl][w * 32 + (lane & 31)] = (__bf16)v;
+                }
+                cs += v;
+            }
+        __syncthreads();
+#pragma unroll
+        for (int p = 0; p < NPL; p++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) {  // piece j: row c >> 4, columns 8 (c & 15), c = t + 256 j
+                const int c = tid + 256 * j, row = m0 + (c >> 4);
+                if (row < a.B)
+                    *reinterpret_cast<uint4*>((p ? a.dz1l : a.dz1) + (size_t)row * HID + by * 128 + (c & 15) * 8) =
+                        *reinterpret_cast<const uint4*>(&Cs[p][c >> 4][(c & 15) * 8]);
+            }
+        __syncthreads();  // the dZ1 image has been read: the next tile's dZ2 may be stashed
     }
-    const int lane = threadIdx.x & 63, h = lane >> 5;
-    const int col = by * 128 + (threadIdx.x >> 6) * 32 + (lane & 31);
     cs += __shfl_xor(cs, 32, 64);  // the two row halves of the column
     if (h == 0) {
         atomicAdd(&a.gb1[col], cs);
         atomicAdd(&a.gw1[(size_t)col * K1 + CENTRE_COL], cs);  // d/dW1 of the constant centre input
     }
-}
-template <bool X3>
-__device__ __forceinline__ void qdz1_tile(const Bwd& a, char* smem, int m0, int by, float& cs) {
-    constexpr int NPL = X3 ? 2 : 1;
-    auto As = reinterpret_cast<__bf16 (*)[NPL][RM][40]>(smem);  // [2][NPL][RM][40], pitch 20 words: conflict-free b128 reads
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
-    const int n0 = by * 128 + w * 32;
-    const int gr = tid >> 2, go = (tid & 3) * 8;
-    const bool rowok = m0 + gr < a.B;
-    f32x16 acc[2];
-#pragma unroll
-    for (int i = 0; i < 2; i++)
-#pragma unroll
-        for (int r = 0; r < 16; r++) acc[i][r] = 0.f;
-    auto loadA = [&](int kc, int pl) -> bf16x8 {
-        bf16x8 v;
-        if (rowok) {
-            v = *reinterpret_cast<const bf16x8*>((pl ? a.dz2l : a.dz2) + (size_t)(m0 + gr) * HID2 + kc * 32 + go);
-        } else {
-#pragma unroll
-            for (int t = 0; t < 8; t++) v[t] = (__bf16)0.f;
-        }
-        return v;
-    };
-    bf16x8 bc[NPL][2], bn[NPL][2];
-    auto loadB = [&](int kc, bf16x8 (&b)[NPL][2]) {
-#pragma unroll
-        for (int s = 0; s < 2; s++) {
-            b[0][s] = *reinterpret_cast<const bf16x8*>(a.w2t + w2t_tile(n0 >> 5, kc, s) + lane * 8);
-            if constexpr (X3) b[NPL - 1][s] = *reinterpret_cast<const bf16x8*>(a.w2tl + w2t_tile(n0 >> 5, kc, s) + lane * 8);
-        }
-    };
-    constexpr int NKC = HID2 / 32;
-#pragma unroll
-    for (int pl = 0; pl < NPL; pl++) *reinterpret_cast<bf16x8*>(&As[0][pl][gr][go]) = loadA(0, pl);
-    loadB(0, bc);
-    __syncthreads();
-    for (int kc = 0; kc < NKC; kc++) {
-        const int buf = kc & 1;
-        bf16x8 an[NPL];
-        if (kc + 1 < NKC) {
-#pragma unroll
-            for (int pl = 0; pl < NPL; pl++) an[pl] = loadA(kc + 1, pl);
-            loadB(kc + 1, bn);
-        }
-#pragma unroll
-        for (int mt = 0; mt < 2; mt++)
-#pragma unroll
-            for (int s = 0; s < 2; s++) {
-                const bf16x8 av = *reinterpret_cast<const bf16x8*>(&As[buf][0][mt * 32 + (lane & 31)][s * 16 + 8 * h]);
-                acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bc[0][s], acc[mt], 0, 0, 0);
-                if constexpr (X3) {
-                    const bf16x8 al =
-                        *reinterpret_cast<const bf16x8*>(&As[buf][NPL - 1][mt * 32 + (lane & 31)][s * 16 + 8 * h]);
-                    acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bc[NPL - 1][s], acc[mt], 0, 0, 0);
-                    acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bc[0][s], acc[mt], 0, 0, 0);
-                }
-            }
-        if (kc + 1 < NKC) {
-#pragma unroll
-            for (int pl = 0; pl < NPL; pl++) {
-                *reinterpret_cast<bf16x8*>(&As[buf ^ 1][pl][gr][go]) = an[pl];
-                bc[pl][0] = bn[pl][0];
-                bc[pl][1] = bn[pl][1];
-            }
-        }
-        __syncthreads();
-    }
-    const int col = n0 + (lane & 31);
-#pragma unroll
-    for (int mt = 0; mt < 2; mt++)
-#pragma unroll
-        for (int r = 0; r < 16; r++) {
-            const int row = m0 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            if (row >= a.B) continue;
-            const float hv = (float)a.h1[(size_t)row * HID + col];
-            const float v = hv > 0.f ? acc[mt][r] * a.scale : 0.f;
-            if constexpr (X3) {
-                split2(v, a.dz1[(size_t)row * HID + col], a.dz1l[(size_t)row * HID + col]);
-            } else {
-                a.dz1[(size_t)row * HID + col] = (__bf16)v;
-            }
-            cs += v;
-        }
 }
 template <bool X3 = false>
 __global__ __launch_bounds__(256, 2) void qdz1_kernel(Bwd a) {
@@ -1351,36 +1380,28 @@ __global__ __launch_bounds__(256, 2) void qdz1_kernel(Bwd a) {
 }
 
 // C[m][n] += sum_k A[k][m] B[k][n] (both operands K-major bf16), 128x128 tiles of
-// 4 waves (2x2 of 64x64), K chunks of 32 staged transposed in LDS; gridDim.z splits
-// K. part == NULL: the partial tiles are added to C with f32 atomics; else split z
-// stores its tile to part[z][m][0, gridDim.x * TT) and reduce2_kernel adds the
-// splits in z order (deterministic, and no atomic traffic through L2). Columns
-// n >= Nc are skipped; remap: column n goes to ref_col(n) (fc1's compact K -> the
-// reference's 726).
-constexpr int TT = 128, TKC = 64, TPAD = TKC + 8;
-// 8x8 transpose of bf16: in[r] holds row r (8 consecutive m) -> out[c] holds column c
-// (8 consecutive k); word j of out[c] = in[2j][c] | in[2j+1][c] << 16
-__device__ __forceinline__ void tr8x8(const uint4 (&in)[8], uint4 (&out)[8]) {
-    uint32_t w[8][4];
-#pragma unroll
-    for (int r = 0; r < 8; r++) {
-        w[r][0] = in[r].x;
-        w[r][1] = in[r].y;
-        w[r][2] = in[r].z;
-        w[r][3] = in[r].w;
-    }
-#pragma unroll
-    for (int c = 0; c < 8; c++) {
-        const int q = c >> 1, hi = c & 1;
-        uint32_t o[4];
-#pragma unroll
-        for (int jj = 0; jj < 4; jj++) {
-            const uint32_t a = hi ? (w[2 * jj][q] >> 16) : (w[2 * jj][q] & 0xffffu);
-            const uint32_t b = hi ? (w[2 * jj + 1][q] & 0xffff0000u) : (w[2 * jj + 1][q] << 16);
-            o[jj] = a | b;
-        }
-        out[c] = make_uint4(o[0], o[1], o[2], o[3]);
-    }
+// 4 waves (2x2 of 64x64), K chunks of 64 staged in LDS in their memory order ([k][m]) and
+// read back by ds_read_b64_tr_b16, which hands every lane the 4 consecutive k of its column:
+// no transpose in registers (the 8x8 VALU shuffle this replaced cost about as many cycles
+// as the chunk's MFMAs). gridDim.z splits K. part == NULL: the partial tiles are added to C
+// with f32 atomics; else split z stores its tile to part[z][m][0, gridDim.x * TT) and
+// reduce2_kernel adds the splits in z order (deterministic, and no atomic traffic through
+// L2). Columns n >= Nc are skipped; remap: column n goes to ref_col(n) (fc1's compact K ->
+// the reference's 726).
+// LDS image of a plane: [TKC][TPT] bf16, 320-B rows: a transposed read's 32-lane half takes
+// 4 rows x 64 B at banks 16 q + [0, 16) -- conflict-free (cdna_hip_programming.md T10)
+constexpr int TT = 128, TKC = 64, TPT = TT + 32;
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+// the 32x32x16 operand fragment of rows (columns of the image) c0 .. c0 + 31, k = k0 .. k0 + 15:
+// lane l gets column c0 + (l & 31), k = k0 + 8 (l >> 5) + 0 .. 7 (two transposed reads; lane
+// 4q + p of each 16-lane group addresses row q of a 4-row block, columns 4p .. 4p + 3)
+__device__ __forceinline__ bf16x8 tr_frag(const __bf16* img, int lane_off, int k0, int c0) {
+    const __bf16* p0 = img + k0 * TPT + c0 + lane_off;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0 + 4 * TPT));
+    const s16x4 v[2] = {lo, hi};
+    return __builtin_bit_cast(bf16x8, v);
 }
 // AP / BP: planes of A / B (2 = X3 hi + lo at Al / Bl: products hi*hi + hi*lo + lo*hi).
 // one weight-gradient GEMM of the backward (gemm_tn_kernel's arguments; grid = (N tiles, M tiles, splits))
@@ -1407,20 +1428,13 @@ __device__ __forceinline__ GemmTN tn_net(const GemmTN& g0, int g) {
     return t;
 }
 template <int AP, int BP>
-constexpr int gemm_tn_lds_bytes() { return (AP + BP) * TT * TPAD * 2; }
+constexpr int gemm_tn_lds_bytes() { return (AP + BP) * TKC * TPT * 2; }
 template <int AP = 1, int BP = 1>
 __device__ __forceinline__ void gemm_tn_body(const GemmTN& g, char* smem, int bx, int by, int bz) {
-    // K chunks of 64 staged [m][k] in LDS: thread b < 128 of each operand loads an 8 (k) x 8 (m)
-    // block (8 x 16-B row segments, whole cache lines per wave), transposes it in registers
-    // and writes 8 x 16 B (8 consecutive k of one m): ds_write_b128, conflict-free; the MFMA
-    // operand reads (ds_read_b128, pitch 36 words) are conflict-free too.
-    constexpr int NP = AP > BP ? AP : BP;
-    auto As = reinterpret_cast<__bf16 (*)[TT][TPAD]>(smem);                       // [AP][TT][TPAD]
-    auto Bs = reinterpret_cast<__bf16 (*)[TT][TPAD]>(smem + AP * TT * TPAD * 2);  // [BP][TT][TPAD]
+    constexpr int NP = AP + BP;  // planes staged per chunk: A's, then B's
+    auto img = reinterpret_cast<__bf16 (*)[TKC][TPT]>(smem);  // [NP][TKC][TPT]
     const __bf16* __restrict__ A = g.A;
     const __bf16* __restrict__ Bm = g.Bm;
-    const __bf16* __restrict__ Al = g.Al;
-    const __bf16* __restrict__ Bl = g.Bl;
     const int lda = g.lda, ldb = g.ldb, K = g.K, M = g.M, Nc = g.Nc, kper = g.kper, ldc = g.ldc, remap = g.remap;
     float* __restrict__ C = g.C;
     float* __restrict__ part = g.part;
@@ -1435,36 +1449,35 @@ __device__ __forceinline__ void gemm_tn_body(const GemmTN& g, char* smem, int bx
         for (int j = 0; j < 2; j++)
 #pragma unroll
             for (int r = 0; r < 16; r++) acc[i][j][r] = 0.f;
-    // threads 0..127 stage A, 128..255 stage B: block b = tid & 127 -> k block b & 7, m block b >> 3
-    const bool isA = tid < 128;
-    const int b = tid & 127, kb = b & 7, mb = b >> 3;
-    const int np = isA ? AP : BP;  // planes this thread stages
+    // staging: thread t moves 16 B (8 columns) of rows (t >> 4) + 16 j of every plane; a
+    // 16-lane group reads one 256-B row segment (whole cache lines)
+    const int sr = tid >> 4, sc = (tid & 15) * 8;
     const __bf16* src[NP];
-    src[0] = isA ? A : Bm;
-    if constexpr (NP > 1) src[NP - 1] = isA ? (AP > 1 ? Al : A) : (BP > 1 ? Bl : Bm);
-    const int ld = isA ? lda : ldb, mlim = isA ? M : ldb, mbase = (isA ? m0 : n0) + mb * 8;
-    uint4 rv[NP][8];
+    int ld[NP];
+#pragma unroll
+    for (int p = 0; p < NP; p++) {
+        src[p] = p < AP ? (p == 0 ? A : g.Al) + m0 + sc : (p == AP ? Bm : g.Bl) + n0 + sc;
+        ld[p] = p < AP ? lda : ldb;
+    }
+    uint4 rv[NP][4];
     auto fetch = [&](int k0) {
 #pragma unroll
         for (int p = 0; p < NP; p++)
 #pragma unroll
-            for (int r = 0; r < 8; r++) {
-                const int k = k0 + kb * 8 + r;
-                rv[p][r] = make_uint4(0u, 0u, 0u, 0u);
-                if (p < np && k < ke && mbase < mlim) rv[p][r] = *reinterpret_cast<const uint4*>(src[p] + (size_t)k * ld + mbase);
+            for (int j = 0; j < 4; j++) {
+                const int k = k0 + sr + 16 * j;
+                rv[p][j] = make_uint4(0u, 0u, 0u, 0u);
+                if (k < ke) rv[p][j] = *reinterpret_cast<const uint4*>(src[p] + (size_t)k * ld[p]);
             }
     };
     auto stash = [&]() {
 #pragma unroll
-        for (int p = 0; p < NP; p++) {
-            if (p >= np) break;
-            uint4 t[8];
-            tr8x8(rv[p], t);
-            __bf16 (*dst)[TPAD] = isA ? As[p < AP ? p : 0] : Bs[p < BP ? p : 0];
+        for (int p = 0; p < NP; p++)
 #pragma unroll
-            for (int c = 0; c < 8; c++) *reinterpret_cast<uint4*>(&dst[mb * 8 + c][kb * 8]) = t[c];
-        }
+            for (int j = 0; j < 4; j++) *reinterpret_cast<uint4*>(&img[p][sr + 16 * j][sc]) = rv[p][j];
     };
+    const int q = (lane >> 2) & 3, pq = lane & 3;
+    const int lane_off = (8 * h + q) * TPT + 16 * ((lane >> 4) & 1) + 4 * pq;
     if (kb0 < ke) fetch(kb0);
     for (int k0 = kb0; k0 < ke; k0 += TKC) {
         stash();
@@ -1476,11 +1489,9 @@ __device__ __forceinline__ void gemm_tn_body(const GemmTN& g, char* smem, int bx
 #pragma unroll
             for (int i = 0; i < 2; i++) {
 #pragma unroll
-                for (int p = 0; p < AP; p++)
-                    av[p][i] = *reinterpret_cast<const bf16x8*>(&As[p][wm * 64 + i * 32 + (lane & 31)][s * 16 + 8 * h]);
+                for (int p = 0; p < AP; p++) av[p][i] = tr_frag(&img[p][0][0], lane_off, s * 16, wm * 64 + i * 32);
 #pragma unroll
-                for (int p = 0; p < BP; p++)
-                    bv[p][i] = *reinterpret_cast<const bf16x8*>(&Bs[p][wn * 64 + i * 32 + (lane & 31)][s * 16 + 8 * h]);
+                for (int p = 0; p < BP; p++) bv[p][i] = tr_frag(&img[AP + p][0][0], lane_off, s * 16, wn * 64 + i * 32);
             }
 #pragma unroll
             for (int i = 0; i < 2; i++)
@@ -2111,8 +2122,15 @@ static void launch_tail(const evxm::Bwd& a, int32_t B, const evx_qmlp_grads* g, 
                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
             attr = true;
         }
-        const unsigned nmid = (unsigned)(ndzx * (evxm::HID / 128) + g2.gx * g2.gy * g2.gz);
-        hipLaunchKernelGGL((evxm::bwd_mid_kernel<X3, AP2, BP2>), dim3(nmid), dim3(256), lds, st, a, ndzx, g2);
+        static const bool split_mid = getenv("EVX_SPLIT_MID") != nullptr;  // diagnostic: qdz1 and dW2 timed apart
+        if (split_mid) {
+            hipLaunchKernelGGL((evxm::bwd_mid_kernel<X3, AP2, BP2>), dim3((unsigned)(ndzx * (evxm::HID / 128))), dim3(256),
+                               lds, st, a, ndzx, g2);
+            hipLaunchKernelGGL((evxm::gemm_tn_kernel<AP2, BP2>), dim3(g2.gx, g2.gy, g2.gz), dim3(256), 0, st, g2);
+        } else {
+            const unsigned nmid = (unsigned)(ndzx * (evxm::HID / 128) + g2.gx * g2.gy * g2.gz);
+            hipLaunchKernelGGL((evxm::bwd_mid_kernel<X3, AP2, BP2>), dim3(nmid), dim3(256), lds, st, a, ndzx, g2);
+        }
         hipLaunchKernelGGL((evxm::gemm_tn_kernel<AP1, BP1>), dim3(g1.gx, g1.gy, g1.gz), dim3(256), 0, st, g1);
         evxm::Red2 r{g->part, g2.gz, g1.part, g1.gz, g1.gx * evxm::TT, 4 * evxm::NCELL, X3 ? 3 : 1,
                      g->w1, g->b1, g->w2, g->b2, g->w3, g->b3, ss,
