@@ -915,6 +915,189 @@ __global__ __launch_bounds__(512, 1) void qact3_kernel(Fwd a0) {
     ACT_ST(11);
 }
 
+// The x3 act on 64-row tiles of 4 waves (256 threads, ACT3H_LDS = 77 KB): two independent
+// workgroups per CU, so one's epilogues, barriers, table loads and fc3 run under the other's
+// MFMAs (the 128-row, 8-wave form serialises them: ~1/3 MFMA-busy). Same arithmetic per row as
+// qact3_kernel: wave w owns columns [64 w, 64 w + 64) of each fc1 half and of fc2 (2 column
+// tiles), both 32-row slabs.
+constexpr int A3H_HBYTES = 2 * 64 * A3_HP * 2;  // 67,584: both H1 half planes of 64 rows
+static_assert(A3H_HBYTES >= 64 * ACT_H2P * 4, "H2 overlays the H1 planes");
+static_assert(A3H_HBYTES >= 2 * 64 * (KC1 + 8) * 2, "fc1 A staging overlays the H1 planes");
+constexpr int ACT3H_LDS = A3H_HBYTES + NACT * HID2 * 4 + 64 * 4 + 32 * 4 + ACT3_OCC;
+template <bool GR = false, int DM = 1>
+__global__ __launch_bounds__(256, 2) void qact3h_kernel(Fwd a0) {
+    Fwd ag;
+    if constexpr (GR) ag = fwd_net(a0, (int)blockIdx.y);
+    const Fwd& a = GR ? ag : a0;
+    extern __shared__ __attribute__((aligned(16))) char dsm[];
+    auto Hh = reinterpret_cast<__bf16 (*)[A3_HP]>(dsm);
+    auto Hl = reinterpret_cast<__bf16 (*)[A3_HP]>(dsm + 64 * A3_HP * 2);
+    auto H2s = reinterpret_cast<float (*)[ACT_H2P]>(dsm);
+    auto W3s = reinterpret_cast<float (*)[HID2]>(dsm + A3H_HBYTES);
+    int* posS = reinterpret_cast<int*>(dsm + A3H_HBYTES + NACT * HID2 * 4);
+    uint32_t* phS = reinterpret_cast<uint32_t*>(dsm + A3H_HBYTES + NACT * HID2 * 4 + 64 * 4);
+    uint4* occT = reinterpret_cast<uint4*>(dsm + A3H_HBYTES + NACT * HID2 * 4 + 64 * 4 + 32 * 4);
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+    const int m0 = blockIdx.x * 64;
+    ACT_ST(0);
+    for (int i = tid; i < NACT * HID2; i += 256) W3s[i / HID2][i % HID2] = a.w3[i];
+    if (DM == 1 && tid >= 224) {  // the tile's 32 row-pair dropout hashes (published by the barriers below)
+        const int r2 = m0 + 2 * (tid - 224);
+        phS[tid - 224] = r2 < a.N ? drop_row(a.drop_seed, a.drop_stream, (a.drop_row0 + (uint32_t)krow(a, r2)) >> 1) : 0u;
+    }
+    bool fast = false;
+    if (a.stat) {  // tile-uniform: every row at the table's fire step, centre inside the map
+        bool ok = true;
+        if (tid < 64) {
+            int pos = 0;
+            if (m0 + tid < a.N) {
+                const evx_obs ob = a.obs[orow(a, m0 + tid)];
+                ok = min(max(ob.fire_step, 0), a.t_max) == a.stat_fs && ob.cx >= a.stat_x0 &&
+                     ob.cx < a.stat_x0 + a.stat_nx && ob.cy >= 0 && ob.cy <= a.W + 1;
+                pos = ok ? (ob.cx - a.stat_x0) * (a.W + 2) + ob.cy : 0;
+            }
+            posS[tid] = pos;
+        }
+        {  // the occupancy-fragment table (published by the same barrier)
+            const uint32_t bits = (uint32_t)tid, one = 0x3f80u;
+            uint32_t v[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) v[j] = ((bits >> (2 * j)) & 1u) * one | (((bits >> (2 * j + 1)) & 1u) * one) << 16;
+            occT[bits] = make_uint4(v[0], v[1], v[2], v[3]);
+        }
+        fast = __syncthreads_and(ok);  // also publishes posS
+    }
+    ACT_ST(1);
+    f32x16 acc2[2][2];
+#pragma unroll
+    for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+        for (int nt = 0; nt < 2; nt++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc2[mt][nt][r] = 0.f;
+#pragma unroll
+    for (int hh = 0; hh < 2; hh++) {
+        f32x16 acc[2][2];
+        const int col0 = hh * 256 + w * 64;  // the wave's column tiles: col0, col0 + 32
+        if (fast) {
+            // fc1 = table[centre] + the occupancy columns x bits (qact3_kernel)
+            uint32_t occ[2][4];
+#pragma unroll
+            for (int mt = 0; mt < 2; mt++) {
+                const int row = m0 + mt * 32 + (lane & 31);
+                uint4 o = make_uint4(0u, 0u, 0u, 0u);
+                if (row < a.N) o = *reinterpret_cast<const uint4*>(&a.obs[orow(a, row)].occ[0]);
+                occ[mt][0] = o.x;
+                occ[mt][1] = o.y;
+                occ[mt][2] = o.z;
+                occ[mt][3] = o.w;
+            }
+            const uint32_t cofs = (uint32_t)(col0 + (lane & 31));
+#pragma unroll
+            for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    const int rl = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    const uint32_t o = (uint32_t)posS[rl] * (uint32_t)HID + cofs;
+                    acc[mt][0][r] = a.stat[o];
+                    acc[mt][1][r] = a.stat[o + 32];
+                }
+#pragma unroll 2
+            for (int ks = 0; ks < 8; ks++) {  // k-step: cells 16 ks + 8 h .. + 7 of the 128
+                bf16x8 bh[2], bl[2];
+#pragma unroll
+                for (int nt = 0; nt < 2; nt++) {
+                    const size_t o = w1o_tile((col0 >> 5) + nt, ks >> 1, ks & 1) + lane * 8;
+                    bh[nt] = *reinterpret_cast<const bf16x8*>(a.w1o + o);
+                    bl[nt] = *reinterpret_cast<const bf16x8*>(a.w1ol + o);
+                }
+                const int c0 = ks * 16 + 8 * h;  // multiple of 8: the 8 bits sit in one word
+#pragma unroll
+                for (int mt = 0; mt < 2; mt++) {
+                    const uint32_t wd = (c0 >> 5) == 0 ? occ[mt][0] : (c0 >> 5) == 1 ? occ[mt][1]
+                                      : (c0 >> 5) == 2 ? occ[mt][2] : occ[mt][3];
+                    const bf16x8 av = __builtin_bit_cast(bf16x8, occT[(wd >> (c0 & 31)) & 0xffu]);
+#pragma unroll
+                    for (int nt = 0; nt < 2; nt++) {
+                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bh[nt], acc[mt][nt], 0, 0, 0);
+                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bl[nt], acc[mt][nt], 0, 0, 0);
+                    }
+                }
+            }
+        } else {
+            fc1_tile<2, 2, 4, true, 2>(a, m0, col0, false, dsm, acc);  // ends with a barrier: A buffers free
+        }
+        ACT_ST(2 + 4 * hh);
+        float bias[2];
+#pragma unroll
+        for (int nt = 0; nt < 2; nt++) bias[nt] = fast ? 0.f : a.b1[col0 + nt * 32 + (lane & 31)];  // the table holds the bias
+#pragma unroll
+        for (int mt = 0; mt < 2; mt++)
+            fc1_slab_m<2, A3_HP, true, DM>(a, acc[mt], bias, m0 + mt * 32, hh * 256, w * 64,
+                                           reinterpret_cast<__bf16 (*)[A3_HP]>(&Hh[mt * 32][0]),
+                                           reinterpret_cast<__bf16 (*)[A3_HP]>(&Hl[mt * 32][0]), phS + mt * 16);
+        ACT_ST(3 + 4 * hh);
+        __syncthreads();
+        ACT_ST(4 + 4 * hh);
+        // fc2 over K = [256 hh, 256 hh + 256): wave w -> columns [64 w, 64 w + 64)
+        bf16x8 bc[2][2], bn[2][2], lc[2][2], ln[2][2];  // [nt][s]
+        auto loadB = [&](int kc, bf16x8 (&b)[2][2], bf16x8 (&l)[2][2]) {
+#pragma unroll
+            for (int nt = 0; nt < 2; nt++)
+#pragma unroll
+                for (int s = 0; s < 2; s++) {
+                    const size_t o = w2_tile(w * 2 + nt, hh * 8 + kc, s) + lane * 8;
+                    b[nt][s] = *reinterpret_cast<const bf16x8*>(a.w2 + o);
+                    l[nt][s] = *reinterpret_cast<const bf16x8*>(a.w2l + o);
+                }
+        };
+        loadB(0, bc, lc);
+        for (int kc = 0; kc < 8; kc++) {
+            if (kc + 1 < 8) loadB(kc + 1, bn, ln);
+#pragma unroll
+            for (int s = 0; s < 2; s++)
+#pragma unroll
+                for (int mt = 0; mt < 2; mt++) {
+                    const int rr = mt * 32 + (lane & 31), kk = kc * 32 + s * 16 + 8 * h;
+                    const bf16x8 ah = *reinterpret_cast<const bf16x8*>(&Hh[rr][kk]);
+                    const bf16x8 al = *reinterpret_cast<const bf16x8*>(&Hl[rr][kk]);
+#pragma unroll
+                    for (int nt = 0; nt < 2; nt++) {
+                        acc2[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bc[nt][s], acc2[mt][nt], 0, 0, 0);
+                        acc2[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, lc[nt][s], acc2[mt][nt], 0, 0, 0);
+                        acc2[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bc[nt][s], acc2[mt][nt], 0, 0, 0);
+                    }
+                }
+#pragma unroll
+            for (int nt = 0; nt < 2; nt++)
+#pragma unroll
+                for (int s = 0; s < 2; s++) {
+                    bc[nt][s] = bn[nt][s];
+                    lc[nt][s] = ln[nt][s];
+                }
+        }
+        ACT_ST(5 + 4 * hh);
+        __syncthreads();  // every wave is done with this half: the next half / H2 reuse the planes
+    }
+#pragma unroll
+    for (int nt = 0; nt < 2; nt++) {
+        const int col = w * 64 + nt * 32 + (lane & 31);
+        const float bias = a.b2[col];
+#pragma unroll
+        for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const float v = acc2[mt][nt][r] + bias;
+                H2s[mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h][col] = v > 0.f ? v : 0.f;
+            }
+    }
+    __syncthreads();
+    ACT_ST(10);
+    const int row = tid >> 2;
+    fc3_act(a, &H2s[row][0], W3s, orow(a, m0 + row), m0 + row < a.N);
+    ACT_ST(11);
+}
+
 // ------------------------------------------------------------ fc2 + fc3
 // X3: A = H1 hi / lo planes, B = fc2.weight hi / lo (3 MFMAs per fragment pair)
 template <bool X3 = false, bool GR = false>
@@ -1832,6 +2015,24 @@ int evx_qmlp_pack3(const float* w1, const float* b1, const float* w2, uint16_t* 
 // the x3 act kernel for the dropout mode of a (fc1_slab_m)
 extern "C++" template <bool GR>
 static void launch_act3(const evxm::Fwd& a, int32_t n, int nets, hipStream_t st) {
+    static const bool half = getenv("EVX_ACT3_FULLTILE") == nullptr;  // 64-row tiles (A/B switch)
+    if (half) {
+        static bool attr = false;
+        if (!attr) {
+            const void* kh[3] = {(const void*)evxm::qact3h_kernel<GR, 0>, (const void*)evxm::qact3h_kernel<GR, 1>,
+                                 (const void*)evxm::qact3h_kernel<GR, 2>};
+            for (const void* k : kh) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, evxm::ACT3H_LDS);
+            attr = true;
+        }
+        const dim3 grid((unsigned)((n + 63) / 64), (unsigned)nets);
+        if (a.drop_mask)
+            hipLaunchKernelGGL((evxm::qact3h_kernel<GR, 2>), grid, dim3(256), evxm::ACT3H_LDS, st, a);
+        else if (a.drop_thresh)
+            hipLaunchKernelGGL((evxm::qact3h_kernel<GR, 1>), grid, dim3(256), evxm::ACT3H_LDS, st, a);
+        else
+            hipLaunchKernelGGL((evxm::qact3h_kernel<GR, 0>), grid, dim3(256), evxm::ACT3H_LDS, st, a);
+        return;
+    }
     const dim3 grid((unsigned)((n + 127) / 128), (unsigned)nets);
     if (a.drop_mask)
         hipLaunchKernelGGL((evxm::qact3_kernel<GR, 2>), grid, dim3(512), evxm::ACT3_LDS, st, a);
@@ -2048,8 +2249,12 @@ int evx_qmlp_forward2(const evx_layout* lay, int32_t n, const evx_obs* obs0, con
 }
 
 // split-K of the weight-gradient GEMMs: about 256 workgroups over `tiles` output tiles
+static int ksplit_wgs() {  // target workgroups of a split-K weight-gradient launch
+    static const int n = getenv("EVX_KSPLIT_WG") ? atoi(getenv("EVX_KSPLIT_WG")) : 256;
+    return n > 0 ? n : 256;
+}
 static int ksplit_kper(int B, int tiles) {
-    const int S = (256 + tiles - 1) / tiles;
+    const int S = (ksplit_wgs() + tiles - 1) / tiles;
     int kper = (B + S - 1) / S;
     return (kper + evxm::TKC - 1) / evxm::TKC * evxm::TKC;
 }
