@@ -580,6 +580,140 @@ __device__ __forceinline__ void fc3_act(const Fwd& a, const float* hrow, const f
 }
 
 // ------------------------------------------------------------ fused act
+constexpr int A3_HP = 256 + 8;  // x3 act: H1 half-plane / H2 plane row pitch (bf16), 528 B
+// X3 fc2 -> fc3 of a 64-row tile of 4 waves. fc2 runs with swapped operands (A = W2 fragments,
+// B = H1 rows), so wave w's acc[mt][nt] is an H2^T tile: lane l holds tile row (batch row)
+// 32 mt + (l & 31), register r column n = 64 w + 32 nt + (r & 3) + 8 (r >> 2) + 4 (l >> 5).
+// fc3t_x3: H2 = relu(acc + b2) (to a.h2 in 16-B row pieces when set: the learner's backward),
+// split into bf16 hi / lo in registers, and Q^T = W3 . H2^T on the matrix cores straight from
+// the accumulators (x3: hi*hi + hi*lo + lo*hi): registers 8 kb .. 8 kb + 7 of a tile are the B
+// operand of the 16 columns n = 64 w + 32 nt + 16 kb + 4 (l >> 5) + {0..3, 8..11} (a fixed
+// permutation of K, which the A operand -- W3's 5 rows padded to 32, split in registers --
+// follows). The 4 waves' partial Q^T over their 64 columns meet in LDS (red: [4][5][64] f32)
+// and are added in wave order; DQNAgent.act's epsilon-greedy follows (q_out). Used by
+// qfc23<X3> and qact3h alike (act and forward give the same Q bit for bit). act_rows: Q and
+// actions go to orow (act), else to the batch row. (Storing H2 and 4-thread f32 dot products
+// in fc3_act cost ~13k cycles per act tile.)
+__device__ __forceinline__ void q_out(const Fwd& a, float (&qv)[NACT], int row) {
+#pragma unroll
+    for (int t = 0; t < NACT; t++) qv[t] += a.b3[t];
+    if (a.q) {
+#pragma unroll
+        for (int t = 0; t < NACT; t++) a.q[(size_t)row * NACT + t] = qv[t];
+    }
+    if (a.actions) {  // DQNAgent.act: epsilon-greedy over argmax (first maximum)
+        int best = 0;
+        float bv = qv[0];
+#pragma unroll
+        for (int t = 1; t < NACT; t++)
+            if (qv[t] > bv) {
+                bv = qv[t];
+                best = t;
+            }
+        if (a.epsilon > 0.f) {
+            const uint64_t c = (uint64_t)row + a.act_offset;
+            const u4 r = philox((uint32_t)c, (uint32_t)(c >> 32), 0xac7u, 0u, (uint32_t)a.act_seed,
+                                (uint32_t)(a.act_seed >> 32));
+            if (u01(r.x) <= a.epsilon) best = (int)((uint64_t)r.y * (uint64_t)NACT >> 32);
+        }
+        a.actions[row] = best;
+    }
+}
+__device__ __forceinline__ void fc3t_x3(const Fwd& a, const f32x16 (&acc)[2][2], const float (*W3s)[HID2],
+                                        float* red, int m0, bool act_rows) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, j = lane & 31;
+    const int t = lane & 31;  // A row: action (< NACT) or padding
+    f32x16 qp[2];
+#pragma unroll
+    for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+        for (int r = 0; r < 16; r++) qp[mt][r] = 0.f;
+#pragma unroll
+    for (int nt = 0; nt < 2; nt++) {
+        const int nb = w * 64 + nt * 32 + 4 * h;  // + (r & 3) + 8 (r >> 2)
+        float b2v[16];
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            const float4 bv = *reinterpret_cast<const float4*>(&a.b2[nb + 8 * g]);
+            b2v[4 * g] = bv.x;
+            b2v[4 * g + 1] = bv.y;
+            b2v[4 * g + 2] = bv.z;
+            b2v[4 * g + 3] = bv.w;
+        }
+        bf16x8 wh[2], wl[2];  // W3 in the K order of k-blocks 0 and 1 of this column tile
+#pragma unroll
+        for (int kb = 0; kb < 2; kb++) {
+            float u[8];
+            if (t < NACT) {
+                const float4 u0 = *reinterpret_cast<const float4*>(&W3s[t][nb + 16 * kb]);
+                const float4 u1 = *reinterpret_cast<const float4*>(&W3s[t][nb + 16 * kb + 8]);
+                u[0] = u0.x; u[1] = u0.y; u[2] = u0.z; u[3] = u0.w;
+                u[4] = u1.x; u[5] = u1.y; u[6] = u1.z; u[7] = u1.w;
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; e++) u[e] = 0.f;
+            }
+#pragma unroll
+            for (int e = 0; e < 8; e++) {
+                __bf16 hi, lo;
+                split2(u[e], hi, lo);
+                wh[kb][e] = hi;
+                wl[kb][e] = lo;
+            }
+        }
+#pragma unroll
+        for (int mt = 0; mt < 2; mt++) {
+            const int row = m0 + mt * 32 + j;
+            float v[16];
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const float x = acc[mt][nt][r] + b2v[r];
+                v[r] = x > 0.f ? x : 0.f;
+            }
+            if (a.h2 && row < a.N) {
+#pragma unroll
+                for (int g = 0; g < 4; g++)
+                    *reinterpret_cast<float4*>(&a.h2[(size_t)row * HID2 + nb + 8 * g]) =
+                        make_float4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
+            }
+#pragma unroll
+            for (int kb = 0; kb < 2; kb++) {
+                bf16x8 bh, bl;
+#pragma unroll
+                for (int e = 0; e < 8; e++) {
+                    __bf16 hi, lo;
+                    split2(v[8 * kb + e], hi, lo);
+                    bh[e] = hi;
+                    bl[e] = lo;
+                }
+                qp[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh[kb], bh, qp[mt], 0, 0, 0);
+                qp[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh[kb], bl, qp[mt], 0, 0, 0);
+                qp[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl[kb], bh, qp[mt], 0, 0, 0);
+            }
+        }
+    }
+    // qp[mt] = this wave's Q^T partial: lane l holds tile row 32 mt + (l & 31), actions
+    // 4 (l >> 5) + r (r < 4; valid below NACT)
+    auto R = reinterpret_cast<float (*)[NACT][64]>(red);  // [4][NACT][64]
+#pragma unroll
+    for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int act = 4 * h + r;
+            if (act < NACT) R[w][act][mt * 32 + j] = qp[mt][r];
+        }
+    __syncthreads();
+    if (tid < 64) {
+        const int rt = m0 + tid;
+        if (rt < a.N) {
+            float qv[NACT];
+#pragma unroll
+            for (int k = 0; k < NACT; k++) qv[k] = ((R[0][k][tid] + R[1][k][tid]) + R[2][k][tid]) + R[3][k][tid];
+            q_out(a, qv, act_rows ? orow(a, rt) : rt);
+        }
+    }
+}
+
 // DQNAgent.act for 128 rows per workgroup (8 waves) in one launch: fc1 as
 // qfc1_kernel<4, 2, 8>, H1 kept in LDS (bf16, never written to HBM), fc2 with wave w
 // on columns [32w, 32w + 32) over all 128 rows (A fragments from the H1 tile, W2
@@ -729,22 +863,17 @@ __global__ __launch_bounds__(512, 1) void qact_kernel(Fwd a) {
     fc3_act(a, &H2s[row][0], W3s, orow(a, m0 + row), m0 + row < a.N);
 }
 
-// X3 (f32-accurate) act: the H1 tile of 128 rows would need 256 KB as hi + lo planes, so
-// H1 goes through LDS in two column halves. fc1 runs once over all 512 columns (the
-// observations are expanded once), wave w owning column tiles 32w (half 0) and 256 + 32w
-// (half 1); half hh's tiles go into the two LDS planes, then fc2 accumulates over that
-// half of its K (3 MFMAs per fragment pair: hi*hi, hi*lo, lo*hi). The A staging of fc1,
-// the H1 half planes and finally H2 share one LDS region.
-constexpr int A3_HP = 256 + 8;                     // H1 half-plane row pitch (bf16)
-constexpr int A3_HBYTES = 2 * 128 * A3_HP * 2;     // 135,168: both planes
-static_assert(A3_HBYTES >= 128 * ACT_H2P * 4, "H2 overlays the H1 planes");
-static_assert(A3_HBYTES >= 2 * 128 * (KC1 + 8) * 2, "fc1 A staging overlays the H1 planes");
-// + W3 + window centres + pair hashes + the occupancy-fragment table (table path: byte of 8 cell
-// bits -> the 8 bf16 A values, 0 or 1.0, of one MFMA k-step; one ds_read_b128 instead of ~25 VALU)
+// X3 (f32-accurate) act: H1 goes through LDS in two column halves (hi + lo planes of a whole
+// 512-column tile would not fit beside a second workgroup). fc1 runs once over all 512 columns
+// (the observations are expanded once per half on the full path); half hh's tiles go into the
+// two LDS planes, then fc2 accumulates over that half of its K (3 MFMAs per fragment pair:
+// hi*hi, hi*lo, lo*hi). The A staging of fc1, the H1 half planes and finally H2 share one
+// LDS region.
+// the occupancy-fragment table (table path: byte of 8 cell bits -> the 8 bf16 A values, 0 or
+// 1.0, of one MFMA k-step; one ds_read_b128 instead of ~25 VALU)
 constexpr int ACT3_OCC = 256 * 16;
-constexpr int ACT3_LDS = A3_HBYTES + NACT * HID2 * 4 + 128 * 4 + 64 * 4 + ACT3_OCC;
 // diagnostic build (-DEVX_ACT_STAMPS, tools/act_stamps.py): wave 0's s_memtime at the phase
-// boundaries of every workgroup (evx_diag_act_stamps)
+// boundaries of every workgroup (evx_diag_act_stamps, qact3h_kernel)
 #ifdef EVX_ACT_STAMPS
 constexpr int ACT_NST = 12;
 __device__ long long g_act_st[8192 * ACT_NST];
@@ -756,172 +885,12 @@ __device__ long long g_act_st[8192 * ACT_NST];
 #else
 #define ACT_ST(i)
 #endif
-// GR: grouped act, blockIdx.y = net (interleaved rows); DM: the dropout mode (fc1_slab_m)
-template <bool GR = false, int DM = 1>
-__global__ __launch_bounds__(512, 1) void qact3_kernel(Fwd a0) {
-    Fwd ag;
-    if constexpr (GR) ag = fwd_net(a0, (int)blockIdx.y);
-    const Fwd& a = GR ? ag : a0;
-    extern __shared__ __attribute__((aligned(16))) char dsm[];
-    auto Hh = reinterpret_cast<__bf16 (*)[A3_HP]>(dsm);
-    auto Hl = reinterpret_cast<__bf16 (*)[A3_HP]>(dsm + 128 * A3_HP * 2);
-    auto H2s = reinterpret_cast<float (*)[ACT_H2P]>(dsm);
-    auto W3s = reinterpret_cast<float (*)[HID2]>(dsm + A3_HBYTES);
-    int* posS = reinterpret_cast<int*>(dsm + A3_HBYTES + NACT * HID2 * 4);
-    uint32_t* phS = reinterpret_cast<uint32_t*>(dsm + A3_HBYTES + NACT * HID2 * 4 + 128 * 4);
-    uint4* occT = reinterpret_cast<uint4*>(dsm + A3_HBYTES + NACT * HID2 * 4 + 128 * 4 + 64 * 4);
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
-    const int m0 = blockIdx.x * 128;
-    ACT_ST(0);
-    for (int i = tid; i < NACT * HID2; i += 512) W3s[i / HID2][i % HID2] = a.w3[i];
-    if (DM == 1 && tid >= 448) {  // the tile's 64 row-pair dropout hashes (published by the barriers below)
-        const int r2 = m0 + 2 * (tid - 448);
-        phS[tid - 448] = r2 < a.N ? drop_row(a.drop_seed, a.drop_stream, (a.drop_row0 + (uint32_t)krow(a, r2)) >> 1) : 0u;
-    }
-    bool fast = false;
-    if (a.stat) {  // tile-uniform: every row at the table's fire step, centre inside the map
-        bool ok = true;
-        if (tid < 128) {
-            int pos = 0;
-            if (m0 + tid < a.N) {
-                const evx_obs ob = a.obs[orow(a, m0 + tid)];
-                ok = min(max(ob.fire_step, 0), a.t_max) == a.stat_fs && ob.cx >= a.stat_x0 &&
-                     ob.cx < a.stat_x0 + a.stat_nx && ob.cy >= 0 && ob.cy <= a.W + 1;
-                pos = ok ? (ob.cx - a.stat_x0) * (a.W + 2) + ob.cy : 0;
-            }
-            posS[tid] = pos;
-        }
-        if (tid >= 256) {  // the occupancy-fragment table (published by the same barrier)
-            const uint32_t bits = (uint32_t)(tid - 256), one = 0x3f80u;
-            uint32_t v[4];
-#pragma unroll
-            for (int j = 0; j < 4; j++) v[j] = ((bits >> (2 * j)) & 1u) * one | (((bits >> (2 * j + 1)) & 1u) * one) << 16;
-            occT[bits] = make_uint4(v[0], v[1], v[2], v[3]);
-        }
-        fast = __syncthreads_and(ok);  // also publishes posS
-    }
-    ACT_ST(1);
-    f32x16 acc2[4];
-#pragma unroll
-    for (int mt = 0; mt < 4; mt++)
-#pragma unroll
-        for (int r = 0; r < 16; r++) acc2[mt][r] = 0.f;
-    // One column half at a time: fc1 of the half (wave w: column tile hh * 8 + w), its H1 slabs
-    // into the LDS planes, fc2 over that half of K. Only one half's fc1 accumulators are ever
-    // live (64 VGPRs; both halves at once spilled ~100 VGPRs to scratch); the full path expands
-    // the observations once per half.
-#pragma unroll
-    for (int hh = 0; hh < 2; hh++) {
-        f32x16 acc[4][1];
-        const int col0 = hh * 256 + w * 32;
-        if (fast) {
-            // fc1 = table[centre] (f32: static features x W1 + b1, x3-accurate) + the occupancy
-            // columns x bits (K = 128 cells; bits exact in bf16: hi and lo weights, 2 MFMAs)
-            uint32_t occ[4][4];  // occupancy bits of the wave's 32-row slabs
-#pragma unroll
-            for (int mt = 0; mt < 4; mt++) {
-                const int row = m0 + mt * 32 + (lane & 31);
-                uint4 o = make_uint4(0u, 0u, 0u, 0u);
-                if (row < a.N) o = *reinterpret_cast<const uint4*>(&a.obs[orow(a, row)].occ[0]);
-                occ[mt][0] = o.x;
-                occ[mt][1] = o.y;
-                occ[mt][2] = o.z;
-                occ[mt][3] = o.w;
-            }
-            // 32-bit offsets from the uniform table base: one VGPR per load address, not two
-            const uint32_t cofs = (uint32_t)(col0 + (lane & 31));
-#pragma unroll
-            for (int mt = 0; mt < 4; mt++)
-#pragma unroll
-                for (int r = 0; r < 16; r++) {
-                    const int rl = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    acc[mt][0][r] = a.stat[(uint32_t)posS[rl] * (uint32_t)HID + cofs];
-                }
-#pragma unroll 2
-            for (int ks = 0; ks < 8; ks++) {  // k-step: cells 16 ks + 8 h .. + 7 of the 128
-                const bf16x8 bh = *reinterpret_cast<const bf16x8*>(a.w1o + w1o_tile(hh * 8 + w, ks >> 1, ks & 1) + lane * 8);
-                const bf16x8 bl = *reinterpret_cast<const bf16x8*>(a.w1ol + w1o_tile(hh * 8 + w, ks >> 1, ks & 1) + lane * 8);
-                const int c0 = ks * 16 + 8 * h;  // multiple of 8: the 8 bits sit in one word
-#pragma unroll
-                for (int mt = 0; mt < 4; mt++) {
-                    const uint32_t wd = (c0 >> 5) == 0 ? occ[mt][0] : (c0 >> 5) == 1 ? occ[mt][1]
-                                      : (c0 >> 5) == 2 ? occ[mt][2] : occ[mt][3];
-                    const uint32_t bits = (wd >> (c0 & 31)) & 0xffu;
-                    const bf16x8 av = __builtin_bit_cast(bf16x8, occT[bits]);
-                    acc[mt][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bh, acc[mt][0], 0, 0, 0);
-                    acc[mt][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bl, acc[mt][0], 0, 0, 0);
-                }
-            }
-        } else {
-            fc1_tile<4, 1, 8, true, 2>(a, m0, col0, false, dsm, acc);  // ends with a barrier: A buffers free
-        }
-        ACT_ST(2 + 4 * hh);
-        const float bias[1] = {fast ? 0.f : a.b1[col0 + (lane & 31)]};  // the table holds the bias
-#pragma unroll
-        for (int mt = 0; mt < 4; mt++)
-            fc1_slab_m<1, A3_HP, true, DM>(a, acc[mt], bias, m0 + mt * 32, hh * 256, w * 32,
-                                           reinterpret_cast<__bf16 (*)[A3_HP]>(&Hh[mt * 32][0]),
-                                           reinterpret_cast<__bf16 (*)[A3_HP]>(&Hl[mt * 32][0]), phS + mt * 16);
-        ACT_ST(3 + 4 * hh);
-        __syncthreads();
-        ACT_ST(4 + 4 * hh);
-        // fc2 over K = [256 hh, 256 hh + 256): wave w -> columns [32w, 32w + 32)
-        bf16x8 bc[2], bn[2], lc[2], ln[2];
-        auto loadB = [&](int kc, bf16x8 (&b)[2], bf16x8 (&l)[2]) {
-#pragma unroll
-            for (int s = 0; s < 2; s++) {
-                b[s] = *reinterpret_cast<const bf16x8*>(a.w2 + w2_tile(w, hh * 8 + kc, s) + lane * 8);
-                l[s] = *reinterpret_cast<const bf16x8*>(a.w2l + w2_tile(w, hh * 8 + kc, s) + lane * 8);
-            }
-        };
-        loadB(0, bc, lc);
-        for (int kc = 0; kc < 8; kc++) {
-            if (kc + 1 < 8) loadB(kc + 1, bn, ln);
-#pragma unroll
-            for (int s = 0; s < 2; s++)
-#pragma unroll
-                for (int mt = 0; mt < 4; mt++) {
-                    const int rr = mt * 32 + (lane & 31), kk = kc * 32 + s * 16 + 8 * h;
-                    const bf16x8 ah = *reinterpret_cast<const bf16x8*>(&Hh[rr][kk]);
-                    const bf16x8 al = *reinterpret_cast<const bf16x8*>(&Hl[rr][kk]);
-                    acc2[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bc[s], acc2[mt], 0, 0, 0);
-                    acc2[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, lc[s], acc2[mt], 0, 0, 0);
-                    acc2[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bc[s], acc2[mt], 0, 0, 0);
-                }
-#pragma unroll
-            for (int s = 0; s < 2; s++) {
-                bc[s] = bn[s];
-                lc[s] = ln[s];
-            }
-        }
-        ACT_ST(5 + 4 * hh);
-        __syncthreads();  // every wave is done with this half: the next half / H2 reuse the planes
-    }
-    {
-        const int col = w * 32 + (lane & 31);
-        const float bias = a.b2[col];
-#pragma unroll
-        for (int mt = 0; mt < 4; mt++)
-#pragma unroll
-            for (int r = 0; r < 16; r++) {
-                const float v = acc2[mt][r] + bias;
-                H2s[mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h][col] = v > 0.f ? v : 0.f;
-            }
-    }
-    __syncthreads();
-    ACT_ST(10);
-    const int row = tid >> 2;
-    fc3_act(a, &H2s[row][0], W3s, orow(a, m0 + row), m0 + row < a.N);
-    ACT_ST(11);
-}
-
 // The x3 act on 64-row tiles of 4 waves (256 threads, ACT3H_LDS = 77 KB): two independent
 // workgroups per CU, so one's epilogues, barriers, table loads and fc3 run under the other's
-// MFMAs (the 128-row, 8-wave form serialises them: ~1/3 MFMA-busy). Same arithmetic per row as
-// qact3_kernel: wave w owns columns [64 w, 64 w + 64) of each fc1 half and of fc2 (2 column
-// tiles), both 32-row slabs.
+// MFMAs (a 128-row, 8-wave form serialised them: ~1/3 MFMA-busy, 747 vs 658 us per 524288
+// rows). Same arithmetic per row as the x3 forward (qfc1 + qfc23): wave w owns columns
+// [64 w, 64 w + 64) of each fc1 half and of fc2 (2 column tiles), both 32-row slabs.
 constexpr int A3H_HBYTES = 2 * 64 * A3_HP * 2;  // 67,584: both H1 half planes of 64 rows
-static_assert(A3H_HBYTES >= 64 * ACT_H2P * 4, "H2 overlays the H1 planes");
 static_assert(A3H_HBYTES >= 2 * 64 * (KC1 + 8) * 2, "fc1 A staging overlays the H1 planes");
 constexpr int ACT3H_LDS = A3H_HBYTES + NACT * HID2 * 4 + 64 * 4 + 32 * 4 + ACT3_OCC;
 template <bool GR = false, int DM = 1>
@@ -932,7 +901,6 @@ __global__ __launch_bounds__(256, 2) void qact3h_kernel(Fwd a0) {
     extern __shared__ __attribute__((aligned(16))) char dsm[];
     auto Hh = reinterpret_cast<__bf16 (*)[A3_HP]>(dsm);
     auto Hl = reinterpret_cast<__bf16 (*)[A3_HP]>(dsm + 64 * A3_HP * 2);
-    auto H2s = reinterpret_cast<float (*)[ACT_H2P]>(dsm);
     auto W3s = reinterpret_cast<float (*)[HID2]>(dsm + A3H_HBYTES);
     int* posS = reinterpret_cast<int*>(dsm + A3H_HBYTES + NACT * HID2 * 4);
     uint32_t* phS = reinterpret_cast<uint32_t*>(dsm + A3H_HBYTES + NACT * HID2 * 4 + 64 * 4);
@@ -980,7 +948,8 @@ __global__ __launch_bounds__(256, 2) void qact3h_kernel(Fwd a0) {
         f32x16 acc[2][2];
         const int col0 = hh * 256 + w * 64;  // the wave's column tiles: col0, col0 + 32
         if (fast) {
-            // fc1 = table[centre] + the occupancy columns x bits (qact3_kernel)
+            // fc1 = table[centre] (f32: static features x W1 + b1, x3-accurate) + the occupancy
+            // columns x bits (K = 128 cells; bits exact in bf16: hi and lo weights, 2 MFMAs)
             uint32_t occ[2][4];
 #pragma unroll
             for (int mt = 0; mt < 2; mt++) {
@@ -1062,10 +1031,10 @@ __global__ __launch_bounds__(256, 2) void qact3h_kernel(Fwd a0) {
                     const bf16x8 ah = *reinterpret_cast<const bf16x8*>(&Hh[rr][kk]);
                     const bf16x8 al = *reinterpret_cast<const bf16x8*>(&Hl[rr][kk]);
 #pragma unroll
-                    for (int nt = 0; nt < 2; nt++) {
-                        acc2[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bc[nt][s], acc2[mt][nt], 0, 0, 0);
-                        acc2[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, lc[nt][s], acc2[mt][nt], 0, 0, 0);
-                        acc2[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bc[nt][s], acc2[mt][nt], 0, 0, 0);
+                    for (int nt = 0; nt < 2; nt++) {  // H2^T tiles (fc3t_x3): W2 as A, H1 rows as B
+                        acc2[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bc[nt][s], ah, acc2[mt][nt], 0, 0, 0);
+                        acc2[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lc[nt][s], ah, acc2[mt][nt], 0, 0, 0);
+                        acc2[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bc[nt][s], al, acc2[mt][nt], 0, 0, 0);
                     }
                 }
 #pragma unroll
@@ -1079,22 +1048,8 @@ __global__ __launch_bounds__(256, 2) void qact3h_kernel(Fwd a0) {
         ACT_ST(5 + 4 * hh);
         __syncthreads();  // every wave is done with this half: the next half / H2 reuse the planes
     }
-#pragma unroll
-    for (int nt = 0; nt < 2; nt++) {
-        const int col = w * 64 + nt * 32 + (lane & 31);
-        const float bias = a.b2[col];
-#pragma unroll
-        for (int mt = 0; mt < 2; mt++)
-#pragma unroll
-            for (int r = 0; r < 16; r++) {
-                const float v = acc2[mt][nt][r] + bias;
-                H2s[mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h][col] = v > 0.f ? v : 0.f;
-            }
-    }
-    __syncthreads();
     ACT_ST(10);
-    const int row = tid >> 2;
-    fc3_act(a, &H2s[row][0], W3s, orow(a, m0 + row), m0 + row < a.N);
+    fc3t_x3(a, acc2, W3s, reinterpret_cast<float*>(dsm), m0, true);
     ACT_ST(11);
 }
 
@@ -1108,8 +1063,9 @@ __global__ __launch_bounds__(256, 2) void qfc23_kernel(Fwd a0, Fwd a1, int np) {
     // A stages (row pitch 40 bf16 = 20 words: conflict-free ds_read_b128), then H2 in the same
     // bytes (pitch 4 mod 32 words: fc3_act reads conflict-free)
     constexpr int AP = 40, NPL = X3 ? 2 : 1;
-    static_assert(NPL * 2 * RM * AP * 2 <= RM * (HID2 + 4) * 4, "A stages fit under H2");
-    __shared__ __attribute__((aligned(16))) char sm23[RM * (HID2 + 4) * 4];
+    constexpr int SMB = X3 ? NPL * 2 * RM * AP * 2 : RM * (HID2 + 4) * 4;  // X3: A stages, then fc3t_x3's partials
+    static_assert(NPL * 2 * RM * AP * 2 <= SMB && 4 * NACT * 64 * 4 <= SMB, "A stages / H2 / partials fit");
+    __shared__ __attribute__((aligned(16))) char sm23[SMB];
     auto As = reinterpret_cast<__bf16 (*)[NPL][RM][AP]>(sm23);  // [buf][plane][row][k]
     auto Hs = reinterpret_cast<float (*)[HID2 + 4]>(sm23);
     __shared__ float W3s[NACT][HID2];
@@ -1165,17 +1121,19 @@ __global__ __launch_bounds__(256, 2) void qfc23_kernel(Fwd a0, Fwd a1, int np) {
 #pragma unroll
             for (int s = 0; s < 2; s++) {
                 const bf16x8 av = *reinterpret_cast<const bf16x8*>(&As[buf][0][mt * 32 + (lane & 31)][s * 16 + 8 * h]);
-#pragma unroll
-                for (int nt = 0; nt < 2; nt++)
-                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bc[0][nt][s], acc[mt][nt], 0, 0, 0);
-                if constexpr (X3) {
+                if constexpr (X3) {  // H2^T tiles (fc3t_x3): W2 as A, H1 rows as B
                     const bf16x8 al =
                         *reinterpret_cast<const bf16x8*>(&As[buf][NPL - 1][mt * 32 + (lane & 31)][s * 16 + 8 * h]);
 #pragma unroll
                     for (int nt = 0; nt < 2; nt++) {
-                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bc[NPL - 1][nt][s], acc[mt][nt], 0, 0, 0);
-                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bc[0][nt][s], acc[mt][nt], 0, 0, 0);
+                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bc[0][nt][s], av, acc[mt][nt], 0, 0, 0);
+                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bc[NPL - 1][nt][s], av, acc[mt][nt], 0, 0, 0);
+                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bc[0][nt][s], al, acc[mt][nt], 0, 0, 0);
                     }
+                } else {
+#pragma unroll
+                    for (int nt = 0; nt < 2; nt++)
+                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bc[0][nt][s], acc[mt][nt], 0, 0, 0);
                 }
             }
         if (kc + 1 < NKC) {
@@ -1190,6 +1148,10 @@ __global__ __launch_bounds__(256, 2) void qfc23_kernel(Fwd a0, Fwd a1, int np) {
                 }
         }
         __syncthreads();
+    }
+    if constexpr (X3) {
+        fc3t_x3(a, acc, W3s, reinterpret_cast<float*>(sm23), m0, false);  // the A stages are free
+        return;
     }
     // H2 = relu(acc + b2) -> LDS (and HBM for the learner)
 #pragma unroll
@@ -1720,14 +1682,36 @@ __device__ __forceinline__ void gemm_tn_body(const GemmTN& g, char* smem, int bx
             }
     }
 }
-template <int AP = 1, int BP = 1, bool GR = false>  // GR: blockIdx.z = net * gz + split
+// XCD-aware placement of a split-K launch's block b (linear over tiles x splits): blocks are
+// dealt round-robin over the 8 XCDs (b and b + 8 share one), so block x + 8 j takes split
+// x + 8 (j / T) and tile j % T -- the T tiles of one K split run on one XCD and share its L2,
+// where the A and B chunks they have in common are fetched once instead of once per tile from
+// the Infinity Cache (dW1: 5 column tiles re-read each A chunk, 4 row tiles each B chunk).
+// gz not a multiple of 8: plain order.
+__device__ __forceinline__ void tn_place(int b, int gx, int gy, int gz, int& bx, int& by, int& bz) {
+    const int T = gx * gy;
+    int tile;
+    if ((gz & 7) == 0) {
+        const int x = b & 7, j = b >> 3;
+        bz = x + 8 * (j / T);
+        tile = j % T;
+    } else {
+        bz = b / T;
+        tile = b - bz * T;
+    }
+    by = tile / gx;
+    bx = tile - by * gx;
+}
+template <int AP = 1, int BP = 1, bool GR = false>  // GR: blockIdx.z = net * gz + split; else a 1-D grid (tn_place)
 __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(GemmTN g) {
     __shared__ __attribute__((aligned(16))) char smem[gemm_tn_lds_bytes<AP, BP>()];
     if constexpr (GR) {
         const int nz = (int)blockIdx.z / g.gz;
         gemm_tn_body<AP, BP>(tn_net(g, nz), smem, blockIdx.x, blockIdx.y, (int)blockIdx.z - nz * g.gz);
     } else {
-        gemm_tn_body<AP, BP>(g, smem, blockIdx.x, blockIdx.y, blockIdx.z);
+        int bx, by, bz;
+        tn_place((int)blockIdx.x, g.gx, g.gy, g.gz, bx, by, bz);
+        gemm_tn_body<AP, BP>(g, smem, bx, by, bz);
     }
 }
 // dZ1 (qdz1) and dW2 = dZ2^T H1 (gemm_tn) in one launch: both need only qbwd3's outputs. Blocks
@@ -1741,9 +1725,14 @@ __global__ __launch_bounds__(256, 2) void bwd_mid_kernel(Bwd a, int ndzx, GemmTN
         if constexpr (GR) qdz1_body<X3>(bwd_net(a, (int)blockIdx.y), smem, b % ndzx, b / ndzx, ndzx);
         else qdz1_body<X3>(a, smem, b % ndzx, b / ndzx, ndzx);
     } else {
-        const int t = b - ndz, gxy = g.gx * g.gy;
-        if constexpr (GR) gemm_tn_body<AP, BP>(tn_net(g, (int)blockIdx.y), smem, t % g.gx, (t % gxy) / g.gx, t / gxy);
-        else gemm_tn_body<AP, BP>(g, smem, t % g.gx, (t % gxy) / g.gx, t / gxy);
+        const int t = b - ndz, gxy = g.gx * g.gy;  // ndz a multiple of 8 (B >= 4096): t keeps b's XCD
+        if constexpr (GR) {
+            gemm_tn_body<AP, BP>(tn_net(g, (int)blockIdx.y), smem, t % g.gx, (t % gxy) / g.gx, t / gxy);
+        } else {
+            int bx, by, bz;
+            tn_place(t, g.gx, g.gy, g.gz, bx, by, bz);
+            gemm_tn_body<AP, BP>(g, smem, bx, by, bz);
+        }
     }
 }
 
@@ -1790,7 +1779,8 @@ __global__ __launch_bounds__(256) void reduce2_kernel(Red2 r0) {
             const int m = q / nq, n = (q - m * nq) * 4;
             const float* src = r.part2 + (size_t)m * HID + n;
             float4 acc = *reinterpret_cast<const float4*>(src);
-            for (int z = 1; z < r.S2; z++) {
+#pragma unroll 8
+            for (int z = 1; z < r.S2; z++) {  // unrolled: 8 loads in flight, the adds still in z order
                 const float4 v = *reinterpret_cast<const float4*>(src + (size_t)z * HID2 * HID);
                 acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
             }
@@ -1807,6 +1797,7 @@ __global__ __launch_bounds__(256) void reduce2_kernel(Red2 r0) {
             const size_t zs = (size_t)HID * r.Np1;
             const float* src = r.part1 + (size_t)m * r.Np1 + n;
             float4 acc = *reinterpret_cast<const float4*>(src);
+#pragma unroll 8
             for (int z = 1; z < r.S1; z++) {
                 const float4 v = *reinterpret_cast<const float4*>(src + (size_t)z * zs);
                 acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
@@ -1815,6 +1806,7 @@ __global__ __launch_bounds__(256) void reduce2_kernel(Red2 r0) {
             if (r.remap1 == 3) {  // X3: cell n / 4's danger residual column (512 + n / 4) into its danger column
                 const float* s2 = r.part1 + (size_t)m * r.Np1 + K1P + (n >> 2);
                 float d = s2[0];
+#pragma unroll 8
                 for (int z = 1; z < r.S1; z++) d += s2[(size_t)z * zs];
                 a4[1] += d;
             }
@@ -2015,31 +2007,20 @@ int evx_qmlp_pack3(const float* w1, const float* b1, const float* w2, uint16_t* 
 // the x3 act kernel for the dropout mode of a (fc1_slab_m)
 extern "C++" template <bool GR>
 static void launch_act3(const evxm::Fwd& a, int32_t n, int nets, hipStream_t st) {
-    static const bool half = getenv("EVX_ACT3_FULLTILE") == nullptr;  // 64-row tiles (A/B switch)
-    if (half) {
-        static bool attr = false;
-        if (!attr) {
-            const void* kh[3] = {(const void*)evxm::qact3h_kernel<GR, 0>, (const void*)evxm::qact3h_kernel<GR, 1>,
-                                 (const void*)evxm::qact3h_kernel<GR, 2>};
-            for (const void* k : kh) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, evxm::ACT3H_LDS);
-            attr = true;
-        }
-        const dim3 grid((unsigned)((n + 63) / 64), (unsigned)nets);
-        if (a.drop_mask)
-            hipLaunchKernelGGL((evxm::qact3h_kernel<GR, 2>), grid, dim3(256), evxm::ACT3H_LDS, st, a);
-        else if (a.drop_thresh)
-            hipLaunchKernelGGL((evxm::qact3h_kernel<GR, 1>), grid, dim3(256), evxm::ACT3H_LDS, st, a);
-        else
-            hipLaunchKernelGGL((evxm::qact3h_kernel<GR, 0>), grid, dim3(256), evxm::ACT3H_LDS, st, a);
-        return;
+    static bool attr = false;
+    if (!attr) {
+        const void* kh[3] = {(const void*)evxm::qact3h_kernel<GR, 0>, (const void*)evxm::qact3h_kernel<GR, 1>,
+                             (const void*)evxm::qact3h_kernel<GR, 2>};
+        for (const void* k : kh) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, evxm::ACT3H_LDS);
+        attr = true;
     }
-    const dim3 grid((unsigned)((n + 127) / 128), (unsigned)nets);
+    const dim3 grid((unsigned)((n + 63) / 64), (unsigned)nets);
     if (a.drop_mask)
-        hipLaunchKernelGGL((evxm::qact3_kernel<GR, 2>), grid, dim3(512), evxm::ACT3_LDS, st, a);
+        hipLaunchKernelGGL((evxm::qact3h_kernel<GR, 2>), grid, dim3(256), evxm::ACT3H_LDS, st, a);
     else if (a.drop_thresh)
-        hipLaunchKernelGGL((evxm::qact3_kernel<GR, 1>), grid, dim3(512), evxm::ACT3_LDS, st, a);
+        hipLaunchKernelGGL((evxm::qact3h_kernel<GR, 1>), grid, dim3(256), evxm::ACT3H_LDS, st, a);
     else
-        hipLaunchKernelGGL((evxm::qact3_kernel<GR, 0>), grid, dim3(512), evxm::ACT3_LDS, st, a);
+        hipLaunchKernelGGL((evxm::qact3h_kernel<GR, 0>), grid, dim3(256), evxm::ACT3H_LDS, st, a);
 }
 
 static int make_fwd(const evx_layout* lay, const evx_obs* obs, int32_t n, const evx_qmlp_params* p,
@@ -2137,7 +2118,12 @@ static int launch_fwd(const evxm::Fwd& a0, const evxm::Fwd& a1, int32_t n, int p
         return mlaunch("qfc23 grouped");
     }
     if (x3) {  // f32-accurate: 128 x 256 tiles for large batches (register budget), else 64 x 128
-        if (big * pairs >= 384)
+        static const int v = getenv("EVX_FC1X3") ? atoi(getenv("EVX_FC1X3")) : 0;  // tile experiments
+        if (v == 1 && big * pairs >= 384)
+            hipLaunchKernelGGL((evxm::qfc1_kernel<2, 2, 4, true>), dim3(blocks, 2, pairs), dim3(256), 0, st, a0, a1, pairs);
+        else if (v == 2 && big * pairs >= 384)
+            hipLaunchKernelGGL((evxm::qfc1_kernel<4, 2, 4, true>), dim3(big, 2, pairs), dim3(256), 0, st, a0, a1, pairs);
+        else if (big * pairs >= 384)
             hipLaunchKernelGGL((evxm::qfc1_kernel<4, 1, 8, true>), dim3(big, 2, pairs), dim3(512), 0, st, a0, a1, pairs);
         else
             hipLaunchKernelGGL((evxm::qfc1_kernel<2, 1, 4, true>), dim3(blocks, 4, pairs), dim3(256), 0, st, a0, a1, pairs);
@@ -2202,10 +2188,6 @@ int evx_qmlp_act(const evx_layout* lay, const evx_obs* obs, int32_t n, const evx
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)evxm::qact_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   evxm::ACT_LDS);
-        const void* ks[6] = {(const void*)evxm::qact3_kernel<false, 0>, (const void*)evxm::qact3_kernel<false, 1>,
-                             (const void*)evxm::qact3_kernel<false, 2>, (const void*)evxm::qact3_kernel<true, 0>,
-                             (const void*)evxm::qact3_kernel<true, 1>, (const void*)evxm::qact3_kernel<true, 2>};
-        for (const void* k : ks) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, evxm::ACT3_LDS);
         attr = true;
     }
     if (p->x3)
@@ -2245,29 +2227,44 @@ int evx_qmlp_forward2(const evx_layout* lay, int32_t n, const evx_obs* obs0, con
     if (!(out0->q || out0->actions || out0->h2) || !(out1->q || out1->actions || out1->h2))
         return mfail(-22, "qmlp_forward2: both problems need an fc2/fc3 output");
     if ((p0->x3 != 0) != (p1->x3 != 0)) return mfail(-22, "qmlp_forward2: both problems in one precision");
+    static const bool tgt_act = !getenv("EVX_TGT_ACT") || atoi(getenv("EVX_TGT_ACT")) != 0;
+    if (tgt_act && p0->x3 && out1->q && !out1->h2 && !out1->actions && !out1->x && n >= 4096) {
+        // x3 learner: the second problem (the target net: Q only) through the fused act kernel
+        // (H1 / H2 stay in LDS, 64-row tiles, two workgroups per CU) instead of qfc1 + qfc23
+        // writing and re-reading both H1 planes; the first problem alone through qfc1 + qfc23
+        a1.stat = nullptr;
+        a1.actions = nullptr;
+        a1.h1 = a1.h1l = nullptr;
+        int rc2 = launch_fwd(a0, a0, n, 1, true, (hipStream_t)stream, true);
+        if (rc2) return rc2;
+        launch_act3<false>(a1, n, 1, (hipStream_t)stream);
+        return mlaunch("qmlp_forward2 target act");
+    }
     return launch_fwd(a0, a1, n, 2, true, (hipStream_t)stream, p0->x3 != 0);
 }
 
-// split-K of the weight-gradient GEMMs: about 256 workgroups over `tiles` output tiles
-static int ksplit_wgs() {  // target workgroups of a split-K weight-gradient launch
-    static const int n = getenv("EVX_KSPLIT_WG") ? atoi(getenv("EVX_KSPLIT_WG")) : 256;
-    return n > 0 ? n : 256;
-}
-static int ksplit_kper(int B, int tiles) {
-    const int S = (ksplit_wgs() + tiles - 1) / tiles;
+// K splits of a weight-gradient GEMM: the most splits, a multiple of 8 (tn_place), whose
+// tiles x splits fit `slots` workgroups at once (two per CU: 512; dW2 shares its launch with
+// the 256 dZ1 workgroups: 256). dW1 (x3: 20 tiles) -> 24 splits, 480 workgroups, 60 per XCD.
+static int ksplit_kper(int B, int tiles, int slots) {
+    static const int env = getenv("EVX_KSPLIT_WG") ? atoi(getenv("EVX_KSPLIT_WG")) : 0;  // experiments
+    if (env > 0 && slots == 512) slots = env;
+    const int S = std::max(8, slots / tiles / 8 * 8);
     int kper = (B + S - 1) / S;
     return (kper + evxm::TKC - 1) / evxm::TKC * evxm::TKC;
 }
+static int dw2_kper(int B) { return ksplit_kper(B, 8, 256); }
+static int dw1_kper(int B, bool x3) { return ksplit_kper(B, x3 ? 20 : 16, 512); }
 
 // split-K partials: dW2's region, then dW1's (both stay live until reduce2_kernel)
 static int64_t part2_floats(int32_t B) {
-    const int64_t s2 = (B + ksplit_kper(B, 8) - 1) / ksplit_kper(B, 8);
+    const int64_t s2 = (B + dw2_kper(B) - 1) / dw2_kper(B);
     return s2 * evxm::HID2 * evxm::HID;
 }
 int64_t evx_qmlp_backward_part_floats(int32_t B) {
     if (B <= 0) return 0;
-    const int64_t s1 = std::max((B + ksplit_kper(B, 24) - 1) / ksplit_kper(B, 24),
-                                (B + ksplit_kper(B, 20) - 1) / ksplit_kper(B, 20));  // bf16 / x3 dW1 splits
+    const int64_t s1 = std::max((B + dw1_kper(B, false) - 1) / dw1_kper(B, false),
+                                (B + dw1_kper(B, true) - 1) / dw1_kper(B, true));  // bf16 / x3 dW1 splits
     return part2_floats(B) + s1 * evxm::HID * evxm::K1X;  // K1X: the x3 dW1 width
 }
 
@@ -2281,12 +2278,12 @@ template <bool X3, int AP2, int BP2, int AP1, int BP1>
 static void launch_tail(const evxm::Bwd& a, int32_t B, const evx_qmlp_grads* g, float* ss, hipStream_t st,
                         int nets = 1) {
     // dW2 = dZ2^T H1 (256 x 512); dW1 = dZ1^T X (512 x compact K -> 726); K = B split into S tiles
-    evxm::GemmTN g2{a.dz2, evxm::HID2, a.h1, evxm::HID, B, evxm::HID2, evxm::HID, ksplit_kper(B, 8), g->w2, evxm::HID, 0,
+    evxm::GemmTN g2{a.dz2, evxm::HID2, a.h1, evxm::HID, B, evxm::HID2, evxm::HID, dw2_kper(B), g->w2, evxm::HID, 0,
                     g->part, X3 ? a.dz2l : nullptr, X3 ? a.h1l : nullptr, evxm::HID / evxm::TT, evxm::HID2 / evxm::TT, 0};
     g2.gz = (B + g2.kper - 1) / g2.kper;
     const int KX = X3 ? evxm::K1X : evxm::K1P;
     evxm::GemmTN g1{a.dz1, evxm::HID, a.x, KX, B, evxm::HID, X3 ? evxm::K1X : 4 * evxm::NCELL,
-                    ksplit_kper(B, X3 ? 20 : 24), g->w1, evxm::K1, X3 ? 3 : 1, g->part ? g->part + part2_floats(B) : nullptr,
+                    dw1_kper(B, X3), g->w1, evxm::K1, X3 ? 3 : 1, g->part ? g->part + part2_floats(B) : nullptr,
                     X3 ? a.dz1l : nullptr, nullptr, KX / evxm::TT, evxm::HID / evxm::TT, 0};
     g1.gz = (B + g1.kper - 1) / g1.kper;
     const int qrt = evxm::qdz1_tiles_per_wg(B);
@@ -2331,12 +2328,12 @@ static void launch_tail(const evxm::Bwd& a, int32_t B, const evx_qmlp_grads* g, 
         if (split_mid) {
             hipLaunchKernelGGL((evxm::bwd_mid_kernel<X3, AP2, BP2>), dim3((unsigned)(ndzx * (evxm::HID / 128))), dim3(256),
                                lds, st, a, ndzx, g2);
-            hipLaunchKernelGGL((evxm::gemm_tn_kernel<AP2, BP2>), dim3(g2.gx, g2.gy, g2.gz), dim3(256), 0, st, g2);
+            hipLaunchKernelGGL((evxm::gemm_tn_kernel<AP2, BP2>), dim3(g2.gx * g2.gy * g2.gz), dim3(256), 0, st, g2);
         } else {
             const unsigned nmid = (unsigned)(ndzx * (evxm::HID / 128) + g2.gx * g2.gy * g2.gz);
             hipLaunchKernelGGL((evxm::bwd_mid_kernel<X3, AP2, BP2>), dim3(nmid), dim3(256), lds, st, a, ndzx, g2);
         }
-        hipLaunchKernelGGL((evxm::gemm_tn_kernel<AP1, BP1>), dim3(g1.gx, g1.gy, g1.gz), dim3(256), 0, st, g1);
+        hipLaunchKernelGGL((evxm::gemm_tn_kernel<AP1, BP1>), dim3(g1.gx * g1.gy * g1.gz), dim3(256), 0, st, g1);
         evxm::Red2 r{g->part, g2.gz, g1.part, g1.gz, g1.gx * evxm::TT, 4 * evxm::NCELL, X3 ? 3 : 1,
                      g->w1, g->b1, g->w2, g->b2, g->w3, g->b3, ss,
                      (evxm::HID2 * evxm::HID / 4 + 255) / 256, (evxm::HID * evxm::NCELL + 255) / 256};
@@ -2345,8 +2342,8 @@ static void launch_tail(const evxm::Bwd& a, int32_t B, const evx_qmlp_grads* g, 
     }
     // f32 atomics into the gradients (no partials)
     hipLaunchKernelGGL(evxm::qdz1_kernel<X3>, dim3((unsigned)ndzx, evxm::HID / 128), dim3(256), 0, st, a);
-    hipLaunchKernelGGL((evxm::gemm_tn_kernel<AP2, BP2>), dim3(g2.gx, g2.gy, g2.gz), dim3(256), 0, st, g2);
-    hipLaunchKernelGGL((evxm::gemm_tn_kernel<AP1, BP1>), dim3(g1.gx, g1.gy, g1.gz), dim3(256), 0, st, g1);
+    hipLaunchKernelGGL((evxm::gemm_tn_kernel<AP2, BP2>), dim3(g2.gx * g2.gy * g2.gz), dim3(256), 0, st, g2);
+    hipLaunchKernelGGL((evxm::gemm_tn_kernel<AP1, BP1>), dim3(g1.gx * g1.gy * g1.gz), dim3(256), 0, st, g1);
     if (ss) hipLaunchKernelGGL(evxm::sumsq_parts_kernel, dim3((unsigned)norm_parts()), dim3(256), 0, st, g->w1, ss);
 }
 }  // extern "C++"
@@ -2504,13 +2501,6 @@ int evx_qmlp_act_g(const evx_layout* lay, const evx_obs* obs, int32_t n, int32_t
     a.h1 = nullptr;
     a.h1l = nullptr;
     a.gn = nets;
-    static bool attr = false;
-    if (!attr) {
-        const void* ks[3] = {(const void*)evxm::qact3_kernel<true, 0>, (const void*)evxm::qact3_kernel<true, 1>,
-                             (const void*)evxm::qact3_kernel<true, 2>};
-        for (const void* k : ks) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, evxm::ACT3_LDS);
-        attr = true;
-    }
     launch_act3<true>(a, n, nets, (hipStream_t)stream);
     return mlaunch("qact_g");
 }
