@@ -2228,7 +2228,9 @@ int evx_qmlp_forward2(const evx_layout* lay, int32_t n, const evx_obs* obs0, con
         return mfail(-22, "qmlp_forward2: both problems need an fc2/fc3 output");
     if ((p0->x3 != 0) != (p1->x3 != 0)) return mfail(-22, "qmlp_forward2: both problems in one precision");
     static const bool tgt_act = !getenv("EVX_TGT_ACT") || atoi(getenv("EVX_TGT_ACT")) != 0;
-    if (tgt_act && p0->x3 && out1->q && !out1->h2 && !out1->actions && !out1->x && n >= 4096) {
+    // (at n >= 32768 only: a fused act workgroup lives ~65 us on the full path, so below a full
+    // round of workgroups the two-kernel forward wins -- B = 4096: learn 187 vs 127 us)
+    if (tgt_act && p0->x3 && out1->q && !out1->h2 && !out1->actions && !out1->x && n >= 32768) {
         // x3 learner: the second problem (the target net: Q only) through the fused act kernel
         // (H1 / H2 stay in LDS, 64-row tiles, two workgroups per CU) instead of qfc1 + qfc23
         // writing and re-reading both H1 planes; the first problem alone through qfc1 + qfc23
@@ -2245,16 +2247,20 @@ int evx_qmlp_forward2(const evx_layout* lay, int32_t n, const evx_obs* obs0, con
 
 // K splits of a weight-gradient GEMM: the most splits, a multiple of 8 (tn_place), whose
 // tiles x splits fit `slots` workgroups at once (two per CU: 512; dW2 shares its launch with
-// the 256 dZ1 workgroups: 256). dW1 (x3: 20 tiles) -> 24 splits, 480 workgroups, 60 per XCD.
-static int ksplit_kper(int B, int tiles, int slots) {
+// the 256 dZ1 workgroups: 256). dW1 (x3: 20 tiles) at B = 32768 -> 24 splits, 480 workgroups,
+// 60 per XCD.
+static int ksplit_kper(int B, int tiles, int slots, int minrows) {
     static const int env = getenv("EVX_KSPLIT_WG") ? atoi(getenv("EVX_KSPLIT_WG")) : 0;  // experiments
     if (env > 0 && slots == 512) slots = env;
-    const int S = std::max(8, slots / tiles / 8 * 8);
+    // ... and no more than one split per `minrows` rows (dW1: 1024 -- below that its partials'
+    // reduction outweighs the parallelism, B = 8192: learn 171 -> 154 us; dW2, whose launch the
+    // dZ1 tiles share: 256)
+    const int S = std::max(8, std::min(slots / tiles / 8 * 8, B / minrows / 8 * 8));
     int kper = (B + S - 1) / S;
     return (kper + evxm::TKC - 1) / evxm::TKC * evxm::TKC;
 }
-static int dw2_kper(int B) { return ksplit_kper(B, 8, 256); }
-static int dw1_kper(int B, bool x3) { return ksplit_kper(B, x3 ? 20 : 16, 512); }
+static int dw2_kper(int B) { return ksplit_kper(B, 8, 256, 256); }
+static int dw1_kper(int B, bool x3) { return ksplit_kper(B, x3 ? 20 : 16, 512, 1024); }
 
 // split-K partials: dW2's region, then dW1's (both stay live until reduce2_kernel)
 static int64_t part2_floats(int32_t B) {
