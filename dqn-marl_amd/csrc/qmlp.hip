@@ -1317,15 +1317,17 @@ __device__ __forceinline__ Bwd bwd_net(const Bwd& a0, int g) {
 // The block's fc3 gradients leave by one f32 atomic per column and output: 32-row blocks put
 // 1024 same-address atomics on every dW3 / db2 word at B = 32768 and ran at their serial rate
 // (38 us); 128-row blocks cut that to 256.
+// Small batches take rb = 64 or 32 rows per block (qbwd3_rows: B = 4096 had 32 blocks).
 constexpr int R3 = 128, R3C = 32;
+inline int qbwd3_rows(int B) { return B >= 16384 ? 128 : B >= 8192 ? 64 : 32; }
 template <bool X3 = false, bool GR = false>  // GR: blockIdx.y = net
-__global__ __launch_bounds__(256) void qbwd3_kernel(Bwd a0) {
+__global__ __launch_bounds__(256) void qbwd3_kernel(Bwd a0, int rb) {
     Bwd ag;
     if constexpr (GR) ag = bwd_net(a0, (int)blockIdx.y);
     const Bwd& a = GR ? ag : a0;
     __shared__ float dqs[R3][NACT];
-    const int n = threadIdx.x, b0 = blockIdx.x * R3;
-    for (int i = n; i < R3 * NACT; i += 256) {
+    const int n = threadIdx.x, b0 = blockIdx.x * rb;
+    for (int i = n; i < rb * NACT; i += 256) {
         const int r = i / NACT;
         dqs[r][i - r * NACT] = b0 + r < a.B ? a.dq[(size_t)(b0 + r) * NACT + (i - r * NACT)] : 0.f;
     }
@@ -1354,7 +1356,7 @@ __global__ __launch_bounds__(256) void qbwd3_kernel(Bwd a0) {
         }
         gb2 += dz;
     };
-    for (int c0 = 0; c0 < R3; c0 += R3C) {
+    for (int c0 = 0; c0 < rb; c0 += R3C) {
         if (b0 + c0 + R3C <= a.B) {
             float hvr[R3C];
 #pragma unroll
@@ -1362,7 +1364,7 @@ __global__ __launch_bounds__(256) void qbwd3_kernel(Bwd a0) {
 #pragma unroll
             for (int r = 0; r < R3C; r++) row(c0 + r, hvr[r]);
         } else {
-            for (int r = c0; r < R3 && b0 + r < a.B; r++) row(r, a.h2[(size_t)(b0 + r) * HID2 + n]);
+            for (int r = c0; r < rb && b0 + r < a.B; r++) row(r, a.h2[(size_t)(b0 + r) * HID2 + n]);
             break;
         }
     }
@@ -1371,7 +1373,7 @@ __global__ __launch_bounds__(256) void qbwd3_kernel(Bwd a0) {
     atomicAdd(&a.gb2[n], gb2);
     if (n < NACT) {
         float s = 0.f;
-        for (int r = 0; r < R3; r++) s += dqs[r][n];
+        for (int r = 0; r < rb; r++) s += dqs[r][n];
         atomicAdd(&a.gb3[n], s);
     }
 }
@@ -2365,6 +2367,7 @@ static int qmlp_backward(const evx_qmlp_params* p, int32_t B, const float* dq, c
         return mfail(-22, "qmlp_backward: norm partials need the gradients as one flat state_dict-order buffer");
     if (B <= 0) return 0;
     hipStream_t st = (hipStream_t)stream;
+    const int rb3 = evxm::qbwd3_rows(B);
     if (zero_grads) {
         evxm::Zero6 z = {{g->w1, g->b1, g->w2, g->b2, g->w3, g->b3},
                          {(int64_t)evxm::HID * evxm::K1, evxm::HID, (int64_t)evxm::HID2 * evxm::HID, evxm::HID2,
@@ -2398,18 +2401,18 @@ static int qmlp_backward(const evx_qmlp_params* p, int32_t B, const float* dq, c
         a.dz2l = a.dz2 + (size_t)B * evxm::HID2;
         a.dz1l = a.dz1 + (size_t)B * evxm::HID;
         if (nets > 1) {
-            hipLaunchKernelGGL((evxm::qbwd3_kernel<true, true>), dim3((unsigned)((B + evxm::R3 - 1) / evxm::R3), nets),
-                               dim3(256), 0, st, a);
+            hipLaunchKernelGGL((evxm::qbwd3_kernel<true, true>), dim3((unsigned)((B + rb3 - 1) / rb3), nets),
+                               dim3(256), 0, st, a, rb3);
             launch_tail<true, 2, 2, 2, 1>(a, B, g, ss, st, nets);
             return mlaunch("qmlp_backward grouped");
         }
-        hipLaunchKernelGGL(evxm::qbwd3_kernel<true>, dim3((unsigned)((B + evxm::R3 - 1) / evxm::R3)), dim3(256), 0, st, a);
+        hipLaunchKernelGGL(evxm::qbwd3_kernel<true>, dim3((unsigned)((B + rb3 - 1) / rb3)), dim3(256), 0, st, a, rb3);
         // dW2: both operands split; dW1 over the 640 x3 columns (X exact in bf16): the danger
         // residual column of a cell adds into its danger column
         launch_tail<true, 2, 2, 2, 1>(a, B, g, ss, st);
         return mlaunch("qmlp_backward");
     }
-    hipLaunchKernelGGL(evxm::qbwd3_kernel<false>, dim3((unsigned)((B + evxm::R3 - 1) / evxm::R3)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(evxm::qbwd3_kernel<false>, dim3((unsigned)((B + rb3 - 1) / rb3)), dim3(256), 0, st, a, rb3);
     launch_tail<false, 1, 1, 1, 1>(a, B, g, ss, st);
     return mlaunch("qmlp_backward");
 }
