@@ -2694,25 +2694,93 @@ __global__ __launch_bounds__(1024) void env_order_kernel(evx_layout lay, evx_sta
 // the x3 act's table fire step) first, then the rest, each part in env order. One workgroup:
 // thread t owns the contiguous envs [t * per, (t + 1) * per); a block scan of the counts
 // places them.
-__global__ __launch_bounds__(1024) void act_perm_kernel(int t_max, evx_state st, int32_t* __restrict__ perm) {
-    __shared__ int cnt[1024];
-    __shared__ int tot;
-    const int t = (int)threadIdx.x, E = st.E;
-    const int per = (E + 1023) / 1024, e0 = min(E, t * per), e1 = min(E, e0 + per);
-    int ns = 0;
-    for (int e = e0; e < e1; e++) ns += st.scal[(size_t)e * 4] >= t_max;
-    cnt[t] = ns;
-    __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {
-        const int v = t >= o ? cnt[t - o] : 0;
-        __syncthreads();
-        cnt[t] += v;
-        __syncthreads();
+// The two scheduling permutations over many workgroups (one per 1024 envs, two launches each):
+// a count launch leaves every chunk's per-class counts and the classes of its envs (one byte per
+// env, so the rank launch sees exactly the state the counts saw), and a rank launch turns the
+// counts of the chunks before it into each class's first rank and places its envs by ballots
+// (stable: env order within a class). One workgroup doing all of it took 55-120 us beside the
+// learner (a 1024-thread workgroup with loads in series, which also slowed the kernels next to it).
+//   order: 16 buckets of persons remaining (0 = most), heavy count in slot 16;
+//   act perm: 2 classes (fire step >= t_max first).
+constexpr int PCL = 17;  // per-chunk count slots: 16 classes + the heavy count
+__global__ __launch_bounds__(1024) void perm_count_kernel(evx_layout lay, evx_state st, int mode, int hmin,
+                                                          uint8_t* __restrict__ cls, int* __restrict__ cnt) {
+    __shared__ int wc[16][16], wh[16];
+    const int t = (int)threadIdx.x, lane = t & 63, w = t >> 6, E = st.E, P = lay.P;
+    const int e = (int)blockIdx.x * 1024 + t;
+    int b = -1, heavy = 0;
+    if (e < E) {
+        if (mode == 0) {
+            const unsigned long long v = __hip_atomic_load(
+                reinterpret_cast<const unsigned long long*>(st.scal + (size_t)e * 4 + 2), __ATOMIC_RELAXED,
+                __HIP_MEMORY_SCOPE_AGENT);
+            const int rem = P - (int)(uint32_t)v - (int)(uint32_t)(v >> 32);
+            b = 15 - min(15, max(0, rem) * 16 / (P + 1));
+            heavy = rem >= hmin;
+        } else {
+            b = st.scal[(size_t)e * 4] >= lay.t_max ? 0 : 1;
+        }
+        cls[e] = (uint8_t)b;
     }
-    if (t == 1023) tot = cnt[1023];
+    int mine = 0;
+#pragma unroll
+    for (int bb = 0; bb < 16; bb++) {
+        const int n = __popcll(__ballot(b == bb));
+        mine = lane == bb ? n : mine;
+    }
+    if (lane < 16) wc[w][lane] = mine;
+    int hs = heavy;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) hs += __shfl_xor(hs, o, 64);
+    if (lane == 0) wh[w] = hs;
     __syncthreads();
-    int ps = cnt[t] - ns, pr = tot + (e0 - (cnt[t] - ns));
-    for (int e = e0; e < e1; e++) perm[st.scal[(size_t)e * 4] >= t_max ? ps++ : pr++] = e;
+    if (t < 16) {
+        int sm = 0;
+        for (int k = 0; k < 16; k++) sm += wc[k][t];
+        cnt[blockIdx.x * PCL + t] = sm;
+    } else if (t == 16) {
+        int sm = 0;
+        for (int k = 0; k < 16; k++) sm += wh[k];
+        cnt[blockIdx.x * PCL + 16] = sm;
+    }
+}
+__global__ __launch_bounds__(1024) void perm_rank_kernel(evx_state st, int mode, int hcap, const uint8_t* __restrict__ cls,
+                                                         const int* __restrict__ cnt, int32_t* __restrict__ out) {
+    __shared__ int base[16], wc[16][16], tot[PCL], pre[PCL];
+    const int t = (int)threadIdx.x, lane = t & 63, w = t >> 6, E = st.E;
+    const int c = (int)blockIdx.x, nch = (E + 1023) / 1024;
+    if (t < 64 * 2 && (t & 63) < PCL) {  // waves 0 / 1: slot s's total over all chunks / over chunks < c
+        const int sl = t & 63;
+        const int kend = t < 64 ? nch : c;
+        int sm = 0;
+#pragma unroll 8
+        for (int k = 0; k < kend; k++) sm += cnt[k * PCL + sl];  // loads in flight 8 at a time
+        if (t < 64) tot[sl] = sm;
+        else pre[sl] = sm;
+    }
+    __syncthreads();
+    if (t < 16) {  // class t: the envs of lower classes, then class t's envs in the chunks before this one
+        int below = 0;
+        for (int bb = 0; bb < t; bb++) below += tot[bb];
+        base[t] = below + pre[t];
+    }
+    if (c == 0 && t == 64 && mode == 0) out[E] = min(hcap, tot[16]);
+    const int e = c * 1024 + t;
+    const int b = e < E ? (int)cls[e] : -1;
+    int mine = 0, r = 0;
+#pragma unroll
+    for (int bb = 0; bb < 16; bb++) {
+        const unsigned long long m = __ballot(b == bb);
+        mine = lane == bb ? __popcll(m) : mine;
+        r = b == bb ? lanes_below(m) : r;
+    }
+    if (lane < 16) wc[w][lane] = mine;
+    __syncthreads();
+    if (b >= 0) {
+        int rank = base[b] + r;
+        for (int k = 0; k < w; k++) rank += wc[k][b];
+        out[rank] = e;
+    }
 }
 
 // ---------------------------------------------------- observation expand
@@ -2954,6 +3022,51 @@ int evx_env_reset(const evx_layout* l, const evx_state* s, const uint8_t* mask, 
     return e == hipSuccess ? 0 : hip_fail(e, "env_reset launch");
 }
 
+// scratch of the scheduling permutations (classes: 1 byte per env, counts: PCL ints per 1024
+// envs), one per (device, stream) -- launches on one stream run in order, so the order and the
+// act perm of a trainer share theirs; env groups on other streams get their own -- grown on
+// demand (64 entries).
+static int perm_scratch(int E, hipStream_t stream, uint8_t** cls, int** cnt) {
+    struct Ent {
+        int dev;
+        hipStream_t st;
+        int64_t cap;
+        void* p;
+    };
+    static Ent ents[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return -1;
+    const int64_t nch = (E + 1023) / 1024, need = ((int64_t)E + 255) / 256 * 256 + nch * evx::PCL * 4;
+    Ent* en = nullptr;
+    for (auto& x : ents)
+        if (x.p && x.dev == dev && x.st == stream) {
+            en = &x;
+            break;
+        }
+    if (!en)
+        for (auto& x : ents)
+            if (!x.p) {
+                en = &x;
+                en->dev = dev;
+                en->st = stream;
+                break;
+            }
+    if (!en) return -1;
+    if (en->cap < need) {
+        if (en->p) {  // launches of this stream may still read the old buffer
+            (void)hipStreamSynchronize(stream);
+            (void)hipFree(en->p);
+        }
+        en->p = nullptr;
+        en->cap = 0;
+        if (hipMalloc(&en->p, (size_t)need) != hipSuccess) return -1;
+        en->cap = need;
+    }
+    *cls = reinterpret_cast<uint8_t*>(en->p);
+    *cnt = reinterpret_cast<int*>(reinterpret_cast<uint8_t*>(en->p) + ((int64_t)E + 255) / 256 * 256);
+    return 0;
+}
+
 int evx_env_order(const evx_layout* l, const evx_state* s, void* stream) {
     int rc = check_layout(l);
     if (rc) return rc;
@@ -2968,8 +3081,17 @@ int evx_env_order(const evx_layout* l, const evx_state* s, void* stream) {
                                   160 * 1024 - 4096);
         attr_set = true;
     }
-    const size_t lds = ((size_t)s->E + 3) & ~(size_t)3;  // one bucket byte per env
-    hipLaunchKernelGGL(evx::env_order_kernel, dim3(1), dim3(1024), lds, (hipStream_t)stream, *l, *s, hcap, hmin);
+    uint8_t* cls = nullptr;
+    int* cnt = nullptr;
+    if (perm_scratch(s->E, (hipStream_t)stream, &cls, &cnt) == 0) {
+        const unsigned nch = (unsigned)((s->E + 1023) / 1024);
+        hipLaunchKernelGGL(evx::perm_count_kernel, dim3(nch), dim3(1024), 0, (hipStream_t)stream, *l, *s, 0, hmin, cls, cnt);
+        hipLaunchKernelGGL(evx::perm_rank_kernel, dim3(nch), dim3(1024), 0, (hipStream_t)stream, *s, 0, hcap, cls, cnt,
+                           s->order);
+    } else {
+        const size_t lds = ((size_t)s->E + 3) & ~(size_t)3;  // one bucket byte per env
+        hipLaunchKernelGGL(evx::env_order_kernel, dim3(1), dim3(1024), lds, (hipStream_t)stream, *l, *s, hcap, hmin);
+    }
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : hip_fail(e, "env_order launch");
 }
@@ -2979,7 +3101,12 @@ int evx_act_perm(const evx_layout* l, const evx_state* s, int32_t* perm, void* s
     if (rc) return rc;
     if (!s || !perm) return fail(-22, "act_perm: NULL argument");
     if (s->E <= 0) return 0;
-    hipLaunchKernelGGL(evx::act_perm_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, l->t_max, *s, perm);
+    uint8_t* cls = nullptr;
+    int* cnt = nullptr;
+    if (perm_scratch(s->E, (hipStream_t)stream, &cls, &cnt)) return fail(-12, "act_perm: scratch allocation failed");
+    const unsigned nch = (unsigned)((s->E + 1023) / 1024);
+    hipLaunchKernelGGL(evx::perm_count_kernel, dim3(nch), dim3(1024), 0, (hipStream_t)stream, *l, *s, 1, 0, cls, cnt);
+    hipLaunchKernelGGL(evx::perm_rank_kernel, dim3(nch), dim3(1024), 0, (hipStream_t)stream, *s, 1, 0, cls, cnt, perm);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : hip_fail(e, "act_perm launch");
 }
