@@ -106,5 +106,12 @@ if s[:, 36:46].any():
     nw = ~hv
     top_single = np.argsort(life * nw)[-10:]
     print("  slowest single-wave envs: life us", (life[top_single] / 100).round(1), "planners", s[top_single, 11])
+if os.environ.get("EVX_FCX_REPORT"):  # -DEVX_FCX build: first changed not-dead-list index vs the list length
+    fcx, nnd = s[:, 36], s[:, 37]
+    frac = np.where(fcx >= 0x7fffffff, 1.0, np.minimum(fcx, nnd) / np.maximum(nnd, 1))
+    print(f"first changed index / list length: median {np.median(frac):.3f} mean {frac.mean():.3f}; "
+          f"unchanged envs {np.mean(fcx >= 0x7fffffff):.3f}; list length median {np.median(nnd):.0f}")
+    for q in (0.1, 0.25, 0.5, 0.75):
+        print(f"  P(frac >= {q}) = {np.mean(frac >= q):.3f}")
 cnt = env.counts.view(E, 2).cpu().numpy()
 print("evacuated median", np.median(cnt[:, 0]), "dead median", np.median(cnt[:, 1]))
