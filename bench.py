@@ -140,7 +140,7 @@ def parse():
                          "(evacx.trainer._Group): one group's env.step tail overlaps the others' work")
     ap.add_argument("--traffic", default=None,
                     help="PMC traffic record of env_step_kernel on this workload and phase (tools/parse_prof.py); "
-                         "default profiles/r2/env_traffic_<phase>.json")
+                         "default profiles/r3/ (else r2/) env_traffic_<phase>.json")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.envs_total > 0:
@@ -285,14 +285,17 @@ def main():
     def ev_mean(evs, n):
         return float(np.mean([evs[s][0].elapsed_time(evs[s][1]) for s in range(n) if s % EV_EVERY == 0]))
 
-    # ----------------------------------------------------------------- warmup
-    acts_env = torch.randint(0, 5, (max(args.steps, args.warmup, 1), E * R), device="cuda", dtype=torch.int32)
-    timed_train(args.warmup)
-
-    # the CPU baseline continues from exactly this state (same envs, same episode phase)
+    # the CPU baseline continues from this state (same envs, same episode phase). Taken before the
+    # warm-up, so the timed steps follow the warm-up at once: a host copy between them left the
+    # GPU idle long enough to start the timed region at lower clocks (16.6 vs 17.6 M env-steps/s
+    # measured on one box)
     cpu_snap = None
     if rank == 0 and not args.no_cpu:
         cpu_snap = [(env.host_state(i), layout_of[i] if layout_of else 0) for i in range(min(args.cpu_envs, E))]
+
+    # ----------------------------------------------------------------- warmup
+    acts_env = torch.randint(0, 5, (max(args.steps, args.warmup, 1), E * R), device="cuda", dtype=torch.int32)
+    timed_train(args.warmup)
 
     # ------------------------------------------------------------ timed steps
     # HIP events bracket env.step on its own stream on every EV_EVERY-th step only: an
@@ -358,14 +361,18 @@ def main():
     bpe = bytes_per_env_step(P, R, G)
     per_launch = E // args.groups if args.mode == "train" else E  # env.step launches of group 0 are timed
     achieved = bpe * per_launch / (kern_ms * 1e-3) / 1e9
-    traffic, traffic_src = None, None
-    tpath = args.traffic or os.path.join(ROOT, "profiles", "r2", f"env_traffic_{args.phase}.json")
+    traffic, traffic_src, traffic_corr = None, None, None
+    tpath = args.traffic or next((q for q in (os.path.join(ROOT, "profiles", r, f"env_traffic_{args.phase}.json")
+                                              for r in ("r3", "r2")) if os.path.exists(q)), "")
     if os.path.exists(tpath):
         # HBM bytes per launch from rocprofv3 PMC passes of this same workload and phase
         # (separate --pmc FETCH_SIZE / WRITE_SIZE runs; cannot be collected inside the timed run)
         rec = json.load(open(tpath))
         if rec.get("kernel") == "env_step_kernel" and rec.get("envs") in (None, per_launch):
-            traffic = rec["bytes_per_env_step"] * per_launch
+            # raw FETCH + WRITE: the x2 FETCH correction of MI355X_MICROARCH.md holds for 16-B/lane
+            # streaming reads, and this kernel's loads are 4-8 B per lane; the corrected figure rides along
+            traffic = rec.get("bytes_per_env_step_raw", rec["bytes_per_env_step"]) * per_launch
+            traffic_corr = rec["bytes_per_env_step"] * per_launch
             traffic_src = os.path.relpath(tpath, ROOT)
     cpu = None
     if cpu_snap is not None:
@@ -427,6 +434,9 @@ def main():
             "last_loss": loss,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                         "traffic_basis": "raw FETCH_SIZE + WRITE_SIZE bytes per launch (PMC)",
+                         "traffic_fetch_x2": traffic_corr,
+                         "frac_traffic": (traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
                          "kernel": "env_step_kernel", "kernel_ms": kern_ms, "bytes_per_env_step": bpe,
                          "env_steps_per_launch": per_launch,
                          "launches_timed": len([s for s in range(args.steps) if s % EV_EVERY == 0])},
@@ -488,7 +498,7 @@ def cpu_learner_ms(args, threads):
 
 def cpu_baseline(snap, R, lay_tables, P, args, E):
     """Oracle (C restatement, OpenMP over envs) on the host cores, started from the GPU
-    state of the first cpu_envs envs at the beginning of the timed region (same episode
+    state of the first cpu_envs envs at the beginning of the warm-up steps (same episode
     phase), stepped with uniform random actions; plus the reference's learn/act in torch
     on the same cores, composed into the rate of the same full training step."""
     try:
@@ -518,7 +528,7 @@ def cpu_baseline(snap, R, lay_tables, P, args, E):
     out = {"value": env_rate, "unit": "env-steps/s", "cores": threads, "kind": "port",
            "nproc": os.cpu_count(), "cpu_model": cpu_model(),
            "sample": f"{n} envs x {steps} env.steps of the same workload from the GPU's state at the start of the "
-                     f"timed region (env.step only), OpenMP {threads} threads (all cores of this process's "
+                     f"warm-up steps (env.step only), OpenMP {threads} threads (all cores of this process's "
                      f"affinity set, capped by OMP_NUM_THREADS), {dt:.2f}s wall, {dt * threads:.1f} core-s; "
                      "compare with env_only_steps_per_s"}
     if args.mode == "train" and args.qnet == "mlp":
