@@ -329,24 +329,6 @@ __device__ __forceinline__ void np_store(uint32_t* ring, int& front, int head, u
     if (lane == 0) gst[MT_N] = (uint32_t)(head - b);
 }
 
-// Ascending bitonic sort of a[0..n), n a power of two, by one wave.
-template <typename T>
-__device__ __forceinline__ void wave_sort(T* a, int n) {
-    const int lane = (int)(threadIdx.x & 63);
-    for (int k = 2; k <= n; k <<= 1)
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int q = lane; q < (n >> 1); q += 64) {
-                const int i = ((q & ~(j - 1)) << 1) | (q & (j - 1));
-                const int l = i | j;
-                const uint32_t x = a[i], y = a[l];
-                if ((x > y) == ((i & k) == 0)) {
-                    a[i] = y;
-                    a[l] = x;
-                }
-            }
-            wave_sync();  // one wave: waits for its own LDS / memory traffic
-        }
-}
 
 // Ascending bitonic sort of a[0..64*R) by one wave in registers: element i = lane*R + r
 // lives in register r of lane `lane`; stages with j < R are compare-exchanges between
@@ -393,9 +375,96 @@ __device__ __forceinline__ void wave_sort_reg(T* a) {
     wave_sync();
 }
 
+// The bitonic merge of a 64 R block in registers in one direction: the stages j = 32 R .. 1 of
+// a k > 64 R pass (the block is bitonic after that pass's larger-j stages).
+template <int R, typename T>
+__device__ __forceinline__ void wave_merge_reg(T* a, bool asc) {
+    const int lane = (int)(threadIdx.x & 63);
+    constexpr int N = 64 * R;
+    uint32_t v[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) v[r] = a[lane * R + r];
+#pragma unroll
+    for (int j = N >> 1; j > 0; j >>= 1) {
+        if (j < R) {
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                if (r & j) continue;
+                const uint32_t x = v[r], y = v[r | j];
+                const uint32_t lo = x < y ? x : y, hi = x < y ? y : x;
+                v[r] = asc ? lo : hi;
+                v[r | j] = asc ? hi : lo;
+            }
+        } else {
+            const int m = j / R;
+            const bool upper = (lane & m) != 0;
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                const uint32_t o = (uint32_t)__shfl_xor((int)v[r], m, 64);
+                const uint32_t lo = v[r] < o ? v[r] : o, hi = v[r] < o ? o : v[r];
+                v[r] = (upper != asc) ? lo : hi;
+            }
+        }
+    }
+    wave_sync();
+#pragma unroll
+    for (int r = 0; r < R; r++) a[lane * R + r] = v[r];
+    wave_sync();
+}
+// Bitonic sort of a[0..n2) (n2 a power of two >= 1024, e.g. the contested list of a big grid in
+// global scratch) with 512-key blocks in registers: every block sorted in its direction, then per
+// k >= 1024 only the stages with j >= 512 cross blocks through memory (8 compare-exchanges per
+// lane in flight) and the rest run in registers -- 10 memory passes at 4096 keys instead of the
+// 78 stages of wave_sort, one wave fence each (cfg4's heaviest envs: ~3 M cycles of sorting).
+template <typename T>
+__device__ __forceinline__ void wave_sort_big(T* a, int n2) {
+    const int lane = (int)(threadIdx.x & 63);
+    constexpr int NB = 512;
+    for (int b = 0; b < n2 / NB; b++) {
+        wave_sort_reg<8>(a + b * NB);
+        if (b & 1) {  // descending block: reverse it
+            const uint32_t x[4] = {a[b * NB + lane], a[b * NB + 64 + lane], a[b * NB + 128 + lane], a[b * NB + 192 + lane]};
+            const uint32_t y[4] = {a[b * NB + NB - 1 - lane], a[b * NB + NB - 65 - lane], a[b * NB + NB - 129 - lane],
+                                   a[b * NB + NB - 193 - lane]};
+            wave_sync();
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                a[b * NB + 64 * q + lane] = y[q];
+                a[b * NB + NB - 1 - 64 * q - lane] = x[q];
+            }
+            wave_sync();
+        }
+    }
+    for (int k = 2 * NB; k <= n2; k <<= 1) {
+        for (int j = k >> 1; j >= NB; j >>= 1) {
+            for (int q0 = 0; q0 < (n2 >> 1); q0 += 64 * 8) {
+                uint32_t xs[8], ys[8];
+                int is[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const int q = q0 + 64 * u + lane;
+                    is[u] = ((q & ~(j - 1)) << 1) | (q & (j - 1));
+                    xs[u] = a[is[u]];
+                    ys[u] = a[is[u] | j];
+                }
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const int i = is[u];
+                    if ((xs[u] > ys[u]) == ((i & k) == 0)) {
+                        a[i] = ys[u];
+                        a[i | j] = xs[u];
+                    }
+                }
+            }
+            wave_sync();
+        }
+        for (int b = 0; b < n2 / NB; b++) wave_merge_reg<8>(a + b * NB, ((b * NB) & k) == 0);
+    }
+}
+
 // Sort a[0..n) ascending (distinct keys): n <= 64 by rank (each lane counts the
 // keys below its own, readlane broadcast); power-of-two padded n2 <= 512 (the caller
-// pads with 0xffffffff) by a register bitonic network, larger by the LDS one.
+// pads with 0xffffffff) by a register bitonic network, larger by wave_sort_big.
 template <typename T>
 __device__ __forceinline__ void wave_sort_keys(T* a, int n, int n2) {
     const int lane = (int)(threadIdx.x & 63);
@@ -414,7 +483,7 @@ __device__ __forceinline__ void wave_sort_keys(T* a, int n, int n2) {
     } else if (n2 == 512) {
         wave_sort_reg<8>(a);
     } else {
-        wave_sort(a, n2);
+        wave_sort_big(a, n2);
     }
 }
 
@@ -3091,6 +3160,26 @@ static int perm_scratch(int E, hipStream_t stream, uint8_t** cls, int** cnt) {
     *cls = reinterpret_cast<uint8_t*>(en->p);
     *cnt = reinterpret_cast<int*>(reinterpret_cast<uint8_t*>(en->p) + ((int64_t)E + 255) / 256 * 256);
     return 0;
+}
+
+namespace evx {
+// diagnostic / test entry (evx_diag_sort_keys): one wave sorts n distinct keys in place in global
+// memory with the contested list's sort (wave_sort_keys), padding to a power of two in pad[]
+__global__ __launch_bounds__(64) void diag_sort_kernel(uint32_t* keys, uint32_t* pad, int n) {
+    const int lane = (int)threadIdx.x;
+    const int n2 = pow2_ceil(n);
+    for (int i = lane; i < n2; i += 64) pad[i] = i < n ? keys[i] : 0xffffffffu;
+    wave_sync();
+    wave_sort_keys(pad, n, n2);
+    for (int i = lane; i < n; i += 64) keys[i] = pad[i];
+}
+}  // namespace evx
+int evx_diag_sort_keys(uint32_t* keys, uint32_t* pad, int32_t n, void* stream) {
+    if (!keys || !pad || n < 0) return fail(-22, "diag_sort_keys: bad argument");
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(evx::diag_sort_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, keys, pad, n);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : hip_fail(e, "diag_sort_keys launch");
 }
 
 int evx_env_order(const evx_layout* l, const evx_state* s, void* stream) {

@@ -153,6 +153,10 @@ int evx_act_perm(const evx_layout *l, const evx_state *s, int32_t *perm, void *s
 int64_t evx_step_lds_bytes(const evx_layout *lay);
 /* 32-bit words of evx_state.scratch the step needs per env. */
 int64_t evx_step_scratch_words(const evx_layout *lay);
+/* Test entry (no reference counterpart): one wave sorts keys[0..n) (distinct u32) in place with
+ * the step's contested-list sort (envs/people.py:284-297 groups movers by target through it);
+ * pad: device scratch of the next power of two >= n words. */
+int evx_diag_sort_keys(uint32_t *keys, uint32_t *pad, int32_t n, void *stream);
 
 const char *evx_last_error(void);
 
