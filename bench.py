@@ -307,6 +307,21 @@ def main():
     learn_ms = ev_mean(ev_learn, args.steps) if args.mode == "train" else None
     loss = float(tr.last_loss.float().mean().item()) if tr.last_loss is not None else None
     value = E * world * args.steps / elapsed
+    split = args.mode == "train" and tr.split and schedule == "strict"
+
+    # ---------------- the learn step alone, one part at B (extra: its MFMA roofline)
+    # with the split learn step the timed events above cover only its tail (fresh rows, clip,
+    # Adam: the part on the step's critical path); the whole learn chain is timed here alone
+    learn_alone_ms = None
+    if args.mode == "train" and tr.fast is not None and tr.replay.size >= args.batch:
+        tr.sync()
+        ev_l = ev_pairs(6)
+        for i in range(6):
+            ev_l[i][0].record()
+            tr.learn()
+            ev_l[i][1].record()
+        torch.cuda.synchronize()
+        learn_alone_ms = float(np.mean([ev_l[i][0].elapsed_time(ev_l[i][1]) for i in range(1, 6)]))
 
     # ------------------------------- the other schedule on the same state (extra)
     other = None
@@ -431,6 +446,11 @@ def main():
             "start_phase": start,
             "env_step_kernel_ms": kern_ms,
             "learn_ms": learn_ms,
+            "learn_ms_what": ("the split learn step's tail on the critical path (fresh rows' forward + backward, "
+                              "clip + Adam); its old rows run on the learn stream beside act and env.step"
+                              if split else "the learn step on the training stream"),
+            "learn_split_rows": list(tr.last_split) if split and tr.last_split else None,
+            "learn_alone_ms": learn_alone_ms,
             "last_loss": loss,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
@@ -442,12 +462,14 @@ def main():
                          "launches_timed": len([s for s in range(args.steps) if s % EV_EVERY == 0])},
             "cpu_baseline": cpu,
         }
-        if learn_ms is not None and args.qnet == "mlp":
+        lm = learn_alone_ms if learn_alone_ms is not None else (None if split else learn_ms)
+        if lm is not None and args.qnet == "mlp":
             fl = qnet_flops(0, args.batch)
-            line["roofline_learn"] = {"bound": "mfma", "achieved": fl / (learn_ms * 1e-3) / 1e12,
+            line["roofline_learn"] = {"bound": "mfma", "achieved": fl / (lm * 1e-3) / 1e12,
                                       "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                                      "frac": fl / (learn_ms * 1e-3) / 1e12 / BF16_PEAK_TFLOPS,
-                                      "flops_basis": "dense f32-equivalent FLOPs of one learn step"}
+                                      "frac": fl / (lm * 1e-3) / 1e12 / BF16_PEAK_TFLOPS, "learn_ms": lm,
+                                      "flops_basis": "dense f32-equivalent FLOPs of one learn step (B rows in one "
+                                                     "part, timed alone)"}
         print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()

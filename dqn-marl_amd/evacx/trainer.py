@@ -23,6 +23,7 @@ import ctypes as C
 import os
 from typing import List, Optional
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -239,6 +240,21 @@ class VecTrainer:
         self.fast = self.learner.fast if self.learner is not None else None
         if self.fast is None:
             self.lagged = False  # the split learn step needs the fused bf16 MLP path
+        # split learn step (the strict schedule's default on the fused x3 MLP with uniform replay):
+        # learn t's batch is drawn from the ring after push t as random.sample draws it -- a uniform
+        # B-subset -- but in two parts: K ~ Hypergeometric(F = E*R pushed slots, the rest, B) rows
+        # from push t's slots and B - K from the slots already there before it (a uniform B-subset
+        # of the union, exactly). The old part's forward + backward runs on the learn stream beside
+        # act t and env.step t (it reads only the weights after learn t-1 and the ring before push
+        # t); the K fresh rows, clip and Adam run after push t. Same batch distribution, weights
+        # and loss as the one-part learn up to f32 summation order. Off by default (EVX_SPLIT_LEARN=1
+        # turns it on): measured slower at cfg3 (tools/gpu_ab_split.sh: 17.36 vs 17.59 M env-steps/s)
+        # -- act and env.step fill every CU's LDS and VGPRs, so the old part mostly runs after the
+        # push anyway while slowing env.step by 4 %.
+        self.split = (not self.per_robot and self.fast is not None and self.learner.fused_opt and not self.prio
+                      and os.environ.get("EVX_SPLIT_LEARN", "0") == "1")
+        self._hg = np.random.Generator(np.random.PCG64([self.seed & 0xFFFFFFFF, 0x5EED5]))
+        self.last_split = None  # (old rows, fresh rows) of the last split learn step
         self._perm = None
         if self.fast is not None and layout_of is None and len(self.groups) == 1 and \
                 os.environ.get("EVX_ACT_STATIC", "1" if self.fast.x3 else "0") == "1":
@@ -347,6 +363,56 @@ class VecTrainer:
             self.learner.sync_target()
         return loss
 
+    def _split_draw(self):
+        """Host part of a split learn step t (before push t): None when learn t does not run, else
+        ((base, count) of the ring's slots before push t that it keeps, (base, F) of push t's
+        slots, K fresh rows). K ~ Hypergeometric(F, count, B): with B - K rows drawn uniformly
+        without replacement from the kept slots and K from push t's, the batch is a uniform
+        B-subset of the ring after push t, the distribution of random.sample(memory, B)
+        (agents/dqn_agent.py:132)."""
+        F = self.n_agents
+        old = self.replay.window(F)
+        if self.t % self.learn_every or old[1] + F < self.batch:  # DQNAgent.learn's len(memory) guard
+            return None
+        k = int(self._hg.hypergeometric(F, old[1], self.batch)) if old[1] > 0 else self.batch
+        return old, (self.replay.pos, F), k
+
+    def _samp_rows(self, r0):
+        sp = self.samp
+        return dict(s=sp["s"][r0 * OBS_WORDS:], s2=sp["s2"][r0 * OBS_WORDS:], a=sp["a"][r0:], r=sp["r"][r0:],
+                    done=sp["done"][r0:])
+
+    def _learn_split_pre(self):
+        """Learn t's rows from the slots before push t (on the learn stream, current)."""
+        d = self._split_draw()
+        if d is None:
+            return None
+        old, fresh, k = d
+        n_old = self.batch - k
+        self.last_split = (n_old, k)
+        if n_old:
+            with torch.cuda.stream(self.lstream):
+                for grp in self.groups:  # push t-1 (the ring's contents) and the act order's inputs
+                    self.lstream.wait_event(grp.ev_push)
+                self.replay.sample_window(old[0], old[1], n_old, self.seed + 1, self.learn_steps * self.batch,
+                                          self._samp_rows(0))
+                sp = self.samp
+                self.learner.learn_obs(self.lay.c, sp["s"], sp["a"], sp["r"], sp["done"], sp["s2"], n_old,
+                                       update=False, part=(self.batch, True, k == 0))
+        return d
+
+    def _learn_split_post(self, d):
+        """Learn t's rows from push t's slots, then clip + Adam (learn stream, after push t)."""
+        old, fresh, k = d
+        n_old = self.batch - k
+        if k:
+            self.replay.sample_window(fresh[0], fresh[1], k, self.seed + 2, self.learn_steps * self.batch,
+                                      self._samp_rows(n_old))
+            sp = self._samp_rows(n_old)
+            self.learner.learn_obs(self.lay.c, sp["s"], sp["a"], sp["r"], sp["done"], sp["s2"], k, update=False,
+                                   part=(self.batch, n_old == 0, True))
+        return self.learn(phase="update")
+
     def step(self, extra_reset: Optional[torch.Tensor] = None, ev_env=None, ev_learn=None):
         """One training step. Finished envs are reset inside the env.step launch
         (auto-reset: the reset of an env that ends runs in its own wave, in the shadow
@@ -362,6 +428,7 @@ class VecTrainer:
         overlap act and env.step, its weight update waits for every group's act to have
         read the weights, and the next acts wait for the update."""
         caller = torch.cuda.current_stream(self.device)
+        join = self.join_caller
         if self.join_caller or extra_reset is not None:  # inputs made on the caller's stream
             for grp in self.groups:
                 grp.main.wait_stream(caller)
@@ -369,18 +436,24 @@ class VecTrainer:
         G = self.groups
         inline = (self.lagged and len(G) == 1) if _ORDER_INLINE_ENV is None else _ORDER_INLINE_ENV == "1"
         reset_wait, self.reset_pending = self.reset_pending, False
+        split = self.split and not self.lagged
+        if split and join:  # the learn stream reads what the caller may have written (weights, ring)
+            self.lstream.wait_stream(caller)
         # act: every group on its own stream, after the previous update (lagged) or learn
         for grp in G:
             with torch.cuda.stream(grp.main):
                 if reset_wait:  # a cross-stream wait costs a gap: only when there was a reset
                     grp.main.wait_event(self.ev_reset)
-                if self.lagged or grp.g > 0:
+                if self.lagged or grp.g > 0 or split:
                     grp.main.wait_event(self.ev_learned)
                 if self._perm is not None and not inline:  # the act order, made after the last push
                     grp.main.wait_event(grp.ev_order)
                 self._act(grp)
                 if self.lagged:
                     grp.ev_act.record(grp.main)
+        # split: learn t's old part on the learn stream (after learn t-1 there and push t-1), beside
+        # act t and env.step t; enqueued after the acts so their dropout streams come first
+        pre = self._learn_split_pre() if split else None
         if self.lagged:
             # learn t: gradients from the ring as it stood after push t-1 (minus the slots
             # push t overwrites), overlapping act t and env.step t; the weight update
@@ -447,7 +520,18 @@ class VecTrainer:
                 grp.env.compute_order()
                 if st is grp.side:
                     grp.ev_order.record(st)
-        if not self.lagged:  # the reference's order: learn after every group's push, on group 0's stream
+        if split:  # learn t's fresh part + clip + Adam, after push t (and so after act t)
+            with torch.cuda.stream(self.lstream):
+                for grp in G:
+                    self.lstream.wait_event(grp.ev_push)
+                if ev_learn is not None:
+                    ev_learn[0].record(self.lstream)
+                if pre is not None:
+                    self.last_loss = self._learn_split_post(pre)
+                if ev_learn is not None:
+                    ev_learn[1].record(self.lstream)
+                self.ev_learned.record(self.lstream)
+        elif not self.lagged:  # the reference's order: learn after every group's push, on group 0's stream
             m = G[0].main
             with torch.cuda.stream(m):
                 for grp in G[1:]:

@@ -195,7 +195,7 @@ def test_x3_learn_at_bench_batch(B):
         # the device's branch pattern, from the forward it saved for the backward
         h1 = lr.net.ws.get("fh1", (2 * B * HID,), torch.int16, torch.device(dev)).view(torch.bfloat16)
         h1 = h1.view(2, B, HID).float().sum(0)
-        h2 = lr.net.ws.get("fh2", (B, HID2), torch.float32, torch.device(dev))
+        h2 = lr.net.ws.get("fh2", (B * HID2,), torch.float32, torch.device(dev)).view(B, HID2)
         g1, g2 = (h1 > 0).float(), (h2 > 0).float()
         X = env.expand_obs(torch.float32, s_obs).reshape(B, K1)
         X2 = env.expand_obs(torch.float32, s2_obs).reshape(B, K1)
