@@ -893,7 +893,10 @@ __device__ long long g_act_st[8192 * ACT_NST];
 constexpr int A3H_HBYTES = 2 * 64 * A3_HP * 2;  // 67,584: both H1 half planes of 64 rows
 static_assert(A3H_HBYTES >= 2 * 64 * (KC1 + 8) * 2, "fc1 A staging overlays the H1 planes");
 constexpr int ACT3H_LDS = A3H_HBYTES + NACT * HID2 * 4 + 64 * 4 + 32 * 4 + ACT3_OCC;
-template <bool GR = false, int DM = 1>
+// SAVE: the learner's online forward (evx_qmlp_forward2) through the same kernel -- X written by
+// fc1's A generator (first half), both H1 planes copied from LDS to a.h1 / a.h1l in 16-B row
+// pieces after each half's fc2, H2 and Q by fc3t_x3; no table path, no actions.
+template <bool GR = false, int DM = 1, bool SAVE = false>
 __global__ __launch_bounds__(256, 2) void qact3h_kernel(Fwd a0) {
     Fwd ag;
     if constexpr (GR) ag = fwd_net(a0, (int)blockIdx.y);
@@ -914,7 +917,7 @@ __global__ __launch_bounds__(256, 2) void qact3h_kernel(Fwd a0) {
         phS[tid - 224] = r2 < a.N ? drop_row(a.drop_seed, a.drop_stream, (a.drop_row0 + (uint32_t)krow(a, r2)) >> 1) : 0u;
     }
     bool fast = false;
-    if (a.stat) {  // tile-uniform: every row at the table's fire step, centre inside the map
+    if (!SAVE && a.stat) {  // tile-uniform: every row at the table's fire step, centre inside the map
         bool ok = true;
         if (tid < 64) {
             int pos = 0;
@@ -994,7 +997,7 @@ __global__ __launch_bounds__(256, 2) void qact3h_kernel(Fwd a0) {
                 }
             }
         } else {
-            fc1_tile<2, 2, 4, true, 2>(a, m0, col0, false, dsm, acc);  // ends with a barrier: A buffers free
+            fc1_tile<2, 2, 4, true, 2>(a, m0, col0, SAVE && hh == 0, dsm, acc);  // ends with a barrier: A buffers free
         }
         ACT_ST(2 + 4 * hh);
         float bias[2];
@@ -1046,6 +1049,15 @@ __global__ __launch_bounds__(256, 2) void qact3h_kernel(Fwd a0) {
                 }
         }
         ACT_ST(5 + 4 * hh);
+        if constexpr (SAVE) {  // this half's H1 planes for the backward: rows m0 .., columns 256 hh ..
+            for (int i = tid; i < 2 * 64 * 32; i += 256) {
+                const int pl = i >> 11, rl = (i >> 5) & 63, pc = i & 31;
+                if (m0 + rl < a.N) {
+                    const uint4 v = *reinterpret_cast<const uint4*>(pl ? &Hl[rl][pc * 8] : &Hh[rl][pc * 8]);
+                    *reinterpret_cast<uint4*>((pl ? a.h1l : a.h1) + (size_t)(m0 + rl) * HID + hh * 256 + pc * 8) = v;
+                }
+            }
+        }
         __syncthreads();  // every wave is done with this half: the next half / H2 reuse the planes
     }
     ACT_ST(10);
@@ -2006,23 +2018,23 @@ int evx_qmlp_pack3(const float* w1, const float* b1, const float* w2, uint16_t* 
     return mlaunch("qmlp_pack3");
 }
 
-// the x3 act kernel for the dropout mode of a (fc1_slab_m)
-extern "C++" template <bool GR>
+// the x3 act kernel for the dropout mode of a (fc1_slab_m); SAVE: the learner's online forward
+extern "C++" template <bool GR, bool SAVE = false>
 static void launch_act3(const evxm::Fwd& a, int32_t n, int nets, hipStream_t st) {
     static bool attr = false;
     if (!attr) {
-        const void* kh[3] = {(const void*)evxm::qact3h_kernel<GR, 0>, (const void*)evxm::qact3h_kernel<GR, 1>,
-                             (const void*)evxm::qact3h_kernel<GR, 2>};
+        const void* kh[3] = {(const void*)evxm::qact3h_kernel<GR, 0, SAVE>, (const void*)evxm::qact3h_kernel<GR, 1, SAVE>,
+                             (const void*)evxm::qact3h_kernel<GR, 2, SAVE>};
         for (const void* k : kh) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, evxm::ACT3H_LDS);
         attr = true;
     }
     const dim3 grid((unsigned)((n + 63) / 64), (unsigned)nets);
     if (a.drop_mask)
-        hipLaunchKernelGGL((evxm::qact3h_kernel<GR, 2>), grid, dim3(256), evxm::ACT3H_LDS, st, a);
+        hipLaunchKernelGGL((evxm::qact3h_kernel<GR, 2, SAVE>), grid, dim3(256), evxm::ACT3H_LDS, st, a);
     else if (a.drop_thresh)
-        hipLaunchKernelGGL((evxm::qact3h_kernel<GR, 1>), grid, dim3(256), evxm::ACT3H_LDS, st, a);
+        hipLaunchKernelGGL((evxm::qact3h_kernel<GR, 1, SAVE>), grid, dim3(256), evxm::ACT3H_LDS, st, a);
     else
-        hipLaunchKernelGGL((evxm::qact3h_kernel<GR, 0>), grid, dim3(256), evxm::ACT3H_LDS, st, a);
+        hipLaunchKernelGGL((evxm::qact3h_kernel<GR, 0, SAVE>), grid, dim3(256), evxm::ACT3H_LDS, st, a);
 }
 
 static int make_fwd(const evx_layout* lay, const evx_obs* obs, int32_t n, const evx_qmlp_params* p,
@@ -2236,11 +2248,28 @@ int evx_qmlp_forward2(const evx_layout* lay, int32_t n, const evx_obs* obs0, con
         // x3 learner: the second problem (the target net: Q only) through the fused act kernel
         // (H1 / H2 stay in LDS, 64-row tiles, two workgroups per CU) instead of qfc1 + qfc23
         // writing and re-reading both H1 planes; the first problem alone through qfc1 + qfc23
-        a1.stat = nullptr;
+        // the target net's own act table (static features x W1, rebuilt at each target sync --
+        // evacx.trainer attaches it to both nets): replay rows past the fire's last step (every
+        // row once the fire has stopped spreading: fire_step persists across resets) start fc1
+        // from it, the others run the full path per 64-row tile. EVX_TGT_TABLE=0: never.
+        static const bool tgt_table = !getenv("EVX_TGT_TABLE") || atoi(getenv("EVX_TGT_TABLE")) != 0;
+        if (!tgt_table) a1.stat = nullptr;
+        a1.perm = nullptr;
         a1.actions = nullptr;
         a1.h1 = a1.h1l = nullptr;
-        int rc2 = launch_fwd(a0, a0, n, 1, true, (hipStream_t)stream, true);
-        if (rc2) return rc2;
+        // the online forward too through the fused kernel when it saves everything the backward
+        // reads (X, both H1 planes, H2, Q): EVX_ONLINE_ACT=1 (measured no faster than qfc1 + qfc23
+        // at B = 32768: learn 0.420 vs 0.427 ms, tools/gpu_onact.sh)
+        static const bool on_act = getenv("EVX_ONLINE_ACT") && atoi(getenv("EVX_ONLINE_ACT")) != 0;
+        if (on_act && a0.x && a0.h1 && a0.h1l && a0.h2 && a0.q && !a0.actions && !a0.perm && !a0.raw) {
+            a0.stat = nullptr;
+            launch_act3<false, true>(a0, n, 1, (hipStream_t)stream);
+            int rc3 = mlaunch("qmlp_forward2 online act");
+            if (rc3) return rc3;
+        } else {
+            int rc2 = launch_fwd(a0, a0, n, 1, true, (hipStream_t)stream, true);
+            if (rc2) return rc2;
+        }
         launch_act3<false>(a1, n, 1, (hipStream_t)stream);
         return mlaunch("qmlp_forward2 target act");
     }

@@ -264,7 +264,13 @@ class VecTrainer:
             # are uniform. x3: on by default (the table replaces ~3/4 of fc1's products); bf16: off
             # by default (the rebuild costs what the act saves, tools/gpu_ab_static.sh)
             lc = self.lay.c  # centres only where robots can be (Map.robot_range): 55 of 130 columns at cfg3
-            self.fast.attach_static(lc, lc.L, lc.W, lc.t_max, x_range=(max(lc.rx_lo, 0), min(lc.rx_hi, lc.L + 1)))
+            xr = (max(lc.rx_lo, 0), min(lc.rx_hi, lc.L + 1))
+            self.fast.attach_static(lc, lc.L, lc.W, lc.t_max, x_range=xr)
+            if self.fast.x3 and os.environ.get("EVX_TGT_TABLE", "1") == "1":
+                # the target net's table too (rebuilt at each target sync): the learner's target
+                # forward (the fused act kernel at B >= 32768) starts fc1 from it for replay rows
+                # past the fire's last step
+                self.learner.fast_t.attach_static(lc, lc.L, lc.W, lc.t_max, x_range=xr)
             self._perm = torch.zeros(E, dtype=torch.int32, device=self.device)
             self.env.act_perm(self._perm)
 
