@@ -2244,7 +2244,8 @@ int evx_qmlp_forward2(const evx_layout* lay, int32_t n, const evx_obs* obs0, con
     static const bool tgt_act = !getenv("EVX_TGT_ACT") || atoi(getenv("EVX_TGT_ACT")) != 0;
     // (at n >= 32768 only: a fused act workgroup lives ~65 us on the full path, so below a full
     // round of workgroups the two-kernel forward wins -- B = 4096: learn 187 vs 127 us)
-    if (tgt_act && p0->x3 && out1->q && !out1->h2 && !out1->actions && !out1->x && n >= 32768) {
+    static const int tgt_min = getenv("EVX_TGT_ACT_MIN") ? atoi(getenv("EVX_TGT_ACT_MIN")) : 32768;
+    if (tgt_act && p0->x3 && out1->q && !out1->h2 && !out1->actions && !out1->x && n >= tgt_min) {
         // x3 learner: the second problem (the target net: Q only) through the fused act kernel
         // (H1 / H2 stay in LDS, 64-row tiles, two workgroups per CU) instead of qfc1 + qfc23
         // writing and re-reading both H1 planes; the first problem alone through qfc1 + qfc23

@@ -113,7 +113,8 @@ class _Group:
         # act, env.step, push on a high-priority stream: the learn stream's workgroups
         # then fill the env launch's tail instead of competing for its first slots
         self.main = torch.cuda.Stream(device=device, priority=int(os.environ.get("EVX_MAIN_PRIO", "-1")))
-        self.side = torch.cuda.Stream(device=device)  # dispatch order (and extra resets)
+        # dispatch order (and extra resets); EVX_SIDE_PRIO=-1: high priority (A/B)
+        self.side = torch.cuda.Stream(device=device, priority=int(os.environ.get("EVX_SIDE_PRIO", "0")))
         cur = torch.cuda.current_stream(device)
         self.ev_push = torch.cuda.Event()
         self.ev_push.record(cur)

@@ -67,6 +67,8 @@ def main():
                 mf = c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0)
                 # MFMA busy cycles summed over SIMDs: fraction of 1024 SIMDs x the kernel's cycles
                 line += f" clk {clk / 1e9:4.2f} GHz mfma {mf / (1024 * clk * dur):5.1%}"
+                # SQ_WAVE_CYCLES per CU-cycle: the mean waves resident per CU (the counter's raw ratio)
+                line += f" waves/CU {wc / (256 * clk * dur):5.2f}"
         print(line)
 
 
