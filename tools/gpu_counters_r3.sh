@@ -13,7 +13,10 @@ run3() {  # name, command...
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/t -o run --output-format csv -- "$@" > $OUT/trace.log 2>&1 || { tail $OUT/trace.log; return 1; }
   timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $SQ -d $OUT/sq -o run --output-format csv -- "$@" > $OUT/sq.log 2>&1 || { tail $OUT/sq.log; return 1; }
   timeout -s KILL 300 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE GRBM_COUNT -d $OUT/gr -o run --output-format csv -- "$@" > $OUT/gr.log 2>&1 || { tail $OUT/gr.log; return 1; }
-  python3 $R/tools/kstats.py $OUT > $OUT/kstats.txt 2>&1; cat $OUT/kstats.txt
+  python3 $R/tools/kstats.py $OUT > $OUT/kstats.txt 2>&1; head -25 $OUT/kstats.txt
+  # keep the summaries only (the raw per-dispatch CSVs of 1300 env launches exceed gpurun's 64 MiB)
+  find $OUT/t -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
+  rm -rf $OUT/t $OUT/sq $OUT/gr
 }
 run3 learn python3 $R/tools/learn_bench.py 32768 10 && \
 run3 act python3 $R/tools/act3_bench.py --table-frac 1.0 && \

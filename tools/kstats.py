@@ -64,11 +64,14 @@ def main():
             if g and gd:
                 dur = sum(gd[-5:]) / len(gd[-5:]) * 1e-6
                 clk = g / 8 / dur
+                if not 1.0e9 <= clk <= 2.6e9:  # GRBM_GUI_ACTIVE is chip-wide: short kernels see others' cycles
+                    clk = 2.4e9  # MI355X peak engine clock
                 mf = c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0)
                 # MFMA busy cycles summed over SIMDs: fraction of 1024 SIMDs x the kernel's cycles
                 line += f" clk {clk / 1e9:4.2f} GHz mfma {mf / (1024 * clk * dur):5.1%}"
-                # SQ_WAVE_CYCLES per CU-cycle: the mean waves resident per CU (the counter's raw ratio)
-                line += f" waves/CU {wc / (256 * clk * dur):5.2f}"
+                # SQ_WAVE_CYCLES counts quad-cycles on gfx950 (x4: the mean waves resident per CU,
+                # cross-checked against the env kernel's stamp-measured 7.95 per CU)
+                line += f" waves/CU {4 * wc / (256 * clk * dur):5.2f}"
         print(line)
 
 
