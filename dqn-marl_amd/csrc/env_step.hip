@@ -2185,9 +2185,12 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     const int nrem = P - evac - dead;
     int* ltab = reinterpret_cast<int*>(aux);  // leaf offsets | lengths
     double* leafsum = reinterpret_cast<double*>(pyring);
-    // the remaining persons' robot distances, in list order, go to the move-plan scratch
-    // (P doubles; the plan is dead once executed); the numpy leaves are summed after the pass
-    double* dist = reinterpret_cast<double*>(plan);
+    // the remaining persons' robot distances, in list order, go to the numpy ring's LDS (free since
+    // the contested lists) when they fit -- the leaf sums then read LDS after a wave fence -- else
+    // to the move-plan scratch (P doubles; the plan is dead once executed, but the leaf sums must
+    // wait for the stores to drain); the numpy leaves are summed after the pass
+    const bool dist_lds = nrem <= MT_N / 2;
+    double* dist = dist_lds ? reinterpret_cast<double*>(npring) : reinterpret_cast<double*>(plan);
     int nleaf = 0;
     if (lane == 0 && nrem > 0)
         nleaf = np_pairwise_leaves(nrem, ltab, ltab + LEAF_CAP, LEAF_CAP, reinterpret_cast<int*>(misc));
@@ -2287,7 +2290,10 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
         PT_END(rtop);
     }
     PT_BEGIN(leaf);
-    wave_sync();  // the distances are visible to every lane
+    if (dist_lds)
+        wave_fence();  // the distances (LDS) are visible to every lane
+    else
+        wave_sync();   // the distances (global scratch) are visible to every lane
     // numpy's pairwise leaves (<= 128 elements), 8 at a time: lane = 8 * leaf + chain j;
     // chain j sums a[j], a[j + 8], ... (numpy's r[j]), the 8 chains meet as
     // ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)) by xor-shuffles, and the leaf's
