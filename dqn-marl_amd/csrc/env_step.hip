@@ -2173,8 +2173,7 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
             }
         }
     }
-    wave_sync();
-    for (int i = lane; i < g.RW; i += 64) st.rmap[(size_t)e * g.RW + i] = rmapb[i];
+    wave_sync();  // the person words of the movers and the rmap bits complete
     EVX_STAMP(4);
 
     // ---------------------------------- fire update (both fire models)
@@ -2250,6 +2249,9 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     }
 #pragma unroll
     for (int k = 0; k < GQ; k++) load_pw(64 * k + lane, nxj[k], nxw[k], nxhv[k]);
+    // People.rmap back to HBM only now: stores issued before those loads would hold their waits
+    // (vmcnt counts loads and stores in issue order)
+    for (int i = lane; i < g.RW; i += 64) st.rmap[(size_t)e * g.RW + i] = rmapb[i];
     const int NITR = (nrl + 64 * GQ - 1) / (64 * GQ);
     for (int it = 0; it < NITR; it++) {
         PT_BEGIN(rtop);
