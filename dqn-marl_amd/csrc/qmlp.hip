@@ -2132,8 +2132,15 @@ static int launch_fwd(const evxm::Fwd& a0, const evxm::Fwd& a1, int32_t n, int p
         return mlaunch("qfc23 grouped");
     }
     if (x3) {  // f32-accurate: 128 x 256 tiles for large batches (register budget), else 64 x 128
-        static const int v = getenv("EVX_FC1X3") ? atoi(getenv("EVX_FC1X3")) : 0;  // tile experiments
-        if (v == 1 && big * pairs >= 384)
+        // tile experiments; the default for one problem (the learner's online forward beside the
+        // target through the fused act) is 64 x 256 (11: learn 391 -> 382 us at B = 32768,
+        // tools/gpu_fc1ab.sh), for two problems the choice below
+        static const int v = getenv("EVX_FC1X3") ? atoi(getenv("EVX_FC1X3")) : -1;
+        if (v == 11 || (v < 0 && pairs == 1 && fc23))  // 64 x 256 tiles at any batch
+            hipLaunchKernelGGL((evxm::qfc1_kernel<2, 2, 4, true>), dim3(blocks, 2, pairs), dim3(256), 0, st, a0, a1, pairs);
+        else if (v == 13)  // 128 x 256 tiles of 8 waves at any batch
+            hipLaunchKernelGGL((evxm::qfc1_kernel<4, 1, 8, true>), dim3(big, 2, pairs), dim3(512), 0, st, a0, a1, pairs);
+        else if (v == 1 && big * pairs >= 384)
             hipLaunchKernelGGL((evxm::qfc1_kernel<2, 2, 4, true>), dim3(blocks, 2, pairs), dim3(256), 0, st, a0, a1, pairs);
         else if (v == 2 && big * pairs >= 384)
             hipLaunchKernelGGL((evxm::qfc1_kernel<4, 2, 4, true>), dim3(big, 2, pairs), dim3(256), 0, st, a0, a1, pairs);
