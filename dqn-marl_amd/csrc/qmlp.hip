@@ -435,6 +435,12 @@ __device__ __forceinline__ void fc1_slab_m(const Fwd& a, const f32x16 (&accm)[NT
         const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;
         // rows rl, rl + 1 (rl even) stay a pair under the act permutation (rpe even)
         uint32_t ph = 0u;
+        uint2 ph3[2];  // MODE 3 (a row-permuted act): rows rl, rl + 1's pair hashes and halves
+        if constexpr (MODE == 3) {
+            const uint2* p3 = reinterpret_cast<const uint2*>(phs);
+            ph3[0] = p3[rl];
+            ph3[1] = p3[rl + 1];
+        }
         if constexpr (MODE == 1)
             ph = phs ? phs[rl >> 1]
                      : drop_row(a.drop_seed, a.drop_stream, (a.drop_row0 + (uint32_t)krow(a, row0 + rl)) >> 1);
@@ -454,6 +460,11 @@ __device__ __forceinline__ void fc1_slab_m(const Fwd& a, const f32x16 (&accm)[NT
                 const uint32_t hh = drop_pair(ph, (uint32_t)(col0 + cl));
                 v0 = (hh & 0xffffu) >= a.drop_thresh ? v0 * a.drop_scale : 0.f;
                 v1 = (hh >> 16) >= a.drop_thresh ? v1 * a.drop_scale : 0.f;
+            } else if constexpr (MODE == 3) {  // rows from different pairs: each its own pair's half
+                const uint32_t c = (uint32_t)(col0 + cl);
+                const uint32_t h0 = drop_pair(ph3[0].x, c), h1 = drop_pair(ph3[1].x, c);
+                v0 = (ph3[0].y ? h0 >> 16 : h0 & 0xffffu) >= a.drop_thresh ? v0 * a.drop_scale : 0.f;
+                v1 = (ph3[1].y ? h1 >> 16 : h1 & 0xffffu) >= a.drop_thresh ? v1 * a.drop_scale : 0.f;
             }
             if constexpr (X3) {
                 split2(v0, dst[rl][cl], dstl[rl][cl]);
@@ -892,7 +903,7 @@ __device__ long long g_act_st[8192 * ACT_NST];
 // [64 w, 64 w + 64) of each fc1 half and of fc2 (2 column tiles), both 32-row slabs.
 constexpr int A3H_HBYTES = 2 * 64 * A3_HP * 2;  // 67,584: both H1 half planes of 64 rows
 static_assert(A3H_HBYTES >= 2 * 64 * (KC1 + 8) * 2, "fc1 A staging overlays the H1 planes");
-constexpr int ACT3H_LDS = A3H_HBYTES + NACT * HID2 * 4 + 64 * 4 + 32 * 4 + ACT3_OCC;
+constexpr int ACT3H_LDS = A3H_HBYTES + NACT * HID2 * 4 + 64 * 4 + 64 * 8 + ACT3_OCC;  // posS, phS (DM 3: [64] uint2)
 // SAVE: the learner's online forward (evx_qmlp_forward2) through the same kernel -- X written by
 // fc1's A generator (first half), both H1 planes copied from LDS to a.h1 / a.h1l in 16-B row
 // pieces after each half's fc2, H2 and Q by fc3t_x3; no table path, no actions.
@@ -907,7 +918,7 @@ __global__ __launch_bounds__(256, 2) void qact3h_kernel(Fwd a0) {
     auto W3s = reinterpret_cast<float (*)[HID2]>(dsm + A3H_HBYTES);
     int* posS = reinterpret_cast<int*>(dsm + A3H_HBYTES + NACT * HID2 * 4);
     uint32_t* phS = reinterpret_cast<uint32_t*>(dsm + A3H_HBYTES + NACT * HID2 * 4 + 64 * 4);
-    uint4* occT = reinterpret_cast<uint4*>(dsm + A3H_HBYTES + NACT * HID2 * 4 + 64 * 4 + 32 * 4);
+    uint4* occT = reinterpret_cast<uint4*>(dsm + A3H_HBYTES + NACT * HID2 * 4 + 64 * 4 + 64 * 8);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
     const int m0 = blockIdx.x * 64;
     ACT_ST(0);
@@ -915,6 +926,15 @@ __global__ __launch_bounds__(256, 2) void qact3h_kernel(Fwd a0) {
     if (DM == 1 && tid >= 224) {  // the tile's 32 row-pair dropout hashes (published by the barriers below)
         const int r2 = m0 + 2 * (tid - 224);
         phS[tid - 224] = r2 < a.N ? drop_row(a.drop_seed, a.drop_stream, (a.drop_row0 + (uint32_t)krow(a, r2)) >> 1) : 0u;
+    }
+    if (DM == 3 && tid >= 192) {  // row-permuted act: every tile row's pair hash and half (the same masks)
+        const int r = m0 + (tid - 192);
+        uint2 v = make_uint2(0u, 0u);
+        if (r < a.N) {
+            const uint32_t k = a.drop_row0 + (uint32_t)krow(a, r);
+            v = make_uint2(drop_row(a.drop_seed, a.drop_stream, k >> 1), k & 1u);
+        }
+        reinterpret_cast<uint2*>(phS)[tid - 192] = v;
     }
     bool fast = false;
     if (!SAVE && a.stat) {  // tile-uniform: every row at the table's fire step, centre inside the map
@@ -1007,7 +1027,8 @@ __global__ __launch_bounds__(256, 2) void qact3h_kernel(Fwd a0) {
         for (int mt = 0; mt < 2; mt++)
             fc1_slab_m<2, A3_HP, true, DM>(a, acc[mt], bias, m0 + mt * 32, hh * 256, w * 64,
                                            reinterpret_cast<__bf16 (*)[A3_HP]>(&Hh[mt * 32][0]),
-                                           reinterpret_cast<__bf16 (*)[A3_HP]>(&Hl[mt * 32][0]), phS + mt * 16);
+                                           reinterpret_cast<__bf16 (*)[A3_HP]>(&Hl[mt * 32][0]),
+                                           phS + (DM == 3 ? mt * 64 : mt * 16));
         ACT_ST(3 + 4 * hh);
         __syncthreads();
         ACT_ST(4 + 4 * hh);
@@ -2023,14 +2044,16 @@ extern "C++" template <bool GR, bool SAVE = false>
 static void launch_act3(const evxm::Fwd& a, int32_t n, int nets, hipStream_t st) {
     static bool attr = false;
     if (!attr) {
-        const void* kh[3] = {(const void*)evxm::qact3h_kernel<GR, 0, SAVE>, (const void*)evxm::qact3h_kernel<GR, 1, SAVE>,
-                             (const void*)evxm::qact3h_kernel<GR, 2, SAVE>};
+        const void* kh[4] = {(const void*)evxm::qact3h_kernel<GR, 0, SAVE>, (const void*)evxm::qact3h_kernel<GR, 1, SAVE>,
+                             (const void*)evxm::qact3h_kernel<GR, 2, SAVE>, (const void*)evxm::qact3h_kernel<GR, 3, SAVE>};
         for (const void* k : kh) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, evxm::ACT3H_LDS);
         attr = true;
     }
     const dim3 grid((unsigned)((n + 63) / 64), (unsigned)nets);
     if (a.drop_mask)
         hipLaunchKernelGGL((evxm::qact3h_kernel<GR, 2, SAVE>), grid, dim3(256), evxm::ACT3H_LDS, st, a);
+    else if (a.drop_thresh && a.perm && a.rpe == 1)  // a row permutation: rows of different pairs share tiles
+        hipLaunchKernelGGL((evxm::qact3h_kernel<GR, 3, SAVE>), grid, dim3(256), evxm::ACT3H_LDS, st, a);
     else if (a.drop_thresh)
         hipLaunchKernelGGL((evxm::qact3h_kernel<GR, 1, SAVE>), grid, dim3(256), evxm::ACT3H_LDS, st, a);
     else
@@ -2112,7 +2135,10 @@ static int make_fwd(const evx_layout* lay, const evx_obs* obs, int32_t n, const 
     a.rpe = out->rows_per_env > 0 ? out->rows_per_env : 1;
     a.gn = 0;
     a.g = 0;
-    if (a.perm && (a.rpe & 1)) return mfail(-22, "qmlp_forward: rows_per_env must be even (dropout row pairs)");
+    // rows_per_env even (dropout row pairs stay together), or 1: a row permutation, the x3 act only
+    // (qact3h_kernel's per-row pair hashes)
+    if (a.perm && (a.rpe & 1) && !(a.rpe == 1 && p->x3))
+        return mfail(-22, "qmlp_forward: rows_per_env must be even (dropout row pairs), or 1 for the x3 act");
     return 0;
 }
 
@@ -2173,6 +2199,7 @@ static int launch_fwd(const evxm::Fwd& a0, const evxm::Fwd& a1, int32_t n, int p
 int evx_qmlp_forward(const evx_layout* lay, const evx_obs* obs, int32_t n, const evx_qmlp_params* p,
                      const evx_qmlp_dropout* drop, const evx_qmlp_fwd_out* out, void* stream) {
     if (n <= 0) return 0;
+    if (out && out->perm && out->rows_per_env == 1) return mfail(-22, "qmlp_forward: row permutations are the act's");
     evxm::Fwd a;
     int rc = make_fwd(lay, obs, n, p, drop, out, a);
     if (rc) return rc;

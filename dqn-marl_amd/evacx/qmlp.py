@@ -274,9 +274,11 @@ class MLPFast:
         _need("act obs", obs, n, 8)
         _need("act q", q, n, NACT)
         _need("act actions", actions, n, 1)
-        if perm is not None and (rows_per_env <= 0 or rows_per_env % 2 or n % rows_per_env
-                                 or perm.numel() < n // rows_per_env):
-            raise ValueError("qmlp act: perm needs an even rows_per_env dividing n and n / rows_per_env entries")
+        # rows_per_env 1: a row permutation (x3 only: the act kernel hashes every row's dropout pair)
+        if perm is not None and (rows_per_env <= 0 or (rows_per_env % 2 and not (rows_per_env == 1 and self.x3))
+                                 or n % rows_per_env or perm.numel() < n // rows_per_env):
+            raise ValueError("qmlp act: perm needs an even rows_per_env (or 1, x3) dividing n and n / rows_per_env "
+                             "entries")
         d = self._drop(drop) if drop else None
         o = evx_qmlp_fwd_out(q=_p(q), actions=_p(actions), epsilon=float(epsilon), act_seed=act_seed,
                              act_offset=act_offset, perm=_p(perm), rows_per_env=int(rows_per_env))

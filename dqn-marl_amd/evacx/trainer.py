@@ -257,6 +257,7 @@ class VecTrainer:
         self._hg = np.random.Generator(np.random.PCG64([self.seed & 0xFFFFFFFF, 0x5EED5]))
         self.last_split = None  # (old rows, fresh rows) of the last split learn step
         self._perm = None
+        self._rowperm = None
         if self.fast is not None and layout_of is None and len(self.groups) == 1 and \
                 os.environ.get("EVX_ACT_STATIC", "1" if self.fast.x3 else "0") == "1":
             # act fast path: envs past the fire's last step start fc1 from a per-centre table of the
@@ -273,7 +274,40 @@ class VecTrainer:
                 # past the fire's last step
                 self.learner.fast_t.attach_static(lc, lc.L, lc.W, lc.t_max, x_range=xr)
             self._perm = torch.zeros(E, dtype=torch.int32, device=self.device)
-            self.env.act_perm(self._perm)
+            self._rowperm = None
+            if self.fast.x3 and os.environ.get("EVX_ACT_ROWPERM", "0") == "1":
+                # the act's rows sorted by (table path, window centre) instead of its envs by table path
+                # (evx_act_row_perm): rows sharing a table row share tiles, which then read a few table
+                # rows from L2 instead of 64 scattered ones; every row keeps its own results and mask
+                L = _lib.lib()
+                L.evx_act_row_perm_bytes.restype = C.c_int64
+                L.evx_act_row_perm_bytes.argtypes = [C.c_int32]
+                L.evx_act_row_perm.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                               C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]
+                L.evx_act_row_perm_last_error.restype = C.c_char_p
+                nb = int(L.evx_act_row_perm_bytes(n))
+                if nb < 0:
+                    raise _lib.EvacxError("evx_act_row_perm_bytes failed")
+                i32 = dict(dtype=torch.int32, device=self.device)
+                self._rowperm = (torch.empty(2 * n, **i32), torch.empty(n, **i32),
+                                 torch.empty(max(nb, 1), dtype=torch.uint8, device=self.device))
+                self._perm = torch.zeros(n, **i32)
+            self._act_order(self.groups[0])
+
+    def _act_order(self, grp: _Group):
+        """The next act's order on the current stream: its rows by (table path, window centre)
+        (evx_act_row_perm) or its envs by table path (VecEnv.act_perm)."""
+        if self._rowperm is None:
+            grp.env.act_perm(self._perm)
+            return
+        keys, rows, tmp = self._rowperm
+        c = self.fast.c
+        L = _lib.lib()
+        rc = L.evx_act_row_perm(C.byref(self.lay.c), grp.env.obs.data_ptr(), grp.n, int(c.stat_fs), int(c.stat_x0),
+                                int(c.stat_nx), keys.data_ptr(), rows.data_ptr(), self._perm.data_ptr(),
+                                tmp.data_ptr(), tmp.numel(), _stream())
+        if rc != 0:
+            raise _lib.EvacxError(f"act_row_perm failed ({rc}): {L.evx_act_row_perm_last_error().decode()}")
 
     def _act(self, grp: _Group):
         """DQNAgent.act in train mode for one group's robots: dropout active, epsilon-greedy
@@ -289,7 +323,8 @@ class VecTrainer:
             self.fast.act(self.lay.c, grp.env.obs, grp.n,
                           drop=(self.learner.seed, self.learner.drop_stream, DROPOUT_P, None, g0),
                           actions=grp.actions, epsilon=float(self.epsilon), act_seed=self.act_seed, act_offset=off,
-                          perm=self._perm, rows_per_env=self.R if self._perm is not None else 0)
+                          perm=self._perm,
+                          rows_per_env=0 if self._perm is None else (1 if self._rowperm is not None else self.R))
             return
         x = grp.env.expand_obs(torch.float32)  # [E/G, R, 11, 11, 6]
         Q = self.learner.q_values(x.view(grp.n, 11, 11, 6), train=True)
@@ -500,7 +535,7 @@ class VecTrainer:
                 self.replay.push(grp.env.obs_prev, grp.env.obs, grp.actions, grp.env.reward, grp.env.done, grp.n,
                                  self.R, s2_term=grp.env.obs_term)
                 if self._perm is not None and inline:  # the next act's env order, on this stream
-                    grp.env.act_perm(self._perm)
+                    self._act_order(grp)
                 grp.ev_push.record(grp.main)
         if extra_reset is not None:  # after every group's push, on group 0's side stream (warm-up only)
             side = G[0].side
@@ -523,7 +558,7 @@ class VecTrainer:
                 if extra_reset is not None:
                     st.wait_event(self.ev_reset)
                 if self._perm is not None:  # the next act's env order (the act waits for ev_order)
-                    grp.env.act_perm(self._perm)
+                    self._act_order(grp)
                 grp.env.compute_order()
                 if st is grp.side:
                     grp.ev_order.record(st)

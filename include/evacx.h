@@ -403,7 +403,8 @@ typedef struct {
     /* x3: h1 holds two planes [2][n][512] (hi, lo) and x spans [n][640] */
     /* act only, optional: batch row i is observation / action row perm[i / rows_per_env] * rows_per_env +
      * i % rows_per_env (evx_act_perm: envs at the table's fire step first, so act tiles are uniform);
-     * dropout rows and epsilon draws stay keyed by that original row */
+     * dropout rows and epsilon draws stay keyed by that original row. rows_per_env 1 (x3 act only):
+     * a row permutation (evx_act_row_perm), every tile row hashing its own dropout pair */
     const int32_t *perm;
     int32_t rows_per_env;
 } evx_qmlp_fwd_out;
@@ -436,6 +437,16 @@ int evx_qmlp_forward(const evx_layout *lay, const evx_obs *obs, int32_t n, const
  * set): the same products summed in another order. */
 int evx_qmlp_act(const evx_layout *lay, const evx_obs *obs, int32_t n, const evx_qmlp_params *p,
                  const evx_qmlp_dropout *drop, const evx_qmlp_fwd_out *out, void *stream);
+/* The x3 act's row order (DQNAgent.act, agents/dqn_agent.py:101-124): perm [n] = the rows of obs
+ * sorted by (not on the table path of p's stat_fs / stat_x0 / stat_nx -- stat_fs < 0: none --,
+ * window centre), stably (a radix sort: deterministic), for evx_qmlp_act's perm with rows_per_env
+ * 1: rows sharing an act-table row share tiles. keys [2n], rows [n] scratch; temp of
+ * evx_act_row_perm_bytes(n) bytes. Changes no result of the act. */
+int64_t evx_act_row_perm_bytes(int32_t n);
+int evx_act_row_perm(const evx_layout *lay, const evx_obs *obs, int32_t n, int32_t stat_fs, int32_t stat_x0,
+                     int32_t stat_nx, uint32_t *keys, int32_t *rows, int32_t *perm, void *temp, int64_t temp_bytes,
+                     void *stream);
+const char *evx_act_row_perm_last_error(void);
 /* Two forwards of n rows in one launch pair (the learner's online and target nets). */
 int evx_qmlp_forward2(const evx_layout *lay, int32_t n, const evx_obs *obs0, const evx_qmlp_params *p0,
                       const evx_qmlp_dropout *drop0, const evx_qmlp_fwd_out *out0, const evx_obs *obs1,

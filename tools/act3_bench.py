@@ -19,6 +19,9 @@ ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--table-frac", type=float, default=0.0,
                 help="fraction of rows (the first ones) at the fire's last step, through the act table "
                      "(attach_static over Map.robot_range, as the trainer)")
+ap.add_argument("--order", choices=["env", "centre", "shuffle"], default="env",
+                help="row order: env (the envs' own), centre (sorted by window centre: rows sharing a table row "
+                     "adjacent), shuffle (random)")
 args = ap.parse_args()
 E, R = 4096, 16
 lay = DeviceLayout(build_tables(synthetic(128, 128, R)), 2276)
@@ -36,6 +39,10 @@ if args.table_frac > 0:
     lr.fast.attach_static(c, c.L, c.W, c.t_max, x_range=(c.rx_lo, c.rx_hi))
     nt = int(args.rows * args.table_frac) // 128 * 128
     obs[:nt, 6] = int(c.t_max)
+if args.order == "centre":
+    obs = obs[torch.argsort(obs[:, 4].long() * 4096 + obs[:, 5].long(), stable=True)].contiguous()
+elif args.order == "shuffle":
+    obs = obs[torch.randperm(obs.shape[0], device="cuda")].contiguous()
 act = torch.empty(args.rows, dtype=torch.int32, device="cuda")
 for i in range(3):
     lr.fast.act(lay.c, obs.view(-1), args.rows, drop=(1, i, DROPOUT_P), actions=act, epsilon=0.1)
