@@ -257,7 +257,10 @@ def test_fused_learn_chain_matches_separate_launches(hook):
     assert abs(sep["norm"] - fus["norm"]) <= 1e-5 * sep["norm"] + 1e-9
     for k in sep["params"]:
         scale = sep["grads"][k].abs().max().item()
-        torch.testing.assert_close(fus["grads"][k], sep["grads"][k], rtol=1e-4, atol=1e-6 * scale + 1e-12)
+        # atol 2e-6 of the tensor's scale: after three Adam steps the runs' parameters differ by the
+        # reassociation of f32 sums (and the order of qbwd3's / qdz1's f32 atomics into W3, b2, b1),
+        # which moved one element 2.1e-8 of a 1.8e-8 bound at 1e-6 in one of many runs
+        torch.testing.assert_close(fus["grads"][k], sep["grads"][k], rtol=1e-4, atol=2e-6 * scale + 1e-12)
         torch.testing.assert_close(fus["params"][k], sep["params"][k], rtol=1e-5, atol=2e-6)
     lr = fus["lr"]
     lr.fast.repack()  # pack3 of the fused run's own parameters
