@@ -2086,6 +2086,20 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
 #endif
     EVX_STAMP(3);
 
+    // the reward's first list entries (the rows phase left the list final) are loaded here, so
+    // their latency runs under execute_move's (the person words they index are read after it)
+    auto load_idx = [&](int i) -> uint32_t {  // person | (list index << 16)
+        uint32_t p = 0u;
+        if (i < nrl) p = rl[i].x;
+        return p;
+    };
+    uint32_t nxj[GQ], nnj[GQ];
+#pragma unroll
+    for (int k = 0; k < GQ; k++) {
+        nxj[k] = load_idx(64 * k + lane);
+        nnj[k] = load_idx(64 * (GQ + k) + lane);
+    }
+
     // --------------------------------------------- execute_move, in order
     plan_pass([&](const uint2 en, bool ok) {
         if (ok) {
@@ -2226,11 +2240,6 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
         q += __popcll(rm);
         PT_END(rew);
     };
-    auto load_idx = [&](int i) -> uint32_t {  // person | (list index << 16)
-        uint32_t p = 0u;
-        if (i < nrl) p = rl[i].x;
-        return p;
-    };
     auto load_pw = [&](int i, uint32_t px, uint32_t& w, double& h) {
         w = DONEPK;
         h = 0.0;
@@ -2240,13 +2249,8 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
             h = h_g[p];
         }
     };
-    uint32_t nxj[GQ], nnj[GQ], nxw[GQ];
+    uint32_t nxw[GQ];
     double nxhv[GQ];
-#pragma unroll
-    for (int k = 0; k < GQ; k++) {
-        nxj[k] = load_idx(64 * k + lane);
-        nnj[k] = load_idx(64 * (GQ + k) + lane);
-    }
 #pragma unroll
     for (int k = 0; k < GQ; k++) load_pw(64 * k + lane, nxj[k], nxw[k], nxhv[k]);
     // People.rmap back to HBM only now: stores issued before those loads would hold their waits
