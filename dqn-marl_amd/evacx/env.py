@@ -21,7 +21,16 @@ REWARD_DEFAULTS = dict(evac_reward=50.0, death_penalty=200.0, death_acc_penalty=
 OBS_WORDS = 8  # sizeof(evx_obs) / 4
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+_cur_dev = getattr(torch._C, "_cuda_getDevice", None)
+
+
 def _stream() -> int:
+    """The current HIP stream handle. Called by every launch: the raw C accessors cost ~1 us, where
+    torch.cuda.current_stream() builds a Stream object after device / availability checks (~8 us
+    of host time each, ~16 per training step -- tools/host_profile.py)."""
+    if _raw_stream is not None and _cur_dev is not None:
+        return _raw_stream(_cur_dev())
     return torch.cuda.current_stream().cuda_stream
 
 

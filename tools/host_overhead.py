@@ -14,7 +14,8 @@ from evacx.layout import build_tables, synthetic  # noqa: E402
 from evacx.trainer import VecTrainer  # noqa: E402
 
 lagged = "--strict" not in sys.argv
-lay = DeviceLayout(build_tables(synthetic(128, 128, 16)), 2276)
+cfg2 = "--cfg2" in sys.argv  # 64x64, 569 people, 8 robots (BASELINE cfg2), else 128x128 / 2276 / 16
+lay = DeviceLayout(build_tables(synthetic(64, 64, 8) if cfg2 else synthetic(128, 128, 16)), 569 if cfg2 else 2276)
 tr = VecTrainer(lay, 4096, batch=4096, lagged_learn=lagged)
 for _ in range(300):
     tr.step()
@@ -30,5 +31,5 @@ tr.sync()
 torch.cuda.synchronize()
 tot = (time.perf_counter() - t0) / 200
 host.sort()
-print(f"lagged={lagged} host per step: median {1e6 * host[100]:.0f} us, mean {1e6 * sum(host) / 200:.0f} us; "
+print(f"cfg2={cfg2} lagged={lagged} host per step: median {1e6 * host[100]:.0f} us, mean {1e6 * sum(host) / 200:.0f} us; "
       f"wall per step {1e6 * tot:.0f} us")
