@@ -149,12 +149,18 @@ def parse():
         args.envs = args.envs_total // world
     if args.batch <= 0:
         args.batch = args.envs
-    if args.replay_capacity <= 0:
-        c = 1
-        while c < 16 * args.envs * args.robots:
-            c <<= 1
-        args.replay_capacity = c
+    args.auto_capacity = args.replay_capacity <= 0
+    if args.auto_capacity:
+        args.replay_capacity = replay_capacity_for(args.envs, args.robots)
     return args
+
+
+def replay_capacity_for(E, R):
+    """The default ring: the power of two >= 16 steps of pushes (E envs x R robots x 16)."""
+    c = 1
+    while c < 16 * E * R:
+        c <<= 1
+    return c
 
 
 def cpu_model():
@@ -232,10 +238,11 @@ def main():
         """The trainer for E envs per rank (global env ids rank * E + e), prepared to the episode
         phase: env-only steps (uniform random actions) where preparation step w force-resets the
         envs with global id % stagger == w, spreading env ages over one episode length."""
+        cap = replay_capacity_for(E, R) if args.auto_capacity else args.replay_capacity
         tr = VecTrainer(lay, E, env_offset=rank * E, kind=args.qnet, precision=args.precision, batch=batch,
                         grad_hook=hook,
                         lagged_learn=args.schedule == "lagged", replay=args.replay,
-                        replay_capacity=args.replay_capacity, groups=args.groups if args.mode == "train" else 1,
+                        replay_capacity=cap, groups=args.groups if args.mode == "train" else 1,
                         layout_of=layout_of, world_envs=E * world, nets=args.nets)
         env = tr.env
         gid = torch.arange(E, device="cuda") + rank * E
@@ -307,21 +314,6 @@ def main():
     learn_ms = ev_mean(ev_learn, args.steps) if args.mode == "train" else None
     loss = float(tr.last_loss.float().mean().item()) if tr.last_loss is not None else None
     value = E * world * args.steps / elapsed
-    split = args.mode == "train" and tr.split and schedule == "strict"
-
-    # ---------------- the learn step alone, one part at B (extra: its MFMA roofline)
-    # with the split learn step the timed events above cover only its tail (fresh rows, clip,
-    # Adam: the part on the step's critical path); the whole learn chain is timed here alone
-    learn_alone_ms = None
-    if args.mode == "train" and tr.fast is not None and tr.replay.size >= args.batch:
-        tr.sync()
-        ev_l = ev_pairs(6)
-        for i in range(6):
-            ev_l[i][0].record()
-            tr.learn()
-            ev_l[i][1].record()
-        torch.cuda.synchronize()
-        learn_alone_ms = float(np.mean([ev_l[i][0].elapsed_time(ev_l[i][1]) for i in range(1, 6)]))
 
     # ------------------------------- the other schedule on the same state (extra)
     other = None
@@ -354,6 +346,22 @@ def main():
         start = {"steps_per_s": E * world * args.start_steps / dt, "env_step_kernel_ms": ev_mean(ev_s, args.start_steps),
                  "steps": args.start_steps,
                  "what": "every env reset (all persons in play), then the timed training steps"}
+
+    # ------ the learn step alone (extra: its MFMA roofline). The last reading on the headline
+    # trainer (its six extra learn steps move the weights, Adam, epsilon); without the gradient
+    # all-reduce, so it is the learn chain's own time at any world size
+    learn_alone_ms = None
+    if args.mode == "train" and tr.fast is not None and tr.replay.size >= args.batch:
+        tr.sync()
+        hook_saved, tr.learner.grad_hook = tr.learner.grad_hook, None
+        ev_l = ev_pairs(6)
+        for i in range(6):
+            ev_l[i][0].record()
+            tr.learn()
+            ev_l[i][1].record()
+        torch.cuda.synchronize()
+        tr.learner.grad_hook = hook_saved
+        learn_alone_ms = float(np.mean([ev_l[i][0].elapsed_time(ev_l[i][1]) for i in range(1, 6)]))
 
     # ---------- BASELINE configs[2] read as envs for the whole job (extra, N > 1 only)
     total = None
@@ -446,10 +454,7 @@ def main():
             "start_phase": start,
             "env_step_kernel_ms": kern_ms,
             "learn_ms": learn_ms,
-            "learn_ms_what": ("the split learn step's tail on the critical path (fresh rows' forward + backward, "
-                              "clip + Adam); its old rows run on the learn stream beside act and env.step"
-                              if split else "the learn step on the training stream"),
-            "learn_split_rows": list(tr.last_split) if split and tr.last_split else None,
+            "learn_ms_what": "the learn step on the training stream (every 5th timed step)",
             "learn_alone_ms": learn_alone_ms,
             "last_loss": loss,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -462,14 +467,14 @@ def main():
                          "launches_timed": len([s for s in range(args.steps) if s % EV_EVERY == 0])},
             "cpu_baseline": cpu,
         }
-        lm = learn_alone_ms if learn_alone_ms is not None else (None if split else learn_ms)
+        lm = learn_alone_ms if learn_alone_ms is not None else learn_ms
         if lm is not None and args.qnet == "mlp":
             fl = qnet_flops(0, args.batch)
             line["roofline_learn"] = {"bound": "mfma", "achieved": fl / (lm * 1e-3) / 1e12,
                                       "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                                       "frac": fl / (lm * 1e-3) / 1e12 / BF16_PEAK_TFLOPS, "learn_ms": lm,
-                                      "flops_basis": "dense f32-equivalent FLOPs of one learn step (B rows in one "
-                                                     "part, timed alone)"}
+                                      "flops_basis": "dense f32-equivalent FLOPs of one learn step (B rows, timed "
+                                                     "alone, no all-reduce)"}
         print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()

@@ -904,10 +904,7 @@ __device__ long long g_act_st[8192 * ACT_NST];
 constexpr int A3H_HBYTES = 2 * 64 * A3_HP * 2;  // 67,584: both H1 half planes of 64 rows
 static_assert(A3H_HBYTES >= 2 * 64 * (KC1 + 8) * 2, "fc1 A staging overlays the H1 planes");
 constexpr int ACT3H_LDS = A3H_HBYTES + NACT * HID2 * 4 + 64 * 4 + 64 * 8 + ACT3_OCC;  // posS, phS (DM 3: [64] uint2)
-// SAVE: the learner's online forward (evx_qmlp_forward2) through the same kernel -- X written by
-// fc1's A generator (first half), both H1 planes copied from LDS to a.h1 / a.h1l in 16-B row
-// pieces after each half's fc2, H2 and Q by fc3t_x3; no table path, no actions.
-template <bool GR = false, int DM = 1, bool SAVE = false>
+template <bool GR = false, int DM = 1>
 __global__ __launch_bounds__(256, 2) void qact3h_kernel(Fwd a0) {
     Fwd ag;
     if constexpr (GR) ag = fwd_net(a0, (int)blockIdx.y);
@@ -937,7 +934,7 @@ __global__ __launch_bounds__(256, 2) void qact3h_kernel(Fwd a0) {
         reinterpret_cast<uint2*>(phS)[tid - 192] = v;
     }
     bool fast = false;
-    if (!SAVE && a.stat) {  // tile-uniform: every row at the table's fire step, centre inside the map
+    if (a.stat) {  // tile-uniform: every row at the table's fire step, centre inside the map
         bool ok = true;
         if (tid < 64) {
             int pos = 0;
@@ -1017,7 +1014,7 @@ __global__ __launch_bounds__(256, 2) void qact3h_kernel(Fwd a0) {
                 }
             }
         } else {
-            fc1_tile<2, 2, 4, true, 2>(a, m0, col0, SAVE && hh == 0, dsm, acc);  // ends with a barrier: A buffers free
+            fc1_tile<2, 2, 4, true, 2>(a, m0, col0, false, dsm, acc);  // ends with a barrier: A buffers free
         }
         ACT_ST(2 + 4 * hh);
         float bias[2];
@@ -1070,15 +1067,6 @@ __global__ __launch_bounds__(256, 2) void qact3h_kernel(Fwd a0) {
                 }
         }
         ACT_ST(5 + 4 * hh);
-        if constexpr (SAVE) {  // this half's H1 planes for the backward: rows m0 .., columns 256 hh ..
-            for (int i = tid; i < 2 * 64 * 32; i += 256) {
-                const int pl = i >> 11, rl = (i >> 5) & 63, pc = i & 31;
-                if (m0 + rl < a.N) {
-                    const uint4 v = *reinterpret_cast<const uint4*>(pl ? &Hl[rl][pc * 8] : &Hh[rl][pc * 8]);
-                    *reinterpret_cast<uint4*>((pl ? a.h1l : a.h1) + (size_t)(m0 + rl) * HID + hh * 256 + pc * 8) = v;
-                }
-            }
-        }
         __syncthreads();  // every wave is done with this half: the next half / H2 reuse the planes
     }
     ACT_ST(10);
@@ -1302,7 +1290,9 @@ __global__ __launch_bounds__(256) void pack_occ3_kernel(const float* __restrict_
 //   fc1: dW1 = dZ1^T X over the compact K, scattered to the reference's columns;
 //        the constant centre column (channel 5, x = 1) gets sum dZ1 = db1, channel 0
 //        (x = 0) gets nothing
-// Gradients accumulate with f32 atomics into a zeroed buffer (split-K).
+// Every gradient sum is ordered (no f32 atomics, the same bits on every run): the weight
+// gradients by split-K partials (gemm_tn_body), the fc3 / bias sums by per-block partials
+// (p3: qbwd3, pz1: qdz1), all added in a fixed order by reduce2_kernel.
 struct Bwd {
     int B;
     const float* dq;    // [B][5]
@@ -1320,6 +1310,9 @@ struct Bwd {
     const __bf16* w2tl;
     __bf16* dz2l;
     __bf16* dz1l;
+    float* p3;    // qbwd3 block partials [nb3][P3W]: dW3 [5][256], db2 [256], db3 [5]
+    float* pz1;   // qdz1 column-sum partials [ndzx][512] (db1 = the centre column of dW1)
+    int64_t gsP;  // grouped: floats between consecutive nets' partial regions
 };
 // net g's view of a blocked grouped backward (see fwd_net; x3: two planes per activation)
 __device__ __forceinline__ Bwd bwd_net(const Bwd& a0, int g) {
@@ -1343,15 +1336,18 @@ __device__ __forceinline__ Bwd bwd_net(const Bwd& a0, int g) {
     a.gb2 += G * NPAR;
     a.gw3 += G * NPAR;
     a.gb3 += G * NPAR;
+    a.p3 += G * a.gsP;
+    a.pz1 += G * a.gsP;
     return a;
 }
 
 // fc3 backward: thread n of a 128-row block walks the rows (coalesced over n) in chunks of 32.
-// The block's fc3 gradients leave by one f32 atomic per column and output: 32-row blocks put
-// 1024 same-address atomics on every dW3 / db2 word at B = 32768 and ran at their serial rate
-// (38 us); 128-row blocks cut that to 256.
+// The block's fc3 gradients leave as one partial row p3[block] (P3W floats: dW3, db2, db3),
+// summed over blocks in block order by reduce2_kernel (f32 atomics here made the learn chain
+// differ between same-seed runs at the ulp level).
 // Small batches take rb = 64 or 32 rows per block (qbwd3_rows: B = 4096 had 32 blocks).
 constexpr int R3 = 128, R3C = 32;
+constexpr int P3W = NACT * HID2 + HID2 + 8;  // dW3 [5][256] | db2 [256] | db3 [5] (+ pad)
 inline int qbwd3_rows(int B) { return B >= 16384 ? 128 : B >= 8192 ? 64 : 32; }
 template <bool X3 = false, bool GR = false>  // GR: blockIdx.y = net
 __global__ __launch_bounds__(256) void qbwd3_kernel(Bwd a0, int rb) {
@@ -1401,13 +1397,14 @@ __global__ __launch_bounds__(256) void qbwd3_kernel(Bwd a0, int rb) {
             break;
         }
     }
+    float* pr = a.p3 + (size_t)blockIdx.x * P3W;
 #pragma unroll
-    for (int t = 0; t < NACT; t++) atomicAdd(&a.gw3[t * HID2 + n], gw[t]);
-    atomicAdd(&a.gb2[n], gb2);
+    for (int t = 0; t < NACT; t++) pr[t * HID2 + n] = gw[t];
+    pr[NACT * HID2 + n] = gb2;
     if (n < NACT) {
         float s = 0.f;
         for (int r = 0; r < rb; r++) s += dqs[r][n];
-        atomicAdd(&a.gb3[n], s);
+        pr[NACT * HID2 + HID2 + n] = s;
     }
 }
 
@@ -1421,9 +1418,9 @@ constexpr int QZ_CP = 128 + 8;  // the dZ1 tile's row pitch (bf16)
 static_assert(QZ_CP <= QZ_P, "each dZ1 plane overlays a dZ2 plane");
 template <bool X3>
 constexpr int qdz1_lds_bytes() { return (X3 ? 2 : 1) * RM * QZ_P * 2 + 2 * RM * 16; }  // + 2 tiles of [H1 > 0] bits
-// Row tiles per qdz1 workgroup: the tile's column sums (db1 and the centre column of dW1) leave by
-// one f32 atomic per column; with one 64-row tile per workgroup every such word took B / 64
-// same-address atomics, which the L2 serialises. Up to QZ_RT tiles per workgroup while the grid
+// Row tiles per qdz1 workgroup: the tiles' column sums (db1 and the centre column of dW1) leave
+// as one partial row pz1[bx] per workgroup row, which reduce2_kernel adds in bx order; fewer,
+// longer workgroups keep that reduction short. Up to QZ_RT tiles per workgroup while the grid
 // keeps >= 256 qdz1 workgroups (qdz1_tiles_per_wg; B = 32768: 8, 8192: 2, 4096: 1).
 constexpr int QZ_RT = 8;
 inline int qdz1_tiles_per_wg(int B) { return B / 4096 < 1 ? 1 : (B / 4096 > QZ_RT ? QZ_RT : B / 4096); }
@@ -1548,26 +1545,17 @@ __device__ __forceinline__ void qdz1_body(const Bwd& a, char* smem, int bx, int 
         __syncthreads();  // the dZ1 image has been read: the next tile's dZ2 may be stashed
     }
     cs += __shfl_xor(cs, 32, 64);  // the two row halves of the column
-    if (h == 0) {
-        atomicAdd(&a.gb1[col], cs);
-        atomicAdd(&a.gw1[(size_t)col * K1 + CENTRE_COL], cs);  // d/dW1 of the constant centre input
-    }
-}
-template <bool X3 = false>
-__global__ __launch_bounds__(256, 2) void qdz1_kernel(Bwd a) {
-    __shared__ __attribute__((aligned(16))) char smem[qdz1_lds_bytes<X3>()];
-    qdz1_body<X3>(a, smem, blockIdx.x, blockIdx.y, gridDim.x);
+    if (h == 0) a.pz1[(size_t)bx * HID + col] = cs;  // db1 = d/dW1 of the constant centre input
 }
 
 // C[m][n] += sum_k A[k][m] B[k][n] (both operands K-major bf16), 128x128 tiles of
 // 4 waves (2x2 of 64x64), K chunks of 64 staged in LDS in their memory order ([k][m]) and
 // read back by ds_read_b64_tr_b16, which hands every lane the 4 consecutive k of its column:
 // no transpose in registers (the 8x8 VALU shuffle this replaced cost about as many cycles
-// as the chunk's MFMAs). gridDim.z splits K. part == NULL: the partial tiles are added to C
-// with f32 atomics; else split z stores its tile to part[z][m][0, gridDim.x * TT) and
-// reduce2_kernel adds the splits in z order (deterministic, and no atomic traffic through
-// L2). Columns n >= Nc are skipped; remap: column n goes to ref_col(n) (fc1's compact K ->
-// the reference's 726).
+// as the chunk's MFMAs). gridDim.z splits K: split z stores its tile to part[z][m][0, gridDim.x
+// * TT) and reduce2_kernel adds the splits in z order into C (deterministic, and no atomic
+// traffic through L2), columns n >= Nc skipped, remap: column n goes to ref_col(n) (fc1's
+// compact K -> the reference's 726).
 // LDS image of a plane: [TKC][TPT] bf16, 320-B rows: a transposed read's 32-lane half takes
 // 4 rows x 64 B at banks 16 q + [0, 16) -- conflict-free (cdna_hip_programming.md T10)
 constexpr int TT = 128, TKC = 64, TPT = TT + 32;
@@ -1615,8 +1603,7 @@ __device__ __forceinline__ void gemm_tn_body(const GemmTN& g, char* smem, int bx
     auto img = reinterpret_cast<__bf16 (*)[TKC][TPT]>(smem);  // [NP][TKC][TPT]
     const __bf16* __restrict__ A = g.A;
     const __bf16* __restrict__ Bm = g.Bm;
-    const int lda = g.lda, ldb = g.ldb, K = g.K, M = g.M, Nc = g.Nc, kper = g.kper, ldc = g.ldc, remap = g.remap;
-    float* __restrict__ C = g.C;
+    const int lda = g.lda, ldb = g.ldb, K = g.K, M = g.M, kper = g.kper;
     float* __restrict__ part = g.part;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
     const int wm = w >> 1, wn = w & 1;
@@ -1686,34 +1673,17 @@ __device__ __forceinline__ void gemm_tn_body(const GemmTN& g, char* smem, int bx
         }
         __syncthreads();
     }
-    if (part) {
-        const int Np = g.gx * TT;
-        float* pz = part + (size_t)bz * M * Np;
-#pragma unroll
-        for (int j = 0; j < 2; j++) {
-            const int n = n0 + wn * 64 + j * 32 + (lane & 31);
-#pragma unroll
-            for (int i = 0; i < 2; i++)
-#pragma unroll
-                for (int r = 0; r < 16; r++) {
-                    const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    if (m < M) pz[(size_t)m * Np + n] = acc[i][j][r];
-                }
-        }
-        return;
-    }
+    const int Np = g.gx * TT;
+    float* pz = part + (size_t)bz * M * Np;
 #pragma unroll
     for (int j = 0; j < 2; j++) {
         const int n = n0 + wn * 64 + j * 32 + (lane & 31);
-        if (n >= Nc) continue;
-        const int nc = remap == 3 ? ref_col3(n) : remap ? ref_col(n) : n;
-        if (nc < 0) continue;
 #pragma unroll
         for (int i = 0; i < 2; i++)
 #pragma unroll
             for (int r = 0; r < 16; r++) {
                 const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (m < M) atomicAdd(&C[(size_t)m * ldc + nc], acc[i][j][r]);
+                if (m < M) pz[(size_t)m * Np + n] = acc[i][j][r];
             }
     }
 }
@@ -1785,7 +1755,15 @@ struct Red2 {
     float* ss;           // [gridDim.x] squared-norm partials, or NULL
     int nb2, nb1;        // workgroups of the two reductions
     int64_t gsP;         // grouped (blockIdx.y = net): floats between consecutive nets' partials
+    const float* p3;     // qbwd3's block partials [nb3][P3W]
+    int nb3;
+    const float* pz1;    // qdz1's column-sum partials [nz1][HID]
+    int nz1;
 };
+// the small sums (dW3, db2, db3 from p3; db1 and W1's centre column from pz1): 64 columns per
+// workgroup, the partial rows in four contiguous quarters (one per wave), quarters added in order
+constexpr int P3L = NACT * HID2 + HID2 + NACT;  // live columns of a p3 row
+constexpr int NRS3 = (P3L + 63) / 64, NRSZ = HID / 64, NRSMALL = NRS3 + NRSZ;
 __device__ __forceinline__ float red_sum256(float x, float* red) {
     red[threadIdx.x] = x;
     __syncthreads();
@@ -1805,6 +1783,8 @@ __global__ __launch_bounds__(256) void reduce2_kernel(Red2 r0) {
         r.gw1 += G * NPAR; r.gb1 += G * NPAR; r.gw2 += G * NPAR;
         r.gb2 += G * NPAR; r.gw3 += G * NPAR; r.gb3 += G * NPAR;
         r.ss = adv(r.ss, G * gridDim.x);
+        r.p3 += G * r.gsP;
+        r.pz1 += G * r.gsP;
     }
     const int b = (int)blockIdx.x;
     float sq = 0.f;
@@ -1853,14 +1833,38 @@ __global__ __launch_bounds__(256) void reduce2_kernel(Red2 r0) {
                 sq += o * o;
             }
         }
-    } else {  // the small gradients, complete before this launch
-        for (int i = (int)threadIdx.x; i < HID; i += 256) {
-            const float v = r.gb1[i], c = r.gw1[(size_t)i * K1 + CENTRE_COL];
-            sq += v * v + c * c;
+    } else {  // the small gradients from qbwd3's / qdz1's partial rows
+        const int sb = b - r.nb2 - r.nb1, c = (int)threadIdx.x & 63, qw = (int)threadIdx.x >> 6;
+        const bool z1 = sb >= NRS3;
+        const int col = (z1 ? sb - NRS3 : sb) * 64 + c;
+        const int nrow = z1 ? r.nz1 : r.nb3, pitch = z1 ? HID : P3W, ncol = z1 ? HID : P3L;
+        const float* src = (z1 ? r.pz1 : r.p3) + col;
+        float acc = 0.f;
+        if (col < ncol) {
+            const int r1 = (qw + 1) * nrow / 4;
+#pragma unroll 8
+            for (int i = qw * nrow / 4; i < r1; i++) acc += src[(size_t)i * pitch];
         }
-        for (int i = (int)threadIdx.x; i < HID2; i += 256) sq += r.gb2[i] * r.gb2[i];
-        for (int i = (int)threadIdx.x; i < NACT * HID2; i += 256) sq += r.gw3[i] * r.gw3[i];
-        if ((int)threadIdx.x < NACT) sq += r.gb3[threadIdx.x] * r.gb3[threadIdx.x];
+        red[threadIdx.x] = acc;
+        __syncthreads();
+        if (qw == 0 && col < ncol) {
+            const float tot = (red[c] + red[64 + c]) + (red[128 + c] + red[192 + c]);
+            if (z1) {
+                const float o = r.gb1[col] + tot;
+                float* cc = r.gw1 + (size_t)col * K1 + CENTRE_COL;  // d/dW1 of the constant centre input
+                const float oc = *cc + tot;
+                r.gb1[col] = o;
+                *cc = oc;
+                sq = o * o + oc * oc;
+            } else {
+                float* dst = col < NACT * HID2 ? r.gw3 + col : col < P3L - NACT ? r.gb2 + (col - NACT * HID2)
+                                                                                 : r.gb3 + (col - (P3L - NACT));
+                const float o = *dst + tot;
+                *dst = o;
+                sq = o * o;
+            }
+        }
+        __syncthreads();  // red is reused below
     }
     const float t = red_sum256(sq, red);
     if (threadIdx.x == 0 && r.ss) r.ss[b] = t;
@@ -2039,25 +2043,25 @@ int evx_qmlp_pack3(const float* w1, const float* b1, const float* w2, uint16_t* 
     return mlaunch("qmlp_pack3");
 }
 
-// the x3 act kernel for the dropout mode of a (fc1_slab_m); SAVE: the learner's online forward
-extern "C++" template <bool GR, bool SAVE = false>
+// the x3 act kernel for the dropout mode of a (fc1_slab_m)
+extern "C++" template <bool GR>
 static void launch_act3(const evxm::Fwd& a, int32_t n, int nets, hipStream_t st) {
     static bool attr = false;
     if (!attr) {
-        const void* kh[4] = {(const void*)evxm::qact3h_kernel<GR, 0, SAVE>, (const void*)evxm::qact3h_kernel<GR, 1, SAVE>,
-                             (const void*)evxm::qact3h_kernel<GR, 2, SAVE>, (const void*)evxm::qact3h_kernel<GR, 3, SAVE>};
+        const void* kh[4] = {(const void*)evxm::qact3h_kernel<GR, 0>, (const void*)evxm::qact3h_kernel<GR, 1>,
+                             (const void*)evxm::qact3h_kernel<GR, 2>, (const void*)evxm::qact3h_kernel<GR, 3>};
         for (const void* k : kh) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, evxm::ACT3H_LDS);
         attr = true;
     }
     const dim3 grid((unsigned)((n + 63) / 64), (unsigned)nets);
     if (a.drop_mask)
-        hipLaunchKernelGGL((evxm::qact3h_kernel<GR, 2, SAVE>), grid, dim3(256), evxm::ACT3H_LDS, st, a);
+        hipLaunchKernelGGL((evxm::qact3h_kernel<GR, 2>), grid, dim3(256), evxm::ACT3H_LDS, st, a);
     else if (a.drop_thresh && a.perm && a.rpe == 1)  // a row permutation: rows of different pairs share tiles
-        hipLaunchKernelGGL((evxm::qact3h_kernel<GR, 3, SAVE>), grid, dim3(256), evxm::ACT3H_LDS, st, a);
+        hipLaunchKernelGGL((evxm::qact3h_kernel<GR, 3>), grid, dim3(256), evxm::ACT3H_LDS, st, a);
     else if (a.drop_thresh)
-        hipLaunchKernelGGL((evxm::qact3h_kernel<GR, 1, SAVE>), grid, dim3(256), evxm::ACT3H_LDS, st, a);
+        hipLaunchKernelGGL((evxm::qact3h_kernel<GR, 1>), grid, dim3(256), evxm::ACT3H_LDS, st, a);
     else
-        hipLaunchKernelGGL((evxm::qact3h_kernel<GR, 0, SAVE>), grid, dim3(256), evxm::ACT3H_LDS, st, a);
+        hipLaunchKernelGGL((evxm::qact3h_kernel<GR, 0>), grid, dim3(256), evxm::ACT3H_LDS, st, a);
 }
 
 static int make_fwd(const evx_layout* lay, const evx_obs* obs, int32_t n, const evx_qmlp_params* p,
@@ -2158,18 +2162,10 @@ static int launch_fwd(const evxm::Fwd& a0, const evxm::Fwd& a1, int32_t n, int p
         return mlaunch("qfc23 grouped");
     }
     if (x3) {  // f32-accurate: 128 x 256 tiles for large batches (register budget), else 64 x 128
-        // tile experiments; the default for one problem (the learner's online forward beside the
-        // target through the fused act) is 64 x 256 (11: learn 391 -> 382 us at B = 32768,
-        // tools/gpu_fc1ab.sh), for two problems the choice below
-        static const int v = getenv("EVX_FC1X3") ? atoi(getenv("EVX_FC1X3")) : -1;
-        if (v == 11 || (v < 0 && pairs == 1 && fc23))  // 64 x 256 tiles at any batch
+        // one problem (the learner's online forward beside the target through the fused act):
+        // 64 x 256 tiles at any batch (learn 391 -> 382 us at B = 32768 vs 128 x 256)
+        if (pairs == 1 && fc23)
             hipLaunchKernelGGL((evxm::qfc1_kernel<2, 2, 4, true>), dim3(blocks, 2, pairs), dim3(256), 0, st, a0, a1, pairs);
-        else if (v == 13)  // 128 x 256 tiles of 8 waves at any batch
-            hipLaunchKernelGGL((evxm::qfc1_kernel<4, 1, 8, true>), dim3(big, 2, pairs), dim3(512), 0, st, a0, a1, pairs);
-        else if (v == 1 && big * pairs >= 384)
-            hipLaunchKernelGGL((evxm::qfc1_kernel<2, 2, 4, true>), dim3(blocks, 2, pairs), dim3(256), 0, st, a0, a1, pairs);
-        else if (v == 2 && big * pairs >= 384)
-            hipLaunchKernelGGL((evxm::qfc1_kernel<4, 2, 4, true>), dim3(big, 2, pairs), dim3(256), 0, st, a0, a1, pairs);
         else if (big * pairs >= 384)
             hipLaunchKernelGGL((evxm::qfc1_kernel<4, 1, 8, true>), dim3(big, 2, pairs), dim3(512), 0, st, a0, a1, pairs);
         else
@@ -2179,14 +2175,7 @@ static int launch_fwd(const evxm::Fwd& a0, const evxm::Fwd& a1, int32_t n, int p
         hipLaunchKernelGGL(evxm::qfc23_kernel<true>, dim3(blocks, 1, pairs), dim3(256), 0, st, a0, a1, pairs);
         return mlaunch("qfc23");
     }
-    static int nwv = -1;  // EVX_FC1_NWV=4: 128 x 256 tiles of 4 waves (tuning)
-    if (nwv < 0) {
-        const char* v = getenv("EVX_FC1_NWV");
-        nwv = v ? atoi(v) : 8;
-    }
-    if (big * pairs >= 384 && nwv == 4)
-        hipLaunchKernelGGL((evxm::qfc1_kernel<4, 2, 4>), dim3(big, 2, pairs), dim3(256), 0, st, a0, a1, pairs);
-    else if (big * pairs >= 384)  // enough 128-row tiles (all 512 columns each) to fill the chip
+    if (big * pairs >= 384)  // enough 128-row tiles (all 512 columns each) to fill the chip
         hipLaunchKernelGGL((evxm::qfc1_kernel<4, 2, 8>), dim3(big, 1, pairs), dim3(512), 0, st, a0, a1, pairs);
     else
         hipLaunchKernelGGL((evxm::qfc1_kernel<2, 1, 4>), dim3(blocks, 4, pairs), dim3(256), 0, st, a0, a1, pairs);
@@ -2275,36 +2264,23 @@ int evx_qmlp_forward2(const evx_layout* lay, int32_t n, const evx_obs* obs0, con
     if (!(out0->q || out0->actions || out0->h2) || !(out1->q || out1->actions || out1->h2))
         return mfail(-22, "qmlp_forward2: both problems need an fc2/fc3 output");
     if ((p0->x3 != 0) != (p1->x3 != 0)) return mfail(-22, "qmlp_forward2: both problems in one precision");
-    static const bool tgt_act = !getenv("EVX_TGT_ACT") || atoi(getenv("EVX_TGT_ACT")) != 0;
     // (at n >= 32768 only: a fused act workgroup lives ~65 us on the full path, so below a full
     // round of workgroups the two-kernel forward wins -- B = 4096: learn 187 vs 127 us)
-    static const int tgt_min = getenv("EVX_TGT_ACT_MIN") ? atoi(getenv("EVX_TGT_ACT_MIN")) : 32768;
-    if (tgt_act && p0->x3 && out1->q && !out1->h2 && !out1->actions && !out1->x && n >= tgt_min) {
+    if (p0->x3 && out1->q && !out1->h2 && !out1->actions && !out1->x && n >= 32768) {
         // x3 learner: the second problem (the target net: Q only) through the fused act kernel
         // (H1 / H2 stay in LDS, 64-row tiles, two workgroups per CU) instead of qfc1 + qfc23
         // writing and re-reading both H1 planes; the first problem alone through qfc1 + qfc23
         // the target net's own act table (static features x W1, rebuilt at each target sync --
         // evacx.trainer attaches it to both nets): replay rows past the fire's last step (every
         // row once the fire has stopped spreading: fire_step persists across resets) start fc1
-        // from it, the others run the full path per 64-row tile. EVX_TGT_TABLE=0: never.
-        static const bool tgt_table = !getenv("EVX_TGT_TABLE") || atoi(getenv("EVX_TGT_TABLE")) != 0;
-        if (!tgt_table) a1.stat = nullptr;
+        // from it, the others run the full path per 64-row tile.
         a1.perm = nullptr;
         a1.actions = nullptr;
         a1.h1 = a1.h1l = nullptr;
-        // the online forward too through the fused kernel when it saves everything the backward
-        // reads (X, both H1 planes, H2, Q): EVX_ONLINE_ACT=1 (measured no faster than qfc1 + qfc23
-        // at B = 32768: learn 0.420 vs 0.427 ms, tools/gpu_onact.sh)
-        static const bool on_act = getenv("EVX_ONLINE_ACT") && atoi(getenv("EVX_ONLINE_ACT")) != 0;
-        if (on_act && a0.x && a0.h1 && a0.h1l && a0.h2 && a0.q && !a0.actions && !a0.perm && !a0.raw) {
-            a0.stat = nullptr;
-            launch_act3<false, true>(a0, n, 1, (hipStream_t)stream);
-            int rc3 = mlaunch("qmlp_forward2 online act");
-            if (rc3) return rc3;
-        } else {
-            int rc2 = launch_fwd(a0, a0, n, 1, true, (hipStream_t)stream, true);
-            if (rc2) return rc2;
-        }
+        // (the online forward through the fused kernel with X / H1 / H2 saves measured no faster
+        // than qfc1 + qfc23 at B = 32768: learn 0.420 vs 0.427 ms; removed)
+        int rc2 = launch_fwd(a0, a0, n, 1, true, (hipStream_t)stream, true);
+        if (rc2) return rc2;
         launch_act3<false>(a1, n, 1, (hipStream_t)stream);
         return mlaunch("qmlp_forward2 target act");
     }
@@ -2316,8 +2292,6 @@ int evx_qmlp_forward2(const evx_layout* lay, int32_t n, const evx_obs* obs0, con
 // the 256 dZ1 workgroups: 256). dW1 (x3: 20 tiles) at B = 32768 -> 24 splits, 480 workgroups,
 // 60 per XCD.
 static int ksplit_kper(int B, int tiles, int slots, int minrows) {
-    static const int env = getenv("EVX_KSPLIT_WG") ? atoi(getenv("EVX_KSPLIT_WG")) : 0;  // experiments
-    if (env > 0 && slots == 512) slots = env;
     // ... and no more than one split per `minrows` rows (dW1: 1024 -- below that its partials'
     // reduction outweighs the parallelism, B = 8192: learn 171 -> 154 us; dW2, whose launch the
     // dZ1 tiles share: 256)
@@ -2327,25 +2301,39 @@ static int ksplit_kper(int B, int tiles, int slots, int minrows) {
 }
 static int dw2_kper(int B) { return ksplit_kper(B, 8, 256, 256); }
 static int dw1_kper(int B, bool x3) { return ksplit_kper(B, x3 ? 20 : 16, 512, 1024); }
+static int qbwd3_blocks(int B) { return (B + evxm::qbwd3_rows(B) - 1) / evxm::qbwd3_rows(B); }
+static int qdz1_wgx(int B) {
+    const int qrt = evxm::qdz1_tiles_per_wg(B);
+    return (B + evxm::RM * qrt - 1) / (evxm::RM * qrt);
+}
 
-// split-K partials: dW2's region, then dW1's (both stay live until reduce2_kernel)
+// the backward's partials, in this order (all live until reduce2_kernel): dW2's split-K tiles,
+// dW1's, qbwd3's block rows [nb3][P3W], qdz1's column sums [ndzx][HID]
 static int64_t part2_floats(int32_t B) {
     const int64_t s2 = (B + dw2_kper(B) - 1) / dw2_kper(B);
     return s2 * evxm::HID2 * evxm::HID;
 }
-int64_t evx_qmlp_backward_part_floats(int32_t B) {
-    if (B <= 0) return 0;
+static int64_t part_p3_off(int32_t B) {
     const int64_t s1 = std::max((B + dw1_kper(B, false) - 1) / dw1_kper(B, false),
                                 (B + dw1_kper(B, true) - 1) / dw1_kper(B, true));  // bf16 / x3 dW1 splits
     return part2_floats(B) + s1 * evxm::HID * evxm::K1X;  // K1X: the x3 dW1 width
 }
+static int64_t part_pz1_off(int32_t B) { return part_p3_off(B) + (int64_t)qbwd3_blocks(B) * evxm::P3W; }
+int64_t evx_qmlp_backward_part_floats(int32_t B) {
+    if (B <= 0) return 0;
+    return part_pz1_off(B) + (int64_t)qdz1_wgx(B) * evxm::HID;
+}
 
 // workgroups of reduce2_kernel = squared-norm partials the backward leaves for evx_qmlp_adam_pack3
-static int norm_parts() { return (evxm::HID2 * evxm::HID / 4 + 255) / 256 + (evxm::HID * evxm::NCELL + 255) / 256 + 1; }
+static int norm_parts() {
+    return (evxm::HID2 * evxm::HID / 4 + 255) / 256 + (evxm::HID * evxm::NCELL + 255) / 256 + evxm::NRSMALL;
+}
 int32_t evx_qmlp_norm_parts(void) { return norm_parts(); }
 int64_t evx_qmlp_nparams(void) { return evxm::NPAR; }
 
 extern "C++" {
+// dZ1 + dW2 (bwd_mid), dW1 (gemm_tn), then every reduction + the squared-norm partials
+// (reduce2): all sums in a fixed order
 template <bool X3, int AP2, int BP2, int AP1, int BP1>
 static void launch_tail(const evxm::Bwd& a, int32_t B, const evx_qmlp_grads* g, float* ss, hipStream_t st,
                         int nets = 1) {
@@ -2355,13 +2343,18 @@ static void launch_tail(const evxm::Bwd& a, int32_t B, const evx_qmlp_grads* g, 
     g2.gz = (B + g2.kper - 1) / g2.kper;
     const int KX = X3 ? evxm::K1X : evxm::K1P;
     evxm::GemmTN g1{a.dz1, evxm::HID, a.x, KX, B, evxm::HID, X3 ? evxm::K1X : 4 * evxm::NCELL,
-                    dw1_kper(B, X3), g->w1, evxm::K1, X3 ? 3 : 1, g->part ? g->part + part2_floats(B) : nullptr,
+                    dw1_kper(B, X3), g->w1, evxm::K1, X3 ? 3 : 1, g->part + part2_floats(B),
                     X3 ? a.dz1l : nullptr, nullptr, KX / evxm::TT, evxm::HID / evxm::TT, 0};
     g1.gz = (B + g1.kper - 1) / g1.kper;
-    const int qrt = evxm::qdz1_tiles_per_wg(B);
-    const int ndzx = (B + evxm::RM * qrt - 1) / (evxm::RM * qrt);
-    if (nets > 1) {  // grouped (x3, partials): net g's operands, gradients and partials (fwd_net / bwd_net)
-        const int64_t pf = evx_qmlp_backward_part_floats(B);
+    const int ndzx = qdz1_wgx(B);
+    const int64_t pf = evx_qmlp_backward_part_floats(B);
+    evxm::Red2 r{g->part, g2.gz, g1.part, g1.gz, g1.gx * evxm::TT, 4 * evxm::NCELL, X3 ? 3 : 1,
+                 g->w1, g->b1, g->w2, g->b2, g->w3, g->b3, ss,
+                 (evxm::HID2 * evxm::HID / 4 + 255) / 256, (evxm::HID * evxm::NCELL + 255) / 256, 0,
+                 a.p3, qbwd3_blocks(B), a.pz1, ndzx};
+    constexpr int lds = std::max(evxm::qdz1_lds_bytes<X3>(), evxm::gemm_tn_lds_bytes<AP2, BP2>());
+    const unsigned nmid = (unsigned)(ndzx * (evxm::HID / 128) + g2.gx * g2.gy * g2.gz);
+    if (nets > 1) {  // grouped (x3): net g's operands, gradients and partials (fwd_net / bwd_net)
         g2.gsA = 2 * (int64_t)B * evxm::HID2;
         g2.gsB = 2 * (int64_t)B * evxm::HID;
         g2.gsC = evxm::NPAR;
@@ -2370,53 +2363,29 @@ static void launch_tail(const evxm::Bwd& a, int32_t B, const evx_qmlp_grads* g, 
         g1.gsB = (int64_t)B * evxm::K1X;
         g1.gsC = evxm::NPAR;
         g1.gsP = pf;
-        constexpr int lds = std::max(evxm::qdz1_lds_bytes<X3>(), evxm::gemm_tn_lds_bytes<AP2, BP2>());
+        r.gsP = pf;
         static bool attr_g = false;
         if (!attr_g) {
             (void)hipFuncSetAttribute((const void*)evxm::bwd_mid_kernel<X3, AP2, BP2, true>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
             attr_g = true;
         }
-        const unsigned nmid = (unsigned)(ndzx * (evxm::HID / 128) + g2.gx * g2.gy * g2.gz);
         hipLaunchKernelGGL((evxm::bwd_mid_kernel<X3, AP2, BP2, true>), dim3(nmid, nets), dim3(256), lds, st, a, ndzx, g2);
         hipLaunchKernelGGL((evxm::gemm_tn_kernel<AP1, BP1, true>), dim3(g1.gx, g1.gy, g1.gz * nets), dim3(256), 0, st, g1);
-        evxm::Red2 r{g->part, g2.gz, g1.part, g1.gz, g1.gx * evxm::TT, 4 * evxm::NCELL, X3 ? 3 : 1,
-                     g->w1, g->b1, g->w2, g->b2, g->w3, g->b3, ss,
-                     (evxm::HID2 * evxm::HID / 4 + 255) / 256, (evxm::HID * evxm::NCELL + 255) / 256, pf};
         hipLaunchKernelGGL(evxm::reduce2_kernel, dim3((unsigned)norm_parts(), nets), dim3(256), 0, st, r);
         return;
     }
-    if (g->part) {
-        // qdz1 and the dW2 tiles in one launch (both read only qbwd3's outputs), then the dW1
-        // tiles, then both reductions + the squared-norm partials in one launch
-        constexpr int lds = std::max(evxm::qdz1_lds_bytes<X3>(), evxm::gemm_tn_lds_bytes<AP2, BP2>());
-        static bool attr = false;
-        if (!attr) {
-            (void)hipFuncSetAttribute((const void*)evxm::bwd_mid_kernel<X3, AP2, BP2>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-            attr = true;
-        }
-        static const bool split_mid = getenv("EVX_SPLIT_MID") != nullptr;  // diagnostic: qdz1 and dW2 timed apart
-        if (split_mid) {
-            hipLaunchKernelGGL((evxm::bwd_mid_kernel<X3, AP2, BP2>), dim3((unsigned)(ndzx * (evxm::HID / 128))), dim3(256),
-                               lds, st, a, ndzx, g2);
-            hipLaunchKernelGGL((evxm::gemm_tn_kernel<AP2, BP2>), dim3(g2.gx * g2.gy * g2.gz), dim3(256), 0, st, g2);
-        } else {
-            const unsigned nmid = (unsigned)(ndzx * (evxm::HID / 128) + g2.gx * g2.gy * g2.gz);
-            hipLaunchKernelGGL((evxm::bwd_mid_kernel<X3, AP2, BP2>), dim3(nmid), dim3(256), lds, st, a, ndzx, g2);
-        }
-        hipLaunchKernelGGL((evxm::gemm_tn_kernel<AP1, BP1>), dim3(g1.gx * g1.gy * g1.gz), dim3(256), 0, st, g1);
-        evxm::Red2 r{g->part, g2.gz, g1.part, g1.gz, g1.gx * evxm::TT, 4 * evxm::NCELL, X3 ? 3 : 1,
-                     g->w1, g->b1, g->w2, g->b2, g->w3, g->b3, ss,
-                     (evxm::HID2 * evxm::HID / 4 + 255) / 256, (evxm::HID * evxm::NCELL + 255) / 256};
-        hipLaunchKernelGGL(evxm::reduce2_kernel, dim3((unsigned)norm_parts()), dim3(256), 0, st, r);
-        return;
+    // qdz1 and the dW2 tiles in one launch (both read only qbwd3's outputs), then the dW1
+    // tiles, then every reduction + the squared-norm partials in one launch
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)evxm::bwd_mid_kernel<X3, AP2, BP2>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        attr = true;
     }
-    // f32 atomics into the gradients (no partials)
-    hipLaunchKernelGGL(evxm::qdz1_kernel<X3>, dim3((unsigned)ndzx, evxm::HID / 128), dim3(256), 0, st, a);
-    hipLaunchKernelGGL((evxm::gemm_tn_kernel<AP2, BP2>), dim3(g2.gx * g2.gy * g2.gz), dim3(256), 0, st, g2);
+    hipLaunchKernelGGL((evxm::bwd_mid_kernel<X3, AP2, BP2>), dim3(nmid), dim3(256), lds, st, a, ndzx, g2);
     hipLaunchKernelGGL((evxm::gemm_tn_kernel<AP1, BP1>), dim3(g1.gx * g1.gy * g1.gz), dim3(256), 0, st, g1);
-    if (ss) hipLaunchKernelGGL(evxm::sumsq_parts_kernel, dim3((unsigned)norm_parts()), dim3(256), 0, st, g->w1, ss);
+    hipLaunchKernelGGL(evxm::reduce2_kernel, dim3((unsigned)norm_parts()), dim3(256), 0, st, r);
 }
 }  // extern "C++"
 
@@ -2429,6 +2398,7 @@ static int qmlp_backward(const evx_qmlp_params* p, int32_t B, const float* dq, c
     if (ss && (g->b1 != g->w1 + evxm::OB1 || g->w2 != g->w1 + evxm::OW2 || g->b2 != g->w1 + evxm::OB2 ||
                g->w3 != g->w1 + evxm::OW3 || g->b3 != g->w1 + evxm::OB3))
         return mfail(-22, "qmlp_backward: norm partials need the gradients as one flat state_dict-order buffer");
+    if (!g->part) return mfail(-22, "qmlp_backward: g->part required (evx_qmlp_backward_part_floats(B) floats)");
     if (B <= 0) return 0;
     hipStream_t st = (hipStream_t)stream;
     const int rb3 = evxm::qbwd3_rows(B);
@@ -2458,6 +2428,9 @@ static int qmlp_backward(const evx_qmlp_params* p, int32_t B, const float* dq, c
     a.h1l = nullptr;
     a.w2tl = nullptr;
     a.dz2l = a.dz1l = nullptr;
+    a.p3 = g->part + part_p3_off(B);
+    a.pz1 = g->part + part_pz1_off(B);
+    a.gsP = evx_qmlp_backward_part_floats(B);
     if (p->x3) {
         if (!p->w2tl) return mfail(-22, "qmlp_backward: x3 needs w2tl (evx_qmlp_pack3)");
         a.h1l = a.h1 + (size_t)B * evxm::HID;  // lo planes after the hi planes

@@ -561,8 +561,7 @@ __global__ __launch_bounds__(256) void td_loss_kernel(const float* __restrict__ 
                                                       float gamma, int B, const float* __restrict__ w,
                                                       float* __restrict__ dQ, float* __restrict__ loss_out,
                                                       float* __restrict__ td_abs, int ntd = 0,
-                                                      float* __restrict__ zero = nullptr, int64_t nzero = 0,
-                                                      int Bnorm = 0, int loss_acc = 0) {
+                                                      float* __restrict__ zero = nullptr, int64_t nzero = 0) {
     __shared__ float red[256];
     __shared__ bool last;
     if (zero && (int)blockIdx.x >= ntd) {  // the extra workgroups clear the gradient buffer for the backward
@@ -586,8 +585,7 @@ __global__ __launch_bounds__(256) void td_loss_kernel(const float* __restrict__ 
         if (td_abs) td_abs += o;
         loss_out += gy;
     }
-    // Bnorm > 0: the rows are one part of a batch of Bnorm (the loss is a mean over Bnorm)
-    const float nrm = (float)(Bnorm > 0 ? Bnorm : B);
+    const float nrm = (float)B;
     const int i = blockIdx.x * 256 + threadIdx.x;
     float part = 0.f;
     if (i < B) {
@@ -629,7 +627,7 @@ __global__ __launch_bounds__(256) void td_loss_kernel(const float* __restrict__ 
         }
         if (threadIdx.x == 0) {
             const float l = red[0] / nrm;
-            loss_out[0] = loss_acc ? loss_out[0] + l : l;  // loss_acc: the batch's earlier parts are in
+            loss_out[0] = l;
             g_td_ticket[gy] = 0;
         }
     }
@@ -1038,21 +1036,6 @@ int evx_td_loss_zero(const float* Q, const float* Qt, int32_t A, const int32_t* 
     hipLaunchKernelGGL(evxq::td_loss_kernel, dim3(ntd + nz), dim3(256), 0, (hipStream_t)stream, Q, Qt, A, act, rew, done,
                        gamma, B, w, dQ, loss, td_abs, ntd, zero, nzero);
     return qlaunch("td_loss_zero");
-}
-
-int evx_td_loss_part(const float* Q, const float* Qt, int32_t A, const int32_t* act, const float* rew,
-                     const uint8_t* done, float gamma, int32_t B, int32_t B_norm, int32_t accumulate, float* dQ,
-                     float* loss, float* zero, int64_t nzero, void* stream) {
-    if (B <= 0) return 0;
-    if (B > 4096 * 256) return qfail(-22, "td_loss_part: batch too large");
-    if (B_norm < B) return qfail(-22, "td_loss_part: B_norm must be >= B (the rows are part of a B_norm batch)");
-    if (accumulate && zero) return qfail(-22, "td_loss_part: only a batch's first part clears the gradients");
-    const int ntd = (B + 255) / 256;
-    const int nz = zero && nzero > 0 ? (int)std::min<int64_t>((nzero + 256 * 16 - 1) / (256 * 16), 512) : 0;
-    hipLaunchKernelGGL(evxq::td_loss_kernel, dim3(ntd + nz), dim3(256), 0, (hipStream_t)stream, Q, Qt, A, act, rew,
-                       done, gamma, B, (const float*)nullptr, dQ, loss, (float*)nullptr, ntd, nz ? zero : nullptr,
-                       nzero, B_norm, accumulate ? 1 : 0);
-    return qlaunch("td_loss_part");
 }
 
 int evx_td_loss_zero_g(const float* Q, const float* Qt, int32_t A, const int32_t* act, const float* rew,

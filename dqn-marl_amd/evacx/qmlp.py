@@ -11,7 +11,6 @@ operands, f32 accumulation).
 from __future__ import annotations
 
 import ctypes as C
-import os
 
 import numpy as np
 import torch
@@ -53,7 +52,6 @@ class evx_qmlp_fwd_out(C.Structure):
 
 
 _inited = False
-_BWD_ATOMIC = os.environ.get("EVX_BWD_ATOMIC", "0") == "1"  # weight-gradient split-K by f32 atomics (A/B)
 
 
 def mlib():
@@ -325,11 +323,11 @@ class MLPFast:
                 raise ValueError(f"qmlp backward: {name} has {t.numel()} elements, needs {n}")
         g = evx_qmlp_grads(**{k: grads[f"fc{k[1]}.{'weight' if k[0] == 'w' else 'bias'}"].data_ptr()
                               for k in ["w1", "b1", "w2", "b2", "w3", "b3"]})
-        if not _BWD_ATOMIC:  # split-K partials summed in a fixed order (deterministic, no f32 atomics)
-            nf = int(mlib().evx_qmlp_backward_part_floats(B))
-            if self._part is None or self._part.numel() < nf:
-                self._part = torch.empty(nf, dtype=torch.float32, device=self.device)
-            g.part = self._part.data_ptr()
+        # every gradient sum through partials added in a fixed order (the same bits on every run)
+        nf = int(mlib().evx_qmlp_backward_part_floats(B))
+        if self._part is None or self._part.numel() < nf:
+            self._part = torch.empty(nf, dtype=torch.float32, device=self.device)
+        g.part = self._part.data_ptr()
         if ss is not None:
             _need("backward ss", ss, 1, int(mlib().evx_qmlp_norm_parts()))
             mcheck(mlib().evx_qmlp_backward_ss(C.byref(self.c), B, dq.data_ptr(), x.data_ptr(), h1.data_ptr(),

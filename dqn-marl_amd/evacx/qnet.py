@@ -66,9 +66,6 @@ def qlib():
         L.evx_td_loss_zero.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
                                        C.c_float, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                        C.c_void_p, C.c_int64, C.c_void_p]
-        L.evx_td_loss_part.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
-                                       C.c_float, C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
-                                       C.c_int64, C.c_void_p]
         L.evx_td_loss_zero_g.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
                                          C.c_float, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
                                          C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]
@@ -462,38 +459,21 @@ class Learner:
         return self.loss
 
     def learn_obs(self, lay_c, s_obs, a, r, done, s2_obs, B, update: bool = True, weights=None, td_abs=None,
-                  mask_online=None, mask_target=None, drop_row0: int = 0, part=None):
+                  mask_online=None, mask_target=None, drop_row0: int = 0):
         """DQNAgent.learn on compact observations with the fused kernels (x3 = f32-accurate,
         or bf16): online forward (saves X, H1, H2), target forward, TD loss, backward,
         clip+Adam. update=False stops after the gradients (the caller runs step_optimizer
         later). mask_online / mask_target: explicit uint8 [B][512] dropout keep masks (tests:
-        the reference's captured torch masks) in place of the hash.
-        part = (B_norm, first, last): the B rows are one part of a batch of B_norm rows learnt
-        in parts (evacx.trainer's split learn step): loss and dQ are means over B_norm, the first
-        part clears the gradients and writes the loss, later parts add theirs (the backward
-        accumulates into the gradient buffer); only the last part leaves the clip norm's
-        partials, runs the gradient hook and (update) the optimizer step. Buffers are sized for
-        B_norm rows, so parts of any size reuse them."""
+        the reference's captured torch masks) in place of the hash."""
         from .qmlp import HID, HID2
         for name, t in (("s_obs", s_obs), ("s2_obs", s2_obs)):  # evx_obs rows are 8 words
             if t.numel() < B * 8:
                 raise ValueError(f"learn_obs: {name} holds {t.numel() // 8} observations, B = {B}")
-        if part is not None:
-            B_norm, first, last = int(part[0]), bool(part[1]), bool(part[2])
-            if not self.fused_opt:
-                raise ValueError("learn_obs: a batch in parts needs the fused x3 MLP path")
-            if not 0 < B <= B_norm:
-                raise ValueError(f"learn_obs: a part of {B} rows of a {B_norm}-row batch")
-            if weights is not None or td_abs is not None:
-                raise ValueError("learn_obs: importance weights / |TD| are not split into parts")
-        else:
-            B_norm, first, last = B, True, True
         ws, dev = self.net.ws, self.device
         pl, kx = self.fast.planes, self.fast.kx
-        cap = B_norm
 
         def buf(name, per_row, dt):
-            return ws.get(name, (cap * per_row,), dt, dev)[:B * per_row]
+            return ws.get(name, (B * per_row,), dt, dev)
         X = buf("fx", kx, torch.int16)
         H1 = buf("fh1", pl * HID, torch.int16)
         H2 = buf("fh2", HID2, torch.float32).view(B, HID2)
@@ -510,17 +490,7 @@ class Learner:
         type(self.fast).forward_pair(lay_c, B, self.fast, s_obs, d_on, dict(h1=H1, x=X, h2=H2, q=Q), self.fast_t,
                                      s2_obs, d_tg, dict(h1=H1t, q=Qt))
         L = qlib()
-        if part is not None:
-            g = self.grads.flat
-            qcheck(L.evx_td_loss_part(_p(Q), _p(Qt), self.actions, _p(a), _p(r), _p(done), self.gamma, B, B_norm,
-                                      int(not first), _p(dQ), _p(self.loss), _p(g) if first else None,
-                                      g.numel() if first else 0, _stream()), "td_loss_part")
-            ss = self._ss if (last and self.grad_hook is None) else None
-            self.fast.backward(B, dQ, X, H1, H2, DROPOUT_P, dz2, dz1, self.grads, zero=False, ss=ss)
-            self._ss_fresh = ss is not None
-            if not last:
-                return self.loss
-        elif self.fused_opt:
+        if self.fused_opt:
             # the TD launch also clears the gradients; the backward leaves the norm partials
             # (its weight-gradient reductions compute them) unless an all-reduce will change the gradients
             g = self.grads.flat

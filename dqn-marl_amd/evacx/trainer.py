@@ -20,7 +20,6 @@ reward) generalised to R robots and E envs; DQNAgent.act/remember/learn
 from __future__ import annotations
 
 import ctypes as C
-import os
 from typing import List, Optional
 
 import numpy as np
@@ -94,13 +93,6 @@ class Replay:
                                    out["done"].data_ptr(), None, _stream()), "replay_sample")
 
 
-# The dispatch order of the lagged schedule runs on the env's own stream right before
-# env.step: its ~13 us kernel on the critical path beats the side stream's event pair
-# (tools/gpu_ab_env.sh EVX_ORDER_INLINE: 9.48 vs 9.03 M env-steps/s). The strict schedule
-# keeps the side stream (its act + learn hide the order). EVX_ORDER_INLINE=0/1 forces.
-_ORDER_INLINE_ENV = os.environ.get("EVX_ORDER_INLINE")
-
-
 class _Group:
     """One part of the envs with its own stream chain (act -> env.step -> push): with
     several groups, one group's env.step launch tail (its heaviest envs, few waves)
@@ -112,9 +104,9 @@ class _Group:
         self.actions = actions  # this group's rows of the trainer's action buffer
         # act, env.step, push on a high-priority stream: the learn stream's workgroups
         # then fill the env launch's tail instead of competing for its first slots
-        self.main = torch.cuda.Stream(device=device, priority=int(os.environ.get("EVX_MAIN_PRIO", "-1")))
-        # dispatch order (and extra resets); EVX_SIDE_PRIO=-1: high priority (A/B)
-        self.side = torch.cuda.Stream(device=device, priority=int(os.environ.get("EVX_SIDE_PRIO", "0")))
+        self.main = torch.cuda.Stream(device=device, priority=-1)
+        # dispatch order (and extra resets)
+        self.side = torch.cuda.Stream(device=device, priority=0)
         cur = torch.cuda.current_stream(device)
         self.ev_push = torch.cuda.Event()
         self.ev_push.record(cur)
@@ -131,7 +123,7 @@ class VecTrainer:
                  grad_hook=None, learn_every: int = 1, lagged_learn: bool = False, replay: str = "uniform",
                  prio_alpha: float = 0.6, prio_beta0: float = 0.4, prio_beta_steps: int = 100000,
                  prio_eps: float = 1e-6, groups: int = 1, layout_of=None, world_envs: Optional[int] = None,
-                 nets: str = "shared"):
+                 nets: str = "shared", act_row_order: bool = False):
         """groups: the envs are split into this many parts, each stepping on its own
         stream chain (see _Group); the env results do not depend on it (every env is
         still stepped once per step with its own streams), the act's dropout masks do.
@@ -145,7 +137,9 @@ class VecTrainer:
         its own network, memory and optimizer, as runners/train_double_dqn.py:35-56 gives each
         robot its own DQNAgent: evacx.qgroup.GroupedLearner, batch / R transitions per net per
         learn step, strict schedule, one GPU) or "qmix" (per-robot nets under a QMIX mixer,
-        runners/train_qmix.py: batch / R joint env-steps per learn step, evacx.qgroup.GroupedQMix)."""
+        runners/train_qmix.py: batch / R joint env-steps per learn step, evacx.qgroup.GroupedQMix).
+        act_row_order: the x3 act visits its rows sorted by (table path, window centre)
+        (evx_act_row_perm) instead of its envs by table path (VecEnv.act_perm); same results."""
         self.lay, self.E, self.R = layout, E, layout.R
         self.device = layout.device
         # the push reads env.obs_prev: no copy per step
@@ -169,11 +163,13 @@ class VecTrainer:
             # qmix: the R robots of an env are the agents of runners/train_qmix.py -- joint samples
             # (the same env-steps for every agent), the mixer's loss over the team reward
             self.qmix = GroupedQMix(self.glearner, seed=learner_seed) if nets == "qmix" else None
-        # conv + f32: the im2col GEMMs in the f32-accurate x3 mode (bf16 hi/lo operand pairs, as
-        # the fused MLP's f32); EVX_CONV_EXACT=1 keeps the exact-f32 MFMA (the golden-test path)
+        # conv + f32: the implicit-GEMM convolutions in the f32-accurate x3 mode (bf16 hi/lo operand
+        # pairs, as the fused MLP's f32); precision="exact" keeps the exact-f32 MFMA (the golden-test path)
         lprec = precision
-        if kind == "conv" and precision == "f32" and os.environ.get("EVX_CONV_EXACT", "0") != "1":
+        if kind == "conv" and precision == "f32":
             lprec = "x3"
+        elif precision == "exact":
+            lprec = "f32"
         self.learner = Learner(kind=kind, device=self.device, lr=lr, gamma=gamma, precision=lprec,
                                seed=learner_seed) if not self.per_robot else None
         # the arithmetic the Q-network actually runs: "x3" (f32 operands as bf16 hi + lo pairs on the
@@ -233,49 +229,32 @@ class VecTrainer:
         self.ev_reset.record(cur)
         self.reset_pending = False
         self.join_caller = True  # the first step waits for the caller's stream (set-up work)
-        self.lstream = torch.cuda.Stream(device=self.device, priority=int(os.environ.get("EVX_LEARN_PRIO", "0")))
+        self.lstream = torch.cuda.Stream(device=self.device, priority=0)
         self.ev_learned = torch.cuda.Event()
         self.ev_learned.record(cur)
         self.last_loss: Optional[torch.Tensor] = None
         # bf16 MLP: act and learn straight from compact observations (csrc/qmlp.hip)
         self.fast = self.learner.fast if self.learner is not None else None
         if self.fast is None:
-            self.lagged = False  # the split learn step needs the fused bf16 MLP path
-        # split learn step (the strict schedule's default on the fused x3 MLP with uniform replay):
-        # learn t's batch is drawn from the ring after push t as random.sample draws it -- a uniform
-        # B-subset -- but in two parts: K ~ Hypergeometric(F = E*R pushed slots, the rest, B) rows
-        # from push t's slots and B - K from the slots already there before it (a uniform B-subset
-        # of the union, exactly). The old part's forward + backward runs on the learn stream beside
-        # act t and env.step t (it reads only the weights after learn t-1 and the ring before push
-        # t); the K fresh rows, clip and Adam run after push t. Same batch distribution, weights
-        # and loss as the one-part learn up to f32 summation order. Off by default (EVX_SPLIT_LEARN=1
-        # turns it on): measured slower at cfg3 (tools/gpu_ab_split.sh: 17.36 vs 17.59 M env-steps/s)
-        # -- act and env.step fill every CU's LDS and VGPRs, so the old part mostly runs after the
-        # push anyway while slowing env.step by 4 %.
-        self.split = (not self.per_robot and self.fast is not None and self.learner.fused_opt and not self.prio
-                      and os.environ.get("EVX_SPLIT_LEARN", "0") == "1")
-        self._hg = np.random.Generator(np.random.PCG64([self.seed & 0xFFFFFFFF, 0x5EED5]))
-        self.last_split = None  # (old rows, fresh rows) of the last split learn step
+            self.lagged = False  # the lagged schedule's two-phase learn needs the fused MLP path
         self._perm = None
         self._rowperm = None
-        if self.fast is not None and layout_of is None and len(self.groups) == 1 and \
-                os.environ.get("EVX_ACT_STATIC", "1" if self.fast.x3 else "0") == "1":
+        if self.fast is not None and self.fast.x3 and layout_of is None and len(self.groups) == 1:
             # act fast path: envs past the fire's last step start fc1 from a per-centre table of the
             # static features' contribution (rebuilt with every weight update) and add only the
             # occupancy columns; the act visits those envs first (VecEnv.act_perm) so its row tiles
-            # are uniform. x3: on by default (the table replaces ~3/4 of fc1's products); bf16: off
-            # by default (the rebuild costs what the act saves, tools/gpu_ab_static.sh)
+            # are uniform. x3 only (the table replaces ~3/4 of fc1's products); bf16: off (the
+            # rebuild costs what the act saves, tools/gpu_ab_static.sh)
             lc = self.lay.c  # centres only where robots can be (Map.robot_range): 55 of 130 columns at cfg3
             xr = (max(lc.rx_lo, 0), min(lc.rx_hi, lc.L + 1))
             self.fast.attach_static(lc, lc.L, lc.W, lc.t_max, x_range=xr)
-            if self.fast.x3 and os.environ.get("EVX_TGT_TABLE", "1") == "1":
-                # the target net's table too (rebuilt at each target sync): the learner's target
-                # forward (the fused act kernel at B >= 32768) starts fc1 from it for replay rows
-                # past the fire's last step
-                self.learner.fast_t.attach_static(lc, lc.L, lc.W, lc.t_max, x_range=xr)
+            # the target net's table too (rebuilt at each target sync): the learner's target
+            # forward (the fused act kernel at B >= 32768) starts fc1 from it for replay rows
+            # past the fire's last step
+            self.learner.fast_t.attach_static(lc, lc.L, lc.W, lc.t_max, x_range=xr)
             self._perm = torch.zeros(E, dtype=torch.int32, device=self.device)
             self._rowperm = None
-            if self.fast.x3 and os.environ.get("EVX_ACT_ROWPERM", "0") == "1":
+            if act_row_order:
                 # the act's rows sorted by (table path, window centre) instead of its envs by table path
                 # (evx_act_row_perm): rows sharing a table row share tiles, which then read a few table
                 # rows from L2 instead of 64 scattered ones; every row keeps its own results and mask
@@ -386,7 +365,7 @@ class VecTrainer:
                                               self.samp["done"], self.samp["s2"], self.batch, update=phase == "all",
                                               weights=w, td_abs=td)
             else:
-                assert phase == "all", "split learn needs the fused bf16 MLP path"
+                assert phase == "all", "a two-phase learn needs the fused MLP path"
                 s = self.env.expand_obs(torch.float32, self.samp["s"]).view(self.batch, 11, 11, 6)
                 s2 = self.env.expand_obs(torch.float32, self.samp["s2"]).view(self.batch, 11, 11, 6)
                 loss = self.learner.learn(s, self.samp["a"], self.samp["r"], self.samp["done"], s2, weights=w,
@@ -404,56 +383,6 @@ class VecTrainer:
         if self.learn_steps % self.target_every == 0:
             self.learner.sync_target()
         return loss
-
-    def _split_draw(self):
-        """Host part of a split learn step t (before push t): None when learn t does not run, else
-        ((base, count) of the ring's slots before push t that it keeps, (base, F) of push t's
-        slots, K fresh rows). K ~ Hypergeometric(F, count, B): with B - K rows drawn uniformly
-        without replacement from the kept slots and K from push t's, the batch is a uniform
-        B-subset of the ring after push t, the distribution of random.sample(memory, B)
-        (agents/dqn_agent.py:132)."""
-        F = self.n_agents
-        old = self.replay.window(F)
-        if self.t % self.learn_every or old[1] + F < self.batch:  # DQNAgent.learn's len(memory) guard
-            return None
-        k = int(self._hg.hypergeometric(F, old[1], self.batch)) if old[1] > 0 else self.batch
-        return old, (self.replay.pos, F), k
-
-    def _samp_rows(self, r0):
-        sp = self.samp
-        return dict(s=sp["s"][r0 * OBS_WORDS:], s2=sp["s2"][r0 * OBS_WORDS:], a=sp["a"][r0:], r=sp["r"][r0:],
-                    done=sp["done"][r0:])
-
-    def _learn_split_pre(self):
-        """Learn t's rows from the slots before push t (on the learn stream, current)."""
-        d = self._split_draw()
-        if d is None:
-            return None
-        old, fresh, k = d
-        n_old = self.batch - k
-        self.last_split = (n_old, k)
-        if n_old:
-            with torch.cuda.stream(self.lstream):
-                for grp in self.groups:  # push t-1 (the ring's contents) and the act order's inputs
-                    self.lstream.wait_event(grp.ev_push)
-                self.replay.sample_window(old[0], old[1], n_old, self.seed + 1, self.learn_steps * self.batch,
-                                          self._samp_rows(0))
-                sp = self.samp
-                self.learner.learn_obs(self.lay.c, sp["s"], sp["a"], sp["r"], sp["done"], sp["s2"], n_old,
-                                       update=False, part=(self.batch, True, k == 0))
-        return d
-
-    def _learn_split_post(self, d):
-        """Learn t's rows from push t's slots, then clip + Adam (learn stream, after push t)."""
-        old, fresh, k = d
-        n_old = self.batch - k
-        if k:
-            self.replay.sample_window(fresh[0], fresh[1], k, self.seed + 2, self.learn_steps * self.batch,
-                                      self._samp_rows(n_old))
-            sp = self._samp_rows(n_old)
-            self.learner.learn_obs(self.lay.c, sp["s"], sp["a"], sp["r"], sp["done"], sp["s2"], k, update=False,
-                                   part=(self.batch, n_old == 0, True))
-        return self.learn(phase="update")
 
     def step(self, extra_reset: Optional[torch.Tensor] = None, ev_env=None, ev_learn=None):
         """One training step. Finished envs are reset inside the env.step launch
@@ -476,26 +405,23 @@ class VecTrainer:
                 grp.main.wait_stream(caller)
             self.join_caller = False
         G = self.groups
-        inline = (self.lagged and len(G) == 1) if _ORDER_INLINE_ENV is None else _ORDER_INLINE_ENV == "1"
+        # the lagged schedule's dispatch order runs on the env's own stream right before env.step:
+        # its ~13 us kernel on the critical path beats the side stream's event pair (9.48 vs 9.03 M
+        # env-steps/s); the strict schedule keeps the side stream (its act + learn hide the order)
+        inline = self.lagged and len(G) == 1
         reset_wait, self.reset_pending = self.reset_pending, False
-        split = self.split and not self.lagged
-        if split and join:  # the learn stream reads what the caller may have written (weights, ring)
-            self.lstream.wait_stream(caller)
         # act: every group on its own stream, after the previous update (lagged) or learn
         for grp in G:
             with torch.cuda.stream(grp.main):
                 if reset_wait:  # a cross-stream wait costs a gap: only when there was a reset
                     grp.main.wait_event(self.ev_reset)
-                if self.lagged or grp.g > 0 or split:
+                if self.lagged or grp.g > 0:
                     grp.main.wait_event(self.ev_learned)
                 if self._perm is not None and not inline:  # the act order, made after the last push
                     grp.main.wait_event(grp.ev_order)
                 self._act(grp)
                 if self.lagged:
                     grp.ev_act.record(grp.main)
-        # split: learn t's old part on the learn stream (after learn t-1 there and push t-1), beside
-        # act t and env.step t; enqueued after the acts so their dropout streams come first
-        pre = self._learn_split_pre() if split else None
         if self.lagged:
             # learn t: gradients from the ring as it stood after push t-1 (minus the slots
             # push t overwrites), overlapping act t and env.step t; the weight update
@@ -562,18 +488,7 @@ class VecTrainer:
                 grp.env.compute_order()
                 if st is grp.side:
                     grp.ev_order.record(st)
-        if split:  # learn t's fresh part + clip + Adam, after push t (and so after act t)
-            with torch.cuda.stream(self.lstream):
-                for grp in G:
-                    self.lstream.wait_event(grp.ev_push)
-                if ev_learn is not None:
-                    ev_learn[0].record(self.lstream)
-                if pre is not None:
-                    self.last_loss = self._learn_split_post(pre)
-                if ev_learn is not None:
-                    ev_learn[1].record(self.lstream)
-                self.ev_learned.record(self.lstream)
-        elif not self.lagged:  # the reference's order: learn after every group's push, on group 0's stream
+        if not self.lagged:  # the reference's order: learn after every group's push, on group 0's stream
             m = G[0].main
             with torch.cuda.stream(m):
                 for grp in G[1:]:

@@ -243,15 +243,6 @@ int evx_td_loss_w(const float *Q, const float *Qt, int32_t A, const int32_t *act
 int evx_td_loss_zero(const float *Q, const float *Qt, int32_t A, const int32_t *act, const float *rew,
                      const uint8_t *done, float gamma, int32_t B, const float *w, float *dQ, float *loss, float *td_abs,
                      float *zero, int64_t nzero, void *stream);
-/* One part of a learn batch of B_norm rows split into row parts (the split learn step of
- * evacx.trainer: the rows already in the ring before this step's push, then the rows it pushed):
- * B of the rows, loss and dQ normalised by B_norm (>= B); accumulate != 0 adds the part's loss to
- * loss[0] (a later part; zero must then be NULL), else writes it; zero[0..nzero) cleared as in
- * evx_td_loss_zero (the first part). Same arithmetic as evx_td_loss per row
- * (agents/dqn_agent.py:143-151 with the mean over the whole batch). */
-int evx_td_loss_part(const float *Q, const float *Qt, int32_t A, const int32_t *act, const float *rew,
-                     const uint8_t *done, float gamma, int32_t B, int32_t B_norm, int32_t accumulate, float *dQ,
-                     float *loss, float *zero, int64_t nzero, void *stream);
 /* ||g||_2 into norm[0] (clip_grad_norm_'s total norm) */
 int evx_sumsq_norm(const float *g, int64_t n, float *scratch, int32_t scratch_elems, float *norm, void *stream);
 /* g *= min(1, max_norm/(norm+1e-6)) (skipped if norm NULL) then one torch.optim.Adam step */

@@ -14,9 +14,10 @@ says nothing about the variant the bench runs:
   (terminal ones through obs_term) bit-exact on every step.
   Reference: envs/people.py:196-314, envs/evacuation_env.py:84-288.
 
-* learn: the x3 learn chain at the bench's batches picks qfc1_kernel<4,1,8,true> (B >=
-  24576) and multi-tile qdz1 workgroups (8 tiles at B = 32768, 2 at 8192;
-  csrc/qmlp.hip: qdz1_tiles_per_wg, launch_fwd). One DQNAgent.learn step
+* learn: the x3 learn chain at the bench's batches: the online forward alone through
+  qfc1_kernel<2,2,4,true> (64 x 256 tiles) + qfc23, the target through the fused act kernel
+  at B >= 32768 (qact3h_kernel), multi-tile qdz1 workgroups (8 tiles at B = 32768, 2 at 8192;
+  csrc/qmlp.hip: qdz1_tiles_per_wg, launch_fwd, evx_qmlp_forward2). One DQNAgent.learn step
   (agents/dqn_agent.py:126-168) from compact observations of a 128x128 R16 env, explicit
   dropout keep masks, against torch fp32 autograd + clip_grad_norm_ + Adam on the expanded
   observations -- the same restatement tests/test_dqn_golden_cpu.py pins to the reference's
@@ -239,3 +240,120 @@ def test_x3_learn_at_bench_batch(B):
             assert (diff > 1e-5).float().mean().item() <= 1e-3, (it, k, diff.max().item())
             assert diff.max().item() <= 2e-3, (it, k, diff.max().item())
     print(f"B={B}: {n_flips} activations on the other ReLU branch than fp32 torch (x3 roundings of 0)")
+
+
+def _torch_conv_gated(sd, x, gates, g1, g2):
+    """DQNNetwork (agents/dqn_agent.py:15-61, conv variant) with every ReLU / dropout branch
+    given: gates[li] = conv layer li's output > 0 on the device (pixel-major [B*121][C]), g1 = keep
+    AND fc1 > 0, g2 = fc2 > 0 -- autograd then walks the branches the device's backward walked."""
+    B = x.shape[0]
+    h = x.permute(0, 3, 1, 2)
+    zs = []
+    for li, c in enumerate(("conv1", "conv2", "conv3")):
+        z = F.conv2d(h, sd[c + ".weight"], sd[c + ".bias"], padding=1)
+        zs.append(z)
+        gate = gates[li].view(B, 11, 11, -1).permute(0, 3, 1, 2)
+        h = z * gate
+    z1 = F.linear(h.reshape(B, -1), sd["fc1.weight"], sd["fc1.bias"])
+    z2 = F.linear(z1 * g1 / 0.8, sd["fc2.weight"], sd["fc2.bias"])
+    return F.linear(z2 * g2, sd["fc3.weight"], sd["fc3.bias"]), zs, z1, z2
+
+
+def _torch_conv_plain(sd, x, mask):
+    B = x.shape[0]
+    h = x.permute(0, 3, 1, 2)
+    for c in ("conv1", "conv2", "conv3"):
+        h = F.relu(F.conv2d(h, sd[c + ".weight"], sd[c + ".bias"], padding=1))
+    h = F.relu(F.linear(h.reshape(B, -1), sd["fc1.weight"], sd["fc1.bias"])) * mask.float() / 0.8
+    h = F.relu(F.linear(h, sd["fc2.weight"], sd["fc2.bias"]))
+    return F.linear(h, sd["fc3.weight"], sd["fc3.bias"])
+
+
+def test_conv_x3_learn_at_cfg4_batch():
+    """Two conv-net learn steps at cfg4's learn batch B = 1024 (the x3 implicit-GEMM convolutions,
+    fc1 over K = 15 488 in 16 split-K slices reduced in slice order) from the same parameters and
+    Adam moments on both sides, observations of a 256x256 env 30 steps into its episode.
+    ReLU branches as test_x3_learn_at_bench_batch: (1) the device's branch differs from torch
+    fp32's only where torch's pre-activation is within 1e-4 of the layer's max |z| (the x3
+    rounding of 0), on at most 1e-4 of the activations; (2) gradients, norm, loss and the Adam
+    update against torch autograd through the DEVICE's branch pattern with the x3 conv bars
+    (tests/test_qnet_gpu.py: gradients rtol 2e-3 / atol 1e-3 of max |grad|); (3) loss and norm
+    against plain torch. Reference: agents/dqn_agent.py:126-168."""
+    _need_gpu()
+    from evacx.env import DeviceLayout, VecEnv
+    from evacx.layout import build_tables, synthetic
+    from evacx.qnet import Learner
+    B, R, P = 1024, 1, 9102
+    E = 2 * B
+    lay = DeviceLayout(build_tables(synthetic(256, 256, R)), P)
+    env = VecEnv(lay, E)
+    env.seed([700 + i for i in range(E)])
+    env.reset()
+    g = torch.Generator(device="cuda").manual_seed(2)
+    for _ in range(30):
+        env.step(torch.randint(0, 5, (E * R,), device="cuda", dtype=torch.int32, generator=g), auto_reset=True)
+    torch.cuda.synchronize()
+    lr = Learner(kind="conv", precision="x3", seed=43, lr=1e-3)
+    sd0 = {k: v.detach().cpu().clone() for k, v in lr.online.state_dict().items()}
+    params = {k: torch.nn.Parameter(v.clone()) for k, v in sd0.items()}
+    tgt = {k: v.clone() for k, v in sd0.items()}
+    opt = torch.optim.Adam(params.values(), lr=1e-3)
+    gh = torch.Generator().manual_seed(B)
+    xall = env.expand_obs(torch.float32).reshape(E * R, 11, 11, 6).cpu()
+    for it in range(2):
+        if it > 0:
+            lr.online.load_state_dict({k: p.detach().cuda() for k, p in params.items()})
+            for key, buf in (("exp_avg", lr.m), ("exp_avg_sq", lr.v)):
+                buf.copy_(torch.cat([opt.state[p][key].reshape(-1) for p in params.values()]).cuda())
+        perm = torch.randperm(E * R, generator=gh)
+        x, x2 = xall[perm[:B]].contiguous(), xall[perm[B:2 * B]].contiguous()
+        a = torch.randint(0, 5, (B,), generator=gh, dtype=torch.int32)
+        r = torch.randn(B, generator=gh) * 30
+        d = (torch.rand(B, generator=gh) < 0.05).to(torch.uint8)
+        m1 = (torch.rand(B, 512, generator=gh) >= 0.2).to(torch.uint8)
+        m2 = (torch.rand(B, 512, generator=gh) >= 0.2).to(torch.uint8)
+        loss = lr.learn(x.cuda(), a.cuda(), r.cuda(), d.cuda(), x2.cuda(), m1.cuda(), m2.cuda())
+        torch.cuda.synchronize()
+        sv = lr.net.saved
+        gates = [(y > 0).float().cpu() for y in sv["ys"]]
+        g1, g2 = (sv["H1"] > 0).float().cpu(), (sv["H2"] > 0).float().cpu()
+        with torch.no_grad():
+            y = r + 0.99 * _torch_conv_plain(tgt, x2, m2).max(1)[0] * (~d.bool())
+            plain = {k: p.detach().clone().requires_grad_(True) for k, p in params.items()}
+        q_plain = _torch_conv_plain(plain, x, m1).gather(1, a.long().unsqueeze(1))
+        plain_loss = F.mse_loss(q_plain.squeeze(), y)
+        plain_loss.backward()
+        plain_norm = torch.sqrt(sum((p.grad.double() ** 2).sum() for p in plain.values())).item()
+        qg, zs, z1, z2 = _torch_conv_gated(params, x, gates, g1, g2)
+        with torch.no_grad():  # (1) torch's own branches vs the device's
+            h = x.permute(0, 3, 1, 2)
+            for li, c in enumerate(("conv1", "conv2", "conv3")):
+                z = F.conv2d(h, params[c + ".weight"], params[c + ".bias"], padding=1)
+                dev_gate = gates[li].view(B, 11, 11, -1).permute(0, 3, 1, 2).bool()
+                f = (z > 0) != dev_gate
+                assert int(f.sum()) <= 1e-4 * f.numel(), (c, int(f.sum()))
+                if f.any():
+                    assert z[f].abs().max().item() <= 1e-4 * z.abs().max().item(), c
+                h = F.relu(z)
+            z1p = F.linear(h.reshape(B, -1), params["fc1.weight"], params["fc1.bias"])
+            f1 = ((z1p > 0) & m1.bool()) != g1.bool()
+            assert int(f1.sum()) <= 1e-4 * f1.numel(), int(f1.sum())
+            if f1.any():
+                assert z1p[f1].abs().max().item() <= 1e-4 * z1p.abs().max().item()
+        ref_loss = F.mse_loss(qg.gather(1, a.long().unsqueeze(1)).squeeze(), y)
+        opt.zero_grad()
+        ref_loss.backward()
+        gnorm = torch.nn.utils.clip_grad_norm_(params.values(), 1.0)
+        grads_ref = {k: p.grad.clone() for k, p in params.items()}
+        opt.step()
+        assert abs(loss.item() - ref_loss.item()) <= 2e-4 * abs(ref_loss.item()) + 1e-5, (it, loss.item())
+        assert abs(loss.item() - plain_loss.item()) <= 2e-4 * abs(loss.item()) + 1e-5
+        assert abs(lr.norm.item() - gnorm.item()) <= 2e-4 * gnorm.item() + 1e-6, (it, lr.norm.item(), gnorm.item())
+        assert abs(lr.norm.item() - plain_norm) <= 1e-3 * plain_norm, (it, lr.norm.item(), plain_norm)
+        for k in params:
+            ref = grads_ref[k]
+            torch.testing.assert_close(lr.grads[k].cpu(), ref, rtol=2e-3, atol=1e-3 * ref.abs().max().item() + 1e-9,
+                                       msg=lambda m: f"step {it} grad {k}: {m}")
+            diff = (lr.online[k].cpu() - params[k].detach()).abs()
+            assert (diff > 1e-5).float().mean().item() <= 2e-3, (it, k, diff.max().item())
+            assert diff.max().item() <= 1e-3 * 3.3, (it, k, diff.max().item())

@@ -4,12 +4,10 @@
   the kernel's own Q-values, row for row;
 * uniform replay sampling (evx_replay_sample / _window, wrapping windows) == oracle.replay_indices,
   and the gathered rows are the ring's rows at those slots;
-* the composed VecTrainer step (strict, split and lagged): the actions are the epsilon-greedy draw
+* the composed VecTrainer step (strict and lagged): the actions are the epsilon-greedy draw
   of an independent forward with the same weights and dropout stream, and the replay push
   holds (obs before the step, action, team reward, done, obs after the step or the terminal
-  obs of an auto-reset env) for every robot; in the split learn step the batch is the old
-  part's window draw followed by the fresh part's (oracle.replay_indices of both windows), one
-  distinct B-subset of the ring after the push, and holds the ring's rows at those slots."""
+  obs of an auto-reset env) for every robot."""
 import numpy as np
 import pytest
 import torch
@@ -152,7 +150,7 @@ def test_per_agent_replay_sampling_matches_restatement():
                                       out["done"].data_ptr(), None) != 0  # size not a multiple of nets
 
 
-@pytest.mark.parametrize("mode", ["strict", "split", "lagged"])
+@pytest.mark.parametrize("mode", ["strict", "lagged"])
 def test_trainer_step_composition(mode):
     _need_gpu()
     from evacx.env import OBS_WORDS, DeviceLayout
@@ -164,9 +162,8 @@ def test_trainer_step_composition(mode):
     lay = DeviceLayout(build_tables(synthetic(32, 32, R)), 120)
     lagged = mode == "lagged"
     tr = VecTrainer(lay, E, batch=128, replay_capacity=8192, lagged_learn=lagged, epsilon=0.5)
-    tr.split = mode == "split"  # the split learn step (VecTrainer._split_draw; EVX_SPLIT_LEARN=1)
     env, n = tr.env, E * R
-    checked_done = split_seen = 0
+    checked_done = 0
     for t in range(12):
         tr.sync()
         torch.cuda.synchronize()
@@ -175,8 +172,7 @@ def test_trainer_step_composition(mode):
         h1 = torch.empty(2 * n * HID, dtype=torch.int16, device="cuda")
         q = torch.empty(n, 5, device="cuda")
         tr.fast.forward(lay.c, obs0, n, h1, drop=(tr.learner.seed, stream, DROPOUT_P, None, tr.agent0), q=q)
-        pos0, size0, ls0 = tr.replay.pos, tr.replay.size, tr.learn_steps
-        tr.last_split = None
+        pos0 = tr.replay.pos
         tr.step()
         tr.sync()
         torch.cuda.synchronize()
@@ -193,22 +189,4 @@ def test_trainer_step_composition(mode):
                          env.obs.view(-1, OBS_WORDS))
         assert torch.equal(rp.s2.view(-1, OBS_WORDS)[sl], s2)
         checked_done += int(done.sum())
-        if not lagged and tr.last_split is not None:  # the split learn step's batch (VecTrainer._split_draw)
-            n_old, k = tr.last_split
-            assert n_old + k == tr.batch and 0 <= k <= n
-            cnt = min(size0, rp.capacity - n)
-            idx = np.concatenate([orc.replay_indices((pos0 - cnt) % rp.capacity, cnt, rp.capacity, n_old,
-                                                     tr.seed + 1, ls0 * tr.batch) if n_old else np.zeros(0, np.int64),
-                                  orc.replay_indices(pos0, n, rp.capacity, k, tr.seed + 2, ls0 * tr.batch)
-                                  if k else np.zeros(0, np.int64)])
-            assert len(np.unique(idx)) == tr.batch  # one uniform B-subset of the ring after the push
-            fresh = (idx[n_old:] - pos0) % rp.capacity
-            assert (fresh < n).all() and ((idx[:n_old] - pos0) % rp.capacity >= n).all()
-            j = torch.from_numpy(idx).cuda()
-            for key in ("a", "r", "done"):
-                assert torch.equal(tr.samp[key], getattr(rp, key)[j]), (t, key)
-            for key in ("s", "s2"):
-                assert torch.equal(tr.samp[key].view(-1, OBS_WORDS), getattr(rp, key).view(-1, OBS_WORDS)[j]), (t, key)
-            split_seen += 1
-    assert mode != "split" or split_seen >= 10
     assert tr.learn_steps >= 10 and np.isfinite(tr.last_loss.item())

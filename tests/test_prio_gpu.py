@@ -45,7 +45,7 @@ def _adopt_leaves(o, rp):
     o.max_leaf[0] = rp.max_leaf.item()
 
 
-@pytest.mark.parametrize("C", [1024, 1 << 15, 1 << 20])
+@pytest.mark.parametrize("C", [1024, 1 << 15, 1 << 20, 1 << 22])  # 2^22: cfg5's ring, a three-pass rebuild
 def test_trees_and_sampling_vs_oracle(C):
     _need_gpu()
     rp = _ring(C)

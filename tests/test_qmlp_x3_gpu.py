@@ -229,7 +229,7 @@ def test_fused_learn_chain_matches_separate_launches(hook):
     assert 2 * B <= env.E * lay.R
     dev = "cuda"
     runs = []
-    for fused in (False, True):
+    for fused in (False, True, True):
         lr = Learner(kind="mlp", precision="f32", seed=33, lr=1e-3)
         lr.fused_opt = fused
         if hook:
@@ -252,15 +252,19 @@ def test_fused_learn_chain_matches_separate_launches(hook):
                          params={k: v.clone() for k, v in lr.online.state_dict().items()},
                          packed=[t.clone() for t in (lr.fast.w1b, lr.fast.w1l, lr.fast.b1c, lr.fast.w2b, lr.fast.w2l,
                                                      lr.fast.w2t, lr.fast.w2tl)], lr=lr))
-    sep, fus = runs
+    sep, fus, fus2 = runs
+    # the same seed and batches give the same bits (every gradient sum in a fixed order)
+    assert fus["loss"] == fus2["loss"] and fus["norm"] == fus2["norm"]
+    for k in fus["params"]:
+        assert torch.equal(fus["grads"][k], fus2["grads"][k]), k
+        assert torch.equal(fus["params"][k], fus2["params"][k]), k
     assert abs(sep["loss"] - fus["loss"]) <= 1e-5 * abs(sep["loss"]) + 1e-7
     assert abs(sep["norm"] - fus["norm"]) <= 1e-5 * sep["norm"] + 1e-9
     for k in sep["params"]:
         scale = sep["grads"][k].abs().max().item()
-        # atol 2e-6 of the tensor's scale: after three Adam steps the runs' parameters differ by the
-        # reassociation of f32 sums (and the order of qbwd3's / qdz1's f32 atomics into W3, b2, b1),
-        # which moved one element 2.1e-8 of a 1.8e-8 bound at 1e-6 in one of many runs
-        torch.testing.assert_close(fus["grads"][k], sep["grads"][k], rtol=1e-4, atol=2e-6 * scale + 1e-12)
+        # after three Adam steps the two chains differ only by the reassociation of the gradient
+        # norm's f32 sum (norm partials of reduce2 vs sumsq_parts)
+        torch.testing.assert_close(fus["grads"][k], sep["grads"][k], rtol=1e-4, atol=1e-6 * scale + 1e-12)
         torch.testing.assert_close(fus["params"][k], sep["params"][k], rtol=1e-5, atol=2e-6)
     lr = fus["lr"]
     lr.fast.repack()  # pack3 of the fused run's own parameters
@@ -323,3 +327,62 @@ def test_x3_act_static_table_and_env_order(xr):
     assert torch.equal(qt[~rows_sat], qp[~rows_sat])    # the full path, same rows: bit for bit
     assert (at0 == ap0).float().mean().item() >= 0.99
     assert torch.equal(at1, ap1)
+
+
+def test_x3_act_at_bench_rows_table_path_env_order():
+    """The act as the cfg3 bench runs it: 524 288 rows (32 768 envs x 16 robots), the per-centre
+    table path for the envs past the fire's last step (85 %), VecEnv.act_perm's env order, dropout
+    and epsilon = 0.1 (agents/dqn_agent.py:101-124). Real 128x128 R16 observations (4096 envs, a few
+    steps) tiled 8 times, fire step raised to t_max on 85 % of the envs. Q of a sample of 64 runs of
+    64 rows against torch fp32 on the expanded observations with the kernel's own dropout masks
+    (rtol 2e-4, atol 1e-4 of the Q scale: the x3 bars plus the table path's reassociation);
+    actions = the epsilon-greedy restatement (oracle.epsilon_greedy) of the kernel's Q on every row,
+    and the greedy argmax of torch's Q on >= 99.5 % of the sampled rows."""
+    _need_gpu()
+    from evacx.env import DeviceLayout, VecEnv
+    from evacx.layout import build_tables, synthetic
+    from evacx.qmlp import HID, K1, dropout_keep
+    from evacx.qnet import DROPOUT_P, Learner
+    from oracle import oracle as orc
+    R, E0, rep = 16, 4096, 8
+    lay = DeviceLayout(build_tables(synthetic(128, 128, R)), 2276)
+    env = VecEnv(lay, E0)
+    env.seed([900 + i for i in range(E0)])
+    env.reset()
+    g = torch.Generator(device="cuda").manual_seed(3)
+    for _ in range(4):
+        env.step(torch.randint(0, 5, (E0 * R,), device="cuda", dtype=torch.int32, generator=g), auto_reset=True)
+    torch.cuda.synchronize()
+    E, n = E0 * rep, E0 * rep * R
+    t_max = int(lay.c.t_max)
+    obs = env.obs.view(E0, R, 8).repeat(rep, 1, 1).contiguous()
+    rng = np.random.RandomState(5)
+    sat = torch.from_numpy(rng.rand(E) < 0.85).cuda()
+    obs[:, :, 6] = torch.where(sat[:, None], torch.full_like(obs[:, :, 6], t_max), obs[:, :, 6])
+    s = sat.cpu().numpy()
+    perm = torch.from_numpy(np.concatenate([np.nonzero(s)[0], np.nonzero(~s)[0]]).astype(np.int32)).cuda()
+    lr = Learner(kind="mlp", precision="f32", seed=41)
+    fast = lr.fast
+    lc = lay.c
+    fast.attach_static(lc, int(lc.L), int(lc.W), t_max, x_range=(max(lc.rx_lo, 0), min(lc.rx_hi, lc.L + 1)))
+    q = torch.empty(n, 5, device="cuda")
+    a = torch.empty(n, dtype=torch.int32, device="cuda")
+    seed, stream, eps, aseed, aoff = 12, 7, 0.1, 4, 1000
+    fast.act(lc, obs.view(-1), n, drop=(seed, stream, DROPOUT_P), q=q, actions=a, epsilon=eps, act_seed=aseed,
+             act_offset=aoff, perm=perm, rows_per_env=R)
+    torch.cuda.synchronize()
+    qk = q.cpu().numpy()
+    assert np.array_equal(a.cpu().numpy(), orc.epsilon_greedy(qk, eps, aseed, aoff))
+    starts = np.sort(rng.choice(n // 64, 64, replace=False)) * 64
+    rows = np.concatenate([np.arange(r0, r0 + 64) for r0 in starts])
+    ob_s = obs.view(n, 8)[torch.from_numpy(rows).cuda()].contiguous()
+    X = env.expand_obs(torch.float32, ob_s.view(-1)).reshape(len(rows), K1)
+    keep = np.concatenate([dropout_keep(seed, stream, DROPOUT_P, 64, HID, row0=int(r0)) for r0 in starts])
+    mask = torch.from_numpy(keep.astype(np.uint8)).cuda()
+    refq, _ = torch_q(lr.online.state_dict(), X, mask)
+    got = q[torch.from_numpy(rows).cuda()]
+    scale = refq.abs().max().item()
+    torch.testing.assert_close(got, refq, rtol=2e-4, atol=1e-4 * scale)
+    assert (got.argmax(1) == refq.argmax(1)).float().mean().item() >= 0.995
+    # the table path ran on the saturated envs' rows (not bit-identical to the full path there)
+    assert s[rows // R].any()

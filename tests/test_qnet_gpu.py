@@ -72,7 +72,8 @@ def test_forward_bf16_close_to_torch():
 
 @pytest.mark.parametrize("kind,prec", [("mlp", "f32"), ("conv", "f32"), ("conv", "x3")])
 def test_learn_steps_match_torch_adam(kind, prec):
-    """3 learn steps: loss, clipped grads and params vs torch (MSE, clip_grad_norm_(1.0), Adam 1e-4)."""
+    """3 learn steps: loss, clipped grads and params vs torch (MSE, clip_grad_norm_(1.0), Adam 1e-4).
+    (cfg4's batch, B = 1024: tests/test_bench_scale_gpu.py::test_conv_x3_learn_at_cfg4_batch.)"""
     _need_gpu()
     from evacx.qnet import Learner
     B = 32

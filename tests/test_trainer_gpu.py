@@ -146,3 +146,39 @@ def test_vec_trainer_groups(lagged):
     assert a.min() >= 0 and a.max() <= 4
     obs = tr.replay.s.view(-1, 8)[:tr.replay.size].cpu().numpy()
     assert (obs[:, 4] >= 0).all() and (obs[:, 4] <= 25).all()
+
+
+def test_same_seed_trainers_are_bit_identical():
+    """Two VecTrainers with the same seeds at cfg3's geometry (128x128, P 2276, R 16; E = 4096,
+    learn batch 4096) agree bit for bit after 10 training steps: weights, target weights, Adam
+    moments, env state (people, health, rmap, robots, MT19937 streams), actions. DQNAgent.learn
+    (agents/dqn_agent.py:126-168) on torch-CPU gives the same weights on every same-seed run; the
+    learn chain here sums every gradient through partials in a fixed order (no f32 atomics)."""
+    _need_gpu()
+    from evacx.env import DeviceLayout
+    from evacx.layout import build_tables, synthetic
+    from evacx.trainer import VecTrainer
+    lay = DeviceLayout(build_tables(synthetic(128, 128, 16)), 2276)
+    snaps = []
+    for _ in range(2):
+        tr = VecTrainer(lay, 4096, batch=4096, replay_capacity=1 << 20, epsilon=0.3, target_every=4)
+        acts = []
+        for _ in range(10):
+            tr.step()
+            with torch.cuda.stream(tr.main):  # the trainer's stream: after this step's act, before the next
+                acts.append(tr.actions.clone())
+        tr.sync()
+        torch.cuda.synchronize()
+        tr.env.check_err()
+        lr, env = tr.learner, tr.env
+        assert tr.learn_steps == 10
+        snaps.append(dict(online=lr.online.flat.clone(), target=lr.target.flat.clone(), m=lr.m.clone(),
+                          v=lr.v.clone(), loss=tr.last_loss.clone(), pk=env.pk.clone(), health=env.health.clone(),
+                          acc=env.acc.clone(), rmap=env.rmap.clone(), robots=env.robots.clone(),
+                          scal=env.scal.clone(), py_mt=env.py_mt.clone(), np_mt=env.np_mt.clone(),
+                          obs=env.obs.clone(), acts=torch.stack(acts), ring=tr.replay.s.clone()))
+        del tr, lr, env
+        torch.cuda.empty_cache()
+    a, b = snaps
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
