@@ -45,10 +45,10 @@ namespace evx {
 constexpr uint32_t NODIR = 0xffu;
 
 // step kernel (one wave per env)
-constexpr int WR = 1024;             // MT ring words per stream (>= 624 + 227)
+constexpr int WR = 1024;             // the reset's MT ring words (>= 624 + 227)
 constexpr int WRM = WR - 1;
-constexpr int WWIN = WR - 64 - 16;   // scoring words made readable per ensure
-constexpr int SHUF_WORDS = 384;      // words per lane-0 shuffle round (keeps mt_store_w's window valid)
+constexpr int WWIN = MT_N - 16;      // scoring words readable per ensure of the step's 624-slot Python ring
+constexpr int SHUF_WORDS = 384;      // words per shuffle chunk (a chunk's words stay in the 624-slot ring)
 constexpr int CL_CAP = 510;          // contested movers sorted in LDS (more: global scratch): the list
                                      // (512 with sort padding) in the numpy ring, heads 256 | starts 256
                                      // in the planner queue (both dead after the rows)
@@ -329,6 +329,54 @@ __device__ __forceinline__ void np_store(uint32_t* ring, int& front, int head, u
     if (lane == 0) gst[MT_N] = (uint32_t)(head - b);
 }
 
+// The step's Python stream in the same 624-slot in-place ring (word n in slot n % 624): unlike the
+// numpy stream it is read ahead of the words consumed (scoring windows, shuffle windows: at most
+// 128 words past the stream's final head), so a block boundary may be crossed before the block
+// that holds the final head is stored. Rounds stop at block boundaries, and when the generation
+// crosses boundary c (words from c on overwrite block [c - 624, c)) while the stream's final head
+// may still lie in that block (head_lb, a lower bound of it, <= c), the block is stored first.
+// The final head is never 624 words below the front, so no later crossing overwrites it.
+__device__ __forceinline__ void py_ensure(uint32_t* ring, int& front, int upto, uint32_t* gst, int head_lb) {
+    const int lane = (int)(threadIdx.x & 63);
+    while (front < upto) {
+        const int r = np_slot(front);
+        if (r == 0 && front >= 2 * MT_N && head_lb <= front) {
+            for (int i = lane; i < MT_N; i += 64) gst[i] = ring[i];  // block [front - 624, front)
+        }
+        const int cnt = min(min(MT_LAG, upto - front), MT_N - r);
+        uint32_t lag[4], a[4], b[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int n = front + lane + 64 * j;
+            lag[j] = ring[np_slot(n - MT_LAG)];
+            a[j] = ring[np_slot(n - 624)];
+            b[j] = ring[np_slot(n - 623)];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int n = front + lane + 64 * j;
+            if (lane + 64 * j < cnt) ring[np_slot(n)] = mt_twist1(lag[j], a[j], b[j]);
+        }
+        front += cnt;
+        wave_fence();
+    }
+}
+// The state after consuming up to raw index `head`: block b = [b, b + 624) holding head - 1, from
+// the ring (front <= b + 624) or as py_ensure stored it when it crossed b + 624.
+__device__ __forceinline__ void py_store(uint32_t* ring, int& front, int head, uint32_t* gst) {
+    const int lane = (int)(threadIdx.x & 63);
+    if (head <= MT_N) {
+        if (lane == 0) gst[MT_N] = (uint32_t)head;  // no twist: words unchanged
+        return;
+    }
+    const int b = MT_N * ((head - 1) / MT_N);
+    if (front <= b + MT_N) {
+        py_ensure(ring, front, b + MT_N, gst, head);
+        for (int i = lane; i < MT_N; i += 64) gst[i] = ring[i];
+    }
+    if (lane == 0) gst[MT_N] = (uint32_t)(head - b);
+}
+
 
 // Ascending bitonic sort of a[0..64*R) by one wave in registers: element i = lane*R + r
 // lives in register r of lane `lane`; stages with j < R are compare-exchanges between
@@ -503,7 +551,7 @@ __device__ __forceinline__ int doff_of(uint32_t d, int GY) { return move_dx((int
 
 template <typename T>
 __device__ __forceinline__ void contested_groups(T* Lp, T* heads, T* gstart, int n, int pb, uint32_t* pyring, int& py_front,
-                                 int& py_head, uint32_t* lost, uint32_t* grp, int& err, long long* prof) {
+                                 int& py_head, uint32_t* lost, uint32_t* grp, int& err, long long* prof, uint32_t* gst) {
     const int lane = (int)(threadIdx.x & 63);
 #ifdef EVX_PROFILE
     long long tq = __builtin_amdgcn_s_memtime();
@@ -574,8 +622,8 @@ __device__ __forceinline__ void contested_groups(T* Lp, T* heads, T* gstart, int
         const long long tb0 = __builtin_amdgcn_s_memtime();
 #endif
         B = b0;
-        mt_ensure_w(pyring, py_front, B + 128);
-        const uint32_t t0 = mt_temper(pyring[(B + lane) & WRM]), t1 = mt_temper(pyring[(B + 64 + lane) & WRM]);
+        py_ensure(pyring, py_front, B + 128, gst, B);
+        const uint32_t t0 = mt_temper(pyring[np_slot(B + lane)]), t1 = mt_temper(pyring[np_slot(B + 64 + lane)]);
         unsigned long long lo[7], hi[7];  // acceptance of bound 2..8 over the 128 words
 #pragma unroll
         for (int bb = 2; bb <= 8; bb++) {
@@ -626,6 +674,9 @@ __device__ __forceinline__ void contested_groups(T* Lp, T* heads, T* gstart, int
         while (nk < 64 && k < ngrp && pos - W0 < SHUF_WORDS) {
             const uint32_t dsc = (uint32_t)__builtin_amdgcn_readlane((int)desc, nk);
             const int cnt = (int)(dsc & 255u);
+            // a group of more than 8 movers (rare) runs alone in its chunk and is shuffled here, by lane
+            // 0 as the words are made (its words need not stay in the ring for pass 2)
+            if (cnt > 8 && nk > 0) break;
             wv = lane == nk ? pos : wv;
             if (cnt <= 8) {
                 while (true) {
@@ -648,18 +699,36 @@ __device__ __forceinline__ void contested_groups(T* Lp, T* heads, T* gstart, int
                     err |= 2;  // > 128 words for <= 8 movers: not a sane stream
                     break;
                 }
-            } else {  // large group: bounds > 8 word by word (rare)
+            } else {  // large group: Lib/random.py shuffle word by word (rare)
+                const int s0 = (int)(dsc >> 8);
+                const bool rep = cnt <= GRP_MAX;  // larger: flagged above, not representable
+                if (rep)
+                    for (int q = lane; q < cnt; q += 64) grp[q] = Lp[s0 + q] & pmask;
+                wave_fence();
                 for (int i = cnt - 1; i >= 1; i--) {
                     const uint32_t bound = (uint32_t)(i + 1);
                     const int kb = bit_length(bound);
                     while (true) {
-                        if (py_front < pos + 1) mt_ensure_w(pyring, py_front, pos + 64);
-                        const uint32_t t = mt_temper(pyring[pos & WRM]);
+                        if (py_front < pos + 1) py_ensure(pyring, py_front, pos + 64, gst, pos);
+                        const uint32_t r = mt_temper(pyring[np_slot(pos)]) >> (32 - kb);
                         pos++;
-                        if ((t >> (32 - kb)) < bound) break;
+                        if (r < bound) {
+                            if (lane == 0 && rep) {
+                                const uint32_t t = grp[i];
+                                grp[i] = grp[r];
+                                grp[r] = t;
+                            }
+                            break;
+                        }
                     }
                 }
+                wave_fence();
+                if (rep)
+                    for (int q = 1 + lane; q < cnt; q += 64) atomicOr(&lost[grp[q] >> 5], 1u << (grp[q] & 31));
                 B = -(1 << 30);  // end tables are stale
+                nk++;
+                k++;
+                break;
             }
             nk++;
             k++;
@@ -684,7 +753,7 @@ __device__ __forceinline__ void contested_groups(T* Lp, T* heads, T* gstart, int
                         const int kb = bit_length(bound);
                         uint32_t r;
                         do {
-                            r = mt_word(pyring, WRM, head++) >> (32 - kb);
+                            r = mt_temper(pyring[np_slot(head++)]) >> (32 - kb);
                         } while (r >= bound);
                         uint32_t ar = a[0];
 #pragma unroll
@@ -698,30 +767,6 @@ __device__ __forceinline__ void contested_groups(T* Lp, T* heads, T* gstart, int
 #pragma unroll
                 for (int j = 1; j < 8; j++)
                     if (j < cnt) atomicOr(&lost[a[j] >> 5], 1u << (a[j] & 31));
-            }
-        }
-        // groups of more than 8 movers (rare): lane 0, same words
-        for (int j = 0; j < nk; j++) {
-            const uint32_t dsc = (uint32_t)__builtin_amdgcn_readlane((int)desc, j);
-            const int cnt = (int)(dsc & 255u);
-            if (cnt <= 8) continue;
-            const int w0 = __builtin_amdgcn_readlane(wv, j);
-            if (lane == 0 && cnt <= GRP_MAX) {
-                const int s0 = (int)(dsc >> 8);
-                for (int q = 0; q < cnt; q++) grp[q] = Lp[s0 + q] & pmask;
-                int head = w0;
-                for (int i = cnt - 1; i >= 1; i--) {
-                    const uint32_t bound = (uint32_t)(i + 1);
-                    const int kb = bit_length(bound);
-                    uint32_t r;
-                    do {
-                        r = mt_word(pyring, WRM, head++) >> (32 - kb);
-                    } while (r >= bound);
-                    const uint32_t t = grp[i];
-                    grp[i] = grp[r];
-                    grp[r] = t;
-                }
-                for (int q = 1; q < cnt; q++) atomicOr(&lost[grp[q] >> 5], 1u << (grp[q] & 31));
             }
         }
         wave_sync();
@@ -761,7 +806,7 @@ __host__ __device__ inline WaveLds wave_lds(int L, int W, int P, int R, bool big
     const int RW = (G + 31) / 32;
     const int NCW = (((L + 2 + 3) >> 2) * ((W + 2 + 3) >> 2) + 31) / 32;
     int o = 0;
-    s.pyring = o; o += WR;                 // after the shuffles: vacated-cell bitmap; reward: leaf sums | leaf buffer
+    s.pyring = o; o += MT_N;               // after the shuffles: vacated-cell bitmap; reward: leaf sums | leaf buffer
     s.npring = o; o += MT_N;               // the numpy ring (np_ensure); after the rows: contested list
     s.aux = o; o += 512 + 16;              // planner queue + health group; events; leaf table
     s.rmapb = o; o += RW;
@@ -769,8 +814,9 @@ __host__ __device__ inline WaveLds wave_lds(int L, int W, int P, int R, bool big
         s.tbits = s.cbits = s.vac = -1;  // global scratch (env_scratch_words)
     } else {
         s.tbits = o; o += RW;
-        s.cbits = o; o += RW;
-        if (RW <= WR) {
+        s.cbits = -1;  // the contested bitmap: global step scratch (cbits_offset), set and read only
+                       // when two planners target one cell
+        if (RW <= MT_N) {
             s.vac = s.pyring;
         } else {
             s.vac = o; o += RW;
@@ -804,10 +850,16 @@ __host__ __device__ inline int64_t wave_scratch_words(int P) { return wave_hv_of
 // count, in-play count, -, the health total as a double at [4..5], -) | the not-dead persons'
 // healths in list order [P] double (the in-play list itself stays in the wide path's health
 // region, which a light step does not otherwise use)
+// ... | other grids: the contested bitmap [RW] (zero between steps: a step that sets bits clears them)
 __host__ __device__ inline int64_t persist_offset(const evx_layout& l) {
     const int RW = ((l.L + 2) * (l.W + 2) + 31) / 32;
-    const int64_t o = wave_scratch_words(l.P) + (big_grid(l.L, l.W) ? 3 * (int64_t)RW + (l.P + 31) / 32 : 0);
+    const int64_t o = wave_scratch_words(l.P) + (big_grid(l.L, l.W) ? 3 * (int64_t)RW + (l.P + 31) / 32 : RW);
     return (o + 1) & ~(int64_t)1;
+}
+// the contested bitmap in an env's step scratch (big grids: after the target bitmap)
+__host__ __device__ inline int64_t cbits_offset(const evx_layout& l) {
+    const int RW = ((l.L + 2) * (l.W + 2) + 31) / 32;
+    return wave_scratch_words(l.P) + (big_grid(l.L, l.W) ? RW : 0);
 }
 constexpr int LHDR = 8;  // words of the kept lists' header
 __host__ __device__ inline int64_t env_scratch_words(const evx_layout& l) { return persist_offset(l) + LHDR + 2 * (int64_t)l.P; }
@@ -952,7 +1004,8 @@ __device__ __forceinline__ uint32_t dir_score(const DirPrep& d, uint32_t cand, i
         if ((cand >> k) & 1u) {
             double effect = 0.0;
             if (((d.nearm >> k) & 1u) && d.md2[k] < rd2) effect = repel_k / (sqrt((double)d.md2[k]) + 0.1);
-            const double u = -0.1 + (0.1 - -0.1) * mt_double(ring, mask, idx - base);
+            // mask 0: the step's 624-slot Python ring; else a power-of-two ring or a linear buffer
+            const double u = -0.1 + (0.1 - -0.1) * (mask ? mt_double(ring, mask, idx - base) : np_double(ring, idx));
             idx += 2;
             const double score = d.f[k] + effect + u;  // delta_p * 5.0 + robot_effect + uniform
             if (score > maxs) {
@@ -1060,7 +1113,6 @@ __device__ __forceinline__ void rows_wide(const evx_layout& lay, const evx_state
     uint32_t* myl = smem + WL.lists + w * WL.CHmax * 3;
     const uint32_t* rmapb = smem + S.rmapb;
     uint32_t* tbits = smem + S.tbits;
-    uint32_t* cbits = smem + S.cbits;
     const uint32_t* nearc = smem + S.nearc;
     const uint32_t* robots = smem + S.robots;
     uint32_t* pyring = smem + S.pyring;
@@ -1071,6 +1123,7 @@ __device__ __forceinline__ void rows_wide(const evx_layout& lay, const evx_state
     double* h_g = st.health + (size_t)e * P;
     double* a_g = st.acc + (size_t)e * P;
     uint32_t* scr = st.scratch + (size_t)e * env_scratch_words(lay);
+    uint32_t* cbits = scr + cbits_offset(lay);  // global (L2): device-scope atomics
     uint2* plan = reinterpret_cast<uint2*>(scr);
     const uint2* ndl = reinterpret_cast<const uint2*>(scr + 2 * P);
     double* hv = reinterpret_cast<double*>(scr + wave_hv_offset(P));
@@ -1349,8 +1402,8 @@ __device__ __forceinline__ void rows_wide(const evx_layout& lay, const evx_state
             if (mover) plan[dst] = make_uint2(e0 & 0xffffu, (uint32_t)(pk_x(e1) * GY + pk_y(e1)) | (best << 24));
         }
     }
-    // hand the Python stream back to wave 0's ring: words [front - 1024, front)
-    for (int n = max(0, front - WR) + tid; n < front; n += 64 * WNW) pyring[n & WRM] = lin[n - base];
+    // hand the Python stream back to wave 0's 624-slot ring: words [front - 624, front)
+    for (int n = max(0, front - MT_N) + tid; n < front; n += 64 * WNW) pyring[np_slot(n)] = lin[n - base];
     if (tid == 0) {
         ctl->nplan = nplan;
         ctl->n_died = nd_all;
@@ -1408,14 +1461,15 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     uint32_t* rmapb = smem + S.rmapb;
     const int64_t SW = env_scratch_words(lay);
     uint32_t* scr = st.scratch + (size_t)e * SW;
-    uint32_t *tbits, *cbits, *vac;
+    uint32_t *tbits, *vac;
+    // the contested bitmap: global (L2) for every grid, read with agent-scope atomic loads past the
+    // L1 and only when some target is contested (any_cont)
+    uint32_t* cbits = scr + cbits_offset(lay);
     if constexpr (BIGG) {  // global (L2): read with agent-scope atomic loads, past the L1
         tbits = scr + wave_scratch_words(P);
-        cbits = tbits + g.RW;
         vac = cbits + g.RW;
     } else {
         tbits = smem + S.tbits;
-        cbits = smem + S.cbits;
         vac = smem + S.vac;
     }
     auto tc_get = [&](const uint32_t* b, int i) -> bool {
@@ -1423,6 +1477,9 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
             return (__hip_atomic_load(b + (i >> 5), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (i & 31)) & 1u;
         else
             return bit_get(b, i);
+    };
+    auto cb_get = [&](int i) -> bool {
+        return (__hip_atomic_load(cbits + (i >> 5), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (i & 31)) & 1u;
     };
     uint32_t* nearc = smem + S.nearc;
     const int NCW = (((g.L + 2 + 3) >> 2) * ((GY + 3) >> 2) + 31) / 32;
@@ -1469,6 +1526,7 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     }
     const uint32_t* gpy = st.py_mt + (size_t)e * EVX_MT_WORDS;
     const uint32_t* gnp = st.np_mt + (size_t)e * EVX_MT_WORDS;
+    uint32_t* gpyw = st.py_mt + (size_t)e * EVX_MT_WORDS;  // py_ensure / py_store (read above first)
     uint32_t wpy[10], wnp[10];
 #pragma unroll
     for (int j = 0; j < 10; j++) {
@@ -1506,7 +1564,7 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
             if (i < g.RW) {
                 rmapb[i] = w[j];
                 tbits[i] = 0;
-                cbits[i] = 0;
+                if constexpr (BIGG) cbits[i] = 0;
             }
         }
     }
@@ -1710,10 +1768,10 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
         uint32_t best = NODIR;
         for (int lo = first; lo < end; lo += WWIN) {  // windowed: a batch may need more words than the ring
             PT_BEGIN(sbm);
-            mt_ensure_w(pyring, py_front, min(end, lo + WWIN + 16));
+            py_ensure(pyring, py_front, min(end, lo + WWIN + 16), gpyw, end);
             PT_END(sbm);
             PT_BEGIN(sbs);
-            if (has && off >= lo && off < lo + WWIN) best = dir_score(dp, cand, off, pyring, 0, WRM, lay.repel_k, rd2);
+            if (has && off >= lo && off < lo + WWIN) best = dir_score(dp, cand, off, pyring, 0, 0, lay.repel_k, rd2);
             PT_END(sbs);
         }
         PT_BEGIN(sbt);
@@ -1776,7 +1834,7 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
         PT_END(np);
         // the list-order health the fold reads; a death leaves -0.0 (adds nothing to the running
         // sum, which is >= +0.0) and marks the slot the fold drops from the kept list
-        if (inr) hl[en.x >> 16] = died ? -0.0 : hh;
+        if (need) hl[en.x >> 16] = died ? -0.0 : hh;  // the others' kept entries are unchanged
         PT_BEGIN(plan);
         // phase 2: accumulate; candidates of find_best_direction
         bool planner = false;
@@ -1970,7 +2028,8 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
                 {
                     const bool keep = i0 + 64 * k + lane < nnd && !signbit(fv[k]);
                     const unsigned long long km = __ballot(keep);
-                    if (keep) hl[nkeep + lanes_below(km)] = fv[k];  // index <= read index: consumed
+                    const int dst = nkeep + lanes_below(km);  // <= read index: a consumed entry
+                    if (keep && dst != i0 + 64 * k + lane) hl[dst] = fv[k];  // only entries behind a death move
                     nkeep += __popcll(km);
                 }
                 wave_fence();
@@ -2033,7 +2092,7 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
             uint32_t key = 0;
             if (ok) {
                 const int t = (int)(en.y & 0xffffffu) + doff_of(en.y >> 24, GY);
-                c = tc_get(cbits, t);
+                c = cb_get(t);
                 key = ((uint32_t)t << pb) | en.x;
             }
             const unsigned long long m = __ballot(c);
@@ -2044,7 +2103,7 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
         PT_END(lp);
         PT_BEGIN(grp);
         if (ncont <= CL_CAP) {
-            contested_groups(Lp, aux, aux + 256, ncont, pb, pyring, py_front, py_head, lost, misc, err, cgp);
+            contested_groups(Lp, aux, aux + 256, ncont, pb, pyring, py_front, py_head, lost, misc, err, cgp, gpyw);
         } else {  // rare: sort in this env's global scratch
             Lp = Lg;
             int k = 0;
@@ -2053,7 +2112,7 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
                 uint32_t key = 0;
                 if (ok) {
                     const int t = (int)(en.y & 0xffffffu) + doff_of(en.y >> 24, GY);
-                    c = tc_get(cbits, t);
+                    c = cb_get(t);
                     key = ((uint32_t)t << pb) | en.x;
                 }
                 const unsigned long long m = __ballot(c);
@@ -2061,13 +2120,13 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
                 k += __popcll(m);
             });
             wave_sync();
-            contested_groups(Lg, Hg, Sg, ncont, pb, pyring, py_front, py_head, lost, misc, err, cgp);
+            contested_groups(Lg, Hg, Sg, ncont, pb, pyring, py_front, py_head, lost, misc, err, cgp, gpyw);
         }
     }
     PT_END(grp);
     PT_BEGIN(mts);
     EVX_COUNT(14, ncont);
-    mt_store_w(pyring, py_front, py_head, st.py_mt + (size_t)e * EVX_MT_WORDS);
+    py_store(pyring, py_front, py_head, gpyw);
     EVX_COUNT(12, py_head);
     // the Python stream is stored: its ring becomes the "vacated by a winner" bitmap
     for (int i = lane; i < g.RW; i += 64) vac[i] = 0;
@@ -2105,7 +2164,7 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
         if (ok) {
             const int cold = (int)(en.y & 0xffffffu);
             const int t = cold + doff_of(en.y >> 24, GY);
-            const bool win = !tc_get(cbits, t) || !tc_get(lost, (int)en.x);
+            const bool win = !any_cont || !cb_get(t) || !tc_get(lost, (int)en.x);
             if (win) atomicOr(&vac[cold >> 5], 1u << (cold & 31));
             if (st.thmap) atomicAdd(&st.thmap[(size_t)e * g.G + (win ? t : cold)], 1);
         }
@@ -2114,6 +2173,9 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     wave_sync();
     uint32_t* ev = aux;  // (cell, key) pairs; groups are done
     int n_evac_new = 0;
+    // a step with <= 64 movers writes back only the rmap words its winners changed (cold, t)
+    const bool rm_dirty = nplan <= 64;
+    int dw0 = -1, dw1 = -1;
     for (int i0 = 0; i0 < nplan; i0 += 256) {
       uint2 en4[4];
       uint32_t ci4[4];
@@ -2137,7 +2199,7 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
             const int cold = (int)(en.y & 0xffffffu);
             const int dd = (int)(en.y >> 24);
             const int t = cold + doff_of((uint32_t)dd, GY);
-            const bool cont = tc_get(cbits, t);
+            const bool cont = any_cont && cb_get(t);
             if (!cont || !tc_get(lost, p)) {
                 const bool ex = (ci4[j] >> 1) & 1u;
                 exw = ex;
@@ -2166,6 +2228,8 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
                 }
                 const int ox = cold / GY, oy = cold - ox * GY;
                 pk_g[p] = (uint32_t)(ox + move_dx(dd)) | ((uint32_t)(oy + move_dy(dd)) << 12) | (ex ? (1u << 24) : 0u);
+                dw0 = cold >> 5;
+                dw1 = t >> 5;
             }
         }
         n_evac_new += __popcll(__ballot(exw));
@@ -2188,6 +2252,11 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
         }
     }
     wave_sync();  // the person words of the movers and the rmap bits complete
+    if constexpr (!BIGG) {
+        if (any_cont) {  // every contested bit this step set, cleared for the next step
+            for (int i = lane; i < g.RW; i += 64) cbits[i] = 0u;
+        }
+    }
     EVX_STAMP(4);
 
     // ---------------------------------- fire update (both fire models)
@@ -2255,7 +2324,12 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     for (int k = 0; k < GQ; k++) load_pw(64 * k + lane, nxj[k], nxw[k], nxhv[k]);
     // People.rmap back to HBM only now: stores issued before those loads would hold their waits
     // (vmcnt counts loads and stores in issue order)
-    for (int i = lane; i < g.RW; i += 64) st.rmap[(size_t)e * g.RW + i] = rmapb[i];
+    if (rm_dirty) {  // the words a winner changed (repeats store the same final value)
+        if (dw0 >= 0) st.rmap[(size_t)e * g.RW + dw0] = rmapb[dw0];
+        if (dw1 >= 0 && dw1 != dw0) st.rmap[(size_t)e * g.RW + dw1] = rmapb[dw1];
+    } else {
+        for (int i = lane; i < g.RW; i += 64) st.rmap[(size_t)e * g.RW + i] = rmapb[i];
+    }
     const int NITR = (nrl + 64 * GQ - 1) / (64 * GQ);
     for (int it = 0; it < NITR; it++) {
         PT_BEGIN(rtop);
@@ -2457,6 +2531,11 @@ __device__ __forceinline__ void reset_one(const evx_layout& lay, const evx_state
     const int P = g.P, R = g.R;
     // fresh people: the light path's kept lists no longer describe this env
     if (lane == 0) st.scratch[(size_t)e * env_scratch_words(lay) + persist_offset(lay)] = 0u;
+    if constexpr (!BIGG) {  // the contested bitmap is zero between steps (a step clears what it sets)
+        const int RW = (((lay.L + 2) * (lay.W + 2)) + 31) / 32;
+        uint32_t* cb = st.scratch + (size_t)e * env_scratch_words(lay) + cbits_offset(lay);
+        for (int i = lane; i < RW; i += 64) cb[i] = 0u;
+    }
     const ResetLds S = reset_lds(g.G, P, BIGG);
     uint32_t* pyring = smem + S.pyring;
     const uint32_t* validb;

@@ -113,5 +113,11 @@ if os.environ.get("EVX_FCX_REPORT"):  # -DEVX_FCX build: first changed not-dead-
           f"unchanged envs {np.mean(fcx >= 0x7fffffff):.3f}; list length median {np.median(nnd):.0f}")
     for q in (0.1, 0.25, 0.5, 0.75):
         print(f"  P(frac >= {q}) = {np.mean(frac >= q):.3f}")
+# cycle share by planners per env-step (light envs: few planners; heavy: early in their episodes)
+npl = s[:, 11]
+print("cycle share by planners/env-step:")
+for lo, hi in [(0, 1), (1, 8), (8, 64), (64, 256), (256, 1024), (1024, 1 << 30)]:
+    m = (npl >= lo) & (npl < hi)
+    print(f"  [{lo:5d},{hi:10d}) envs {m.mean():6.1%}  cycles {tot[m].sum() / tot.sum():6.1%}  mean {tot[m].mean() if m.any() else 0:9.0f}")
 cnt = env.counts.view(E, 2).cpu().numpy()
 print("evacuated median", np.median(cnt[:, 0]), "dead median", np.median(cnt[:, 1]))
