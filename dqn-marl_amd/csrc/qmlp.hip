@@ -1310,9 +1310,17 @@ struct Bwd {
     const __bf16* w2tl;
     __bf16* dz2l;
     __bf16* dz1l;
-    float* p3;    // qbwd3 block partials [nb3][P3W]: dW3 [5][256], db2 [256], db3 [5]
+    float* p3;    // qbwd3 block partials [nb3][P3W]: dW3 [5][256], db2 [256], db3 [5], TD loss
     float* pz1;   // qdz1 column-sum partials [ndzx][512] (db1 = the centre column of dW1)
     int64_t gsP;  // grouped: floats between consecutive nets' partial regions
+    // TD step inside qbwd3 (td != 0; else dq is given): DQNAgent.learn's target and MSE
+    // (agents/dqn_agent.py:143-151) per row from Q, Qt, act, rew, done (and importance weights w)
+    int td;
+    const float *Q, *Qt, *rew, *w;
+    const int32_t* act;
+    const uint8_t* done;
+    float gamma;
+    float* td_abs;
 };
 // net g's view of a blocked grouped backward (see fwd_net; x3: two planes per activation)
 __device__ __forceinline__ Bwd bwd_net(const Bwd& a0, int g) {
@@ -1347,7 +1355,8 @@ __device__ __forceinline__ Bwd bwd_net(const Bwd& a0, int g) {
 // differ between same-seed runs at the ulp level).
 // Small batches take rb = 64 or 32 rows per block (qbwd3_rows: B = 4096 had 32 blocks).
 constexpr int R3 = 128, R3C = 32;
-constexpr int P3W = NACT * HID2 + HID2 + 8;  // dW3 [5][256] | db2 [256] | db3 [5] (+ pad)
+constexpr int P3W = NACT * HID2 + HID2 + 8;  // dW3 [5][256] | db2 [256] | db3 [5] | TD loss (+ pad)
+constexpr int P3G = NACT * HID2 + HID2 + NACT;  // gradient columns of a p3 row; column P3G: the TD loss
 inline int qbwd3_rows(int B) { return B >= 16384 ? 128 : B >= 8192 ? 64 : 32; }
 template <bool X3 = false, bool GR = false>  // GR: blockIdx.y = net
 __global__ __launch_bounds__(256) void qbwd3_kernel(Bwd a0, int rb) {
@@ -1355,12 +1364,45 @@ __global__ __launch_bounds__(256) void qbwd3_kernel(Bwd a0, int rb) {
     if constexpr (GR) ag = bwd_net(a0, (int)blockIdx.y);
     const Bwd& a = GR ? ag : a0;
     __shared__ float dqs[R3][NACT];
+    __shared__ float lred[R3];
     const int n = threadIdx.x, b0 = blockIdx.x * rb;
-    for (int i = n; i < rb * NACT; i += 256) {
-        const int r = i / NACT;
-        dqs[r][i - r * NACT] = b0 + r < a.B ? a.dq[(size_t)(b0 + r) * NACT + (i - r * NACT)] : 0.f;
+    if (a.td) {  // thread n < rb: row b0 + n's TD error -> its dQ row and squared error (the mean over B)
+        if (n < rb) {
+            const int i = b0 + n;
+            float part = 0.f;
+            float dq[NACT];
+#pragma unroll
+            for (int t = 0; t < NACT; t++) dq[t] = 0.f;
+            if (i < a.B) {
+                float mx = a.Qt[(size_t)i * NACT];
+#pragma unroll
+                for (int j = 1; j < NACT; j++) mx = fmaxf(mx, a.Qt[(size_t)i * NACT + j]);
+                const float y = a.rew[i] + a.gamma * mx * (a.done[i] ? 0.f : 1.f);
+                const int ai = a.act[i];
+                const float d = a.Q[(size_t)i * NACT + ai] - y;
+                const float wi = a.w ? a.w[i] : 1.f;
+                part = a.w ? wi * (d * d) : d * d;
+                const float gd = a.w ? wi * (2.f * d) : 2.f * d;
+#pragma unroll
+                for (int t = 0; t < NACT; t++) dq[t] = t == ai ? gd / (float)a.B : 0.f;
+                if (a.td_abs) a.td_abs[i] = fabsf(d);
+            }
+#pragma unroll
+            for (int t = 0; t < NACT; t++) dqs[n][t] = dq[t];
+            lred[n] = part;
+        }
+    } else {
+        for (int i = n; i < rb * NACT; i += 256) {
+            const int r = i / NACT;
+            dqs[r][i - r * NACT] = b0 + r < a.B ? a.dq[(size_t)(b0 + r) * NACT + (i - r * NACT)] : 0.f;
+        }
     }
     __syncthreads();
+    if (a.td && n == 0) {  // the block's squared errors in row order
+        float l = 0.f;
+        for (int r = 0; r < rb; r++) l += lred[r];
+        a.p3[(size_t)blockIdx.x * P3W + P3G] = l;
+    }
     float w3[NACT], gw[NACT], gb2 = 0.f;
 #pragma unroll
     for (int t = 0; t < NACT; t++) {
@@ -1759,10 +1801,14 @@ struct Red2 {
     int nb3;
     const float* pz1;    // qdz1's column-sum partials [nz1][HID]
     int nz1;
+    int acc;             // 1: the sums are added to the gradients; 0: they overwrite them (and W1's
+                         // columns of constant inputs -- channel 0, channel 5 off the centre -- are zeroed)
+    float* loss;         // qbwd3's TD step: loss[0] = the block partials' sum / B, or NULL
+    int B;
 };
 // the small sums (dW3, db2, db3 from p3; db1 and W1's centre column from pz1): 64 columns per
 // workgroup, the partial rows in four contiguous quarters (one per wave), quarters added in order
-constexpr int P3L = NACT * HID2 + HID2 + NACT;  // live columns of a p3 row
+constexpr int P3L = NACT * HID2 + HID2 + NACT + 1;  // live columns of a p3 row (the gradients, the TD loss)
 constexpr int NRS3 = (P3L + 63) / 64, NRSZ = HID / 64, NRSMALL = NRS3 + NRSZ;
 __device__ __forceinline__ float red_sum256(float x, float* red) {
     red[threadIdx.x] = x;
@@ -1785,6 +1831,7 @@ __global__ __launch_bounds__(256) void reduce2_kernel(Red2 r0) {
         r.ss = adv(r.ss, G * gridDim.x);
         r.p3 += G * r.gsP;
         r.pz1 += G * r.gsP;
+        r.loss = adv(r.loss, G);
     }
     const int b = (int)blockIdx.x;
     float sq = 0.f;
@@ -1800,7 +1847,7 @@ __global__ __launch_bounds__(256) void reduce2_kernel(Red2 r0) {
                 acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
             }
             float* dst = r.gw2 + (size_t)m * HID + n;
-            const float4 old = *reinterpret_cast<const float4*>(dst);
+            const float4 old = r.acc ? *reinterpret_cast<const float4*>(dst) : make_float4(0.f, 0.f, 0.f, 0.f);
             const float4 o = make_float4(old.x + acc.x, old.y + acc.y, old.z + acc.z, old.w + acc.w);
             *reinterpret_cast<float4*>(dst) = o;
             sq = o.x * o.x + o.y * o.y + o.z * o.z + o.w * o.w;
@@ -1828,9 +1875,14 @@ __global__ __launch_bounds__(256) void reduce2_kernel(Red2 r0) {
 #pragma unroll
             for (int t = 0; t < 4; t++) {
                 float* dst = r.gw1 + (size_t)m * K1 + ref_col(n + t);
-                const float o = *dst + a4[t];
+                const float o = (r.acc ? *dst : 0.f) + a4[t];
                 *dst = o;
                 sq += o * o;
+            }
+            if (!r.acc) {  // the cell's constant-input columns: channel 0 (always 0), channel 5 off the centre
+                float* row = r.gw1 + (size_t)m * K1 + (n >> 2) * 6;
+                row[0] = 0.f;
+                if ((n >> 2) * 6 + 5 != CENTRE_COL) row[5] = 0.f;
             }
         }
     } else {  // the small gradients from qbwd3's / qdz1's partial rows
@@ -1850,16 +1902,18 @@ __global__ __launch_bounds__(256) void reduce2_kernel(Red2 r0) {
         if (qw == 0 && col < ncol) {
             const float tot = (red[c] + red[64 + c]) + (red[128 + c] + red[192 + c]);
             if (z1) {
-                const float o = r.gb1[col] + tot;
+                const float o = (r.acc ? r.gb1[col] : 0.f) + tot;
                 float* cc = r.gw1 + (size_t)col * K1 + CENTRE_COL;  // d/dW1 of the constant centre input
-                const float oc = *cc + tot;
+                const float oc = (r.acc ? *cc : 0.f) + tot;
                 r.gb1[col] = o;
                 *cc = oc;
                 sq = o * o + oc * oc;
+            } else if (col == P3G) {  // the TD loss (qbwd3's TD step)
+                if (r.loss) r.loss[0] = tot / (float)r.B;
             } else {
-                float* dst = col < NACT * HID2 ? r.gw3 + col : col < P3L - NACT ? r.gb2 + (col - NACT * HID2)
-                                                                                 : r.gb3 + (col - (P3L - NACT));
-                const float o = *dst + tot;
+                float* dst = col < NACT * HID2 ? r.gw3 + col : col < P3G - NACT ? r.gb2 + (col - NACT * HID2)
+                                                                                 : r.gb3 + (col - (P3G - NACT));
+                const float o = (r.acc ? *dst : 0.f) + tot;
                 *dst = o;
                 sq = o * o;
             }
@@ -1981,16 +2035,6 @@ __global__ __launch_bounds__(256) void sumsq_parts_kernel(const float* __restric
     for (int i = (int)blockIdx.x * 256 + (int)threadIdx.x; i < NPAR; i += (int)gridDim.x * 256) sq += g[i] * g[i];
     const float t = red_sum256(sq, red);
     if (threadIdx.x == 0) ss[blockIdx.x] = t;
-}
-
-struct Zero6 {
-    float* p[6];
-    int64_t n[6];
-};
-__global__ __launch_bounds__(256) void zero_kernel(Zero6 z) {
-    float* p = z.p[blockIdx.y];
-    const int64_t n = z.n[blockIdx.y];
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) p[i] = 0.f;
 }
 
 }  // namespace evxm
@@ -2336,7 +2380,7 @@ extern "C++" {
 // (reduce2): all sums in a fixed order
 template <bool X3, int AP2, int BP2, int AP1, int BP1>
 static void launch_tail(const evxm::Bwd& a, int32_t B, const evx_qmlp_grads* g, float* ss, hipStream_t st,
-                        int nets = 1) {
+                        int nets, int acc, float* loss) {
     // dW2 = dZ2^T H1 (256 x 512); dW1 = dZ1^T X (512 x compact K -> 726); K = B split into S tiles
     evxm::GemmTN g2{a.dz2, evxm::HID2, a.h1, evxm::HID, B, evxm::HID2, evxm::HID, dw2_kper(B), g->w2, evxm::HID, 0,
                     g->part, X3 ? a.dz2l : nullptr, X3 ? a.h1l : nullptr, evxm::HID / evxm::TT, evxm::HID2 / evxm::TT, 0};
@@ -2351,7 +2395,7 @@ static void launch_tail(const evxm::Bwd& a, int32_t B, const evx_qmlp_grads* g, 
     evxm::Red2 r{g->part, g2.gz, g1.part, g1.gz, g1.gx * evxm::TT, 4 * evxm::NCELL, X3 ? 3 : 1,
                  g->w1, g->b1, g->w2, g->b2, g->w3, g->b3, ss,
                  (evxm::HID2 * evxm::HID / 4 + 255) / 256, (evxm::HID * evxm::NCELL + 255) / 256, 0,
-                 a.p3, qbwd3_blocks(B), a.pz1, ndzx};
+                 a.p3, qbwd3_blocks(B), a.pz1, ndzx, acc, loss, B};
     constexpr int lds = std::max(evxm::qdz1_lds_bytes<X3>(), evxm::gemm_tn_lds_bytes<AP2, BP2>());
     const unsigned nmid = (unsigned)(ndzx * (evxm::HID / 128) + g2.gx * g2.gy * g2.gz);
     if (nets > 1) {  // grouped (x3): net g's operands, gradients and partials (fwd_net / bwd_net)
@@ -2389,10 +2433,23 @@ static void launch_tail(const evxm::Bwd& a, int32_t B, const evx_qmlp_grads* g, 
 }
 }  // extern "C++"
 
+// td: the TD step runs inside qbwd3 (dq unused; the loss from reduce2), or NULL (dq given).
+// zero_grads != 0: the reductions overwrite the gradients (every element: W1's constant-input
+// columns are written as zeros), else they add to them.
+struct TdIn {
+    const float *Q, *Qt, *rew, *w;
+    const int32_t* act;
+    const uint8_t* done;
+    float gamma;
+    float *loss, *td_abs;
+};
 static int qmlp_backward(const evx_qmlp_params* p, int32_t B, const float* dq, const uint16_t* x, const uint16_t* h1,
                          const float* h2, float drop_p, uint16_t* dz2, uint16_t* dz1, const evx_qmlp_grads* g,
-                         int32_t zero_grads, float* ss, void* stream, int nets = 1) {
-    if (!p || !g || !dq || !x || !h1 || !h2 || !dz2 || !dz1) return mfail(-22, "qmlp_backward: NULL argument");
+                         int32_t zero_grads, float* ss, void* stream, int nets = 1, const TdIn* td = nullptr) {
+    if (!p || !g || !(dq || td) || !x || !h1 || !h2 || !dz2 || !dz1) return mfail(-22, "qmlp_backward: NULL argument");
+    if (td && (!td->Q || !td->Qt || !td->act || !td->rew || !td->done || !td->loss))
+        return mfail(-22, "qmlp_td_backward: NULL TD argument");
+    if (td && nets > 1) return mfail(-22, "qmlp_td_backward: one net");
     if (!p->w2t || !p->w3) return mfail(-22, "qmlp_backward: w2t / w3 required");
     if (!g->w1 || !g->b1 || !g->w2 || !g->b2 || !g->w3 || !g->b3) return mfail(-22, "qmlp_backward: missing grad");
     if (ss && (g->b1 != g->w1 + evxm::OB1 || g->w2 != g->w1 + evxm::OW2 || g->b2 != g->w1 + evxm::OB2 ||
@@ -2402,12 +2459,7 @@ static int qmlp_backward(const evx_qmlp_params* p, int32_t B, const float* dq, c
     if (B <= 0) return 0;
     hipStream_t st = (hipStream_t)stream;
     const int rb3 = evxm::qbwd3_rows(B);
-    if (zero_grads) {
-        evxm::Zero6 z = {{g->w1, g->b1, g->w2, g->b2, g->w3, g->b3},
-                         {(int64_t)evxm::HID * evxm::K1, evxm::HID, (int64_t)evxm::HID2 * evxm::HID, evxm::HID2,
-                          (int64_t)evxm::NACT * evxm::HID2, evxm::NACT}};
-        hipLaunchKernelGGL(evxm::zero_kernel, dim3(256, 6), dim3(256), 0, st, z);
-    }
+    const int acc = zero_grads ? 0 : 1;
     evxm::Bwd a;
     a.B = B;
     a.dq = dq;
@@ -2431,6 +2483,16 @@ static int qmlp_backward(const evx_qmlp_params* p, int32_t B, const float* dq, c
     a.p3 = g->part + part_p3_off(B);
     a.pz1 = g->part + part_pz1_off(B);
     a.gsP = evx_qmlp_backward_part_floats(B);
+    a.td = td != nullptr;
+    a.Q = td ? td->Q : nullptr;
+    a.Qt = td ? td->Qt : nullptr;
+    a.rew = td ? td->rew : nullptr;
+    a.w = td ? td->w : nullptr;
+    a.act = td ? td->act : nullptr;
+    a.done = td ? td->done : nullptr;
+    a.gamma = td ? td->gamma : 0.f;
+    a.td_abs = td ? td->td_abs : nullptr;
+    float* loss = td ? td->loss : nullptr;
     if (p->x3) {
         if (!p->w2tl) return mfail(-22, "qmlp_backward: x3 needs w2tl (evx_qmlp_pack3)");
         a.h1l = a.h1 + (size_t)B * evxm::HID;  // lo planes after the hi planes
@@ -2440,18 +2502,26 @@ static int qmlp_backward(const evx_qmlp_params* p, int32_t B, const float* dq, c
         if (nets > 1) {
             hipLaunchKernelGGL((evxm::qbwd3_kernel<true, true>), dim3((unsigned)((B + rb3 - 1) / rb3), nets),
                                dim3(256), 0, st, a, rb3);
-            launch_tail<true, 2, 2, 2, 1>(a, B, g, ss, st, nets);
+            launch_tail<true, 2, 2, 2, 1>(a, B, g, ss, st, nets, acc, nullptr);
             return mlaunch("qmlp_backward grouped");
         }
         hipLaunchKernelGGL(evxm::qbwd3_kernel<true>, dim3((unsigned)((B + rb3 - 1) / rb3)), dim3(256), 0, st, a, rb3);
         // dW2: both operands split; dW1 over the 640 x3 columns (X exact in bf16): the danger
         // residual column of a cell adds into its danger column
-        launch_tail<true, 2, 2, 2, 1>(a, B, g, ss, st);
+        launch_tail<true, 2, 2, 2, 1>(a, B, g, ss, st, 1, acc, loss);
         return mlaunch("qmlp_backward");
     }
     hipLaunchKernelGGL(evxm::qbwd3_kernel<false>, dim3((unsigned)((B + rb3 - 1) / rb3)), dim3(256), 0, st, a, rb3);
-    launch_tail<false, 1, 1, 1, 1>(a, B, g, ss, st);
+    launch_tail<false, 1, 1, 1, 1>(a, B, g, ss, st, 1, acc, loss);
     return mlaunch("qmlp_backward");
+}
+
+int evx_qmlp_td_backward_ss(const evx_qmlp_params* p, int32_t B, const float* Q, const float* Qt, const int32_t* act,
+                            const float* rew, const uint8_t* done, float gamma, const float* w, float* loss,
+                            float* td_abs, const uint16_t* x, const uint16_t* h1, const float* h2, float drop_p,
+                            uint16_t* dz2, uint16_t* dz1, const evx_qmlp_grads* g, float* ss, void* stream) {
+    const TdIn td{Q, Qt, rew, w, act, done, gamma, loss, td_abs};
+    return qmlp_backward(p, B, nullptr, x, h1, h2, drop_p, dz2, dz1, g, 1, ss, stream, 1, &td);
 }
 
 int evx_qmlp_backward(const evx_qmlp_params* p, int32_t B, const float* dq, const uint16_t* x, const uint16_t* h1,

@@ -74,6 +74,9 @@ def mlib():
         L.evx_qmlp_backward_ss.argtypes = [C.POINTER(evx_qmlp_params), C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
                                            C.c_void_p, C.c_float, C.c_void_p, C.c_void_p, C.POINTER(evx_qmlp_grads),
                                            C.c_int32, C.c_void_p, C.c_void_p]
+        L.evx_qmlp_td_backward_ss.argtypes = [C.POINTER(evx_qmlp_params), C.c_int32] + [C.c_void_p] * 5 + \
+            [C.c_float] + [C.c_void_p] * 6 + [C.c_float, C.c_void_p, C.c_void_p, C.POINTER(evx_qmlp_grads),
+                                              C.c_void_p, C.c_void_p]
         L.evx_qmlp_norm_parts.restype = C.c_int32
         L.evx_qmlp_nparams.restype = C.c_int64
         L.evx_qmlp_sumsq_parts.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
@@ -310,6 +313,35 @@ class MLPFast:
                                         obs1.data_ptr(), C.byref(net1.c), C.byref(d1), C.byref(o1), _stream()),
                "qmlp_forward2")
 
+    def _grads(self, B, grads):
+        g = evx_qmlp_grads(**{k: grads[f"fc{k[1]}.{'weight' if k[0] == 'w' else 'bias'}"].data_ptr()
+                              for k in ["w1", "b1", "w2", "b2", "w3", "b3"]})
+        # every gradient sum through partials added in a fixed order (the same bits on every run)
+        nf = int(mlib().evx_qmlp_backward_part_floats(B))
+        if self._part is None or self._part.numel() < nf:
+            self._part = torch.empty(nf, dtype=torch.float32, device=self.device)
+        g.part = self._part.data_ptr()
+        return g
+
+    def td_backward(self, B: int, Q, Qt, act, rew, done, gamma: float, loss, x, h1, h2, drop_p: float, dz2, dz1, grads,
+                    weights=None, td_abs=None, ss: Optional[torch.Tensor] = None):
+        """DQNAgent.learn's TD step + loss.backward() in one (evx_qmlp_td_backward_ss): loss[0] = the
+        mean squared TD error, the gradients overwritten; ss (or None) as backward's."""
+        pl = self.planes
+        for name, t, n in [("x", x, B * self.kx), ("h1", h1, pl * B * HID), ("dz1", dz1, pl * B * HID),
+                           ("dz2", dz2, pl * B * HID2), ("h2", h2, B * HID2), ("Q", Q, B * NACT), ("Qt", Qt, B * NACT),
+                           ("act", act, B), ("rew", rew, B), ("done", done, B)]:
+            if t.numel() < n:
+                raise ValueError(f"qmlp td_backward: {name} has {t.numel()} elements, needs {n}")
+        if ss is not None:
+            _need("td_backward ss", ss, 1, int(mlib().evx_qmlp_norm_parts()))
+        g = self._grads(B, grads)
+        mcheck(mlib().evx_qmlp_td_backward_ss(C.byref(self.c), B, Q.data_ptr(), Qt.data_ptr(), act.data_ptr(),
+                                              rew.data_ptr(), done.data_ptr(), float(gamma), _p(weights),
+                                              loss.data_ptr(), _p(td_abs), x.data_ptr(), h1.data_ptr(), h2.data_ptr(),
+                                              float(drop_p), dz2.data_ptr(), dz1.data_ptr(), C.byref(g), _p(ss),
+                                              _stream()), "qmlp_td_backward_ss")
+
     def backward(self, B: int, dq: torch.Tensor, x: torch.Tensor, h1: torch.Tensor, h2: torch.Tensor, drop_p: float,
                  dz2: torch.Tensor, dz1: torch.Tensor, grads, zero=True, ss: Optional[torch.Tensor] = None):
         """d loss / d params of the saved forward into `grads` (evacx.qnet.FlatParams).
@@ -321,13 +353,7 @@ class MLPFast:
                            ("dz2", dz2, pl * B * HID2), ("h2", h2, B * HID2), ("dq", dq, B * NACT)]:
             if t.numel() < n:
                 raise ValueError(f"qmlp backward: {name} has {t.numel()} elements, needs {n}")
-        g = evx_qmlp_grads(**{k: grads[f"fc{k[1]}.{'weight' if k[0] == 'w' else 'bias'}"].data_ptr()
-                              for k in ["w1", "b1", "w2", "b2", "w3", "b3"]})
-        # every gradient sum through partials added in a fixed order (the same bits on every run)
-        nf = int(mlib().evx_qmlp_backward_part_floats(B))
-        if self._part is None or self._part.numel() < nf:
-            self._part = torch.empty(nf, dtype=torch.float32, device=self.device)
-        g.part = self._part.data_ptr()
+        g = self._grads(B, grads)
         if ss is not None:
             _need("backward ss", ss, 1, int(mlib().evx_qmlp_norm_parts()))
             mcheck(mlib().evx_qmlp_backward_ss(C.byref(self.c), B, dq.data_ptr(), x.data_ptr(), h1.data_ptr(),

@@ -16,7 +16,6 @@ gradient all-reduce is one collective. Every contraction runs in evx_gemm
 from __future__ import annotations
 
 import ctypes as C
-import os
 from collections import OrderedDict
 from typing import Dict, List, Optional, Tuple
 
@@ -241,8 +240,8 @@ class QNet:
     def __init__(self, kind: str, params: FlatParams, precision="f32", hidden=512, actions=5):
         self.kind, self.P, self.prec = kind, params, precision
         self.hidden, self.actions = hidden, actions
-        # x3 conv layers as implicit GEMMs (EVX_CONV_IM2COL=1: im2col + GEMM, for A/B checks)
-        self.implicit = kind == "conv" and precision == "x3" and os.environ.get("EVX_CONV_IM2COL", "0") != "1"
+        # x3 conv layers as implicit GEMMs (the exact-f32 path keeps im2col + GEMM)
+        self.implicit = kind == "conv" and precision == "x3"
         self.device = params.flat.device
         self.ws = _Workspace()
         self.saved = None
@@ -413,10 +412,10 @@ class Learner:
             self.fast = MLPFast(self.online, self.device, x3=precision != "bf16")
             self.fast_t = MLPFast(self.target, self.device, x3=precision != "bf16")
         self.drop_stream = 0
-        # x3 MLP: TD + gradient clear in one launch, the norm partials out of the backward's
-        # reductions, clip + Adam + operand repack in one launch (EVX_FUSED_OPT=0: the separate
-        # td_loss / zero / sumsq / clip_adam / pack3 launches)
-        self.fused_opt = self.fast is not None and self.fast.x3 and os.environ.get("EVX_FUSED_OPT", "1") != "0"
+        # x3 MLP: the TD step inside the backward, the norm partials out of its reductions, clip +
+        # Adam + operand repack in one launch (fused_opt = False: the separate td_loss / backward /
+        # sumsq / clip_adam / pack3 launches -- tests compare the two)
+        self.fused_opt = self.fast is not None and self.fast.x3
         if self.fused_opt:
             from .qmlp import mlib
             assert self.online.numel == int(mlib().evx_qmlp_nparams()), "MLP parameter count"
@@ -491,14 +490,11 @@ class Learner:
                                      s2_obs, d_tg, dict(h1=H1t, q=Qt))
         L = qlib()
         if self.fused_opt:
-            # the TD launch also clears the gradients; the backward leaves the norm partials
-            # (its weight-gradient reductions compute them) unless an all-reduce will change the gradients
-            g = self.grads.flat
-            qcheck(L.evx_td_loss_zero(_p(Q), _p(Qt), self.actions, _p(a), _p(r), _p(done), self.gamma, B,
-                                      _p(weights), _p(dQ), _p(self.loss), _p(td_abs), _p(g), g.numel(), _stream()),
-                   "td_loss_zero")
-            self.fast.backward(B, dQ, X, H1, H2, DROPOUT_P, dz2, dz1, self.grads, zero=False,
-                               ss=self._ss if self.grad_hook is None else None)
+            # the TD step inside the backward's first kernel, the gradients overwritten by its ordered
+            # reductions, which also leave the norm partials unless an all-reduce will change the gradients
+            self.fast.td_backward(B, Q, Qt, a, r, done, self.gamma, self.loss, X, H1, H2, DROPOUT_P, dz2, dz1,
+                                  self.grads, weights=weights, td_abs=td_abs,
+                                  ss=self._ss if self.grad_hook is None else None)
             self._ss_fresh = self.grad_hook is None
         else:
             qcheck(L.evx_td_loss_w(_p(Q), _p(Qt), self.actions, _p(a), _p(r), _p(done), self.gamma, B, _p(weights),

@@ -447,16 +447,16 @@ int evx_qmlp_forward2(const evx_layout *lay, int32_t n, const evx_obs *obs0, con
 /* fp32 gradient tensors (the reference's parameter shapes: fc1.weight [512][726], ...) */
 typedef struct {
     float *w1, *b1, *w2, *b2, *w3, *b3;
-    /* optional split-K scratch of the weight-gradient GEMMs, evx_qmlp_backward_part_floats(B)
-     * floats: the splits are summed in a fixed order (deterministic gradients, no f32 atomics);
-     * NULL = atomics */
+    /* required scratch of the backward's partial sums, evx_qmlp_backward_part_floats(B) floats
+     * (weight-gradient split-K tiles, fc3 / bias block rows): every gradient sum is added in a
+     * fixed order -- the same bits on every run, no f32 atomics */
     float *part;
 } evx_qmlp_grads;
 int64_t evx_qmlp_backward_part_floats(int32_t B);
 
 /* loss.backward() of DQNAgent.learn (agents/dqn_agent.py:150-158) for the saved online
- * forward (x, h1, h2 of evx_qmlp_forward) given dQ = d loss / d Q [B][5]. Gradients are
- * accumulated with atomics (zero_grads = 1 clears them first). dz2 [B][256] and dz1
+ * forward (x, h1, h2 of evx_qmlp_forward) given dQ = d loss / d Q [B][5]. zero_grads != 0: the
+ * gradients are overwritten (every element), else added to. dz2 [B][256] and dz1
  * [B][512] are bf16 scratch. Needs p->w2t. With p->x3 the activations are the x3 forward's
  * (h1 two planes, x 640 wide), dz2 / dz1 hold two planes each (hi, lo) and every product
  * is split as in the forward. */
@@ -469,6 +469,15 @@ int evx_qmlp_backward(const evx_qmlp_params *p, int32_t B, const float *dq, cons
 int evx_qmlp_backward_ss(const evx_qmlp_params *p, int32_t B, const float *dq, const uint16_t *x, const uint16_t *h1,
                          const float *h2, float drop_p, uint16_t *dz2, uint16_t *dz1, const evx_qmlp_grads *g,
                          int32_t zero_grads, float *ss, void *stream);
+/* DQNAgent.learn's TD step and loss.backward() in one (agents/dqn_agent.py:143-158): dQ from the
+ * online Q [B][5], the target Qt [B][5], actions, rewards, done flags and gamma (as evx_td_loss_w,
+ * importance weights w or NULL) inside the backward's first kernel; loss[0] = the mean (weighted)
+ * squared TD error, td_abs [B] = |TD error| (or NULL); the gradients overwritten; ss as in
+ * evx_qmlp_backward_ss, or NULL (no norm partials: an all-reduce will change the gradients). */
+int evx_qmlp_td_backward_ss(const evx_qmlp_params *p, int32_t B, const float *Q, const float *Qt, const int32_t *act,
+                            const float *rew, const uint8_t *done, float gamma, const float *w, float *loss,
+                            float *td_abs, const uint16_t *x, const uint16_t *h1, const float *h2, float drop_p,
+                            uint16_t *dz2, uint16_t *dz1, const evx_qmlp_grads *g, float *ss, void *stream);
 int32_t evx_qmlp_norm_parts(void);
 int64_t evx_qmlp_nparams(void);
 /* the same partials of a flat gradient buffer (after an all-reduce changed it) */
