@@ -1550,6 +1550,14 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
         if (!kept && p < P) vv[j] = pk_g[p];
         if constexpr (!WIDE) hr[j] = !kept && p < P ? h_g[p] : 0.0;
     }
+    // kept lists: the rows' first in-play entries, in flight with the state loads (read past the
+    // list's end only within the buffer; entries >= nip are dropped below)
+    uint2 pre_e[2 * GQ];
+#pragma unroll
+    for (int j = 0; j < 2 * GQ; j++) {
+        pre_e[j] = make_uint2(0u, DONEPK);
+        if (!WIDE && kept && 64 * j + lane < P) pre_e[j] = ipl[64 * j + lane];
+    }
     const uint32_t* grm = st.rmap + (size_t)e * g.RW;
     for (int i0 = 0; i0 < g.RW; i0 += 16 * 64) {
         uint32_t w[16];
@@ -1716,6 +1724,12 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     PT_DECL(sbt);
     double total = 0.0;  // CPython sum(p.health for p in self.people.list if not p.dead): sequential
     int fold_kept = 0;   // light path: entries of the kept list-order healths after this step
+    // a light step whose planners were scored in one batch keeps its move plan in registers (lane k:
+    // the batch's planner k, its target's cell info loaded at scoring time): no plan round trip
+    uint2 rp_en = make_uint2(0u, 0u);
+    uint32_t rp_ci = 0u;
+    bool rp_mov = false;
+    int nbatch = 0;
     if constexpr (WIDE) {
         WideCtl* ctl = reinterpret_cast<WideCtl*>(smem + wide_lds(lay).ctl);
         if (lane == 0) {
@@ -1743,7 +1757,8 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     int* qc = reinterpret_cast<int*>(aux + 256);        // first Python-stream word
     int qn = 0;
     int nal = 0;  // alive persons in play so far (see nrl)
-    auto score_batch = [&](int n) {  // People.find_best_direction for queue entries [0, n)
+    auto score_batch = [&](int n, bool only) {  // People.find_best_direction for queue entries [0, n)
+        // (only: the step's one batch -- its plan stays in registers, not in HBM)
         PT_BEGIN(sbl);
         const bool has = lane < n;
         uint32_t ea = 0, eb = 0;
@@ -1777,15 +1792,19 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
         PT_BEGIN(sbt);
         const bool mover = best != NODIR;
         const unsigned long long mm = __ballot(mover);
+        nbatch++;
+        rp_mov = mover;
         if (mover) {
             const int t = cold + doff_of(best, GY);
+            rp_en = make_uint2((uint32_t)p, (uint32_t)cold | (best << 24));
+            rp_ci = lay.cellinfo[t];
             const uint32_t bit = 1u << (t & 31);
             const uint32_t old = atomicOr(&tbits[t >> 5], bit);
             if (old & bit) {
                 atomicOr(&cbits[t >> 5], bit);
                 any_cont = true;
             }
-            plan[nplan + lanes_below(mm)] = make_uint2((uint32_t)p, (uint32_t)cold | (best << 24));
+            if (!only) plan[nplan + lanes_below(mm)] = make_uint2((uint32_t)p, (uint32_t)cold | (best << 24));
         }
         nplan += __popcll(mm);
         PT_END(sbt);
@@ -1901,8 +1920,13 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     uint32_t nxv[GQ];
 #pragma unroll
     for (int k = 0; k < GQ; k++) {
-        nxe[k] = load_entry(64 * k + lane);
-        nne[k] = load_entry(64 * (GQ + k) + lane);
+        if (kept) {  // loaded with the state
+            nxe[k] = 64 * k + lane < nip ? pre_e[k] : NOONE;
+            nne[k] = 64 * (GQ + k) + lane < nip ? pre_e[GQ + k] : NOONE;
+        } else {
+            nxe[k] = load_entry(64 * k + lane);
+            nne[k] = load_entry(64 * (GQ + k) + lane);
+        }
     }
 #pragma unroll
     for (int k = 0; k < GQ; k++) load_data(64 * k + lane, nxe[k], nxh[k], nxa[k], nxg[k], nxv[k]);
@@ -1954,7 +1978,7 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
             while (qn >= 64 || (fin && qn > 0)) {
                 const int n = min(qn, 64);
                 wave_fence();
-                score_batch(n);
+                score_batch(n, fin && nbatch == 0 && qn <= 64);
                 const int rest = qn - n;  // move entries [n, qn) to the front (rest <= 63)
                 uint32_t ta = 0, tb = 0;
                 int tc = 0;
@@ -2062,8 +2086,14 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     }
     EVX_STAMP(2);
 
-    // The move plan in HBM is walked 4 x 64 entries at a time, loads first.
+    // The move plan in HBM is walked 4 x 64 entries at a time, loads first (or, one batch, from
+    // the registers its scoring left: lane k's entry is valid iff it moves).
+    const bool preg = !WIDE && nbatch <= 1;
     auto plan_pass = [&](auto&& fn) {
+        if (preg) {
+            fn(rp_en, rp_mov);
+            return;
+        }
         for (int i0 = 0; i0 < nplan; i0 += 256) {
             uint2 en[4];
 #pragma unroll
@@ -2130,7 +2160,7 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     EVX_COUNT(12, py_head);
     // the Python stream is stored: its ring becomes the "vacated by a winner" bitmap
     for (int i = lane; i < g.RW; i += 64) vac[i] = 0;
-    wave_sync();
+    if constexpr (BIGG) wave_sync(); else wave_fence();  // LDS (big grids: global); the state stores drain later
     PT_END(mts);
     PT_STORE(lp, 24);
     PT_STORE(grp, 25);
@@ -2170,38 +2200,22 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
         }
     });
     if (lane == 0) misc[0] = 0;
-    wave_sync();
+    if constexpr (BIGG) wave_sync(); else wave_fence();  // vac: LDS (big grids: global)
     uint32_t* ev = aux;  // (cell, key) pairs; groups are done
     int n_evac_new = 0;
     // a step with <= 64 movers writes back only the rmap words its winners changed (cold, t)
     const bool rm_dirty = nplan <= 64;
     int dw0 = -1, dw1 = -1;
-    for (int i0 = 0; i0 < nplan; i0 += 256) {
-      uint2 en4[4];
-      uint32_t ci4[4];
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-          en4[j] = make_uint2(0u, 0u);
-          if (i0 + 64 * j + lane < nplan) en4[j] = plan[i0 + 64 * j + lane];
-      }
-#pragma unroll
-      for (int j = 0; j < 4; j++) {  // exit bits of the targets, all in flight
-          ci4[j] = 0u;
-          if (i0 + 64 * j + lane < nplan) ci4[j] = lay.cellinfo[(int)(en4[j].y & 0xffffffu) + doff_of(en4[j].y >> 24, GY)];
-      }
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const int i = i0 + 64 * j + lane;
+    auto exec_entry = [&](const uint2 en, const uint32_t ci, const bool valid) {
         bool exw = false;
-        if (i < nplan) {
-            const uint2 en = en4[j];
+        if (valid) {
             const int p = (int)en.x;
             const int cold = (int)(en.y & 0xffffffu);
             const int dd = (int)(en.y >> 24);
             const int t = cold + doff_of((uint32_t)dd, GY);
             const bool cont = any_cont && cb_get(t);
             if (!cont || !tc_get(lost, p)) {
-                const bool ex = (ci4[j] >> 1) & 1u;
+                const bool ex = (ci >> 1) & 1u;
                 exw = ex;
                 const bool ev_old = tc_get(tbits, cold), ev_new = tc_get(vac, t);
                 int pf = p;
@@ -2233,9 +2247,29 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
             }
         }
         n_evac_new += __popcll(__ballot(exw));
-      }
+    };
+    if (preg) {
+        exec_entry(rp_en, rp_ci, rp_mov);
+    } else {
+        for (int i0 = 0; i0 < nplan; i0 += 256) {
+            uint2 en4[4];
+            uint32_t ci4[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                en4[j] = make_uint2(0u, 0u);
+                if (i0 + 64 * j + lane < nplan) en4[j] = plan[i0 + 64 * j + lane];
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) {  // exit bits of the targets, all in flight
+                ci4[j] = 0u;
+                if (i0 + 64 * j + lane < nplan) ci4[j] = lay.cellinfo[(int)(en4[j].y & 0xffffffu) + doff_of(en4[j].y >> 24, GY)];
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) exec_entry(en4[j], ci4[j], i0 + 64 * j + lane < nplan);
+        }
     }
-    wave_sync();
+    // LDS hand-offs only (the person words are drained below); big grids' bitmaps are global
+    if constexpr (BIGG) wave_sync(); else wave_fence();
     {
         const int nev = (int)misc[0];
         if (nev > EV_CAP) err |= 16;
