@@ -3060,18 +3060,11 @@ static size_t step_launch_lds(const evx_layout& l, int nwb, bool bigg = false) {
 // plateau in the training step (cfg3 lagged 9.63 -> 10.07 M, strict 7.44 -> 7.75 M,
 // env-only 13.3 -> 13.9 M, cfg2 17.9 -> 18.3 M, cfg5 8.72 -> 8.88 M env-steps/s).
 static int heavy_cap(const evx_layout& l, int* hmin) {
-    static int cap_env = -2, min_env = -2;
-    if (cap_env == -2) {
-        const char* v = getenv("EVX_HEAVY_CAP");
-        cap_env = v ? atoi(v) : -1;
-        const char* m = getenv("EVX_HEAVY_MIN");
-        min_env = m ? atoi(m) : -1;
-    }
-    *hmin = std::max(1, min_env >= 0 ? min_env : l.P / 4);
+    *hmin = std::max(1, l.P / 4);
     if (evx::big_grid(l.L, l.W)) return 0;  // BIGG kernels: no heavy workgroups
     const evx::WideLds wl = evx::wide_lds(l);
     if (step_launch_lds(l, evx::WNW) > 160 * 1024 || wl.end > wl.ctl) return 0;
-    return cap_env >= 0 ? cap_env : 176;
+    return 176;
 }
 
 namespace {
@@ -3144,12 +3137,6 @@ int evx_env_step_part(const evx_layout* l, const evx_state* s, const int32_t* ac
         for (const void* k : ks) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_set = true;
     }
-    // envs per workgroup (one per wave): EVX_STEP_NWB overrides (diagnostics)
-    static int nwb_env = -1;
-    if (nwb_env < 0) {
-        const char* v = getenv("EVX_STEP_NWB");
-        nwb_env = v ? atoi(v) : 0;
-    }
     // Default: 4-wave workgroups with the heavy-env path while a launch is short enough for
     // its heaviest env to set its length (fewer than 32 envs per CU); one-wave workgroups
     // beyond, where throughput rules: a wave's VGPRs and LDS free the moment its env is done
@@ -3161,19 +3148,14 @@ int evx_env_step_part(const evx_layout* l, const evx_state* s, const int32_t* ac
             hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
             ncu = 256;
     }
-    int nwb = nwb_env == 1 || nwb_env == 2 || nwb_env == 4 ? nwb_env : (s->E >= 32 * ncu ? 1 : 4);
+    int nwb = s->E >= 32 * ncu ? 1 : 4;
     if (bigg && nwb > 2) nwb = 2;  // BIGG kernels: 1 or 2 envs per workgroup
     while (nwb > 1 && step_launch_lds(*l, nwb, bigg) > 160 * 1024) nwb >>= 1;
     int hmin = 0;
     const int hcap = (nwb == evx::WNW && s->order) ? heavy_cap(*l, &hmin) : 0;
-    // EVX_PRIO_SLOTS: single-wave envs at order slots < H + this run at raised priority
-    // (0 disables the priority raise, the heavy workgroups' included)
-    static int pslots_env = -2;
-    if (pslots_env == -2) {
-        const char* v = getenv("EVX_PRIO_SLOTS");
-        pslots_env = v ? atoi(v) : -1;
-    }
-    const int pslots = s->order ? (pslots_env >= 0 ? pslots_env : 0) : 0;
+    // single-wave envs at order slots < H + pslots could run at raised wave priority: 0 (a sweep
+    // of 0 / 1 / 256 / 768 / 1536 slots measured box noise in the training step)
+    const int pslots = 0;
     const size_t blds = step_launch_lds(*l, nwb, bigg);
     // heavy envs take a workgroup each; part 1: only those, part 2: only the rest
     if (part == 1 && hcap == 0) return 0;  // no heavy workgroups for this layout: part 2 steps every env

@@ -8,3 +8,4 @@ timeout -k 10 400 rocprofv3 --kernel-trace -d $OUT/t -o run --output-format csv 
     --no-cpu --other-steps 0 --env-steps 0 --start-steps 0 > $OUT/bench.json 2> $OUT/bench.err || { tail $OUT/bench.err; exit 1; }
 python3 -c "import json; d=json.load(open('$OUT/bench.json')); print('value', d['value']/1e6, 'ms', d['ms_per_step'], 'env', d['env_step_kernel_ms'], 'learn', d['learn_ms'])"
 python3 $R/tools/step_timeline.py $OUT/t ${2:-26}
+find $OUT/t -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv ;
