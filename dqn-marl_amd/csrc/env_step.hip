@@ -290,29 +290,39 @@ __device__ __forceinline__ void mt_store_w(uint32_t* ring, int& front, int head,
 // operand of a round loaded before any word of it is written -- never overwrites an unread
 // word). 400 words less LDS per env than a 1024-word ring.
 __device__ __forceinline__ int np_slot(int n) { return n - MT_N * (int)((uint32_t)n / (uint32_t)MT_N); }
+// slot s + d of a 624-slot ring for 0 <= s < 624, 0 <= d < 624 (no division)
+__device__ __forceinline__ int ring_add(int s, int d) { return s + d >= MT_N ? s + d - MT_N : s + d; }
+// One in-place round of the 624-slot ring: words [front, front + cnt) (cnt <= 227), the slot of
+// `front` given: word n's operands x[n - 624] (its own slot), x[n - 623] (the next), x[n - 227]
+// (397 on) all sit at fixed offsets from n's slot, read before any word of the round is written.
+__device__ __forceinline__ void ring_round(uint32_t* ring, int r0, int cnt) {
+    const int lane = (int)(threadIdx.x & 63);
+    uint32_t lag[4], a[4], b[4];
+    int sl[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        sl[j] = ring_add(r0, min(lane + 64 * j, MT_N - 1));
+        const int s1 = sl[j] + 1 == MT_N ? 0 : sl[j] + 1;
+        lag[j] = ring[ring_add(sl[j], MT_N - MT_LAG)];
+        a[j] = ring[sl[j]];
+        b[j] = ring[s1];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+        if (lane + 64 * j < cnt) ring[sl[j]] = mt_twist1(lag[j], a[j], b[j]);
+    wave_fence();
+}
 __device__ __forceinline__ void np_ensure(uint32_t* ring, int& front, int upto) {
     const int lane = (int)(threadIdx.x & 63);
     while (front < upto) {
         const int cnt = min(MT_LAG, upto - front);
-        uint32_t lag[4], a[4], b[4];
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int n = front + lane + 64 * j;
-            lag[j] = ring[np_slot(n - MT_LAG)];
-            a[j] = ring[np_slot(n - 624)];
-            b[j] = ring[np_slot(n - 623)];
-        }
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int n = front + lane + 64 * j;
-            if (lane + 64 * j < cnt) ring[np_slot(n)] = mt_twist1(lag[j], a[j], b[j]);
-        }
+        ring_round(ring, np_slot(front), cnt);
         front += cnt;
-        wave_fence();
     }
 }
 __device__ __forceinline__ double np_double(const uint32_t* ring, int idx) {
-    const uint32_t a = mt_temper(ring[np_slot(idx)]) >> 5, b = mt_temper(ring[np_slot(idx + 1)]) >> 6;
+    const int s0 = np_slot(idx), s1 = s0 + 1 == MT_N ? 0 : s0 + 1;
+    const uint32_t a = mt_temper(ring[s0]) >> 5, b = mt_temper(ring[s1]) >> 6;
     return ((double)a * 67108864.0 + (double)b) * (1.0 / 9007199254740992.0);
 }
 // mt_store_w for the numpy ring: the stream is consumed exactly up to front, so the block
@@ -338,27 +348,17 @@ __device__ __forceinline__ void np_store(uint32_t* ring, int& front, int head, u
 // The final head is never 624 words below the front, so no later crossing overwrites it.
 __device__ __forceinline__ void py_ensure(uint32_t* ring, int& front, int upto, uint32_t* gst, int head_lb) {
     const int lane = (int)(threadIdx.x & 63);
+    int r = np_slot(front);
     while (front < upto) {
-        const int r = np_slot(front);
         if (r == 0 && front >= 2 * MT_N && head_lb <= front) {
             for (int i = lane; i < MT_N; i += 64) gst[i] = ring[i];  // block [front - 624, front)
         }
-        const int cnt = min(min(MT_LAG, upto - front), MT_N - r);
-        uint32_t lag[4], a[4], b[4];
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int n = front + lane + 64 * j;
-            lag[j] = ring[np_slot(n - MT_LAG)];
-            a[j] = ring[np_slot(n - 624)];
-            b[j] = ring[np_slot(n - 623)];
-        }
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int n = front + lane + 64 * j;
-            if (lane + 64 * j < cnt) ring[np_slot(n)] = mt_twist1(lag[j], a[j], b[j]);
-        }
+        int cnt = min(MT_LAG, upto - front);
+        // stop at the block boundary only where its block may have to be stored there
+        if (head_lb <= front - r + MT_N) cnt = min(cnt, MT_N - r);
+        ring_round(ring, r, cnt);
         front += cnt;
-        wave_fence();
+        r = ring_add(r, cnt);
     }
 }
 // The state after consuming up to raw index `head`: block b = [b, b + 624) holding head - 1, from
@@ -550,7 +550,7 @@ __host__ __device__ __forceinline__ int pow2_ceil(int n) {
 __device__ __forceinline__ int doff_of(uint32_t d, int GY) { return move_dx((int)d) * GY + move_dy((int)d); }
 
 template <typename T>
-__device__ __forceinline__ void contested_groups(T* Lp, T* heads, T* gstart, int n, int pb, uint32_t* pyring, int& py_front,
+__device__ __forceinline__ void contested_groups(T* Lp, T* heads, T* gstart, int& n, int pb, uint32_t* pyring, int& py_front,
                                  int& py_head, uint32_t* lost, uint32_t* grp, int& err, long long* prof, uint32_t* gst) {
     const int lane = (int)(threadIdx.x & 63);
 #ifdef EVX_PROFILE
@@ -569,7 +569,29 @@ __device__ __forceinline__ void contested_groups(T* Lp, T* heads, T* gstart, int
     for (int i = n + lane; i < n2; i += 64) Lp[i] = 0xffffffffu;
     wave_sync();
     wave_sort_keys(Lp, n, n2);
-    CG_T(0);
+    // candidates alone on their target (their cell pair held a contested target: the contested
+    // bitmap is at half resolution) are dropped, in order: the groups are then the contested
+    // targets exactly (>= 2 movers each, so at most n / 2 of them)
+    {
+        int nn = 0;
+        uint32_t prevlast = 0xffffffffu;
+        for (int i0 = 0; i0 < n; i0 += 64) {
+            const int i = i0 + lane;
+            const uint32_t key = i < n ? (uint32_t)Lp[i] : 0xffffffffu;
+            const uint32_t nxt = i + 1 < n ? (uint32_t)Lp[i + 1] : 0xffffffffu;  // read before this chunk writes
+            uint32_t prv = (uint32_t)__shfl_up((int)key, 1, 64);
+            if (lane == 0) prv = prevlast;
+            const uint32_t tk = key >> pb;
+            const bool keep = i < n && ((i > 0 && (prv >> pb) == tk) || (i + 1 < n && (nxt >> pb) == tk));
+            prevlast = (uint32_t)__builtin_amdgcn_readlane((int)key, 63);
+            const unsigned long long m = __ballot(keep);
+            wave_fence();
+            if (keep) Lp[nn + lanes_below(m)] = (T)key;
+            nn += __popcll(m);
+        }
+        n = nn;
+        wave_sync();
+    }
     int ngrp = 0;
     for (int i0 = 0; i0 < n; i0 += 64) {
         const int i = i0 + lane;
@@ -678,7 +700,10 @@ __device__ __forceinline__ void contested_groups(T* Lp, T* heads, T* gstart, int
             // 0 as the words are made (its words need not stay in the ring for pass 2)
             if (cnt > 8 && nk > 0) break;
             wv = lane == nk ? pos : wv;
-            if (cnt <= 8) {
+            if (cnt == 1) {
+                // a lone mover (its cell pair held a contested target, its own target is not
+                // contested): random.shuffle of one element draws nothing, the mover wins
+            } else if (cnt <= 8) {
                 while (true) {
                     if (pos - B >= 64 || pos < B) build_window(pos);
                     const uint32_t tab = cnt == 2 ? endt[0] : cnt == 3 ? endt[1] : cnt == 4 ? endt[2] : cnt == 5 ? endt[3]
@@ -776,14 +801,16 @@ __device__ __forceinline__ void contested_groups(T* Lp, T* heads, T* gstart, int
 #undef CG_T
 }
 
-// First planner of contested target t (the group's smallest person index).
-__device__ __forceinline__ int find_pf(const uint32_t* Lp, int n, int t, int pb) {
+// First planner of contested target t (the group's smallest person index); p when t is not
+// contested (a candidate of the half-resolution bitmap alone on its target: its own first planner).
+__device__ __forceinline__ int find_pf(const uint32_t* Lp, int n, int t, int pb, int p) {
     int lo = 0, hi = n;
     while (lo < hi) {
         const int mid = (lo + hi) >> 1;
         if ((int)(Lp[mid] >> pb) < t) lo = mid + 1;
         else hi = mid;
     }
+    if (lo >= n || (int)(Lp[lo] >> pb) != t) return p;
     return (int)(Lp[lo] & ((1u << pb) - 1u));
 }
 
@@ -800,6 +827,7 @@ struct WaveLds {  // word offsets into dynamic LDS
 #endif
 __host__ __device__ inline bool big_grid(int L, int W) { return ((L + 2) * (W + 2) + 31) / 32 > EVX_BIGG_RW; }
 
+__host__ __device__ inline int cbits_words(int G) { return ((G + 1) / 2 + 31) / 32; }
 __host__ __device__ inline WaveLds wave_lds(int L, int W, int P, int R, bool bigg = false) {
     WaveLds s;
     const int G = (L + 2) * (W + 2);
@@ -814,8 +842,10 @@ __host__ __device__ inline WaveLds wave_lds(int L, int W, int P, int R, bool big
         s.tbits = s.cbits = s.vac = -1;  // global scratch (env_scratch_words)
     } else {
         s.tbits = o; o += RW;
-        s.cbits = -1;  // the contested bitmap: global step scratch (cbits_offset), set and read only
-                       // when two planners target one cell
+        // contested targets at half resolution (cell pairs t >> 1): a set bit marks a pair holding a
+        // contested target; the exact test happens when the candidates are grouped by target (a
+        // mover alone on its target forms a group of one, which shuffles nothing and wins)
+        s.cbits = o; o += cbits_words(G);
         if (RW <= MT_N) {
             s.vac = s.pyring;
         } else {
@@ -850,16 +880,10 @@ __host__ __device__ inline int64_t wave_scratch_words(int P) { return wave_hv_of
 // count, in-play count, -, the health total as a double at [4..5], -) | the not-dead persons'
 // healths in list order [P] double (the in-play list itself stays in the wide path's health
 // region, which a light step does not otherwise use)
-// ... | other grids: the contested bitmap [RW] (zero between steps: a step that sets bits clears them)
 __host__ __device__ inline int64_t persist_offset(const evx_layout& l) {
     const int RW = ((l.L + 2) * (l.W + 2) + 31) / 32;
-    const int64_t o = wave_scratch_words(l.P) + (big_grid(l.L, l.W) ? 3 * (int64_t)RW + (l.P + 31) / 32 : RW);
+    const int64_t o = wave_scratch_words(l.P) + (big_grid(l.L, l.W) ? 3 * (int64_t)RW + (l.P + 31) / 32 : 0);
     return (o + 1) & ~(int64_t)1;
-}
-// the contested bitmap in an env's step scratch (big grids: after the target bitmap)
-__host__ __device__ inline int64_t cbits_offset(const evx_layout& l) {
-    const int RW = ((l.L + 2) * (l.W + 2) + 31) / 32;
-    return wave_scratch_words(l.P) + (big_grid(l.L, l.W) ? RW : 0);
 }
 constexpr int LHDR = 8;  // words of the kept lists' header
 __host__ __device__ inline int64_t env_scratch_words(const evx_layout& l) { return persist_offset(l) + LHDR + 2 * (int64_t)l.P; }
@@ -1123,7 +1147,7 @@ __device__ __forceinline__ void rows_wide(const evx_layout& lay, const evx_state
     double* h_g = st.health + (size_t)e * P;
     double* a_g = st.acc + (size_t)e * P;
     uint32_t* scr = st.scratch + (size_t)e * env_scratch_words(lay);
-    uint32_t* cbits = scr + cbits_offset(lay);  // global (L2): device-scope atomics
+    uint32_t* cbits = smem + S.cbits;  // contested cell pairs (LDS)
     uint2* plan = reinterpret_cast<uint2*>(scr);
     const uint2* ndl = reinterpret_cast<const uint2*>(scr + 2 * P);
     double* hv = reinterpret_cast<double*>(scr + wave_hv_offset(P));
@@ -1333,7 +1357,7 @@ __device__ __forceinline__ void rows_wide(const evx_layout& lay, const evx_state
                     const uint32_t bit = 1u << (t & 31);
                     const uint32_t old = atomicOr(&tbits[t >> 5], bit);
                     if (old & bit) {
-                        atomicOr(&cbits[t >> 5], bit);
+                        atomicOr(&cbits[(t >> 1) >> 5], 1u << ((t >> 1) & 31));
                         anyc = true;
                     }
                 }
@@ -1461,15 +1485,14 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     uint32_t* rmapb = smem + S.rmapb;
     const int64_t SW = env_scratch_words(lay);
     uint32_t* scr = st.scratch + (size_t)e * SW;
-    uint32_t *tbits, *vac;
-    // the contested bitmap: global (L2) for every grid, read with agent-scope atomic loads past the
-    // L1 and only when some target is contested (any_cont)
-    uint32_t* cbits = scr + cbits_offset(lay);
+    uint32_t *tbits, *cbits, *vac;
     if constexpr (BIGG) {  // global (L2): read with agent-scope atomic loads, past the L1
         tbits = scr + wave_scratch_words(P);
+        cbits = tbits + g.RW;
         vac = cbits + g.RW;
     } else {
         tbits = smem + S.tbits;
+        cbits = smem + S.cbits;  // contested cell pairs (half resolution, see wave_lds)
         vac = smem + S.vac;
     }
     auto tc_get = [&](const uint32_t* b, int i) -> bool {
@@ -1478,9 +1501,9 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
         else
             return bit_get(b, i);
     };
-    auto cb_get = [&](int i) -> bool {
-        return (__hip_atomic_load(cbits + (i >> 5), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (i & 31)) & 1u;
-    };
+    // contested target t (big grids: exact, global; others: its cell pair, LDS)
+    auto cb_idx = [&](int t) -> int { return BIGG ? t : t >> 1; };
+    auto cb_get = [&](int t) -> bool { return tc_get(cbits, cb_idx(t)); };
     uint32_t* nearc = smem + S.nearc;
     const int NCW = (((g.L + 2 + 3) >> 2) * ((GY + 3) >> 2) + 31) / 32;
     uint32_t* lost = BIGG ? vac + g.RW : smem + S.lost;  // BIGG: set by atomics, read by tc_get
@@ -1586,6 +1609,8 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     int py_head = __builtin_amdgcn_readlane((int)wpy[9], MT_N - 576);  // word 624 = index
     int np_head = __builtin_amdgcn_readlane((int)wnp[9], MT_N - 576);
     for (int i = lane; i < (P + 31) / 32; i += 64) lost[i] = 0;
+    if constexpr (!BIGG)
+        for (int i = lane; i < cbits_words(g.G); i += 64) cbits[i] = 0;
     for (int i = lane; i < NCW; i += 64) nearc[i] = 0;
     int py_front = MT_N, np_front = MT_N;
     // Map.move_robot for every robot (envs/map.py:160-201); robots never interact.
@@ -1801,7 +1826,8 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
             const uint32_t bit = 1u << (t & 31);
             const uint32_t old = atomicOr(&tbits[t >> 5], bit);
             if (old & bit) {
-                atomicOr(&cbits[t >> 5], bit);
+                const int ci = cb_idx(t);
+                atomicOr(&cbits[ci >> 5], 1u << (ci & 31));
                 any_cont = true;
             }
             if (!only) plan[nplan + lanes_below(mm)] = make_uint2((uint32_t)p, (uint32_t)cold | (best << 24));
@@ -1976,22 +2002,28 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
             const bool fin = it == NIT && k == GQ - 1;
             PT_BEGIN(drain);
             while (qn >= 64 || (fin && qn > 0)) {
-                const int n = min(qn, 64);
                 wave_fence();
-                score_batch(n, fin && nbatch == 0 && qn <= 64);
-                const int rest = qn - n;  // move entries [n, qn) to the front (rest <= 63)
-                uint32_t ta = 0, tb = 0;
-                int tc = 0;
-                if (lane < rest) {
-                    ta = qa[n + lane];
-                    tb = qb[n + lane];
-                    tc = qc[n + lane];
+                const int n = min(qn, 64);
+                score_batch(n, fin && nbatch == 0 && qn == n);
+                const int rest = qn - n;  // move entries [n, qn) to the front (rest <= 126)
+                uint32_t ta[2] = {0u, 0u}, tb[2] = {0u, 0u};
+                int tc[2] = {0, 0};
+#pragma unroll
+                for (int j = 0; j < 2; j++) {
+                    if (lane + 64 * j < rest) {
+                        ta[j] = qa[n + lane + 64 * j];
+                        tb[j] = qb[n + lane + 64 * j];
+                        tc[j] = qc[n + lane + 64 * j];
+                    }
                 }
                 wave_fence();
-                if (lane < rest) {
-                    qa[lane] = ta;
-                    qb[lane] = tb;
-                    qc[lane] = tc;
+#pragma unroll
+                for (int j = 0; j < 2; j++) {
+                    if (lane + 64 * j < rest) {
+                        qa[lane + 64 * j] = ta[j];
+                        qb[lane + 64 * j] = tb[j];
+                        qc[lane + 64 * j] = tc[j];
+                    }
                 }
                 qn = rest;
                 wave_fence();
@@ -2116,15 +2148,42 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     long long cgp[7] = {0, 0, 0, 0, 0, 0, 0};  // EVX_PROFILE: sort, heads, pass 1, pass 2, windows, groups, window cycles
     PT_BEGIN(lp);
     uint32_t* Lp = npring;  // the numpy ring is free now
-    if (any_cont) {
-        plan_pass([&](const uint2 en, bool ok) {
-            bool c = false;
-            uint32_t key = 0;
-            if (ok) {
-                const int t = (int)(en.y & 0xffffffu) + doff_of(en.y >> 24, GY);
-                c = cb_get(t);
-                key = ((uint32_t)t << pb) | en.x;
+    // the (candidate) contested movers, their contested-bitmap words loaded 4 x 64 at a time before
+    // any is used (big grids: from L2)
+    auto cont_pass = [&](auto&& fn) {
+        auto one = [&](const uint2 en, bool ok, uint32_t cw) {
+            const int t = (int)(en.y & 0xffffffu) + doff_of(en.y >> 24, GY);
+            const bool c = ok && ((cw >> (cb_idx(t) & 31)) & 1u);
+            fn(c, ((uint32_t)t << pb) | en.x);
+        };
+        auto cword = [&](const uint2 en, bool ok) -> uint32_t {
+            if (!ok) return 0u;
+            const int t = (int)(en.y & 0xffffffu) + doff_of(en.y >> 24, GY);
+            if constexpr (BIGG)
+                return __hip_atomic_load(cbits + (t >> 5), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else
+                return cbits[cb_idx(t) >> 5];
+        };
+        if (preg) {
+            one(rp_en, rp_mov, cword(rp_en, rp_mov));
+            return;
+        }
+        for (int i0 = 0; i0 < nplan; i0 += 256) {
+            uint2 en[4];
+            uint32_t cw[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                en[j] = make_uint2(0u, 0u);
+                if (i0 + 64 * j + lane < nplan) en[j] = plan[i0 + 64 * j + lane];
             }
+#pragma unroll
+            for (int j = 0; j < 4; j++) cw[j] = cword(en[j], i0 + 64 * j + lane < nplan);
+#pragma unroll
+            for (int j = 0; j < 4; j++) one(en[j], i0 + 64 * j + lane < nplan, cw[j]);
+        }
+    };
+    if (any_cont) {
+        cont_pass([&](bool c, uint32_t key) {
             const unsigned long long m = __ballot(c);
             const int pos = ncont + lanes_below(m);
             if (c && pos < CL_CAP) Lp[pos] = key;
@@ -2137,14 +2196,7 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
         } else {  // rare: sort in this env's global scratch
             Lp = Lg;
             int k = 0;
-            plan_pass([&](const uint2 en, bool ok) {
-                bool c = false;
-                uint32_t key = 0;
-                if (ok) {
-                    const int t = (int)(en.y & 0xffffffu) + doff_of(en.y >> 24, GY);
-                    c = cb_get(t);
-                    key = ((uint32_t)t << pb) | en.x;
-                }
+            cont_pass([&](bool c, uint32_t key) {
                 const unsigned long long m = __ballot(c);
                 if (c) Lg[k + lanes_below(m)] = key;
                 k += __popcll(m);
@@ -2194,7 +2246,8 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
         if (ok) {
             const int cold = (int)(en.y & 0xffffffu);
             const int t = cold + doff_of(en.y >> 24, GY);
-            const bool win = !any_cont || !cb_get(t) || !tc_get(lost, (int)en.x);
+            const bool cont = any_cont && cb_get(t);
+            const bool win = !cont || !tc_get(lost, (int)en.x);
             if (win) atomicOr(&vac[cold >> 5], 1u << (cold & 31));
             if (st.thmap) atomicAdd(&st.thmap[(size_t)e * g.G + (win ? t : cold)], 1);
         }
@@ -2219,7 +2272,7 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
                 exw = ex;
                 const bool ev_old = tc_get(tbits, cold), ev_new = tc_get(vac, t);
                 int pf = p;
-                if ((ev_old || ev_new) && cont) pf = find_pf(Lp, ncont, t, pb);
+                if ((ev_old || ev_new) && cont) pf = find_pf(Lp, ncont, t, pb, p);
                 if (ev_old) {
                     const int s = atomicAdd((int*)&misc[0], 1);
                     if (s < EV_CAP) {
@@ -2286,11 +2339,6 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
         }
     }
     wave_sync();  // the person words of the movers and the rmap bits complete
-    if constexpr (!BIGG) {
-        if (any_cont) {  // every contested bit this step set, cleared for the next step
-            for (int i = lane; i < g.RW; i += 64) cbits[i] = 0u;
-        }
-    }
     EVX_STAMP(4);
 
     // ---------------------------------- fire update (both fire models)
@@ -2565,11 +2613,6 @@ __device__ __forceinline__ void reset_one(const evx_layout& lay, const evx_state
     const int P = g.P, R = g.R;
     // fresh people: the light path's kept lists no longer describe this env
     if (lane == 0) st.scratch[(size_t)e * env_scratch_words(lay) + persist_offset(lay)] = 0u;
-    if constexpr (!BIGG) {  // the contested bitmap is zero between steps (a step clears what it sets)
-        const int RW = (((lay.L + 2) * (lay.W + 2)) + 31) / 32;
-        uint32_t* cb = st.scratch + (size_t)e * env_scratch_words(lay) + cbits_offset(lay);
-        for (int i = lane; i < RW; i += 64) cb[i] = 0u;
-    }
     const ResetLds S = reset_lds(g.G, P, BIGG);
     uint32_t* pyring = smem + S.pyring;
     const uint32_t* validb;
@@ -3138,7 +3181,7 @@ int evx_env_step_part(const evx_layout* l, const evx_state* s, const int32_t* ac
         attr_set = true;
     }
     // Default: 4-wave workgroups with the heavy-env path while a launch is short enough for
-    // its heaviest env to set its length (fewer than 32 envs per CU); one-wave workgroups
+    // its heaviest env to set its length (fewer than 64 envs per CU); one-wave workgroups
     // beyond, where throughput rules: a wave's VGPRs and LDS free the moment its env is done
     // instead of when the slowest of four is (32768 envs: env_step 1.50 -> 1.31 ms).
     static int ncu = 0;
@@ -3148,7 +3191,9 @@ int evx_env_step_part(const evx_layout* l, const evx_state* s, const int32_t* ac
             hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
             ncu = 256;
     }
-    int nwb = s->E >= 32 * ncu ? 1 : 4;
+    // (64 envs per CU: the 8192-env share of cfg5 keeps the heavy-env workgroups -- env_step 0.42 ->
+    // 0.37 ms; big grids, which have no heavy path, switch at 32)
+    int nwb = s->E >= (bigg ? 32 : 64) * ncu ? 1 : 4;
     if (bigg && nwb > 2) nwb = 2;  // BIGG kernels: 1 or 2 envs per workgroup
     while (nwb > 1 && step_launch_lds(*l, nwb, bigg) > 160 * 1024) nwb >>= 1;
     int hmin = 0;

@@ -3,9 +3,11 @@
 The kernel variant a launch picks depends on its size, so parity at small E / small B
 says nothing about the variant the bench runs:
 
-* env.step: at E >= 32 x CUs (8192 on MI355X) evx_env_step picks one-wave workgroups
-  (env_step_kernel<1, ...>, csrc/env_step.hip: evx_env_step_part), for cfg4's 256x256
-  grid the big-grid instantiation <1, false, true>. cfg4 (256x256, P 9102, R 1, 8192 envs)
+* env.step: evx_env_step picks one-wave workgroups at E >= 64 x CUs (32 x CUs for big grids;
+  env_step_kernel<1, ...>, csrc/env_step.hip: evx_env_step_part), 4-wave workgroups with the
+  heavy-env path below: cfg4's 256x256 grid at 8192 envs runs the big-grid instantiation
+  <1, false, true>, cfg5's 8192 envs the 4-wave path (cfg3's 32768-env one-wave launch:
+  tests/test_env_gpu.py::test_env_parity_bench_scale). cfg4 (256x256, P 9102, R 1, 8192 envs)
   and cfg5 (128x128, P 2276, R 32, 8192 envs) are prepared as bench.py prepares them
   (env-only steps, env g force-reset at step g % stagger: ages spread over an episode,
   fused auto-resets), then envs spread over the age mix are snapshotted into the oracle
@@ -54,8 +56,6 @@ def _bench_mix_parity(L, P, R, E, age_steps, stagger, n_snap, steps, min_age_spa
     from evacx.env import DeviceLayout, VecEnv
     from evacx.layout import build_tables, synthetic
     from oracle import oracle as orc
-    ncu = torch.cuda.get_device_properties(0).multi_processor_count
-    assert E >= 32 * ncu, "the test must reach the one-wave-workgroup launch the bench runs"
     tables = build_tables(synthetic(L, L, R))
     lay = DeviceLayout(tables, P)
     env = VecEnv(lay, E)
@@ -109,7 +109,7 @@ def test_cfg4_env_at_bench_scale():
 
 
 def test_cfg5_env_at_bench_scale():
-    """cfg5: 128x128, P 2276, R 32, 8192 envs (env_step_kernel<1, false>), prepared as the bench
+    """cfg5: 128x128, P 2276, R 32, 8192 envs (4-wave workgroups, heavy-env path), prepared as the bench
     (--age-steps 1300 --stagger 1200); 48 envs x 50 steps vs the oracle."""
     _need_gpu()
     ages, n_done = _bench_mix_parity(L=128, P=2276, R=32, E=8192, age_steps=1300, stagger=1200, n_snap=48,

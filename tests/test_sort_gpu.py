@@ -11,7 +11,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("n", [1, 63, 64, 100, 512, 513, 1000, 1024, 2500, 4096, 7000])
+@pytest.mark.parametrize("n", [1, 63, 64, 100, 512, 513, 1000, 1024, 2500, 4096, 7000, 8193, 9102])
 def test_step_key_sort_matches_numpy(n):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
