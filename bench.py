@@ -278,7 +278,7 @@ def main():
                 env.compute_order()
                 if ev_env is not None and s % EV_EVERY == 0:
                     ev_env[s][0].record()
-                env.step(acts_env[s], order=False, auto_reset=True)
+                env.step(acts_env[s % acts_env.shape[0]], order=False, auto_reset=True)
                 if ev_env is not None and s % EV_EVERY == 0:
                     ev_env[s][1].record()
         if args.mode == "train":

@@ -904,7 +904,10 @@ __device__ long long g_act_st[8192 * ACT_NST];
 constexpr int A3H_HBYTES = 2 * 64 * A3_HP * 2;  // 67,584: both H1 half planes of 64 rows
 static_assert(A3H_HBYTES >= 2 * 64 * (KC1 + 8) * 2, "fc1 A staging overlays the H1 planes");
 constexpr int ACT3H_LDS = A3H_HBYTES + NACT * HID2 * 4 + 64 * 4 + 64 * 8 + ACT3_OCC;  // posS, phS (DM 3: [64] uint2)
-template <bool GR = false, int DM = 1>
+// SAVE: the learner's online forward (evx_qmlp_forward2 at B >= 32768 with the online net's act
+// table): the tables' tiles start fc1 from it like the act, each half's H1 planes go to a.h1 /
+// a.h1l for the backward, H2 to a.h2 and Q to a.q by batch row; X is written by x_expand_kernel.
+template <bool GR = false, int DM = 1, bool SAVE = false>
 __global__ __launch_bounds__(256, 2) void qact3h_kernel(Fwd a0) {
     Fwd ag;
     if constexpr (GR) ag = fwd_net(a0, (int)blockIdx.y);
@@ -1029,6 +1032,15 @@ __global__ __launch_bounds__(256, 2) void qact3h_kernel(Fwd a0) {
         ACT_ST(3 + 4 * hh);
         __syncthreads();
         ACT_ST(4 + 4 * hh);
+        if constexpr (SAVE) {  // this half's H1 planes for the backward: rows m0 .., columns 256 hh ..
+            for (int i = tid; i < 2 * 64 * 32; i += 256) {
+                const int pl = i >> 11, rl = (i >> 5) & 63, pc = i & 31;
+                if (m0 + rl < a.N) {
+                    const uint4 v = *reinterpret_cast<const uint4*>(pl ? &Hl[rl][pc * 8] : &Hh[rl][pc * 8]);
+                    *reinterpret_cast<uint4*>((pl ? a.h1l : a.h1) + (size_t)(m0 + rl) * HID + hh * 256 + pc * 8) = v;
+                }
+            }
+        }
         // fc2 over K = [256 hh, 256 hh + 256): wave w -> columns [64 w, 64 w + 64)
         bf16x8 bc[2][2], bn[2][2], lc[2][2], ln[2][2];  // [nt][s]
         auto loadB = [&](int kc, bf16x8 (&b)[2][2], bf16x8 (&l)[2][2]) {
@@ -1070,8 +1082,39 @@ __global__ __launch_bounds__(256, 2) void qact3h_kernel(Fwd a0) {
         __syncthreads();  // every wave is done with this half: the next half / H2 reuse the planes
     }
     ACT_ST(10);
-    fc3t_x3(a, acc2, W3s, reinterpret_cast<float*>(dsm), m0, true);
+    fc3t_x3(a, acc2, W3s, reinterpret_cast<float*>(dsm), m0, !SAVE);
     ACT_ST(11);
+}
+
+// X (the x3 compact input of every batch row, [N][640] bf16: per cell (occ | danger hi, barrier |
+// exit), then the 128 cells' danger residuals) for the backward's dW1 when the online forward runs
+// through the act kernel's table path -- what qfc1_kernel's staging writes as it goes (fc1_tile's
+// stash). One 16-B piece per thread: pieces 0..63 two cells' features, 64..79 eight residuals.
+__global__ __launch_bounds__(256) void x_expand_kernel(Fwd a) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int row = (int)(i / 80), q = (int)(i - (int64_t)row * 80);
+    if (row >= a.N) return;
+    const evx_obs ob = a.obs[orow(a, row)];
+    const int fbase = feat_base(a, ob);
+    uint4 v;
+    if (q < 64) {
+        const uint32_t* fb = (a.feats ? a.feats[ob.layout] : a.feat) + fbase;
+        const uint2 f0 = cell_feat(ob, 2 * q, fb[feat_off(a, 2 * q)]);
+        const uint2 f1 = cell_feat(ob, 2 * q + 1, fb[feat_off(a, 2 * q + 1)]);
+        v = make_uint4(f0.x, f0.y, f1.x, f1.y);
+    } else {
+        const uint16_t* flb = (a.feats_lo ? a.feats_lo[ob.layout] : a.feat_lo) + fbase;
+        uint32_t w[4];
+#pragma unroll
+        for (int t = 0; t < 8; t += 2) {
+            const int c0 = 8 * (q - 64) + t;
+            const uint32_t l0 = c0 < NCELL ? (uint32_t)flb[feat_off(a, c0)] : 0u;
+            const uint32_t l1 = c0 + 1 < NCELL ? (uint32_t)flb[feat_off(a, c0 + 1)] : 0u;
+            w[t >> 1] = l0 | (l1 << 16);
+        }
+        v = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    *reinterpret_cast<uint4*>(a.x + (size_t)row * K1X + 8 * q) = v;
 }
 
 // ------------------------------------------------------------ fc2 + fc3
@@ -2088,24 +2131,25 @@ int evx_qmlp_pack3(const float* w1, const float* b1, const float* w2, uint16_t* 
 }
 
 // the x3 act kernel for the dropout mode of a (fc1_slab_m)
-extern "C++" template <bool GR>
+// SAVE: the learner's online forward (no row permutation; X from x_expand_kernel)
+extern "C++" template <bool GR, bool SAVE = false>
 static void launch_act3(const evxm::Fwd& a, int32_t n, int nets, hipStream_t st) {
     static bool attr = false;
     if (!attr) {
-        const void* kh[4] = {(const void*)evxm::qact3h_kernel<GR, 0>, (const void*)evxm::qact3h_kernel<GR, 1>,
-                             (const void*)evxm::qact3h_kernel<GR, 2>, (const void*)evxm::qact3h_kernel<GR, 3>};
+        const void* kh[4] = {(const void*)evxm::qact3h_kernel<GR, 0, SAVE>, (const void*)evxm::qact3h_kernel<GR, 1, SAVE>,
+                             (const void*)evxm::qact3h_kernel<GR, 2, SAVE>, (const void*)evxm::qact3h_kernel<GR, 3, SAVE>};
         for (const void* k : kh) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, evxm::ACT3H_LDS);
         attr = true;
     }
     const dim3 grid((unsigned)((n + 63) / 64), (unsigned)nets);
     if (a.drop_mask)
-        hipLaunchKernelGGL((evxm::qact3h_kernel<GR, 2>), grid, dim3(256), evxm::ACT3H_LDS, st, a);
-    else if (a.drop_thresh && a.perm && a.rpe == 1)  // a row permutation: rows of different pairs share tiles
-        hipLaunchKernelGGL((evxm::qact3h_kernel<GR, 3>), grid, dim3(256), evxm::ACT3H_LDS, st, a);
+        hipLaunchKernelGGL((evxm::qact3h_kernel<GR, 2, SAVE>), grid, dim3(256), evxm::ACT3H_LDS, st, a);
+    else if (!SAVE && a.drop_thresh && a.perm && a.rpe == 1)  // a row permutation: rows of different pairs share tiles
+        hipLaunchKernelGGL((evxm::qact3h_kernel<GR, 3, SAVE>), grid, dim3(256), evxm::ACT3H_LDS, st, a);
     else if (a.drop_thresh)
-        hipLaunchKernelGGL((evxm::qact3h_kernel<GR, 1>), grid, dim3(256), evxm::ACT3H_LDS, st, a);
+        hipLaunchKernelGGL((evxm::qact3h_kernel<GR, 1, SAVE>), grid, dim3(256), evxm::ACT3H_LDS, st, a);
     else
-        hipLaunchKernelGGL((evxm::qact3h_kernel<GR, 0>), grid, dim3(256), evxm::ACT3H_LDS, st, a);
+        hipLaunchKernelGGL((evxm::qact3h_kernel<GR, 0, SAVE>), grid, dim3(256), evxm::ACT3H_LDS, st, a);
 }
 
 static int make_fwd(const evx_layout* lay, const evx_obs* obs, int32_t n, const evx_qmlp_params* p,
@@ -2321,10 +2365,21 @@ int evx_qmlp_forward2(const evx_layout* lay, int32_t n, const evx_obs* obs0, con
         a1.perm = nullptr;
         a1.actions = nullptr;
         a1.h1 = a1.h1l = nullptr;
-        // (the online forward through the fused kernel with X / H1 / H2 saves measured no faster
-        // than qfc1 + qfc23 at B = 32768: learn 0.420 vs 0.427 ms; removed)
-        int rc2 = launch_fwd(a0, a0, n, 1, true, (hipStream_t)stream, true);
-        if (rc2) return rc2;
+        if (a0.stat && !a0.perm && !a0.actions && a0.x && a0.h1 && a0.h1l && a0.h2 && a0.q) {
+            // the online net's act table too (rebuilt after every update, so it matches the weights
+            // this forward reads): the online forward through the fused act kernel's table path,
+            // H1 planes / H2 / Q saved for the backward, X expanded by its own launch -- instead of
+            // qfc1's K = 640 products over staged A tiles and qfc23 re-reading both H1 planes
+            const int64_t nx = (int64_t)n * 80;
+            hipLaunchKernelGGL(evxm::x_expand_kernel, dim3((unsigned)((nx + 255) / 256)), dim3(256), 0,
+                               (hipStream_t)stream, a0);
+            launch_act3<false, true>(a0, n, 1, (hipStream_t)stream);
+        } else {
+            // (the online forward through the fused kernel on the full path with X saved measured no
+            // faster than qfc1 + qfc23 at B = 32768: learn 0.420 vs 0.427 ms)
+            int rc2 = launch_fwd(a0, a0, n, 1, true, (hipStream_t)stream, true);
+            if (rc2) return rc2;
+        }
         launch_act3<false>(a1, n, 1, (hipStream_t)stream);
         return mlaunch("qmlp_forward2 target act");
     }

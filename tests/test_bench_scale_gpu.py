@@ -135,12 +135,15 @@ def _torch_q_gated(sd, X, g1, g2):
     return F.linear(z2 * g2, sd["fc3.weight"], sd["fc3.bias"]), z1, z2
 
 
-@pytest.mark.parametrize("B", [8192, 32768])
-def test_x3_learn_at_bench_batch(B):
+@pytest.mark.parametrize("B,table", [(8192, False), (32768, False), (32768, True)])
+def test_x3_learn_at_bench_batch(B, table):
     """Two learn steps (each from the same parameters and Adam moments on both sides) at the
-    bench's learn batch: cfg5's 8192 (2-tile qdz1) and cfg3's 32768 (qfc1<4,1,8,true>, 8-tile
-    qdz1). Observations: a 128x128 R16 env 40 steps into its episode (fire spreading, people
-    moving), sampled without replacement into s and s'.
+    bench's learn batch: cfg5's 8192 (2-tile qdz1) and cfg3's 32768 (8-tile qdz1); the online
+    forward through qfc1<2,2,4,true> + qfc23, or (table: as VecTrainer runs it, the online net
+    with its act table) through x_expand_kernel + qact3h_kernel SAVE, with three quarters of the
+    s rows moved to the layout's last fire step so their tiles start fc1 from the table.
+    Observations: a 128x128 R16 env 40 steps into its episode (fire spreading, people moving),
+    sampled without replacement into s and s'.
 
     ReLU branches. x3 products are ~2^-17 off, so a pre-activation within that of 0 can take
     the other ReLU branch than fp32 torch; at these batches (16.8 M fc1 and 8.4 M fc2
@@ -170,6 +173,9 @@ def test_x3_learn_at_bench_batch(B):
     dev = "cuda"
     lr = Learner(kind="mlp", precision="f32", seed=41, lr=1e-3)
     assert lr.fast is not None and lr.fast.x3 and lr.fused_opt  # the trainer's chain
+    c = lay.c
+    if table:
+        lr.fast.attach_static(c, c.L, c.W, c.t_max, x_range=(max(c.rx_lo, 0), min(c.rx_hi, c.L + 1)))
     sd0 = {k: v.clone() for k, v in lr.online.state_dict().items()}
     params = {k: torch.nn.Parameter(v.clone()) for k, v in sd0.items()}
     tgt = {k: v.clone() for k, v in sd0.items()}
@@ -184,7 +190,10 @@ def test_x3_learn_at_bench_batch(B):
             for key, buf in (("exp_avg", lr.m), ("exp_avg_sq", lr.v)):
                 buf.copy_(torch.cat([opt.state[p][key].reshape(-1) for p in params.values()]))
         perm = torch.randperm(E * R, generator=gh)
-        s_obs = obs[perm[:B].to(dev)].contiguous().view(-1)
+        s_obs = obs[perm[:B].to(dev)].contiguous()
+        if table:
+            s_obs[:3 * B // 4, 6] = int(c.t_max)
+        s_obs = s_obs.view(-1)
         s2_obs = obs[perm[B:2 * B].to(dev)].contiguous().view(-1)
         a = torch.randint(0, 5, (B,), generator=gh, dtype=torch.int32).to(dev)
         r = (torch.randn(B, generator=gh) * 30).to(dev)
@@ -235,11 +244,11 @@ def test_x3_learn_at_bench_batch(B):
         for k in params:
             ref = grads_ref[k]
             torch.testing.assert_close(lr.grads[k], ref, rtol=2e-3, atol=1e-5 * ref.abs().max().item() + 1e-9,
-                                       msg=lambda m: f"B={B} step {it} grad {k}: {m}")
+                                       msg=lambda m: f"B={B} table={table} step {it} grad {k}: {m}")
             diff = (lr.online[k] - params[k].detach()).abs()
             assert (diff > 1e-5).float().mean().item() <= 1e-3, (it, k, diff.max().item())
             assert diff.max().item() <= 2e-3, (it, k, diff.max().item())
-    print(f"B={B}: {n_flips} activations on the other ReLU branch than fp32 torch (x3 roundings of 0)")
+    print(f"B={B} table={table}: {n_flips} activations on the other ReLU branch than fp32 torch (x3 roundings of 0)")
 
 
 def _torch_conv_gated(sd, x, gates, g1, g2):
