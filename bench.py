@@ -140,7 +140,7 @@ def parse():
                          "(evacx.trainer._Group): one group's env.step tail overlaps the others' work")
     ap.add_argument("--traffic", default=None,
                     help="PMC traffic record of env_step_kernel on this workload and phase (tools/parse_prof.py); "
-                         "default profiles/r3/ (else r2/) env_traffic_<phase>.json")
+                         "default profiles/r4/ (else r3/, r2/) env_traffic_<phase>.json")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.envs_total > 0:
@@ -386,7 +386,7 @@ def main():
     achieved = bpe * per_launch / (kern_ms * 1e-3) / 1e9
     traffic, traffic_src, traffic_corr = None, None, None
     tpath = args.traffic or next((q for q in (os.path.join(ROOT, "profiles", r, f"env_traffic_{args.phase}.json")
-                                              for r in ("r3", "r2")) if os.path.exists(q)), "")
+                                              for r in ("r4", "r3", "r2")) if os.path.exists(q)), "")
     if os.path.exists(tpath):
         # HBM bytes per launch from rocprofv3 PMC passes of this same workload and phase
         # (separate --pmc FETCH_SIZE / WRITE_SIZE runs; cannot be collected inside the timed run)
