@@ -1089,32 +1089,39 @@ __global__ __launch_bounds__(256, 2) void qact3h_kernel(Fwd a0) {
 // X (the x3 compact input of every batch row, [N][640] bf16: per cell (occ | danger hi, barrier |
 // exit), then the 128 cells' danger residuals) for the backward's dW1 when the online forward runs
 // through the act kernel's table path -- what qfc1_kernel's staging writes as it goes (fc1_tile's
-// stash). One 16-B piece per thread: pieces 0..63 two cells' features, 64..79 eight residuals.
+// stash). 80 16-B pieces per row (0..63: two cells' features, 64..79: eight residuals), 20 threads
+// per row, each with 4 pieces t, t + 20, t + 40, t + 60: one observation load, then 4 independent
+// gathers in flight (one piece per thread left the launch bound by its dependent load chain).
 __global__ __launch_bounds__(256) void x_expand_kernel(Fwd a) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int row = (int)(i / 80), q = (int)(i - (int64_t)row * 80);
+    const int row = (int)(i / 20), t = (int)(i - (int64_t)row * 20);
     if (row >= a.N) return;
     const evx_obs ob = a.obs[orow(a, row)];
     const int fbase = feat_base(a, ob);
-    uint4 v;
-    if (q < 64) {
-        const uint32_t* fb = (a.feats ? a.feats[ob.layout] : a.feat) + fbase;
-        const uint2 f0 = cell_feat(ob, 2 * q, fb[feat_off(a, 2 * q)]);
-        const uint2 f1 = cell_feat(ob, 2 * q + 1, fb[feat_off(a, 2 * q + 1)]);
-        v = make_uint4(f0.x, f0.y, f1.x, f1.y);
-    } else {
-        const uint16_t* flb = (a.feats_lo ? a.feats_lo[ob.layout] : a.feat_lo) + fbase;
-        uint32_t w[4];
+    const uint32_t* fb = (a.feats ? a.feats[ob.layout] : a.feat) + fbase;
+    const uint16_t* flb = (a.feats_lo ? a.feats_lo[ob.layout] : a.feat_lo) + fbase;
+    uint4 v[4];
 #pragma unroll
-        for (int t = 0; t < 8; t += 2) {
-            const int c0 = 8 * (q - 64) + t;
-            const uint32_t l0 = c0 < NCELL ? (uint32_t)flb[feat_off(a, c0)] : 0u;
-            const uint32_t l1 = c0 + 1 < NCELL ? (uint32_t)flb[feat_off(a, c0 + 1)] : 0u;
-            w[t >> 1] = l0 | (l1 << 16);
+    for (int k = 0; k < 4; k++) {
+        const int q = t + 20 * k;
+        if (q < 64) {
+            const uint2 f0 = cell_feat(ob, 2 * q, fb[feat_off(a, 2 * q)]);
+            const uint2 f1 = cell_feat(ob, 2 * q + 1, fb[feat_off(a, 2 * q + 1)]);
+            v[k] = make_uint4(f0.x, f0.y, f1.x, f1.y);
+        } else {
+            uint32_t w[4];
+#pragma unroll
+            for (int u = 0; u < 8; u += 2) {
+                const int c0 = 8 * (q - 64) + u;
+                const uint32_t l0 = c0 < NCELL ? (uint32_t)flb[feat_off(a, c0)] : 0u;
+                const uint32_t l1 = c0 + 1 < NCELL ? (uint32_t)flb[feat_off(a, c0 + 1)] : 0u;
+                w[u >> 1] = l0 | (l1 << 16);
+            }
+            v[k] = make_uint4(w[0], w[1], w[2], w[3]);
         }
-        v = make_uint4(w[0], w[1], w[2], w[3]);
     }
-    *reinterpret_cast<uint4*>(a.x + (size_t)row * K1X + 8 * q) = v;
+#pragma unroll
+    for (int k = 0; k < 4; k++) *reinterpret_cast<uint4*>(a.x + (size_t)row * K1X + 8 * (t + 20 * k)) = v[k];
 }
 
 // ------------------------------------------------------------ fc2 + fc3
@@ -2370,7 +2377,7 @@ int evx_qmlp_forward2(const evx_layout* lay, int32_t n, const evx_obs* obs0, con
             // this forward reads): the online forward through the fused act kernel's table path,
             // H1 planes / H2 / Q saved for the backward, X expanded by its own launch -- instead of
             // qfc1's K = 640 products over staged A tiles and qfc23 re-reading both H1 planes
-            const int64_t nx = (int64_t)n * 80;
+            const int64_t nx = (int64_t)n * 20;
             hipLaunchKernelGGL(evxm::x_expand_kernel, dim3((unsigned)((nx + 255) / 256)), dim3(256), 0,
                                (hipStream_t)stream, a0);
             launch_act3<false, true>(a0, n, 1, (hipStream_t)stream);
