@@ -71,6 +71,14 @@ print("py words/step median", np.median(s[:, 12]), " np words/step median", np.m
 print(f"  slowest 1%: planners {s[top, 11].mean():.0f}, contested {s[top, 14].mean():.0f}")
 life = s[:, 10] - s[:, 9]  # s_memrealtime: constant 100 MHz on every XCD
 span = s[:, 10].max() - s[:, 9].min()
+# resident envs per CU over the launch (10-us buckets): ramp, plateau, tail
+t0r = s[:, 9].min()
+nb = int(span // 1000) + 1
+occ = np.zeros(nb)
+for st_, en_ in zip((s[:, 9] - t0r) / 1000.0, (s[:, 10] - t0r) / 1000.0):
+    a_, b_ = int(st_), int(en_)
+    occ[a_:b_ + 1] += 1
+print("resident envs per CU by 10-us bucket:", " ".join(f"{x / 256:.1f}" for x in occ))
 print(f"launch span {span / 100:.1f} us; median env lifetime {np.median(life) / 100:.1f} us, max {life.max() / 100:.1f} us; "
       f"mean concurrent envs {life.sum() / span:.0f} ({life.sum() / span / 256:.2f} per CU)")
 PROF = [(16, "rows: np draws+health"), (17, "rows: health sum"), (18, "rows: plan+queue+stores"),
