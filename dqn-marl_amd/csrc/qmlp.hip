@@ -630,13 +630,15 @@ __device__ __forceinline__ void q_out(const Fwd& a, float (&qv)[NACT], int row) 
         a.actions[row] = best;
     }
 }
-__device__ __forceinline__ void fc3t_x3(const Fwd& a, const f32x16 (&acc)[2][2], const float (*W3s)[HID2],
+// MT: 32-row slabs of the tile (2: 64 rows; 1: qfc23's 32-row tiles for small batches)
+template <int MT = 2>
+__device__ __forceinline__ void fc3t_x3(const Fwd& a, const f32x16 (&acc)[MT][2], const float (*W3s)[HID2],
                                         float* red, int m0, bool act_rows) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, j = lane & 31;
     const int t = lane & 31;  // A row: action (< NACT) or padding
-    f32x16 qp[2];
+    f32x16 qp[MT];
 #pragma unroll
-    for (int mt = 0; mt < 2; mt++)
+    for (int mt = 0; mt < MT; mt++)
 #pragma unroll
         for (int r = 0; r < 16; r++) qp[mt][r] = 0.f;
 #pragma unroll
@@ -673,7 +675,7 @@ __device__ __forceinline__ void fc3t_x3(const Fwd& a, const f32x16 (&acc)[2][2],
             }
         }
 #pragma unroll
-        for (int mt = 0; mt < 2; mt++) {
+        for (int mt = 0; mt < MT; mt++) {
             const int row = m0 + mt * 32 + j;
             float v[16];
 #pragma unroll
@@ -707,14 +709,14 @@ __device__ __forceinline__ void fc3t_x3(const Fwd& a, const f32x16 (&acc)[2][2],
     // 4 (l >> 5) + r (r < 4; valid below NACT)
     auto R = reinterpret_cast<float (*)[NACT][64]>(red);  // [4][NACT][64]
 #pragma unroll
-    for (int mt = 0; mt < 2; mt++)
+    for (int mt = 0; mt < MT; mt++)
 #pragma unroll
         for (int r = 0; r < 4; r++) {
             const int act = 4 * h + r;
             if (act < NACT) R[w][act][mt * 32 + j] = qp[mt][r];
         }
     __syncthreads();
-    if (tid < 64) {
+    if (tid < 32 * MT) {
         const int rt = m0 + tid;
         if (rt < a.N) {
             float qv[NACT];
@@ -1126,8 +1128,11 @@ __global__ __launch_bounds__(256) void x_expand_kernel(Fwd a) {
 
 // ------------------------------------------------------------ fc2 + fc3
 // X3: A = H1 hi / lo planes, B = fc2.weight hi / lo (3 MFMAs per fragment pair)
-template <bool X3 = false, bool GR = false>
+// MT = 1 (x3 only): 32-row tiles, twice the workgroups of a small batch (the LDS stages keep
+// their 64-row shape; rows 32.. are not staged)
+template <bool X3 = false, bool GR = false, int MT = 2>
 __global__ __launch_bounds__(256, 2) void qfc23_kernel(Fwd a0, Fwd a1, int np) {
+    static_assert(MT == 2 || X3, "32-row tiles: the x3 epilogue only");
     Fwd ag;
     if constexpr (GR) ag = fwd_net((int)blockIdx.z % np ? a1 : a0, (int)blockIdx.z / np);
     const Fwd& a = GR ? ag : (blockIdx.z ? a1 : a0);
@@ -1141,13 +1146,14 @@ __global__ __launch_bounds__(256, 2) void qfc23_kernel(Fwd a0, Fwd a1, int np) {
     auto Hs = reinterpret_cast<float (*)[HID2 + 4]>(sm23);
     __shared__ float W3s[NACT][HID2];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
-    const int m0 = blockIdx.x * RM;
+    const int m0 = blockIdx.x * (32 * MT);
     for (int i = tid; i < NACT * HID2; i += 256) W3s[i / HID2][i % HID2] = a.w3[i];
     const int gr = tid >> 2, go = (tid & 3) * 8;
-    const bool rowok = m0 + gr < a.N;
-    f32x16 acc[2][2];
+    const bool stg = gr < 32 * MT;  // this thread stages A row gr
+    const bool rowok = stg && m0 + gr < a.N;
+    f32x16 acc[MT][2];
 #pragma unroll
-    for (int i = 0; i < 2; i++)
+    for (int i = 0; i < MT; i++)
 #pragma unroll
         for (int j = 0; j < 2; j++)
 #pragma unroll
@@ -1175,8 +1181,10 @@ __global__ __launch_bounds__(256, 2) void qfc23_kernel(Fwd a0, Fwd a1, int np) {
         return v;
     };
     constexpr int NKC = HID / 32;
+    if (stg) {
 #pragma unroll
-    for (int pl = 0; pl < NPL; pl++) *reinterpret_cast<bf16x8*>(&As[0][pl][gr][go]) = loadA(0, pl);
+        for (int pl = 0; pl < NPL; pl++) *reinterpret_cast<bf16x8*>(&As[0][pl][gr][go]) = loadA(0, pl);
+    }
     loadB(0, bc);
     __syncthreads();
     for (int kc = 0; kc < NKC; kc++) {
@@ -1188,7 +1196,7 @@ __global__ __launch_bounds__(256, 2) void qfc23_kernel(Fwd a0, Fwd a1, int np) {
             loadB(kc + 1, bn);
         }
 #pragma unroll
-        for (int mt = 0; mt < 2; mt++)
+        for (int mt = 0; mt < MT; mt++)
 #pragma unroll
             for (int s = 0; s < 2; s++) {
                 const bf16x8 av = *reinterpret_cast<const bf16x8*>(&As[buf][0][mt * 32 + (lane & 31)][s * 16 + 8 * h]);
@@ -1208,8 +1216,10 @@ __global__ __launch_bounds__(256, 2) void qfc23_kernel(Fwd a0, Fwd a1, int np) {
                 }
             }
         if (kc + 1 < NKC) {
+            if (stg) {
 #pragma unroll
-            for (int pl = 0; pl < NPL; pl++) *reinterpret_cast<bf16x8*>(&As[buf ^ 1][pl][gr][go]) = an[pl];
+                for (int pl = 0; pl < NPL; pl++) *reinterpret_cast<bf16x8*>(&As[buf ^ 1][pl][gr][go]) = an[pl];
+            }
 #pragma unroll
             for (int pl = 0; pl < NPL; pl++)
 #pragma unroll
@@ -1221,9 +1231,9 @@ __global__ __launch_bounds__(256, 2) void qfc23_kernel(Fwd a0, Fwd a1, int np) {
         __syncthreads();
     }
     if constexpr (X3) {
-        fc3t_x3(a, acc, W3s, reinterpret_cast<float*>(sm23), m0, false);  // the A stages are free
+        fc3t_x3<MT>(a, acc, W3s, reinterpret_cast<float*>(sm23), m0, false);  // the A stages are free
         return;
-    }
+    } else {
     // H2 = relu(acc + b2) -> LDS (and HBM for the learner)
 #pragma unroll
     for (int nt = 0; nt < 2; nt++) {
@@ -1242,6 +1252,7 @@ __global__ __launch_bounds__(256, 2) void qfc23_kernel(Fwd a0, Fwd a1, int np) {
     }
     __syncthreads();
     fc3_act(a, &Hs[gr][0], W3s, m0 + gr, rowok);
+    }
 }
 
 // f32 parameters -> bf16 copies: W1 (compact K, w1_tile order) + the folded fc1 bias,
@@ -2267,7 +2278,13 @@ static int launch_fwd(const evxm::Fwd& a0, const evxm::Fwd& a1, int32_t n, int p
             hipLaunchKernelGGL((evxm::qfc1_kernel<2, 1, 4, true>), dim3(blocks, 4, pairs), dim3(256), 0, st, a0, a1, pairs);
         int rc = mlaunch("qfc1");
         if (rc || !fc23) return rc;
-        hipLaunchKernelGGL(evxm::qfc23_kernel<true>, dim3(blocks, 1, pairs), dim3(256), 0, st, a0, a1, pairs);
+        // 32-row tiles while 64-row ones would leave CUs without a workgroup (cfg2's B = 4096: learn
+        // 0.133 -> 0.128 ms; fc1 in 32 x 64 tiles of 2 waves for small problems measured slower)
+        if ((int64_t)blocks * pairs < 256)
+            hipLaunchKernelGGL((evxm::qfc23_kernel<true, false, 1>), dim3((n + 31) / 32, 1, pairs), dim3(256), 0, st, a0, a1,
+                               pairs);
+        else
+            hipLaunchKernelGGL(evxm::qfc23_kernel<true>, dim3(blocks, 1, pairs), dim3(256), 0, st, a0, a1, pairs);
         return mlaunch("qfc23");
     }
     if (big * pairs >= 384)  // enough 128-row tiles (all 512 columns each) to fill the chip
