@@ -947,6 +947,158 @@ int gemm_slices(const evx_gemm_desc* g, int64_t ws_cap, int* klen_out) {
     return S;
 }
 
+}  // namespace
+namespace evxq {
+// 3x3 convolution forward (padding 1, 11x11 maps, x3) of one image per workgroup
+// (agents/dqn_agent.py:22-24,48-50: conv1 6 -> 32, conv2 32 -> 64, conv3 64 -> 128 channels, each
+// + bias, ReLU). The image's input is staged ONCE in LDS as bf16 hi / lo planes over a 13x13
+// zero-bordered grid (channels padded to CP, a multiple of 16), so each of the 9 taps reads its
+// shifted A fragments straight from LDS -- no per-element bounds tests or global gathers per tap
+// and K tile as in gemm128x3_kernel<CV_FWD>. Output pixels are 4 row tiles of 32 (121 live), the
+// NT = Cout / 32 column tiles are dealt to the 4 waves (wave w: column tile w % NT, NT row tiles);
+// K = 9 taps x CP channels in 16-deep steps, tap-major like the generic kernel. B fragments come
+// pre-split from conv_wpack_kernel (one contiguous 1-KB hi and lo block per wave and k-step, two
+// k-steps ahead). x3 products (hi*hi + hi*lo + lo*hi), f32 accumulation; the epilogue adds the
+// bias, applies ReLU and stores pixel-major rows Y[img * 121 + p][n].
+// Weights packed per call (the caller's workspace, per stream tag): fragment (nt, ks) lane l holds
+// W[n = 32 nt + (l & 31)][c][tap] for tap = ks / (CP / 16), c = 16 (ks % (CP / 16)) + 8 (l >> 5)
+// + e, e < 8 (0 past Cin), as bf16 hi at wp[((nt * KS + ks) * 64 + l) * 8 + e] and lo NT * KS *
+// 512 bf16 further.
+template <int CP>
+__global__ __launch_bounds__(256) void conv_wpack_kernel(const float* __restrict__ W, int64_t sbk, int64_t sbn, int cin,
+                                                         int NT, __bf16* __restrict__ wp) {
+    constexpr int KS = 9 * CP / 16;
+    const int i = (int)(blockIdx.x * 256 + threadIdx.x);
+    if (i >= NT * KS * 64) return;
+    const int l = i & 63, f = i >> 6, ks = f % KS, nt = f / KS;
+    const int n = nt * 32 + (l & 31), tap = ks / (CP / 16), c0 = (ks - tap * (CP / 16)) * 16 + 8 * (l >> 5);
+    bf16x8 hi, lo;
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+        const float v = c0 + e < cin ? W[(int64_t)n * sbn + (int64_t)(c0 + e) * sbk + tap] : 0.f;
+        const __bf16 h = (__bf16)v;
+        hi[e] = h;
+        lo[e] = (__bf16)(v - (float)h);
+    }
+    *reinterpret_cast<bf16x8*>(wp + (size_t)i * 8) = hi;
+    *reinterpret_cast<bf16x8*>(wp + (size_t)(NT * KS * 64 + i) * 8) = lo;
+}
+template <int CP, int NT>
+__global__ __launch_bounds__(256, 2) void conv3x3_fwd_x3_kernel(evx_gemm_desc g, int cin, const __bf16* __restrict__ wp) {
+    constexpr int XP = CP + 8;  // LDS row pitch (bf16): 16-B aligned rows, spread banks
+    constexpr int KS = 9 * CP / 16;
+    __shared__ __attribute__((aligned(16))) __bf16 Xs[2][169][XP];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+    const int img = blockIdx.x;
+    const float* __restrict__ X = g.A + (size_t)img * 121 * cin;
+    // stage: every (13x13 cell, channel) of both planes; border cells and padded channels are 0
+    for (int i = tid; i < 169 * CP; i += 256) {
+        const int q = i / CP, c = i - q * CP;
+        const int y = q / 13 - 1, x = q - (q / 13) * 13 - 1;
+        float v = 0.f;
+        if (c < cin && (unsigned)y < 11u && (unsigned)x < 11u) v = X[(y * 11 + x) * cin + c];
+        const __bf16 hi = (__bf16)v;
+        Xs[0][q][c] = hi;
+        Xs[1][q][c] = (__bf16)(v - (float)hi);
+    }
+    const int nt = w % NT, mt0 = (w / NT) * NT;  // this wave: column tile nt, row tiles mt0 .. mt0 + NT - 1
+    const int n = nt * 32 + (lane & 31);         // the lane's output channel (B operand row)
+    int base[NT];                                // LDS cell of the lane's A row at tap offset (0, 0)
+#pragma unroll
+    for (int k = 0; k < NT; k++) {
+        int m = (mt0 + k) * 32 + (lane & 31);
+        m = m < 121 ? m : 0;  // rows 121.. read pixel 0 (their outputs are not stored)
+        const int y = (m * 187) >> 11, x = m - 11 * y;
+        base[k] = (y + 1) * 13 + (x + 1);
+    }
+    f32x16 acc[NT];
+#pragma unroll
+    for (int k = 0; k < NT; k++)
+#pragma unroll
+        for (int r = 0; r < 16; r++) acc[k][r] = 0.f;
+    const __bf16* __restrict__ wh = wp + ((size_t)nt * KS * 64 + lane) * 8;
+    const __bf16* __restrict__ wl = wh + (size_t)NT * KS * 512;
+    bf16x8 bh = *reinterpret_cast<const bf16x8*>(wh), bl = *reinterpret_cast<const bf16x8*>(wl);
+    bf16x8 bh1 = bh, bl1 = bl;
+    if (KS > 1) {
+        bh1 = *reinterpret_cast<const bf16x8*>(wh + 512);
+        bl1 = *reinterpret_cast<const bf16x8*>(wl + 512);
+    }
+    __syncthreads();
+    for (int ks = 0; ks < KS; ks++) {
+        bf16x8 bh2 = bh1, bl2 = bl1;
+        if (ks + 2 < KS) {
+            bh2 = *reinterpret_cast<const bf16x8*>(wh + (size_t)(ks + 2) * 512);
+            bl2 = *reinterpret_cast<const bf16x8*>(wl + (size_t)(ks + 2) * 512);
+        }
+        const int tap = ks / (CP / 16), c0 = (ks - tap * (CP / 16)) * 16 + 8 * h;
+        const int toff = (tap / 3 - 1) * 13 + (tap % 3 - 1);
+#pragma unroll
+        for (int k = 0; k < NT; k++) {
+            const int q = base[k] + toff;
+            const bf16x8 ah = *reinterpret_cast<const bf16x8*>(&Xs[0][q][c0]);
+            const bf16x8 al = *reinterpret_cast<const bf16x8*>(&Xs[1][q][c0]);
+            acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[k], 0, 0, 0);
+            acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[k], 0, 0, 0);
+            acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[k], 0, 0, 0);
+        }
+        bh = bh1;
+        bl = bl1;
+        bh1 = bh2;
+        bl1 = bl2;
+    }
+    const float bias = g.bias ? g.bias[n] : 0.f;
+    const bool relu = (g.flags & EVX_GEMM_RELU) != 0;
+    float* __restrict__ Y = g.C + (size_t)img * 121 * g.ldc + n;
+#pragma unroll
+    for (int k = 0; k < NT; k++)
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+            const int m = (mt0 + k) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            float v = acc[k][r] + bias;
+            if (relu) v = v > 0.f ? v : 0.f;
+            if (m < 121) Y[(size_t)m * g.ldc] = v;
+        }
+}
+}  // namespace evxq
+namespace {
+
+// The LDS-staged conv forward (conv3x3_fwd_x3_kernel) applies to a plain call -- bias / ReLU
+// epilogue, the torch weight layout -- over cfg4's layer shapes; its packed weights need this many
+// floats of workspace (0: not applicable).
+static int conv_fwd_cp(const evx_gemm_desc* g, int cs) {
+    if (g->mask || g->gate || (g->flags & EVX_GEMM_ACCUM) || g->alpha != 1.f) return 0;
+    if (g->sbk != 9 || g->sbn != 9 * cs || g->ldc != g->N || g->M % 121 != 0) return 0;
+    if (cs <= 16 && g->N == 32) return 16;
+    if (cs == 32 && g->N == 64) return 32;
+    if (cs == 64 && g->N == 128) return 64;
+    return 0;
+}
+static int64_t conv_fwd_ws(const evx_gemm_desc* g, int cs) {
+    const int cp = conv_fwd_cp(g, cs);
+    return cp ? (int64_t)(g->N / 32) * (9 * cp / 16) * 512 : 0;
+}
+static bool conv_fwd_direct(const evx_gemm_desc* g, int cs, hipStream_t st) {
+    const int cp = conv_fwd_cp(g, cs);
+    const int64_t need = conv_fwd_ws(g, cs);
+    if (!cp || !g->ws || g->ws_elems < need) return false;
+    const unsigned B = (unsigned)(g->M / 121);
+    const int NT = g->N / 32;
+    __bf16* wp = reinterpret_cast<__bf16*>(g->ws);
+    const unsigned pb = (unsigned)((NT * (9 * cp / 16) * 64 + 255) / 256);
+    if (cp == 16) {
+        hipLaunchKernelGGL(evxq::conv_wpack_kernel<16>, dim3(pb), dim3(256), 0, st, g->B, g->sbk, g->sbn, cs, NT, wp);
+        hipLaunchKernelGGL((evxq::conv3x3_fwd_x3_kernel<16, 1>), dim3(B), dim3(256), 0, st, *g, cs, wp);
+    } else if (cp == 32) {
+        hipLaunchKernelGGL(evxq::conv_wpack_kernel<32>, dim3(pb), dim3(256), 0, st, g->B, g->sbk, g->sbn, cs, NT, wp);
+        hipLaunchKernelGGL((evxq::conv3x3_fwd_x3_kernel<32, 2>), dim3(B), dim3(256), 0, st, *g, cs, wp);
+    } else {
+        hipLaunchKernelGGL(evxq::conv_wpack_kernel<64>, dim3(pb), dim3(256), 0, st, g->B, g->sbk, g->sbn, cs, NT, wp);
+        hipLaunchKernelGGL((evxq::conv3x3_fwd_x3_kernel<64, 4>), dim3(B), dim3(256), 0, st, *g, cs, wp);
+    }
+    return true;
+}
+
 int gemm_launch(const evx_gemm_desc* g, int cm, int cs, void* stream) {
     if (!g || !g->A || !g->B || !g->C) return qfail(-22, "gemm: NULL operand");
     if (g->M <= 0 || g->N <= 0 || g->K <= 0) return 0;
@@ -957,6 +1109,7 @@ int gemm_launch(const evx_gemm_desc* g, int cm, int cs, void* stream) {
     dim3 grid((unsigned)((g->N + TB - 1) / TB), (unsigned)((g->M + TB - 1) / TB), (unsigned)S);
     if (grid.y > 65535u) return qfail(-22, "gemm: M too large for one launch");
     hipStream_t st = (hipStream_t)stream;
+    if (cm == evxq::CV_FWD && S == 1 && conv_fwd_direct(g, cs, st)) return qlaunch("conv3x3 fwd");
     if (cm == evxq::CV_FWD)
         hipLaunchKernelGGL(evxq::gemm128x3_kernel<evxq::CV_FWD>, grid, dim3(256), 0, st, *g, klen, cs);
     else if (cm == evxq::CV_DX)
@@ -987,6 +1140,15 @@ int64_t evx_gemm_ws_elems(const evx_gemm_desc* g) {
     if (!g || g->M <= 0 || g->N <= 0 || g->K <= 0) return 0;
     const int S = gemm_slices(g, INT64_MAX, nullptr);
     return S > 1 ? (int64_t)S * g->M * g->N : 0;
+}
+
+int64_t evx_conv3x3_ws_elems(const evx_gemm_desc* g, int32_t mode, int32_t cs) {
+    if (!g || g->M <= 0 || g->N <= 0 || g->K <= 0 || cs <= 0) return 0;
+    if (mode == EVX_CONV_FWD && g->precision == EVX_PREC_X3) {
+        const int64_t w = conv_fwd_ws(g, cs);
+        if (w > 0) return w;
+    }
+    return evx_gemm_ws_elems(g);
 }
 
 int evx_conv3x3_gemm(const evx_gemm_desc* g, int32_t mode, int32_t cs, void* stream) {

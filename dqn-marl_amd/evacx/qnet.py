@@ -55,6 +55,8 @@ def qlib():
         L.evx_gemm.argtypes = [C.POINTER(evx_gemm_desc), C.c_void_p]
         L.evx_gemm_ws_elems.argtypes = [C.POINTER(evx_gemm_desc)]
         L.evx_gemm_ws_elems.restype = C.c_int64
+        L.evx_conv3x3_ws_elems.argtypes = [C.POINTER(evx_gemm_desc), C.c_int32, C.c_int32]
+        L.evx_conv3x3_ws_elems.restype = C.c_int64
         L.evx_colsum.argtypes = [C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p,
                                  C.c_int32, C.c_void_p]
         L.evx_td_loss.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_float,
@@ -95,16 +97,18 @@ def _p(t):
 _WS_NEED: Dict[Tuple, int] = {}
 
 
-def _attach_ws(d, ws, tag, device):
-    """Split-K workspace of a descriptor (evx_gemm_ws_elems): ws is a _Workspace (a buffer per
-    tag and size, kept for the pool's life, so a stream never sees another stream's scratch
-    freed under it), a f32 tensor, or None (the GEMM runs in one pass)."""
+def _attach_ws(d, ws, tag, device, conv=None):
+    """Workspace of a descriptor (evx_gemm_ws_elems: split-K partials; conv = (mode, channels):
+    evx_conv3x3_ws_elems, which also covers the conv forward's packed weights): ws is a _Workspace
+    (a buffer per tag and size, kept for the pool's life, so a stream never sees another stream's
+    scratch freed or rewritten under it), a f32 tensor, or None (the GEMM runs in one pass)."""
     if ws is None:
         return
-    key = (d.M, d.N, d.K, d.precision, d.flags, bool(d.bias), bool(d.mask), bool(d.gate))
+    key = (d.M, d.N, d.K, d.precision, d.flags, bool(d.bias), bool(d.mask), bool(d.gate), d.sbk, d.sbn, conv)
     need = _WS_NEED.get(key)
     if need is None:
-        need = _WS_NEED[key] = int(qlib().evx_gemm_ws_elems(C.byref(d)))
+        need = _WS_NEED[key] = int(qlib().evx_conv3x3_ws_elems(C.byref(d), conv[0], conv[1]) if conv
+                                   else qlib().evx_gemm_ws_elems(C.byref(d)))
     if need <= 0:
         return
     if isinstance(ws, torch.Tensor):
@@ -134,7 +138,7 @@ def conv_gemm(mode, M, N, K, A, B, Cm, cs, sam=0, sak=0, sbk=0, sbn=0, bias=None
     d = evx_gemm_desc(M=M, N=N, K=K, precision=PREC["x3"], flags=RELU if relu else 0, alpha=1.0, A=_p(A),
                       sam=sam, sak=sak, B=_p(B), sbk=sbk, sbn=sbn, C=_p(Cm), ldc=N, bias=_p(bias), mask=None,
                       ldm=0, mask_scale=1.0, gate=_p(gate), ldg=ldg)
-    _attach_ws(d, ws, tag, Cm.device)
+    _attach_ws(d, ws, tag + f"cv{mode}_", Cm.device, conv=(mode, cs))
     qcheck(qlib().evx_conv3x3_gemm(C.byref(d), mode, cs, _stream()), "evx_conv3x3_gemm")
 
 
