@@ -949,21 +949,30 @@ int gemm_slices(const evx_gemm_desc* g, int64_t ws_cap, int* klen_out) {
 
 }  // namespace
 namespace evxq {
-// 3x3 convolution forward (padding 1, 11x11 maps, x3) of one image per workgroup
+// 3x3 convolution (padding 1, 11x11 maps, x3) of one image per workgroup, forward or dX
 // (agents/dqn_agent.py:22-24,48-50: conv1 6 -> 32, conv2 32 -> 64, conv3 64 -> 128 channels, each
-// + bias, ReLU). The image's input is staged ONCE in LDS as bf16 hi / lo planes over a 13x13
-// zero-bordered grid (channels padded to CP, a multiple of 16), so each of the 9 taps reads its
-// shifted A fragments straight from LDS -- no per-element bounds tests or global gathers per tap
-// and K tile as in gemm128x3_kernel<CV_FWD>. Output pixels are 4 row tiles of 32 (121 live), the
-// NT = Cout / 32 column tiles are dealt to the 4 waves (wave w: column tile w % NT, NT row tiles);
-// K = 9 taps x CP channels in 16-deep steps, tap-major like the generic kernel. B fragments come
-// pre-split from conv_wpack_kernel (one contiguous 1-KB hi and lo block per wave and k-step, two
-// k-steps ahead). x3 products (hi*hi + hi*lo + lo*hi), f32 accumulation; the epilogue adds the
-// bias, applies ReLU and stores pixel-major rows Y[img * 121 + p][n].
-// Weights packed per call (the caller's workspace, per stream tag): fragment (nt, ks) lane l holds
-// W[n = 32 nt + (l & 31)][c][tap] for tap = ks / (CP / 16), c = 16 (ks % (CP / 16)) + 8 (l >> 5)
-// + e, e < 8 (0 past Cin), as bf16 hi at wp[((nt * KS + ks) * 64 + l) * 8 + e] and lo NT * KS *
-// 512 bf16 further.
+// + bias, ReLU; the backward's dX = dY (*) flip(W) with the lower layer's ReLU gate). The image
+// (the layer input, or dY for dX) is staged in LDS as bf16 hi / lo planes over a 13x13
+// zero-bordered grid, CB <= 64 channels at a time (channels padded to CP, a multiple of 16), so
+// each of the 9 taps reads its shifted A fragments straight from LDS -- no per-element bounds tests
+// or global gathers per tap and K tile as in gemm128x3_kernel<CV_FWD / CV_DX>. Output pixels are 4
+// row tiles of 32 (121 live), the NT = N / 32 column tiles are dealt to the 4 waves (wave w: column
+// tile w % NT, NT row tiles); K = channel blocks x 9 taps x CB channels in 16-deep steps. B
+// fragments come pre-split from conv_wpack_kernel (a contiguous 1-KB hi and lo block per wave and
+// k-step, two k-steps ahead). x3 products (hi*hi + hi*lo + lo*hi), f32 accumulation. Epilogue:
+// forward -- bias, ReLU; dX -- the gate (the lower layer's output > 0); pixel-major rows
+// C[img * 121 + p][n].
+// Weights packed per call (the caller's workspace, per stream tag): k-step ks = (b * 9 + tap) *
+// (CB / 16) + j, fragment (nt, ks) lane l holds W[n = 32 nt + (l & 31)][c][tap] (forward: sbn, sbk
+// the torch strides; dX: c the dY channel) for c = b CB + 16 j + 8 (l >> 5) + e, e < 8 (0 past the
+// staged channels), as bf16 hi at wp[((nt * KS + ks) * 64 + l) * 8 + e], lo NT * KS * 512 further.
+template <int CP>
+__device__ __forceinline__ void conv_kstep(int ks, int h, int& tap, int& c0) {
+    constexpr int CB = CP > 64 ? 64 : CP, KJ = CB / 16;
+    const int b = ks / (9 * KJ), r = ks - b * 9 * KJ;
+    tap = r / KJ;
+    c0 = b * CB + (r - tap * KJ) * 16 + 8 * h;
+}
 template <int CP>
 __global__ __launch_bounds__(256) void conv_wpack_kernel(const float* __restrict__ W, int64_t sbk, int64_t sbn, int cin,
                                                          int NT, __bf16* __restrict__ wp) {
@@ -971,7 +980,9 @@ __global__ __launch_bounds__(256) void conv_wpack_kernel(const float* __restrict
     const int i = (int)(blockIdx.x * 256 + threadIdx.x);
     if (i >= NT * KS * 64) return;
     const int l = i & 63, f = i >> 6, ks = f % KS, nt = f / KS;
-    const int n = nt * 32 + (l & 31), tap = ks / (CP / 16), c0 = (ks - tap * (CP / 16)) * 16 + 8 * (l >> 5);
+    const int n = nt * 32 + (l & 31);
+    int tap, c0;
+    conv_kstep<CP>(ks, l >> 5, tap, c0);
     bf16x8 hi, lo;
 #pragma unroll
     for (int e = 0; e < 8; e++) {
@@ -983,24 +994,29 @@ __global__ __launch_bounds__(256) void conv_wpack_kernel(const float* __restrict
     *reinterpret_cast<bf16x8*>(wp + (size_t)i * 8) = hi;
     *reinterpret_cast<bf16x8*>(wp + (size_t)(NT * KS * 64 + i) * 8) = lo;
 }
-template <int CP, int NT>
-__global__ __launch_bounds__(256, 2) void conv3x3_fwd_x3_kernel(evx_gemm_desc g, int cin, const __bf16* __restrict__ wp) {
-    constexpr int XP = CP + 8;  // LDS row pitch (bf16): 16-B aligned rows, spread banks
-    constexpr int KS = 9 * CP / 16;
+template <int CP, int NT, bool DX>
+__global__ __launch_bounds__(256, 2) void conv3x3_x3_kernel(evx_gemm_desc g, int cin, const __bf16* __restrict__ wp) {
+    constexpr int CB = CP > 64 ? 64 : CP, NB = CP / CB;
+    constexpr int XP = CB + 8;  // LDS row pitch (bf16): 16-B aligned rows, spread banks
+    constexpr int KSB = 9 * CB / 16, KS = NB * KSB;
     __shared__ __attribute__((aligned(16))) __bf16 Xs[2][169][XP];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
     const int img = blockIdx.x;
     const float* __restrict__ X = g.A + (size_t)img * 121 * cin;
-    // stage: every (13x13 cell, channel) of both planes; border cells and padded channels are 0
-    for (int i = tid; i < 169 * CP; i += 256) {
-        const int q = i / CP, c = i - q * CP;
-        const int y = q / 13 - 1, x = q - (q / 13) * 13 - 1;
-        float v = 0.f;
-        if (c < cin && (unsigned)y < 11u && (unsigned)x < 11u) v = X[(y * 11 + x) * cin + c];
-        const __bf16 hi = (__bf16)v;
-        Xs[0][q][c] = hi;
-        Xs[1][q][c] = (__bf16)(v - (float)hi);
-    }
+    // stage channel block b: every (13x13 cell, channel) of both planes; border cells and padded
+    // channels are 0
+    auto stage = [&](int b) {
+        for (int i = tid; i < 169 * CB; i += 256) {
+            const int q = i / CB, c = i - q * CB;
+            const int y = q / 13 - 1, x = q - (q / 13) * 13 - 1;
+            float v = 0.f;
+            if (b * CB + c < cin && (unsigned)y < 11u && (unsigned)x < 11u) v = X[(y * 11 + x) * cin + b * CB + c];
+            const __bf16 hi = (__bf16)v;
+            Xs[0][q][c] = hi;
+            Xs[1][q][c] = (__bf16)(v - (float)hi);
+        }
+    };
+    stage(0);
     const int nt = w % NT, mt0 = (w / NT) * NT;  // this wave: column tile nt, row tiles mt0 .. mt0 + NT - 1
     const int n = nt * 32 + (lane & 31);         // the lane's output channel (B operand row)
     int base[NT];                                // LDS cell of the lane's A row at tap offset (0, 0)
@@ -1026,13 +1042,20 @@ __global__ __launch_bounds__(256, 2) void conv3x3_fwd_x3_kernel(evx_gemm_desc g,
     }
     __syncthreads();
     for (int ks = 0; ks < KS; ks++) {
+        if (NB > 1 && ks > 0 && ks % KSB == 0) {  // the next channel block
+            __syncthreads();
+            stage(ks / KSB);
+            __syncthreads();
+        }
         bf16x8 bh2 = bh1, bl2 = bl1;
         if (ks + 2 < KS) {
             bh2 = *reinterpret_cast<const bf16x8*>(wh + (size_t)(ks + 2) * 512);
             bl2 = *reinterpret_cast<const bf16x8*>(wl + (size_t)(ks + 2) * 512);
         }
-        const int tap = ks / (CP / 16), c0 = (ks - tap * (CP / 16)) * 16 + 8 * h;
-        const int toff = (tap / 3 - 1) * 13 + (tap % 3 - 1);
+        int tap, c0;
+        conv_kstep<CP>(ks, h, tap, c0);
+        c0 -= (ks / KSB) * CB;  // channel within the staged block
+        const int toff = (DX ? -1 : 1) * ((tap / 3 - 1) * 13 + (tap % 3 - 1));
 #pragma unroll
         for (int k = 0; k < NT; k++) {
             const int q = base[k] + toff;
@@ -1047,54 +1070,64 @@ __global__ __launch_bounds__(256, 2) void conv3x3_fwd_x3_kernel(evx_gemm_desc g,
         bh1 = bh2;
         bl1 = bl2;
     }
-    const float bias = g.bias ? g.bias[n] : 0.f;
-    const bool relu = (g.flags & EVX_GEMM_RELU) != 0;
+    const float bias = !DX && g.bias ? g.bias[n] : 0.f;
+    const bool relu = !DX && (g.flags & EVX_GEMM_RELU) != 0;
     float* __restrict__ Y = g.C + (size_t)img * 121 * g.ldc + n;
+    const float* __restrict__ gate = DX && g.gate ? g.gate + (size_t)img * 121 * g.ldg + n : nullptr;
 #pragma unroll
     for (int k = 0; k < NT; k++)
 #pragma unroll
         for (int r = 0; r < 16; r++) {
             const int m = (mt0 + k) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (m >= 121) continue;
             float v = acc[k][r] + bias;
             if (relu) v = v > 0.f ? v : 0.f;
-            if (m < 121) Y[(size_t)m * g.ldc] = v;
+            if (gate) v = gate[(size_t)m * g.ldg] > 0.f ? v : 0.f;
+            Y[(size_t)m * g.ldc] = v;
         }
 }
 }  // namespace evxq
 namespace {
 
-// The LDS-staged conv forward (conv3x3_fwd_x3_kernel) applies to a plain call -- bias / ReLU
-// epilogue, the torch weight layout -- over cfg4's layer shapes; its packed weights need this many
-// floats of workspace (0: not applicable).
-static int conv_fwd_cp(const evx_gemm_desc* g, int cs) {
-    if (g->mask || g->gate || (g->flags & EVX_GEMM_ACCUM) || g->alpha != 1.f) return 0;
-    if (g->sbk != 9 || g->sbn != 9 * cs || g->ldc != g->N || g->M % 121 != 0) return 0;
-    if (cs <= 16 && g->N == 32) return 16;
-    if (cs == 32 && g->N == 64) return 32;
-    if (cs == 64 && g->N == 128) return 64;
+// The LDS-staged conv kernels (conv3x3_x3_kernel) apply to plain calls -- forward: bias / ReLU
+// epilogue and the torch weight layout; dX: the ReLU gate -- over cfg4's layer shapes; CP of the
+// staged channels (0: not applicable). Their packed weights need conv_direct_ws floats of workspace.
+static int conv_direct_cp(const evx_gemm_desc* g, int mode, int cs) {
+    if (g->mask || (g->flags & EVX_GEMM_ACCUM) || g->alpha != 1.f || g->ldc != g->N || g->M % 121 != 0) return 0;
+    if (mode == EVX_CONV_FWD) {
+        if (g->gate || g->sbk != 9 || g->sbn != 9 * cs) return 0;
+        if (cs <= 16 && g->N == 32) return 16;
+        if (cs == 32 && g->N == 64) return 32;
+        if (cs == 64 && g->N == 128) return 64;
+    } else if (mode == EVX_CONV_DX) {
+        if (g->bias || (g->flags & EVX_GEMM_RELU) || g->sbn != 9 || g->sbk != 9 * (int64_t)g->N) return 0;
+        if (cs == 64 && g->N == 32) return 64;
+        if (cs == 128 && g->N == 64) return 128;
+    }
     return 0;
 }
-static int64_t conv_fwd_ws(const evx_gemm_desc* g, int cs) {
-    const int cp = conv_fwd_cp(g, cs);
+static int64_t conv_direct_ws(const evx_gemm_desc* g, int mode, int cs) {
+    const int cp = conv_direct_cp(g, mode, cs);
     return cp ? (int64_t)(g->N / 32) * (9 * cp / 16) * 512 : 0;
 }
-static bool conv_fwd_direct(const evx_gemm_desc* g, int cs, hipStream_t st) {
-    const int cp = conv_fwd_cp(g, cs);
-    const int64_t need = conv_fwd_ws(g, cs);
-    if (!cp || !g->ws || g->ws_elems < need) return false;
-    const unsigned B = (unsigned)(g->M / 121);
-    const int NT = g->N / 32;
+template <int CP, int NT, bool DX>
+static void conv_direct_launch(const evx_gemm_desc* g, int cs, __bf16* wp, hipStream_t st) {
+    const unsigned pb = (unsigned)((NT * (9 * CP / 16) * 64 + 255) / 256);
+    hipLaunchKernelGGL(evxq::conv_wpack_kernel<CP>, dim3(pb), dim3(256), 0, st, g->B, g->sbk, g->sbn, cs, NT, wp);
+    hipLaunchKernelGGL((evxq::conv3x3_x3_kernel<CP, NT, DX>), dim3((unsigned)(g->M / 121)), dim3(256), 0, st, *g, cs,
+                       (const __bf16*)wp);
+}
+static bool conv_direct(const evx_gemm_desc* g, int mode, int cs, hipStream_t st) {
+    const int cp = conv_direct_cp(g, mode, cs);
+    if (!cp || !g->ws || g->ws_elems < conv_direct_ws(g, mode, cs)) return false;
     __bf16* wp = reinterpret_cast<__bf16*>(g->ws);
-    const unsigned pb = (unsigned)((NT * (9 * cp / 16) * 64 + 255) / 256);
-    if (cp == 16) {
-        hipLaunchKernelGGL(evxq::conv_wpack_kernel<16>, dim3(pb), dim3(256), 0, st, g->B, g->sbk, g->sbn, cs, NT, wp);
-        hipLaunchKernelGGL((evxq::conv3x3_fwd_x3_kernel<16, 1>), dim3(B), dim3(256), 0, st, *g, cs, wp);
-    } else if (cp == 32) {
-        hipLaunchKernelGGL(evxq::conv_wpack_kernel<32>, dim3(pb), dim3(256), 0, st, g->B, g->sbk, g->sbn, cs, NT, wp);
-        hipLaunchKernelGGL((evxq::conv3x3_fwd_x3_kernel<32, 2>), dim3(B), dim3(256), 0, st, *g, cs, wp);
+    if (mode == EVX_CONV_FWD) {
+        if (cp == 16) conv_direct_launch<16, 1, false>(g, cs, wp, st);
+        else if (cp == 32) conv_direct_launch<32, 2, false>(g, cs, wp, st);
+        else conv_direct_launch<64, 4, false>(g, cs, wp, st);
     } else {
-        hipLaunchKernelGGL(evxq::conv_wpack_kernel<64>, dim3(pb), dim3(256), 0, st, g->B, g->sbk, g->sbn, cs, NT, wp);
-        hipLaunchKernelGGL((evxq::conv3x3_fwd_x3_kernel<64, 4>), dim3(B), dim3(256), 0, st, *g, cs, wp);
+        if (cp == 64) conv_direct_launch<64, 1, true>(g, cs, wp, st);
+        else conv_direct_launch<128, 2, true>(g, cs, wp, st);
     }
     return true;
 }
@@ -1109,7 +1142,7 @@ int gemm_launch(const evx_gemm_desc* g, int cm, int cs, void* stream) {
     dim3 grid((unsigned)((g->N + TB - 1) / TB), (unsigned)((g->M + TB - 1) / TB), (unsigned)S);
     if (grid.y > 65535u) return qfail(-22, "gemm: M too large for one launch");
     hipStream_t st = (hipStream_t)stream;
-    if (cm == evxq::CV_FWD && S == 1 && conv_fwd_direct(g, cs, st)) return qlaunch("conv3x3 fwd");
+    if ((cm == evxq::CV_FWD || cm == evxq::CV_DX) && S == 1 && conv_direct(g, cm, cs, st)) return qlaunch("conv3x3");
     if (cm == evxq::CV_FWD)
         hipLaunchKernelGGL(evxq::gemm128x3_kernel<evxq::CV_FWD>, grid, dim3(256), 0, st, *g, klen, cs);
     else if (cm == evxq::CV_DX)
@@ -1144,8 +1177,8 @@ int64_t evx_gemm_ws_elems(const evx_gemm_desc* g) {
 
 int64_t evx_conv3x3_ws_elems(const evx_gemm_desc* g, int32_t mode, int32_t cs) {
     if (!g || g->M <= 0 || g->N <= 0 || g->K <= 0 || cs <= 0) return 0;
-    if (mode == EVX_CONV_FWD && g->precision == EVX_PREC_X3) {
-        const int64_t w = conv_fwd_ws(g, cs);
+    if (g->precision == EVX_PREC_X3) {
+        const int64_t w = conv_direct_ws(g, mode, cs);
         if (w > 0) return w;
     }
     return evx_gemm_ws_elems(g);

@@ -225,10 +225,10 @@ int64_t evx_gemm_ws_elems(const evx_gemm_desc *g);
 #define EVX_CONV_DX 2
 #define EVX_CONV_DW 3
 int evx_conv3x3_gemm(const evx_gemm_desc *g, int32_t mode, int32_t cs, void *stream);
-/* Workspace floats (evx_gemm_desc.ws / ws_elems) an evx_conv3x3_gemm call can use: the forward's
-   LDS-staged kernel (bias / ReLU epilogue over cfg4's layer shapes) packs the weights there as
-   bf16 hi / lo MFMA fragments; otherwise the split-K partials of evx_gemm_ws_elems. Without it the
-   call runs the generic implicit-GEMM kernel. */
+/* Workspace floats (evx_gemm_desc.ws / ws_elems) an evx_conv3x3_gemm call can use: the LDS-staged
+   forward (bias / ReLU epilogue) and dX (ReLU gate) kernels over cfg4's layer shapes pack the
+   weights there as bf16 hi / lo MFMA fragments; otherwise the split-K partials of
+   evx_gemm_ws_elems. Without it the call runs the generic implicit-GEMM kernel. */
 int64_t evx_conv3x3_ws_elems(const evx_gemm_desc *g, int32_t mode, int32_t cs);
 /* out[n] (+)= sum_m X[m*ld+n] (bias gradients), fixed summation order */
 int evx_colsum(const float *X, int64_t ld, int32_t M, int32_t N, float *out, int32_t accum, float *scratch,
