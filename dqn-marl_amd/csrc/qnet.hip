@@ -870,18 +870,35 @@ __global__ __launch_bounds__(256) void col2im_kernel(const float* __restrict__ d
     dx[gid] = s;
 }
 
-// [B*121][C] (GEMM output, pixel-major) <-> [B][C][121] (NCHW)
+// [B*121][C] (GEMM output, pixel-major) <-> [B][C][121] (NCHW): one workgroup per b, its 121 C
+// values read contiguously into LDS (pixel rows padded to C + 1 words: the column reads of the
+// pixel-major side hit distinct banks) and written back contiguously in the other order
 __global__ __launch_bounds__(256) void pix2nchw_kernel(const float* __restrict__ src, int B, int C, int to_nchw,
                                                        float* __restrict__ dst) {
-    const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int64_t total = (int64_t)B * C * 121;
-    if (gid >= total) return;
-    const int b = (int)(gid / (C * 121));
-    const int rem = (int)(gid - (int64_t)b * C * 121);
-    const int c = rem / 121, pix = rem - c * 121;
-    const int64_t pm = ((int64_t)b * 121 + pix) * C + c;
-    if (to_nchw) dst[gid] = src[pm];
-    else dst[pm] = src[gid];
+    extern __shared__ float tl[];  // [121][C + 1]
+    const int n = 121 * C;
+    const float* __restrict__ s = src + (size_t)blockIdx.x * n;
+    float* __restrict__ d = dst + (size_t)blockIdx.x * n;
+    for (int j = threadIdx.x; j < n; j += 256) {
+        const float v = s[j];
+        if (to_nchw) {  // s: pixel-major (p * C + c)
+            const int p = j / C, c = j - p * C;
+            tl[p * (C + 1) + c] = v;
+        } else {  // s: NCHW (c * 121 + p)
+            const int c = j / 121, p = j - c * 121;
+            tl[p * (C + 1) + c] = v;
+        }
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < n; j += 256) {
+        if (to_nchw) {  // d: NCHW
+            const int c = j / 121, p = j - c * 121;
+            d[j] = tl[p * (C + 1) + c];
+        } else {  // d: pixel-major
+            const int p = j / C, c = j - p * C;
+            d[j] = tl[p * (C + 1) + c];
+        }
+    }
 }
 
 // dy[i] = y[i] > 0 ? dy[i] : 0 (ReLU backward for outputs that do not come out of a GEMM)
@@ -1392,7 +1409,9 @@ int evx_relu_grad(float* dy, const float* y, int64_t n, void* stream) {
 int evx_pix_nchw(const float* src, int32_t B, int32_t C, int32_t to_nchw, float* dst, void* stream) {
     const int64_t total = (int64_t)B * C * 121;
     if (total <= 0) return 0;
-    hipLaunchKernelGGL(evxq::pix2nchw_kernel, dim3(nblk(total)), dim3(256), 0, (hipStream_t)stream, src, B, C, to_nchw,
+    const size_t lds = (size_t)121 * (C + 1) * 4;
+    if (lds > 64 * 1024) return qfail(-22, "pix_nchw: C > 134 channels");
+    hipLaunchKernelGGL(evxq::pix2nchw_kernel, dim3((unsigned)B), dim3(256), lds, (hipStream_t)stream, src, B, C, to_nchw,
                        dst);
     return qlaunch("pix_nchw");
 }

@@ -343,6 +343,7 @@ int evx_gather_obs(const evx_obs *src, const int64_t *idx, int32_t n, evx_obs *d
 /* DQNNetwork conv layers (agents/dqn_agent.py:22-24) as im2col + GEMM on 11x11 maps */
 int evx_im2col3x3(const float *x, int32_t B, int32_t C, int32_t nhwc, float *cols, void *stream);
 int evx_col2im3x3(const float *dcols, int32_t B, int32_t C, float *dx, void *stream);
+/* [B*121][C] pixel-major <-> [B][C][121] NCHW (to_nchw), C <= 134 */
 int evx_pix_nchw(const float *src, int32_t B, int32_t C, int32_t to_nchw, float *dst, void *stream);
 int evx_relu_grad(float *dy, const float *y, int64_t n, void *stream);
 const char *evx_q_last_error(void);
