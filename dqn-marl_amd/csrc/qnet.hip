@@ -514,6 +514,48 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(evx_gemm_desc g, int
     }
 }
 
+// splitk_reduce_kernel for many slices (S >= 8, M N a multiple of 4): a workgroup takes 64 float4
+// of C, each wave sums a contiguous quarter of the slices (in slice order) and wave 0 adds the four
+// quarter sums in order -- 4x the workgroups and a quarter of the dependent loads per thread of
+// the one-thread-per-float4 form (the conv weight gradients: S ~ 100 slices of a 73 728-float C)
+__global__ __launch_bounds__(256) void splitk_reduce4_kernel(evx_gemm_desc g, int S) {
+    __shared__ float4 part[3][64];
+    const int64_t MN = (int64_t)g.M * g.N;
+    const int q = (int)threadIdx.x >> 6, l = (int)threadIdx.x & 63;
+    const int64_t i0 = ((int64_t)blockIdx.x * 64 + l) * 4;
+    const bool live = i0 < MN;
+    const int z0 = q * S / 4, z1 = (q + 1) * S / 4;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (live) {
+        a = *reinterpret_cast<const float4*>(g.ws + (int64_t)z0 * MN + i0);
+        for (int z = z0 + 1; z < z1; z++) {
+            const float4 b = *reinterpret_cast<const float4*>(g.ws + (int64_t)z * MN + i0);
+            a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+        }
+    }
+    if (q) part[q - 1][l] = a;
+    __syncthreads();
+    if (q || !live) return;
+    float v[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const float4 b = part[k][l];
+        v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+    }
+    for (int j = 0; j < 4; j++) {
+        const int64_t i = i0 + j;
+        const int64_t gm = i / g.N;
+        const int gn = (int)(i - gm * g.N);
+        float* cp = g.C + gm * g.ldc + gn;
+        float x = v[j] + (g.bias ? g.bias[gn] : 0.f);
+        if (g.flags & EVX_GEMM_RELU) x = x > 0.f ? x : 0.f;
+        if (g.mask) x = g.mask[gm * g.ldm + gn] ? x * g.mask_scale : 0.f;
+        if (g.gate) x = g.gate[gm * g.ldg + gn] > 0.f ? x : 0.f;
+        if (g.flags & EVX_GEMM_ACCUM) x += *cp;
+        *cp = x;
+    }
+}
+
 // ------------------------------------------------------------- column sums
 // out[n] (+)= sum_m X[m*ld + n], deterministic: fixed-order partials then a fixed-order total.
 // Partials: COLSUM_ROWS rows per chunk; a block covers 64 columns x 4 chunks (the 4 waves), so a
@@ -1175,8 +1217,11 @@ int gemm_launch(const evx_gemm_desc* g, int cm, int cs, void* stream) {
     if (S > 1) {  // the slices' partials summed in slice order, then the epilogue
         const int e = qlaunch("gemm");
         if (e) return e;
-        hipLaunchKernelGGL(evxq::splitk_reduce_kernel, dim3(nblk(((int64_t)g->M * g->N + 3) / 4)), dim3(256), 0, st,
-                           *g, S);
+        const int64_t MN = (int64_t)g->M * g->N;
+        if (S >= 8 && (MN & 3) == 0)
+            hipLaunchKernelGGL(evxq::splitk_reduce4_kernel, dim3((unsigned)((MN / 4 + 63) / 64)), dim3(256), 0, st, *g, S);
+        else
+            hipLaunchKernelGGL(evxq::splitk_reduce_kernel, dim3(nblk((MN + 3) / 4)), dim3(256), 0, st, *g, S);
     }
     return qlaunch("gemm");
 }
