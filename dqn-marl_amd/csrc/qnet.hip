@@ -253,7 +253,9 @@ __global__ __launch_bounds__(256) void gemm128_kernel(evx_gemm_desc g, int kspli
 enum { CV_NONE = 0, CV_FWD = 1, CV_DX = 2, CV_DW = 3 };
 __device__ __forceinline__ uint32_t div121(uint32_t m) { return __umulhi(m, 35495598u); }  // m < 2^26
 __device__ __forceinline__ int div11(int p) { return (p * 187) >> 11; }                     // p < 121
-template <int CM>
+// SPL (CV_NONE, EVX_GEMM_SPLIT_AB): A and B already hold bf16 hi / lo planes, k-contiguous; a
+// K tile is staged as 16-B pieces (2 per thread and plane) with no per-element split
+template <int CM, bool SPL = false>
 __global__ __launch_bounds__(256) void gemm128x3_kernel(evx_gemm_desc g, int ksplit_len, int cs) {
     constexpr int PK = BK + 8;  // row pitch (bf16): 20 words, conflict-free 16-B reads
     __shared__ __attribute__((aligned(16))) __bf16 As[2][TB][PK];
@@ -289,8 +291,32 @@ __global__ __launch_bounds__(256) void gemm128x3_kernel(evx_gemm_desc g, int ksp
         dw_dx = tap - (tap / 3) * 3 - 1;
     }
     const int kp = 2 * (tid & 15), rp = tid >> 4;  // pair layout: k offset, first row
+    bf16x8 sa[2][2], sb[2][2];                     // SPL: [plane][piece], piece i: row (tid + 256 i) >> 2
     auto fetch = [&](int k0) {
-        if constexpr (CM == CV_FWD || CM == CV_DX) {
+        if constexpr (SPL) {
+            const __bf16* ah = reinterpret_cast<const __bf16*>(g.A);
+            const __bf16* bh = reinterpret_cast<const __bf16*>(g.B);
+            const int64_t alo = (int64_t)g.M * g.sam, blo = (int64_t)g.N * g.sbn;
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+                const int pc = tid + 256 * i, row = pc >> 2, kq = k0 + (pc & 3) * 8;
+                const int gm = m0 + row, gn = n0 + row;
+                const bool ka = kq < ke;
+#pragma unroll
+                for (int pl = 0; pl < 2; pl++) {
+                    bf16x8 va, vb;
+#pragma unroll
+                    for (int e = 0; e < 8; e++) {
+                        va[e] = (__bf16)0.f;
+                        vb[e] = (__bf16)0.f;
+                    }
+                    if (ka && gm < g.M) va = *reinterpret_cast<const bf16x8*>(ah + pl * alo + (int64_t)gm * g.sam + kq);
+                    if (ka && gn < g.N) vb = *reinterpret_cast<const bf16x8*>(bh + pl * blo + (int64_t)gn * g.sbn + kq);
+                    sa[pl][i] = va;
+                    sb[pl][i] = vb;
+                }
+            }
+        } else if constexpr (CM == CV_FWD || CM == CV_DX) {
             int64_t toff[2], boff[2];
             int dyq[2], dxq[2];
             bool kin[2];
@@ -391,6 +417,18 @@ __global__ __launch_bounds__(256) void gemm128x3_kernel(evx_gemm_desc g, int ksp
             (uint32_t)__builtin_bit_cast(uint16_t, l0) | ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
     };
     auto stash = [&]() {
+        if constexpr (SPL) {
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+                const int pc = tid + 256 * i, row = pc >> 2, kq = (pc & 3) * 8;
+#pragma unroll
+                for (int pl = 0; pl < 2; pl++) {
+                    *reinterpret_cast<bf16x8*>(&As[pl][row][kq]) = sa[pl][i];
+                    *reinterpret_cast<bf16x8*>(&Bs[pl][row][kq]) = sb[pl][i];
+                }
+            }
+            return;
+        }
         if (a_kc) {
 #pragma unroll
             for (int i = 0; i < 8; i++) put2(As, rp + 16 * i, kp, ra[2 * i], ra[2 * i + 1]);
@@ -943,6 +981,28 @@ __global__ __launch_bounds__(256) void pix2nchw_kernel(const float* __restrict__
     }
 }
 
+// NCHW [B][C][121] -> pixel-major [B][121 * C] bf16 hi / lo planes (evx_pix_split)
+__global__ __launch_bounds__(256) void pix_split_kernel(const float* __restrict__ src, int B, int C,
+                                                        __bf16* __restrict__ dst) {
+    extern __shared__ float tl[];  // [121][C + 1]
+    const int n = 121 * C;
+    const float* __restrict__ s = src + (size_t)blockIdx.x * n;
+    __bf16* __restrict__ d = dst + (size_t)blockIdx.x * n;
+    const size_t lo = (size_t)B * n;
+    for (int j = threadIdx.x; j < n; j += 256) {
+        const int c = j / 121, p = j - c * 121;
+        tl[p * (C + 1) + c] = s[j];
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < n; j += 256) {
+        const int p = j / C, c = j - p * C;
+        const float v = tl[p * (C + 1) + c];
+        const __bf16 hi = (__bf16)v;
+        d[j] = hi;
+        d[j + lo] = (__bf16)(v - (float)hi);
+    }
+}
+
 // dy[i] = y[i] > 0 ? dy[i] : 0 (ReLU backward for outputs that do not come out of a GEMM)
 __global__ __launch_bounds__(256) void relu_grad_kernel(float* __restrict__ dy, const float* __restrict__ y,
                                                         int64_t n) {
@@ -1131,7 +1191,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x3_kernel(evx_gemm_desc g, int
     }
     const float bias = !DX && g.bias ? g.bias[n] : 0.f;
     const bool relu = !DX && (g.flags & EVX_GEMM_RELU) != 0;
+    const bool osp = !DX && (g.flags & EVX_GEMM_OUT_SPLIT) != 0;  // bf16 hi / lo planes
     float* __restrict__ Y = g.C + (size_t)img * 121 * g.ldc + n;
+    __bf16* __restrict__ Yh = reinterpret_cast<__bf16*>(g.C) + (size_t)img * 121 * g.ldc + n;
+    const size_t ylo = (size_t)g.M * g.ldc;
     const float* __restrict__ gate = DX && g.gate ? g.gate + (size_t)img * 121 * g.ldg + n : nullptr;
 #pragma unroll
     for (int k = 0; k < NT; k++)
@@ -1142,7 +1205,13 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x3_kernel(evx_gemm_desc g, int
             float v = acc[k][r] + bias;
             if (relu) v = v > 0.f ? v : 0.f;
             if (gate) v = gate[(size_t)m * g.ldg] > 0.f ? v : 0.f;
-            Y[(size_t)m * g.ldc] = v;
+            if (osp) {
+                const __bf16 hi = (__bf16)v;
+                Yh[(size_t)m * g.ldc] = hi;
+                Yh[(size_t)m * g.ldc + ylo] = (__bf16)(v - (float)hi);
+            } else {
+                Y[(size_t)m * g.ldc] = v;
+            }
         }
 }
 }  // namespace evxq
@@ -1202,6 +1271,13 @@ int gemm_launch(const evx_gemm_desc* g, int cm, int cs, void* stream) {
     if (grid.y > 65535u) return qfail(-22, "gemm: M too large for one launch");
     hipStream_t st = (hipStream_t)stream;
     if ((cm == evxq::CV_FWD || cm == evxq::CV_DX) && S == 1 && conv_direct(g, cm, cs, st)) return qlaunch("conv3x3");
+    if (g->flags & EVX_GEMM_OUT_SPLIT) return qfail(-22, "gemm: OUT_SPLIT needs the LDS-staged conv forward (and its workspace)");
+    if (g->flags & EVX_GEMM_SPLIT_AB) {
+        if (cm != evxq::CV_NONE || g->precision != EVX_PREC_X3 || g->sak != 1 || g->sbk != 1 || (g->K & 7) ||
+            (g->sam & 7) || (g->sbn & 7))
+            return qfail(-22, "gemm: SPLIT_AB needs x3, k-contiguous operands, K and row strides multiples of 8");
+        hipLaunchKernelGGL((evxq::gemm128x3_kernel<evxq::CV_NONE, true>), grid, dim3(256), 0, st, *g, klen, 0);
+    } else
     if (cm == evxq::CV_FWD)
         hipLaunchKernelGGL(evxq::gemm128x3_kernel<evxq::CV_FWD>, grid, dim3(256), 0, st, *g, klen, cs);
     else if (cm == evxq::CV_DX)
@@ -1449,6 +1525,15 @@ int evx_relu_grad(float* dy, const float* y, int64_t n, void* stream) {
     if (n <= 0) return 0;
     hipLaunchKernelGGL(evxq::relu_grad_kernel, dim3(nblk(n)), dim3(256), 0, (hipStream_t)stream, dy, y, n);
     return qlaunch("relu_grad");
+}
+
+int evx_pix_split(const float* src, int32_t B, int32_t C, uint16_t* dst, void* stream) {
+    if (B <= 0 || C <= 0) return 0;
+    const size_t lds = (size_t)121 * (C + 1) * 4;
+    if (lds > 64 * 1024) return qfail(-22, "pix_split: C > 134 channels");
+    hipLaunchKernelGGL(evxq::pix_split_kernel, dim3((unsigned)B), dim3(256), lds, (hipStream_t)stream, src, B, C,
+                       reinterpret_cast<__bf16*>(dst));
+    return qlaunch("pix_split");
 }
 
 int evx_pix_nchw(const float* src, int32_t B, int32_t C, int32_t to_nchw, float* dst, void* stream) {

@@ -25,7 +25,7 @@ from . import _lib
 from .env import _stream
 
 PREC = {"f32": 0, "bf16": 1, "x3": 2}
-RELU, ACCUM = 1, 2
+RELU, ACCUM, SPLIT_AB, OUT_SPLIT = 1, 2, 4, 8
 DROPOUT_P = 0.2
 
 
@@ -79,6 +79,7 @@ def qlib():
         L.evx_im2col3x3.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]
         L.evx_col2im3x3.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]
         L.evx_pix_nchw.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]
+        L.evx_pix_split.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]
         L.evx_relu_grad.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]
         L.evx_conv3x3_gemm.argtypes = [C.POINTER(evx_gemm_desc), C.c_int32, C.c_int32, C.c_void_p]
         _q_inited = True
@@ -121,8 +122,10 @@ def _attach_ws(d, ws, tag, device, conv=None):
 
 
 def gemm(M, N, K, A, sam, sak, B, sbk, sbn, Cm, ldc, precision="f32", bias=None, relu=False, mask=None,
-         ldm=0, mask_scale=1.0, gate=None, ldg=0, accumulate=False, alpha=1.0, ws=None, tag=""):
-    d = evx_gemm_desc(M=M, N=N, K=K, precision=PREC[precision], flags=(RELU if relu else 0) | (ACCUM if accumulate else 0),
+         ldm=0, mask_scale=1.0, gate=None, ldg=0, accumulate=False, alpha=1.0, ws=None, tag="", split_ab=False):
+    """evx_gemm; split_ab: A and B are bf16 hi / lo planes (int16 tensors, x3, k-contiguous)."""
+    d = evx_gemm_desc(M=M, N=N, K=K, precision=PREC[precision],
+                      flags=(RELU if relu else 0) | (ACCUM if accumulate else 0) | (SPLIT_AB if split_ab else 0),
                       alpha=alpha, A=_p(A), sam=sam, sak=sak, B=_p(B), sbk=sbk, sbn=sbn, C=_p(Cm), ldc=ldc,
                       bias=_p(bias), mask=_p(mask), ldm=ldm, mask_scale=mask_scale, gate=_p(gate), ldg=ldg)
     _attach_ws(d, ws, tag, Cm.device)
@@ -133,9 +136,11 @@ CONV_FWD, CONV_DX, CONV_DW = 1, 2, 3
 
 
 def conv_gemm(mode, M, N, K, A, B, Cm, cs, sam=0, sak=0, sbk=0, sbn=0, bias=None, relu=False, gate=None,
-              ldg=0, ws=None, tag=""):
-    """evx_conv3x3_gemm (x3): implicit-GEMM 3x3 conv forward / dX / dW on pixel-major activations."""
-    d = evx_gemm_desc(M=M, N=N, K=K, precision=PREC["x3"], flags=RELU if relu else 0, alpha=1.0, A=_p(A),
+              ldg=0, ws=None, tag="", out_split=False):
+    """evx_conv3x3_gemm (x3): implicit-GEMM 3x3 conv forward / dX / dW on pixel-major activations.
+    out_split: the output as bf16 hi / lo planes (Cm int16 [2][M][N]; the LDS-staged forward)."""
+    d = evx_gemm_desc(M=M, N=N, K=K, precision=PREC["x3"], flags=(RELU if relu else 0) | (OUT_SPLIT if out_split else 0),
+                      alpha=1.0, A=_p(A),
                       sam=sam, sak=sak, B=_p(B), sbk=sbk, sbn=sbn, C=_p(Cm), ldc=N, bias=_p(bias), mask=None,
                       ldm=0, mask_scale=1.0, gate=_p(gate), ldg=ldg)
     _attach_ws(d, ws, tag + f"cv{mode}_", Cm.device, conv=(mode, cs))
@@ -251,12 +256,13 @@ class QNet:
         self.saved = None
 
     # ------------------------------------------------------------ fc stack
-    def _fc_forward(self, X, B, K0, mask, tag, w1=None):
+    def _fc_forward(self, X, B, K0, mask, tag, w1=None, split=False):
+        """split: X and w1 are bf16 hi / lo planes (int16 [2][B][K0], [2][H][K0]) -- the act's fc1."""
         P, ws, dev, H, A = self.P, self.ws, self.device, self.hidden, self.actions
         H1 = ws.get(tag + "h1", (B, H), torch.float32, dev)
         gemm(B, H, K0, X, K0, 1, P["fc1.weight"] if w1 is None else w1, 1, K0, H1, H, self.prec, bias=P["fc1.bias"],
              relu=True,
-             mask=mask, ldm=H, mask_scale=1.0 / (1.0 - DROPOUT_P), ws=self.ws, tag=tag)
+             mask=mask, ldm=H, mask_scale=1.0 / (1.0 - DROPOUT_P), ws=self.ws, tag=tag, split_ab=split)
         H2 = ws.get(tag + "h2", (B, H // 2), torch.float32, dev)
         gemm(B, H // 2, H, H1, H, 1, P["fc2.weight"], 1, H, H2, H // 2, self.prec, bias=P["fc2.bias"], relu=True, ws=self.ws, tag=tag)
         Q = ws.get(tag + "q", (B, A), torch.float32, dev)
@@ -277,12 +283,17 @@ class QNet:
         Mp = B * 121
         ins, cols, ys = [x], [], []
         cur, C_in = x, 6
+        # without saves (the act): conv3's output leaves as bf16 hi / lo planes and fc1 runs on
+        # pre-split operands (EVX_GEMM_SPLIT_AB: its K tiles staged as 16-B copies)
+        split = self.implicit and not save
         for li, (cname, cout) in enumerate([("conv1", 32), ("conv2", 64), ("conv3", 128)]):
             K9 = C_in * 9
             if self.implicit:  # x3: the taps gathered in the GEMM's tile fetch (no im2col buffer)
-                Y = ws.get(tag + f"y{li}", (Mp, cout), torch.float32, dev)
+                osp = split and li == 2
+                Y = ws.get(tag + f"y{li}" + ("s" if osp else ""), (2 * Mp, cout) if osp else (Mp, cout),
+                           torch.int16 if osp else torch.float32, dev)
                 conv_gemm(CONV_FWD, Mp, cout, K9, cur, P[cname + ".weight"], Y, C_in, sbk=9, sbn=K9,
-                          bias=P[cname + ".bias"], relu=True, ws=self.ws, tag=tag)
+                          bias=P[cname + ".bias"], relu=True, ws=self.ws, tag=tag, out_split=osp)
                 cols.append(cur)  # the layer input, gathered again by the dW GEMM
                 ys.append(Y)
                 cur, C_in = Y, cout
@@ -300,6 +311,11 @@ class QNet:
             # against a copy of fc1.weight with its columns in that order (the reference flattens
             # NCHW: column c * 121 + p). The copy is made per forward (31.7 MB, ~20 us) instead of
             # transposing the activations (8192 rows: 507 MB, 0.57 ms).
+            if split:
+                W1s = ws.get(tag + "w1s", (2 * self.hidden, 128 * 121), torch.int16, dev)
+                qcheck(L.evx_pix_split(_p(P["fc1.weight"]), self.hidden, 128, _p(W1s), _stream()), "pix_split")
+                _, _, Q = self._fc_forward(cur, B, 128 * 121, mask, tag, w1=W1s, split=True)
+                return Q
             W1p = ws.get(tag + "w1p", (self.hidden, 128 * 121), torch.float32, dev)
             qcheck(L.evx_pix_nchw(_p(P["fc1.weight"]), self.hidden, 128, 0, _p(W1p), _stream()), "pix_nchw")
             F = cur.view(B, 128 * 121)

@@ -168,6 +168,12 @@ const char *evx_last_error(void);
 #define EVX_PREC_X3 2    /* f32-accurate: bf16 hi + lo operand pairs, hi*hi + hi*lo + lo*hi on the bf16 MFMA */
 #define EVX_GEMM_RELU 1
 #define EVX_GEMM_ACCUM 2
+/* X3 only. SPLIT_AB: A and B hold bf16 hi / lo planes (k-contiguous: sak = sbk = 1; A's lo plane
+ * M*sam elements after its hi plane, B's N*sbn after) -- their staging copies 16-B pieces instead
+ * of splitting f32 per element. OUT_SPLIT (evx_conv3x3_gemm forward, LDS-staged kernel only): C is
+ * written as bf16 hi / lo planes, the lo plane M*ldc elements after the hi plane. */
+#define EVX_GEMM_SPLIT_AB 4
+#define EVX_GEMM_OUT_SPLIT 8
 
 /* C[m][n] = epi(alpha * sum_k A(m,k) B(k,n) + bias[n]) with A(m,k) = A[m*sam + k*sak],
  * B(k,n) = B[k*sbk + n*sbn], C[m*ldc + n]; epilogue order: bias, ReLU, dropout mask
@@ -344,6 +350,9 @@ int evx_gather_obs(const evx_obs *src, const int64_t *idx, int32_t n, evx_obs *d
 int evx_im2col3x3(const float *x, int32_t B, int32_t C, int32_t nhwc, float *cols, void *stream);
 int evx_col2im3x3(const float *dcols, int32_t B, int32_t C, float *dx, void *stream);
 /* [B*121][C] pixel-major <-> [B][C][121] NCHW (to_nchw), C <= 134 */
+/* NCHW [B][C][121] f32 -> pixel-major [B][121*C] as bf16 hi / lo planes (lo B*121*C elements after
+   hi): the x3 operand of an EVX_GEMM_SPLIT_AB GEMM (the conv net's fc1 weights), C <= 134 */
+int evx_pix_split(const float *src, int32_t B, int32_t C, uint16_t *dst, void *stream);
 int evx_pix_nchw(const float *src, int32_t B, int32_t C, int32_t to_nchw, float *dst, void *stream);
 int evx_relu_grad(float *dy, const float *y, int64_t n, void *stream);
 const char *evx_q_last_error(void);
