@@ -1581,6 +1581,27 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
         pre_e[j] = make_uint2(0u, DONEPK);
         if (!WIDE && kept && 64 * j + lane < P) pre_e[j] = ipl[64 * j + lane];
     }
+    // Map.move_robot (envs/map.py:160-201): a robot's candidate cell and whether it may move there
+    // (action in 0..4, inside the robots' range and the map); the cell's validity word is the one
+    // read that depends on the state loads -- issued here, ahead of the MT / rmap LDS stores
+    auto robot_cand = [&](uint32_t rp, int a, int& nx, int& ny) -> bool {
+        const int x = rp_x(rp), y = rp_y(rp);
+        nx = x;
+        ny = y;
+        if (a == 0) nx = x + 1;
+        else if (a == 1) ny = y - 1;
+        else if (a == 2) nx = x - 1;
+        else if (a == 3) ny = y + 1;
+        return a >= 0 && a <= 4 && lay.rx_lo <= nx && nx <= lay.rx_hi && 0 <= ny && ny <= g.W && nx >= 1 &&
+               nx <= g.L && ny >= 1 && ny <= g.W;
+    };
+    int nx_pre = 0, ny_pre = 0;
+    bool ok_pre = false;
+    uint32_t vw_pre = 0u;
+    if (lane < R) {
+        ok_pre = robot_cand(rp_pre, a_pre, nx_pre, ny_pre);
+        if (ok_pre) vw_pre = validg[(nx_pre * GY + ny_pre) >> 5];
+    }
     const uint32_t* grm = st.rmap + (size_t)e * g.RW;
     for (int i0 = 0; i0 < g.RW; i0 += 16 * 64) {
         uint32_t w[16];
@@ -1618,18 +1639,14 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     for (int r = lane; r < R; r += 64) {
         uint32_t rp = r == lane ? rp_pre : st.robots[(size_t)e * R + r];
         const int a = r == lane ? a_pre : actions[(size_t)e * R + r];
-        if (a >= 0 && a <= 4) {
-            const int x = rp_x(rp), y = rp_y(rp);
-            int nx = x, ny = y;
-            if (a == 0) nx = x + 1;
-            else if (a == 1) ny = y - 1;
-            else if (a == 2) nx = x - 1;
-            else if (a == 3) ny = y + 1;
-            const int c = nx * GY + ny;
-            if (lay.rx_lo <= nx && nx <= lay.rx_hi && 0 <= ny && ny <= g.W && nx >= 1 && nx <= g.L && ny >= 1 &&
-                ny <= g.W && ((validg[c >> 5] >> (c & 31)) & 1u))
-                rp = rp_pack(nx, ny);
+        int nx = nx_pre, ny = ny_pre;
+        bool ok = ok_pre;
+        uint32_t vw = vw_pre;
+        if (r != lane) {  // robots beyond the first 64 (R > 64)
+            ok = robot_cand(rp, a, nx, ny);
+            if (ok) vw = validg[(nx * GY + ny) >> 5];
         }
+        if (ok && ((vw >> ((nx * GY + ny) & 31)) & 1u)) rp = rp_pack(nx, ny);
         robots[r] = rp;
         st.robots[(size_t)e * R + r] = rp;
         if (r == 0) valid_a0 = (a >= 0 && a <= 4);
