@@ -2,7 +2,8 @@
 """Microbenchmark of the x3 learn chain (Learner.learn_obs, the trainer's learn step without the
 replay sample) at a bench batch: compact observations of a 128x128 R16 env; prints the mean
 time per learn step from HIP events (run under rocprofv3 for per-kernel times / counters).
-Usage: learn_bench.py [B] [iters]"""
+Usage: learn_bench.py [B] [iters] [table]; table: both nets get their act tables and the
+observations sit at the layout's last fire step, as in VecTrainer's stationary phase."""
 import os
 import sys
 
@@ -30,6 +31,13 @@ def main():
         env.step(torch.randint(0, 5, (E * R,), device="cuda", dtype=torch.int32, generator=g), auto_reset=True)
     lr = Learner(kind="mlp", precision="f32", seed=1, lr=1e-4)
     obs = env.obs.view(-1, 8)
+    if len(sys.argv) > 3 and sys.argv[3] == "table":
+        c = lay.c
+        xr = (max(c.rx_lo, 0), min(c.rx_hi, c.L + 1))
+        lr.fast.attach_static(c, c.L, c.W, c.t_max, x_range=xr)
+        lr.fast_t.attach_static(c, c.L, c.W, c.t_max, x_range=xr)
+        obs = obs.clone()
+        obs[:, 6] = int(c.t_max)
     perm = torch.randperm(E * R, device="cuda", generator=g)
     s, s2 = obs[perm[:B]].contiguous().view(-1), obs[perm[B:2 * B]].contiguous().view(-1)
     a = torch.randint(0, 5, (B,), device="cuda", dtype=torch.int32, generator=g)
