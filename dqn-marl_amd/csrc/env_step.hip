@@ -2138,22 +2138,6 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     // The move plan in HBM is walked 4 x 64 entries at a time, loads first (or, one batch, from
     // the registers its scoring left: lane k's entry is valid iff it moves).
     const bool preg = !WIDE && nbatch <= 1;
-    auto plan_pass = [&](auto&& fn) {
-        if (preg) {
-            fn(rp_en, rp_mov);
-            return;
-        }
-        for (int i0 = 0; i0 < nplan; i0 += 256) {
-            uint2 en[4];
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                en[j] = make_uint2(0u, 0u);
-                if (i0 + 64 * j + lane < nplan) en[j] = plan[i0 + 64 * j + lane];
-            }
-#pragma unroll
-            for (int j = 0; j < 4; j++) fn(en[j], i0 + 64 * j + lane < nplan);
-        }
-    };
 
     // ------------------------- contested targets: groups, shuffle, losers
     int err = 0;
@@ -2259,16 +2243,56 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     }
 
     // --------------------------------------------- execute_move, in order
-    plan_pass([&](const uint2 en, bool ok) {
+    // The word of bitmap b holding bit i. Big grids keep the contested / loser / target / vacated
+    // bitmaps in L2 (agent-scope loads past the L1): both passes below load every word an entry
+    // needs for all (up to 4 x 64) entries of a block before using any -- one round trip per block
+    // instead of two or three per 64 entries.
+    auto bit_w = [&](const uint32_t* b, int i) -> uint32_t {
+        if constexpr (BIGG)
+            return __hip_atomic_load(b + (i >> 5), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+            return b[i >> 5];
+    };
+    auto vac_entry = [&](const uint2 en, bool ok, uint32_t wc, uint32_t wl) {
         if (ok) {
             const int cold = (int)(en.y & 0xffffffu);
             const int t = cold + doff_of(en.y >> 24, GY);
-            const bool cont = any_cont && cb_get(t);
-            const bool win = !cont || !tc_get(lost, (int)en.x);
+            const bool cont = any_cont && ((wc >> (cb_idx(t) & 31)) & 1u);
+            const bool win = !cont || !((wl >> ((int)en.x & 31)) & 1u);
             if (win) atomicOr(&vac[cold >> 5], 1u << (cold & 31));
             if (st.thmap) atomicAdd(&st.thmap[(size_t)e * g.G + (win ? t : cold)], 1);
         }
-    });
+    };
+    if (preg) {
+        uint32_t wc = 0u, wl = 0u;
+        if (rp_mov) {
+            const int t = (int)(rp_en.y & 0xffffffu) + doff_of(rp_en.y >> 24, GY);
+            if (any_cont) wc = bit_w(cbits, cb_idx(t));
+            wl = bit_w(lost, (int)rp_en.x);
+        }
+        vac_entry(rp_en, rp_mov, wc, wl);
+    } else {
+        for (int i0 = 0; i0 < nplan; i0 += 256) {
+            uint2 en[4];
+            uint32_t wc[4], wl[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                en[j] = make_uint2(0u, 0u);
+                if (i0 + 64 * j + lane < nplan) en[j] = plan[i0 + 64 * j + lane];
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                wc[j] = wl[j] = 0u;
+                if (i0 + 64 * j + lane < nplan) {
+                    const int t = (int)(en[j].y & 0xffffffu) + doff_of(en[j].y >> 24, GY);
+                    if (any_cont) wc[j] = bit_w(cbits, cb_idx(t));
+                    wl[j] = bit_w(lost, (int)en[j].x);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) vac_entry(en[j], i0 + 64 * j + lane < nplan, wc[j], wl[j]);
+        }
+    }
     if (lane == 0) misc[0] = 0;
     if constexpr (BIGG) wave_sync(); else wave_fence();  // vac: LDS (big grids: global)
     uint32_t* ev = aux;  // (cell, key) pairs; groups are done
@@ -2276,18 +2300,19 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     // a step with <= 64 movers writes back only the rmap words its winners changed (cold, t)
     const bool rm_dirty = nplan <= 64;
     int dw0 = -1, dw1 = -1;
-    auto exec_entry = [&](const uint2 en, const uint32_t ci, const bool valid) {
+    // bits: the words of the contested, loser, target (cold) and vacated (t) bitmaps (bit_w)
+    auto exec_entry = [&](const uint2 en, const uint32_t ci, const bool valid, const uint4 wb) {
         bool exw = false;
         if (valid) {
             const int p = (int)en.x;
             const int cold = (int)(en.y & 0xffffffu);
             const int dd = (int)(en.y >> 24);
             const int t = cold + doff_of((uint32_t)dd, GY);
-            const bool cont = any_cont && cb_get(t);
-            if (!cont || !tc_get(lost, p)) {
+            const bool cont = any_cont && ((wb.x >> (cb_idx(t) & 31)) & 1u);
+            if (!cont || !((wb.y >> (p & 31)) & 1u)) {
                 const bool ex = (ci >> 1) & 1u;
                 exw = ex;
-                const bool ev_old = tc_get(tbits, cold), ev_new = tc_get(vac, t);
+                const bool ev_old = (wb.z >> (cold & 31)) & 1u, ev_new = (wb.w >> (t & 31)) & 1u;
                 int pf = p;
                 if ((ev_old || ev_new) && cont) pf = find_pf(Lp, ncont, t, pb, p);
                 if (ev_old) {
@@ -2318,24 +2343,35 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
         }
         n_evac_new += __popcll(__ballot(exw));
     };
+    auto exec_words = [&](const uint2 en) -> uint4 {
+        const int cold = (int)(en.y & 0xffffffu);
+        const int t = cold + doff_of(en.y >> 24, GY);
+        return make_uint4(any_cont ? bit_w(cbits, cb_idx(t)) : 0u, bit_w(lost, (int)en.x), bit_w(tbits, cold),
+                          bit_w(vac, t));
+    };
     if (preg) {
-        exec_entry(rp_en, rp_ci, rp_mov);
+        exec_entry(rp_en, rp_ci, rp_mov, rp_mov ? exec_words(rp_en) : make_uint4(0u, 0u, 0u, 0u));
     } else {
         for (int i0 = 0; i0 < nplan; i0 += 256) {
             uint2 en4[4];
             uint32_t ci4[4];
+            uint4 wb4[4];
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 en4[j] = make_uint2(0u, 0u);
                 if (i0 + 64 * j + lane < nplan) en4[j] = plan[i0 + 64 * j + lane];
             }
 #pragma unroll
-            for (int j = 0; j < 4; j++) {  // exit bits of the targets, all in flight
+            for (int j = 0; j < 4; j++) {  // exit bits and bitmap words of the targets, all in flight
                 ci4[j] = 0u;
-                if (i0 + 64 * j + lane < nplan) ci4[j] = lay.cellinfo[(int)(en4[j].y & 0xffffffu) + doff_of(en4[j].y >> 24, GY)];
+                wb4[j] = make_uint4(0u, 0u, 0u, 0u);
+                if (i0 + 64 * j + lane < nplan) {
+                    ci4[j] = lay.cellinfo[(int)(en4[j].y & 0xffffffu) + doff_of(en4[j].y >> 24, GY)];
+                    wb4[j] = exec_words(en4[j]);
+                }
             }
 #pragma unroll
-            for (int j = 0; j < 4; j++) exec_entry(en4[j], ci4[j], i0 + 64 * j + lane < nplan);
+            for (int j = 0; j < 4; j++) exec_entry(en4[j], ci4[j], i0 + 64 * j + lane < nplan, wb4[j]);
         }
     }
     // LDS hand-offs only (the person words are drained below); big grids' bitmaps are global
