@@ -23,6 +23,7 @@ namespace evxq {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BM = 64, BN = 64, BK = 32;
 
@@ -1125,6 +1126,27 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x3_kernel(evx_gemm_desc g, int
     // stage channel block b: every (13x13 cell, channel) of both planes; border cells and padded
     // channels are 0
     auto stage = [&](int b) {
+        if (CB >= 32 && (cin & 3) == 0) {  // 4 channels per thread and pass: 16-B loads, 8-B LDS stores
+            constexpr int C4 = CB / 4;
+            for (int i = tid; i < 169 * C4; i += 256) {
+                const int q = i / C4, c = (i - q * C4) * 4;
+                const int y = q / 13 - 1, x = q - (q / 13) * 13 - 1;
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (b * CB + c < cin && (unsigned)y < 11u && (unsigned)x < 11u)
+                    v = *reinterpret_cast<const float4*>(X + (y * 11 + x) * cin + b * CB + c);
+                const float f[4] = {v.x, v.y, v.z, v.w};
+                bf16x4 hi, lo;
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    const __bf16 h = (__bf16)f[e];
+                    hi[e] = h;
+                    lo[e] = (__bf16)(f[e] - (float)h);
+                }
+                *reinterpret_cast<bf16x4*>(&Xs[0][q][c]) = hi;
+                *reinterpret_cast<bf16x4*>(&Xs[1][q][c]) = lo;
+            }
+            return;
+        }
         for (int i = tid; i < 169 * CB; i += 256) {
             const int q = i / CB, c = i - q * CB;
             const int y = q / 13 - 1, x = q - (q / 13) * 13 - 1;
