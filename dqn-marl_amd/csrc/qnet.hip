@@ -1126,6 +1126,37 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x3_kernel(evx_gemm_desc g, int
     // stage channel block b: every (13x13 cell, channel) of both planes; border cells and padded
     // channels are 0
     auto stage = [&](int b) {
+        if (CB == 16 && cin == 6) {  // conv1: one cell per thread, its 6 channels as 3 8-B loads, 10 zeros
+            for (int q = tid; q < 169; q += 256) {
+                const int y = q / 13 - 1, x = q - (q / 13) * 13 - 1;
+                float f[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+                if ((unsigned)y < 11u && (unsigned)x < 11u) {
+                    const float2* s2 = reinterpret_cast<const float2*>(X + (y * 11 + x) * 6);
+#pragma unroll
+                    for (int e = 0; e < 3; e++) {
+                        const float2 v = s2[e];
+                        f[2 * e] = v.x;
+                        f[2 * e + 1] = v.y;
+                    }
+                }
+                bf16x8 h0, h1, l0, l1;
+#pragma unroll
+                for (int e = 0; e < 8; e++) {
+                    h0[e] = h1[e] = l0[e] = l1[e] = (__bf16)0.f;
+                }
+#pragma unroll
+                for (int e = 0; e < 6; e++) {
+                    const __bf16 h = (__bf16)f[e];
+                    h0[e] = h;
+                    l0[e] = (__bf16)(f[e] - (float)h);
+                }
+                *reinterpret_cast<bf16x8*>(&Xs[0][q][0]) = h0;
+                *reinterpret_cast<bf16x8*>(&Xs[0][q][8]) = h1;
+                *reinterpret_cast<bf16x8*>(&Xs[1][q][0]) = l0;
+                *reinterpret_cast<bf16x8*>(&Xs[1][q][8]) = l1;
+            }
+            return;
+        }
         if (CB >= 32 && (cin & 3) == 0) {  // 4 channels per thread and pass: 16-B loads, 8-B LDS stores
             constexpr int C4 = CB / 4;
             for (int i = tid; i < 169 * C4; i += 256) {
