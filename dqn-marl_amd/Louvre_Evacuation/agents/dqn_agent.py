@@ -50,6 +50,7 @@ class DQNNetwork:
         if strict and missing:
             raise KeyError(f"missing keys {missing}")
         self._params.load_state_dict(sd)
+        self._lr.weights_written(target=self._target)  # operand copies / act table follow the weights
 
     def to(self, device):
         return self

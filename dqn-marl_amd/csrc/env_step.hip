@@ -39,6 +39,7 @@
 
 #include "evacx.h"
 #include "evx_device.h"
+#include "evx_host.h"
 
 namespace evx {
 
@@ -2209,6 +2210,9 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
     PT_END(grp);
     PT_BEGIN(mts);
     EVX_COUNT(14, ncont);
+    // py_ensure stores a block only while the stream's final head may lie in it; once the front runs
+    // 2 blocks past the head's block, a later crossing has overwritten that stored copy: flag it
+    if (py_head > MT_N && py_front > MT_N * ((py_head - 1) / MT_N) + 2 * MT_N) err |= 64;
     py_store(pyring, py_front, py_head, gpyw);
     EVX_COUNT(12, py_head);
     // the Python stream is stored: its ring becomes the "vacated by a winner" bitmap
@@ -3221,8 +3225,8 @@ int evx_env_step_part(const evx_layout* l, const evx_state* s, const int32_t* ac
     const size_t lds = step_lds_bytes(*l, bigg);
     if (lds > 160 * 1024) return fail(-7, "layout needs more than 160 KiB of LDS");
     const bool multi = l->layout_set && s->layout_idx;
-    static bool attr_set = false;
-    if (!attr_set) {
+    {
+        static std::atomic<uint64_t> attr_done;
         const void* ks[10] = {(const void*)evx::env_step_kernel<1, false>, (const void*)evx::env_step_kernel<2, false>,
                               (const void*)evx::env_step_kernel<4, false>, (const void*)evx::env_step_kernel<1, true>,
                               (const void*)evx::env_step_kernel<2, true>, (const void*)evx::env_step_kernel<4, true>,
@@ -3230,20 +3234,13 @@ int evx_env_step_part(const evx_layout* l, const evx_state* s, const int32_t* ac
                               (const void*)evx::env_step_kernel<2, false, true>,
                               (const void*)evx::env_step_kernel<1, true, true>,
                               (const void*)evx::env_step_kernel<2, true, true>};
-        for (const void* k : ks) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attr_set = true;
+        evxh::max_lds_once(attr_done, ks, 10, 160 * 1024);
     }
     // Default: 4-wave workgroups with the heavy-env path while a launch is short enough for
     // its heaviest env to set its length (fewer than 64 envs per CU); one-wave workgroups
     // beyond, where throughput rules: a wave's VGPRs and LDS free the moment its env is done
     // instead of when the slowest of four is (32768 envs: env_step 1.50 -> 1.31 ms).
-    static int ncu = 0;
-    if (ncu <= 0) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
-            ncu = 256;
-    }
+    const int ncu = evxh::cu_count();
     // (64 envs per CU: the 8192-env share of cfg5 keeps the heavy-env workgroups -- env_step 0.42 ->
     // 0.37 ms; big grids, which have no heavy path, switch at 32)
     int nwb = s->E >= (bigg ? 32 : 64) * ncu ? 1 : 4;
@@ -3304,13 +3301,10 @@ int evx_env_reset(const evx_layout* l, const evx_state* s, const uint8_t* mask, 
     const int G = (l->L + 2) * (l->W + 2);
     const size_t lds = (size_t)evx::reset_lds(G, l->P).total * 4;
     if (lds > 160 * 1024) return fail(-7, "layout needs more than 160 KiB of LDS");
-    static bool attr_set = false;
-    if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)evx::env_reset_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
-        (void)hipFuncSetAttribute((const void*)evx::env_reset_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
-        attr_set = true;
+    {
+        static std::atomic<uint64_t> attr_done;
+        const void* ks[2] = {(const void*)evx::env_reset_kernel<false>, (const void*)evx::env_reset_kernel<true>};
+        evxh::max_lds_once(attr_done, ks, 2, 160 * 1024);
     }
     if (l->layout_set && s->layout_idx)
         hipLaunchKernelGGL(evx::env_reset_kernel<true>, dim3(s->E), dim3(64), lds, (hipStream_t)stream, *l, *s, mask,
@@ -3322,50 +3316,9 @@ int evx_env_reset(const evx_layout* l, const evx_state* s, const uint8_t* mask, 
     return e == hipSuccess ? 0 : hip_fail(e, "env_reset launch");
 }
 
-// scratch of the scheduling permutations (classes: 1 byte per env, counts: PCL ints per 1024
-// envs), one per (device, stream) -- launches on one stream run in order, so the order and the
-// act perm of a trainer share theirs; env groups on other streams get their own -- grown on
-// demand (64 entries).
-static int perm_scratch(int E, hipStream_t stream, uint8_t** cls, int** cnt) {
-    struct Ent {
-        int dev;
-        hipStream_t st;
-        int64_t cap;
-        void* p;
-    };
-    static Ent ents[64] = {};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return -1;
-    const int64_t nch = (E + 1023) / 1024, need = ((int64_t)E + 255) / 256 * 256 + nch * evx::PCL * 4;
-    Ent* en = nullptr;
-    for (auto& x : ents)
-        if (x.p && x.dev == dev && x.st == stream) {
-            en = &x;
-            break;
-        }
-    if (!en)
-        for (auto& x : ents)
-            if (!x.p) {
-                en = &x;
-                en->dev = dev;
-                en->st = stream;
-                break;
-            }
-    if (!en) return -1;
-    if (en->cap < need) {
-        if (en->p) {  // launches of this stream may still read the old buffer
-            (void)hipStreamSynchronize(stream);
-            (void)hipFree(en->p);
-        }
-        en->p = nullptr;
-        en->cap = 0;
-        if (hipMalloc(&en->p, (size_t)need) != hipSuccess) return -1;
-        en->cap = need;
-    }
-    *cls = reinterpret_cast<uint8_t*>(en->p);
-    *cnt = reinterpret_cast<int*>(reinterpret_cast<uint8_t*>(en->p) + ((int64_t)E + 255) / 256 * 256);
-    return 0;
-}
+// The scheduling permutations' workspace in evx_state.perm_ws: the class byte of every env (rounded
+// up to 256 B), then PCL counts per 1024 envs.
+static int64_t perm_ws_need(int64_t E) { return (E + 255) / 256 * 256 + (E + 1023) / 1024 * evx::PCL * 4; }
 
 namespace evx {
 // diagnostic / test entry (evx_diag_sort_keys): one wave sorts n distinct keys in place in global
@@ -3395,20 +3348,19 @@ int evx_env_order(const evx_layout* l, const evx_state* s, void* stream) {
     if (s->E > 160 * 1024 - 4096) return fail(-22, "env_order: too many envs for one workgroup's LDS");
     int hmin = 0;
     const int hcap = heavy_cap(*l, &hmin);
-    static bool attr_set = false;
-    if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)evx::env_order_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024 - 4096);
-        attr_set = true;
+    {
+        static std::atomic<uint64_t> attr_done;
+        const void* ks[1] = {(const void*)evx::env_order_kernel};
+        evxh::max_lds_once(attr_done, ks, 1, 160 * 1024 - 4096);
     }
-    uint8_t* cls = nullptr;
-    int* cnt = nullptr;
-    if (perm_scratch(s->E, (hipStream_t)stream, &cls, &cnt) == 0) {
+    if (s->perm_ws) {  // count + rank launches, one workgroup per 1024 envs
+        uint8_t* cls = s->perm_ws;
+        int* cnt = reinterpret_cast<int*>(s->perm_ws + ((int64_t)s->E + 255) / 256 * 256);
         const unsigned nch = (unsigned)((s->E + 1023) / 1024);
         hipLaunchKernelGGL(evx::perm_count_kernel, dim3(nch), dim3(1024), 0, (hipStream_t)stream, *l, *s, 0, hmin, cls, cnt);
         hipLaunchKernelGGL(evx::perm_rank_kernel, dim3(nch), dim3(1024), 0, (hipStream_t)stream, *s, 0, hcap, cls, cnt,
                            s->order);
-    } else {
+    } else {  // no workspace: one 1024-thread workgroup walks every env
         const size_t lds = ((size_t)s->E + 3) & ~(size_t)3;  // one bucket byte per env
         hipLaunchKernelGGL(evx::env_order_kernel, dim3(1), dim3(1024), lds, (hipStream_t)stream, *l, *s, hcap, hmin);
     }
@@ -3416,14 +3368,16 @@ int evx_env_order(const evx_layout* l, const evx_state* s, void* stream) {
     return e == hipSuccess ? 0 : hip_fail(e, "env_order launch");
 }
 
+int64_t evx_perm_ws_bytes(int32_t E) { return E > 0 ? perm_ws_need(E) : 0; }
+
 int evx_act_perm(const evx_layout* l, const evx_state* s, int32_t* perm, void* stream) {
     int rc = check_layout(l);
     if (rc) return rc;
     if (!s || !perm) return fail(-22, "act_perm: NULL argument");
     if (s->E <= 0) return 0;
-    uint8_t* cls = nullptr;
-    int* cnt = nullptr;
-    if (perm_scratch(s->E, (hipStream_t)stream, &cls, &cnt)) return fail(-12, "act_perm: scratch allocation failed");
+    if (!s->perm_ws) return fail(-22, "act_perm: state.perm_ws is NULL (evx_perm_ws_bytes(E) bytes)");
+    uint8_t* cls = s->perm_ws;
+    int* cnt = reinterpret_cast<int*>(s->perm_ws + ((int64_t)s->E + 255) / 256 * 256);
     const unsigned nch = (unsigned)((s->E + 1023) / 1024);
     hipLaunchKernelGGL(evx::perm_count_kernel, dim3(nch), dim3(1024), 0, (hipStream_t)stream, *l, *s, 1, 0, cls, cnt);
     hipLaunchKernelGGL(evx::perm_rank_kernel, dim3(nch), dim3(1024), 0, (hipStream_t)stream, *s, 1, 0, cls, cnt, perm);

@@ -25,6 +25,7 @@
 #include <string>
 
 #include "evacx.h"
+#include "evx_host.h"
 
 namespace evxf {
 constexpr int NT = 1024;
@@ -121,13 +122,13 @@ int evx_floor_field(int32_t n_layouts, int32_t GX, int32_t GY, const uint8_t* va
     hipStream_t s = (hipStream_t)stream;
     if (n <= LDS_CELLS) {
         const size_t lds = (size_t)n * sizeof(double);
-        static bool attr = false;
-        if (!attr) {
-            if (hipFuncSetAttribute((const void*)floor_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    LDS_CELLS * (int)sizeof(double)) != hipSuccess)
-                return fail(-5, "floor_field: cannot raise the LDS limit");
-            attr = true;
-        }
+        static std::atomic<uint64_t> attr_done;
+        bool ok = true;
+        evxh::once_per_device(attr_done, [&] {
+            ok = hipFuncSetAttribute((const void*)floor_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     LDS_CELLS * (int)sizeof(double)) == hipSuccess;
+        });
+        if (!ok) return fail(-5, "floor_field: cannot raise the LDS limit");
         hipLaunchKernelGGL(floor_kernel<true>, dim3(n_layouts), dim3(NT), lds, s, GX, GY, valid, source, pen, floor,
                            passes, max_passes);
     } else {

@@ -23,6 +23,7 @@
 #include <algorithm>
 
 #include "evacx.h"
+#include "evx_host.h"
 
 namespace evxx {
 
@@ -187,11 +188,10 @@ int evx_qmix_loss(const float* Q, const float* Qt, int32_t A, const int32_t* act
     const int nrb = (B + evxx::ROWS - 1) / evxx::ROWS;
     const int nz = zero && nzero > 0 ? (int)std::min<int64_t>((nzero + 256 * 16 - 1) / (256 * 16), 512) : 0;
     const size_t lds = (size_t)evxx::ROWS * (n + 2 * evxx::EMB + 2) * 4;
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)evxx::qmix_rows_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
-        attr = true;
+    {
+        static std::atomic<uint64_t> attr_done;
+        const void* ks[1] = {(const void*)evxx::qmix_rows_kernel};
+        evxh::max_lds_once(attr_done, ks, 1, 160 * 1024);
     }
     hipStream_t st = (hipStream_t)stream;
     hipLaunchKernelGGL(evxx::qmix_rows_kernel, dim3(nrb + nz), dim3(evxx::ROWS), lds, st, Q, Qt, A, act, rew, done, gamma,

@@ -38,6 +38,7 @@
 #include <algorithm>
 
 #include "evacx.h"
+#include "evx_host.h"
 
 namespace evxm {
 
@@ -929,15 +930,6 @@ __global__ __launch_bounds__(256, 2) void qact3h_kernel(Fwd a0) {
         const int r2 = m0 + 2 * (tid - 224);
         phS[tid - 224] = r2 < a.N ? drop_row(a.drop_seed, a.drop_stream, (a.drop_row0 + (uint32_t)krow(a, r2)) >> 1) : 0u;
     }
-    if (DM == 3 && tid >= 192) {  // row-permuted act: every tile row's pair hash and half (the same masks)
-        const int r = m0 + (tid - 192);
-        uint2 v = make_uint2(0u, 0u);
-        if (r < a.N) {
-            const uint32_t k = a.drop_row0 + (uint32_t)krow(a, r);
-            v = make_uint2(drop_row(a.drop_seed, a.drop_stream, k >> 1), k & 1u);
-        }
-        reinterpret_cast<uint2*>(phS)[tid - 192] = v;
-    }
     bool fast = false;
     if (a.stat) {  // tile-uniform: every row at the table's fire step, centre inside the map
         bool ok = true;
@@ -1030,7 +1022,7 @@ __global__ __launch_bounds__(256, 2) void qact3h_kernel(Fwd a0) {
             fc1_slab_m<2, A3_HP, true, DM>(a, acc[mt], bias, m0 + mt * 32, hh * 256, w * 64,
                                            reinterpret_cast<__bf16 (*)[A3_HP]>(&Hh[mt * 32][0]),
                                            reinterpret_cast<__bf16 (*)[A3_HP]>(&Hl[mt * 32][0]),
-                                           phS + (DM == 3 ? mt * 64 : mt * 16));
+                                           phS + mt * 16);
         ACT_ST(3 + 4 * hh);
         __syncthreads();
         ACT_ST(4 + 4 * hh);
@@ -2152,18 +2144,15 @@ int evx_qmlp_pack3(const float* w1, const float* b1, const float* w2, uint16_t* 
 // SAVE: the learner's online forward (no row permutation; X from x_expand_kernel)
 extern "C++" template <bool GR, bool SAVE = false>
 static void launch_act3(const evxm::Fwd& a, int32_t n, int nets, hipStream_t st) {
-    static bool attr = false;
-    if (!attr) {
-        const void* kh[4] = {(const void*)evxm::qact3h_kernel<GR, 0, SAVE>, (const void*)evxm::qact3h_kernel<GR, 1, SAVE>,
-                             (const void*)evxm::qact3h_kernel<GR, 2, SAVE>, (const void*)evxm::qact3h_kernel<GR, 3, SAVE>};
-        for (const void* k : kh) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, evxm::ACT3H_LDS);
-        attr = true;
+    {
+        static std::atomic<uint64_t> attr_done;
+        const void* kh[3] = {(const void*)evxm::qact3h_kernel<GR, 0, SAVE>, (const void*)evxm::qact3h_kernel<GR, 1, SAVE>,
+                             (const void*)evxm::qact3h_kernel<GR, 2, SAVE>};
+        evxh::max_lds_once(attr_done, kh, 3, evxm::ACT3H_LDS);
     }
     const dim3 grid((unsigned)((n + 63) / 64), (unsigned)nets);
     if (a.drop_mask)
         hipLaunchKernelGGL((evxm::qact3h_kernel<GR, 2, SAVE>), grid, dim3(256), evxm::ACT3H_LDS, st, a);
-    else if (!SAVE && a.drop_thresh && a.perm && a.rpe == 1)  // a row permutation: rows of different pairs share tiles
-        hipLaunchKernelGGL((evxm::qact3h_kernel<GR, 3, SAVE>), grid, dim3(256), evxm::ACT3H_LDS, st, a);
     else if (a.drop_thresh)
         hipLaunchKernelGGL((evxm::qact3h_kernel<GR, 1, SAVE>), grid, dim3(256), evxm::ACT3H_LDS, st, a);
     else
@@ -2245,10 +2234,8 @@ static int make_fwd(const evx_layout* lay, const evx_obs* obs, int32_t n, const 
     a.rpe = out->rows_per_env > 0 ? out->rows_per_env : 1;
     a.gn = 0;
     a.g = 0;
-    // rows_per_env even (dropout row pairs stay together), or 1: a row permutation, the x3 act only
-    // (qact3h_kernel's per-row pair hashes)
-    if (a.perm && (a.rpe & 1) && !(a.rpe == 1 && p->x3))
-        return mfail(-22, "qmlp_forward: rows_per_env must be even (dropout row pairs), or 1 for the x3 act");
+    // rows_per_env even: dropout row pairs stay together in a tile
+    if (a.perm && (a.rpe & 1)) return mfail(-22, "qmlp_forward: rows_per_env must be even (dropout row pairs)");
     return 0;
 }
 
@@ -2300,7 +2287,6 @@ static int launch_fwd(const evxm::Fwd& a0, const evxm::Fwd& a1, int32_t n, int p
 int evx_qmlp_forward(const evx_layout* lay, const evx_obs* obs, int32_t n, const evx_qmlp_params* p,
                      const evx_qmlp_dropout* drop, const evx_qmlp_fwd_out* out, void* stream) {
     if (n <= 0) return 0;
-    if (out && out->perm && out->rows_per_env == 1) return mfail(-22, "qmlp_forward: row permutations are the act's");
     evxm::Fwd a;
     int rc = make_fwd(lay, obs, n, p, drop, out, a);
     if (rc) return rc;
@@ -2333,11 +2319,10 @@ int evx_qmlp_act(const evx_layout* lay, const evx_obs* obs, int32_t n, const evx
     if (rc) return rc;
     a.h1 = nullptr;
     a.h1l = nullptr;
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)evxm::qact_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  evxm::ACT_LDS);
-        attr = true;
+    {
+        static std::atomic<uint64_t> attr_done;
+        const void* ks[1] = {(const void*)evxm::qact_kernel};
+        evxh::max_lds_once(attr_done, ks, 1, evxm::ACT_LDS);
     }
     if (p->x3)
         launch_act3<false>(a, n, 1, (hipStream_t)stream);
@@ -2487,11 +2472,10 @@ static void launch_tail(const evxm::Bwd& a, int32_t B, const evx_qmlp_grads* g, 
         g1.gsC = evxm::NPAR;
         g1.gsP = pf;
         r.gsP = pf;
-        static bool attr_g = false;
-        if (!attr_g) {
-            (void)hipFuncSetAttribute((const void*)evxm::bwd_mid_kernel<X3, AP2, BP2, true>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-            attr_g = true;
+        {  // the LDS limit at the device's maximum: lds depends on B, the attribute is set once
+            static std::atomic<uint64_t> attr_done;
+            const void* ks[1] = {(const void*)evxm::bwd_mid_kernel<X3, AP2, BP2, true>};
+            evxh::max_lds_once(attr_done, ks, 1, 160 * 1024);
         }
         hipLaunchKernelGGL((evxm::bwd_mid_kernel<X3, AP2, BP2, true>), dim3(nmid, nets), dim3(256), lds, st, a, ndzx, g2);
         hipLaunchKernelGGL((evxm::gemm_tn_kernel<AP1, BP1, true>), dim3(g1.gx, g1.gy, g1.gz * nets), dim3(256), 0, st, g1);
@@ -2500,11 +2484,10 @@ static void launch_tail(const evxm::Bwd& a, int32_t B, const evx_qmlp_grads* g, 
     }
     // qdz1 and the dW2 tiles in one launch (both read only qbwd3's outputs), then the dW1
     // tiles, then every reduction + the squared-norm partials in one launch
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)evxm::bwd_mid_kernel<X3, AP2, BP2>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        attr = true;
+    {
+        static std::atomic<uint64_t> attr_done;
+        const void* ks[1] = {(const void*)evxm::bwd_mid_kernel<X3, AP2, BP2>};
+        evxh::max_lds_once(attr_done, ks, 1, 160 * 1024);
     }
     hipLaunchKernelGGL((evxm::bwd_mid_kernel<X3, AP2, BP2>), dim3(nmid), dim3(256), lds, st, a, ndzx, g2);
     hipLaunchKernelGGL((evxm::gemm_tn_kernel<AP1, BP1>), dim3(g1.gx * g1.gy * g1.gz), dim3(256), 0, st, g1);

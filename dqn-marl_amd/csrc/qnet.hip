@@ -632,19 +632,17 @@ __global__ __launch_bounds__(256) void colsum_finish(const float* __restrict__ p
 // DQNAgent.learn (agents/dqn_agent.py:143-151): q = Q(s).gather(a); y = r + gamma *
 // max Q_tgt(s') * ~done; loss = mean((q - y)^2); dQ[i, a_i] = 2 (q - y) / B. With
 // importance weights w (prioritized replay): loss = mean(w (q - y)^2), and |q - y| out.
-// One row per thread over many blocks; the last block to finish sums the block
-// partials in block order (deterministic).
-__device__ float g_td_part[4096];
-__device__ unsigned int g_td_ticket[64];  // one per net of a grouped launch (blockIdx.y)
+// One row per thread over many blocks, each block's partial into the caller's workspace; a
+// one-block launch per net then sums them in block order (deterministic; no module state, so
+// launches on different streams with their own workspaces never meet).
 __global__ __launch_bounds__(256) void td_loss_kernel(const float* __restrict__ Q, const float* __restrict__ Qt,
                                                       int A, const int32_t* __restrict__ act,
                                                       const float* __restrict__ rew, const uint8_t* __restrict__ done,
                                                       float gamma, int B, const float* __restrict__ w,
-                                                      float* __restrict__ dQ, float* __restrict__ loss_out,
+                                                      float* __restrict__ dQ, float* __restrict__ part,
                                                       float* __restrict__ td_abs, int ntd = 0,
                                                       float* __restrict__ zero = nullptr, int64_t nzero = 0) {
     __shared__ float red[256];
-    __shared__ bool last;
     if (zero && (int)blockIdx.x >= ntd) {  // the extra workgroups clear the gradient buffer for the backward
         if (blockIdx.y) return;
         const int64_t z0 = ((int64_t)blockIdx.x - ntd) * 256 + threadIdx.x, zs = ((int64_t)gridDim.x - ntd) * 256;
@@ -664,11 +662,10 @@ __global__ __launch_bounds__(256) void td_loss_kernel(const float* __restrict__ 
         if (w) w += o;
         dQ += o * A;
         if (td_abs) td_abs += o;
-        loss_out += gy;
     }
     const float nrm = (float)B;
     const int i = blockIdx.x * 256 + threadIdx.x;
-    float part = 0.f;
+    float pt = 0.f;
     if (i < B) {
         float mx = Qt[(int64_t)i * A];
         for (int j = 1; j < A; j++) mx = fmaxf(mx, Qt[(int64_t)i * A + j]);
@@ -677,41 +674,33 @@ __global__ __launch_bounds__(256) void td_loss_kernel(const float* __restrict__ 
         const float d = Q[(int64_t)i * A + a] - y;
         // prioritized replay: importance weights scale each squared error and its gradient
         const float wi = w ? w[i] : 1.f;
-        part = w ? wi * (d * d) : d * d;
+        pt = w ? wi * (d * d) : d * d;
         const float g = w ? wi * (2.f * d) : 2.f * d;
         for (int j = 0; j < A; j++) dQ[(int64_t)i * A + j] = (j == a) ? g / nrm : 0.f;
         if (td_abs) td_abs[i] = fabsf(d);
     }
-    red[threadIdx.x] = part;
+    red[threadIdx.x] = pt;
     __syncthreads();
     for (int s = 128; s > 0; s >>= 1) {
         if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
         __syncthreads();
     }
-    if (threadIdx.x == 0) {
-        g_td_part[gy * nb + blockIdx.x] = red[0];
-        __threadfence();
-        last = atomicAdd(&g_td_ticket[gy], 1u) == nb - 1;
-    }
+    if (threadIdx.x == 0) part[gy * nb + blockIdx.x] = red[0];
+}
+// loss[y] = (sum of net y's nb block partials) / B: strided partial sums, then a fixed LDS tree
+__global__ __launch_bounds__(256) void td_finish_kernel(const float* __restrict__ part, int nb, int B,
+                                                        float* __restrict__ loss_out) {
+    __shared__ float red[256];
+    const float* p = part + (size_t)blockIdx.x * nb;
+    float t = 0.f;
+    for (int k = threadIdx.x; k < nb; k += 256) t += p[k];
+    red[threadIdx.x] = t;
     __syncthreads();
-    if (last) {  // the whole last block: strided partial sums, then a fixed LDS tree (deterministic;
-                 // one thread walking the 128 partials of a 32768-row batch took ~20 us)
-        __threadfence();
-        float t = 0.f;
-        for (unsigned k = threadIdx.x; k < nb; k += 256)
-            t += __hip_atomic_load(&g_td_part[gy * nb + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        red[threadIdx.x] = t;
+    for (int s = 128; s > 0; s >>= 1) {
+        if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
         __syncthreads();
-        for (int s = 128; s > 0; s >>= 1) {
-            if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
-            __syncthreads();
-        }
-        if (threadIdx.x == 0) {
-            const float l = red[0] / nrm;
-            loss_out[0] = l;
-            g_td_ticket[gy] = 0;
-        }
     }
+    if (threadIdx.x == 0) loss_out[blockIdx.x] = red[0] / (float)B;
 }
 
 // ------------------------------------------------- clip_grad_norm_ + Adam
@@ -980,6 +969,25 @@ __global__ __launch_bounds__(256) void pix2nchw_kernel(const float* __restrict__
             d[j] = tl[p * (C + 1) + c];
         }
     }
+}
+
+// the same permutation element-wise, one output element per thread (C beyond the LDS tile)
+__global__ __launch_bounds__(256) void pix2nchw_flat_kernel(const float* __restrict__ src, int64_t total, int C,
+                                                            int to_nchw, float* __restrict__ dst) {
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= total) return;
+    const int64_t n = (int64_t)121 * C;
+    const int64_t b = j / n;
+    const int r = (int)(j - b * n);
+    int p, c;
+    if (to_nchw) {  // d: NCHW (c * 121 + p), s: pixel-major
+        c = r / 121;
+        p = r - c * 121;
+    } else {  // d: pixel-major (p * C + c), s: NCHW
+        p = r / C;
+        c = r - p * C;
+    }
+    dst[j] = src[b * n + (to_nchw ? (int64_t)p * C + c : (int64_t)c * 121 + p)];
 }
 
 // NCHW [B][C][121] -> pixel-major [B][121 * C] bf16 hi / lo planes (evx_pix_split)
@@ -1401,45 +1409,52 @@ int evx_colsum(const float* X, int64_t ld, int32_t M, int32_t N, float* out, int
     return qlaunch("colsum");
 }
 
+int64_t evx_td_loss_ws_floats(int32_t B, int32_t nets) {
+    if (B <= 0 || nets < 1) return 0;
+    return (int64_t)((B + 255) / 256) * nets;
+}
+
+static int td_launch(const float* Q, const float* Qt, int32_t A, const int32_t* act, const float* rew,
+                     const uint8_t* done, float gamma, int32_t B, int32_t nets, const float* w, float* dQ, float* loss,
+                     float* td_abs, float* zero, int64_t nzero, float* ws, int64_t ws_floats, void* stream,
+                     const char* what) {
+    if (B <= 0) return 0;
+    if (nets < 1 || nets > 65535) return qfail(-22, "td_loss: nets must be 1..65535");
+    if (!Q || !Qt || !act || !rew || !done || !dQ || !loss) return qfail(-22, "td_loss: NULL argument");
+    const int ntd = (B + 255) / 256;
+    if (!ws || ws_floats < (int64_t)ntd * nets) return qfail(-22, "td_loss: workspace smaller than evx_td_loss_ws_floats");
+    const int nz = zero && nzero > 0 ? (int)std::min<int64_t>((nzero + 256 * 16 - 1) / (256 * 16), 512) : 0;
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(evxq::td_loss_kernel, dim3(ntd + nz, nets), dim3(256), 0, st, Q, Qt, A, act, rew, done, gamma, B,
+                       w, dQ, ws, td_abs, ntd, nz ? zero : nullptr, nzero);
+    hipLaunchKernelGGL(evxq::td_finish_kernel, dim3(nets), dim3(256), 0, st, (const float*)ws, ntd, B, loss);
+    return qlaunch(what);
+}
+
 int evx_td_loss_w(const float* Q, const float* Qt, int32_t A, const int32_t* act, const float* rew,
                   const uint8_t* done, float gamma, int32_t B, const float* w, float* dQ, float* loss, float* td_abs,
-                  void* stream) {
-    if (B <= 0) return 0;
-    if (B > 4096 * 256) return qfail(-22, "td_loss: batch too large");
-    hipLaunchKernelGGL(evxq::td_loss_kernel, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream, Q, Qt, A, act, rew, done,
-                       gamma, B, w, dQ, loss, td_abs);
-    return qlaunch("td_loss");
+                  float* ws, int64_t ws_floats, void* stream) {
+    return td_launch(Q, Qt, A, act, rew, done, gamma, B, 1, w, dQ, loss, td_abs, nullptr, 0, ws, ws_floats, stream,
+                     "td_loss");
 }
 
 int evx_td_loss_zero(const float* Q, const float* Qt, int32_t A, const int32_t* act, const float* rew,
                      const uint8_t* done, float gamma, int32_t B, const float* w, float* dQ, float* loss, float* td_abs,
-                     float* zero, int64_t nzero, void* stream) {
-    if (B <= 0) return 0;
-    if (B > 4096 * 256) return qfail(-22, "td_loss: batch too large");
-    if (!zero || nzero <= 0) return evx_td_loss_w(Q, Qt, A, act, rew, done, gamma, B, w, dQ, loss, td_abs, stream);
-    const int ntd = (B + 255) / 256;
-    const int nz = (int)std::min<int64_t>((nzero + 256 * 16 - 1) / (256 * 16), 512);
-    hipLaunchKernelGGL(evxq::td_loss_kernel, dim3(ntd + nz), dim3(256), 0, (hipStream_t)stream, Q, Qt, A, act, rew, done,
-                       gamma, B, w, dQ, loss, td_abs, ntd, zero, nzero);
-    return qlaunch("td_loss_zero");
+                     float* zero, int64_t nzero, float* ws, int64_t ws_floats, void* stream) {
+    return td_launch(Q, Qt, A, act, rew, done, gamma, B, 1, w, dQ, loss, td_abs, zero, nzero, ws, ws_floats, stream,
+                     "td_loss_zero");
 }
 
 int evx_td_loss_zero_g(const float* Q, const float* Qt, int32_t A, const int32_t* act, const float* rew,
                        const uint8_t* done, float gamma, int32_t B, int32_t nets, const float* w, float* dQ, float* loss,
-                       float* td_abs, float* zero, int64_t nzero, void* stream) {
-    if (B <= 0) return 0;
-    if (nets < 1 || nets > 64) return qfail(-22, "td_loss_g: nets must be 1..64");
-    const int ntd = (B + 255) / 256;
-    if ((int64_t)ntd * nets > 4096) return qfail(-22, "td_loss_g: batch x nets too large");
-    const int nz = zero && nzero > 0 ? (int)std::min<int64_t>((nzero + 256 * 16 - 1) / (256 * 16), 512) : 0;
-    hipLaunchKernelGGL(evxq::td_loss_kernel, dim3(ntd + nz, nets), dim3(256), 0, (hipStream_t)stream, Q, Qt, A, act, rew,
-                       done, gamma, B, w, dQ, loss, td_abs, ntd, nz ? zero : nullptr, nzero);
-    return qlaunch("td_loss_zero_g");
+                       float* td_abs, float* zero, int64_t nzero, float* ws, int64_t ws_floats, void* stream) {
+    return td_launch(Q, Qt, A, act, rew, done, gamma, B, nets, w, dQ, loss, td_abs, zero, nzero, ws, ws_floats, stream,
+                     "td_loss_zero_g");
 }
 
 int evx_td_loss(const float* Q, const float* Qt, int32_t A, const int32_t* act, const float* rew, const uint8_t* done,
-                float gamma, int32_t B, float* dQ, float* loss, void* stream) {
-    return evx_td_loss_w(Q, Qt, A, act, rew, done, gamma, B, nullptr, dQ, loss, nullptr, stream);
+                float gamma, int32_t B, float* dQ, float* loss, float* ws, int64_t ws_floats, void* stream) {
+    return evx_td_loss_w(Q, Qt, A, act, rew, done, gamma, B, nullptr, dQ, loss, nullptr, ws, ws_floats, stream);
 }
 
 int evx_sumsq_norm(const float* g, int64_t n, float* scratch, int32_t scratch_elems, float* norm, void* stream) {
@@ -1593,7 +1608,11 @@ int evx_pix_nchw(const float* src, int32_t B, int32_t C, int32_t to_nchw, float*
     const int64_t total = (int64_t)B * C * 121;
     if (total <= 0) return 0;
     const size_t lds = (size_t)121 * (C + 1) * 4;
-    if (lds > 64 * 1024) return qfail(-22, "pix_nchw: C > 134 channels");
+    if (lds > 64 * 1024) {  // the LDS tile holds C <= 134: element-wise beyond
+        hipLaunchKernelGGL(evxq::pix2nchw_flat_kernel, dim3(nblk(total)), dim3(256), 0, (hipStream_t)stream, src, total,
+                           C, to_nchw, dst);
+        return qlaunch("pix_nchw");
+    }
     hipLaunchKernelGGL(evxq::pix2nchw_kernel, dim3((unsigned)B), dim3(256), lds, (hipStream_t)stream, src, B, C, to_nchw,
                        dst);
     return qlaunch("pix_nchw");

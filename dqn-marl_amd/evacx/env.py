@@ -265,6 +265,11 @@ class LayoutSet:
         return len(self.layouts)
 
 
+def _perm_ws(E: int, device) -> torch.Tensor:
+    n = int(_lib.lib().evx_perm_ws_bytes(E))
+    return torch.zeros(max(n, 1), dtype=torch.uint8, device=device)
+
+
 class VecEnv:
     """E env instances of one layout (or of a LayoutSet, one layout per env), state
     resident in HBM (SoA, env-major)."""
@@ -320,11 +325,14 @@ class VecEnv:
         self._obs = [torch.zeros(E * R * OBS_WORDS, **i32) for _ in range(obs_buffers)]
         self._ob = 0
         self.err = torch.zeros(1, **i32)
+        # the scheduling permutations' workspace (evx_env_order / evx_act_perm): caller-owned, one per
+        # VecEnv (split parts get their own: they order on their own streams)
+        self.perm_ws = _perm_ws(E, d)
         self.c = _lib.evx_state(E=E, pk=_ptr(self.pk), health=_ptr(self.health), acc=_ptr(self.acc),
                                 rmap=_ptr(self.rmap), thmap=_ptr(self.thmap), robots=_ptr(self.robots),
                                 view=_ptr(self.view), scal=_ptr(self.scal), py_mt=_ptr(self.py_mt),
                                 np_mt=_ptr(self.np_mt), scratch=_ptr(self.scratch), order=_ptr(self.order),
-                                layout_idx=_ptr(self.layout_idx))
+                                layout_idx=_ptr(self.layout_idx), perm_ws=_ptr(self.perm_ws))
         self.obs_term: Optional[torch.Tensor] = None
         self._parts: List["VecEnv"] = []
         self.out = _lib.evx_step_out(reward=_ptr(self.reward), done=_ptr(self.done), counts=_ptr(self.counts),
@@ -363,10 +371,12 @@ class VecEnv:
             p._ob = self._ob
             p.err = self.err
             p.obs_term = cut(self.obs_term, R * OBS_WORDS)
+            p.perm_ws = _perm_ws(n, lay.device)
             p.c = _lib.evx_state(E=n, pk=_ptr(p.pk), health=_ptr(p.health), acc=_ptr(p.acc), rmap=_ptr(p.rmap),
                                  thmap=_ptr(p.thmap), robots=_ptr(p.robots), view=_ptr(p.view), scal=_ptr(p.scal),
                                  py_mt=_ptr(p.py_mt), np_mt=_ptr(p.np_mt), scratch=_ptr(p.scratch),
-                                 order=_ptr(p.order), layout_idx=_ptr(cut(self.layout_idx, 1)))
+                                 order=_ptr(p.order), layout_idx=_ptr(cut(self.layout_idx, 1)),
+                                 perm_ws=_ptr(p.perm_ws))
             p.layout_idx = cut(self.layout_idx, 1)
             p.out = _lib.evx_step_out(reward=_ptr(p.reward), done=_ptr(p.done), counts=_ptr(p.counts),
                                       obs=_ptr(p.obs), err=_ptr(p.err))

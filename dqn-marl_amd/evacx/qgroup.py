@@ -135,9 +135,11 @@ class GroupedLearner:
                                           C.byref(o_on), s2_obs.data_ptr(), C.byref(self.fast_t.c), C.byref(d_tg),
                                           C.byref(o_tg), _stream()), "qmlp_forward2_g")
         dQ = self._buf("dq", G * B * NACT, torch.float32)
+        tw = self._buf("td_ws", max(1, int(qlib().evx_td_loss_ws_floats(B, G))), torch.float32)
         qcheck(qlib().evx_td_loss_zero_g(Q.data_ptr(), Qt.data_ptr(), NACT, a.data_ptr(), r.data_ptr(), done.data_ptr(),
                                          self.gamma, B, G, None, dQ.data_ptr(), self.loss.data_ptr(), None,
-                                         self.gflat.data_ptr(), self.gflat.numel(), _stream()), "td_loss_zero_g")
+                                         self.gflat.data_ptr(), self.gflat.numel(), tw.data_ptr(), tw.numel(),
+                                         _stream()), "td_loss_zero_g")
         self._backward(B, dQ, X, H1, H2)
         if update:
             self.step_optimizer()

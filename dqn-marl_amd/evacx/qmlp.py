@@ -226,7 +226,11 @@ class MLPFast:
         stopped spreading): fc1's pre-activation at zero occupancy for every window centre
         of the layout, [nx (W+2)][512] f32 (x3: f32-accurate), rebuilt with every repack and
         every optimizer step (adam_step). x_range = (x0, x1): only centres with x0 <= x <= x1
-        (Map.robot_range, envs/map.py:75: a robot never leaves it), default every x."""
+        (Map.robot_range, envs/map.py:75: a robot never leaves it), default every x.
+        The table (like the operand copies) follows the fp32 parameters only through repack() and
+        adam_step(): after any other write of the weights (load_state_dict, a broadcast) call
+        repack() (Learner.weights_written) -- the act and, at B >= 32768, the learner's online
+        forward read fc1 from this table."""
         x0, x1 = (0, L + 1) if x_range is None else (int(x_range[0]), int(x_range[1]))
         if not 0 <= x0 <= x1 <= L + 1:
             raise ValueError("attach_static: x_range must lie in [0, L + 1]")
@@ -275,10 +279,10 @@ class MLPFast:
         _need("act obs", obs, n, 8)
         _need("act q", q, n, NACT)
         _need("act actions", actions, n, 1)
-        # rows_per_env 1: a row permutation (x3 only: the act kernel hashes every row's dropout pair)
-        if perm is not None and (rows_per_env <= 0 or (rows_per_env % 2 and not (rows_per_env == 1 and self.x3))
+        # rows_per_env even: dropout row pairs stay together in a tile
+        if perm is not None and (rows_per_env <= 0 or rows_per_env % 2
                                  or n % rows_per_env or perm.numel() < n // rows_per_env):
-            raise ValueError("qmlp act: perm needs an even rows_per_env (or 1, x3) dividing n and n / rows_per_env "
+            raise ValueError("qmlp act: perm needs an even rows_per_env dividing n and n / rows_per_env "
                              "entries")
         d = self._drop(drop) if drop else None
         o = evx_qmlp_fwd_out(q=_p(q), actions=_p(actions), epsilon=float(epsilon), act_seed=act_seed,

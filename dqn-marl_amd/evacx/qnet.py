@@ -59,17 +59,19 @@ def qlib():
         L.evx_conv3x3_ws_elems.restype = C.c_int64
         L.evx_colsum.argtypes = [C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p,
                                  C.c_int32, C.c_void_p]
+        L.evx_td_loss_ws_floats.restype = C.c_int64
+        L.evx_td_loss_ws_floats.argtypes = [C.c_int32, C.c_int32]
         L.evx_td_loss.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_float,
-                                  C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]
+                                  C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]
         L.evx_td_loss_w.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
                                     C.c_float, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
-                                    C.c_void_p]
+                                    C.c_void_p, C.c_int64, C.c_void_p]
         L.evx_td_loss_zero.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
                                        C.c_float, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
-                                       C.c_void_p, C.c_int64, C.c_void_p]
+                                       C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_void_p]
         L.evx_td_loss_zero_g.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
                                          C.c_float, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
-                                         C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]
+                                         C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_void_p]
         L.evx_sumsq_norm.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
         L.evx_clip_adam.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p,
                                     C.c_float, C.POINTER(evx_adam), C.c_void_p]
@@ -93,6 +95,12 @@ def qcheck(rc, what):
 
 def _p(t):
     return None if t is None else t.data_ptr()
+
+
+def td_workspace(ws, B: int, nets: int, device, tag: str = "") -> torch.Tensor:
+    """The TD loss's partials buffer (evx_td_loss_ws_floats) from a _Workspace pool."""
+    n = max(1, int(qlib().evx_td_loss_ws_floats(B, nets)))
+    return ws.get(tag + "td_ws", (n,), torch.float32, device)
 
 
 _WS_NEED: Dict[Tuple, int] = {}
@@ -403,6 +411,11 @@ class Learner:
 
     def __init__(self, kind="mlp", device="cuda", lr=1e-4, gamma=0.99, max_norm=1.0, precision="f32",
                  hidden=512, actions=5, seed=0, betas=(0.9, 0.999), eps=1e-8):
+        if precision not in ("f32", "bf16", "x3", "exact"):
+            raise ValueError(f"precision must be 'f32', 'bf16', 'x3' or 'exact', not {precision!r}")
+        # "exact": every product on the exact-f32 MFMA GEMMs (evx_gemm f32), no fused MLP kernels
+        fused_ok = precision != "exact"
+        precision = "f32" if precision == "exact" else precision
         self.kind, self.device = kind, torch.device(device)
         self.shapes = param_shapes(layer_specs(kind, hidden, actions))
         self.online = FlatParams(self.shapes, self.device)
@@ -427,7 +440,7 @@ class Learner:
         # them in the x3 (f32-accurate) mode, bf16 with bf16 operands. The dense-tensor path
         # (forward / learn on expanded observations) keeps evx_gemm at `precision`.
         self.fast = self.fast_t = None
-        if kind == "mlp" and precision in ("bf16", "f32", "x3") and hidden == 512 and actions == 5:
+        if fused_ok and kind == "mlp" and hidden == 512 and actions == 5:
             from .qmlp import MLPFast
             self.fast = MLPFast(self.online, self.device, x3=precision != "bf16")
             self.fast_t = MLPFast(self.target, self.device, x3=precision != "bf16")
@@ -450,12 +463,14 @@ class Learner:
         self.rng_offset += (m.numel() + 3) // 4
         return m
 
-    def q_values(self, x, train=True, mask=None, target=False):
+    def q_values(self, x, train=True, mask=None, target=False, tag: str = "act"):
+        """tag names this call's scratch (activations, split-K partials, packed weights, dropout
+        mask): forwards that may run concurrently on different streams need different tags."""
         B = x.shape[0]
         if mask is None and train:
-            mask = self.dropout_mask(B, "act")
+            mask = self.dropout_mask(B, tag)
         net = self.tnet if target else self.net
-        return net.forward(x, mask if train else None, save=False, tag="act_")
+        return net.forward(x, mask if train else None, save=False, tag=tag + "_")
 
     def learn(self, s, a, r, done, s2, mask_online=None, mask_target=None, weights=None, td_abs=None):
         """One DQNAgent.learn step on device tensors; returns the loss tensor (no host sync).
@@ -469,8 +484,9 @@ class Learner:
         Qt = self.tnet.forward(s2, mask_target, save=False, tag="t_")
         dQ = self.net.ws.get("dq", (B, self.actions), torch.float32, self.device)
         L = qlib()
+        tw = td_workspace(self.net.ws, B, 1, self.device)
         qcheck(L.evx_td_loss_w(_p(Q), _p(Qt), self.actions, _p(a), _p(r), _p(done), self.gamma, B, _p(weights),
-                               _p(dQ), _p(self.loss), _p(td_abs), _stream()), "td_loss")
+                               _p(dQ), _p(self.loss), _p(td_abs), _p(tw), tw.numel(), _stream()), "td_loss")
         self.net.backward(dQ, self.grads)
         if self.grad_hook is not None:
             self.grad_hook(self.grads.flat)
@@ -517,8 +533,9 @@ class Learner:
                                   ss=self._ss if self.grad_hook is None else None)
             self._ss_fresh = self.grad_hook is None
         else:
+            tw = td_workspace(ws, B, 1, dev)
             qcheck(L.evx_td_loss_w(_p(Q), _p(Qt), self.actions, _p(a), _p(r), _p(done), self.gamma, B, _p(weights),
-                                   _p(dQ), _p(self.loss), _p(td_abs), _stream()), "td_loss")
+                                   _p(dQ), _p(self.loss), _p(td_abs), _p(tw), tw.numel(), _stream()), "td_loss")
             self.fast.backward(B, dQ, X, H1, H2, DROPOUT_P, dz2, dz1, self.grads)
         if self.grad_hook is not None:
             self.grad_hook(self.grads.flat)
@@ -563,3 +580,13 @@ class Learner:
         self.target.flat.copy_(self.online.flat)
         if self.fast_t is not None:
             self.fast_t.repack()
+
+    def weights_written(self, target: bool = False):
+        """Call after writing a network's fp32 parameters from outside the learner (a
+        load_state_dict, a broadcast from another rank): the fused kernels read operand copies
+        (bf16 hi / lo tiles) and, once attach_static ran, a per-centre act table of fc1 --
+        the learner's online forward reads that table too -- and those are rebuilt only
+        here, in sync_target and in the optimizer step."""
+        fast = self.fast_t if target else self.fast
+        if fast is not None:
+            fast.repack()

@@ -123,7 +123,7 @@ class VecTrainer:
                  grad_hook=None, learn_every: int = 1, lagged_learn: bool = False, replay: str = "uniform",
                  prio_alpha: float = 0.6, prio_beta0: float = 0.4, prio_beta_steps: int = 100000,
                  prio_eps: float = 1e-6, groups: int = 1, layout_of=None, world_envs: Optional[int] = None,
-                 nets: str = "shared", act_row_order: bool = False):
+                 nets: str = "shared"):
         """groups: the envs are split into this many parts, each stepping on its own
         stream chain (see _Group); the env results do not depend on it (every env is
         still stepped once per step with its own streams), the act's dropout masks do.
@@ -137,9 +137,9 @@ class VecTrainer:
         its own network, memory and optimizer, as runners/train_double_dqn.py:35-56 gives each
         robot its own DQNAgent: evacx.qgroup.GroupedLearner, batch / R transitions per net per
         learn step, strict schedule, one GPU) or "qmix" (per-robot nets under a QMIX mixer,
-        runners/train_qmix.py: batch / R joint env-steps per learn step, evacx.qgroup.GroupedQMix).
-        act_row_order: the x3 act visits its rows sorted by (table path, window centre)
-        (evx_act_row_perm) instead of its envs by table path (VecEnv.act_perm); same results."""
+        runners/train_qmix.py: batch / R joint env-steps per learn step, evacx.qgroup.GroupedQMix)."""
+        if precision not in ("f32", "bf16", "exact"):
+            raise ValueError(f"precision must be 'f32', 'bf16' or 'exact', not {precision!r}")
         self.lay, self.E, self.R = layout, E, layout.R
         self.device = layout.device
         # the push reads env.obs_prev: no copy per step
@@ -163,22 +163,21 @@ class VecTrainer:
             # qmix: the R robots of an env are the agents of runners/train_qmix.py -- joint samples
             # (the same env-steps for every agent), the mixer's loss over the team reward
             self.qmix = GroupedQMix(self.glearner, seed=learner_seed) if nets == "qmix" else None
-        # conv + f32: the implicit-GEMM convolutions in the f32-accurate x3 mode (bf16 hi/lo operand
-        # pairs, as the fused MLP's f32); precision="exact" keeps the exact-f32 MFMA (the golden-test path)
-        lprec = precision
-        if kind == "conv" and precision == "f32":
-            lprec = "x3"
-        elif precision == "exact":
-            lprec = "f32"
+        # precision: "f32" -- f32-accurate x3 (the fused MLP kernels; the conv net's implicit-GEMM
+        # convolutions, bf16 hi/lo operand pairs); "bf16"; "exact" -- every product on the exact-f32
+        # MFMA GEMMs (evx_gemm f32, no fused kernels: the golden-test path, either kind)
+        lprec = "x3" if (kind == "conv" and precision == "f32") else precision
         self.learner = Learner(kind=kind, device=self.device, lr=lr, gamma=gamma, precision=lprec,
                                seed=learner_seed) if not self.per_robot else None
         # the arithmetic the Q-network actually runs: "x3" (f32 operands as bf16 hi + lo pairs on the
         # bf16 MFMA, f32 accumulation: f32 within the tests' stated tolerances), "f32" (exact f32
-        # MFMA) or "bf16"; the fused MLP kernels run x3 for precision "f32"
-        if self.per_robot or (kind == "mlp" and precision == "f32"):
+        # MFMA) or "bf16" -- read from what the learner built
+        if self.per_robot:
             self.q_arith = "x3"
+        elif self.learner.fast is not None:
+            self.q_arith = "x3" if self.learner.fast.x3 else "bf16"
         else:
-            self.q_arith = lprec
+            self.q_arith = {"exact": "f32"}.get(lprec, lprec)
         if self.learner is not None:
             self.learner.grad_hook = grad_hook
         # replay: "uniform" (DQNAgent.memory's random.sample) or "prioritized" (evacx.prio:
@@ -238,7 +237,6 @@ class VecTrainer:
         if self.fast is None:
             self.lagged = False  # the lagged schedule's two-phase learn needs the fused MLP path
         self._perm = None
-        self._rowperm = None
         if self.fast is not None and self.fast.x3 and layout_of is None and len(self.groups) == 1:
             # act fast path: envs past the fire's last step start fc1 from a per-centre table of the
             # static features' contribution (rebuilt with every weight update) and add only the
@@ -253,40 +251,11 @@ class VecTrainer:
             # past the fire's last step
             self.learner.fast_t.attach_static(lc, lc.L, lc.W, lc.t_max, x_range=xr)
             self._perm = torch.zeros(E, dtype=torch.int32, device=self.device)
-            self._rowperm = None
-            if act_row_order:
-                # the act's rows sorted by (table path, window centre) instead of its envs by table path
-                # (evx_act_row_perm): rows sharing a table row share tiles, which then read a few table
-                # rows from L2 instead of 64 scattered ones; every row keeps its own results and mask
-                L = _lib.lib()
-                L.evx_act_row_perm_bytes.restype = C.c_int64
-                L.evx_act_row_perm_bytes.argtypes = [C.c_int32]
-                L.evx_act_row_perm.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
-                                               C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]
-                L.evx_act_row_perm_last_error.restype = C.c_char_p
-                nb = int(L.evx_act_row_perm_bytes(n))
-                if nb < 0:
-                    raise _lib.EvacxError("evx_act_row_perm_bytes failed")
-                i32 = dict(dtype=torch.int32, device=self.device)
-                self._rowperm = (torch.empty(2 * n, **i32), torch.empty(n, **i32),
-                                 torch.empty(max(nb, 1), dtype=torch.uint8, device=self.device))
-                self._perm = torch.zeros(n, **i32)
             self._act_order(self.groups[0])
 
     def _act_order(self, grp: _Group):
-        """The next act's order on the current stream: its rows by (table path, window centre)
-        (evx_act_row_perm) or its envs by table path (VecEnv.act_perm)."""
-        if self._rowperm is None:
-            grp.env.act_perm(self._perm)
-            return
-        keys, rows, tmp = self._rowperm
-        c = self.fast.c
-        L = _lib.lib()
-        rc = L.evx_act_row_perm(C.byref(self.lay.c), grp.env.obs.data_ptr(), grp.n, int(c.stat_fs), int(c.stat_x0),
-                                int(c.stat_nx), keys.data_ptr(), rows.data_ptr(), self._perm.data_ptr(),
-                                tmp.data_ptr(), tmp.numel(), _stream())
-        if rc != 0:
-            raise _lib.EvacxError(f"act_row_perm failed ({rc}): {L.evx_act_row_perm_last_error().decode()}")
+        """The next act's env order on the current stream: its envs by table path (VecEnv.act_perm)."""
+        grp.env.act_perm(self._perm)
 
     def _act(self, grp: _Group):
         """DQNAgent.act in train mode for one group's robots: dropout active, epsilon-greedy
@@ -302,11 +271,11 @@ class VecTrainer:
             self.fast.act(self.lay.c, grp.env.obs, grp.n,
                           drop=(self.learner.seed, self.learner.drop_stream, DROPOUT_P, None, g0),
                           actions=grp.actions, epsilon=float(self.epsilon), act_seed=self.act_seed, act_offset=off,
-                          perm=self._perm,
-                          rows_per_env=0 if self._perm is None else (1 if self._rowperm is not None else self.R))
+                          perm=self._perm, rows_per_env=0 if self._perm is None else self.R)
             return
         x = grp.env.expand_obs(torch.float32)  # [E/G, R, 11, 11, 6]
-        Q = self.learner.q_values(x.view(grp.n, 11, 11, 6), train=True)
+        # per-group scratch: the groups' acts run concurrently on their own streams
+        Q = self.learner.q_values(x.view(grp.n, 11, 11, 6), train=True, tag=f"act{grp.g}" if grp.g else "act")
         qcheck(qlib().evx_act(Q.data_ptr(), grp.n, self.learner.actions, float(self.epsilon), self.act_seed, off,
                               grp.actions.data_ptr(), _stream()), "act")
 

@@ -88,6 +88,9 @@ typedef struct {
     int32_t *order;    /* [E+1] dispatch order of the step's envs (evx_env_order), or NULL = 0..E-1;
                         * order[E] = H: the first H of them are heavy (rows phase on a 4-wave workgroup) */
     const int32_t *layout_idx; /* [E] each env's layout in evx_layout.layout_set, or NULL (one layout) */
+    uint8_t *perm_ws;  /* [evx_perm_ws_bytes(E)] workspace of evx_env_order / evx_act_perm (their
+                        * count and rank launches); calls on one state must be stream-ordered.
+                        * NULL: evx_env_order runs its one-workgroup kernel, evx_act_perm fails */
 } evx_state;
 
 /* Compact per-robot observation (32 B). Expands to the reference's 11x11x6
@@ -105,7 +108,10 @@ typedef struct {
     uint8_t *done;     /* [E] */
     int32_t *counts;   /* [E*2] evacuated, dead after the step (may be NULL) */
     evx_obs *obs;      /* [E*R] observation after the step */
-    int32_t *err;      /* [1] sticky device error word (may be NULL) */
+    int32_t *err;      /* [1] sticky device error word (may be NULL); bits: 1 > 128 movers on one
+                        * target, 2 a runaway Python-stream window, 4 reset placement, 8 / 16
+                        * scratch or event-list overflow, 32 kept-list mismatch, 64 an MT block
+                        * overwritten before the state store (any bit: results not bit-exact) */
     int64_t *stamps;   /* [E*48] diagnostic per-phase s_memtime stamps + counters (NULL = off) */
     /* Auto-reset (NULL = off, the reference's separate env.reset): envs that finish this
      * step are reset in the same launch (evx_env_reset semantics); their terminal
@@ -148,6 +154,8 @@ int evx_env_order(const evx_layout *lay, const evx_state *st, void *stream);
 /* act row permutation for the x3 act fast path: perm[0..E) lists the envs whose fire step is >= the
  * layout's t_max (the static-table fire step) first, then the rest, each in env order (stable) */
 int evx_act_perm(const evx_layout *l, const evx_state *s, int32_t *perm, void *stream);
+/* Bytes of evx_state.perm_ws for E envs. */
+int64_t evx_perm_ws_bytes(int32_t E);
 
 /* Bytes of dynamic LDS the step kernel needs for a layout (diagnostics). */
 int64_t evx_step_lds_bytes(const evx_layout *lay);
@@ -240,20 +248,24 @@ int64_t evx_conv3x3_ws_elems(const evx_gemm_desc *g, int32_t mode, int32_t cs);
 int evx_colsum(const float *X, int64_t ld, int32_t M, int32_t N, float *out, int32_t accum, float *scratch,
                int32_t scratch_elems, void *stream);
 /* DQNAgent.learn TD step (agents/dqn_agent.py:143-151): loss = mean((Q[a] - (r + gamma*max Qt * !done))^2),
- * dQ = d loss / d Q. Q, Qt: [B][A]. */
+ * dQ = d loss / d Q. Q, Qt: [B][A]. ws: caller workspace of evx_td_loss_ws_floats(B, nets) floats
+ * (the per-block partials of the loss, summed in block order by a second launch: deterministic,
+ * no state in the library; calls on different streams need different workspaces). */
+int64_t evx_td_loss_ws_floats(int32_t B, int32_t nets);
 int evx_td_loss(const float *Q, const float *Qt, int32_t A, const int32_t *act, const float *rew,
-                const uint8_t *done, float gamma, int32_t B, float *dQ, float *loss, void *stream);
+                const uint8_t *done, float gamma, int32_t B, float *dQ, float *loss, float *ws, int64_t ws_floats,
+                void *stream);
 /* evx_td_loss with optional importance weights w [B] (prioritized replay: loss = mean(w (q - y)^2),
  * dQ scaled by w) and optional td_abs [B] = |q - y| (the new priorities); w = td_abs = NULL is
  * evx_td_loss. */
 int evx_td_loss_w(const float *Q, const float *Qt, int32_t A, const int32_t *act, const float *rew,
                   const uint8_t *done, float gamma, int32_t B, const float *w, float *dQ, float *loss,
-                  float *td_abs, void *stream);
+                  float *td_abs, float *ws, int64_t ws_floats, void *stream);
 /* evx_td_loss_w plus clearing zero[0..nzero) (the gradient buffer the backward accumulates into)
  * in the same launch (extra workgroups) */
 int evx_td_loss_zero(const float *Q, const float *Qt, int32_t A, const int32_t *act, const float *rew,
                      const uint8_t *done, float gamma, int32_t B, const float *w, float *dQ, float *loss, float *td_abs,
-                     float *zero, int64_t nzero, void *stream);
+                     float *zero, int64_t nzero, float *ws, int64_t ws_floats, void *stream);
 /* ||g||_2 into norm[0] (clip_grad_norm_'s total norm) */
 int evx_sumsq_norm(const float *g, int64_t n, float *scratch, int32_t scratch_elems, float *norm, void *stream);
 /* g *= min(1, max_norm/(norm+1e-6)) (skipped if norm NULL) then one torch.optim.Adam step */
@@ -349,10 +361,11 @@ int evx_gather_obs(const evx_obs *src, const int64_t *idx, int32_t n, evx_obs *d
 /* DQNNetwork conv layers (agents/dqn_agent.py:22-24) as im2col + GEMM on 11x11 maps */
 int evx_im2col3x3(const float *x, int32_t B, int32_t C, int32_t nhwc, float *cols, void *stream);
 int evx_col2im3x3(const float *dcols, int32_t B, int32_t C, float *dx, void *stream);
-/* [B*121][C] pixel-major <-> [B][C][121] NCHW (to_nchw), C <= 134 */
 /* NCHW [B][C][121] f32 -> pixel-major [B][121*C] as bf16 hi / lo planes (lo B*121*C elements after
    hi): the x3 operand of an EVX_GEMM_SPLIT_AB GEMM (the conv net's fc1 weights), C <= 134 */
 int evx_pix_split(const float *src, int32_t B, int32_t C, uint16_t *dst, void *stream);
+/* [B*121][C] pixel-major <-> [B][C][121] NCHW (to_nchw): through LDS for C <= 134, element-wise
+   beyond (any C) */
 int evx_pix_nchw(const float *src, int32_t B, int32_t C, int32_t to_nchw, float *dst, void *stream);
 int evx_relu_grad(float *dy, const float *y, int64_t n, void *stream);
 const char *evx_q_last_error(void);
@@ -409,8 +422,8 @@ typedef struct {
     /* x3: h1 holds two planes [2][n][512] (hi, lo) and x spans [n][640] */
     /* act only, optional: batch row i is observation / action row perm[i / rows_per_env] * rows_per_env +
      * i % rows_per_env (evx_act_perm: envs at the table's fire step first, so act tiles are uniform);
-     * dropout rows and epsilon draws stay keyed by that original row. rows_per_env 1 (x3 act only):
-     * a row permutation (evx_act_row_perm), every tile row hashing its own dropout pair */
+     * dropout rows and epsilon draws stay keyed by that original row; rows_per_env even (dropout
+     * row pairs stay together) */
     const int32_t *perm;
     int32_t rows_per_env;
 } evx_qmlp_fwd_out;
@@ -443,16 +456,6 @@ int evx_qmlp_forward(const evx_layout *lay, const evx_obs *obs, int32_t n, const
  * set): the same products summed in another order. */
 int evx_qmlp_act(const evx_layout *lay, const evx_obs *obs, int32_t n, const evx_qmlp_params *p,
                  const evx_qmlp_dropout *drop, const evx_qmlp_fwd_out *out, void *stream);
-/* The x3 act's row order (DQNAgent.act, agents/dqn_agent.py:101-124): perm [n] = the rows of obs
- * sorted by (not on the table path of p's stat_fs / stat_x0 / stat_nx -- stat_fs < 0: none --,
- * window centre), stably (a radix sort: deterministic), for evx_qmlp_act's perm with rows_per_env
- * 1: rows sharing an act-table row share tiles. keys [2n], rows [n] scratch; temp of
- * evx_act_row_perm_bytes(n) bytes. Changes no result of the act. */
-int64_t evx_act_row_perm_bytes(int32_t n);
-int evx_act_row_perm(const evx_layout *lay, const evx_obs *obs, int32_t n, int32_t stat_fs, int32_t stat_x0,
-                     int32_t stat_nx, uint32_t *keys, int32_t *rows, int32_t *perm, void *temp, int64_t temp_bytes,
-                     void *stream);
-const char *evx_act_row_perm_last_error(void);
 /* Two forwards of n rows in one launch pair (the learner's online and target nets). */
 int evx_qmlp_forward2(const evx_layout *lay, int32_t n, const evx_obs *obs0, const evx_qmlp_params *p0,
                       const evx_qmlp_dropout *drop0, const evx_qmlp_fwd_out *out0, const evx_obs *obs1,
@@ -523,10 +526,11 @@ int evx_qmlp_forward2_g(const evx_layout *lay, int32_t n, int32_t nets, const ev
                         const evx_obs *obs1, const evx_qmlp_params *p1, const evx_qmlp_dropout *drop1,
                         const evx_qmlp_fwd_out *out1, void *stream);
 /* evx_td_loss_zero per net: rows [g B, (g + 1) B) of Q / Qt / act / rew / done / dQ, loss[g]
- * = mean over the net's rows (nets <= 64, nets * ceil(B / 256) <= 4096). */
+ * = mean over the net's rows; ws of evx_td_loss_ws_floats(B, nets) floats. */
 int evx_td_loss_zero_g(const float *Q, const float *Qt, int32_t A, const int32_t *act, const float *rew,
                        const uint8_t *done, float gamma, int32_t B, int32_t nets, const float *w, float *dQ,
-                       float *loss, float *td_abs, float *zero, int64_t nzero, void *stream);
+                       float *loss, float *td_abs, float *zero, int64_t nzero, float *ws, int64_t ws_floats,
+                       void *stream);
 /* evx_qmlp_backward_ss for the blocked forward of evx_qmlp_forward2_g (gradients cleared by the
  * caller); g->part: [nets][evx_qmlp_backward_part_floats(B)], ss [nets][evx_qmlp_norm_parts()]. */
 int evx_qmlp_backward_ss_g(const evx_qmlp_params *p, int32_t B, int32_t nets, const float *dq, const uint16_t *x,

@@ -352,21 +352,23 @@ def test_heavy_and_light_parts_on_two_streams_match_one_launch():
     b.check_err()
 
 
-@pytest.mark.parametrize("E", [4096, 32768])
-def test_stationary_mix_matches_oracle_at_bench_scale(E):
+@pytest.mark.parametrize("L,P,R,E", [(128, 2276, 16, 4096), (128, 2276, 16, 32768), (64, 569, 8, 4096)],
+                         ids=["cfg3-4096", "cfg3-32768", "cfg2-4096"])
+def test_stationary_mix_matches_oracle_at_bench_scale(L, P, R, E):
     """Parity where bench.py times: cfg3 (128x128, P 2276, R 16) at E envs -- 32768 is the bench
-    workload (one-wave workgroups), 4096 the 4-wave workgroups with the heavy-env path --
-    prepared exactly as bench.py --phase stationary does (1300 env-only steps, env g force-reset
-    at preparation step g % 1200: env ages spread over an episode, saturated fire, heavy and
-    light envs, fused auto-resets); then 64 envs spread over the age mix are snapshotted into
-    the oracle and both step 100 more steps with the same actions -- every state field, MT
-    stream, reward and done flag bit-exact on every step (the GPU steps all E envs with the
-    heavy-first dispatch order, as in the bench)."""
+    workload (one-wave workgroups, env_step_kernel<1,false,false>), 4096 the 4-wave workgroups with
+    the heavy-env path -- and cfg2 (64x64, P 569, R 8) at its bench size of 4096 envs, prepared
+    exactly as bench.py --phase stationary does (1300 env-only steps, env g force-reset at
+    preparation step g % 1200: env ages spread over an episode, saturated fire, heavy and light
+    envs, fused auto-resets); then 64 envs spread over the age mix are snapshotted into the oracle
+    and both step 100 more steps with the same actions -- every state field, MT stream, reward,
+    done flag, observation and terminal observation (obs_term, on done) bit-exact on every step
+    (the GPU steps all E envs with the heavy-first dispatch order, as in the bench).
+    Reference: envs/evacuation_env.py:84-120 (_get_state), :122-172 (step), people.py:196-314."""
     _need_gpu()
     from evacx.env import DeviceLayout, VecEnv
     from evacx.layout import build_tables, synthetic
     from oracle import oracle as orc
-    P, R, L = 2276, 16, 128
     tables = build_tables(synthetic(L, L, R))
     lay = DeviceLayout(tables, P)
     env = VecEnv(lay, E)
@@ -381,6 +383,7 @@ def test_stationary_mix_matches_oracle_at_bench_scale(E):
         if w < 1200:
             env.reset(mask=(gid % 1200 == w) & ~env.done.bool())
     ids = list(range(0, E, E // 64))
+    idt = torch.tensor(ids, device="cuda")
     olay = orc.Layout.from_tables(tables, P)
     oenvs = []
     for st in env.host_states(ids):
@@ -397,15 +400,21 @@ def test_stationary_mix_matches_oracle_at_bench_scale(E):
         env.step(torch.from_numpy(a.reshape(-1)).cuda(), auto_reset=True)
         rew = env.reward[ids].cpu().numpy()
         dn = env.done[ids].cpu().numpy()
+        ob = env.expand_obs(torch.float64, env.obs.view(E, -1)[idt].reshape(-1)).cpu().numpy()
+        term = env.expand_obs(torch.float64, env.obs_term.view(E, -1)[idt].reshape(-1)).cpu().numpy() \
+            if dn.any() else None
         sts = env.host_states(ids)
         for j, (e, oe) in enumerate(zip(ids, oenvs)):
-            _, r, d = oe.step(a[e])
+            oobs, r, d = oe.step(a[e])
             assert rew[j] == r and bool(dn[j]) == d, (s, e, rew[j], r)
             if d:
-                oe.reset()
+                assert np.array_equal(term[j], oobs), (s, e, "terminal obs")
+                oobs = oe.reset()
                 n_done += 1
+            assert np.array_equal(ob[j], oobs), (s, e, "obs")
             st = sts[j]
             for k in ["pos", "flags", "health", "acc", "rmap", "robots", "view", "scal", "py_mt", "np_mt"]:
                 assert np.array_equal(st[k], getattr(oe, k)), (s, e, k)
     env.check_err()
-    print(f"stationary mix: ages {ages.min()}..{ages.max()}, heavy at start {heavy0}, resets {n_done}")
+    print(f"stationary mix {L}x{L} R{R} E{E}: ages {ages.min()}..{ages.max()}, heavy at start {heavy0}, "
+          f"resets {n_done}")

@@ -137,8 +137,9 @@ def test_fused_backward_matches_torch_autograd():
     loss = torch.empty(1, device=dev)
     fast.forward(lay.c, obs_s, B, H1, drop=(5, 1, 0.2), x=X, h2=H2, q=Q)
     fast_t.forward(lay.c, obs_s2, B, H1t, drop=(5, 2, 0.2), q=Qt)
+    tw = torch.empty(int(qlib().evx_td_loss_ws_floats(B, 1)), device=dev)
     qcheck(qlib().evx_td_loss(Q.data_ptr(), Qt.data_ptr(), 5, a.data_ptr(), r.data_ptr(), done.data_ptr(), 0.99, B,
-                              dQ.data_ptr(), loss.data_ptr(), 0), "td")
+                              dQ.data_ptr(), loss.data_ptr(), tw.data_ptr(), tw.numel(), 0), "td")
     dz2 = torch.empty(B * 256, dtype=torch.int16, device=dev)
     dz1 = torch.empty(B * HID, dtype=torch.int16, device=dev)
     fast.backward(B, dQ, X, H1, H2, 0.2, dz2, dz1, lr.grads)

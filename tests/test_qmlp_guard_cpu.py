@@ -79,3 +79,18 @@ def test_backward_rejects_short_saved_buffers(short):
     bufs[short] = bufs[short][:-1]
     with pytest.raises(ValueError, match=f"backward: {short}"):
         f.backward(B, bufs["dq"], bufs["x"], bufs["h1"], bufs["h2"], 0.2, bufs["dz2"], bufs["dz1"], grads=None)
+
+
+@pytest.mark.parametrize("prec", ["fp32", "x3", "exactf32", ""])
+def test_trainer_rejects_unknown_precision(prec):
+    """VecTrainer takes "f32" (x3 fused kernels / x3 conv), "bf16" or "exact" (dense exact-f32 GEMMs),
+    and refuses anything else before touching the device."""
+    from evacx.trainer import VecTrainer
+    with pytest.raises(ValueError, match="precision"):
+        VecTrainer(None, 1, precision=prec)
+
+
+def test_learner_rejects_unknown_precision():
+    from evacx.qnet import Learner
+    with pytest.raises(ValueError, match="precision"):
+        Learner(kind="mlp", device="cpu", precision="f16")
