@@ -55,7 +55,8 @@ constexpr int CL_CAP = 510;          // contested movers sorted in LDS (more: gl
                                      // in the planner queue (both dead after the rows)
 constexpr int EV_CAP = 256;          // order-sensitive occupancy events
 constexpr int LEAF_CAP = 256;        // numpy pairwise leaves (n <= 16383 needs <= 128)
-constexpr int GRP_MAX = 128;         // movers of one contested target
+constexpr int GRP_MAX = 128;         // movers of one contested target (8 neighbour cells; more only
+                                     // where placement stacked persons on one cell; beyond: err 1)
 constexpr int GBITS = 13;            // group index bits in a sorted group head
 constexpr uint32_t DONEPK = 3u << 24;
 #ifndef EVX_GQ
@@ -621,7 +622,7 @@ __device__ __forceinline__ void contested_groups(T* Lp, T* heads, T* gstart, int
         const int gi = (int)(heads[k] & ((1u << GBITS) - 1u));
         const int s0 = (int)gstart[gi], cnt = (int)gstart[gi + 1] - s0;
         heads[k] = ((uint32_t)s0 << 8) | (uint32_t)min(cnt, 255);
-        if (cnt > GRP_MAX) err |= 1;  // > 128 movers on one target: not representable, flagged
+        if (cnt > GRP_MAX) err |= 1;  // > GRP_MAX movers on one target: not representable, flagged
     }
     err = __ballot(err != 0) ? (err | 1) : err;
     wave_sync();
@@ -853,7 +854,6 @@ __host__ __device__ inline WaveLds wave_lds(int L, int W, int P, int R, bool big
             s.vac = o; o += RW;
         }
     }
-    s.nearc = o; o += NCW;
     if (bigg) {
         s.lost = -1;  // global scratch, after the three bitmaps
     } else {
@@ -863,6 +863,14 @@ __host__ __device__ inline WaveLds wave_lds(int L, int W, int P, int R, bool big
     s.robots = o; o += (R + 3) & ~3;  // 16-B aligned: read 4 robots at a time
     o = (o + 1) & ~1;
     s.misc = o; o += GRP_MAX + 16;         // shuffle group; event counter; pairwise stacks
+    // the near-robot block map is read only by the rows (dir_prep), before misc is first written
+    // (the contested groups): it overlays misc when it fits (256x256: 16.6 -> 16.1 KB per env, 9 -> 10
+    // envs per CU by LDS; 128x128 stays at 12, its VGPR limit)
+    if (NCW <= GRP_MAX + 16) {
+        s.nearc = s.misc;
+    } else {
+        s.nearc = o; o += NCW;
+    }
     s.total = (o + 3) & ~3;
     return s;
 }
@@ -935,6 +943,13 @@ __device__ __forceinline__ double readlane_d(double v, int k) {
     return __hiloint2double(hi, lo);
 }
 
+// the class byte of an env (evx_state.perm_ws; see env_orders_kernel)
+__device__ __forceinline__ uint8_t env_class(const evx_layout& lay, int fs, int evac, int dead) {
+    const int P = lay.P, rem = P - evac - dead;
+    const int b = 15 - min(15, max(0, rem) * 16 / (P + 1));
+    const int hmin = max(1, P / 4);  // heavy_cap's threshold
+    return (uint8_t)(b | (fs >= lay.t_max ? 0x10 : 0) | (rem >= hmin ? 0x20 : 0));
+}
 template <bool BIGG = false>
 __device__ __forceinline__ void reset_one(const evx_layout& lay, const evx_state& st, const int e, uint32_t* smem,
                                           evx_obs* obs, int32_t* err);
@@ -2613,6 +2628,7 @@ __device__ __forceinline__ void step_env(const evx_layout& lay, const evx_state&
         sg[2] = evac;
         sg[3] = dead;
         st.view[e] = view;
+        if (st.perm_ws) st.perm_ws[e] = env_class(lay, fs1, evac, dead);  // a fused reset rewrites it
         if (err && out.err) atomicOr(out.err, err);
         // the lists the next light step starts from (a wide step's are not kept; a fused reset
         // below invalidates them again)
@@ -2827,6 +2843,7 @@ __device__ __forceinline__ void reset_one(const evx_layout& lay, const evx_state
         sg[3] = 0;
     }
     const int fs = st.scal[(size_t)e * 4];
+    if (lane == 0 && st.perm_ws) st.perm_ws[e] = env_class(lay, fs, 0, 0);
     if (obs) {
         for (int r = 0; r < R; r++) {
             const uint32_t c = (r == 0) ? view : st.robots[(size_t)e * R + r];
@@ -3010,96 +3027,140 @@ __global__ __launch_bounds__(1024) void env_order_kernel(evx_layout lay, evx_sta
 }
 
 // ------------------------------------------------------- act permutation
-// evx_act_perm: the envs whose fire has reached the layout's last step (fire_step >= t_max,
-// the x3 act's table fire step) first, then the rest, each part in env order. One workgroup:
-// thread t owns the contiguous envs [t * per, (t + 1) * per); a block scan of the counts
-// places them.
-// The two scheduling permutations over many workgroups (one per 1024 envs, two launches each):
-// a count launch leaves every chunk's per-class counts and the classes of its envs (one byte per
-// env, so the rank launch sees exactly the state the counts saw), and a rank launch turns the
-// counts of the chunks before it into each class's first rank and places its envs by ballots
-// (stable: env order within a class). One workgroup doing all of it took 55-120 us beside the
-// learner (a 1024-thread workgroup with loads in series, which also slowed the kernels next to it).
-//   order: 16 buckets of persons remaining (0 = most), heavy count in slot 16;
-//   act perm: 2 classes (fire step >= t_max first).
-constexpr int PCL = 17;  // per-chunk count slots: 16 classes + the heavy count
-__global__ __launch_bounds__(1024) void perm_count_kernel(evx_layout lay, evx_state st, int mode, int hmin,
-                                                          uint8_t* __restrict__ cls, int* __restrict__ cnt) {
-    __shared__ int wc[16][16], wh[16];
-    const int t = (int)threadIdx.x, lane = t & 63, w = t >> 6, E = st.E, P = lay.P;
-    const int e = (int)blockIdx.x * 1024 + t;
-    int b = -1, heavy = 0;
-    if (e < E) {
-        if (mode == 0) {
-            const unsigned long long v = __hip_atomic_load(
-                reinterpret_cast<const unsigned long long*>(st.scal + (size_t)e * 4 + 2), __ATOMIC_RELAXED,
-                __HIP_MEMORY_SCOPE_AGENT);
-            const int rem = P - (int)(uint32_t)v - (int)(uint32_t)(v >> 32);
-            b = 15 - min(15, max(0, rem) * 16 / (P + 1));
-            heavy = rem >= hmin;
-        } else {
-            b = st.scal[(size_t)e * 4] >= lay.t_max ? 0 : 1;
-        }
-        cls[e] = (uint8_t)b;
-    }
-    int mine = 0;
-#pragma unroll
-    for (int bb = 0; bb < 16; bb++) {
-        const int n = __popcll(__ballot(b == bb));
-        mine = lane == bb ? n : mine;
-    }
-    if (lane < 16) wc[w][lane] = mine;
-    int hs = heavy;
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) hs += __shfl_xor(hs, o, 64);
-    if (lane == 0) wh[w] = hs;
-    __syncthreads();
-    if (t < 16) {
-        int sm = 0;
-        for (int k = 0; k < 16; k++) sm += wc[k][t];
-        cnt[blockIdx.x * PCL + t] = sm;
-    } else if (t == 16) {
-        int sm = 0;
-        for (int k = 0; k < 16; k++) sm += wh[k];
-        cnt[blockIdx.x * PCL + 16] = sm;
-    }
+// The two scheduling permutations (results never depend on them) from one class byte per env
+// (evx_state.perm_ws): bits 0-3 the bucket of persons remaining (0 = most), bit 4 fire step >=
+// t_max (the x3 act's table path), bit 5 heavy (>= P/4 persons remaining). The step and reset
+// kernels write an env's byte as they finish with it, so the orders of the next step need no pass
+// over the state (evx_env_classes rewrites every byte from the state words, for states written
+// from the host).
+__global__ __launch_bounds__(256) void env_classes_kernel(evx_layout lay, evx_state st) {
+    const int e = (int)blockIdx.x * 256 + (int)threadIdx.x;
+    if (e >= st.E) return;
+    const int4 v = *reinterpret_cast<const int4*>(st.scal + (size_t)e * 4);
+    st.perm_ws[e] = env_class(lay, v.x, v.z, v.w);
 }
-__global__ __launch_bounds__(1024) void perm_rank_kernel(evx_state st, int mode, int hcap, const uint8_t* __restrict__ cls,
-                                                         const int* __restrict__ cnt, int32_t* __restrict__ out) {
-    __shared__ int base[16], wc[16][16], tot[PCL], pre[PCL];
-    const int t = (int)threadIdx.x, lane = t & 63, w = t >> 6, E = st.E;
-    const int c = (int)blockIdx.x, nch = (E + 1023) / 1024;
-    if (t < 64 * 2 && (t & 63) < PCL) {  // waves 0 / 1: slot s's total over all chunks / over chunks < c
-        const int sl = t & 63;
-        const int kend = t < 64 ? nch : c;
-        int sm = 0;
-#pragma unroll 8
-        for (int k = 0; k < kend; k++) sm += cnt[k * PCL + sl];  // loads in flight 8 at a time
-        if (t < 64) tot[sl] = sm;
-        else pre[sl] = sm;
-    }
-    __syncthreads();
-    if (t < 16) {  // class t: the envs of lower classes, then class t's envs in the chunks before this one
-        int below = 0;
-        for (int bb = 0; bb < t; bb++) below += tot[bb];
-        base[t] = below + pre[t];
-    }
-    if (c == 0 && t == 64 && mode == 0) out[E] = min(hcap, tot[16]);
-    const int e = c * 1024 + t;
-    const int b = e < E ? (int)cls[e] : -1;
-    int mine = 0, r = 0;
+// One launch, workgroup c ranking the envs [1024 c, 1024 c + 1024) (stable: env order within a
+// class):
+//   order[0, E): the envs by bucket (most persons remaining first), order[E] = min(hcap, heavy);
+//   perm[0, E): the envs at fire step >= t_max first, then the rest.
+// Either output may be NULL. Every workgroup counts the classes of all E envs (one byte each, L2)
+// itself -- the totals set where each class starts, the chunks before c where this chunk's run of
+// it starts -- so no second launch or workspace carries counts between workgroups. Per 64 envs a
+// wave takes 7 ballots (4 bucket bits, valid, fire, heavy); lane k < 16 counts bucket k as the AND
+// of the bit ballots that match k. Slots: 0-15 buckets, 16 fire class, 17 heavy, 18 valid.
+constexpr int OSL = 19;
+__device__ __forceinline__ unsigned long long bucket_eq(int k, const unsigned long long (&m)[4], unsigned long long v) {
 #pragma unroll
-    for (int bb = 0; bb < 16; bb++) {
-        const unsigned long long m = __ballot(b == bb);
-        mine = lane == bb ? __popcll(m) : mine;
-        r = b == bb ? lanes_below(m) : r;
+    for (int j = 0; j < 4; j++) v &= ((k >> j) & 1) ? m[j] : ~m[j];
+    return v;
+}
+template <bool V16>  // V16: cls 16-B aligned -- the scan reads 16 class bytes per lane
+__global__ __launch_bounds__(1024) void env_orders_kernel(const uint8_t* __restrict__ cls, int E, int hcap,
+                                                          int32_t* __restrict__ order, int32_t* __restrict__ perm) {
+    __shared__ int wt[16][OSL], wp[16][OSL], wc[16][OSL];
+    const int tid = (int)threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int c0 = (int)blockIdx.x * 1024;
+    auto ballots = [&](int b, unsigned long long (&m)[4], unsigned long long& mv, unsigned long long& mf,
+                       unsigned long long& mh) {
+        mv = __ballot(b >= 0);
+#pragma unroll
+        for (int j = 0; j < 4; j++) m[j] = __ballot(b >= 0 && ((b >> j) & 1));
+        mf = __ballot(b >= 0 && (b & 0x10));
+        mh = __ballot(b >= 0 && (b & 0x20));
+    };
+    auto slot_count = [&](const unsigned long long (&m)[4], unsigned long long mv, unsigned long long mf,
+                          unsigned long long mh) -> int {  // lane k < OSL: this block's count of slot k
+        const int k = lane < 16 ? lane : 0;
+        const unsigned long long sel = lane < 16 ? bucket_eq(k, m, mv) : lane == 16 ? mf : lane == 17 ? mh : mv;
+        return lane < OSL ? __popcll(sel) : 0;
+    };
+    // every class byte of the launch: totals (t) and the chunks before this one (p)
+    int t = 0, pr = 0;
+    if constexpr (V16) {
+        // wave w reads the 1024-env chunks w, w + 16, ..: lane l holds envs 16 l .. 16 l + 15 of one,
+        // two chunks' loads in flight before either is counted (byte j of every lane: one ballot set)
+        for (int q0 = w; q0 * 1024 < E; q0 += 32) {
+            uint4 v[2];
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+                const int e0 = (q0 + 16 * i) * 1024 + 16 * lane;
+                v[i] = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
+                if (e0 < E) v[i] = *reinterpret_cast<const uint4*>(cls + e0);
+            }
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+                const int q = q0 + 16 * i, e0 = q * 1024 + 16 * lane;
+                const uint32_t wd[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+                int n = 0;
+#pragma unroll
+                for (int j = 0; j < 16; j++) {
+                    const int b = e0 + j < E ? (int)((wd[j >> 2] >> (8 * (j & 3))) & 0xffu) : -1;
+                    unsigned long long m[4], mv, mf, mh;
+                    ballots(b, m, mv, mf, mh);
+                    n += slot_count(m, mv, mf, mh);
+                }
+                t += n;
+                pr += q * 1024 < c0 ? n : 0;
+            }
+        }
+    } else {
+        const int nb = (E + 63) / 64;
+#pragma unroll 4
+        for (int blk = w; blk < nb; blk += 16) {
+            const int e = blk * 64 + lane;
+            const int b = e < E ? (int)cls[e] : -1;
+            unsigned long long m[4], mv, mf, mh;
+            ballots(b, m, mv, mf, mh);
+            const int n = slot_count(m, mv, mf, mh);
+            t += n;
+            pr += blk * 64 < c0 ? n : 0;
+        }
     }
-    if (lane < 16) wc[w][lane] = mine;
+    if (lane < OSL) {
+        wt[w][lane] = t;
+        wp[w][lane] = pr;
+    }
+    // this chunk: the waves' counts (for the ranks across waves) and the in-wave masks
+    const int e = c0 + tid;
+    const int b = e < E ? (int)cls[e] : -1;
+    unsigned long long m[4], mv, mf, mh;
+    ballots(b, m, mv, mf, mh);
+    const int n = slot_count(m, mv, mf, mh);
+    if (lane < OSL) wc[w][lane] = n;
     __syncthreads();
-    if (b >= 0) {
-        int rank = base[b] + r;
-        for (int k = 0; k < w; k++) rank += wc[k][b];
-        out[rank] = e;
+    if (tid < OSL) {  // totals and prefix over the waves' partial counts (into wt[0], wp[0])
+        int st = 0, sp = 0;
+        for (int k = 0; k < 16; k++) {
+            st += wt[k][tid];
+            sp += wp[k][tid];
+        }
+        wt[0][tid] = st;
+        wp[0][tid] = sp;
+    }
+    __syncthreads();
+    if (b < 0) return;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    if (order) {
+        const int bk = b & 15;
+        int base = wp[0][bk];
+        for (int k = 0; k < bk; k++) base += wt[0][k];
+        for (int k = 0; k < w; k++) base += wc[k][bk];
+        order[base + __popcll(bucket_eq(bk, m, mv) & lt)] = e;
+        if (e == 0) order[E] = min(hcap, wt[0][17]);
+    }
+    if (perm) {
+        const bool f = (b & 0x10) != 0;
+        int base;
+        if (f) {
+            base = wp[0][16];
+            for (int k = 0; k < w; k++) base += wc[k][16];
+            base += __popcll(mf & lt);
+        } else {  // after every fire-class env: the non-fire envs before this one
+            base = wt[0][16] + (wp[0][18] - wp[0][16]);
+            for (int k = 0; k < w; k++) base += wc[k][18] - wc[k][16];
+            base += __popcll(mv & ~mf & lt);
+        }
+        perm[base] = e;
     }
 }
 
@@ -3316,9 +3377,9 @@ int evx_env_reset(const evx_layout* l, const evx_state* s, const uint8_t* mask, 
     return e == hipSuccess ? 0 : hip_fail(e, "env_reset launch");
 }
 
-// The scheduling permutations' workspace in evx_state.perm_ws: the class byte of every env (rounded
-// up to 256 B), then PCL counts per 1024 envs.
-static int64_t perm_ws_need(int64_t E) { return (E + 255) / 256 * 256 + (E + 1023) / 1024 * evx::PCL * 4; }
+// The scheduling permutations' workspace in evx_state.perm_ws: the class byte of every env.
+static int64_t perm_ws_need(int64_t E) { return (E + 255) / 256 * 256; }
+constexpr int ORDERS_MAX_E = 160 * 1024 - 4096;  // env_order_kernel's LDS (no workspace): one byte per env
 
 namespace evx {
 // diagnostic / test entry (evx_diag_sort_keys): one wave sorts n distinct keys in place in global
@@ -3340,30 +3401,37 @@ int evx_diag_sort_keys(uint32_t* keys, uint32_t* pad, int32_t n, void* stream) {
     return e == hipSuccess ? 0 : hip_fail(e, "diag_sort_keys launch");
 }
 
+static int launch_orders(const evx_layout* l, const evx_state* s, int32_t* order, int32_t* perm, hipStream_t st) {
+    int hmin = 0;
+    const int hcap = heavy_cap(*l, &hmin);
+    const dim3 grid((unsigned)((s->E + 1023) / 1024));
+    if (((uintptr_t)s->perm_ws & 15) == 0)
+        hipLaunchKernelGGL(evx::env_orders_kernel<true>, grid, dim3(1024), 0, st, (const uint8_t*)s->perm_ws, s->E,
+                           hcap, order, perm);
+    else  // a part's slice of the class bytes at an unaligned offset
+        hipLaunchKernelGGL(evx::env_orders_kernel<false>, grid, dim3(1024), 0, st, (const uint8_t*)s->perm_ws, s->E,
+                           hcap, order, perm);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : hip_fail(e, "env_orders launch");
+}
+
 int evx_env_order(const evx_layout* l, const evx_state* s, void* stream) {
     int rc = check_layout(l);
     if (rc) return rc;
     if (!s || !s->order) return fail(-22, "env_order: state.order is NULL");
     if (s->E <= 0) return 0;
-    if (s->E > 160 * 1024 - 4096) return fail(-22, "env_order: too many envs for one workgroup's LDS");
+    if (s->perm_ws) return launch_orders(l, s, s->order, nullptr, (hipStream_t)stream);
+    if (s->E > ORDERS_MAX_E) return fail(-22, "env_order: too many envs for one workgroup's LDS");
+    // no workspace: the one-workgroup kernel reads every env's counters from the state
     int hmin = 0;
     const int hcap = heavy_cap(*l, &hmin);
     {
         static std::atomic<uint64_t> attr_done;
         const void* ks[1] = {(const void*)evx::env_order_kernel};
-        evxh::max_lds_once(attr_done, ks, 1, 160 * 1024 - 4096);
+        evxh::max_lds_once(attr_done, ks, 1, ORDERS_MAX_E);
     }
-    if (s->perm_ws) {  // count + rank launches, one workgroup per 1024 envs
-        uint8_t* cls = s->perm_ws;
-        int* cnt = reinterpret_cast<int*>(s->perm_ws + ((int64_t)s->E + 255) / 256 * 256);
-        const unsigned nch = (unsigned)((s->E + 1023) / 1024);
-        hipLaunchKernelGGL(evx::perm_count_kernel, dim3(nch), dim3(1024), 0, (hipStream_t)stream, *l, *s, 0, hmin, cls, cnt);
-        hipLaunchKernelGGL(evx::perm_rank_kernel, dim3(nch), dim3(1024), 0, (hipStream_t)stream, *s, 0, hcap, cls, cnt,
-                           s->order);
-    } else {  // no workspace: one 1024-thread workgroup walks every env
-        const size_t lds = ((size_t)s->E + 3) & ~(size_t)3;  // one bucket byte per env
-        hipLaunchKernelGGL(evx::env_order_kernel, dim3(1), dim3(1024), lds, (hipStream_t)stream, *l, *s, hcap, hmin);
-    }
+    const size_t lds = ((size_t)s->E + 3) & ~(size_t)3;  // one bucket byte per env
+    hipLaunchKernelGGL(evx::env_order_kernel, dim3(1), dim3(1024), lds, (hipStream_t)stream, *l, *s, hcap, hmin);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : hip_fail(e, "env_order launch");
 }
@@ -3376,13 +3444,26 @@ int evx_act_perm(const evx_layout* l, const evx_state* s, int32_t* perm, void* s
     if (!s || !perm) return fail(-22, "act_perm: NULL argument");
     if (s->E <= 0) return 0;
     if (!s->perm_ws) return fail(-22, "act_perm: state.perm_ws is NULL (evx_perm_ws_bytes(E) bytes)");
-    uint8_t* cls = s->perm_ws;
-    int* cnt = reinterpret_cast<int*>(s->perm_ws + ((int64_t)s->E + 255) / 256 * 256);
-    const unsigned nch = (unsigned)((s->E + 1023) / 1024);
-    hipLaunchKernelGGL(evx::perm_count_kernel, dim3(nch), dim3(1024), 0, (hipStream_t)stream, *l, *s, 1, 0, cls, cnt);
-    hipLaunchKernelGGL(evx::perm_rank_kernel, dim3(nch), dim3(1024), 0, (hipStream_t)stream, *s, 1, 0, cls, cnt, perm);
+    return launch_orders(l, s, nullptr, perm, (hipStream_t)stream);
+}
+
+int evx_env_orders(const evx_layout* l, const evx_state* s, int32_t* perm, void* stream) {
+    int rc = check_layout(l);
+    if (rc) return rc;
+    if (!s || !s->order || !s->perm_ws) return fail(-22, "env_orders: state.order / state.perm_ws is NULL");
+    if (s->E <= 0) return 0;
+    return launch_orders(l, s, s->order, perm, (hipStream_t)stream);
+}
+
+int evx_env_classes(const evx_layout* l, const evx_state* s, void* stream) {
+    int rc = check_layout(l);
+    if (rc) return rc;
+    if (!s || !s->scal || !s->perm_ws) return fail(-22, "env_classes: state.scal / state.perm_ws is NULL");
+    if (s->E <= 0) return 0;
+    hipLaunchKernelGGL(evx::env_classes_kernel, dim3((unsigned)((s->E + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       *l, *s);
     hipError_t e = hipGetLastError();
-    return e == hipSuccess ? 0 : hip_fail(e, "act_perm launch");
+    return e == hipSuccess ? 0 : hip_fail(e, "env_classes launch");
 }
 
 int evx_obs_expand_f32(const evx_layout* l, const evx_obs* obs, int64_t n, float* out, void* stream) {

@@ -70,6 +70,8 @@ def lib():
         L.evx_seed_host.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
         L.evx_env_order.argtypes = [C.POINTER(evx_layout), C.POINTER(evx_state), C.c_void_p]
         L.evx_act_perm.argtypes = [C.POINTER(evx_layout), C.POINTER(evx_state), C.c_void_p, C.c_void_p]
+        L.evx_env_orders.argtypes = [C.POINTER(evx_layout), C.POINTER(evx_state), C.c_void_p, C.c_void_p]
+        L.evx_env_classes.argtypes = [C.POINTER(evx_layout), C.POINTER(evx_state), C.c_void_p]
         L.evx_perm_ws_bytes.restype = C.c_int64
         L.evx_perm_ws_bytes.argtypes = [C.c_int32]
         _lib = L
@@ -83,4 +85,5 @@ def check(rc: int, what: str):
 
 # every C symbol include/evacx.h declares (checked by tests/test_abi.py)
 EXPORTS = ["evx_env_step", "evx_env_reset", "evx_obs_expand_f32", "evx_obs_expand_f64", "evx_seed_host",
-           "evx_step_lds_bytes", "evx_step_scratch_words", "evx_last_error", "evx_perm_ws_bytes"]
+           "evx_step_lds_bytes", "evx_step_scratch_words", "evx_last_error", "evx_perm_ws_bytes",
+           "evx_env_order", "evx_act_perm", "evx_env_orders", "evx_env_classes"]

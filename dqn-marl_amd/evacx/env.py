@@ -325,8 +325,8 @@ class VecEnv:
         self._obs = [torch.zeros(E * R * OBS_WORDS, **i32) for _ in range(obs_buffers)]
         self._ob = 0
         self.err = torch.zeros(1, **i32)
-        # the scheduling permutations' workspace (evx_env_order / evx_act_perm): caller-owned, one per
-        # VecEnv (split parts get their own: they order on their own streams)
+        # every env's class byte for the scheduling permutations (evx_env_orders): written by the step
+        # and reset kernels; split parts view their envs' slice of it
         self.perm_ws = _perm_ws(E, d)
         self.c = _lib.evx_state(E=E, pk=_ptr(self.pk), health=_ptr(self.health), acc=_ptr(self.acc),
                                 rmap=_ptr(self.rmap), thmap=_ptr(self.thmap), robots=_ptr(self.robots),
@@ -371,7 +371,7 @@ class VecEnv:
             p._ob = self._ob
             p.err = self.err
             p.obs_term = cut(self.obs_term, R * OBS_WORDS)
-            p.perm_ws = _perm_ws(n, lay.device)
+            p.perm_ws = self.perm_ws[lo:lo + n]
             p.c = _lib.evx_state(E=n, pk=_ptr(p.pk), health=_ptr(p.health), acc=_ptr(p.acc), rmap=_ptr(p.rmap),
                                  thmap=_ptr(p.thmap), robots=_ptr(p.robots), view=_ptr(p.view), scal=_ptr(p.scal),
                                  py_mt=_ptr(p.py_mt), np_mt=_ptr(p.np_mt), scratch=_ptr(p.scratch),
@@ -437,6 +437,20 @@ class VecEnv:
         _lib.check(_lib.lib().evx_act_perm(C.byref(self.lay.c), C.byref(self.c), out.data_ptr(), _stream()),
                    "evx_act_perm")
         return out
+
+    def compute_orders(self, perm: Optional[torch.Tensor] = None):
+        """The next step's dispatch order and (perm, int32 [>= E]) the next act's env order in one
+        launch (evx_env_orders) from the class bytes the last step / reset wrote. Scheduling only."""
+        if self._parts:
+            raise ValueError("compute_orders: order each part")
+        if perm is not None and (perm.numel() < self.E or perm.dtype != torch.int32):
+            raise ValueError("compute_orders: perm must be int32 with >= E entries")
+        _lib.check(_lib.lib().evx_env_orders(C.byref(self.lay.c), C.byref(self.c), _ptr(perm), _stream()),
+                   "evx_env_orders")
+
+    def refresh_classes(self):
+        """Rewrite the class bytes from the state words (after writing scal from the host)."""
+        _lib.check(_lib.lib().evx_env_classes(C.byref(self.lay.c), C.byref(self.c), _stream()), "evx_env_classes")
 
     def compute_order(self, force: bool = False, ahead: bool = False):
         """Dispatch order of the next step: heavy env-steps first, the heaviest with a

@@ -9,7 +9,8 @@ One ``step()`` = for all E envs x R robots of this rank:
               gradient all-reduce (RCCL over xGMI when world > 1), clip + Adam
   reset    -- auto-reset of finished envs (reference reset semantics) fused into
               the env.step launch; the heavy-first dispatch order of the next
-              env.step (evx_env_order) runs on a side stream
+              env.step and the next act's env order (evx_env_orders) follow it in
+              one launch on the same stream
 With groups > 1 the envs are split into parts that run act -> env.step -> push on
 their own streams, so one part's env.step tail overlaps the others' work.
 
@@ -105,14 +106,15 @@ class _Group:
         # act, env.step, push on a high-priority stream: the learn stream's workgroups
         # then fill the env launch's tail instead of competing for its first slots
         self.main = torch.cuda.Stream(device=device, priority=-1)
-        # dispatch order (and extra resets)
+        # one group: the next step's orders (evx_env_orders) beside the learn; extra resets
         self.side = torch.cuda.Stream(device=device, priority=0)
         cur = torch.cuda.current_stream(device)
         self.ev_push = torch.cuda.Event()
         self.ev_push.record(cur)
+        self.ev_act = torch.cuda.Event()
         self.ev_order = torch.cuda.Event()
         self.ev_order.record(cur)
-        self.ev_act = torch.cuda.Event()
+        self.perm = None  # the act's env order over this group's envs (x3 table path), or None
 
 
 class VecTrainer:
@@ -125,8 +127,9 @@ class VecTrainer:
                  prio_eps: float = 1e-6, groups: int = 1, layout_of=None, world_envs: Optional[int] = None,
                  nets: str = "shared"):
         """groups: the envs are split into this many parts, each stepping on its own
-        stream chain (see _Group); the env results do not depend on it (every env is
-        still stepped once per step with its own streams), the act's dropout masks do.
+        stream chain (see _Group), group g's act after group g - 1's (it overlaps that
+        group's env.step); neither the env results nor the act's dropout masks (one stream
+        per step, rows keyed by global agent id) depend on it.
         layout: a DeviceLayout, or an evacx.env.LayoutSet with layout_of = each env's
         layout (per-env layouts; observations in the replay carry their layout).
         world_envs: envs over all ranks (default E). This rank's envs are global ids
@@ -147,7 +150,6 @@ class VecTrainer:
         self.env.seed([seed_base + env_offset + i for i in range(E)])
         self.env.reset()
         parts = self.env.split(groups) if groups > 1 else [self.env]
-        self.env.compute_order()
         self.per_robot = nets in ("per_robot", "qmix")
         if nets not in ("shared", "per_robot", "qmix"):
             raise ValueError(f"nets must be 'shared', 'per_robot' or 'qmix', not {nets!r}")
@@ -237,7 +239,7 @@ class VecTrainer:
         if self.fast is None:
             self.lagged = False  # the lagged schedule's two-phase learn needs the fused MLP path
         self._perm = None
-        if self.fast is not None and self.fast.x3 and layout_of is None and len(self.groups) == 1:
+        if self.fast is not None and self.fast.x3 and layout_of is None:
             # act fast path: envs past the fire's last step start fc1 from a per-centre table of the
             # static features' contribution (rebuilt with every weight update) and add only the
             # occupancy columns; the act visits those envs first (VecEnv.act_perm) so its row tiles
@@ -250,12 +252,12 @@ class VecTrainer:
             # forward (the fused act kernel at B >= 32768) starts fc1 from it for replay rows
             # past the fire's last step
             self.learner.fast_t.attach_static(lc, lc.L, lc.W, lc.t_max, x_range=xr)
+            # the act's env order, per group (each group's act visits its own envs)
             self._perm = torch.zeros(E, dtype=torch.int32, device=self.device)
-            self._act_order(self.groups[0])
-
-    def _act_order(self, grp: _Group):
-        """The next act's env order on the current stream: its envs by table path (VecEnv.act_perm)."""
-        grp.env.act_perm(self._perm)
+            for grp in self.groups:
+                grp.perm = self._perm[grp.g * grp.env.E:(grp.g + 1) * grp.env.E]
+        for grp in self.groups:  # the first step's orders (the reset wrote every class byte)
+            grp.env.compute_orders(perm=grp.perm)
 
     def _act(self, grp: _Group):
         """DQNAgent.act in train mode for one group's robots: dropout active, epsilon-greedy
@@ -266,12 +268,11 @@ class VecTrainer:
             self.glearner.act(self.lay.c, grp.env.obs, grp.env.E, actions=grp.actions, epsilon=float(self.epsilon),
                               act_seed=self.act_seed, act_offset=off)
             return
-        if self.fast is not None:
-            self.learner.drop_stream += 1
+        if self.fast is not None:  # one mask stream per step (act_streams), rows keyed by global agent id
             self.fast.act(self.lay.c, grp.env.obs, grp.n,
                           drop=(self.learner.seed, self.learner.drop_stream, DROPOUT_P, None, g0),
                           actions=grp.actions, epsilon=float(self.epsilon), act_seed=self.act_seed, act_offset=off,
-                          perm=self._perm, rows_per_env=0 if self._perm is None else self.R)
+                          perm=grp.perm, rows_per_env=0 if grp.perm is None else self.R)
             return
         x = grp.env.expand_obs(torch.float32)  # [E/G, R, 11, 11, 6]
         # per-group scratch: the groups' acts run concurrently on their own streams
@@ -279,7 +280,14 @@ class VecTrainer:
         qcheck(qlib().evx_act(Q.data_ptr(), grp.n, self.learner.actions, float(self.epsilon), self.act_seed, off,
                               grp.actions.data_ptr(), _stream()), "act")
 
+    def _act_stream(self):
+        """A fresh dropout mask stream for this step's act: every group's act draws from it (rows keyed
+        by global agent id), so the masks do not depend on the group count."""
+        if self.fast is not None and not self.per_robot:
+            self.learner.drop_stream += 1
+
     def act(self):
+        self._act_stream()
         for grp in self.groups:
             self._act(grp)
         return self.actions
@@ -357,9 +365,12 @@ class VecTrainer:
         """One training step. Finished envs are reset inside the env.step launch
         (auto-reset: the reset of an env that ends runs in its own wave, in the shadow
         of the launch's heavy envs); the replay push takes their terminal observations.
-        The heavy-first dispatch order of each group's next env.step is computed on a
-        side stream, concurrently with push / learn / act. extra_reset: bool [E] of
-        further envs to reset (benchmark staggering, side stream); ev_env / ev_learn:
+        The heavy-first dispatch order of each group's next env.step and the next act's
+        env order come from one launch over the class bytes the step wrote
+        (evx_env_orders): one group on its side stream beside the push and the learn (the
+        act waits for it, long complete by then), several groups on their own streams.
+        extra_reset: bool [E] of further envs to reset (benchmark staggering, side
+        stream); ev_env / ev_learn:
         optional (start, end) CUDA events (env: group 0's env.step).
 
         Default order is the reference's (act, env.step, remember, learn). With
@@ -374,11 +385,8 @@ class VecTrainer:
                 grp.main.wait_stream(caller)
             self.join_caller = False
         G = self.groups
-        # the lagged schedule's dispatch order runs on the env's own stream right before env.step:
-        # its ~13 us kernel on the critical path beats the side stream's event pair (9.48 vs 9.03 M
-        # env-steps/s); the strict schedule keeps the side stream (its act + learn hide the order)
-        inline = self.lagged and len(G) == 1
         reset_wait, self.reset_pending = self.reset_pending, False
+        self._act_stream()
         # act: every group on its own stream, after the previous update (lagged) or learn
         for grp in G:
             with torch.cuda.stream(grp.main):
@@ -386,10 +394,12 @@ class VecTrainer:
                     grp.main.wait_event(self.ev_reset)
                 if self.lagged or grp.g > 0:
                     grp.main.wait_event(self.ev_learned)
-                if self._perm is not None and not inline:  # the act order, made after the last push
+                if grp.g > 0:  # the acts run one after the other: act g overlaps env.step g - 1
+                    grp.main.wait_event(G[grp.g - 1].ev_act)
+                if len(G) == 1:  # the orders from the side stream (the act's env order, the step's)
                     grp.main.wait_event(grp.ev_order)
                 self._act(grp)
-                if self.lagged:
+                if self.lagged or grp.g + 1 < len(G):  # read by the update / the next group's act
                     grp.ev_act.record(grp.main)
         if self.lagged:
             # learn t: gradients from the ring as it stood after push t-1 (minus the slots
@@ -412,16 +422,9 @@ class VecTrainer:
                 if ev_learn is not None:
                     ev_learn[1].record(self.lstream)
                 self.ev_learned.record(self.lstream)
+        # a cross-stream reader of the push: the lagged learn stream, group 0's learn, a reset
         for grp in G:
             with torch.cuda.stream(grp.main):
-                # the order was computed on the side stream from the state after the previous
-                # step, concurrently with act: by now the event is complete and the wait costs
-                # no gap (an order one step older would miss the envs that just auto-reset:
-                # they would be dispatched as light envs and become the launch's tail)
-                if inline:  # on this stream, right before the step: no cross-stream event
-                    grp.env.compute_order()
-                elif len(G) == 1:
-                    grp.main.wait_event(grp.ev_order)
                 if ev_env is not None and grp.g == 0:
                     ev_env[0].record(grp.main)
                 grp.env.step(grp.actions, order=False, auto_reset=True)
@@ -429,8 +432,8 @@ class VecTrainer:
                     ev_env[1].record(grp.main)
                 self.replay.push(grp.env.obs_prev, grp.env.obs, grp.actions, grp.env.reward, grp.env.done, grp.n,
                                  self.R, s2_term=grp.env.obs_term)
-                if self._perm is not None and inline:  # the next act's env order, on this stream
-                    self._act_order(grp)
+                if len(G) > 1:  # several groups: the orders on this stream, after the push
+                    grp.env.compute_orders(perm=grp.perm)
                 grp.ev_push.record(grp.main)
         if extra_reset is not None:  # after every group's push, on group 0's side stream (warm-up only)
             side = G[0].side
@@ -440,23 +443,20 @@ class VecTrainer:
                 for grp in G:
                     side.wait_event(grp.ev_push)
                 self.env.reset(mask=extra_reset & ~self.env.done.bool())
+                if len(G) > 1:
+                    for grp in G:  # the orders again, with the reset envs' new classes
+                        grp.env.compute_orders(perm=grp.perm)
                 self.ev_reset.record(side)
             self.reset_pending = True
-        for grp in ([] if inline else G):
-            # one group: the order on a side stream (overlaps act); several: on the group's own
-            # stream after its push (the groups overlap each other, and more streams than
-            # the GPU_MAX_HW_QUEUES hardware queues would serialise unrelated work)
-            st = grp.side if len(G) == 1 else grp.main
-            with torch.cuda.stream(st):
-                if st is grp.side:
-                    st.wait_event(grp.ev_push)
-                if extra_reset is not None:
-                    st.wait_event(self.ev_reset)
-                if self._perm is not None:  # the next act's env order (the act waits for ev_order)
-                    self._act_order(grp)
-                grp.env.compute_order()
-                if st is grp.side:
-                    grp.ev_order.record(st)
+        if len(G) == 1:
+            # the next step's dispatch order and the next act's env order from the class bytes the
+            # step (and a reset) just wrote, auto-reset envs included: one launch on the side stream,
+            # beside the push and the learn's first kernels
+            grp = G[0]
+            with torch.cuda.stream(grp.side):
+                grp.side.wait_event(grp.ev_push)  # (after an extra reset: the same stream)
+                grp.env.compute_orders(perm=grp.perm)
+                grp.ev_order.record(grp.side)
         if not self.lagged:  # the reference's order: learn after every group's push, on group 0's stream
             m = G[0].main
             with torch.cuda.stream(m):

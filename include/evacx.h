@@ -88,9 +88,12 @@ typedef struct {
     int32_t *order;    /* [E+1] dispatch order of the step's envs (evx_env_order), or NULL = 0..E-1;
                         * order[E] = H: the first H of them are heavy (rows phase on a 4-wave workgroup) */
     const int32_t *layout_idx; /* [E] each env's layout in evx_layout.layout_set, or NULL (one layout) */
-    uint8_t *perm_ws;  /* [evx_perm_ws_bytes(E)] workspace of evx_env_order / evx_act_perm (their
-                        * count and rank launches); calls on one state must be stream-ordered.
-                        * NULL: evx_env_order runs its one-workgroup kernel, evx_act_perm fails */
+    uint8_t *perm_ws;  /* [evx_perm_ws_bytes(E)] one class byte per env for the scheduling
+                        * permutations (persons-remaining bucket, fire step >= t_max, heavy),
+                        * written by the step and reset kernels as they finish an env (or by
+                        * evx_env_classes from the state words) and read by evx_env_order /
+                        * evx_act_perm / evx_env_orders, one launch each. NULL: evx_env_order
+                        * reads the state words itself, evx_act_perm / evx_env_orders fail */
 } evx_state;
 
 /* Compact per-robot observation (32 B). Expands to the reference's 11x11x6
@@ -154,6 +157,11 @@ int evx_env_order(const evx_layout *lay, const evx_state *st, void *stream);
 /* act row permutation for the x3 act fast path: perm[0..E) lists the envs whose fire step is >= the
  * layout's t_max (the static-table fire step) first, then the rest, each in env order (stable) */
 int evx_act_perm(const evx_layout *l, const evx_state *s, int32_t *perm, void *stream);
+/* Both of the above in one launch: st->order for the next step and perm for the
+ * next act, from the class bytes the step just wrote. */
+int evx_env_orders(const evx_layout *l, const evx_state *s, int32_t *perm, void *stream);
+/* Rewrites every env's class byte in st->perm_ws from st->scal (a state written from the host). */
+int evx_env_classes(const evx_layout *l, const evx_state *s, void *stream);
 /* Bytes of evx_state.perm_ws for E envs. */
 int64_t evx_perm_ws_bytes(int32_t E);
 

@@ -1,16 +1,18 @@
-"""The two scheduling permutations the training step computes on its side stream, against
+"""The two scheduling permutations the training step computes after every env.step, against
 numpy restatements on the same state words (evx_state.scal: fire step at [4e], persons
 evacuated / dead at [4e + 2] / [4e + 3]):
 
-  * evx_act_perm (act_perm_kernel): the stable partition of the envs by fire step >= t_max
-    (the x3 act's table rows first), chunked ballot ranks, one pass per 32768 envs;
-  * evx_env_order (env_order32_kernel up to 32768 envs, env_order_kernel beyond): the stable
-    counting sort by 16 buckets of persons remaining, heaviest first, and order[E] = the heavy
-    count min(176, #envs with >= P/4 persons remaining).
+  * evx_act_perm: the stable partition of the envs by fire step >= t_max (the x3 act's table
+    rows first);
+  * evx_env_order: the stable counting sort by 16 buckets of persons remaining, heaviest first,
+    and order[E] = the heavy count min(176, #envs with >= P/4 persons remaining);
+  * evx_env_orders: both in one launch.
+All three read one class byte per env (evx_state.perm_ws), which the step and reset kernels write
+as they finish an env (checked against the state words after real steps with auto-resets) and
+evx_env_classes rewrites from the state words (here, after scal is written from the host).
 
-Sizes: ragged (1000), the cfg3 share (32768, one full pass) and 40000 (two act_perm passes, the
-slice-per-wave order kernel). Scheduling only -- the env results never depend on these -- but a
-wrong permutation would drop or repeat envs."""
+Sizes: ragged (1000), the cfg3 share (32768) and 40000. Scheduling only -- the env results never
+depend on these -- but a wrong permutation would drop or repeat envs."""
 import numpy as np
 import pytest
 import torch
@@ -44,10 +46,16 @@ def test_act_perm_and_env_order_match_numpy(E):
     scal[:, 2] = ev
     scal[:, 3] = dead
     env.scal.view(E, 4).copy_(torch.from_numpy(scal))
+    env.refresh_classes()
     perm = torch.full((E + 5,), -7, dtype=torch.int32, device="cuda")
     env.act_perm(perm)
     env.compute_order(force=True)
+    perm2 = torch.full((E + 5,), -7, dtype=torch.int32, device="cuda")
+    order1 = env.order.clone()
+    env.order.fill_(-3)
+    env.compute_orders(perm2)  # both in one launch
     torch.cuda.synchronize()
+    assert torch.equal(perm, perm2) and torch.equal(order1, env.order)
     sel = scal[:, 0] >= t_max
     want = np.concatenate([np.nonzero(sel)[0], np.nonzero(~sel)[0]]).astype(np.int32)
     got = perm.cpu().numpy()
@@ -59,3 +67,37 @@ def test_act_perm_and_env_order_match_numpy(E):
     order = env.order.cpu().numpy()
     assert np.array_equal(order[:E], want_order)
     assert order[E] == min(176, int(np.sum(rem >= max(1, P // 4))))
+
+
+def _want_classes(scal, P, t_max):
+    rem = P - scal[:, 2] - scal[:, 3]
+    b = 15 - np.minimum(15, np.maximum(0, rem) * 16 // (P + 1))
+    return (b | np.where(scal[:, 0] >= t_max, 0x10, 0) | np.where(rem >= max(1, P // 4), 0x20, 0)).astype(np.uint8)
+
+
+def test_step_and_reset_write_class_bytes():
+    """The class bytes the step kernel (fused resets included) and the reset kernel leave equal the
+    ones the state words give, so the orders after a step need no pass over the state."""
+    _need_gpu()
+    from evacx.env import DeviceLayout, VecEnv
+    from evacx.layout import build_tables, synthetic
+    lay = DeviceLayout(build_tables(synthetic(24, 20, 4)), 380)
+    E = 700
+    env = VecEnv(lay, E)
+    env.seed([31 + i for i in range(E)])
+    env.reset()
+    P, t_max = int(lay.c.P), int(lay.c.t_max)
+    g = torch.Generator(device="cuda").manual_seed(2)
+    n_done = 0
+    for t in range(260):
+        env.step(torch.randint(0, 5, (E * lay.R,), device="cuda", dtype=torch.int32, generator=g), auto_reset=True)
+        n_done += int(env.done.sum().item())
+        if t == 100:
+            m = torch.zeros(E, dtype=torch.bool, device="cuda")
+            m[::5] = True
+            env.reset(mask=m)
+        if t % 37 == 0 or t == 101:
+            torch.cuda.synchronize()
+            scal = env.scal.view(E, 4).cpu().numpy()
+            assert np.array_equal(env.perm_ws[:E].cpu().numpy(), _want_classes(scal, P, t_max)), t
+    assert n_done > 0

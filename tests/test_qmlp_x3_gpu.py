@@ -295,6 +295,7 @@ def test_x3_act_static_table_and_env_order(xr):
                                             env.scal.view(E, 4)[:, 0])
     ob = env.obs.view(E, R, 8)
     ob[:, :, 6] = torch.where(sat[:, None], torch.full_like(ob[:, :, 6], t_max), ob[:, :, 6])
+    env.refresh_classes()  # the class bytes act_perm reads follow the state words written here
     perm = torch.full((E,), -1, dtype=torch.int32, device="cuda")
     env.act_perm(perm)
     torch.cuda.synchronize()

@@ -182,3 +182,34 @@ def test_same_seed_trainers_are_bit_identical():
     a, b = snaps
     for k in a:
         assert torch.equal(a[k], b[k]), k
+
+
+def test_groups_match_one_group():
+    """VecTrainer(groups=2) -- two stream chains, group 1's act overlapping group 0's env.step --
+    against groups=1 from the same seeds (epsilon 1: the actions do not depend on the Q values):
+    env states, the replay ring (transitions land in global agent order), the act's dropout stream
+    and, through identical learn batches, the online weights are bit-identical after 8 steps."""
+    _need_gpu()
+    from evacx.env import DeviceLayout
+    from evacx.layout import build_tables, synthetic
+    from evacx.trainer import VecTrainer
+    lay = DeviceLayout(build_tables(synthetic(128, 128, 16)), 2276)
+    snaps = []
+    for G in (1, 2):
+        tr = VecTrainer(lay, 2048, batch=2048, replay_capacity=1 << 18, epsilon=1.0, epsilon_decay=1.0,
+                        target_every=3, groups=G)
+        for _ in range(8):
+            tr.step()
+        tr.sync()
+        torch.cuda.synchronize()
+        tr.env.check_err()
+        env = tr.env
+        snaps.append(dict(online=tr.learner.online.flat.clone(), pk=env.pk.clone(), health=env.health.clone(),
+                          scal=env.scal.clone(), py_mt=env.py_mt.clone(), np_mt=env.np_mt.clone(),
+                          ring=tr.replay.s.clone(), ring_a=tr.replay.a.clone(), ring_r=tr.replay.r.clone(),
+                          drop=tr.learner.drop_stream))
+        del tr, env
+        torch.cuda.empty_cache()
+    a, b = snaps
+    for k in a:
+        assert (a[k] == b[k]) if k == "drop" else torch.equal(a[k], b[k]), k
