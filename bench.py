@@ -32,6 +32,7 @@ other schedule's rate, the env-only rate, the roofline of the dominant kernel
 (env_step_kernel, HBM-bound) and the CPU baseline. Prints ONE JSON line on rank 0.
 """
 import argparse
+import glob
 import json
 import os
 import platform
@@ -385,8 +386,17 @@ def main():
     per_launch = E // args.groups if args.mode == "train" else E  # env.step launches of group 0 are timed
     achieved = bpe * per_launch / (kern_ms * 1e-3) / 1e9
     traffic, traffic_src, traffic_corr = None, None, None
-    tpath = args.traffic or next((q for q in (os.path.join(ROOT, "profiles", r, f"env_traffic_{args.phase}.json")
-                                              for r in ("r4", "r3", "r2")) if os.path.exists(q)), "")
+    def traffic_match(q):  # a PMC record of this kernel, phase, launch size and grid
+        try:
+            rec = json.load(open(q))
+        except (OSError, ValueError):
+            return False
+        return (rec.get("kernel") == "env_step_kernel" and rec.get("envs") in (None, per_launch)
+                and rec.get("grid", [L, W]) == [L, W])
+    tpath = args.traffic or next((q for r in ("r5", "r4", "r3", "r2")
+                                  for q in sorted(glob.glob(os.path.join(ROOT, "profiles", r,
+                                                                         f"env_traffic_{args.phase}*.json")))
+                                  if traffic_match(q)), "")
     if os.path.exists(tpath):
         # HBM bytes per launch from rocprofv3 PMC passes of this same workload and phase
         # (separate --pmc FETCH_SIZE / WRITE_SIZE runs; cannot be collected inside the timed run)
