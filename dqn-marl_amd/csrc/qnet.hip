@@ -13,11 +13,13 @@
 // with f32 accumulation (v_mfma_f32_32x32x16_bf16, the throughput path).
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <type_traits>
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
 
 #include "evacx.h"
+#include "evx_host.h"
 
 namespace evxq {
 
@@ -1275,6 +1277,197 @@ __global__ __launch_bounds__(256, 2) void conv3x3_x3_kernel(evx_gemm_desc g, int
             }
         }
 }
+// The forward of conv2 over many images (the act's 8192, the learner's 1024): 512-thread
+// workgroups (one per CU) walk the images with their share of the layer's packed weights held in
+// VGPRs for the whole launch -- conv3x3_x3_kernel re-read every weight fragment from L2 per image
+// (295 KB per conv3 image: 2.4 GB per 8192-image act). A workgroup owns NTW of the layer's NT
+// 32-channel column tiles (column group cg; the CG = NT / NTW groups of an image run on one XCD,
+// so its input is fetched into that L2 once); wave w takes column tile w % NTW, and the 8 / NTW
+// waves of a column tile split the 4 row tiles and (KH > 1) the K steps, the K parts added through
+// LDS in a fixed order; conv2 (NT 2, NTW 2, KH 1): one row tile and all 18 k-steps per wave (act
+// 223 -> 139 us at 8192 images). (conv3 as NT 4, NTW 2, KH 4 -- a quarter of the 36 k-steps per
+// wave -- measured slower than the per-image kernel: see conv_direct.) Row tiles RP at a time. The next image's input is loaded into registers while the current one is
+// computed, then staged as bf16 hi / lo planes over the 13x13 zero-bordered grid (the layout,
+// fragments, x3 products and epilogue of conv3x3_x3_kernel).
+template <int CP, int NT, int NTW, int KH, int RP>
+__global__ __launch_bounds__(512, 1) void conv3x3_wreg_kernel(evx_gemm_desc g, int cin, const __bf16* __restrict__ wp,
+                                                              int nimg, int nslot) {
+    static_assert(CP == 32 || CP == 64, "conv2 / conv3 inputs");
+    constexpr int XP = CP + 8, KJ = CP / 16, KS = 9 * KJ, KW = KS / KH, WPT = 8 / NTW, RW = 4 * KH / WPT;
+    constexpr int CG = NT / NTW;
+    static_assert(KS % KH == 0 && WPT % KH == 0 && RW * (WPT / KH) == 4 && RW % RP == 0 && NT % NTW == 0, "split");
+    constexpr int C4 = CP / 4, NI = 169 * C4, NPF = (NI + 511) / 512;  // float4 staging pieces per thread
+    __shared__ __attribute__((aligned(16))) __bf16 Xs[2][169][XP];
+    __shared__ __attribute__((aligned(16))) float Red[KH > 1 ? (KH - 1) * NTW * RP * 32 * 32 : 1];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+    // workgroup -> (column group, image slot): the CG groups of a slot 8 workgroups apart (one XCD)
+    const int b = (int)blockIdx.x;
+    int cg, slot;
+    if (CG > 1 && (gridDim.x & (8 * CG - 1)) == 0) {
+        cg = (b >> 3) % CG;
+        slot = (b & 7) + ((b >> 3) / CG) * 8;
+    } else {
+        cg = b % CG;
+        slot = b / CG;
+    }
+    const int ctl = w % NTW, ct = cg * NTW + ctl, g2 = w / NTW, kh = g2 % KH, rt0 = (g2 / KH) * RW;
+    const int n = ct * 32 + (lane & 31);
+    bf16x8 wh[KW], wl[KW];
+#pragma unroll
+    for (int j = 0; j < KW; j++) {
+        const size_t o = ((size_t)(ct * KS + kh * KW + j) * 64 + lane) * 8;
+        wh[j] = *reinterpret_cast<const bf16x8*>(wp + o);
+        wl[j] = *reinterpret_cast<const bf16x8*>(wp + o + (size_t)NT * KS * 512);
+    }
+    int base[RW];
+#pragma unroll
+    for (int k = 0; k < RW; k++) {
+        int m = (rt0 + k) * 32 + (lane & 31);
+        m = m < 121 ? m : 0;  // rows 121.. read pixel 0 (their outputs are not stored)
+        const int y = (m * 187) >> 11, x = m - 11 * y;
+        base[k] = (y + 1) * 13 + (x + 1);
+    }
+    auto opaque = [](int v) {  // hides the image index from loop strength reduction
+        asm volatile("" : "+s"(v));
+        return v;
+    };
+    auto opaque_v = [](int v) {  // per-thread staging offsets: recomputed per image, not held live
+        asm volatile("" : "+v"(v));
+        return v;
+    };
+    // 32-bit element offsets from a wave-uniform image base (64-bit pointers per piece and per output
+    // row, strength-reduced across the image loop, took 80 VGPRs and spilled the weights)
+    float4 pf[NPF];
+    auto load = [&](int img) {
+        const float* __restrict__ X = g.A + (size_t)opaque(img) * 121 * cin;
+        const int tv = opaque_v(tid);
+#pragma unroll
+        for (int t = 0; t < NPF; t++) {
+            const int i = tv + 512 * t, q = i / C4, c = (i - q * C4) * 4;
+            const int y = q / 13 - 1, x = q - (q / 13) * 13 - 1;
+            pf[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (i < NI && (unsigned)y < 11u && (unsigned)x < 11u)
+                pf[t] = *reinterpret_cast<const float4*>(X + (uint32_t)((y * 11 + x) * cin + c));
+        }
+    };
+    auto store = [&]() {
+        const int tv = opaque_v(tid);
+#pragma unroll
+        for (int t = 0; t < NPF; t++) {
+            const int i = tv + 512 * t, q = i / C4, c = (i - q * C4) * 4;
+            if (i < NI) {
+                const float f[4] = {pf[t].x, pf[t].y, pf[t].z, pf[t].w};
+                bf16x4 hi, lo;
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    const __bf16 v = (__bf16)f[e];
+                    hi[e] = v;
+                    lo[e] = (__bf16)(f[e] - (float)v);
+                }
+                *reinterpret_cast<bf16x4*>(&Xs[0][q][c]) = hi;
+                *reinterpret_cast<bf16x4*>(&Xs[1][q][c]) = lo;
+            }
+        }
+    };
+    const float bias = g.bias ? g.bias[n] : 0.f;
+    const bool relu = (g.flags & EVX_GEMM_RELU) != 0;
+    const bool osp = (g.flags & EVX_GEMM_OUT_SPLIT) != 0;
+    const size_t ylo = (size_t)g.M * g.ldc;
+    const uint32_t ldc = (uint32_t)g.ldc;
+    int img = slot;
+    if (img < nimg) load(img);
+    for (; img < nimg; img += nslot) {
+        __syncthreads();  // the previous image's fragments and partials have been read
+        store();
+        __syncthreads();
+        if (img + nslot < nimg) load(img + nslot);  // in flight during the MFMAs
+        const size_t ib = (size_t)opaque(img) * 121 * g.ldc;
+        float* __restrict__ Y = g.C + ib;
+        __bf16* __restrict__ Yh = reinterpret_cast<__bf16*>(g.C) + ib;
+        __bf16* __restrict__ Yl = Yh + ylo;
+#pragma unroll
+        for (int p0 = 0; p0 < RW; p0 += RP) {
+            f32x16 acc[RP];
+#pragma unroll
+            for (int k = 0; k < RP; k++)
+#pragma unroll
+                for (int r = 0; r < 16; r++) acc[k][r] = 0.f;
+            // the K part as a compile-time constant: each k-step's tap and channel offset fold into
+            // the LDS reads' immediate offsets (a runtime part kept its addresses live and spilled)
+            auto ksteps = [&](auto khc) {
+                constexpr int KHC = decltype(khc)::value;
+#pragma unroll
+                for (int j = 0; j < KW; j++) {
+                    asm volatile("" ::: "memory");  // one k-step's fragment reads at a time
+                    const int ks = KHC * KW + j, tap = ks / KJ, cj = (ks - tap * KJ) * 16;
+                    const int toff = (tap / 3 - 1) * 13 + (tap % 3 - 1);
+#pragma unroll
+                    for (int k = 0; k < RP; k++) {
+                        const __bf16* x0 = &Xs[0][base[p0 + k]][8 * h] + toff * XP + cj;
+                        const __bf16* x1 = &Xs[1][base[p0 + k]][8 * h] + toff * XP + cj;
+                        const bf16x8 ah = *reinterpret_cast<const bf16x8*>(x0);
+                        const bf16x8 al = *reinterpret_cast<const bf16x8*>(x1);
+                        acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, wh[j], acc[k], 0, 0, 0);
+                        acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, wl[j], acc[k], 0, 0, 0);
+                        acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, wh[j], acc[k], 0, 0, 0);
+                    }
+                }
+            };
+            if constexpr (KH == 1) {
+                ksteps(std::integral_constant<int, 0>());
+            } else {
+                switch (kh) {
+                    case 0: ksteps(std::integral_constant<int, 0>()); break;
+                    case 1: ksteps(std::integral_constant<int, 1 % KH>()); break;
+                    case 2: ksteps(std::integral_constant<int, 2 % KH>()); break;
+                    default: ksteps(std::integral_constant<int, 3 % KH>()); break;
+                }
+                // the other K parts' partials through LDS, added by part 0 in part order
+                float* red = Red + (size_t)(kh - 1) * NTW * RP * 1024 + ctl * RP * 1024;
+                if (kh > 0) {
+#pragma unroll
+                    for (int k = 0; k < RP; k++)
+#pragma unroll
+                        for (int r = 0; r < 16; r++)
+                            red[(k * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * 32 + (lane & 31)] = acc[k][r];
+                }
+                __syncthreads();
+                if (kh == 0) {
+#pragma unroll
+                    for (int q = 0; q < KH - 1; q++) {
+                        const float* rq = Red + (size_t)q * NTW * RP * 1024 + ctl * RP * 1024;
+#pragma unroll
+                        for (int k = 0; k < RP; k++)
+#pragma unroll
+                            for (int r = 0; r < 16; r++)
+                                acc[k][r] += rq[(k * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * 32 + (lane & 31)];
+                    }
+                }
+                __syncthreads();  // Red is rewritten by the next pass
+                if (kh != 0) continue;
+            }
+#pragma unroll
+            for (int k = 0; k < RP; k++) {
+                const int mb = opaque_v((rt0 + p0 + k) * 32 + 4 * h);  // output offsets not held live
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    const int m = mb + (r & 3) + 8 * (r >> 2);
+                    if (m >= 121) continue;
+                    const uint32_t o = (uint32_t)m * ldc + (uint32_t)n;
+                    float v = acc[k][r] + bias;
+                    if (relu) v = v > 0.f ? v : 0.f;
+                    if (osp) {
+                        const __bf16 hi = (__bf16)v;
+                        Yh[o] = hi;
+                        Yl[o] = (__bf16)(v - (float)hi);
+                    } else {
+                        Y[o] = v;
+                    }
+                }
+            }
+        }
+    }
+}
 }  // namespace evxq
 namespace {
 
@@ -1306,13 +1499,28 @@ static void conv_direct_launch(const evx_gemm_desc* g, int cs, __bf16* wp, hipSt
     hipLaunchKernelGGL((evxq::conv3x3_x3_kernel<CP, NT, DX>), dim3((unsigned)(g->M / 121)), dim3(256), 0, st, *g, cs,
                        (const __bf16*)wp);
 }
+// conv2 forward with the weights in registers (conv3x3_wreg_kernel): one workgroup per CU
+template <int CP, int NT, int NTW, int KH, int RP>
+static void conv_wreg_launch(const evx_gemm_desc* g, int cs, __bf16* wp, hipStream_t st) {
+    const unsigned pb = (unsigned)((NT * (9 * CP / 16) * 64 + 255) / 256);
+    hipLaunchKernelGGL(evxq::conv_wpack_kernel<CP>, dim3(pb), dim3(256), 0, st, g->B, g->sbk, g->sbn, cs, NT, wp);
+    constexpr int CG = NT / NTW;
+    const int nimg = (int)(g->M / 121);
+    int nslot = std::min(nimg, evxh::cu_count() / CG);
+    if (nslot >= 8) nslot &= ~7;  // whole XCD rounds (the column groups of a slot share one)
+    hipLaunchKernelGGL((evxq::conv3x3_wreg_kernel<CP, NT, NTW, KH, RP>), dim3((unsigned)(nslot * CG)), dim3(512), 0, st,
+                       *g, cs, (const __bf16*)wp, nimg, nslot);
+}
 static bool conv_direct(const evx_gemm_desc* g, int mode, int cs, hipStream_t st) {
     const int cp = conv_direct_cp(g, mode, cs);
     if (!cp || !g->ws || g->ws_elems < conv_direct_ws(g, mode, cs)) return false;
     __bf16* wp = reinterpret_cast<__bf16*>(g->ws);
     if (mode == EVX_CONV_FWD) {
         if (cp == 16) conv_direct_launch<16, 1, false>(g, cs, wp, st);
-        else if (cp == 32) conv_direct_launch<32, 2, false>(g, cs, wp, st);
+        else if (cp == 32) conv_wreg_launch<32, 2, 2, 1, 1>(g, cs, wp, st);
+        // conv3 keeps the per-image kernel: with its 36 k-steps of weights split over four waves
+        // (conv3x3_wreg_kernel<64, 4, 2, 4, 2>, 254 VGPRs) the K-part reductions and their barriers
+        // per image cost more than the weight re-reads saved (act 654 -> ~1000 us, learn 88 -> 130 us)
         else conv_direct_launch<64, 4, false>(g, cs, wp, st);
     } else {
         if (cp == 64) conv_direct_launch<64, 1, true>(g, cs, wp, st);
