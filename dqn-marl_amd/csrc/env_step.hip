@@ -60,11 +60,13 @@ constexpr int GRP_MAX = 128;         // movers of one contested target (8 neighb
 constexpr int GBITS = 13;            // group index bits in a sorted group head
 constexpr uint32_t DONEPK = 3u << 24;
 #ifndef EVX_GQ
-#define EVX_GQ 2
+#define EVX_GQ 1
 #endif
-// 64-person groups per pipelined iteration of the rows loop: 2 keeps the kernel at 168 VGPRs
-// (3 waves per SIMD) -- 4 needs 218 (2 waves); one-wave workgroups gain more from the
-// occupancy than they lose in prefetch depth (env_step 1.30 -> 1.21 ms at 32768 envs)
+// 64-person groups per pipelined iteration of the rows loop (and the reward's): 1 -- the next
+// group's data in flight while one is processed, no per-group selects -- keeps the kernel at 144
+// VGPRs with no spill. Round 5 A/B (tools/gpu_r5_envab2.sh, env-only): GQ 2 (166 VGPRs) 0.704 ->
+// 0.655 ms at 32768 envs, cfg4 6.03 -> 5.88 ms; GQ 3 / 4 at 2 waves per SIMD 0.86 ms, cfg4 6.21.
+// (Round 2: 4 -> 2, 218 -> 168 VGPRs, 1.30 -> 1.21 ms.)
 constexpr int GQ = EVX_GQ;
 
 struct Geo {
