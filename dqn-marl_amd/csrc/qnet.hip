@@ -258,7 +258,13 @@ __device__ __forceinline__ uint32_t div121(uint32_t m) { return __umulhi(m, 3549
 __device__ __forceinline__ int div11(int p) { return (p * 187) >> 11; }                     // p < 121
 // SPL (CV_NONE, EVX_GEMM_SPLIT_AB): A and B already hold bf16 hi / lo planes, k-contiguous; a
 // K tile is staged as 16-B pieces (2 per thread and plane) with no per-element split
-template <int CM, bool SPL = false>
+// VEC (CV_NONE f32 operands, host-checked strides / alignment): a k-contiguous operand staged from
+// 16-B global loads of 4 consecutive k (8-B hi / lo LDS stores) instead of 4-B loads of one --
+// bit 0: A (sak 1), bit 2: B (sbk 1). (m / n-contiguous operands vectorised along m / n measured
+// slower -- 4-way LDS bank conflicts on the 2-byte stores: fc1's dW 132 -> 263 us -- and keep the
+// one-element path.)
+enum { VA_K = 1, VB_K = 4 };
+template <int CM, bool SPL = false, int VEC = 0>
 __global__ __launch_bounds__(256) void gemm128x3_kernel(evx_gemm_desc g, int ksplit_len, int cs) {
     constexpr int PK = BK + 8;  // row pitch (bf16): 20 words, conflict-free 16-B reads
     __shared__ __attribute__((aligned(16))) __bf16 As[2][TB][PK];
@@ -295,7 +301,25 @@ __global__ __launch_bounds__(256) void gemm128x3_kernel(evx_gemm_desc g, int ksp
     }
     const int kp = 2 * (tid & 15), rp = tid >> 4;  // pair layout: k offset, first row
     bf16x8 sa[2][2], sb[2][2];                     // SPL: [plane][piece], piece i: row (tid + 256 i) >> 2
+    float4 va4[4], vb4[4];  // VEC pieces: k-vector (row (t >> 3) + 32 i, k 4 (t & 7)) or m / n-vector
+                            // (k (t >> 5) + 8 i, rows 4 (t & 31) .. + 3)
     auto fetch = [&](int k0) {
+        if constexpr ((VEC & VA_K) != 0) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int gm = m0 + (tid >> 3) + 32 * i, gk = k0 + 4 * (tid & 7);
+                va4[i] = gm < g.M && gk < ke ? *reinterpret_cast<const float4*>(g.A + (int64_t)gm * g.sam + gk)
+                                             : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+        if constexpr ((VEC & VB_K) != 0) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int gn = n0 + (tid >> 3) + 32 * i, gk = k0 + 4 * (tid & 7);
+                vb4[i] = gn < g.N && gk < ke ? *reinterpret_cast<const float4*>(g.B + (int64_t)gn * g.sbn + gk)
+                                             : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
         if constexpr (SPL) {
             const __bf16* ah = reinterpret_cast<const __bf16*>(g.A);
             const __bf16* bh = reinterpret_cast<const __bf16*>(g.B);
@@ -356,7 +380,9 @@ __global__ __launch_bounds__(256) void gemm128x3_kernel(evx_gemm_desc g, int ksp
                     rb[2 * i + q] = (gn < g.N && kin[q]) ? g.B[boff[q] + (int64_t)gn * g.sbn] : 0.f;
             }
         } else {
-            if (a_kc) {
+            if constexpr ((VEC & VA_K) != 0) {
+                // A staged from va4 (the 16-B loads above)
+            } else if (a_kc) {
 #pragma unroll
                 for (int i = 0; i < 8; i++) {
                     const int gm = m0 + rp + 16 * i;
@@ -375,7 +401,9 @@ __global__ __launch_bounds__(256) void gemm128x3_kernel(evx_gemm_desc g, int ksp
                     ra[i] = (gm < g.M && gk < ke) ? g.A[(int64_t)gm * g.sam + (int64_t)gk * g.sak] : 0.f;
                 }
             }
-            if constexpr (CM == CV_DW) {
+            if constexpr ((VEC & VB_K) != 0) {
+                // B staged from vb4
+            } else if constexpr (CM == CV_DW) {
                 const int gn = n0 + (tid & 127);
                 const int m1 = k0 + (tid >> 7);
                 int p = (int)((uint32_t)m1 - div121((uint32_t)m1) * 121u);
@@ -420,6 +448,20 @@ __global__ __launch_bounds__(256) void gemm128x3_kernel(evx_gemm_desc g, int ksp
             (uint32_t)__builtin_bit_cast(uint16_t, l0) | ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
     };
     auto stash = [&]() {
+        // 4 consecutive k of one row (the 16-B loads): 8-B hi and lo stores
+        auto put4 = [&](__bf16 (*S)[TB][PK], const float4 v, int i) {
+            const float f[4] = {v.x, v.y, v.z, v.w};
+            bf16x4 hi, lo;
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const __bf16 b = (__bf16)f[e];
+                hi[e] = b;
+                lo[e] = (__bf16)(f[e] - (float)b);
+            }
+            const int row = (tid >> 3) + 32 * i, kk = 4 * (tid & 7);
+            *reinterpret_cast<bf16x4*>(&S[0][row][kk]) = hi;
+            *reinterpret_cast<bf16x4*>(&S[1][row][kk]) = lo;
+        };
         if constexpr (SPL) {
 #pragma unroll
             for (int i = 0; i < 2; i++) {
@@ -432,7 +474,10 @@ __global__ __launch_bounds__(256) void gemm128x3_kernel(evx_gemm_desc g, int ksp
             }
             return;
         }
-        if (a_kc) {
+        if constexpr ((VEC & VA_K) != 0) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) put4(As, va4[i], i);
+        } else if (a_kc) {
 #pragma unroll
             for (int i = 0; i < 8; i++) put2(As, rp + 16 * i, kp, ra[2 * i], ra[2 * i + 1]);
         } else {
@@ -445,7 +490,10 @@ __global__ __launch_bounds__(256) void gemm128x3_kernel(evx_gemm_desc g, int ksp
                 As[1][mm][kk] = (__bf16)(ra[i] - (float)hi);
             }
         }
-        if (!b_nc) {
+        if constexpr ((VEC & VB_K) != 0) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) put4(Bs, vb4[i], i);
+        } else if (!b_nc) {
 #pragma unroll
             for (int i = 0; i < 8; i++) put2(Bs, rp + 16 * i, kp, rb[2 * i], rb[2 * i + 1]);
         } else {
@@ -1555,8 +1603,23 @@ int gemm_launch(const evx_gemm_desc* g, int cm, int cs, void* stream) {
         hipLaunchKernelGGL(evxq::gemm128x3_kernel<evxq::CV_DW>, grid, dim3(256), 0, st, *g, klen, cs);
     else if (g->precision == EVX_PREC_BF16)
         hipLaunchKernelGGL(evxq::gemm128_kernel<__bf16>, grid, dim3(256), 0, st, *g, klen);
-    else if (g->precision == EVX_PREC_X3)
-        hipLaunchKernelGGL(evxq::gemm128x3_kernel<evxq::CV_NONE>, grid, dim3(256), 0, st, *g, klen, 0);
+    else if (g->precision == EVX_PREC_X3) {
+        // k-contiguous f32 operands staged from 16-B loads (the fc layers' forward: A and B; dX: A)
+        auto al16 = [](const float* p) { return ((uintptr_t)p & 15) == 0; };
+        const bool ak = g->sak == 1 && (g->sam & 3) == 0 && (g->K & 3) == 0 && al16(g->A);
+        const bool bk = g->sbk == 1 && (g->sbn & 3) == 0 && (g->K & 3) == 0 && al16(g->B);
+        if (ak && bk)
+            hipLaunchKernelGGL((evxq::gemm128x3_kernel<evxq::CV_NONE, false, evxq::VA_K | evxq::VB_K>), grid, dim3(256), 0,
+                               st, *g, klen, 0);
+        else if (ak)
+            hipLaunchKernelGGL((evxq::gemm128x3_kernel<evxq::CV_NONE, false, evxq::VA_K>), grid, dim3(256), 0, st, *g,
+                               klen, 0);
+        else if (bk)
+            hipLaunchKernelGGL((evxq::gemm128x3_kernel<evxq::CV_NONE, false, evxq::VB_K>), grid, dim3(256), 0, st, *g,
+                               klen, 0);
+        else
+            hipLaunchKernelGGL(evxq::gemm128x3_kernel<evxq::CV_NONE>, grid, dim3(256), 0, st, *g, klen, 0);
+    }
     else
         hipLaunchKernelGGL(evxq::gemm128_kernel<float>, grid, dim3(256), 0, st, *g, klen);
     if (S > 1) {  // the slices' partials summed in slice order, then the epilogue
