@@ -3056,12 +3056,14 @@ __device__ __forceinline__ unsigned long long bucket_eq(int k, const unsigned lo
     for (int j = 0; j < 4; j++) v &= ((k >> j) & 1) ? m[j] : ~m[j];
     return v;
 }
-template <bool V16>  // V16: cls 16-B aligned -- the scan reads 16 class bytes per lane
-__global__ __launch_bounds__(1024) void env_orders_kernel(const uint8_t* __restrict__ cls, int E, int hcap,
-                                                          int32_t* __restrict__ order, int32_t* __restrict__ perm) {
-    __shared__ int wt[16][OSL], wp[16][OSL], wc[16][OSL];
+// NW waves per workgroup, 64 NW envs ranked per workgroup (blk): env_orders_kernel and the orders
+// blocks of env_orders_push_kernel (NW 16; smaller workgroups straddle the 1024-env scan chunks).
+template <bool V16, int NW>  // V16: cls 16-B aligned -- the scan reads 16 class bytes per lane
+__device__ __forceinline__ void orders_body(const uint8_t* __restrict__ cls, int E, int hcap, int32_t* __restrict__ order,
+                                            int32_t* __restrict__ perm, int blk) {
+    __shared__ int wt[NW][OSL], wp[NW][OSL], wc[NW][OSL];
     const int tid = (int)threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int c0 = (int)blockIdx.x * 1024;
+    const int c0 = blk * 64 * NW;
     auto ballots = [&](int b, unsigned long long (&m)[4], unsigned long long& mv, unsigned long long& mf,
                        unsigned long long& mh) {
         mv = __ballot(b >= 0);
@@ -3076,53 +3078,59 @@ __global__ __launch_bounds__(1024) void env_orders_kernel(const uint8_t* __restr
         const unsigned long long sel = lane < 16 ? bucket_eq(k, m, mv) : lane == 16 ? mf : lane == 17 ? mh : mv;
         return lane < OSL ? __popcll(sel) : 0;
     };
-    // every class byte of the launch: totals (t) and the chunks before this one (p)
+    // every class byte of the launch: totals (t) and the envs before this workgroup's (pr)
     int t = 0, pr = 0;
     if constexpr (V16) {
-        // wave w reads the 1024-env chunks w, w + 16, ..: lane l holds envs 16 l .. 16 l + 15 of one,
+        // wave w reads the 1024-env chunks w, w + NW, ..: lane l holds envs 16 l .. 16 l + 15 of one,
         // two chunks' loads in flight before either is counted (byte j of every lane: one ballot set)
-        for (int q0 = w; q0 * 1024 < E; q0 += 32) {
+        for (int q0 = w; q0 * 1024 < E; q0 += 2 * NW) {
             uint4 v[2];
 #pragma unroll
             for (int i = 0; i < 2; i++) {
-                const int e0 = (q0 + 16 * i) * 1024 + 16 * lane;
+                const int e0 = (q0 + NW * i) * 1024 + 16 * lane;
                 v[i] = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
                 if (e0 < E) v[i] = *reinterpret_cast<const uint4*>(cls + e0);
             }
 #pragma unroll
             for (int i = 0; i < 2; i++) {
-                const int q = q0 + 16 * i, e0 = q * 1024 + 16 * lane;
+                const int q = q0 + NW * i, e0 = q * 1024 + 16 * lane;
                 const uint32_t wd[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
-                int n = 0;
+                // a chunk that straddles c0 (NW < 16) counts its envs below c0 separately
+                const bool split = q * 1024 < c0 && c0 < q * 1024 + 1024;
+                int n = 0, nb = 0;
 #pragma unroll
                 for (int j = 0; j < 16; j++) {
                     const int b = e0 + j < E ? (int)((wd[j >> 2] >> (8 * (j & 3))) & 0xffu) : -1;
                     unsigned long long m[4], mv, mf, mh;
                     ballots(b, m, mv, mf, mh);
                     n += slot_count(m, mv, mf, mh);
+                    if (split) {
+                        ballots(e0 + j < c0 ? b : -1, m, mv, mf, mh);
+                        nb += slot_count(m, mv, mf, mh);
+                    }
                 }
                 t += n;
-                pr += q * 1024 < c0 ? n : 0;
+                pr += q * 1024 + 1024 <= c0 ? n : nb;
             }
         }
     } else {
         const int nb = (E + 63) / 64;
 #pragma unroll 4
-        for (int blk = w; blk < nb; blk += 16) {
-            const int e = blk * 64 + lane;
+        for (int bk = w; bk < nb; bk += NW) {
+            const int e = bk * 64 + lane;
             const int b = e < E ? (int)cls[e] : -1;
             unsigned long long m[4], mv, mf, mh;
             ballots(b, m, mv, mf, mh);
             const int n = slot_count(m, mv, mf, mh);
             t += n;
-            pr += blk * 64 < c0 ? n : 0;
+            pr += bk * 64 < c0 ? n : 0;
         }
     }
     if (lane < OSL) {
         wt[w][lane] = t;
         wp[w][lane] = pr;
     }
-    // this chunk: the waves' counts (for the ranks across waves) and the in-wave masks
+    // this workgroup's envs: the waves' counts (for the ranks across waves) and the in-wave masks
     const int e = c0 + tid;
     const int b = e < E ? (int)cls[e] : -1;
     unsigned long long m[4], mv, mf, mh;
@@ -3132,7 +3140,7 @@ __global__ __launch_bounds__(1024) void env_orders_kernel(const uint8_t* __restr
     __syncthreads();
     if (tid < OSL) {  // totals and prefix over the waves' partial counts (into wt[0], wp[0])
         int st = 0, sp = 0;
-        for (int k = 0; k < 16; k++) {
+        for (int k = 0; k < NW; k++) {
             st += wt[k][tid];
             sp += wp[k][tid];
         }
@@ -3164,6 +3172,43 @@ __global__ __launch_bounds__(1024) void env_orders_kernel(const uint8_t* __restr
         }
         perm[base] = e;
     }
+}
+template <bool V16>
+__global__ __launch_bounds__(1024) void env_orders_kernel(const uint8_t* __restrict__ cls, int E, int hcap,
+                                                          int32_t* __restrict__ order, int32_t* __restrict__ perm) {
+    orders_body<V16, 16>(cls, E, hcap, order, perm, (int)blockIdx.x);
+}
+// DQNAgent.remember for every robot of the step (the replay push: evxq::replay_push_kernel's body)
+// and the next step's orders in one launch: workgroups [0, nord) the orders (1024 envs each), the
+// rest one transition per thread -- the orders then need no launch or cross-stream event of their
+// own, and run beside the push's memory traffic. (256-env order workgroups of 4 waves, each
+// scanning every class byte, made the launch 32 us.)
+struct PushArgs {
+    evx_replay rp;
+    const evx_obs *s, *s2, *s2_term;
+    const int32_t* a;
+    const double* r_env;
+    const uint8_t* done_env;
+    int n, agents_per_env;
+    int64_t pos;
+};
+template <bool V16>
+__global__ __launch_bounds__(1024) void env_orders_push_kernel(const uint8_t* __restrict__ cls, int E, int hcap,
+                                                               int32_t* __restrict__ order, int32_t* __restrict__ perm,
+                                                               int nord, PushArgs pa) {
+    if ((int)blockIdx.x < nord) {
+        orders_body<V16, 16>(cls, E, hcap, order, perm, (int)blockIdx.x);
+        return;
+    }
+    const int i = ((int)blockIdx.x - nord) * 1024 + (int)threadIdx.x;
+    if (i >= pa.n) return;
+    const int64_t slot = (pa.pos + i) & (pa.rp.capacity - 1);  // power-of-two capacity (host-checked)
+    const int e = i / pa.agents_per_env;
+    pa.rp.s[slot] = pa.s[i];
+    pa.rp.s2[slot] = (pa.s2_term && pa.done_env[e]) ? pa.s2_term[i] : pa.s2[i];
+    pa.rp.a[slot] = pa.a[i];
+    pa.rp.r[slot] = (float)pa.r_env[e];
+    pa.rp.done[slot] = pa.done_env[e];
 }
 
 // ---------------------------------------------------- observation expand
@@ -3455,6 +3500,33 @@ int evx_env_orders(const evx_layout* l, const evx_state* s, int32_t* perm, void*
     if (!s || !s->order || !s->perm_ws) return fail(-22, "env_orders: state.order / state.perm_ws is NULL");
     if (s->E <= 0) return 0;
     return launch_orders(l, s, s->order, perm, (hipStream_t)stream);
+}
+
+int evx_env_orders_push(const evx_layout* l, const evx_state* s, int32_t* perm, const evx_replay* rp,
+                        const evx_obs* s_obs, const evx_obs* s2, const evx_obs* s2_term, const int32_t* a,
+                        const double* r_env, const uint8_t* done_env, int32_t n, int32_t agents_per_env, int64_t pos,
+                        void* stream) {
+    int rc = check_layout(l);
+    if (rc) return rc;
+    if (!s || !s->order || !s->perm_ws) return fail(-22, "env_orders_push: state.order / state.perm_ws is NULL");
+    if (!rp || rp->capacity <= 0 || (rp->capacity & (rp->capacity - 1)))
+        return fail(-22, "env_orders_push: replay capacity must be a power of two");
+    if (n < 0 || agents_per_env <= 0 || (n > 0 && (!s_obs || !s2 || !a || !r_env || !done_env)))
+        return fail(-22, "env_orders_push: bad push arguments");
+    int hmin = 0;
+    const int hcap = heavy_cap(*l, &hmin);
+    const int nord = s->E > 0 ? (s->E + 1023) / 1024 : 0;
+    const unsigned nblk = (unsigned)(nord + (n + 1023) / 1024);
+    if (nblk == 0) return 0;
+    evx::PushArgs pa{*rp, s_obs, s2, s2_term, a, r_env, done_env, n, agents_per_env, pos};
+    if (((uintptr_t)s->perm_ws & 15) == 0)
+        hipLaunchKernelGGL(evx::env_orders_push_kernel<true>, dim3(nblk), dim3(1024), 0, (hipStream_t)stream,
+                           (const uint8_t*)s->perm_ws, s->E, hcap, s->order, perm, nord, pa);
+    else
+        hipLaunchKernelGGL(evx::env_orders_push_kernel<false>, dim3(nblk), dim3(1024), 0, (hipStream_t)stream,
+                           (const uint8_t*)s->perm_ws, s->E, hcap, s->order, perm, nord, pa);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : hip_fail(e, "env_orders_push launch");
 }
 
 int evx_env_classes(const evx_layout* l, const evx_state* s, void* stream) {

@@ -37,6 +37,11 @@ class evx_state(C.Structure):
                                       "py_mt", "np_mt", "scratch", "order", "layout_idx", "perm_ws"]]
 
 
+class evx_replay(C.Structure):
+    _fields_ = [("capacity", C.c_int64), ("s", C.c_void_p), ("s2", C.c_void_p), ("a", C.c_void_p),
+                ("r", C.c_void_p), ("done", C.c_void_p)]
+
+
 class evx_step_out(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in ["reward", "done", "counts", "obs", "err", "stamps", "obs_term"]]
 
@@ -71,6 +76,9 @@ def lib():
         L.evx_env_order.argtypes = [C.POINTER(evx_layout), C.POINTER(evx_state), C.c_void_p]
         L.evx_act_perm.argtypes = [C.POINTER(evx_layout), C.POINTER(evx_state), C.c_void_p, C.c_void_p]
         L.evx_env_orders.argtypes = [C.POINTER(evx_layout), C.POINTER(evx_state), C.c_void_p, C.c_void_p]
+        L.evx_env_orders_push.argtypes = [C.POINTER(evx_layout), C.POINTER(evx_state), C.c_void_p,
+                                          C.POINTER(evx_replay)] + [C.c_void_p] * 6 + [C.c_int32, C.c_int32,
+                                                                                        C.c_int64, C.c_void_p]
         L.evx_env_classes.argtypes = [C.POINTER(evx_layout), C.POINTER(evx_state), C.c_void_p]
         L.evx_perm_ws_bytes.restype = C.c_int64
         L.evx_perm_ws_bytes.argtypes = [C.c_int32]
@@ -86,4 +94,4 @@ def check(rc: int, what: str):
 # every C symbol include/evacx.h declares (checked by tests/test_abi.py)
 EXPORTS = ["evx_env_step", "evx_env_reset", "evx_obs_expand_f32", "evx_obs_expand_f64", "evx_seed_host",
            "evx_step_lds_bytes", "evx_step_scratch_words", "evx_last_error", "evx_perm_ws_bytes",
-           "evx_env_order", "evx_act_perm", "evx_env_orders", "evx_env_classes"]
+           "evx_env_order", "evx_act_perm", "evx_env_orders", "evx_env_classes", "evx_env_orders_push"]

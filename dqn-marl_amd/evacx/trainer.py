@@ -27,13 +27,9 @@ import numpy as np
 import torch
 
 from . import _lib
-from .env import OBS_WORDS, DeviceLayout, VecEnv, _stream
+from ._lib import evx_replay
+from .env import OBS_WORDS, DeviceLayout, VecEnv, _ptr, _stream
 from .qnet import DROPOUT_P, Learner, qcheck, qlib
-
-
-class evx_replay(C.Structure):
-    _fields_ = [("capacity", C.c_int64), ("s", C.c_void_p), ("s2", C.c_void_p), ("a", C.c_void_p),
-                ("r", C.c_void_p), ("done", C.c_void_p)]
 
 
 class Replay:
@@ -66,6 +62,16 @@ class Replay:
             qcheck(L.evx_replay_push_term(C.byref(self.c), s.data_ptr(), s2.data_ptr(), s2_term.data_ptr(),
                                           a.data_ptr(), r_env.data_ptr(), done_env.data_ptr(), n, agents_per_env,
                                           self.pos, _stream()), "replay_push_term")
+        self.pos = (self.pos + n) % self.capacity
+        self.size = min(self.capacity, self.size + n)
+
+    def push_orders(self, env, perm, s, s2, a, r_env, done_env, n, agents_per_env, s2_term=None):
+        """push with env's next dispatch order and act env order (perm) in the same launch
+        (evx_env_orders_push; power-of-two capacity)."""
+        qcheck(_lib.lib().evx_env_orders_push(
+            C.byref(env.lay.c), C.byref(env.c), _ptr(perm), C.byref(self.c), s.data_ptr(), s2.data_ptr(),
+            _ptr(s2_term), a.data_ptr(), r_env.data_ptr(), done_env.data_ptr(), n, agents_per_env, self.pos,
+            _stream()), "env_orders_push")
         self.pos = (self.pos + n) % self.capacity
         self.size = min(self.capacity, self.size + n)
 
@@ -230,6 +236,7 @@ class VecTrainer:
         self.ev_reset.record(cur)
         self.reset_pending = False
         self.join_caller = True  # the first step waits for the caller's stream (set-up work)
+        self._orders_side = False  # the last step's orders were made on the side stream (act waits for them)
         self.lstream = torch.cuda.Stream(device=self.device, priority=0)
         self.ev_learned = torch.cuda.Event()
         self.ev_learned.record(cur)
@@ -385,6 +392,10 @@ class VecTrainer:
                 grp.main.wait_stream(caller)
             self.join_caller = False
         G = self.groups
+        # one group, uniform replay, no warm-up reset: the push and the next step's orders in one launch
+        # on the main stream (no side-stream event); otherwise the orders on the side stream
+        fused = (len(G) == 1 and extra_reset is None and type(self.replay) is Replay
+                 and (self.replay.capacity & (self.replay.capacity - 1)) == 0)
         reset_wait, self.reset_pending = self.reset_pending, False
         self._act_stream()
         # act: every group on its own stream, after the previous update (lagged) or learn
@@ -396,7 +407,7 @@ class VecTrainer:
                     grp.main.wait_event(self.ev_learned)
                 if grp.g > 0:  # the acts run one after the other: act g overlaps env.step g - 1
                     grp.main.wait_event(G[grp.g - 1].ev_act)
-                if len(G) == 1:  # the orders from the side stream (the act's env order, the step's)
+                if len(G) == 1 and self._orders_side:  # the orders from the side stream
                     grp.main.wait_event(grp.ev_order)
                 self._act(grp)
                 if self.lagged or grp.g + 1 < len(G):  # read by the update / the next group's act
@@ -430,11 +441,16 @@ class VecTrainer:
                 grp.env.step(grp.actions, order=False, auto_reset=True)
                 if ev_env is not None and grp.g == 0:
                     ev_env[1].record(grp.main)
-                self.replay.push(grp.env.obs_prev, grp.env.obs, grp.actions, grp.env.reward, grp.env.done, grp.n,
-                                 self.R, s2_term=grp.env.obs_term)
+                if fused:
+                    self.replay.push_orders(grp.env, grp.perm, grp.env.obs_prev, grp.env.obs, grp.actions,
+                                            grp.env.reward, grp.env.done, grp.n, self.R, s2_term=grp.env.obs_term)
+                else:
+                    self.replay.push(grp.env.obs_prev, grp.env.obs, grp.actions, grp.env.reward, grp.env.done,
+                                     grp.n, self.R, s2_term=grp.env.obs_term)
                 if len(G) > 1:  # several groups: the orders on this stream, after the push
                     grp.env.compute_orders(perm=grp.perm)
-                grp.ev_push.record(grp.main)
+                if not fused or self.lagged:  # read by the side stream / the lagged learn stream
+                    grp.ev_push.record(grp.main)
         if extra_reset is not None:  # after every group's push, on group 0's side stream (warm-up only)
             side = G[0].side
             extra_reset.record_stream(side)  # the caller may free it before the side stream reads it
@@ -448,10 +464,11 @@ class VecTrainer:
                         grp.env.compute_orders(perm=grp.perm)
                 self.ev_reset.record(side)
             self.reset_pending = True
-        if len(G) == 1:
+        self._orders_side = len(G) == 1 and not fused
+        if self._orders_side:
             # the next step's dispatch order and the next act's env order from the class bytes the
             # step (and a reset) just wrote, auto-reset envs included: one launch on the side stream,
-            # beside the push and the learn's first kernels
+            # beside the learn's first kernels
             grp = G[0]
             with torch.cuda.stream(grp.side):
                 grp.side.wait_event(grp.ev_push)  # (after an extra reset: the same stream)

@@ -293,6 +293,14 @@ int evx_replay_push(const evx_replay *rp, const evx_obs *s, const evx_obs *s2, c
 int evx_replay_push_term(const evx_replay *rp, const evx_obs *s, const evx_obs *s2, const evx_obs *s2_term,
                          const int32_t *a, const double *r_env, const uint8_t *done_env, int32_t n,
                          int32_t agents_per_env, int64_t pos, void *stream);
+/* evx_replay_push_term and evx_env_orders (the next step's order and the next act's env order
+ * `perm`, from the class bytes of state `s`) in one launch; the replay capacity must be a power of
+ * two. Replaces DQNAgent.remember for every robot of a step (agents/dqn_agent.py:97-99) plus the
+ * scheduling permutations. */
+int evx_env_orders_push(const evx_layout *l, const evx_state *s, int32_t *perm, const evx_replay *rp,
+                        const evx_obs *s_obs, const evx_obs *s2, const evx_obs *s2_term, const int32_t *a,
+                        const double *r_env, const uint8_t *done_env, int32_t n, int32_t agents_per_env,
+                        int64_t pos, void *stream);
 int evx_replay_sample(const evx_replay *rp, int64_t size, int32_t B, uint64_t seed, uint64_t offset, evx_obs *s,
                       evx_obs *s2, int32_t *a, float *r, uint8_t *done, int64_t *idx_out, void *stream);
 /* B uniform indices over the ring window [base, base+count) mod capacity (same draws as

@@ -101,3 +101,46 @@ def test_step_and_reset_write_class_bytes():
             scal = env.scal.view(E, 4).cpu().numpy()
             assert np.array_equal(env.perm_ws[:E].cpu().numpy(), _want_classes(scal, P, t_max)), t
     assert n_done > 0
+
+
+@pytest.mark.parametrize("E", [1000, 32768, 40000])
+def test_orders_push_launch_matches_separate_launches(E):
+    """evx_env_orders_push (the trainer's one-group step: the replay push and the next orders in one
+    launch) equals evx_replay_push_term + evx_env_orders."""
+    _need_gpu()
+    from evacx.trainer import Replay
+    lay, env = _env(E)
+    P, t_max = int(lay.c.P), int(lay.c.t_max)
+    rng = np.random.default_rng(E + 1)
+    scal = np.zeros((E, 4), np.int32)
+    scal[:, 0] = rng.integers(0, t_max + 3, E)
+    ev = rng.integers(0, P + 1, E)
+    scal[:, 2] = ev
+    scal[:, 3] = np.minimum(rng.integers(0, P + 1, E), P - ev)
+    env.scal.view(E, 4).copy_(torch.from_numpy(scal))
+    env.refresh_classes()
+    R = int(lay.c.R)
+    n = E * R
+    g = torch.Generator(device="cuda").manual_seed(E)
+    obs_words = 8
+    s = torch.randint(-2**31, 2**31 - 1, (n * obs_words,), device="cuda", dtype=torch.int32, generator=g)
+    s2 = torch.randint(-2**31, 2**31 - 1, (n * obs_words,), device="cuda", dtype=torch.int32, generator=g)
+    s2t = torch.randint(-2**31, 2**31 - 1, (n * obs_words,), device="cuda", dtype=torch.int32, generator=g)
+    a = torch.randint(0, 5, (n,), device="cuda", dtype=torch.int32, generator=g)
+    r = torch.randn(E, device="cuda", dtype=torch.float64, generator=g)
+    d = (torch.rand(E, device="cuda", generator=g) < 0.3).to(torch.uint8)
+    cap = 1 << max(14, (2 * n - 1).bit_length())
+    ra, rb = Replay(cap, "cuda"), Replay(cap, "cuda")
+    ra.pos = rb.pos = cap - n // 2  # the push wraps around the ring's end
+    perm1 = torch.full((E + 5,), -7, dtype=torch.int32, device="cuda")
+    perm2 = torch.full((E + 5,), -7, dtype=torch.int32, device="cuda")
+    ra.push(s, s2, a, r, d, n, R, s2_term=s2t)
+    env.compute_orders(perm1)
+    order1 = env.order.clone()
+    env.order.fill_(-3)
+    rb.push_orders(env, perm2, s, s2, a, r, d, n, R, s2_term=s2t)
+    torch.cuda.synchronize()
+    assert torch.equal(perm1, perm2) and torch.equal(order1, env.order)
+    for name in ("s", "s2", "a", "r", "done"):
+        assert torch.equal(getattr(ra, name), getattr(rb, name)), name
+    assert (ra.pos, ra.size) == (rb.pos, rb.size)
