@@ -39,6 +39,7 @@
 
 #include "evacx.h"
 #include "evx_device.h"
+#include "evx_draws.h"
 #include "evx_host.h"
 
 namespace evx {
@@ -3192,17 +3193,53 @@ struct PushArgs {
     int n, agents_per_env;
     int64_t pos;
 };
+// the learn step's batch drawn in the same launch (evx_replay_sample's draws over the ring as it
+// stands after the push: a drawn slot inside the push window is read from the push's sources)
+struct SampleArgs {
+    int64_t size;  // ring size after the push
+    int B;
+    uint64_t seed, offset;
+    evx_obs *s, *s2;
+    int32_t* a;
+    float* r;
+    uint8_t* done;
+};
 template <bool V16>
 __global__ __launch_bounds__(1024) void env_orders_push_kernel(const uint8_t* __restrict__ cls, int E, int hcap,
                                                                int32_t* __restrict__ order, int32_t* __restrict__ perm,
-                                                               int nord, PushArgs pa) {
-    if ((int)blockIdx.x < nord) {
-        orders_body<V16, 16>(cls, E, hcap, order, perm, (int)blockIdx.x);
+                                                               int nord, int nsmp, PushArgs pa, SampleArgs sa) {
+    const int64_t cm = pa.rp.capacity - 1;  // power-of-two capacity (host-checked)
+    if ((int)blockIdx.x < nsmp) {  // 256 draws per workgroup: the dependent draw-and-gather chains
+                                   // spread over 4x the CUs (the other 12 waves leave at once)
+        if (threadIdx.x >= 256) return;
+        const int i = (int)blockIdx.x * 256 + (int)threadIdx.x;
+        if (i >= sa.B) return;
+        const evxd::perm_key pk = evxd::make_perm_key((uint64_t)sa.size, sa.seed, sa.offset, 0u);
+        const int64_t j = (int64_t)evxd::perm_apply(pk, (uint64_t)i, (uint64_t)sa.size);  // base 0: the whole ring
+        const int64_t off = (j - pa.pos) & cm;
+        if (off < pa.n) {  // written by this launch's push: its source
+            const int k = (int)off, e = k / pa.agents_per_env;
+            sa.s[i] = pa.s[k];
+            sa.s2[i] = (pa.s2_term && pa.done_env[e]) ? pa.s2_term[k] : pa.s2[k];
+            sa.a[i] = pa.a[k];
+            sa.r[i] = (float)pa.r_env[e];
+            sa.done[i] = pa.done_env[e];
+        } else {
+            sa.s[i] = pa.rp.s[j];
+            sa.s2[i] = pa.rp.s2[j];
+            sa.a[i] = pa.rp.a[j];
+            sa.r[i] = pa.rp.r[j];
+            sa.done[i] = pa.rp.done[j];
+        }
         return;
     }
-    const int i = ((int)blockIdx.x - nord) * 1024 + (int)threadIdx.x;
+    if ((int)blockIdx.x < nsmp + nord) {
+        orders_body<V16, 16>(cls, E, hcap, order, perm, (int)blockIdx.x - nsmp);
+        return;
+    }
+    const int i = ((int)blockIdx.x - nord - nsmp) * 1024 + (int)threadIdx.x;
     if (i >= pa.n) return;
-    const int64_t slot = (pa.pos + i) & (pa.rp.capacity - 1);  // power-of-two capacity (host-checked)
+    const int64_t slot = (pa.pos + i) & cm;
     const int e = i / pa.agents_per_env;
     pa.rp.s[slot] = pa.s[i];
     pa.rp.s2[slot] = (pa.s2_term && pa.done_env[e]) ? pa.s2_term[i] : pa.s2[i];
@@ -3506,6 +3543,21 @@ int evx_env_orders_push(const evx_layout* l, const evx_state* s, int32_t* perm, 
                         const evx_obs* s_obs, const evx_obs* s2, const evx_obs* s2_term, const int32_t* a,
                         const double* r_env, const uint8_t* done_env, int32_t n, int32_t agents_per_env, int64_t pos,
                         void* stream) {
+    return evx_env_orders_push_sample(l, s, perm, rp, s_obs, s2, s2_term, a, r_env, done_env, n, agents_per_env, pos,
+                                      0, 0, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr, stream);
+}
+
+int evx_env_orders_push_sample(const evx_layout* l, const evx_state* s, int32_t* perm, const evx_replay* rp,
+                               const evx_obs* s_obs, const evx_obs* s2, const evx_obs* s2_term, const int32_t* a,
+                               const double* r_env, const uint8_t* done_env, int32_t n, int32_t agents_per_env,
+                               int64_t pos, int32_t B, int64_t size, uint64_t seed, uint64_t offset, evx_obs* out_s,
+                               evx_obs* out_s2, int32_t* out_a, float* out_r, uint8_t* out_done, void* stream) {
+    if (B > 0) {
+        if (!rp || size <= 0 || size > rp->capacity) return fail(-22, "env_orders_push_sample: bad ring size");
+        if (B > size) return fail(-22, "env_orders_push_sample: sample larger than population (random.sample)");
+        if (!out_s || !out_s2 || !out_a || !out_r || !out_done) return fail(-22, "env_orders_push_sample: NULL output");
+        if (pos < 0 || n > rp->capacity) return fail(-22, "env_orders_push_sample: bad push window");
+    }
     int rc = check_layout(l);
     if (rc) return rc;
     if (!s || !s->order || !s->perm_ws) return fail(-22, "env_orders_push: state.order / state.perm_ws is NULL");
@@ -3516,15 +3568,17 @@ int evx_env_orders_push(const evx_layout* l, const evx_state* s, int32_t* perm, 
     int hmin = 0;
     const int hcap = heavy_cap(*l, &hmin);
     const int nord = s->E > 0 ? (s->E + 1023) / 1024 : 0;
-    const unsigned nblk = (unsigned)(nord + (n + 1023) / 1024);
+    const int nsmp = B > 0 ? (B + 255) / 256 : 0;
+    const unsigned nblk = (unsigned)(nord + nsmp + (n + 1023) / 1024);
     if (nblk == 0) return 0;
-    evx::PushArgs pa{*rp, s_obs, s2, s2_term, a, r_env, done_env, n, agents_per_env, pos};
+    evx::PushArgs pa{*rp, s_obs, s2, s2_term, a, r_env, done_env, n, agents_per_env, pos & (rp->capacity - 1)};
+    evx::SampleArgs sa{size, B, seed, offset, out_s, out_s2, out_a, out_r, out_done};
     if (((uintptr_t)s->perm_ws & 15) == 0)
         hipLaunchKernelGGL(evx::env_orders_push_kernel<true>, dim3(nblk), dim3(1024), 0, (hipStream_t)stream,
-                           (const uint8_t*)s->perm_ws, s->E, hcap, s->order, perm, nord, pa);
+                           (const uint8_t*)s->perm_ws, s->E, hcap, s->order, perm, nord, nsmp, pa, sa);
     else
         hipLaunchKernelGGL(evx::env_orders_push_kernel<false>, dim3(nblk), dim3(1024), 0, (hipStream_t)stream,
-                           (const uint8_t*)s->perm_ws, s->E, hcap, s->order, perm, nord, pa);
+                           (const uint8_t*)s->perm_ws, s->E, hcap, s->order, perm, nord, nsmp, pa, sa);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : hip_fail(e, "env_orders_push launch");
 }

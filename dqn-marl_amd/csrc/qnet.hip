@@ -20,6 +20,7 @@
 
 #include "evacx.h"
 #include "evx_host.h"
+#include "evx_draws.h"
 
 namespace evxq {
 
@@ -29,24 +30,13 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BM = 64, BN = 64, BK = 32;
 
-// ----------------------------------------------------------------- Philox4x32-10
-struct u4 {
-    uint32_t x, y, z, w;
-};
-__device__ __forceinline__ u4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
-#pragma unroll
-    for (int i = 0; i < 10; i++) {
-        const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
-        const uint32_t h0 = (uint32_t)(p0 >> 32), l0 = (uint32_t)p0, h1 = (uint32_t)(p1 >> 32), l1 = (uint32_t)p1;
-        c0 = h1 ^ c1 ^ k0;
-        c1 = l1;
-        c2 = h0 ^ c3 ^ k1;
-        c3 = l0;
-        k0 += 0x9E3779B9u;
-        k1 += 0xBB67AE85u;
-    }
-    return {c0, c1, c2, c3};
-}
+// Philox4x32-10, the replay permutation (evx_draws.h)
+using evxd::u4;
+using evxd::philox;
+using evxd::perm_key;
+using evxd::fmix32;
+using evxd::make_perm_key;
+using evxd::perm_apply;
 __device__ __forceinline__ float u01(uint32_t v) { return (float)(v >> 8) * (1.0f / 16777216.0f); }
 
 // ------------------------------------------------------------------------ GEMM
@@ -867,47 +857,6 @@ __global__ __launch_bounds__(256) void replay_push_kernel(evx_replay rp, const e
 // itself; expected < 4 rounds of walking since 2^w < 4n). Round keys from Philox4x32-10 of the
 // draw's (offset, stream) under the seed, so each learn step's batch is a fresh permutation and
 // the B draws are distinct (B <= n). oracle/draw_oracle.c orc_replay_indices restates it.
-struct perm_key {
-    uint32_t k[6];
-    int half;       // bits per Feistel half
-    uint64_t hmask; // (1 << half) - 1
-};
-__device__ __forceinline__ uint32_t fmix32(uint32_t h) {
-    h ^= h >> 16;
-    h *= 0x85ebca6bu;
-    h ^= h >> 13;
-    h *= 0xc2b2ae35u;
-    h ^= h >> 16;
-    return h;
-}
-__device__ __forceinline__ perm_key make_perm_key(uint64_t n, uint64_t seed, uint64_t offset, uint32_t stream) {
-    perm_key pk;
-    const u4 q = philox((uint32_t)offset, (uint32_t)(offset >> 32), 0x5a3b1eu, stream, (uint32_t)seed,
-                        (uint32_t)(seed >> 32));
-    const uint32_t qq[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-    for (int r = 0; r < 6; r++) pk.k[r] = fmix32(qq[r & 3] + (uint32_t)r * 0x9e3779b9u);
-    int w = 2;
-    while (w < 62 && (1ull << w) < n) w += 2;
-    pk.half = w / 2;
-    pk.hmask = (1ull << pk.half) - 1;
-    return pk;
-}
-__device__ __forceinline__ uint64_t perm_apply(const perm_key& pk, uint64_t x, uint64_t n) {
-    do {
-        uint64_t L = x >> pk.half, R = x & pk.hmask;
-#pragma unroll
-        for (int r = 0; r < 6; r++) {
-            const uint64_t F = (uint64_t)fmix32((uint32_t)R ^ pk.k[r]) & pk.hmask;  // R < 2^31
-            const uint64_t t = R;
-            R = L ^ F;
-            L = t;
-        }
-        x = (L << pk.half) | R;
-    } while (x >= n);
-    return x;
-}
-
 __global__ __launch_bounds__(256) void replay_sample_kernel(evx_replay rp, int64_t base, int64_t size, int B, uint64_t seed,
                                                             uint64_t offset, evx_obs* __restrict__ s,
                                                             evx_obs* __restrict__ s2, int32_t* __restrict__ a,

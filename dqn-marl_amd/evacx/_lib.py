@@ -79,6 +79,10 @@ def lib():
         L.evx_env_orders_push.argtypes = [C.POINTER(evx_layout), C.POINTER(evx_state), C.c_void_p,
                                           C.POINTER(evx_replay)] + [C.c_void_p] * 6 + [C.c_int32, C.c_int32,
                                                                                         C.c_int64, C.c_void_p]
+        L.evx_env_orders_push_sample.argtypes = ([C.POINTER(evx_layout), C.POINTER(evx_state), C.c_void_p,
+                                                  C.POINTER(evx_replay)] + [C.c_void_p] * 6 +
+                                                 [C.c_int32, C.c_int32, C.c_int64, C.c_int32, C.c_int64, C.c_uint64,
+                                                  C.c_uint64] + [C.c_void_p] * 6)
         L.evx_env_classes.argtypes = [C.POINTER(evx_layout), C.POINTER(evx_state), C.c_void_p]
         L.evx_perm_ws_bytes.restype = C.c_int64
         L.evx_perm_ws_bytes.argtypes = [C.c_int32]
@@ -94,4 +98,4 @@ def check(rc: int, what: str):
 # every C symbol include/evacx.h declares (checked by tests/test_abi.py)
 EXPORTS = ["evx_env_step", "evx_env_reset", "evx_obs_expand_f32", "evx_obs_expand_f64", "evx_seed_host",
            "evx_step_lds_bytes", "evx_step_scratch_words", "evx_last_error", "evx_perm_ws_bytes",
-           "evx_env_order", "evx_act_perm", "evx_env_orders", "evx_env_classes", "evx_env_orders_push"]
+           "evx_env_order", "evx_act_perm", "evx_env_orders", "evx_env_classes", "evx_env_orders_push", "evx_env_orders_push_sample"]

@@ -65,15 +65,19 @@ class Replay:
         self.pos = (self.pos + n) % self.capacity
         self.size = min(self.capacity, self.size + n)
 
-    def push_orders(self, env, perm, s, s2, a, r_env, done_env, n, agents_per_env, s2_term=None):
+    def push_orders(self, env, perm, s, s2, a, r_env, done_env, n, agents_per_env, s2_term=None, sample=None):
         """push with env's next dispatch order and act env order (perm) in the same launch
-        (evx_env_orders_push; power-of-two capacity)."""
-        qcheck(_lib.lib().evx_env_orders_push(
+        (evx_env_orders_push_sample; power-of-two capacity). sample = (B, seed, offset, out): also
+        draw the learn step's batch into out, as sample() would right after the push."""
+        size = min(self.capacity, self.size + n)
+        B, seed, offset, out = sample if sample is not None else (0, 0, 0, None)
+        o = (lambda k: out[k].data_ptr()) if out is not None else (lambda k: None)
+        qcheck(_lib.lib().evx_env_orders_push_sample(
             C.byref(env.lay.c), C.byref(env.c), _ptr(perm), C.byref(self.c), s.data_ptr(), s2.data_ptr(),
             _ptr(s2_term), a.data_ptr(), r_env.data_ptr(), done_env.data_ptr(), n, agents_per_env, self.pos,
-            _stream()), "env_orders_push")
+            B, size, seed, offset, o("s"), o("s2"), o("a"), o("r"), o("done"), _stream()), "env_orders_push_sample")
         self.pos = (self.pos + n) % self.capacity
-        self.size = min(self.capacity, self.size + n)
+        self.size = size
 
     def window(self, n_next):
         """(base, count): the entries already in the ring that a push of n_next
@@ -237,6 +241,7 @@ class VecTrainer:
         self.reset_pending = False
         self.join_caller = True  # the first step waits for the caller's stream (set-up work)
         self._orders_side = False  # the last step's orders were made on the side stream (act waits for them)
+        self._presampled = False   # this step's learn batch was drawn by the push launch
         self.lstream = torch.cuda.Stream(device=self.device, priority=0)
         self.ev_learned = torch.cuda.Event()
         self.ev_learned.record(cur)
@@ -340,7 +345,9 @@ class VecTrainer:
                 self.replay.sample_prio(self.batch, beta, self.seed + 1, self.learn_steps * self.batch, self.samp,
                                         self.samp["idx"], w)
             elif window is None:
-                self.replay.sample(self.batch, self.seed + 1, self.learn_steps * self.batch, self.samp)
+                if not self._presampled:  # (drawn by the push launch of this step)
+                    self.replay.sample(self.batch, self.seed + 1, self.learn_steps * self.batch, self.samp)
+                self._presampled = False
             else:
                 self.replay.sample_window(window[0], window[1], self.batch, self.seed + 1,
                                           self.learn_steps * self.batch, self.samp)
@@ -397,6 +404,7 @@ class VecTrainer:
         fused = (len(G) == 1 and extra_reset is None and type(self.replay) is Replay
                  and (self.replay.capacity & (self.replay.capacity - 1)) == 0)
         reset_wait, self.reset_pending = self.reset_pending, False
+        self._presampled = False
         self._act_stream()
         # act: every group on its own stream, after the previous update (lagged) or learn
         for grp in G:
@@ -442,8 +450,15 @@ class VecTrainer:
                 if ev_env is not None and grp.g == 0:
                     ev_env[1].record(grp.main)
                 if fused:
+                    # the strict schedule's learn batch drawn in the same launch (the ring after this push)
+                    smp = None
+                    if (not self.lagged and not self.prio and not self.per_robot and self.t % self.learn_every == 0
+                            and min(self.replay.capacity, self.replay.size + grp.n) >= self.batch):
+                        smp = (self.batch, self.seed + 1, self.learn_steps * self.batch, self.samp)
                     self.replay.push_orders(grp.env, grp.perm, grp.env.obs_prev, grp.env.obs, grp.actions,
-                                            grp.env.reward, grp.env.done, grp.n, self.R, s2_term=grp.env.obs_term)
+                                            grp.env.reward, grp.env.done, grp.n, self.R, s2_term=grp.env.obs_term,
+                                            sample=smp)
+                    self._presampled = smp is not None
                 else:
                     self.replay.push(grp.env.obs_prev, grp.env.obs, grp.actions, grp.env.reward, grp.env.done,
                                      grp.n, self.R, s2_term=grp.env.obs_term)
@@ -489,6 +504,7 @@ class VecTrainer:
                     ev_learn[1].record(m)
                 if len(G) > 1:
                     self.ev_learned.record(m)
+        self._presampled = False
         self.t += 1
 
     def sync(self):

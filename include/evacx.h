@@ -301,6 +301,13 @@ int evx_env_orders_push(const evx_layout *l, const evx_state *s, int32_t *perm, 
                         const evx_obs *s_obs, const evx_obs *s2, const evx_obs *s2_term, const int32_t *a,
                         const double *r_env, const uint8_t *done_env, int32_t n, int32_t agents_per_env,
                         int64_t pos, void *stream);
+/* ... and the learn step's batch (evx_replay_sample over the ring as it stands after the push:
+ * size = the ring size after it; B = 0 draws nothing) in the same launch. */
+int evx_env_orders_push_sample(const evx_layout *l, const evx_state *s, int32_t *perm, const evx_replay *rp,
+                               const evx_obs *s_obs, const evx_obs *s2, const evx_obs *s2_term, const int32_t *a,
+                               const double *r_env, const uint8_t *done_env, int32_t n, int32_t agents_per_env,
+                               int64_t pos, int32_t B, int64_t size, uint64_t seed, uint64_t offset, evx_obs *out_s,
+                               evx_obs *out_s2, int32_t *out_a, float *out_r, uint8_t *out_done, void *stream);
 int evx_replay_sample(const evx_replay *rp, int64_t size, int32_t B, uint64_t seed, uint64_t offset, evx_obs *s,
                       evx_obs *s2, int32_t *a, float *r, uint8_t *done, int64_t *idx_out, void *stream);
 /* B uniform indices over the ring window [base, base+count) mod capacity (same draws as

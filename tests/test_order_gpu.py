@@ -105,8 +105,9 @@ def test_step_and_reset_write_class_bytes():
 
 @pytest.mark.parametrize("E", [1000, 32768, 40000])
 def test_orders_push_launch_matches_separate_launches(E):
-    """evx_env_orders_push (the trainer's one-group step: the replay push and the next orders in one
-    launch) equals evx_replay_push_term + evx_env_orders."""
+    """evx_env_orders_push_sample (the trainer's one-group step: the replay push, the next orders and
+    the learn step's batch in one launch) equals evx_replay_push_term + evx_replay_sample +
+    evx_env_orders."""
     _need_gpu()
     from evacx.trainer import Replay
     lay, env = _env(E)
@@ -132,15 +133,33 @@ def test_orders_push_launch_matches_separate_launches(E):
     cap = 1 << max(14, (2 * n - 1).bit_length())
     ra, rb = Replay(cap, "cuda"), Replay(cap, "cuda")
     ra.pos = rb.pos = cap - n // 2  # the push wraps around the ring's end
+    for rr in (ra, rb):  # older transitions everywhere else in the ring (the same in both)
+        rr.s.copy_(torch.arange(rr.s.numel(), device="cuda", dtype=torch.int32))
+        rr.s2.copy_(-torch.arange(rr.s2.numel(), device="cuda", dtype=torch.int32))
+        rr.a.copy_(torch.arange(cap, device="cuda", dtype=torch.int32) % 5)
+        rr.r.copy_(torch.arange(cap, device="cuda", dtype=torch.float32))
+        rr.done.copy_((torch.arange(cap, device="cuda") % 3 == 0).to(torch.uint8))
+        rr.size = cap - n // 4
     perm1 = torch.full((E + 5,), -7, dtype=torch.int32, device="cuda")
     perm2 = torch.full((E + 5,), -7, dtype=torch.int32, device="cuda")
+    B = min(4096, cap // 2)
+    out = [dict(s=torch.zeros(B * 8, dtype=torch.int32, device="cuda"),
+                s2=torch.zeros(B * 8, dtype=torch.int32, device="cuda"),
+                a=torch.zeros(B, dtype=torch.int32, device="cuda"), r=torch.zeros(B, device="cuda"),
+                done=torch.zeros(B, dtype=torch.uint8, device="cuda")) for _ in range(2)]
     ra.push(s, s2, a, r, d, n, R, s2_term=s2t)
+    ra.sample(B, 77, 12345, out[0])
     env.compute_orders(perm1)
     order1 = env.order.clone()
     env.order.fill_(-3)
-    rb.push_orders(env, perm2, s, s2, a, r, d, n, R, s2_term=s2t)
+    rb.push_orders(env, perm2, s, s2, a, r, d, n, R, s2_term=s2t, sample=(B, 77, 12345, out[1]))  # one launch
     torch.cuda.synchronize()
     assert torch.equal(perm1, perm2) and torch.equal(order1, env.order)
     for name in ("s", "s2", "a", "r", "done"):
         assert torch.equal(getattr(ra, name), getattr(rb, name)), name
+        assert torch.equal(out[0][name], out[1][name]), name
     assert (ra.pos, ra.size) == (rb.pos, rb.size)
+    # the batch drew slots the push wrote (read from the push's sources) and older ones
+    pushed = set(((ra.pos - n + np.arange(n)) % cap).tolist())
+    got_r = out[1]["r"].cpu().numpy()
+    assert np.any(got_r != np.floor(got_r)) or len(pushed) < cap  # fractional rewards come from the push

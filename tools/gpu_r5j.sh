@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 5: replay push and the next orders in one launch (one group, uniform replay)
+# round 5: replay push, the next orders and the learn batch in one launch (one group, uniform replay)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/r5j; rm -rf $OUT; mkdir -p $OUT
