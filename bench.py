@@ -306,15 +306,20 @@ def main():
     timed_train(args.warmup)
 
     # ------------------------------------------------------------ timed steps
-    # HIP events bracket env.step on its own stream on every EV_EVERY-th step only: an
-    # event record costs the stream a ~6 us gap (tools/gap_probe.py)
+    # no instrumentation inside the timed region: an event record costs the stream a ~6 us gap
+    # (tools/gap_probe.py), 4 records per instrumented step -- 1.6 % of cfg2's step at one
+    # instrumented step in EV_EVERY
+    elapsed = timed_train(args.steps)
+    env.check_err()
+    loss = float(tr.last_loss.float().mean().item()) if tr.last_loss is not None else None
+    value = E * world * args.steps / elapsed
+    # the kernel / learn times: a second pass of the same length right after (same episode phase),
+    # HIP events bracketing env.step and the learn step on every EV_EVERY-th step
     ev_env, ev_learn = ev_pairs(args.steps), ev_pairs(args.steps)
-    elapsed = timed_train(args.steps, ev_env, ev_learn if args.mode == "train" else None)
+    timed_train(args.steps, ev_env, ev_learn if args.mode == "train" else None)
     env.check_err()
     kern_ms = ev_mean(ev_env, args.steps)
     learn_ms = ev_mean(ev_learn, args.steps) if args.mode == "train" else None
-    loss = float(tr.last_loss.float().mean().item()) if tr.last_loss is not None else None
-    value = E * world * args.steps / elapsed
 
     # ------------------------------- the other schedule on the same state (extra)
     other = None
@@ -464,7 +469,8 @@ def main():
             "start_phase": start,
             "env_step_kernel_ms": kern_ms,
             "learn_ms": learn_ms,
-            "learn_ms_what": "the learn step on the training stream (every 5th timed step)",
+            "learn_ms_what": "the learn step on the training stream (every 5th step of the instrumented pass "
+                             "that follows the timed steps)",
             "learn_alone_ms": learn_alone_ms,
             "last_loss": loss,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -1,0 +1,24 @@
+#!/bin/bash
+# round 5: act-table build in two K parts + small-batch backward splits (libevacx.so) vs the previous commit's
+# kernels (libevacx_old.so): qmlp / table / learner parity on the new build, then cfg2 and cfg3 lines alternating
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/r5tab; rm -rf $OUT; mkdir -p $OUT
+cd $R
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_target_table_gpu.py tests/test_qmlp_x3_gpu.py \
+  tests/test_qmlp_gpu.py tests/test_learner_golden_gpu.py tests/test_trainer_gpu.py tests/test_bench_scale_gpu.py tests/test_qgroup_gpu.py \
+  tests/test_concurrency_gpu.py > $OUT/tests.log 2>&1
+rc=$?; tail -1 $OUT/tests.log; [ $rc -ne 0 ] && { grep -E "^E |FAILED" $OUT/tests.log | head -30; exit $rc; }
+summ() { python3 -c "
+import json; d=json.load(open('$1'))
+print('$2', 'value %.3f M' % (d['value']/1e6), 'ms %.4f' % d['ms_per_step'], 'env %.4f' % d['env_step_kernel_ms'], 'learn', d.get('learn_ms'), 'alone', d.get('learn_alone_ms'))"; }
+for i in 1 2; do
+for tag in new old; do
+  L=$R/dqn-marl_amd/evacx/libevacx.so; [ $tag = old ] && L=$R/dqn-marl_amd/evacx/libevacx_old.so
+  EVX_LIB=$L timeout -k 10 300 python3 bench.py --no-cpu --grid 64 --people 569 --robots 8 --envs 4096 --steps 300 --warmup 20 --other-steps 0 \
+      --env-steps 0 --start-steps 0 > $OUT/c2_${tag}_$i.json 2> $OUT/c2_${tag}_$i.err || { tail -5 $OUT/c2_${tag}_$i.err; exit 1; }
+  summ $OUT/c2_${tag}_$i.json "cfg2 $tag"
+  EVX_LIB=$L timeout -k 10 300 python3 bench.py --no-cpu --steps 100 --warmup 10 --other-steps 0 --env-steps 0 --start-steps 0 \
+      > $OUT/c3_${tag}_$i.json 2> $OUT/c3_${tag}_$i.err || { tail -5 $OUT/c3_${tag}_$i.err; exit 1; }
+  summ $OUT/c3_${tag}_$i.json "cfg3 $tag"
+done; done

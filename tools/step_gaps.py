@@ -27,3 +27,14 @@ for r in rows[a:b + 1]:
                                               r["Kernel_Name"][:70]))
 span = int(rows[b]["Start_Timestamp"]) - t0
 print("step span %.1f us, idle gaps %.1f us (%.1f %%)" % (span / 1e3, gap / 1e3, 100.0 * gap / span))
+# every step of the trace between consecutive env launches: span and idle gaps (host-bound steps show
+# up as gaps here even when the one printed above has none)
+print("all steps (env launch k -> k+1): span us / idle us")
+for a, b in zip(env[:-1], env[1:]):
+    t0 = int(rows[a]["Start_Timestamp"])
+    busy_end, gap = t0, 0
+    for r in rows[a:b + 1]:
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        gap += max(0, s - busy_end)
+        busy_end = max(busy_end, e)
+    print("  %8.1f %7.1f" % ((int(rows[b]["Start_Timestamp"]) - t0) / 1e3, gap / 1e3))
