@@ -22,6 +22,7 @@ ap.add_argument("--table-frac", type=float, default=0.0,
 ap.add_argument("--order", choices=["env", "centre", "shuffle"], default="env",
                 help="row order: env (the envs' own), centre (sorted by window centre: rows sharing a table row "
                      "adjacent), shuffle (random)")
+ap.add_argument("--drop-p", type=float, default=DROPOUT_P, help="dropout p of the act (0: no dropout epilogue)")
 args = ap.parse_args()
 E, R = 4096, 16
 lay = DeviceLayout(build_tables(synthetic(128, 128, R)), 2276)
@@ -45,12 +46,12 @@ elif args.order == "shuffle":
     obs = obs[torch.randperm(obs.shape[0], device="cuda")].contiguous()
 act = torch.empty(args.rows, dtype=torch.int32, device="cuda")
 for i in range(3):
-    lr.fast.act(lay.c, obs.view(-1), args.rows, drop=(1, i, DROPOUT_P), actions=act, epsilon=0.1)
+    lr.fast.act(lay.c, obs.view(-1), args.rows, drop=(1, i, args.drop_p), actions=act, epsilon=0.1)
 torch.cuda.synchronize()
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 e0.record()
 for i in range(args.iters):
-    lr.fast.act(lay.c, obs.view(-1), args.rows, drop=(1, i, DROPOUT_P), actions=act, epsilon=0.1)
+    lr.fast.act(lay.c, obs.view(-1), args.rows, drop=(1, i, args.drop_p), actions=act, epsilon=0.1)
 e1.record()
 torch.cuda.synchronize()
 us = e0.elapsed_time(e1) / args.iters * 1e3
