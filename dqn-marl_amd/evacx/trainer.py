@@ -299,6 +299,9 @@ class VecTrainer:
             self.learner.drop_stream += 1
 
     def act(self):
+        """Launch DQNAgent.act for every robot of every env on the trainer's stream and return
+        the actions buffer. The kernels run asynchronously: read the returned tensor only after
+        sync() (or on a stream that waits for the trainer's), since the next step overwrites it."""
         self._act_stream()
         for grp in self.groups:
             self._act(grp)
