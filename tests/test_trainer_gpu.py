@@ -213,3 +213,54 @@ def test_groups_match_one_group():
     a, b = snaps
     for k in a:
         assert (a[k] == b[k]) if k == "drop" else torch.equal(a[k], b[k]), k
+
+
+@pytest.mark.gpu
+def test_fused_push_orders_sample_matches_separate_launches():
+    """The one-group strict step draws its learn batch in the replay push + orders launch
+    (evx_env_orders_push_sample). Against the same trainer with that launch disabled (a Replay
+    subclass: separate push, orders on the side stream, the sample in learn()) from the same seeds,
+    10 steps at cfg3's geometry (E = 4096, B = 4096, capacity 2^17 so the ring wraps): weights, Adam
+    moments, the replay ring, the env state and every step's actions are bit-identical."""
+    _need_gpu()
+    from evacx.env import DeviceLayout
+    from evacx.layout import build_tables, synthetic
+    from evacx.trainer import Replay, VecTrainer
+
+    class _Separate(Replay):  # type(replay) is not Replay: the trainer takes the separate launches
+        pass
+
+    lay = DeviceLayout(build_tables(synthetic(128, 128, 16)), 2276)
+    snaps = []
+    for separate in (False, True):
+        tr = VecTrainer(lay, 4096, batch=4096, replay_capacity=1 << 17, epsilon=0.3, target_every=4)
+        drawn = []
+        if separate:
+            tr.replay.__class__ = _Separate
+        else:  # count the fused launches that drew the learn batch
+            fused_call = tr.replay.push_orders
+
+            def counted(*args, sample=None, **kw):
+                drawn.append(sample is not None)
+                return fused_call(*args, sample=sample, **kw)
+            tr.replay.push_orders = counted
+        acts = []
+        for _ in range(10):
+            tr.step()
+            with torch.cuda.stream(tr.main):
+                acts.append(tr.actions.clone())
+        tr.sync()
+        torch.cuda.synchronize()
+        tr.env.check_err()
+        assert tr.learn_steps == 10
+        assert drawn == ([] if separate else [True] * 10), drawn
+        lr, env = tr.learner, tr.env
+        snaps.append(dict(online=lr.online.flat.clone(), target=lr.target.flat.clone(), m=lr.m.clone(),
+                          v=lr.v.clone(), loss=tr.last_loss.clone(), pk=env.pk.clone(), health=env.health.clone(),
+                          rmap=env.rmap.clone(), robots=env.robots.clone(), obs=env.obs.clone(),
+                          acts=torch.stack(acts), ring=tr.replay.s.clone(), ring_a=tr.replay.a.clone()))
+        del tr, lr, env
+        torch.cuda.empty_cache()
+    a, b = snaps
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
