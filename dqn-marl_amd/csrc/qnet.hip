@@ -593,6 +593,135 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(evx_gemm_desc g, int
     }
 }
 
+// x3 GEMM with both f32 operands k-major ("TN": the weight gradients dW = dY^T X, K = the batch or
+// pixel rows): C[m][n] = sum_k A[k][m] B[k][n], A[k][m] = g.A[k sak + m] (sam = 1), B[k][n] =
+// g.B[k sbk + n] (sbn = 1) or, CONV (EVX_CONV_DW), B[k][n] = X[pixel k shifted by tap][c] for the
+// tap-major column n = tap cs + c, stored at the reference's column c * 9 + tap. 128 x 128 tiles of
+// 4 waves (2 x 2 of 64 x 64), K chunks of 64 rows staged in their memory order ([k][m] / [k][n])
+// as bf16 hi and lo planes (split in registers from 16-B f32 loads, 8-B LDS stores) and read back
+// by ds_read_b64_tr_b16, which hands each lane the 8 consecutive k of its column -- the generic
+// kernel's one-element transposing staging took ~0.3 PF on these shapes. The next chunk's loads
+// are in flight while the current one's MFMAs run. x3 products hi*hi + hi*lo + lo*hi, f32
+// accumulation; gridDim.z splits K into the workspace ws[z][M][N] (splitk_reduce adds in order).
+constexpr int T3K = 64, T3P = TB + 32;  // K chunk, LDS row pitch (bf16): 320-B rows, conflict-free tr reads
+constexpr int TN3_LDS = 4 * T3K * T3P * 2;  // A hi, A lo, B hi, B lo: 80 KB (two workgroups per CU)
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
+__device__ __forceinline__ bf16x8 tr_frag3(const __bf16* img, int lane_off, int k0, int c0) {
+    const __bf16* p0 = img + k0 * T3P + c0 + lane_off;
+    const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(p0));
+    const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(p0 + 4 * T3P));
+    const s16x4_t v[2] = {lo, hi};
+    return __builtin_bit_cast(bf16x8, v);
+}
+template <bool CONV>
+__global__ __launch_bounds__(256, 2) void tn3_kernel(evx_gemm_desc g, int klen, int cs) {
+    extern __shared__ __attribute__((aligned(16))) char tsm[];
+    auto img = reinterpret_cast<__bf16 (*)[T3K][T3P]>(tsm);  // [4][T3K][T3P]
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+    const int wm = w >> 1, wn = w & 1;
+    const int m0 = blockIdx.y * TB, n0 = blockIdx.x * TB;
+    const int kb = blockIdx.z * klen, ke = min(g.K, kb + klen);
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int j = 0; j < 2; j++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc[i][j][r] = 0.f;
+    // staging: thread t moves 4 columns 4 (t & 31) .. + 3 of rows (t >> 5) + 8 j (j < 8) of each operand
+    const int sc = 4 * (tid & 31), sr = tid >> 5;
+    const int am = m0 + sc, bn = n0 + sc;
+    // CONV: this thread's 4 columns share one tap (cs % 4 == 0): its pixel shift and channel
+    int cdy = 0, cdx = 0, cc = 0;
+    if constexpr (CONV) {
+        const int tap = bn / cs;
+        cc = bn - tap * cs;
+        cdy = tap / 3 - 1;
+        cdx = tap - (tap / 3) * 3 - 1;
+    }
+    float4 ra[8], rb[8];
+    auto fetch = [&](int k0) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int k = k0 + sr + 8 * j;
+            const bool kin = k < ke;
+            ra[j] = kin && am < g.M ? *reinterpret_cast<const float4*>(g.A + (int64_t)k * g.sak + am) : make_float4(0.f, 0.f, 0.f, 0.f);
+            if constexpr (CONV) {
+                const int q = (int)((uint32_t)k - div121((uint32_t)k) * 121u), y = div11(q), x = q - 11 * y;
+                const bool ok = kin && bn < g.N && (unsigned)(y + cdy) < 11u && (unsigned)(x + cdx) < 11u;
+                rb[j] = ok ? *reinterpret_cast<const float4*>(g.B + (int64_t)(k + cdy * 11 + cdx) * cs + cc)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+            } else {
+                rb[j] = kin && bn < g.N ? *reinterpret_cast<const float4*>(g.B + (int64_t)k * g.sbk + bn) : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+    };
+    auto put4 = [&](int pl, int row, float4 v) {  // 4 columns: hi into plane pl, lo into pl + 1 (8-B stores)
+        const float f[4] = {v.x, v.y, v.z, v.w};
+        __bf16 hi[4], lo[4];
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            hi[e] = (__bf16)f[e];
+            lo[e] = (__bf16)(f[e] - (float)hi[e]);
+        }
+        *reinterpret_cast<uint2*>(&img[pl][row][sc]) = __builtin_bit_cast(uint2, hi);
+        *reinterpret_cast<uint2*>(&img[pl + 1][row][sc]) = __builtin_bit_cast(uint2, lo);
+    };
+    const int q4 = (lane >> 2) & 3, pq = lane & 3;
+    const int lane_off = (8 * h + q4) * T3P + 16 * ((lane >> 4) & 1) + 4 * pq;
+    if (kb < ke) fetch(kb);
+    for (int k0 = kb; k0 < ke; k0 += T3K) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            put4(0, sr + 8 * j, ra[j]);
+            put4(2, sr + 8 * j, rb[j]);
+        }
+        __syncthreads();
+        if (k0 + T3K < ke) fetch(k0 + T3K);
+#pragma unroll
+        for (int s = 0; s < T3K / 16; s++) {
+            bf16x8 av[2][2], bv[2][2];  // [plane][tile]
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+#pragma unroll
+                for (int p = 0; p < 2; p++) {
+                    av[p][i] = tr_frag3(&img[p][0][0], lane_off, s * 16, wm * 64 + i * 32);
+                    bv[p][i] = tr_frag3(&img[2 + p][0][0], lane_off, s * 16, wn * 64 + i * 32);
+                }
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+#pragma unroll
+                for (int j = 0; j < 2; j++) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[0][j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[1][j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1][i], bv[0][j], acc[i][j], 0, 0, 0);
+                }
+        }
+        __syncthreads();
+    }
+    // raw sums: C itself (one K slice) or the slice's workspace part; CONV columns to c * 9 + tap
+    float* out = gridDim.z == 1 ? g.C : g.ws + (int64_t)blockIdx.z * g.M * g.N;
+    const int64_t ld = gridDim.z == 1 ? g.ldc : g.N;
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        const int n = n0 + wn * 64 + j * 32 + (lane & 31);
+        if (n >= g.N) continue;
+        int col = n;
+        if constexpr (CONV) {
+            const int tap = n / cs;
+            col = (n - tap * cs) * 9 + tap;
+        }
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (m < g.M) out[(int64_t)m * ld + col] = acc[i][j][r];
+            }
+    }
+}
+
 // splitk_reduce_kernel for many slices (S >= 8, M N a multiple of 4): a workgroup takes 64 float4
 // of C, each wave sums a contiguous quarter of the slices (in slice order) and wave 0 adds the four
 // quarter sums in order -- 4x the workgroups and a quarter of the dependent loads per thread of
@@ -1526,6 +1655,16 @@ static bool conv_direct(const evx_gemm_desc* g, int mode, int cs, hipStream_t st
     return true;
 }
 
+// tn3_kernel's cases: x3, no epilogue, A m-contiguous (sam 1) and B n-contiguous (sbn 1) or the
+// conv dW gather (channels a multiple of 4), row strides and widths multiples of 4, 16-B aligned
+static bool tn3_ok(const evx_gemm_desc* g, int cm, int cs) {
+    if (g->precision != EVX_PREC_X3 || g->bias || g->mask || g->gate || g->flags || g->alpha != 1.f) return false;
+    auto al16 = [](const float* p) { return ((uintptr_t)p & 15) == 0; };
+    if (g->sam != 1 || (g->sak & 3) || (g->M & 3) || !al16(g->A) || !al16(g->B)) return false;
+    if (g->K < 256) return false;
+    if (cm == evxq::CV_DW) return (cs & 3) == 0 && g->N == 9 * cs;
+    return cm == evxq::CV_NONE && g->sbn == 1 && (g->sbk & 3) == 0 && (g->N & 3) == 0;
+}
 int gemm_launch(const evx_gemm_desc* g, int cm, int cs, void* stream) {
     if (!g || !g->A || !g->B || !g->C) return qfail(-22, "gemm: NULL operand");
     if (g->M <= 0 || g->N <= 0 || g->K <= 0) return 0;
@@ -1538,6 +1677,17 @@ int gemm_launch(const evx_gemm_desc* g, int cm, int cs, void* stream) {
     hipStream_t st = (hipStream_t)stream;
     if ((cm == evxq::CV_FWD || cm == evxq::CV_DX) && S == 1 && conv_direct(g, cm, cs, st)) return qlaunch("conv3x3");
     if (g->flags & EVX_GEMM_OUT_SPLIT) return qfail(-22, "gemm: OUT_SPLIT needs the LDS-staged conv forward (and its workspace)");
+    if (tn3_ok(g, cm, cs)) {  // weight gradients with both f32 operands k-major (fc layers' dW, conv dW)
+        {
+            static std::atomic<uint64_t> attr_done;
+            const void* ks[2] = {(const void*)evxq::tn3_kernel<false>, (const void*)evxq::tn3_kernel<true>};
+            evxh::max_lds_once(attr_done, ks, 2, evxq::TN3_LDS);
+        }
+        if (cm == evxq::CV_DW)
+            hipLaunchKernelGGL(evxq::tn3_kernel<true>, grid, dim3(256), evxq::TN3_LDS, st, *g, klen, cs);
+        else
+            hipLaunchKernelGGL(evxq::tn3_kernel<false>, grid, dim3(256), evxq::TN3_LDS, st, *g, klen, cs);
+    } else
     if (g->flags & EVX_GEMM_SPLIT_AB) {
         if (cm != evxq::CV_NONE || g->precision != EVX_PREC_X3 || g->sak != 1 || g->sbk != 1 || (g->K & 7) ||
             (g->sam & 7) || (g->sbn & 7))

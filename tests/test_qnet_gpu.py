@@ -201,6 +201,45 @@ def test_conv3x3_implicit_gemm_vs_torch(cin, cout, B):
         torch.testing.assert_close(got.cpu(), ref, rtol=1e-4, atol=2e-5 * ref.abs().max().item())
 
 
+@pytest.mark.parametrize("cin,cout,B,split", [(32, 64, 16, False), (64, 128, 16, False), (64, 128, 64, True),
+                                              (32, 64, 40, True)])
+def test_conv3x3_dw_tn_kernel_vs_torch(cin, cout, B, split):
+    """The conv weight gradient on the k-major x3 kernel (tn3_kernel: channels a multiple of 4,
+    K = B*121 >= 256), one K pass or split into the workspace: against torch autograd in float64."""
+    _need_gpu()
+    from evacx import qnet
+    g = torch.Generator().manual_seed(cin * 7 + B)
+    x = torch.randn(B, 11, 11, cin, generator=g)
+    w = torch.randn(cout, cin, 3, 3, generator=g) * 0.2
+    dy = torch.randn(B, 11, 11, cout, generator=g)
+    Mp, K9 = B * 121, cin * 9
+    xd, dyd = x.cuda().contiguous(), dy.cuda().contiguous()
+    dw = torch.full((cout, K9), 7.0, device="cuda")
+    ws = torch.zeros(1 << 24, device="cuda") if split else None
+    qnet.conv_gemm(qnet.CONV_DW, cout, K9, Mp, dyd, xd, dw, cin, sam=1, sak=cout, ws=ws)
+    xr = x.double().permute(0, 3, 1, 2)
+    wr = w.double().requires_grad_(True)
+    F.conv2d(xr, wr, padding=1).backward(dy.double().permute(0, 3, 1, 2))
+    ref = wr.grad.reshape(cout, K9).float()
+    torch.testing.assert_close(dw.cpu(), ref, rtol=1e-4, atol=2e-5 * ref.abs().max().item())
+
+
+@pytest.mark.parametrize("M,N,K,split", [(512, 1000, 1500, False), (256, 512, 4100, True), (64, 96, 3000, True)])
+def test_gemm_x3_k_major_operands_vs_float64(M, N, K, split):
+    """evx_gemm x3 with A[k][m] (sam 1) and B[k][n] (sbn 1) -- the fc layers' weight gradients
+    dW = dZ^T X on tn3_kernel (ragged M / N / K tiles, one pass or split-K) -- against float64."""
+    _need_gpu()
+    from evacx import qnet
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn(K, M, generator=g)
+    Bm = torch.randn(K, N, generator=g)
+    C = torch.full((M, N), 3.0, device="cuda")
+    ws = torch.zeros(1 << 24, device="cuda") if split else None
+    qnet.gemm(M, N, K, A.cuda(), 1, M, Bm.cuda(), N, 1, C, N, "x3", ws=ws)
+    ref = (A.double().t() @ Bm.double()).float()
+    torch.testing.assert_close(C.cpu(), ref, rtol=1e-4, atol=2e-5 * ref.abs().max().item())
+
+
 def test_conv_x3_act_and_learn_are_deterministic():
     """The conv Q-net in x3 at the cfg4 act's 8192 rows splits fc1 over K (256 tiles) and its
     learn splits the weight gradients: the K slices are summed in slice order (evx_gemm's
