@@ -605,6 +605,10 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(evx_gemm_desc g, int
 // accumulation; gridDim.z splits K into the workspace ws[z][M][N] (splitk_reduce adds in order).
 constexpr int T3K = 64, T3P = TB + 32;  // K chunk, LDS row pitch (bf16): 320-B rows, conflict-free tr reads
 constexpr int TN3_LDS = 4 * T3K * T3P * 2;  // A hi, A lo, B hi, B lo: 80 KB (two workgroups per CU)
+// AK (A k-contiguous, A[m][k] = g.A[m sam + k]): A staged as [m][k] rows (pitch T3K + 8: conflict-free
+// 16-B fragment reads) -- the activation gradients dX = dY W of the fc layers
+constexpr int T3AP = T3K + 8;
+static_assert(2 * TB * T3AP <= 2 * T3K * T3P, "the AK A planes fit the [k][m] ones' space");
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
 __device__ __forceinline__ bf16x8 tr_frag3(const __bf16* img, int lane_off, int k0, int c0) {
@@ -614,13 +618,15 @@ __device__ __forceinline__ bf16x8 tr_frag3(const __bf16* img, int lane_off, int 
     const s16x4_t v[2] = {lo, hi};
     return __builtin_bit_cast(bf16x8, v);
 }
-template <bool CONV>
+template <bool CONV, bool AK = false>
 __global__ __launch_bounds__(256, 2) void tn3_kernel(evx_gemm_desc g, int klen, int cs) {
     extern __shared__ __attribute__((aligned(16))) char tsm[];
     auto img = reinterpret_cast<__bf16 (*)[T3K][T3P]>(tsm);  // [4][T3K][T3P]
+    auto imga = reinterpret_cast<__bf16 (*)[TB][T3AP]>(tsm);  // AK: [2][TB][T3AP] over planes 0-1
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
     const int wm = w >> 1, wn = w & 1;
-    const int m0 = blockIdx.y * TB, n0 = blockIdx.x * TB;
+    const int bx = (int)blockIdx.x, by = (int)blockIdx.y;
+    const int m0 = by * TB, n0 = bx * TB;
     const int kb = blockIdx.z * klen, ke = min(g.K, kb + klen);
     f32x16 acc[2][2];
 #pragma unroll
@@ -641,12 +647,21 @@ __global__ __launch_bounds__(256, 2) void tn3_kernel(evx_gemm_desc g, int klen, 
         cdx = tap - (tap / 3) * 3 - 1;
     }
     float4 ra[8], rb[8];
+    // AK: thread t moves k 4 (t & 15) .. + 3 of rows m0 + (t >> 4) + 16 j
+    const int akk = 4 * (tid & 15), akm = tid >> 4;
     auto fetch = [&](int k0) {
 #pragma unroll
         for (int j = 0; j < 8; j++) {
             const int k = k0 + sr + 8 * j;
             const bool kin = k < ke;
-            ra[j] = kin && am < g.M ? *reinterpret_cast<const float4*>(g.A + (int64_t)k * g.sak + am) : make_float4(0.f, 0.f, 0.f, 0.f);
+            if constexpr (AK) {
+                const int m = m0 + akm + 16 * j, kk = k0 + akk;
+                ra[j] = m < g.M && kk < ke ? *reinterpret_cast<const float4*>(g.A + (int64_t)m * g.sam + kk)
+                                           : make_float4(0.f, 0.f, 0.f, 0.f);
+            } else {
+                ra[j] = kin && am < g.M ? *reinterpret_cast<const float4*>(g.A + (int64_t)k * g.sak + am)
+                                        : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
             if constexpr (CONV) {
                 const int q = (int)((uint32_t)k - div121((uint32_t)k) * 121u), y = div11(q), x = q - 11 * y;
                 const bool ok = kin && bn < g.N && (unsigned)(y + cdy) < 11u && (unsigned)(x + cdx) < 11u;
@@ -657,7 +672,7 @@ __global__ __launch_bounds__(256, 2) void tn3_kernel(evx_gemm_desc g, int klen, 
             }
         }
     };
-    auto put4 = [&](int pl, int row, float4 v) {  // 4 columns: hi into plane pl, lo into pl + 1 (8-B stores)
+    auto split4 = [](float4 v, uint2& hv, uint2& lv) {
         const float f[4] = {v.x, v.y, v.z, v.w};
         __bf16 hi[4], lo[4];
 #pragma unroll
@@ -665,8 +680,14 @@ __global__ __launch_bounds__(256, 2) void tn3_kernel(evx_gemm_desc g, int klen, 
             hi[e] = (__bf16)f[e];
             lo[e] = (__bf16)(f[e] - (float)hi[e]);
         }
-        *reinterpret_cast<uint2*>(&img[pl][row][sc]) = __builtin_bit_cast(uint2, hi);
-        *reinterpret_cast<uint2*>(&img[pl + 1][row][sc]) = __builtin_bit_cast(uint2, lo);
+        hv = __builtin_bit_cast(uint2, hi);
+        lv = __builtin_bit_cast(uint2, lo);
+    };
+    auto put4 = [&](int pl, int row, float4 v) {  // 4 columns: hi into plane pl, lo into pl + 1 (8-B stores)
+        uint2 hv, lv;
+        split4(v, hv, lv);
+        *reinterpret_cast<uint2*>(&img[pl][row][sc]) = hv;
+        *reinterpret_cast<uint2*>(&img[pl + 1][row][sc]) = lv;
     };
     const int q4 = (lane >> 2) & 3, pq = lane & 3;
     const int lane_off = (8 * h + q4) * T3P + 16 * ((lane >> 4) & 1) + 4 * pq;
@@ -674,7 +695,14 @@ __global__ __launch_bounds__(256, 2) void tn3_kernel(evx_gemm_desc g, int klen, 
     for (int k0 = kb; k0 < ke; k0 += T3K) {
 #pragma unroll
         for (int j = 0; j < 8; j++) {
-            put4(0, sr + 8 * j, ra[j]);
+            if constexpr (AK) {
+                uint2 hv, lv;
+                split4(ra[j], hv, lv);
+                *reinterpret_cast<uint2*>(&imga[0][akm + 16 * j][akk]) = hv;
+                *reinterpret_cast<uint2*>(&imga[1][akm + 16 * j][akk]) = lv;
+            } else {
+                put4(0, sr + 8 * j, ra[j]);
+            }
             put4(2, sr + 8 * j, rb[j]);
         }
         __syncthreads();
@@ -686,7 +714,10 @@ __global__ __launch_bounds__(256, 2) void tn3_kernel(evx_gemm_desc g, int klen, 
             for (int i = 0; i < 2; i++)
 #pragma unroll
                 for (int p = 0; p < 2; p++) {
-                    av[p][i] = tr_frag3(&img[p][0][0], lane_off, s * 16, wm * 64 + i * 32);
+                    if constexpr (AK)
+                        av[p][i] = *reinterpret_cast<const bf16x8*>(&imga[p][wm * 64 + i * 32 + (lane & 31)][s * 16 + 8 * h]);
+                    else
+                        av[p][i] = tr_frag3(&img[p][0][0], lane_off, s * 16, wm * 64 + i * 32);
                     bv[p][i] = tr_frag3(&img[2 + p][0][0], lane_off, s * 16, wn * 64 + i * 32);
                 }
 #pragma unroll
@@ -712,12 +743,23 @@ __global__ __launch_bounds__(256, 2) void tn3_kernel(evx_gemm_desc g, int klen, 
             const int tap = n / cs;
             col = (n - tap * cs) * 9 + tap;
         }
+        const bool epi = !CONV && gridDim.z == 1;  // one K pass: evx_gemm's epilogue here (else the reduction's)
+        const float bv = epi && g.bias ? g.bias[n] : 0.f;
 #pragma unroll
         for (int i = 0; i < 2; i++)
 #pragma unroll
             for (int r = 0; r < 16; r++) {
                 const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (m < g.M) out[(int64_t)m * ld + col] = acc[i][j][r];
+                if (m >= g.M) continue;
+                float x = acc[i][j][r];
+                if (epi) {
+                    x += bv;
+                    if (g.flags & EVX_GEMM_RELU) x = x > 0.f ? x : 0.f;
+                    if (g.mask) x = g.mask[(int64_t)m * g.ldm + n] ? x * g.mask_scale : 0.f;
+                    if (g.gate) x = g.gate[(int64_t)m * g.ldg + n] > 0.f ? x : 0.f;
+                    if (g.flags & EVX_GEMM_ACCUM) x += out[(int64_t)m * ld + col];
+                }
+                out[(int64_t)m * ld + col] = x;
             }
     }
 }
@@ -1655,15 +1697,22 @@ static bool conv_direct(const evx_gemm_desc* g, int mode, int cs, hipStream_t st
     return true;
 }
 
-// tn3_kernel's cases: x3, no epilogue, A m-contiguous (sam 1) and B n-contiguous (sbn 1) or the
-// conv dW gather (channels a multiple of 4), row strides and widths multiples of 4, 16-B aligned
-static bool tn3_ok(const evx_gemm_desc* g, int cm, int cs) {
-    if (g->precision != EVX_PREC_X3 || g->bias || g->mask || g->gate || g->flags || g->alpha != 1.f) return false;
+// tn3_kernel's cases: x3, alpha 1, B n-contiguous (sbn 1) or the conv dW gather (channels a multiple
+// of 4, no epilogue), A m- or k-contiguous, row strides and widths multiples of 4, 16-B aligned
+// returns 0 (not this kernel's case), 1 (A k-major: A[k][m], sam 1) or 2 (A k-contiguous: A[m][k], sak 1;
+// plain B only)
+static int tn3_ok(const evx_gemm_desc* g, int cm, int cs) {
+    if (g->precision != EVX_PREC_X3 || (g->flags & ~(EVX_GEMM_RELU | EVX_GEMM_ACCUM)) || g->alpha != 1.f) return 0;
+    if (cm == evxq::CV_DW && (g->bias || g->mask || g->gate || g->flags)) return 0;
     auto al16 = [](const float* p) { return ((uintptr_t)p & 15) == 0; };
-    if (g->sam != 1 || (g->sak & 3) || (g->M & 3) || !al16(g->A) || !al16(g->B)) return false;
-    if (g->K < 256) return false;
-    if (cm == evxq::CV_DW) return (cs & 3) == 0 && g->N == 9 * cs;
-    return cm == evxq::CV_NONE && g->sbn == 1 && (g->sbk & 3) == 0 && (g->N & 3) == 0;
+    if (!al16(g->A) || !al16(g->B) || g->K < 256) return 0;
+    const bool bplain = cm == evxq::CV_NONE && g->sbn == 1 && (g->sbk & 3) == 0 && (g->N & 3) == 0;
+    if (g->sam == 1 && (g->sak & 3) == 0 && (g->M & 3) == 0) {
+        if (cm == evxq::CV_DW) return (cs & 3) == 0 && g->N == 9 * cs ? 1 : 0;
+        return bplain ? 1 : 0;
+    }
+    if (g->sak == 1 && (g->sam & 3) == 0 && (g->K & 3) == 0 && bplain) return 2;
+    return 0;
 }
 int gemm_launch(const evx_gemm_desc* g, int cm, int cs, void* stream) {
     if (!g || !g->A || !g->B || !g->C) return qfail(-22, "gemm: NULL operand");
@@ -1677,16 +1726,20 @@ int gemm_launch(const evx_gemm_desc* g, int cm, int cs, void* stream) {
     hipStream_t st = (hipStream_t)stream;
     if ((cm == evxq::CV_FWD || cm == evxq::CV_DX) && S == 1 && conv_direct(g, cm, cs, st)) return qlaunch("conv3x3");
     if (g->flags & EVX_GEMM_OUT_SPLIT) return qfail(-22, "gemm: OUT_SPLIT needs the LDS-staged conv forward (and its workspace)");
-    if (tn3_ok(g, cm, cs)) {  // weight gradients with both f32 operands k-major (fc layers' dW, conv dW)
+    if (const int tk = tn3_ok(g, cm, cs)) {  // B k-major (weight gradients: fc and conv dW; activation gradients)
         {
             static std::atomic<uint64_t> attr_done;
-            const void* ks[2] = {(const void*)evxq::tn3_kernel<false>, (const void*)evxq::tn3_kernel<true>};
-            evxh::max_lds_once(attr_done, ks, 2, evxq::TN3_LDS);
+            const void* ks[3] = {(const void*)evxq::tn3_kernel<false>, (const void*)evxq::tn3_kernel<true>,
+                                 (const void*)evxq::tn3_kernel<false, true>};
+            evxh::max_lds_once(attr_done, ks, 3, evxq::TN3_LDS);
         }
-        if (cm == evxq::CV_DW)
-            hipLaunchKernelGGL(evxq::tn3_kernel<true>, grid, dim3(256), evxq::TN3_LDS, st, *g, klen, cs);
+        const dim3 tg = grid;
+        if (tk == 2)
+            hipLaunchKernelGGL((evxq::tn3_kernel<false, true>), tg, dim3(256), evxq::TN3_LDS, st, *g, klen, cs);
+        else if (cm == evxq::CV_DW)
+            hipLaunchKernelGGL(evxq::tn3_kernel<true>, tg, dim3(256), evxq::TN3_LDS, st, *g, klen, cs);
         else
-            hipLaunchKernelGGL(evxq::tn3_kernel<false>, grid, dim3(256), evxq::TN3_LDS, st, *g, klen, cs);
+            hipLaunchKernelGGL(evxq::tn3_kernel<false>, tg, dim3(256), evxq::TN3_LDS, st, *g, klen, cs);
     } else
     if (g->flags & EVX_GEMM_SPLIT_AB) {
         if (cm != evxq::CV_NONE || g->precision != EVX_PREC_X3 || g->sak != 1 || g->sbk != 1 || (g->K & 7) ||

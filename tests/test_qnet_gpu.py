@@ -240,6 +240,44 @@ def test_gemm_x3_k_major_operands_vs_float64(M, N, K, split):
     torch.testing.assert_close(C.cpu(), ref, rtol=1e-4, atol=2e-5 * ref.abs().max().item())
 
 
+@pytest.mark.parametrize("M,N,K,epi", [(1024, 1000, 512, "gate"), (300, 512, 256, "mask_gate"), (256, 640, 1000, "bias_relu"),
+                                       (96, 128, 4096, "accum")])
+def test_gemm_x3_k_contiguous_a_n_contiguous_b_vs_float64(M, N, K, epi):
+    """evx_gemm x3 with A[m][k] (sak 1) and B[k][n] (sbn 1) -- the fc layers' activation gradients
+    dX = dY W (tn3_kernel's k-contiguous A) -- with evx_gemm's epilogues (bias, ReLU, dropout mask x
+    scale, ReLU gate, accumulate), against float64."""
+    _need_gpu()
+    from evacx import qnet
+    g = torch.Generator().manual_seed(M * 3 + N + K)
+    A = torch.randn(M, K, generator=g)
+    Bm = torch.randn(K, N, generator=g)
+    C0 = torch.randn(M, N, generator=g)
+    bias = torch.randn(N, generator=g)
+    mask = (torch.rand(M, N, generator=g) < 0.8).to(torch.uint8)
+    gate = torch.randn(M, N, generator=g)
+    ref = A.double() @ Bm.double()
+    kw = {}
+    if "bias" in epi:
+        kw["bias"] = bias.cuda()
+        ref = ref + bias.double()
+    if "relu" in epi:
+        kw["relu"] = True
+        ref = ref.clamp_min(0)
+    if "mask" in epi:
+        kw.update(mask=mask.cuda(), ldm=N, mask_scale=1.25)
+        ref = torch.where(mask.bool(), ref * 1.25, torch.zeros_like(ref))
+    if "gate" in epi:
+        kw.update(gate=gate.cuda(), ldg=N)
+        ref = torch.where(gate > 0, ref, torch.zeros_like(ref))
+    if epi == "accum":
+        kw["accumulate"] = True
+        ref = ref + C0.double()
+    C = C0.clone().cuda()
+    qnet.gemm(M, N, K, A.cuda(), K, 1, Bm.cuda(), N, 1, C, N, "x3", **kw)
+    ref = ref.float()
+    torch.testing.assert_close(C.cpu(), ref, rtol=1e-4, atol=2e-5 * ref.abs().max().item())
+
+
 def test_conv_x3_act_and_learn_are_deterministic():
     """The conv Q-net in x3 at the cfg4 act's 8192 rows splits fc1 over K (256 tiles) and its
     learn splits the weight gradients: the K slices are summed in slice order (evx_gemm's
