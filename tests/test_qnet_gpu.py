@@ -278,6 +278,29 @@ def test_gemm_x3_k_contiguous_a_n_contiguous_b_vs_float64(M, N, K, epi):
     torch.testing.assert_close(C.cpu(), ref, rtol=1e-4, atol=2e-5 * ref.abs().max().item())
 
 
+@pytest.mark.parametrize("M,N,K,split", [(8192, 512, 15488, False), (300, 200, 1000, False), (256, 512, 6144, True)])
+def test_gemm_x3_split_ab_vs_float64(M, N, K, split):
+    """evx_gemm with EVX_GEMM_SPLIT_AB (A [2][M][K], B [2][N][K] bf16 hi / lo planes, k-contiguous: the
+    conv net's fc1 forward) with bias and ReLU, against float64 of the unsplit values;
+    cfg4's act shape (8192 x 512 x 15488), ragged tiles, and split-K."""
+    _need_gpu()
+    from evacx import qnet
+    g = torch.Generator().manual_seed(M + 7 * N + K)
+    A = torch.randn(M, K, generator=g)
+    Bm = torch.randn(N, K, generator=g) * 0.05
+    bias = torch.randn(N, generator=g)
+
+    def planes(x):
+        hi = x.to(torch.bfloat16)
+        lo = (x - hi.float()).to(torch.bfloat16)
+        return torch.stack([hi, lo]).view(torch.int16).cuda().contiguous()
+    C = torch.full((M, N), 5.0, device="cuda")
+    ws = torch.zeros(1 << 24, device="cuda") if split else None
+    qnet.gemm(M, N, K, planes(A), K, 1, planes(Bm), 1, K, C, N, "x3", bias=bias.cuda(), relu=True, ws=ws, split_ab=True)
+    ref = (A.double() @ Bm.double().t() + bias.double()).clamp_min(0).float()
+    torch.testing.assert_close(C.cpu(), ref, rtol=1e-4, atol=2e-5 * ref.abs().max().item())
+
+
 def test_conv_x3_act_and_learn_are_deterministic():
     """The conv Q-net in x3 at the cfg4 act's 8192 rows splits fc1 over K (256 tiles) and its
     learn splits the weight gradients: the K slices are summed in slice order (evx_gemm's
