@@ -565,6 +565,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(evx_gemm_desc g, int
     if (vec) {
         float4 a = *reinterpret_cast<const float4*>(g.ws + i0);
         v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+#pragma unroll 8
         for (int z = 1; z < S; z++) {
             const float4 b = *reinterpret_cast<const float4*>(g.ws + (int64_t)z * MN + i0);
             v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
@@ -778,6 +779,7 @@ __global__ __launch_bounds__(256) void splitk_reduce4_kernel(evx_gemm_desc g, in
     float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
     if (live) {
         a = *reinterpret_cast<const float4*>(g.ws + (int64_t)z0 * MN + i0);
+#pragma unroll 8  // 8 loads in flight; the adds stay in slice order (the same bits)
         for (int z = z0 + 1; z < z1; z++) {
             const float4 b = *reinterpret_cast<const float4*>(g.ws + (int64_t)z * MN + i0);
             a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
