@@ -823,6 +823,7 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ X
     const int rows = (M + chunks - 1) / chunks;
     const int r0 = c * rows, r1 = min(M, r0 + rows);
     float s = 0.f;
+#pragma unroll 8  // 8 loads in flight; the adds in row order (the same bits)
     for (int m = r0; m < r1; m++) s += X[(int64_t)m * ld + n];
     part[(int64_t)c * N + n] = s;
 }
@@ -831,6 +832,7 @@ __global__ __launch_bounds__(256) void colsum_finish(const float* __restrict__ p
     __shared__ float red[256];
     const int n = blockIdx.x, t = threadIdx.x;
     float s = 0.f;
+#pragma unroll 8
     for (int c = t; c < chunks; c += 256) s += part[(int64_t)c * N + n];
     red[t] = s;
     __syncthreads();
