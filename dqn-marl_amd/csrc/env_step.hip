@@ -3253,37 +3253,36 @@ __global__ __launch_bounds__(1024) void env_orders_push_kernel(const uint8_t* __
 template <typename T>
 __global__ __launch_bounds__(256) void obs_expand_kernel(evx_layout lay0, const evx_obs* __restrict__ obs, int64_t n,
                                                          T* __restrict__ out) {
+    // one thread per (row, window cell): the cell's six channels from one observation load and one
+    // cellinfo load, written as 6 consecutive values (was one thread per value)
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t total = n * 726;
-    if (gid >= total) return;
-    const int64_t o = gid / 726;
-    const int rem = (int)(gid - o * 726);
-    const int c = rem / 6, ch = rem - c * 6;
+    if (gid >= n * 121) return;
+    const int64_t o = gid / 121;
+    const int c = (int)(gid - o * 121);
     const int i = c / 11, j = c - i * 11;
     const evx_obs ob = obs[o];
     const evx_layout& lay = lay0.layout_set ? reinterpret_cast<const evx_layout*>(lay0.layout_set)[ob.layout] : lay0;
     const int mx = ob.cx + i - 5, my = ob.cy + j - 5;
     const int GY = lay.W + 2;
     const bool inb = mx >= 0 && mx <= lay.L + 1 && my >= 0 && my <= lay.W + 1;
-    const bool valid = mx >= 1 && mx <= lay.L && my >= 1 && my <= lay.W && (lay.cellinfo[mx * GY + my] & 1u);
-    T v = 0;
-    if (ch == 1) {
-        v = ((ob.occ[c >> 5] >> (c & 31)) & 1u) ? (T)1 : (T)0;
-    } else if (ch == 2) {
-        const int ti = mx - lay.ox0, tj = my - lay.oy0;
-        if (ti >= 0 && ti < lay.OX && tj >= 0 && tj < lay.OY) {
-            const size_t idx = ((size_t)ob.fire_step * lay.OX + ti) * lay.OY + tj;
-            if constexpr (sizeof(T) == 8) v = (T)lay.danger_o[idx];
-            else v = (T)lay.danger_o32[idx];
-        }
-    } else if (ch == 3) {
-        v = (!valid || (inb && ((lay.cellinfo[mx * GY + my] >> 2) & 1u))) ? (T)1 : (T)0;
-    } else if (ch == 4) {
-        v = (mx == lay.exit_x && my == lay.exit_y) ? (T)1 : (T)0;
-    } else if (ch == 5) {
-        v = (i == 5 && j == 5) ? (T)1 : (T)0;
+    const uint8_t ci = inb ? lay.cellinfo[mx * GY + my] : (uint8_t)0;
+    const bool valid = mx >= 1 && mx <= lay.L && my >= 1 && my <= lay.W && (ci & 1u);
+    T v[6];
+    v[0] = 0;
+    v[1] = ((ob.occ[c >> 5] >> (c & 31)) & 1u) ? (T)1 : (T)0;
+    v[2] = 0;
+    const int ti = mx - lay.ox0, tj = my - lay.oy0;
+    if (ti >= 0 && ti < lay.OX && tj >= 0 && tj < lay.OY) {
+        const size_t idx = ((size_t)ob.fire_step * lay.OX + ti) * lay.OY + tj;
+        if constexpr (sizeof(T) == 8) v[2] = (T)lay.danger_o[idx];
+        else v[2] = (T)lay.danger_o32[idx];
     }
-    out[gid] = v;
+    v[3] = (!valid || (inb && ((ci >> 2) & 1u))) ? (T)1 : (T)0;
+    v[4] = (mx == lay.exit_x && my == lay.exit_y) ? (T)1 : (T)0;
+    v[5] = (i == 5 && j == 5) ? (T)1 : (T)0;
+    T* dst = out + o * 726 + c * 6;
+#pragma unroll
+    for (int ch = 0; ch < 6; ch++) dst[ch] = v[ch];
 }
 
 }  // namespace evx
@@ -3600,7 +3599,7 @@ int evx_obs_expand_f32(const evx_layout* l, const evx_obs* obs, int64_t n, float
     if (!l->danger_o32) return fail(-22, "danger_o32 missing");
     if (n <= 0) return 0;
     const int64_t total = n * 726;
-    hipLaunchKernelGGL(evx::obs_expand_kernel<float>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+    hipLaunchKernelGGL(evx::obs_expand_kernel<float>, dim3((unsigned)((total / 6 + 255) / 256)), dim3(256), 0,
                        (hipStream_t)stream, *l, obs, n, out);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : hip_fail(e, "obs_expand launch");
@@ -3611,7 +3610,7 @@ int evx_obs_expand_f64(const evx_layout* l, const evx_obs* obs, int64_t n, doubl
     if (rc) return rc;
     if (n <= 0) return 0;
     const int64_t total = n * 726;
-    hipLaunchKernelGGL(evx::obs_expand_kernel<double>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+    hipLaunchKernelGGL(evx::obs_expand_kernel<double>, dim3((unsigned)((total / 6 + 255) / 256)), dim3(256), 0,
                        (hipStream_t)stream, *l, obs, n, out);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : hip_fail(e, "obs_expand launch");
