@@ -70,6 +70,36 @@ def qnet_flops(n_act, B, hidden=512, in_dim=484, actions=5):
     return n_act * fwd + B * (2 * fwd + bwd)
 
 
+def learn_flops_executed(B, tab_on, tab_tg, stat_rows, hidden=512, in_dim=484, occ=121, actions=5):
+    """f32-equivalent FLOPs the fused learn chain EXECUTES for one learn step (csrc/qmlp.hip): a forward
+    row whose fc1 starts from the per-centre act table (tab_on / tab_tg: the fraction of the batch's
+    online / target rows that take it) contracts only fc1's 121 occupancy inputs, the others all 484;
+    fc2, fc3 for every row; the backward dW3 + dH2, dW2 + dH1 and dW1 over all 484 inputs (no dX for
+    the input layer); and the rebuild of the online net's table after the update (stat_rows centres x
+    the full fc1 at zero occupancy)."""
+    h2 = hidden // 2
+    fc23 = hidden * h2 + h2 * actions
+    row = lambda frac: frac * 2 * (occ * hidden + fc23) + (1 - frac) * 2 * (in_dim * hidden + fc23)  # noqa: E731
+    bwd = 2 * (2 * h2 * actions + 2 * hidden * h2 + in_dim * hidden)
+    return B * (row(tab_on) + row(tab_tg) + bwd) + stat_rows * 2 * in_dim * hidden
+
+
+def counter_record(kind, phase, per_launch, L, P, R):
+    """The newest SQ counter record (tools/env_counters.py via tools/gpu_r6_counters.sh) of env_step_kernel
+    on exactly this workload: phase, envs per launch, grid, people and robots."""
+    for r in ("r6",):
+        for q in sorted(glob.glob(os.path.join(ROOT, "profiles", r, f"{kind}_*.json"))):
+            try:
+                rec = json.load(open(q))
+            except (OSError, ValueError):
+                continue
+            if (rec.get("kernel") == "env_step_kernel" and rec.get("phase") == phase and rec.get("envs") == per_launch
+                    and rec.get("grid") == [L, L] and rec.get("people") == P and rec.get("robots") == R
+                    and rec.get("sq_insts_valu_per_wave") and rec.get("clock_ghz")):
+                return rec, os.path.relpath(q, ROOT)
+    return None, None
+
+
 def cfg_name(args):
     """BASELINE.json configs: cfg2 64x64 x 8 robots, cfg3 128x128 x 16 (the headline), cfg4
     256x256 conv Q-net, cfg5 128x128 x 32 with prioritized replay."""
@@ -141,7 +171,8 @@ def parse():
                          "(evacx.trainer._Group): one group's env.step tail overlaps the others' work")
     ap.add_argument("--traffic", default=None,
                     help="PMC traffic record of env_step_kernel on this workload and phase (tools/parse_prof.py); "
-                         "default profiles/r4/ (else r3/, r2/) env_traffic_<phase>.json")
+                         "default: the newest profiles/r*/ env_counters_<phase>*.json or env_traffic_<phase>*.json "
+                         "record of this workload")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.envs_total > 0:
@@ -368,6 +399,23 @@ def main():
         torch.cuda.synchronize()
         tr.learner.grad_hook = hook_saved
         learn_alone_ms = float(np.mean([ev_l[i][0].elapsed_time(ev_l[i][1]) for i in range(1, 6)]))
+    # which forward rows of the learn batch start fc1 from an act table (the fused act kernel's table
+    # path: the online / target forwards at B >= 32768, rows at the layout's last fire step, whole
+    # 64-row tiles), from the last drawn batch -- for the executed-FLOP basis of roofline_learn
+    learn_tab = None
+    if args.mode == "train" and tr.fast is not None and tr.learner is not None and not tr.per_robot:
+        st = getattr(tr.fast, "_static", None)
+        stat_rows = int(st[1].shape[0]) if st is not None else 0
+        fr = [0.0, 0.0]
+        if st is not None and args.batch >= 32768:
+            t_max = int(tr.lay.c.t_max)
+            for i, key in enumerate(("s", "s2")):
+                fs = tr.samp[key].view(-1, 8)[:args.batch, 6]
+                tile_all = (fs >= t_max).view(-1, 64).all(dim=1) if args.batch % 64 == 0 else None
+                fr[i] = float(tile_all.float().mean().item()) if tile_all is not None else 0.0
+            if getattr(tr.learner, "fast_t", None) is None or getattr(tr.learner.fast_t, "_static", None) is None:
+                fr[1] = 0.0
+        learn_tab = (fr[0], fr[1], stat_rows)
 
     # ---------- BASELINE configs[2] read as envs for the whole job (extra, N > 1 only)
     total = None
@@ -397,10 +445,10 @@ def main():
         except (OSError, ValueError):
             return False
         return (rec.get("kernel") == "env_step_kernel" and rec.get("envs") in (None, per_launch)
-                and rec.get("grid", [L, W]) == [L, W])
-    tpath = args.traffic or next((q for r in ("r5", "r4", "r3", "r2")
-                                  for q in sorted(glob.glob(os.path.join(ROOT, "profiles", r,
-                                                                         f"env_traffic_{args.phase}*.json")))
+                and rec.get("grid", [L, W]) == [L, W] and rec.get("people", P) == P and rec.get("robots", R) == R)
+    tpath = args.traffic or next((q for r in ("r6", "r5", "r4", "r3", "r2")
+                                  for pat in (f"env_counters_{args.phase}*.json", f"env_traffic_{args.phase}*.json")
+                                  for q in sorted(glob.glob(os.path.join(ROOT, "profiles", r, pat)))
                                   if traffic_match(q)), "")
     if os.path.exists(tpath):
         # HBM bytes per launch from rocprofv3 PMC passes of this same workload and phase
@@ -412,6 +460,41 @@ def main():
             traffic = rec.get("bytes_per_env_step_raw", rec["bytes_per_env_step"]) * per_launch
             traffic_corr = rec["bytes_per_env_step"] * per_launch
             traffic_src = os.path.relpath(tpath, ROOT)
+    # the issue roofline of the same kernel: VALU + SALU instructions per wave x waves
+    # per launch (SQ_INSTS_VALU / SQ_INSTS_SALU / SQ_WAVES, one --pmc pass of this workload) against one
+    # instruction per SIMD per cycle (256 CUs x 4 SIMDs x the clock the GRBM pass measured) over the
+    # launch time measured here; valu_pipe_frac prices a wave64 VALU at 2 cycles of its SIMD-32
+    # (MI355X_MICROARCH.md, cycle constants)
+    roof_hbm = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                "traffic_basis": "raw FETCH_SIZE + WRITE_SIZE bytes per launch (PMC)",
+                "traffic_fetch_x2": traffic_corr,
+                "frac_traffic": (traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
+                "frac_basis": "algorithmic bytes (bytes_per_env_step x env-steps per launch) / kernel_ms / peak; "
+                              "frac_traffic: the PMC bytes the kernel actually moved, same time",
+                "kernel": "env_step_kernel", "kernel_ms": kern_ms, "bytes_per_env_step": bpe,
+                "env_steps_per_launch": per_launch,
+                "launches_timed": len([s for s in range(args.steps) if s % EV_EVERY == 0])}
+    roof_issue = None
+    srec, ssrc = counter_record("env_counters", args.phase, per_launch, L, P, R)
+    if srec is not None:
+        waves = srec["waves"]
+        insts = (srec["sq_insts_valu_per_wave"] + srec["sq_insts_salu_per_wave"]) * waves
+        clk = srec["clock_ghz"] * 1e9
+        t = kern_ms * 1e-3
+        roof_issue = {"bound": "issue", "achieved": insts / t / 1e9, "peak": 1024 * clk / 1e9, "unit": "Ginst/s",
+                      "frac": insts / (1024 * clk * t),
+                      "valu_pipe_frac": srec["sq_insts_valu_per_wave"] * waves * 2 / (1024 * clk * t),
+                      "valu_per_wave": srec["sq_insts_valu_per_wave"], "salu_per_wave": srec["sq_insts_salu_per_wave"],
+                      "waves_per_launch": waves, "clock_ghz": srec["clock_ghz"], "kernel_ms": kern_ms,
+                      "sq_active_inst_any_frac": srec.get("sq_active_inst_any_frac"),
+                      "sq_wait_any_frac": srec.get("sq_wait_any_frac"), "source": ssrc,
+                      "basis": "(VALU + SALU instructions per wave) x waves / (256 CUs x 4 SIMDs x clock x kernel_ms): "
+                               "one instruction per SIMD per cycle"}
+    # the binding roof: the larger of the measured-traffic HBM fraction and the issue fraction
+    roof = roof_hbm
+    if roof_issue is not None and roof_issue["frac"] > (roof_hbm["frac_traffic"] or 0.0):
+        roof = dict(roof_issue, traffic=traffic, traffic_source=traffic_src)
     cpu = None
     if cpu_snap is not None:
         cpu = cpu_baseline(cpu_snap, env.lay.R, lay_tables, P, args, E)
@@ -473,24 +556,31 @@ def main():
                              "that follows the timed steps)",
             "learn_alone_ms": learn_alone_ms,
             "last_loss": loss,
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                         "traffic_basis": "raw FETCH_SIZE + WRITE_SIZE bytes per launch (PMC)",
-                         "traffic_fetch_x2": traffic_corr,
-                         "frac_traffic": (traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
-                         "kernel": "env_step_kernel", "kernel_ms": kern_ms, "bytes_per_env_step": bpe,
-                         "env_steps_per_launch": per_launch,
-                         "launches_timed": len([s for s in range(args.steps) if s % EV_EVERY == 0])},
+            "roofline": roof,
+            "roofline_hbm": roof_hbm,
+            "roofline_issue": roof_issue,
+            "roofline_binding": ("the larger of roofline_hbm.frac_traffic (PMC bytes moved) and roofline_issue.frac "
+                                 "(SQ instruction counts) on this workload; roofline_hbm.frac is on the "
+                                 "algorithmic bytes") if roof_issue is not None else "no SQ record for this workload",
             "cpu_baseline": cpu,
         }
         lm = learn_alone_ms if learn_alone_ms is not None else learn_ms
-        if lm is not None and args.qnet == "mlp":
-            fl = qnet_flops(0, args.batch)
+        if lm is not None and args.qnet == "mlp" and learn_tab is not None:
+            fl = learn_flops_executed(args.batch, *learn_tab)
+            fd = qnet_flops(0, args.batch)
             line["roofline_learn"] = {"bound": "mfma", "achieved": fl / (lm * 1e-3) / 1e12,
                                       "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                                       "frac": fl / (lm * 1e-3) / 1e12 / BF16_PEAK_TFLOPS, "learn_ms": lm,
-                                      "flops_basis": "dense f32-equivalent FLOPs of one learn step (B rows, timed "
-                                                     "alone, no all-reduce)"}
+                                      "flops": fl, "flops_dense": fd,
+                                      "frac_dense": fd / (lm * 1e-3) / 1e12 / BF16_PEAK_TFLOPS,
+                                      "table_rows": {"online": learn_tab[0], "target": learn_tab[1],
+                                                     "rebuild_centres": learn_tab[2]},
+                                      "flops_basis": "f32-equivalent FLOPs the learn chain executes (learn_flops_executed: "
+                                                     "fc1 over the 121 occupancy inputs for rows that start from the act "
+                                                     "table, 484 otherwise, plus the table rebuild); frac_dense: every "
+                                                     "row over all 484 inputs, no rebuild. B rows, timed alone, no "
+                                                     "all-reduce. The x3 arithmetic issues 2-3 bf16 MFMA products per "
+                                                     "f32 product"}
         print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()

@@ -3036,17 +3036,23 @@ __global__ __launch_bounds__(1024) void env_order_kernel(evx_layout lay, evx_sta
 // kernels write an env's byte as they finish with it, so the orders of the next step need no pass
 // over the state (evx_env_classes rewrites every byte from the state words, for states written
 // from the host).
+// Each env's byte is computed against its own layout (a layout set: its entry), as the step and
+// reset kernels write it.
 __global__ __launch_bounds__(256) void env_classes_kernel(evx_layout lay, evx_state st) {
     const int e = (int)blockIdx.x * 256 + (int)threadIdx.x;
     if (e >= st.E) return;
     const int4 v = *reinterpret_cast<const int4*>(st.scal + (size_t)e * 4);
-    st.perm_ws[e] = env_class(lay, v.x, v.z, v.w);
+    const evx_layout* le = &lay;
+    if (lay.layout_set && st.layout_idx) le = reinterpret_cast<const evx_layout*>(lay.layout_set) + st.layout_idx[e];
+    st.perm_ws[e] = env_class(*le, v.x, v.z, v.w);
 }
 // One launch, workgroup c ranking the envs [1024 c, 1024 c + 1024) (stable: env order within a
 // class):
 //   order[0, E): the envs by bucket (most persons remaining first), order[E] = min(hcap, heavy);
 //   perm[0, E): the envs at fire step >= t_max first, then the rest.
-// Either output may be NULL. Every workgroup counts the classes of all E envs (one byte each, L2)
+// Either output may be NULL. The class bytes are read more than once (the counts, then the ranks):
+// this launch must not overlap a step or reset of the same envs (VecEnv.compute_order(ahead=True)
+// runs env_order_kernel instead, which reads each env's counters once). Every workgroup counts the classes of all E envs (one byte each, L2)
 // itself -- the totals set where each class starts, the chunks before c where this chunk's run of
 // it starts -- so no second launch or workspace carries counts between workgroups. Per 64 envs a
 // wave takes 7 ballots (4 bucket bits, valid, fire, heavy); lane k < 16 counts bucket k as the AND

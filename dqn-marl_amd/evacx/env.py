@@ -457,7 +457,14 @@ class VecEnv:
         whole workgroup each (scheduling only; the results do not depend on it). Small
         batches keep the identity order unless forced (tests). ahead=True: fill the other
         order buffer, for the step after the next one, from the state as it is when the
-        kernel runs (it may overlap the next step, which reads the current buffer)."""
+        kernel runs (it may overlap the next step, which reads the current buffer).
+
+        The default form ranks the class bytes the last step / reset wrote (evx_state.perm_ws),
+        reading each byte more than once, so it must not overlap a step or reset of these envs.
+        ahead=True therefore clears perm_ws in its copy of the state: evx_env_order then takes the
+        one-workgroup kernel, which reads every env's counters from the state words ONCE into LDS
+        and so yields a permutation even while a step rewrites them. After writing evx_state.scal
+        from the host, call refresh_classes() before the next compute_order() / compute_orders()."""
         if self._parts:
             for p in self._parts:
                 p.compute_order(force=force, ahead=ahead)
@@ -468,6 +475,7 @@ class VecEnv:
         if ahead:
             c = _lib.evx_state.from_buffer_copy(self.c)
             c.order = _ptr(self._orders[self._ord ^ 1])
+            c.perm_ws = None  # one read per env (env_order_kernel's LDS snapshot), see above
             self._order_ahead = True
         _lib.check(_lib.lib().evx_env_order(C.byref(self.lay.c), C.byref(c), _stream()), "evx_env_order")
 

@@ -215,6 +215,42 @@ def test_groups_match_one_group():
         assert (a[k] == b[k]) if k == "drop" else torch.equal(a[k], b[k]), k
 
 
+def test_groups_greedy_act_matches_one_group():
+    """The x3 act's table path with per-group env orders (grp.perm, a slice of the trainer's
+    permutation, rows_per_env = R) at epsilon 0, so the actions are the argmax of the act's Q:
+    every env at the layout's last fire step (every tile takes the table path, where a row's Q
+    does not depend on the tile it shares), G = 2 against G = 1 from the same seeds -- the
+    greedy actions are identical and depend on the Q values (not all one action). A wrong perm
+    slice or row offset in a group would move Q values between robots."""
+    _need_gpu()
+    from evacx.env import DeviceLayout
+    from evacx.layout import build_tables, synthetic
+    from evacx.trainer import VecTrainer
+    lay = DeviceLayout(build_tables(synthetic(128, 128, 16)), 2276)
+    t_max = int(lay.c.t_max)
+    acts = []
+    for G in (1, 2):
+        tr = VecTrainer(lay, 2048, batch=2048, replay_capacity=1 << 16, epsilon=0.0, epsilon_min=0.0,
+                        epsilon_decay=1.0, groups=G)
+        env = tr.env
+        assert tr.fast is not None
+        env.scal.view(env.E, 4)[:, 0] = t_max
+        env.obs.view(-1, 8)[:, 6] = t_max
+        env.refresh_classes()
+        for grp in tr.groups:
+            grp.env.compute_orders(perm=grp.perm)
+        torch.cuda.synchronize()
+        tr.act()
+        tr.sync()
+        torch.cuda.synchronize()
+        acts.append(tr.actions.clone())
+        del tr, env
+        torch.cuda.empty_cache()
+    assert torch.equal(acts[0], acts[1])
+    counts = torch.bincount(acts[0].long(), minlength=5)
+    assert int((counts > 0).sum()) >= 2, counts
+
+
 @pytest.mark.gpu
 def test_fused_push_orders_sample_matches_separate_launches():
     """The one-group strict step draws its learn batch in the replay push + orders launch
