@@ -36,6 +36,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "evacx.h"
 #include "evx_host.h"
@@ -44,6 +45,8 @@ namespace evxm {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 constexpr int HID = 512, HID2 = 256, NACT = 5, K1 = 726, NCELL = 121;
 // fc1's compact K: 4 features per cell (occ, danger, barrier, exit = the reference's
@@ -184,7 +187,8 @@ struct Fwd {
 __device__ __forceinline__ int orow(const Fwd& a, int row) {
     int r = row;
     if (a.perm) {
-        const int s = row / a.rpe;
+        // rows_per_env a power of two (the trainer's R): a shift instead of a 32-bit division
+        const int s = (a.rpe & (a.rpe - 1)) == 0 ? row >> (__builtin_ffs(a.rpe) - 1) : row / a.rpe;
         r = a.perm[s] * a.rpe + (row - s * a.rpe);
     }
     return a.gn ? r * a.gn + a.g : r;
@@ -708,7 +712,7 @@ __device__ __forceinline__ void fc3t_x3(const Fwd& a, const f32x16 (&acc)[MT][2]
     }
     // qp[mt] = this wave's Q^T partial: lane l holds tile row 32 mt + (l & 31), actions
     // 4 (l >> 5) + r (r < 4; valid below NACT)
-    auto R = reinterpret_cast<float (*)[NACT][64]>(red);  // [4][NACT][64]
+    auto R = reinterpret_cast<float (*)[NACT][32 * MT]>(red);  // [4][NACT][32 MT]
 #pragma unroll
     for (int mt = 0; mt < MT; mt++)
 #pragma unroll
@@ -724,6 +728,103 @@ __device__ __forceinline__ void fc3t_x3(const Fwd& a, const f32x16 (&acc)[MT][2]
 #pragma unroll
             for (int k = 0; k < NACT; k++) qv[k] = ((R[0][k][tid] + R[1][k][tid]) + R[2][k][tid]) + R[3][k][tid];
             q_out(a, qv, act_rows ? orow(a, rt) : rt);
+        }
+    }
+}
+
+// fc3t_x3 for qact3p_kernel's 8 waves, in two parts. fc3p_partials: wave (column group cg, row half
+// at r0) holds the H2^T tiles of fc2 columns 64 cg .. + 63 for rows r0 .. r0 + 63 (acc[mt][nt] as
+// fc3t_x3's); H2 = relu(acc + b2) (b2 from LDS), and its Q^T partials (x3 MFMAs against W3, as
+// fc3t_x3) go to red [4][NACT][128] by column group. fc3p_rows (after a barrier): thread t < 128 adds
+// row t's partials in column-group order -- as fc3t_x3 adds its 4 waves' (the same bits) -- and runs
+// DQNAgent.act's epsilon-greedy (q_out).
+__device__ __forceinline__ void fc3p_partials(const f32x16 (&acc)[2][2], const float (*W3s)[HID2], const float* b2s,
+                                              float* red, int cg, int r0, int lane) {
+    const int h = lane >> 5, j = lane & 31;
+    const int t = lane & 31;
+    f32x16 qp[2];
+#pragma unroll
+    for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+        for (int r = 0; r < 16; r++) qp[mt][r] = 0.f;
+#pragma unroll
+    for (int nt = 0; nt < 2; nt++) {
+        const int nb = cg * 64 + nt * 32 + 4 * h;  // + (r & 3) + 8 (r >> 2)
+        float b2v[16];
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            const float4 bv = *reinterpret_cast<const float4*>(&b2s[nb + 8 * g]);
+            b2v[4 * g] = bv.x;
+            b2v[4 * g + 1] = bv.y;
+            b2v[4 * g + 2] = bv.z;
+            b2v[4 * g + 3] = bv.w;
+        }
+        bf16x8 wh[2], wl[2];
+#pragma unroll
+        for (int kb = 0; kb < 2; kb++) {
+            float u[8];
+            if (t < NACT) {
+                const float4 u0 = *reinterpret_cast<const float4*>(&W3s[t][nb + 16 * kb]);
+                const float4 u1 = *reinterpret_cast<const float4*>(&W3s[t][nb + 16 * kb + 8]);
+                u[0] = u0.x; u[1] = u0.y; u[2] = u0.z; u[3] = u0.w;
+                u[4] = u1.x; u[5] = u1.y; u[6] = u1.z; u[7] = u1.w;
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; e++) u[e] = 0.f;
+            }
+#pragma unroll
+            for (int e = 0; e < 8; e++) {
+                __bf16 hi, lo;
+                split2(u[e], hi, lo);
+                wh[kb][e] = hi;
+                wl[kb][e] = lo;
+            }
+        }
+#pragma unroll
+        for (int mt = 0; mt < 2; mt++) {
+            float v[16];
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const float x = acc[mt][nt][r] + b2v[r];
+                v[r] = x > 0.f ? x : 0.f;
+            }
+#pragma unroll
+            for (int kb = 0; kb < 2; kb++) {
+                bf16x8 bh, bl;
+#pragma unroll
+                for (int e = 0; e < 8; e++) {
+                    __bf16 hi, lo;
+                    split2(v[8 * kb + e], hi, lo);
+                    bh[e] = hi;
+                    bl[e] = lo;
+                }
+                qp[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh[kb], bh, qp[mt], 0, 0, 0);
+                qp[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh[kb], bl, qp[mt], 0, 0, 0);
+                qp[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl[kb], bh, qp[mt], 0, 0, 0);
+            }
+        }
+    }
+    auto R = reinterpret_cast<float (*)[NACT][128]>(red);  // [4][NACT][128]
+#pragma unroll
+    for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int act = 4 * h + r;
+            if (act < NACT) R[cg][act][r0 + mt * 32 + j] = qp[mt][r];
+        }
+}
+// rows spread over waves 0..3 (32 each, lanes 0..31: one wave per SIMD) -- q_out's epsilon draw is a
+// 10-round Philox per row, and two waves carrying all 128 rows held the next slot back
+__device__ __forceinline__ void fc3p_rows(const Fwd& a, const float* red, int m0) {
+    const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+    auto R = reinterpret_cast<const float (*)[NACT][128]>(red);
+    if (w < 4 && l < 32) {
+        const int r = 32 * w + l, rt = m0 + r;
+        if (rt < a.N) {
+            float qv[NACT];
+#pragma unroll
+            for (int k = 0; k < NACT; k++) qv[k] = ((R[0][k][r] + R[1][k][r]) + R[2][k][r]) + R[3][k][r];
+            q_out(a, qv, orow(a, rt));
         }
     }
 }
@@ -910,12 +1011,11 @@ constexpr int ACT3H_LDS = A3H_HBYTES + NACT * HID2 * 4 + 64 * 4 + 64 * 8 + ACT3_
 // SAVE: the learner's online forward (evx_qmlp_forward2 at B >= 32768 with the online net's act
 // table): the tables' tiles start fc1 from it like the act, each half's H1 planes go to a.h1 /
 // a.h1l for the backward, H2 to a.h2 and Q to a.q by batch row; X is written by x_expand_kernel.
-template <bool GR = false, int DM = 1, bool SAVE = false>
-__global__ __launch_bounds__(256, 2) void qact3h_kernel(Fwd a0) {
-    Fwd ag;
-    if constexpr (GR) ag = fwd_net(a0, (int)blockIdx.y);
-    const Fwd& a = GR ? ag : a0;
-    extern __shared__ __attribute__((aligned(16))) char dsm[];
+// One 64-row tile [m0, m0 + 64) on the workgroup's 4 waves (256 threads), LDS at dsm (ACT3H_LDS
+// bytes): the body of qact3h_kernel, and the fallback of the persistent act (qact3p_kernel) for
+// tiles that cannot take the table path.
+template <int DM = 1, bool SAVE = false>
+__device__ __forceinline__ void act3h_tile(const Fwd& a, char* dsm, const int m0) {
     auto Hh = reinterpret_cast<__bf16 (*)[A3_HP]>(dsm);
     auto Hl = reinterpret_cast<__bf16 (*)[A3_HP]>(dsm + 64 * A3_HP * 2);
     auto W3s = reinterpret_cast<float (*)[HID2]>(dsm + A3H_HBYTES);
@@ -923,7 +1023,6 @@ __global__ __launch_bounds__(256, 2) void qact3h_kernel(Fwd a0) {
     uint32_t* phS = reinterpret_cast<uint32_t*>(dsm + A3H_HBYTES + NACT * HID2 * 4 + 64 * 4);
     uint4* occT = reinterpret_cast<uint4*>(dsm + A3H_HBYTES + NACT * HID2 * 4 + 64 * 4 + 64 * 8);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
-    const int m0 = blockIdx.x * 64;
     ACT_ST(0);
     for (int i = tid; i < NACT * HID2; i += 256) W3s[i / HID2][i % HID2] = a.w3[i];
     if (DM == 1 && tid >= 224) {  // the tile's 32 row-pair dropout hashes (published by the barriers below)
@@ -1078,6 +1177,385 @@ __global__ __launch_bounds__(256, 2) void qact3h_kernel(Fwd a0) {
     ACT_ST(10);
     fc3t_x3(a, acc2, W3s, reinterpret_cast<float*>(dsm), m0, !SAVE);
     ACT_ST(11);
+}
+template <bool GR = false, int DM = 1, bool SAVE = false>
+__global__ __launch_bounds__(256, 2) void qact3h_kernel(Fwd a0) {
+    Fwd ag;
+    if constexpr (GR) ag = fwd_net(a0, (int)blockIdx.y);
+    const Fwd& a = GR ? ag : a0;
+    extern __shared__ __attribute__((aligned(16))) char dsm[];
+    act3h_tile<DM, SAVE>(a, dsm, (int)blockIdx.x * 64);
+}
+
+// ------------------------------------------------------------ persistent x3 act
+// DQNAgent.act (agents/dqn_agent.py:101-124), f32-accurate, for 128-row tiles on one 4-wave
+// workgroup per CU (one wave per SIMD, up to 512 registers), workgroup b looping over tiles b,
+// b + grid, ...: fc1's occupancy weights and fc2's weights (hi + lo) are streamed from L2 once per
+// 128 rows instead of once per 64 (act3h_tile moved ~14 KB of weights and table per row), and the
+// fc1 epilogue runs under fc2's MFMAs instead of beside another workgroup's. fc1 -> H1 -> fc2 goes
+// in quarters of fc1's 512 columns:
+//   slot q (0..3): fc1 of quarter q (the table row of every row's window centre + the occupancy
+//     columns x bits; wave w on columns 128 q + 32 w, all 128 rows), then fc2's accumulation over
+//     quarter q - 1's 128 K (wave w: fc2 columns 64 w .. 64 w + 63, all 128 rows) from one LDS
+//     buffer with quarter q's epilogue (ReLU, dropout, hi / lo split) writing the other buffer
+//     between its MFMAs; one barrier per slot;
+//   slot 4: fc2 over quarter 3, then fc3 + epsilon-greedy (fc3t_x3).
+// The table loads of quarter q + 1 are issued in slot q after the weight loads that fc1 waits on
+// (vmcnt counts loads in issue order). Per element the same products in the same order as
+// act3h_tile: Q and actions are bit-identical to the 64-row kernel (tests/test_qmlp_x3_gpu.py).
+// H1 of a quarter is stored transposed, H1^T [128 k][128 rows] bf16 per plane (256-B rows, 8-B
+// pieces XOR-swizzled by h1t_swz): the epilogue writes 4 consecutive rows of a column per
+// ds_write_b64 (16 lanes = 16 k rows: distinct banks), and fc2 reads its B operand (rows x 8 k) with
+// ds_read_b64_tr_b16 (4 k rows x 64 B per 32 lanes: distinct banks). A tile with a row off the table
+// path (fire step < the table's, or a centre outside it) runs act3h_tile on its two halves.
+typedef const __attribute__((address_space(1))) char gbyte;  // global-memory views (explicit: the
+typedef const __attribute__((address_space(1))) float gfloat;  // bases pass through asm, which would
+typedef const __attribute__((address_space(1))) bf16x8 gbf16x8;  // leave generic pointers -> flat loads)
+constexpr int A3P_PL = 128 * 128;                      // bf16 elements of one H1^T plane
+constexpr int A3P_HB = 2 * 2 * A3P_PL * 2;             // 2 buffers x (hi, lo) planes: 131,072 B
+constexpr int A3P_W3 = A3P_HB;                         // W3, f32 [5][256]
+constexpr int A3P_RED = A3P_W3 + NACT * HID2 * 4;      // fc3t_x3's partials [4][5][128] f32
+constexpr int A3P_POS = A3P_RED + 4 * NACT * 128 * 4;  // table row of each tile row [2][128] (this / next tile)
+constexpr int A3P_PH = A3P_POS + 2 * 128 * 4;          // row-pair dropout hashes [2][64]
+constexpr int A3P_OCC = A3P_PH + 2 * 64 * 4;           // occupancy-fragment table [256] uint4
+constexpr int A3P_B2 = A3P_OCC + 256 * 16;             // fc2.bias f32 [256]
+constexpr int ACT3P_LDS = A3P_B2 + HID2 * 4;           // 153,088 B: one workgroup per CU
+static_assert(ACT3P_LDS <= 160 * 1024 && ACT3H_LDS <= A3P_HB, "LDS: the fallback tile lives in the H1 buffers");
+// H1^T row k: XOR on the dword index of its 8-B pieces -- bits 4-5 <- k & 3 (the 4 k rows of a
+// transposed read in distinct 16-bank blocks), bits 1-3 <- (k >> 1) & 7 (with bit 4 = k & 1: the 16
+// consecutive k rows of a ds_write_b64 lane group in distinct bank pairs)
+__device__ __forceinline__ int h1t_swz(int k) { return ((k & 3) << 4) | (((k >> 1) & 7) << 1); }
+// bf16 offset of rows r .. r + 3 (r a multiple of 4) in H1^T row k
+__device__ __forceinline__ int h1t_off(int k, int r) { return k * 128 + 2 * ((r >> 1) ^ h1t_swz(k)); }
+
+// diagnostic build (-DEVX_ACT_STAMPS, tools/act3p_stamps.py): wave 0's s_memtime at the slot
+// boundaries of every tile of every workgroup (evx_diag_act3p_stamps)
+#ifdef EVX_ACT_STAMPS
+constexpr int A3P_NST = 16, A3P_MAXIT = 32;
+__device__ long long g_act3p_st[256 * A3P_MAXIT * A3P_NST];
+#define A3P_ST(i)                                                                                        \
+    do {                                                                                                 \
+        if (threadIdx.x == 0 && blockIdx.x < 256 && it_ < A3P_MAXIT)                                     \
+            g_act3p_st[((int)blockIdx.x * A3P_MAXIT + it_) * A3P_NST + (i)] = (long long)__builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define A3P_ST(i)
+#endif
+// The tiles off the table path (a row below the table's fire step, or a centre outside it), which
+// qact3p_kernel skips: workgroup b checks rows [1024 b, 1024 b + 1024) (4 per thread, one round of
+// loads, the same test as qact3p_kernel) and runs act3h_tile on both halves of each such 128-row tile.
+// A launch with no such tile costs one round of observation loads (512 workgroups at cfg3).
+template <int DM>
+__global__ __launch_bounds__(256, 2) void qact3h_rest_kernel(Fwd a) {
+    extern __shared__ __attribute__((aligned(16))) char dsm[];
+    __shared__ int bad[8];
+    const int tid = threadIdx.x, m0 = (int)blockIdx.x * 1024;
+    if (tid < 8) bad[tid] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int r = tid + 256 * j;
+        if (m0 + r < a.N) {
+            const evx_obs ob = a.obs[orow(a, m0 + r)];
+            const bool ok = min(max(ob.fire_step, 0), a.t_max) == a.stat_fs && ob.cx >= a.stat_x0 &&
+                            ob.cx < a.stat_x0 + a.stat_nx && ob.cy >= 0 && ob.cy <= a.W + 1;
+            if (!ok) bad[r >> 7] = 1;
+        }
+    }
+    __syncthreads();
+    for (int k = 0; k < 16; k++) {  // 64-row halves (one call site: the body is inlined once)
+        if (!bad[k >> 1] || m0 + 64 * k >= a.N) continue;  // uniform
+        // the arguments re-read per half through an opaque pointer: nothing derived from them is
+        // hoisted out of the loop (hoisted, ~320 VGPRs of addresses were live across it and spilled)
+        const Fwd* ap = &a;
+        asm volatile("" : "+s"(ap));
+        const Fwd ak = *ap;
+        act3h_tile<DM, false>(ak, dsm, m0 + 64 * k);
+        __syncthreads();
+    }
+}
+
+// 8 waves (two per SIMD): wave w owns fc1 columns 128 q + 32 (w & 3) and fc2 columns 64 (w & 3) ..
+// + 63 for the tile's rows 64 (w >> 2) .. + 63, so the two waves of a SIMD (w, w + 4) stream the same
+// weight fragments and cover each other's waits. Tiles are pipelined: the next tile's rows are
+// checked and its table rows (quarter 0) loaded during this tile's slots 2 and 3, and fc2 over this
+// tile's quarter 3 runs in the next tile's slot 0 beside that tile's first epilogue (then fc3).
+template <int DM>
+__global__ __launch_bounds__(512, 2) void qact3p_kernel(Fwd a, int ntiles) {
+    extern __shared__ __attribute__((aligned(16))) char dsm[];
+    __bf16* H = reinterpret_cast<__bf16*>(dsm);  // [buffer][plane][A3P_PL]
+    __bf16* const H1b = H + 2 * A3P_PL;          // buffer 1 (odd quarters)
+    auto W3s = reinterpret_cast<float (*)[HID2]>(dsm + A3P_W3);
+    float* red = reinterpret_cast<float*>(dsm + A3P_RED);
+    int* posS = reinterpret_cast<int*>(dsm + A3P_POS);
+    uint32_t* phS = reinterpret_cast<uint32_t*>(dsm + A3P_PH);
+    const uint4* occT = reinterpret_cast<const uint4*>(dsm + A3P_OCC);
+    float* b2s = reinterpret_cast<float*>(dsm + A3P_B2);
+    const int tid = threadIdx.x;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: weight offsets stay scalar
+    const int c = w & 3, rh = w >> 2;                        // column group, row half
+    const int r0 = 64 * rh;                                  // the wave's first tile row
+    for (int i = tid; i < NACT * HID2; i += 512) W3s[i / HID2][i % HID2] = a.w3[i];
+    if (tid < HID2) b2s[tid] = a.b2[tid];
+    if (tid < 256) {  // byte of 8 cell bits -> the 8 bf16 A values (0 or 1.0) of one occupancy k-step
+        const uint32_t bits = (uint32_t)tid, one = 0x3f80u;
+        uint32_t v[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) v[j] = ((bits >> (2 * j)) & 1u) * one | (((bits >> (2 * j + 1)) & 1u) * one) << 16;
+        reinterpret_cast<uint4*>(dsm + A3P_OCC)[tid] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+    const gbyte *w2p = (const gbyte*)a.w2, *w2lp = (const gbyte*)a.w2l;
+    const gbyte *w1op = (const gbyte*)a.w1o, *w1olp = (const gbyte*)a.w1ol, *statp = (const gbyte*)a.stat;
+    // tile-uniform table path of tile tt's row tid (< 128): every row at the table's fire step with its
+    // centre inside the table; its table row into posS[buf], the row-pair hashes into phS[buf]
+    auto setup_rows = [&](int tt, int buf, bool& ok, const evx_obs* pre) {  // pre: row tid's observation, loaded
+        ok = true;
+        const int mm = tt * 128;
+        if (tid < 128) {
+            int pos = 0;
+            if (mm + tid < a.N) {
+                const evx_obs ob = pre ? *pre : a.obs[orow(a, mm + tid)];
+                ok = min(max(ob.fire_step, 0), a.t_max) == a.stat_fs && ob.cx >= a.stat_x0 &&
+                     ob.cx < a.stat_x0 + a.stat_nx && ob.cy >= 0 && ob.cy <= a.W + 1;
+                pos = ok ? (ob.cx - a.stat_x0) * (a.W + 2) + ob.cy : 0;
+            }
+            posS[buf * 128 + tid] = pos;
+        } else if (DM == 1 && tid < 192) {
+            const int r2 = mm + 2 * (tid - 128);
+            phS[buf * 64 + tid - 128] =
+                r2 < a.N ? drop_row(a.drop_seed, a.drop_stream, (a.drop_row0 + (uint32_t)krow(a, r2)) >> 1) : 0u;
+        }
+    };
+    int it_ = -1;
+    (void)it_;
+    int tile = blockIdx.x, cur = 0, pm0 = 0;
+    bool ready = false;  // tile is set up in buffer cur (posS / phS), its occupancy and quarter-0 table loaded
+    bool pend = false;   // the previous tile (rows pm0 ..) still owes fc2 over its quarter 3 and fc3
+    f32x16 acc2[2][2];
+#pragma unroll
+    for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+        for (int nt = 0; nt < 2; nt++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc2[mt][nt][r] = 0.f;
+    f32x16 tab[2], acc1[2];
+    uint32_t occ[2][4];
+    bf16x8 wb[2][2], wl[2][2];  // fc2 weight fragments: ring of 2, one k-step ahead
+    bf16x8 bh[3], bl[3];        // fc1's occupancy weight fragments: ring of 3, two k-steps ahead
+    while (true) {
+        it_++;
+        A3P_ST(0);
+        // the lane index, opaque per iteration: the per-lane offsets derived from it are formed inside
+        // it (hoisted out of the tile loop, a few hundred of them were live across it and spilled)
+        int lane = tid & 63;
+        asm volatile("" : "+v"(lane));
+        const int h = lane >> 5, j32 = lane & 31;
+        const uint32_t l16 = (uint32_t)lane * 16u;  // a lane's 16 B of a 1-KB operand fragment
+        // fc2's transposed B reads: lane l takes k rows 8 h + (l >> 2 & 3) (+ 4) of a k-step, rows
+        // r0 + 32 mt + 16 (l >> 4 & 1) + 4 (l & 3) .. + 3 (tr_frag's addressing on the swizzled image)
+        const int kq = 8 * h + ((lane >> 2) & 3), rq = r0 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+        auto trf = [&](const __bf16* plane, int ks, int mt) -> bf16x8 {
+            const __bf16* b = plane + ks * 16 * 128;
+            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b + h1t_off(kq, 32 * mt + rq)));
+            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b + h1t_off(kq + 4, 32 * mt + rq)));
+            const s16x4 v[2] = {lo, hi};
+            return __builtin_bit_cast(bf16x8, v);
+        };
+        auto load_occ = [&](int mm) {
+#pragma unroll
+            for (int mt = 0; mt < 2; mt++) {
+                const int row = mm + r0 + mt * 32 + j32;
+                uint4 o = make_uint4(0u, 0u, 0u, 0u);
+                if (row < a.N) o = *reinterpret_cast<const uint4*>(&a.obs[orow(a, row)].occ[0]);
+                occ[mt][0] = o.x;
+                occ[mt][1] = o.y;
+                occ[mt][2] = o.z;
+                occ[mt][3] = o.w;
+            }
+        };
+        // table rows of quarter q (rows of posS[buf]): register r of tile mt is row r0 + 32 mt + (r & 3) +
+        // 8 (r >> 2) + 4 h
+        auto load_tab = [&](int buf, int q) {
+            const uint32_t cofs = (uint32_t)(128 * q + 32 * c + j32) * 4u;  // + the row's table offset
+#pragma unroll
+            for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+                for (int g = 0; g < 4; g++) {
+                    const int4 p4 = *reinterpret_cast<const int4*>(&posS[buf * 128 + r0 + 32 * mt + 8 * g + 4 * h]);
+                    const int pp[4] = {p4.x, p4.y, p4.z, p4.w};
+#pragma unroll
+                    for (int i = 0; i < 4; i++)  // 32-bit byte offsets from the uniform base
+                        tab[mt][4 * g + i] = *(const gfloat*)(statp + ((uint32_t)pp[i] * (uint32_t)(HID * 4) + cofs));
+                }
+        };
+        auto load_w2 = [&](int q, int ks, int slot) {
+#pragma unroll
+            for (int nt = 0; nt < 2; nt++) {  // uniform base + (fragment offset + the lane's 16 B)
+                const uint32_t o = (uint32_t)w2_tile(c * 2 + nt, 4 * q + (ks >> 1), ks & 1) * 2u + l16;
+                wb[slot][nt] = *(const gbf16x8*)(w2p + o);
+                wl[slot][nt] = *(const gbf16x8*)(w2lp + o);
+            }
+        };
+        // fc1 of quarter q: acc1 = tab + occupancy columns x bits (ks ascending, hi then lo per
+        // fragment, as act3h_tile); at ks 5, behind every fc1 weight load (tab was read at ks 0), the
+        // table loads of the quarter after (tbuf, tq; tq < 0: none)
+        // fc1 weight fragments of k-step ks of quarter q (column tile 4 q + c) into ring slot ks % 3
+        auto ldw = [&](int q, int ks) {
+            const uint32_t o = (uint32_t)w1o_tile(4 * q + c, ks >> 1, ks & 1) * 2u + l16;
+            bh[ks % 3] = *(const gbf16x8*)(w1op + o);
+            bl[ks % 3] = *(const gbf16x8*)(w1olp + o);
+        };
+        // (its first two k-steps' fragments were loaded by the phase before: fc2q's last k-steps)
+        auto fc1q = [&](int q, int tbuf, int tq) {
+#pragma unroll
+            for (int ks = 0; ks < 8; ks++) {
+                if (ks + 2 < 8) ldw(q, ks + 2);
+                if (ks == 5 && tq >= 0) load_tab(tbuf, tq);
+                const int c0 = ks * 16 + 8 * h;  // cells c0 .. c0 + 7, in word ks >> 1
+#pragma unroll
+                for (int mt = 0; mt < 2; mt++) {
+                    const bf16x8 av = __builtin_bit_cast(bf16x8, occT[(occ[mt][ks >> 1] >> (c0 & 31)) & 0xffu]);
+                    acc1[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bh[ks % 3], ks == 0 ? tab[mt] : acc1[mt], 0, 0, 0);
+                    acc1[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bl[ks % 3], acc1[mt], 0, 0, 0);
+                }
+            }
+        };
+        // quarter q's epilogue for rows r0 + 32 mt + 8 g + 4 h .. + 3 of the lane's column -> H1^T (buffer Hb)
+        auto epi = [&](int q, __bf16* Hb, int mt, int g) {
+            const int k = 32 * c + j32, rb = r0 + 32 * mt + 8 * g + 4 * h;
+            float v[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const float x = acc1[mt][4 * g + i];
+                v[i] = x > 0.f ? x : 0.f;
+            }
+            if constexpr (DM == 1) {
+                const uint2 ph = *reinterpret_cast<const uint2*>(&phS[cur * 64 + (rb >> 1)]);
+                const uint32_t col = (uint32_t)(128 * q + k);
+                const uint32_t h0 = drop_pair(ph.x, col), h1 = drop_pair(ph.y, col);
+                v[0] = (h0 & 0xffffu) >= a.drop_thresh ? v[0] * a.drop_scale : 0.f;
+                v[1] = (h0 >> 16) >= a.drop_thresh ? v[1] * a.drop_scale : 0.f;
+                v[2] = (h1 & 0xffffu) >= a.drop_thresh ? v[2] * a.drop_scale : 0.f;
+                v[3] = (h1 >> 16) >= a.drop_thresh ? v[3] * a.drop_scale : 0.f;
+            }
+            __bf16 hi[4], lo[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) split2(v[i], hi[i], lo[i]);
+            const int o = h1t_off(k, rb);
+            *reinterpret_cast<uint2*>(Hb + o) = __builtin_bit_cast(uint2, hi);
+            *reinterpret_cast<uint2*>(Hb + A3P_PL + o) = __builtin_bit_cast(uint2, lo);
+        };
+        // fc2 over quarter qq's K from buffer Hb (k-step ks: fc2 K 128 qq + 16 ks; kc, s order as
+        // act3h_tile); EPI: quarter eq's epilogue into buffer He, one row group per k-step; the last
+        // k-step loads the first fragments of quarter (qq + 1) & 3 (the next tile's 0 after 3)
+        // wq >= 0: the next fc1's quarter -- its first two k-steps' weight fragments (k-steps 5, 6)
+        auto fc2q = [&](int qq, const __bf16* Hb, auto epi_on, int eq, __bf16* He, int wq) {
+#pragma unroll
+            for (int ks = 0; ks < 8; ks++) {
+                if (ks + 1 < 8) load_w2(qq, ks + 1, (ks + 1) & 1);
+                else load_w2((qq + 1) & 3, 0, 0);
+                if (ks == 5 && wq >= 0) ldw(wq, 0);
+                if (ks == 6 && wq >= 0) ldw(wq, 1);
+                const int sl = ks & 1;
+#pragma unroll
+                for (int mt = 0; mt < 2; mt++) {
+                    const bf16x8 ah = trf(Hb, ks, mt), al = trf(Hb + A3P_PL, ks, mt);
+#pragma unroll
+                    for (int nt = 0; nt < 2; nt++) {  // H2^T tiles (fc3t_x3): W2 as A, H1 rows as B
+                        acc2[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wb[sl][nt], ah, acc2[mt][nt], 0, 0, 0);
+                        acc2[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl[sl][nt], ah, acc2[mt][nt], 0, 0, 0);
+                        acc2[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wb[sl][nt], al, acc2[mt][nt], 0, 0, 0);
+                    }
+                }
+                if constexpr (decltype(epi_on)::value) epi(eq, He, ks >> 2, ks & 3);
+            }
+        };
+        auto fc3_prev = [&]() {  // the previous tile's fc3 partials, then a fresh fc2 sum
+            fc3p_partials(acc2, W3s, b2s, red, c, r0, lane);
+#pragma unroll
+            for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+                for (int nt = 0; nt < 2; nt++)
+#pragma unroll
+                    for (int r = 0; r < 16; r++) acc2[mt][nt][r] = 0.f;
+        };
+        if (!ready) {  // no tile set up ahead (the first, or the one after a skipped tile)
+            if (pend) {
+                fc2q(3, H1b, std::false_type{}, 0, H, -1);
+                fc3_prev();
+                __syncthreads();
+                fc3p_rows(a, red, pm0);
+                pend = false;
+            }
+            bool fast = false;
+            for (; tile < ntiles; tile += gridDim.x) {
+                __syncthreads();  // the last readers of posS / phS / H1 / the partials are done
+                bool ok;
+                setup_rows(tile, cur, ok, nullptr);
+                fast = __syncthreads_and(ok);
+                if (fast) break;  // else qact3h_rest_kernel's
+            }
+            if (!fast) break;
+            load_occ(tile * 128);
+            load_tab(cur, 0);
+            load_w2(0, 0, 0);
+            ldw(0, 0);
+            ldw(0, 1);
+        }
+        const int m0 = tile * 128;
+        A3P_ST(1);
+        // slot 0: fc1 of quarter 0; fc2 over the previous tile's quarter 3 with this epilogue beside it
+        fc1q(0, cur, 1);
+        A3P_ST(2);
+        if (pend) {
+            fc2q(3, H1b, std::true_type{}, 0, H, 1);
+        } else {
+            ldw(1, 0);
+            ldw(1, 1);
+#pragma unroll
+            for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+                for (int g = 0; g < 4; g++) epi(0, H, mt, g);
+        }
+        if (pend) fc3_prev();  // the previous tile's fc3 partials (its fc2 sum is complete)
+        A3P_ST(3);
+        __syncthreads();
+        if (pend) fc3p_rows(a, red, pm0);  // its rows: Q, epsilon-greedy
+        A3P_ST(4);
+        // slot 1
+        fc1q(1, cur, 2);
+        A3P_ST(5);
+        fc2q(0, H, std::true_type{}, 1, H1b, 2);
+        A3P_ST(6);
+        __syncthreads();
+        A3P_ST(7);
+        // slot 2, and the next tile's rows checked (posS / phS of the other buffer; its observations
+        // loaded at the slot's start)
+        const int nt2 = tile + (int)gridDim.x;
+        evx_obs obn{{0u, 0u, 0u, 0u}, 0, 0, 0, 0};
+        if (tid < 128 && nt2 < ntiles && nt2 * 128 + tid < a.N) obn = a.obs[orow(a, nt2 * 128 + tid)];
+        fc1q(2, cur, 3);
+        A3P_ST(8);
+        fc2q(1, H1b, std::true_type{}, 2, H, 3);
+        bool okn = true;
+        if (nt2 < ntiles) setup_rows(nt2, cur ^ 1, okn, &obn);
+        A3P_ST(9);
+        const bool fast_next = __syncthreads_and(okn) && nt2 < ntiles;
+        A3P_ST(10);
+        // slot 3: the next tile's quarter-0 table rows (fc1q's ks 5) and occupancy after fc1
+        fc1q(3, cur ^ 1, fast_next ? 0 : -1);
+        if (fast_next) load_occ(nt2 * 128);
+        A3P_ST(11);
+        fc2q(2, H, std::true_type{}, 3, H1b, fast_next ? 0 : -1);
+        A3P_ST(12);
+        __syncthreads();
+        A3P_ST(13);
+        pend = true;
+        pm0 = m0;
+        tile = nt2;
+        ready = fast_next;
+        if (fast_next) cur ^= 1;
+    }
 }
 
 // X (the x3 compact input of every batch row, [N][640] bf16: per cell (occ | danger hi, barrier |
@@ -1662,8 +2140,6 @@ __device__ __forceinline__ void qdz1_body(const Bwd& a, char* smem, int bx, int 
 // LDS image of a plane: [TKC][TPT] bf16, 320-B rows: a transposed read's 32-lane half takes
 // 4 rows x 64 B at banks 16 q + [0, 16) -- conflict-free (cdna_hip_programming.md T10)
 constexpr int TT = 128, TKC = 64, TPT = TT + 32;
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 // the 32x32x16 operand fragment of rows (columns of the image) c0 .. c0 + 31, k = k0 .. k0 + 15:
 // lane l gets column c0 + (l & 31), k = k0 + 8 (l >> 5) + 0 .. 7 (two transposed reads; lane
 // 4q + p of each 16-lane group addresses row q of a 4-row block, columns 4p .. 4p + 3)
@@ -2302,6 +2778,17 @@ int evx_qmlp_forward(const evx_layout* lay, const evx_obs* obs, int32_t n, const
 }
 
 // diagnostic builds only: copy the act stamps out (-1 when the build has none)
+int evx_diag_act3p_stamps(long long* host, int32_t n) {
+#ifdef EVX_ACT_STAMPS
+    if (n > 256 * evxm::A3P_MAXIT * evxm::A3P_NST) n = 256 * evxm::A3P_MAXIT * evxm::A3P_NST;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(evxm::g_act3p_st), (size_t)n * 8) == hipSuccess ? n : -5;
+#else
+    (void)host;
+    (void)n;
+    return -1;
+#endif
+}
+
 int evx_diag_act_stamps(long long* host, int32_t n) {
 #ifdef EVX_ACT_STAMPS
     if (n > 8192 * evxm::ACT_NST) n = 8192 * evxm::ACT_NST;
@@ -2313,8 +2800,37 @@ int evx_diag_act_stamps(long long* host, int32_t n) {
 #endif
 }
 
-int evx_qmlp_act(const evx_layout* lay, const evx_obs* obs, int32_t n, const evx_qmlp_params* p,
-                 const evx_qmlp_dropout* drop, const evx_qmlp_fwd_out* out, void* stream) {
+}  // extern "C"
+
+// the x3 act: the persistent 128-row kernel when its table path applies (a table attached, the hash
+// or no dropout) and the launch has a tile for every CU; else (or kernel64) the 64-row kernel
+static void act_x3(const evxm::Fwd& a, int32_t n, hipStream_t st, bool kernel64) {
+    const int ntiles = (n + 127) / 128, ncu = evxh::cu_count();
+    if (!kernel64 && a.stat && !a.drop_mask && ntiles >= ncu) {
+        {
+            static std::atomic<uint64_t> attr_done;
+            const void* kp[2] = {(const void*)evxm::qact3p_kernel<0>, (const void*)evxm::qact3p_kernel<1>};
+            evxh::max_lds_once(attr_done, kp, 2, evxm::ACT3P_LDS);
+            static std::atomic<uint64_t> attr_done2;
+            const void* kr[2] = {(const void*)evxm::qact3h_rest_kernel<0>, (const void*)evxm::qact3h_rest_kernel<1>};
+            evxh::max_lds_once(attr_done2, kr, 2, evxm::ACT3H_LDS);
+        }
+        // the table-path tiles on the persistent kernel, then the others (if any) on the 64-row body
+        const dim3 grid((unsigned)std::min(ntiles, ncu)), rgrid((unsigned)((n + 1023) / 1024));
+        if (a.drop_thresh) {
+            hipLaunchKernelGGL(evxm::qact3p_kernel<1>, grid, dim3(512), evxm::ACT3P_LDS, st, a, ntiles);
+            hipLaunchKernelGGL(evxm::qact3h_rest_kernel<1>, rgrid, dim3(256), evxm::ACT3H_LDS, st, a);
+        } else {
+            hipLaunchKernelGGL(evxm::qact3p_kernel<0>, grid, dim3(512), evxm::ACT3P_LDS, st, a, ntiles);
+            hipLaunchKernelGGL(evxm::qact3h_rest_kernel<0>, rgrid, dim3(256), evxm::ACT3H_LDS, st, a);
+        }
+        return;
+    }
+    launch_act3<false>(a, n, 1, st);
+}
+
+static int qmlp_act_impl(const evx_layout* lay, const evx_obs* obs, int32_t n, const evx_qmlp_params* p,
+                         const evx_qmlp_dropout* drop, const evx_qmlp_fwd_out* out, void* stream, bool kernel64) {
     if (n <= 0) return 0;
     if (!out) return mfail(-22, "qmlp_act: NULL out");
     if (!out->q && !out->actions) return mfail(-22, "qmlp_act: needs q or actions");
@@ -2333,11 +2849,23 @@ int evx_qmlp_act(const evx_layout* lay, const evx_obs* obs, int32_t n, const evx
         evxh::max_lds_once(attr_done, ks, 1, evxm::ACT_LDS);
     }
     if (p->x3)
-        launch_act3<false>(a, n, 1, (hipStream_t)stream);
+        act_x3(a, n, (hipStream_t)stream, kernel64);
     else
         hipLaunchKernelGGL(evxm::qact_kernel, dim3((unsigned)((n + 127) / 128)), dim3(512), evxm::ACT_LDS,
                            (hipStream_t)stream, a);
     return mlaunch("qact");
+}
+
+extern "C" {
+
+int evx_qmlp_act(const evx_layout* lay, const evx_obs* obs, int32_t n, const evx_qmlp_params* p,
+                 const evx_qmlp_dropout* drop, const evx_qmlp_fwd_out* out, void* stream) {
+    return qmlp_act_impl(lay, obs, n, p, drop, out, stream, false);
+}
+
+int evx_qmlp_act64(const evx_layout* lay, const evx_obs* obs, int32_t n, const evx_qmlp_params* p,
+                   const evx_qmlp_dropout* drop, const evx_qmlp_fwd_out* out, void* stream) {
+    return qmlp_act_impl(lay, obs, n, p, drop, out, stream, true);
 }
 
 int evx_qmlp_stat(const evx_layout* lay, const evx_obs* obs, int32_t n, const evx_qmlp_params* p, float* out,

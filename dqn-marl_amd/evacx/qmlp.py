@@ -67,6 +67,7 @@ def mlib():
                                        C.POINTER(evx_qmlp_dropout), C.POINTER(evx_qmlp_fwd_out), C.c_void_p]
         L.evx_qmlp_act.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(evx_qmlp_params),
                                    C.POINTER(evx_qmlp_dropout), C.POINTER(evx_qmlp_fwd_out), C.c_void_p]
+        L.evx_qmlp_act64.argtypes = L.evx_qmlp_act.argtypes
         L.evx_qmlp_forward2.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.POINTER(evx_qmlp_params),
                                         C.POINTER(evx_qmlp_dropout), C.POINTER(evx_qmlp_fwd_out), C.c_void_p,
                                         C.POINTER(evx_qmlp_params), C.POINTER(evx_qmlp_dropout),
@@ -272,10 +273,11 @@ class MLPFast:
 
 
     def act(self, lay_c, obs: torch.Tensor, n: int, drop=None, q=None, actions=None, epsilon=0.0, act_seed=0,
-            act_offset=0, perm=None, rows_per_env=0):
+            act_offset=0, perm=None, rows_per_env=0, kernel64: bool = False):
         """DQNAgent.act in one launch (evx_qmlp_act): Q values and/or epsilon-greedy actions.
         perm (int32 [n / rows_per_env], device; evacx.env.VecEnv.act_perm): the batch visits the
-        envs in this order (results stay at their own rows)."""
+        envs in this order (results stay at their own rows). kernel64: the 64-row kernel only
+        (evx_qmlp_act64; the default may take the persistent 128-row kernel, same bits)."""
         _need("act obs", obs, n, 8)
         _need("act q", q, n, NACT)
         _need("act actions", actions, n, 1)
@@ -287,8 +289,9 @@ class MLPFast:
         d = self._drop(drop) if drop else None
         o = evx_qmlp_fwd_out(q=_p(q), actions=_p(actions), epsilon=float(epsilon), act_seed=act_seed,
                              act_offset=act_offset, perm=_p(perm), rows_per_env=int(rows_per_env))
-        mcheck(mlib().evx_qmlp_act(C.byref(lay_c), obs.data_ptr(), n, C.byref(self.c),
-                                   C.byref(d) if d is not None else None, C.byref(o), _stream()), "qmlp_act")
+        fn = mlib().evx_qmlp_act64 if kernel64 else mlib().evx_qmlp_act
+        mcheck(fn(C.byref(lay_c), obs.data_ptr(), n, C.byref(self.c), C.byref(d) if d is not None else None,
+                  C.byref(o), _stream()), "qmlp_act")
 
     @staticmethod
     def _drop(drop):

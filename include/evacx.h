@@ -479,6 +479,11 @@ int evx_qmlp_forward(const evx_layout *lay, const evx_obs *obs, int32_t n, const
  * set): the same products summed in another order. */
 int evx_qmlp_act(const evx_layout *lay, const evx_obs *obs, int32_t n, const evx_qmlp_params *p,
                  const evx_qmlp_dropout *drop, const evx_qmlp_fwd_out *out, void *stream);
+/* The same act on the 64-row kernel only. x3 evx_qmlp_act runs a persistent kernel of 128-row tiles
+ * (one workgroup per CU) when the table path is attached, the dropout is the hash or off and n
+ * covers a tile per CU; it gives the same bits as this one (tests compare the two). */
+int evx_qmlp_act64(const evx_layout *lay, const evx_obs *obs, int32_t n, const evx_qmlp_params *p,
+                   const evx_qmlp_dropout *drop, const evx_qmlp_fwd_out *out, void *stream);
 /* Two forwards of n rows in one launch pair (the learner's online and target nets). */
 int evx_qmlp_forward2(const evx_layout *lay, int32_t n, const evx_obs *obs0, const evx_qmlp_params *p0,
                       const evx_qmlp_dropout *drop0, const evx_qmlp_fwd_out *out0, const evx_obs *obs1,

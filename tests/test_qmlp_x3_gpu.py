@@ -387,3 +387,64 @@ def test_x3_act_at_bench_rows_table_path_env_order():
     assert (got.argmax(1) == refq.argmax(1)).float().mean().item() >= 0.995
     # the table path ran on the saturated envs' rows (not bit-identical to the full path there)
     assert s[rows // R].any()
+
+
+@pytest.mark.parametrize("case", ["bench_rows_perm", "ragged_no_dropout", "all_full_path"])
+def test_x3_persistent_act_matches_64_row_kernel(case):
+    """evx_qmlp_act's persistent 128-row kernel (qact3p_kernel: one workgroup per CU, fc1 quarters
+    pipelined against fc2, H1^T in swizzled LDS read by ds_read_b64_tr_b16) against the 64-row kernel
+    (evx_qmlp_act64) on the same inputs: Q and epsilon-greedy actions bit for bit.
+    bench_rows_perm: 524 288 rows (32 768 envs x 16 robots), 85 % of the envs at the table's fire step
+    first in the act order (the boundary tiles and the rest take the fallback, act3h_tile), hash
+    dropout, epsilon 0.1; ragged_no_dropout: 256 x 128 + 72 rows, every row on the table path, no
+    perm, p = 0 (the DM 0 instantiation, a partial last tile); all_full_path: 262 144 rows with no row at
+    the table's fire step (every tile through the fallback)."""
+    _need_gpu()
+    from evacx.env import DeviceLayout, VecEnv
+    from evacx.layout import build_tables, synthetic
+    from evacx.qnet import DROPOUT_P, Learner
+    R, E0 = 16, 2048
+    lay = DeviceLayout(build_tables(synthetic(128, 128, R)), 2276)
+    env = VecEnv(lay, E0)
+    env.seed([300 + i for i in range(E0)])
+    env.reset()
+    g = torch.Generator(device="cuda").manual_seed(8)
+    for _ in range(6):
+        env.step(torch.randint(0, 5, (E0 * R,), device="cuda", dtype=torch.int32, generator=g), auto_reset=True)
+    torch.cuda.synchronize()
+    t_max = int(lay.c.t_max)
+    lr = Learner(kind="mlp", precision="f32", seed=17)
+    fast, lc = lr.fast, lay.c
+    fast.attach_static(lc, int(lc.L), int(lc.W), t_max, x_range=(max(lc.rx_lo, 0), min(lc.rx_hi, lc.L + 1)))
+    kw, drop, eps = {}, (21, 5, DROPOUT_P), 0.1
+    if case == "bench_rows_perm":
+        rep = 16
+        E, n = E0 * rep, E0 * rep * R
+        obs = env.obs.view(E0, R, 8).repeat(rep, 1, 1).contiguous()
+        sat = torch.from_numpy(np.random.RandomState(2).rand(E) < 0.85).cuda()
+        obs[:, :, 6] = torch.where(sat[:, None], torch.full_like(obs[:, :, 6], t_max), obs[:, :, 6])
+        s = sat.cpu().numpy()
+        perm = torch.from_numpy(np.concatenate([np.nonzero(s)[0], np.nonzero(~s)[0]]).astype(np.int32)).cuda()
+        kw = dict(perm=perm, rows_per_env=R)
+    elif case == "ragged_no_dropout":
+        n = 256 * 128 + 72
+        obs = env.obs.view(-1, 8).repeat(2, 1)[:n].contiguous()
+        obs[:, 6] = t_max
+        drop = (21, 5, 0.0)
+    else:
+        rep = 8
+        n = E0 * rep * R
+        obs = env.obs.view(-1, 8).repeat(rep, 1).contiguous()
+        obs[:, 6] = torch.clamp(obs[:, 6], max=t_max - 1)
+    out = {}
+    for k64 in (False, True):
+        q = torch.full((n, 5), float("nan"), device="cuda")
+        a = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+        fast.act(lc, obs.view(-1), n, drop=drop, q=q, actions=a, epsilon=eps, act_seed=6, act_offset=33,
+                 kernel64=k64, **kw)
+        torch.cuda.synchronize()
+        out[k64] = (q, a)
+    (qp, ap), (q6, a6) = out[False], out[True]
+    assert torch.isfinite(q6).all() and (a6 >= 0).all()
+    assert torch.equal(qp, q6)
+    assert torch.equal(ap, a6)

@@ -23,6 +23,7 @@ ap.add_argument("--order", choices=["env", "centre", "shuffle"], default="env",
                 help="row order: env (the envs' own), centre (sorted by window centre: rows sharing a table row "
                      "adjacent), shuffle (random)")
 ap.add_argument("--drop-p", type=float, default=DROPOUT_P, help="dropout p of the act (0: no dropout epilogue)")
+ap.add_argument("--kernel64", action="store_true", help="the 64-row kernel only (evx_qmlp_act64)")
 args = ap.parse_args()
 E, R = 4096, 16
 lay = DeviceLayout(build_tables(synthetic(128, 128, R)), 2276)
@@ -46,15 +47,21 @@ elif args.order == "shuffle":
     obs = obs[torch.randperm(obs.shape[0], device="cuda")].contiguous()
 act = torch.empty(args.rows, dtype=torch.int32, device="cuda")
 for i in range(3):
-    lr.fast.act(lay.c, obs.view(-1), args.rows, drop=(1, i, args.drop_p), actions=act, epsilon=0.1)
+    lr.fast.act(lay.c, obs.view(-1), args.rows, drop=(1, i, args.drop_p), actions=act, epsilon=0.1,
+                kernel64=args.kernel64)
 torch.cuda.synchronize()
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 e0.record()
 for i in range(args.iters):
-    lr.fast.act(lay.c, obs.view(-1), args.rows, drop=(1, i, args.drop_p), actions=act, epsilon=0.1)
+    lr.fast.act(lay.c, obs.view(-1), args.rows, drop=(1, i, args.drop_p), actions=act, epsilon=0.1,
+                kernel64=args.kernel64)
 e1.record()
 torch.cuda.synchronize()
 us = e0.elapsed_time(e1) / args.iters * 1e3
-fl = args.rows * 2 * (512 * (640 + 512) + 256 * 512 * 3)
-print(f"rows {args.rows}: {us:.1f} us per act, {fl / us / 1e6:.0f} TF/s of bf16 MFMA products "
-      f"({fl / us / 1e6 / 2500:.1%} of 2.5 PF)")
+# bf16 MFMA products per row: the table path's fc1 occupancy columns (128 K, hi + lo), else the full
+# fc1 (640 hi*hi + 512 hi*lo K); fc2 3 x 512 K; fc3 (5 rows padded to 32) 3 x 256 K
+tf = args.table_frac
+fc1 = tf * 512 * 128 * 2 + (1 - tf) * 512 * (640 + 512)
+fl = args.rows * 2 * (fc1 + 256 * 512 * 3 + 32 * 256 * 3)
+print(f"rows {args.rows}{' (64-row kernel)' if args.kernel64 else ''}: {us:.1f} us per act, {fl / us / 1e6:.0f} TF/s "
+      f"of bf16 MFMA products ({fl / us / 1e6 / 2500:.1%} of 2.5 PF)")
