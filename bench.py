@@ -299,13 +299,14 @@ def main():
     lagged_ok = tr.fast is not None  # the lagged schedule needs the fused MLP path
     schedule = args.schedule if lagged_ok else "strict"
 
-    def timed_train(n, ev_env=None, ev_learn=None):
+    def timed_train(n, ev_env=None, ev_learn=None, ev_act=None):
         barrier()
         t0 = time.perf_counter()
         for s in range(n):
             if args.mode == "train":
                 tr.step(ev_env=None if ev_env is None or s % EV_EVERY else ev_env[s],
-                        ev_learn=None if ev_learn is None or s % EV_EVERY else ev_learn[s])
+                        ev_learn=None if ev_learn is None or s % EV_EVERY else ev_learn[s],
+                        ev_act=None if ev_act is None or s % EV_EVERY else ev_act[s])
             else:
                 env.compute_order()
                 if ev_env is not None and s % EV_EVERY == 0:
@@ -346,11 +347,17 @@ def main():
     value = E * world * args.steps / elapsed
     # the kernel / learn times: a second pass of the same length right after (same episode phase),
     # HIP events bracketing env.step and the learn step on every EV_EVERY-th step
-    ev_env, ev_learn = ev_pairs(args.steps), ev_pairs(args.steps)
-    timed_train(args.steps, ev_env, ev_learn if args.mode == "train" else None)
+    ev_env, ev_learn, ev_act = ev_pairs(args.steps), ev_pairs(args.steps), ev_pairs(args.steps)
+    train = args.mode == "train"
+    timed_train(args.steps, ev_env, ev_learn if train else None, ev_act if train else None)
     env.check_err()
     kern_ms = ev_mean(ev_env, args.steps)
-    learn_ms = ev_mean(ev_learn, args.steps) if args.mode == "train" else None
+    learn_ms = ev_mean(ev_learn, args.steps) if train else None
+    act_ms = ev_mean(ev_act, args.steps) if train else None
+    # the act's rows on the table path (fire step at the layout's last: fc1 = table + occupancy columns)
+    act_tab = None
+    if train and tr.fast is not None and getattr(tr.fast, "_static", None) is not None:
+        act_tab = float((env.obs.view(-1, 8)[:, 6] >= int(tr.lay.c.t_max)).float().mean().item())
 
     # ------------------------------- the other schedule on the same state (extra)
     other = None
@@ -480,13 +487,13 @@ def main():
     if srec is not None:
         waves = srec["waves"]
         insts = (srec["sq_insts_valu_per_wave"] + srec["sq_insts_salu_per_wave"]) * waves
-        clk = srec["clock_ghz"] * 1e9
+        clk = min(srec["clock_ghz"], 2.4) * 1e9  # GRBM reads high on dispatches under ~0.3 ms: at most the 2.4 GHz peak
         t = kern_ms * 1e-3
         roof_issue = {"bound": "issue", "achieved": insts / t / 1e9, "peak": 1024 * clk / 1e9, "unit": "Ginst/s",
                       "frac": insts / (1024 * clk * t),
                       "valu_pipe_frac": srec["sq_insts_valu_per_wave"] * waves * 2 / (1024 * clk * t),
                       "valu_per_wave": srec["sq_insts_valu_per_wave"], "salu_per_wave": srec["sq_insts_salu_per_wave"],
-                      "waves_per_launch": waves, "clock_ghz": srec["clock_ghz"], "kernel_ms": kern_ms,
+                      "waves_per_launch": waves, "clock_ghz": min(srec["clock_ghz"], 2.4), "kernel_ms": kern_ms,
                       "sq_active_inst_any_frac": srec.get("sq_active_inst_any_frac"),
                       "sq_wait_any_frac": srec.get("sq_wait_any_frac"), "source": ssrc,
                       "basis": "(VALU + SALU instructions per wave) x waves / (256 CUs x 4 SIMDs x clock x kernel_ms): "
@@ -564,6 +571,23 @@ def main():
                                  "algorithmic bytes") if roof_issue is not None else "no SQ record for this workload",
             "cpu_baseline": cpu,
         }
+        if act_ms is not None and args.qnet == "mlp" and tr.q_arith == "x3" and not tr.per_robot:
+            rows = E * R
+            tf = act_tab or 0.0
+            # bf16 MFMA products the x3 act issues per row: fc1 (table rows: the 128 occupancy columns,
+            # hi + lo weights; others: 640 hi*hi + 512 hi*lo of K), fc2 3 x 512 K, fc3 (5 actions padded to
+            # the 32-row MFMA tile) 3 x 256 K; f32-equivalent: the reference's products, fc1 over the 121
+            # occupancy inputs on the table path, else the 484 live inputs
+            prod = 2 * (tf * 512 * 128 * 2 + (1 - tf) * 512 * (640 + 512) + 256 * 512 * 3 + 32 * 256 * 3)
+            f32eq = 2 * (tf * 121 * 512 + (1 - tf) * 484 * 512 + 512 * 256 + 256 * 5)
+            ach = rows * prod / (act_ms * 1e-3) / 1e12
+            line["roofline_act"] = {"bound": "mfma", "achieved": ach, "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                    "frac": ach / BF16_PEAK_TFLOPS, "act_ms": act_ms, "rows": rows,
+                                    "table_rows": tf,
+                                    "frac_f32eq": rows * f32eq / (act_ms * 1e-3) / 1e12 / BF16_PEAK_TFLOPS,
+                                    "flops_basis": "bf16 MFMA products issued by the x3 act (frac) and the reference's "
+                                                   "f32 products (frac_f32eq) per row x rows / act_ms (HIP events around "
+                                                   "the act launch(es), every 5th step of the instrumented pass)"}
         lm = learn_alone_ms if learn_alone_ms is not None else learn_ms
         if lm is not None and args.qnet == "mlp" and learn_tab is not None:
             fl = learn_flops_executed(args.batch, *learn_tab)

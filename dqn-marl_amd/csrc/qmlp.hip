@@ -2803,10 +2803,12 @@ int evx_diag_act_stamps(long long* host, int32_t n) {
 }  // extern "C"
 
 // the x3 act: the persistent 128-row kernel when its table path applies (a table attached, the hash
-// or no dropout) and the launch has a tile for every CU; else (or kernel64) the 64-row kernel
+// or no dropout) and the launch has >= 4 tiles per CU (its cross-tile pipeline; with one tile per CU,
+// cfg2's 32 768 rows, the 64-row kernel's two workgroups per CU measured faster: 16.1 vs 15.3 M
+// env-steps/s); else (or kernel64) the 64-row kernel
 static void act_x3(const evxm::Fwd& a, int32_t n, hipStream_t st, bool kernel64) {
     const int ntiles = (n + 127) / 128, ncu = evxh::cu_count();
-    if (!kernel64 && a.stat && !a.drop_mask && ntiles >= ncu) {
+    if (!kernel64 && a.stat && !a.drop_mask && ntiles >= 4 * ncu) {
         {
             static std::atomic<uint64_t> attr_done;
             const void* kp[2] = {(const void*)evxm::qact3p_kernel<0>, (const void*)evxm::qact3p_kernel<1>};

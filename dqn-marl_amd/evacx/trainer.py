@@ -378,7 +378,7 @@ class VecTrainer:
             self.learner.sync_target()
         return loss
 
-    def step(self, extra_reset: Optional[torch.Tensor] = None, ev_env=None, ev_learn=None):
+    def step(self, extra_reset: Optional[torch.Tensor] = None, ev_env=None, ev_learn=None, ev_act=None):
         """One training step. Finished envs are reset inside the env.step launch
         (auto-reset: the reset of an env that ends runs in its own wave, in the shadow
         of the launch's heavy envs); the replay push takes their terminal observations.
@@ -388,7 +388,7 @@ class VecTrainer:
         act waits for it, long complete by then), several groups on their own streams.
         extra_reset: bool [E] of further envs to reset (benchmark staggering, side
         stream); ev_env / ev_learn:
-        optional (start, end) CUDA events (env: group 0's env.step).
+        optional (start, end) CUDA events (env: group 0's env.step); ev_act: group 0's act.
 
         Default order is the reference's (act, env.step, remember, learn). With
         lagged_learn the learn step runs on its own stream from the ring as it was
@@ -420,7 +420,11 @@ class VecTrainer:
                     grp.main.wait_event(G[grp.g - 1].ev_act)
                 if len(G) == 1 and self._orders_side:  # the orders from the side stream
                     grp.main.wait_event(grp.ev_order)
+                if ev_act is not None and grp.g == 0:
+                    ev_act[0].record(grp.main)
                 self._act(grp)
+                if ev_act is not None and grp.g == 0:
+                    ev_act[1].record(grp.main)
                 if self.lagged or grp.g + 1 < len(G):  # read by the update / the next group's act
                     grp.ev_act.record(grp.main)
         if self.lagged:

@@ -481,7 +481,7 @@ int evx_qmlp_act(const evx_layout *lay, const evx_obs *obs, int32_t n, const evx
                  const evx_qmlp_dropout *drop, const evx_qmlp_fwd_out *out, void *stream);
 /* The same act on the 64-row kernel only. x3 evx_qmlp_act runs a persistent kernel of 128-row tiles
  * (one workgroup per CU) when the table path is attached, the dropout is the hash or off and n
- * covers a tile per CU; it gives the same bits as this one (tests compare the two). */
+ * covers 4 tiles per CU; it gives the same bits as this one (tests compare the two). */
 int evx_qmlp_act64(const evx_layout *lay, const evx_obs *obs, int32_t n, const evx_qmlp_params *p,
                    const evx_qmlp_dropout *drop, const evx_qmlp_fwd_out *out, void *stream);
 /* Two forwards of n rows in one launch pair (the learner's online and target nets). */

@@ -396,7 +396,7 @@ def test_x3_persistent_act_matches_64_row_kernel(case):
     (evx_qmlp_act64) on the same inputs: Q and epsilon-greedy actions bit for bit.
     bench_rows_perm: 524 288 rows (32 768 envs x 16 robots), 85 % of the envs at the table's fire step
     first in the act order (the boundary tiles and the rest take the fallback, act3h_tile), hash
-    dropout, epsilon 0.1; ragged_no_dropout: 256 x 128 + 72 rows, every row on the table path, no
+    dropout, epsilon 0.1; ragged_no_dropout: 2048 x 128 + 72 rows, every row on the table path, no
     perm, p = 0 (the DM 0 instantiation, a partial last tile); all_full_path: 262 144 rows with no row at
     the table's fire step (every tile through the fallback)."""
     _need_gpu()
@@ -427,8 +427,8 @@ def test_x3_persistent_act_matches_64_row_kernel(case):
         perm = torch.from_numpy(np.concatenate([np.nonzero(s)[0], np.nonzero(~s)[0]]).astype(np.int32)).cuda()
         kw = dict(perm=perm, rows_per_env=R)
     elif case == "ragged_no_dropout":
-        n = 256 * 128 + 72
-        obs = env.obs.view(-1, 8).repeat(2, 1)[:n].contiguous()
+        n = 8 * 256 * 128 + 72  # >= 4 tiles per CU (the persistent kernel's threshold)
+        obs = env.obs.view(-1, 8).repeat(9, 1)[:n].contiguous()
         obs[:, 6] = t_max
         drop = (21, 5, 0.0)
     else:
