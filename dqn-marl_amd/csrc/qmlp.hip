@@ -815,7 +815,8 @@ __device__ __forceinline__ void fc3p_partials(const f32x16 (&acc)[2][2], const f
 }
 // rows spread over waves 0..3 (32 each, lanes 0..31: one wave per SIMD) -- q_out's epsilon draw is a
 // 10-round Philox per row, and two waves carrying all 128 rows held the next slot back
-__device__ __forceinline__ void fc3p_rows(const Fwd& a, const float* red, int m0) {
+// rowS: the tile rows' output rows (orow), recorded when the rows were set up
+__device__ __forceinline__ void fc3p_rows(const Fwd& a, const float* red, int m0, const int* rowS) {
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
     auto R = reinterpret_cast<const float (*)[NACT][128]>(red);
     if (w < 4 && l < 32) {
@@ -824,7 +825,7 @@ __device__ __forceinline__ void fc3p_rows(const Fwd& a, const float* red, int m0
             float qv[NACT];
 #pragma unroll
             for (int k = 0; k < NACT; k++) qv[k] = ((R[0][k][r] + R[1][k][r]) + R[2][k][r]) + R[3][k][r];
-            q_out(a, qv, orow(a, rt));
+            q_out(a, qv, rowS[r]);
         }
     }
 }
@@ -1219,7 +1220,8 @@ constexpr int A3P_POS = A3P_RED + 4 * NACT * 128 * 4;  // table row of each tile
 constexpr int A3P_PH = A3P_POS + 2 * 128 * 4;          // row-pair dropout hashes [2][64]
 constexpr int A3P_OCC = A3P_PH + 2 * 64 * 4;           // occupancy-fragment table [256] uint4
 constexpr int A3P_B2 = A3P_OCC + 256 * 16;             // fc2.bias f32 [256]
-constexpr int ACT3P_LDS = A3P_B2 + HID2 * 4;           // 153,088 B: one workgroup per CU
+constexpr int A3P_ROW = A3P_B2 + HID2 * 4;             // each tile row's output row (orow) [2][128]
+constexpr int ACT3P_LDS = A3P_ROW + 2 * 128 * 4;       // 154,112 B: one workgroup per CU
 static_assert(ACT3P_LDS <= 160 * 1024 && ACT3H_LDS <= A3P_HB, "LDS: the fallback tile lives in the H1 buffers");
 // H1^T row k: XOR on the dword index of its 8-B pieces -- bits 4-5 <- k & 3 (the 4 k rows of a
 // transposed read in distinct 16-bank blocks), bits 1-3 <- (k >> 1) & 7 (with bit 4 = k & 1: the 16
@@ -1291,6 +1293,7 @@ __global__ __launch_bounds__(512, 2) void qact3p_kernel(Fwd a, int ntiles) {
     uint32_t* phS = reinterpret_cast<uint32_t*>(dsm + A3P_PH);
     const uint4* occT = reinterpret_cast<const uint4*>(dsm + A3P_OCC);
     float* b2s = reinterpret_cast<float*>(dsm + A3P_B2);
+    int* rowS = reinterpret_cast<int*>(dsm + A3P_ROW);
     const int tid = threadIdx.x;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: weight offsets stay scalar
     const int c = w & 3, rh = w >> 2;                        // column group, row half
@@ -1308,13 +1311,16 @@ __global__ __launch_bounds__(512, 2) void qact3p_kernel(Fwd a, int ntiles) {
     const gbyte *w1op = (const gbyte*)a.w1o, *w1olp = (const gbyte*)a.w1ol, *statp = (const gbyte*)a.stat;
     // tile-uniform table path of tile tt's row tid (< 128): every row at the table's fire step with its
     // centre inside the table; its table row into posS[buf], the row-pair hashes into phS[buf]
-    auto setup_rows = [&](int tt, int buf, bool& ok, const evx_obs* pre) {  // pre: row tid's observation, loaded
+    // pre: row tid's observation and output row, loaded (else loaded here); the output rows go to rowS[buf]
+    auto setup_rows = [&](int tt, int buf, bool& ok, const evx_obs* pre, int prow) {
         ok = true;
         const int mm = tt * 128;
         if (tid < 128) {
             int pos = 0;
             if (mm + tid < a.N) {
-                const evx_obs ob = pre ? *pre : a.obs[orow(a, mm + tid)];
+                const int orw = pre ? prow : orow(a, mm + tid);
+                rowS[buf * 128 + tid] = orw;
+                const evx_obs ob = pre ? *pre : a.obs[orw];
                 ok = min(max(ob.fire_step, 0), a.t_max) == a.stat_fs && ob.cx >= a.stat_x0 &&
                      ob.cx < a.stat_x0 + a.stat_nx && ob.cy >= 0 && ob.cy <= a.W + 1;
                 pos = ok ? (ob.cx - a.stat_x0) * (a.W + 2) + ob.cy : 0;
@@ -1328,7 +1334,7 @@ __global__ __launch_bounds__(512, 2) void qact3p_kernel(Fwd a, int ntiles) {
     };
     int it_ = -1;
     (void)it_;
-    int tile = blockIdx.x, cur = 0, pm0 = 0;
+    int tile = blockIdx.x, cur = 0, pm0 = 0, pcur = 0;
     bool ready = false;  // tile is set up in buffer cur (posS / phS), its occupancy and quarter-0 table loaded
     bool pend = false;   // the previous tile (rows pm0 ..) still owes fc2 over its quarter 3 and fc3
     f32x16 acc2[2][2];
@@ -1484,14 +1490,14 @@ __global__ __launch_bounds__(512, 2) void qact3p_kernel(Fwd a, int ntiles) {
                 fc2q(3, H1b, std::false_type{}, 0, H, -1);
                 fc3_prev();
                 __syncthreads();
-                fc3p_rows(a, red, pm0);
+                fc3p_rows(a, red, pm0, rowS + pcur * 128);
                 pend = false;
             }
             bool fast = false;
             for (; tile < ntiles; tile += gridDim.x) {
                 __syncthreads();  // the last readers of posS / phS / H1 / the partials are done
                 bool ok;
-                setup_rows(tile, cur, ok, nullptr);
+                setup_rows(tile, cur, ok, nullptr, 0);
                 fast = __syncthreads_and(ok);
                 if (fast) break;  // else qact3h_rest_kernel's
             }
@@ -1520,7 +1526,7 @@ __global__ __launch_bounds__(512, 2) void qact3p_kernel(Fwd a, int ntiles) {
         if (pend) fc3_prev();  // the previous tile's fc3 partials (its fc2 sum is complete)
         A3P_ST(3);
         __syncthreads();
-        if (pend) fc3p_rows(a, red, pm0);  // its rows: Q, epsilon-greedy
+        if (pend) fc3p_rows(a, red, pm0, rowS + pcur * 128);  // its rows: Q, epsilon-greedy
         A3P_ST(4);
         // slot 1
         fc1q(1, cur, 2);
@@ -1533,12 +1539,16 @@ __global__ __launch_bounds__(512, 2) void qact3p_kernel(Fwd a, int ntiles) {
         // loaded at the slot's start)
         const int nt2 = tile + (int)gridDim.x;
         evx_obs obn{{0u, 0u, 0u, 0u}, 0, 0, 0, 0};
-        if (tid < 128 && nt2 < ntiles && nt2 * 128 + tid < a.N) obn = a.obs[orow(a, nt2 * 128 + tid)];
+        int orn = 0;
+        if (tid < 128 && nt2 < ntiles && nt2 * 128 + tid < a.N) {
+            orn = orow(a, nt2 * 128 + tid);
+            obn = a.obs[orn];
+        }
         fc1q(2, cur, 3);
         A3P_ST(8);
         fc2q(1, H1b, std::true_type{}, 2, H, 3);
         bool okn = true;
-        if (nt2 < ntiles) setup_rows(nt2, cur ^ 1, okn, &obn);
+        if (nt2 < ntiles) setup_rows(nt2, cur ^ 1, okn, &obn, orn);
         A3P_ST(9);
         const bool fast_next = __syncthreads_and(okn) && nt2 < ntiles;
         A3P_ST(10);
@@ -1552,6 +1562,7 @@ __global__ __launch_bounds__(512, 2) void qact3p_kernel(Fwd a, int ntiles) {
         A3P_ST(13);
         pend = true;
         pm0 = m0;
+        pcur = cur;
         tile = nt2;
         ready = fast_next;
         if (fast_next) cur ^= 1;
