@@ -1189,18 +1189,18 @@ __global__ __launch_bounds__(256, 2) void qact3h_kernel(Fwd a0) {
 }
 
 // ------------------------------------------------------------ persistent x3 act
-// DQNAgent.act (agents/dqn_agent.py:101-124), f32-accurate, for 128-row tiles on one 4-wave
-// workgroup per CU (one wave per SIMD, up to 512 registers), workgroup b looping over tiles b,
+// DQNAgent.act (agents/dqn_agent.py:101-124), f32-accurate, for 128-row tiles on one 8-wave
+// workgroup per CU (two waves per SIMD, up to 256 registers each), workgroup b looping over tiles b,
 // b + grid, ...: fc1's occupancy weights and fc2's weights (hi + lo) are streamed from L2 once per
 // 128 rows instead of once per 64 (act3h_tile moved ~14 KB of weights and table per row), and the
 // fc1 epilogue runs under fc2's MFMAs instead of beside another workgroup's. fc1 -> H1 -> fc2 goes
 // in quarters of fc1's 512 columns:
 //   slot q (0..3): fc1 of quarter q (the table row of every row's window centre + the occupancy
-//     columns x bits; wave w on columns 128 q + 32 w, all 128 rows), then fc2's accumulation over
-//     quarter q - 1's 128 K (wave w: fc2 columns 64 w .. 64 w + 63, all 128 rows) from one LDS
-//     buffer with quarter q's epilogue (ReLU, dropout, hi / lo split) writing the other buffer
-//     between its MFMAs; one barrier per slot;
-//   slot 4: fc2 over quarter 3, then fc3 + epsilon-greedy (fc3t_x3).
+//     columns x bits; layout of the waves below), then fc2's accumulation over quarter q - 1's
+//     128 K from one LDS buffer with quarter q's epilogue (ReLU, dropout, hi / lo split) writing
+//     the other buffer between its MFMAs; one barrier per slot;
+//   then fc2 over quarter 3 and fc3 + epsilon-greedy (fc3p_partials / fc3p_rows), in the next
+//   tile's slot 0.
 // The table loads of quarter q + 1 are issued in slot q after the weight loads that fc1 waits on
 // (vmcnt counts loads in issue order). Per element the same products in the same order as
 // act3h_tile: Q and actions are bit-identical to the 64-row kernel (tests/test_qmlp_x3_gpu.py).
