@@ -183,6 +183,9 @@ struct Fwd {
     // grouped act (evx_qmlp_act_g): gn nets interleaved in the shared row buffers -- batch row i
     // of net g reads / writes row i * gn + g (0: not interleaved)
     int gn, g;
+    // persistent x3 act (evx_qmlp_fwd_out.act_ws, or NULL): [0] tiles left to the 64-row kernel,
+    // [1] qact3h_rest_kernel's finished workgroups, [2 ..] those tiles
+    int* rest_ws;
 };
 __device__ __forceinline__ int orow(const Fwd& a, int row) {
     int r = row;
@@ -1247,32 +1250,62 @@ __device__ long long g_act3p_st[256 * A3P_MAXIT * A3P_NST];
 // qact3p_kernel skips: workgroup b checks rows [1024 b, 1024 b + 1024) (4 per thread, one round of
 // loads, the same test as qact3p_kernel) and runs act3h_tile on both halves of each such 128-row tile.
 // A launch with no such tile costs one round of observation loads (512 workgroups at cfg3).
+// With a.rest_ws (the tiles qact3p_kernel listed): halves 2 k, 2 k + 1 of listed tile k go to workgroups
+// b, b + grid, ...; a launch with no listed tile costs one load per workgroup (no atomic), else the
+// last workgroup to read the count zeroes it for the next act. One workgroup per CU (one wave per SIMD): the tile
+// loop's body fits the 512 registers of a lone wave (at two per SIMD it spilled ~330 VGPRs to scratch).
 template <int DM>
-__global__ __launch_bounds__(256, 2) void qact3h_rest_kernel(Fwd a) {
+__global__ __launch_bounds__(256, 1) void qact3h_rest_kernel(Fwd a) {
     extern __shared__ __attribute__((aligned(16))) char dsm[];
     __shared__ int bad[8];
     const int tid = threadIdx.x, m0 = (int)blockIdx.x * 1024;
-    if (tid < 8) bad[tid] = 0;
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const int r = tid + 256 * j;
-        if (m0 + r < a.N) {
-            const evx_obs ob = a.obs[orow(a, m0 + r)];
-            const bool ok = min(max(ob.fire_step, 0), a.t_max) == a.stat_fs && ob.cx >= a.stat_x0 &&
-                            ob.cx < a.stat_x0 + a.stat_nx && ob.cy >= 0 && ob.cy <= a.W + 1;
-            if (!ok) bad[r >> 7] = 1;
+    int* const ws = a.rest_ws;
+    int nh = 16, h0 = 0, hs = 1;  // halves h0, h0 + hs, ... below nh
+    if (ws) {
+        if (tid == 0) {
+            const int n = __hip_atomic_load(ws, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            bad[0] = n;
+            // n > 0 (every workgroup sees the same count): the last to have read it zeroes both counters
+            // (acq_rel: the count is read before this workgroup counts as done); n = 0: both are zero
+            if (n > 0 && __hip_atomic_fetch_add(ws + 1, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+                             (int)gridDim.x - 1) {
+                __hip_atomic_store(ws, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(ws + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
+        __syncthreads();
+        nh = 2 * bad[0];
+        h0 = (int)blockIdx.x;
+        hs = (int)gridDim.x;
+    } else {
+        if (tid < 8) bad[tid] = 0;
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int r = tid + 256 * j;
+            if (m0 + r < a.N) {
+                const evx_obs ob = a.obs[orow(a, m0 + r)];
+                const bool ok = min(max(ob.fire_step, 0), a.t_max) == a.stat_fs && ob.cx >= a.stat_x0 &&
+                                ob.cx < a.stat_x0 + a.stat_nx && ob.cy >= 0 && ob.cy <= a.W + 1;
+                if (!ok) bad[r >> 7] = 1;
+            }
+        }
+        __syncthreads();
     }
-    __syncthreads();
-    for (int k = 0; k < 16; k++) {  // 64-row halves (one call site: the body is inlined once)
-        if (!bad[k >> 1] || m0 + 64 * k >= a.N) continue;  // uniform
+    for (int hf = h0; hf < nh; hf += hs) {  // 64-row halves (one call site: the body is inlined once); uniform
+        int mh;
+        if (ws) {
+            mh = ws[2 + (hf >> 1)] * 128 + 64 * (hf & 1);
+        } else {
+            if (!bad[hf >> 1] || m0 + 64 * hf >= a.N) continue;
+            mh = m0 + 64 * hf;
+        }
         // the arguments re-read per half through an opaque pointer: nothing derived from them is
         // hoisted out of the loop (hoisted, ~320 VGPRs of addresses were live across it and spilled)
         const Fwd* ap = &a;
         asm volatile("" : "+s"(ap));
         const Fwd ak = *ap;
-        act3h_tile<DM, false>(ak, dsm, m0 + 64 * k);
+        act3h_tile<DM, false>(ak, dsm, mh);
         __syncthreads();
     }
 }
@@ -1499,7 +1532,8 @@ __global__ __launch_bounds__(512, 2) void qact3p_kernel(Fwd a, int ntiles) {
                 bool ok;
                 setup_rows(tile, cur, ok, nullptr, 0);
                 fast = __syncthreads_and(ok);
-                if (fast) break;  // else qact3h_rest_kernel's
+                if (fast) break;  // else qact3h_rest_kernel's: listed for it
+                if (tid == 0 && a.rest_ws) a.rest_ws[2 + atomicAdd(a.rest_ws, 1)] = tile;
             }
             if (!fast) break;
             load_occ(tile * 128);
@@ -2706,6 +2740,7 @@ static int make_fwd(const evx_layout* lay, const evx_obs* obs, int32_t n, const 
     if (a.stat && (a.stat_x0 < 0 || a.stat_x0 + a.stat_nx > lay->L + 2))
         return mfail(-22, "qmlp: the table's centre range must lie in [0, L + 2)");
     a.raw = nullptr;
+    a.rest_ws = nullptr;
     a.drop_mask = drop ? drop->mask : nullptr;
     if (a.drop_mask && !(dp > 0.f)) return mfail(-22, "qmlp_forward: an explicit dropout mask needs p > 0 (its scale)");
     a.feat_lo = nullptr;
@@ -2829,7 +2864,9 @@ static void act_x3(const evxm::Fwd& a, int32_t n, hipStream_t st, bool kernel64)
             evxh::max_lds_once(attr_done2, kr, 2, evxm::ACT3H_LDS);
         }
         // the table-path tiles on the persistent kernel, then the others (if any) on the 64-row body
-        const dim3 grid((unsigned)std::min(ntiles, ncu)), rgrid((unsigned)((n + 1023) / 1024));
+        // (listed: one workgroup per CU over their halves; else every row re-checked)
+        const dim3 grid((unsigned)std::min(ntiles, ncu));
+        const dim3 rgrid(a.rest_ws ? (unsigned)std::min(2 * ntiles, ncu) : (unsigned)((n + 1023) / 1024));
         if (a.drop_thresh) {
             hipLaunchKernelGGL(evxm::qact3p_kernel<1>, grid, dim3(512), evxm::ACT3P_LDS, st, a, ntiles);
             hipLaunchKernelGGL(evxm::qact3h_rest_kernel<1>, rgrid, dim3(256), evxm::ACT3H_LDS, st, a);
@@ -2856,6 +2893,7 @@ static int qmlp_act_impl(const evx_layout* lay, const evx_obs* obs, int32_t n, c
     if (rc) return rc;
     a.h1 = nullptr;
     a.h1l = nullptr;
+    a.rest_ws = out->act_ws;
     {
         static std::atomic<uint64_t> attr_done;
         const void* ks[1] = {(const void*)evxm::qact_kernel};
@@ -2870,6 +2908,8 @@ static int qmlp_act_impl(const evx_layout* lay, const evx_obs* obs, int32_t n, c
 }
 
 extern "C" {
+
+int64_t evx_qmlp_act_ws_ints(int32_t n) { return n > 0 ? 2 + ((int64_t)n + 127) / 128 : 2; }
 
 int evx_qmlp_act(const evx_layout* lay, const evx_obs* obs, int32_t n, const evx_qmlp_params* p,
                  const evx_qmlp_dropout* drop, const evx_qmlp_fwd_out* out, void* stream) {

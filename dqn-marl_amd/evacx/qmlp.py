@@ -48,7 +48,8 @@ class evx_qmlp_grads(C.Structure):
 class evx_qmlp_fwd_out(C.Structure):
     _fields_ = [("h1", C.c_void_p), ("x", C.c_void_p), ("h2", C.c_void_p), ("q", C.c_void_p),
                 ("actions", C.c_void_p), ("epsilon", C.c_float), ("act_seed", C.c_uint64),
-                ("act_offset", C.c_uint64), ("perm", C.c_void_p), ("rows_per_env", C.c_int32)]
+                ("act_offset", C.c_uint64), ("perm", C.c_void_p), ("rows_per_env", C.c_int32),
+                ("act_ws", C.c_void_p)]
 
 
 _inited = False
@@ -80,6 +81,9 @@ def mlib():
                                               C.c_void_p, C.c_void_p]
         L.evx_qmlp_norm_parts.restype = C.c_int32
         L.evx_qmlp_nparams.restype = C.c_int64
+        if hasattr(L, "evx_qmlp_act_ws_ints"):  # (absent from older builds loaded through EVX_LIB for A/Bs)
+            L.evx_qmlp_act_ws_ints.restype = C.c_int64
+            L.evx_qmlp_act_ws_ints.argtypes = [C.c_int32]
         L.evx_qmlp_sumsq_parts.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         L.evx_qmlp_adam_pack3.argtypes = [C.c_void_p] * 4 + [C.c_float, C.c_void_p] + [C.c_void_p] * 10 + \
             [C.c_int32, C.c_void_p, C.c_void_p]
@@ -110,6 +114,12 @@ def mlib():
                                     C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]
         _inited = True
     return L
+
+
+def act_ws_ints(n: int) -> int:
+    """int32 elements of the act's workspace for n rows (evx_qmlp_act_ws_ints)."""
+    L = mlib()
+    return int(L.evx_qmlp_act_ws_ints(int(n))) if hasattr(L, "evx_qmlp_act_ws_ints") else 0
 
 
 def mcheck(rc, what):
@@ -273,11 +283,15 @@ class MLPFast:
 
 
     def act(self, lay_c, obs: torch.Tensor, n: int, drop=None, q=None, actions=None, epsilon=0.0, act_seed=0,
-            act_offset=0, perm=None, rows_per_env=0, kernel64: bool = False):
+            act_offset=0, perm=None, rows_per_env=0, kernel64: bool = False, ws=None):
         """DQNAgent.act in one launch (evx_qmlp_act): Q values and/or epsilon-greedy actions.
         perm (int32 [n / rows_per_env], device; evacx.env.VecEnv.act_perm): the batch visits the
         envs in this order (results stay at their own rows). kernel64: the 64-row kernel only
-        (evx_qmlp_act64; the default may take the persistent 128-row kernel, same bits)."""
+        (evx_qmlp_act64; the default may take the persistent 128-row kernel, same bits).
+        ws: an int32 workspace of act_ws_ints(n) elements (evx_qmlp_fwd_out.act_ws), zeroed once,
+        one per act in flight; every act resets its counters."""
+        if ws is not None and (ws.dtype != torch.int32 or ws.numel() < act_ws_ints(n) or not ws.is_cuda):
+            raise ValueError("qmlp act: ws must be a device int32 tensor of act_ws_ints(n) elements")
         _need("act obs", obs, n, 8)
         _need("act q", q, n, NACT)
         _need("act actions", actions, n, 1)
@@ -288,7 +302,7 @@ class MLPFast:
                              "entries")
         d = self._drop(drop) if drop else None
         o = evx_qmlp_fwd_out(q=_p(q), actions=_p(actions), epsilon=float(epsilon), act_seed=act_seed,
-                             act_offset=act_offset, perm=_p(perm), rows_per_env=int(rows_per_env))
+                             act_offset=act_offset, perm=_p(perm), rows_per_env=int(rows_per_env), act_ws=_p(ws))
         fn = mlib().evx_qmlp_act64 if kernel64 else mlib().evx_qmlp_act
         mcheck(fn(C.byref(lay_c), obs.data_ptr(), n, C.byref(self.c), C.byref(d) if d is not None else None,
                   C.byref(o), _stream()), "qmlp_act")

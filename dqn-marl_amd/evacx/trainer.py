@@ -29,6 +29,7 @@ import torch
 from . import _lib
 from ._lib import evx_replay
 from .env import OBS_WORDS, DeviceLayout, VecEnv, _ptr, _stream
+from .qmlp import act_ws_ints
 from .qnet import DROPOUT_P, Learner, qcheck, qlib
 
 
@@ -125,6 +126,7 @@ class _Group:
         self.ev_order = torch.cuda.Event()
         self.ev_order.record(cur)
         self.perm = None  # the act's env order over this group's envs (x3 table path), or None
+        self.act_ws = None  # the x3 act's workspace (evx_qmlp_fwd_out.act_ws), made at the first act
 
 
 class VecTrainer:
@@ -281,10 +283,12 @@ class VecTrainer:
                               act_seed=self.act_seed, act_offset=off)
             return
         if self.fast is not None:  # one mask stream per step (act_streams), rows keyed by global agent id
+            if grp.act_ws is None and act_ws_ints(grp.n) > 0:  # the persistent act's list of tiles off the table path
+                grp.act_ws = torch.zeros(act_ws_ints(grp.n), dtype=torch.int32, device=self.device)
             self.fast.act(self.lay.c, grp.env.obs, grp.n,
                           drop=(self.learner.seed, self.learner.drop_stream, DROPOUT_P, None, g0),
                           actions=grp.actions, epsilon=float(self.epsilon), act_seed=self.act_seed, act_offset=off,
-                          perm=grp.perm, rows_per_env=0 if grp.perm is None else self.R)
+                          perm=grp.perm, rows_per_env=0 if grp.perm is None else self.R, ws=grp.act_ws)
             return
         x = grp.env.expand_obs(torch.float32)  # [E/G, R, 11, 11, 6]
         # per-group scratch: the groups' acts run concurrently on their own streams

@@ -449,7 +449,15 @@ typedef struct {
      * row pairs stay together) */
     const int32_t *perm;
     int32_t rows_per_env;
+    /* act only, optional: int32 workspace of evx_qmlp_act_ws_ints(n) elements, zeroed once by the
+     * caller (every act leaves its two counters zeroed; one workspace per act in flight). With it the x3 persistent act lists
+     * the 128-row tiles it leaves to the 64-row kernel (a row below stat_fs or a centre outside the
+     * table), so that kernel runs only those instead of re-checking every row (NULL: it re-checks). */
+    int32_t *act_ws;
 } evx_qmlp_fwd_out;
+
+/* elements of evx_qmlp_fwd_out.act_ws for an act of n rows */
+int64_t evx_qmlp_act_ws_ints(int32_t n);
 
 /* bf16 copies of fc1.weight [512][726] over fc1's compact K and fc2.weight [256][512]
  * (w2t may be NULL), and b1c. Compact K: 4 features per cell c < 121 at k = 4c + f for

@@ -436,15 +436,24 @@ def test_x3_persistent_act_matches_64_row_kernel(case):
         n = E0 * rep * R
         obs = env.obs.view(-1, 8).repeat(rep, 1).contiguous()
         obs[:, 6] = torch.clamp(obs[:, 6], max=t_max - 1)
+    from evacx.qmlp import act_ws_ints
+    ws = torch.zeros(act_ws_ints(n), dtype=torch.int32, device="cuda")
     out = {}
-    for k64 in (False, True):
+    # the persistent kernel without a workspace (its fallback re-checks every row), with one (the
+    # tiles off the table path listed; twice on the same workspace, whose counters each act resets),
+    # and the 64-row kernel
+    for key, k64, w in (("p", False, None), ("pw", False, ws), ("pw2", False, ws), ("k64", True, None)):
         q = torch.full((n, 5), float("nan"), device="cuda")
         a = torch.full((n,), -1, dtype=torch.int32, device="cuda")
         fast.act(lc, obs.view(-1), n, drop=drop, q=q, actions=a, epsilon=eps, act_seed=6, act_offset=33,
-                 kernel64=k64, **kw)
+                 kernel64=k64, ws=w, **kw)
         torch.cuda.synchronize()
-        out[k64] = (q, a)
-    (qp, ap), (q6, a6) = out[False], out[True]
+        out[key] = (q, a)
+        if w is not None:
+            assert w[:2].tolist() == [0, 0]  # the count and the done counter, reset for the next act
+    q6, a6 = out["k64"]
     assert torch.isfinite(q6).all() and (a6 >= 0).all()
-    assert torch.equal(qp, q6)
-    assert torch.equal(ap, a6)
+    for key in ("p", "pw", "pw2"):
+        qp, ap = out[key]
+        assert torch.equal(qp, q6), key
+        assert torch.equal(ap, a6), key

@@ -24,6 +24,7 @@ ap.add_argument("--order", choices=["env", "centre", "shuffle"], default="env",
                      "adjacent), shuffle (random)")
 ap.add_argument("--drop-p", type=float, default=DROPOUT_P, help="dropout p of the act (0: no dropout epilogue)")
 ap.add_argument("--kernel64", action="store_true", help="the 64-row kernel only (evx_qmlp_act64)")
+ap.add_argument("--no-ws", action="store_true", help="no act workspace (the fallback kernel re-checks every row)")
 args = ap.parse_args()
 E, R = 4096, 16
 lay = DeviceLayout(build_tables(synthetic(128, 128, R)), 2276)
@@ -46,15 +47,19 @@ if args.order == "centre":
 elif args.order == "shuffle":
     obs = obs[torch.randperm(obs.shape[0], device="cuda")].contiguous()
 act = torch.empty(args.rows, dtype=torch.int32, device="cuda")
+ws = None
+if not args.no_ws:
+    from evacx.qmlp import act_ws_ints
+    ws = torch.zeros(act_ws_ints(args.rows), dtype=torch.int32, device="cuda")
 for i in range(3):
     lr.fast.act(lay.c, obs.view(-1), args.rows, drop=(1, i, args.drop_p), actions=act, epsilon=0.1,
-                kernel64=args.kernel64)
+                kernel64=args.kernel64, ws=ws)
 torch.cuda.synchronize()
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 e0.record()
 for i in range(args.iters):
     lr.fast.act(lay.c, obs.view(-1), args.rows, drop=(1, i, args.drop_p), actions=act, epsilon=0.1,
-                kernel64=args.kernel64)
+                kernel64=args.kernel64, ws=ws)
 e1.record()
 torch.cuda.synchronize()
 us = e0.elapsed_time(e1) / args.iters * 1e3

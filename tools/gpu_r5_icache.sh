@@ -8,10 +8,10 @@ cd /tmp && export TMPDIR=/tmp
 HB=$!
 trap "kill $HB" EXIT
 timeout -k 10 120 rocprofv3 --list-avail > $OUT/avail.txt 2>&1 || true
-grep -i -E "ICACHE|IFETCH|INST_LEVEL|SQC_TC" $OUT/avail.txt | head -40
-CMD="python3 $R/bench.py --mode env --steps 10 --warmup 2 --no-cpu --env-steps 0 --other-steps 0 --start-steps 0 --age-steps 700 --stagger 600"
-timeout -s KILL 300 rocprofv3 --kernel-trace --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_IFETCH -d $OUT/ic -o run --output-format csv -- $CMD > $OUT/ic.log 2>&1 || { tail $OUT/ic.log; exit 1; }
-python3 - $OUT/ic <<'PY'
+grep -i -E "ICACHE|IFETCH|INST_LEVEL|SQC_TC" $OUT/avail.txt > $OUT/avail_ic.txt || true
+CMD="python3 $R/bench.py --mode env --steps 10 --warmup 2 --no-cpu --env-steps 0 --other-steps 0 --start-steps 0 --age-steps 250 --stagger 250"
+timeout -s KILL 420 rocprofv3 --kernel-trace --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_IFETCH -d $OUT/ic -o run --output-format csv -- $CMD > $OUT/ic.log 2>&1 || { tail $OUT/ic.log; exit 1; }
+python3 - $OUT/ic > $OUT/icache.txt <<'PY'
 import csv, glob, sys, collections
 f = glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True)[0]
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
@@ -22,4 +22,4 @@ for k, d in acc.items():
     if "env_step" in k or "orders" in k:
         print(k, {c: sum(v[-5:]) / len(v[-5:]) for c, v in d.items()})
 PY
-rm -rf $OUT/ic
+cat $OUT/icache.txt; rm -rf $OUT/ic
