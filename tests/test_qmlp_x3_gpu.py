@@ -274,6 +274,33 @@ def test_fused_learn_chain_matches_separate_launches(hook):
         assert torch.equal(got, want)
 
 
+@pytest.mark.parametrize("grid,xr", [(48, "all"), (128, "robot_range")])
+def test_x3_static_table_vs_float64(grid, xr):
+    """evx_qmlp_stat in x3 (the act table: fc1's pre-activation, bias included) against the same in
+    float64 on the table's own observations (every window centre at the last fire step, zero
+    occupancy), within the x3 products' 2^-16 relative rounding: grid 48 over every centre (a
+    ragged last row tile), grid 128 over Map.robot_range's columns (the trainer's table)."""
+    _need_gpu()
+    from evacx.qmlp import K1
+    from evacx.qnet import Learner
+    lay, env = _env_obs(E=8, steps=2, R=2, grid=grid, people=300)
+    c = lay.c
+    lr = Learner(kind="mlp", precision="f32", seed=41)
+    x_range = (max(int(c.rx_lo), 0), min(int(c.rx_hi), int(c.L) + 1)) if xr == "robot_range" else None
+    lr.fast.attach_static(c, int(c.L), int(c.W), int(c.t_max), x_range=x_range)
+    ob, T = lr.fast._static[1], lr.fast._static[2]
+    n = ob.shape[0]
+    torch.cuda.synchronize()
+    X = env.expand_obs(torch.float32, ob.reshape(-1)).reshape(n, K1).double()
+    sd = lr.online.state_dict()
+    W1, b1 = sd["fc1.weight"].double(), sd["fc1.bias"].double()
+    ref = X @ W1.t() + b1
+    bound = X.abs() @ W1.abs().t() + b1.abs()  # |terms|: the x3 rounding is relative to them
+    err = (T.double() - ref).abs()
+    assert torch.isfinite(T).all()
+    assert (err <= 4e-5 * bound + 1e-7).all(), float((err / (bound + 1e-12)).max())
+
+
 @pytest.mark.parametrize("xr", ["all", "robot_range"])
 def test_x3_act_static_table_and_env_order(xr):
     """x3 act fast path: rows whose fire has reached the layout's last step start fc1 from the
