@@ -1641,6 +1641,17 @@ __global__ __launch_bounds__(256) void x_expand_kernel(Fwd a) {
     for (int k = 0; k < 4; k++) *reinterpret_cast<uint4*>(a.x + (size_t)row * K1X + 8 * (t + 20 * k)) = v[k];
 }
 
+// The learner's online (SAVE) and target forwards through the act table in one launch of 2 x the
+// 64-row tiles (blockIdx.y = net), for batches whose separate launches would each fill at most one
+// round of workgroups (evx_qmlp_forward2 at 8192 <= B < 32768: cfg5's B = 8192 -- one round for both
+// nets instead of qfc1 + qfc23; at B = 32768 the paired form measured no faster than two launches).
+template <int DM>
+__global__ __launch_bounds__(256, 2) void qfwd2_kernel(Fwd a0, Fwd a1) {
+    extern __shared__ __attribute__((aligned(16))) char dsm[];
+    if (blockIdx.y == 0) act3h_tile<DM, true>(a0, dsm, (int)blockIdx.x * 64);
+    else act3h_tile<DM, false>(a1, dsm, (int)blockIdx.x * 64);
+}
+
 // ------------------------------------------------------------ fc2 + fc3
 // X3: A = H1 hi / lo planes, B = fc2.weight hi / lo (3 MFMAs per fragment pair)
 // MT = 1 (x3 only): 32-row tiles, twice the workgroups of a small batch (the LDS stages keep
@@ -2952,6 +2963,30 @@ int evx_qmlp_forward2(const evx_layout* lay, int32_t n, const evx_obs* obs0, con
     if ((p0->x3 != 0) != (p1->x3 != 0)) return mfail(-22, "qmlp_forward2: both problems in one precision");
     // (at n >= 32768 only: a fused act workgroup lives ~65 us on the full path, so below a full
     // round of workgroups the two-kernel forward wins -- B = 4096: learn 187 vs 127 us)
+    const int dm0 = a0.drop_mask ? 2 : a0.drop_thresh ? 1 : 0, dm1 = a1.drop_mask ? 2 : a1.drop_thresh ? 1 : 0;
+    if (p0->x3 && out1->q && !out1->h2 && !out1->actions && !out1->x && n >= 8192 && n < 32768 && a0.stat && a1.stat &&
+        !a0.perm && !a0.actions && a0.x && a0.h1 && a0.h1l && a0.h2 && a0.q && dm0 == dm1) {
+        // both forwards through the act tables in one launch (qfwd2_kernel), X by its own launch
+        a1.perm = nullptr;
+        a1.actions = nullptr;
+        a1.h1 = a1.h1l = nullptr;
+        {
+            static std::atomic<uint64_t> attr_done;
+            const void* kf[3] = {(const void*)evxm::qfwd2_kernel<0>, (const void*)evxm::qfwd2_kernel<1>,
+                                 (const void*)evxm::qfwd2_kernel<2>};
+            evxh::max_lds_once(attr_done, kf, 3, evxm::ACT3H_LDS);
+        }
+        const int64_t nx = (int64_t)n * 20;
+        hipLaunchKernelGGL(evxm::x_expand_kernel, dim3((unsigned)((nx + 255) / 256)), dim3(256), 0, (hipStream_t)stream, a0);
+        const dim3 grid((unsigned)((n + 63) / 64), 2);
+        if (dm0 == 2)
+            hipLaunchKernelGGL(evxm::qfwd2_kernel<2>, grid, dim3(256), evxm::ACT3H_LDS, (hipStream_t)stream, a0, a1);
+        else if (dm0 == 1)
+            hipLaunchKernelGGL(evxm::qfwd2_kernel<1>, grid, dim3(256), evxm::ACT3H_LDS, (hipStream_t)stream, a0, a1);
+        else
+            hipLaunchKernelGGL(evxm::qfwd2_kernel<0>, grid, dim3(256), evxm::ACT3H_LDS, (hipStream_t)stream, a0, a1);
+        return mlaunch("qmlp_forward2 paired");
+    }
     if (p0->x3 && out1->q && !out1->h2 && !out1->actions && !out1->x && n >= 32768) {
         // x3 learner: the second problem (the target net: Q only) through the fused act kernel
         // (H1 / H2 stay in LDS, 64-row tiles, two workgroups per CU) instead of qfc1 + qfc23

@@ -135,13 +135,14 @@ def _torch_q_gated(sd, X, g1, g2):
     return F.linear(z2 * g2, sd["fc3.weight"], sd["fc3.bias"]), z1, z2
 
 
-@pytest.mark.parametrize("B,table", [(8192, False), (32768, False), (32768, True)])
+@pytest.mark.parametrize("B,table", [(8192, False), (8192, True), (32768, False), (32768, True)])
 def test_x3_learn_at_bench_batch(B, table):
     """Two learn steps (each from the same parameters and Adam moments on both sides) at the
     bench's learn batch: cfg5's 8192 (2-tile qdz1) and cfg3's 32768 (8-tile qdz1); the online
     forward through qfc1<2,2,4,true> + qfc23, or (table: as VecTrainer runs it, the online net
-    with its act table) through x_expand_kernel + qact3h_kernel SAVE, with three quarters of the
-    s rows moved to the layout's last fire step so their tiles start fc1 from the table.
+    with its act table) through x_expand_kernel + qact3h_kernel SAVE (B = 8192: both nets in one
+    qfwd2_kernel launch), with three quarters of the s and s' rows moved to the layout's last fire
+    step so their tiles start fc1 from the tables.
     Observations: a 128x128 R16 env 40 steps into its episode (fire spreading, people moving),
     sampled without replacement into s and s'.
 
@@ -174,8 +175,9 @@ def test_x3_learn_at_bench_batch(B, table):
     lr = Learner(kind="mlp", precision="f32", seed=41, lr=1e-3)
     assert lr.fast is not None and lr.fast.x3 and lr.fused_opt  # the trainer's chain
     c = lay.c
-    if table:
+    if table:  # both nets' act tables, as VecTrainer attaches them
         lr.fast.attach_static(c, c.L, c.W, c.t_max, x_range=(max(c.rx_lo, 0), min(c.rx_hi, c.L + 1)))
+        lr.fast_t.attach_static(c, c.L, c.W, c.t_max, x_range=(max(c.rx_lo, 0), min(c.rx_hi, c.L + 1)))
     sd0 = {k: v.clone() for k, v in lr.online.state_dict().items()}
     params = {k: torch.nn.Parameter(v.clone()) for k, v in sd0.items()}
     tgt = {k: v.clone() for k, v in sd0.items()}
@@ -194,7 +196,10 @@ def test_x3_learn_at_bench_batch(B, table):
         if table:
             s_obs[:3 * B // 4, 6] = int(c.t_max)
         s_obs = s_obs.view(-1)
-        s2_obs = obs[perm[B:2 * B].to(dev)].contiguous().view(-1)
+        s2_obs = obs[perm[B:2 * B].to(dev)].contiguous()
+        if table:
+            s2_obs[B // 4:, 6] = int(c.t_max)
+        s2_obs = s2_obs.view(-1)
         a = torch.randint(0, 5, (B,), generator=gh, dtype=torch.int32).to(dev)
         r = (torch.randn(B, generator=gh) * 30).to(dev)
         d = (torch.rand(B, generator=gh) < 0.05).to(torch.uint8).to(dev)
