@@ -166,6 +166,9 @@ def parse():
                     help="per_robot: every robot index has its own Q-network, memory and optimizer (SURVEY F3; "
                          "grouped launches, batch / robots transitions per net); qmix: those nets under a QMIX mixer "
                          "(batch / robots joint env-steps)")
+    ap.add_argument("--act-table", choices=["auto", "on", "off"], default="auto",
+                    help="x3 act table path (the per-centre table of fc1's static features, rebuilt every "
+                         "update); auto: the trainer's choice")
     ap.add_argument("--groups", type=int, default=1,
                     help="env groups per GPU, each with its own act -> env.step -> push stream chain "
                          "(evacx.trainer._Group): one group's env.step tail overlaps the others' work")
@@ -275,7 +278,8 @@ def main():
                         grad_hook=hook,
                         lagged_learn=args.schedule == "lagged", replay=args.replay,
                         replay_capacity=cap, groups=args.groups if args.mode == "train" else 1,
-                        layout_of=layout_of, world_envs=E * world, nets=args.nets)
+                        layout_of=layout_of, world_envs=E * world, nets=args.nets,
+                        act_table=None if args.act_table == "auto" else args.act_table == "on")
         env = tr.env
         gid = torch.arange(E, device="cuda") + rank * E
         S = args.stagger

@@ -137,7 +137,7 @@ class VecTrainer:
                  grad_hook=None, learn_every: int = 1, lagged_learn: bool = False, replay: str = "uniform",
                  prio_alpha: float = 0.6, prio_beta0: float = 0.4, prio_beta_steps: int = 100000,
                  prio_eps: float = 1e-6, groups: int = 1, layout_of=None, world_envs: Optional[int] = None,
-                 nets: str = "shared"):
+                 nets: str = "shared", act_table: Optional[bool] = None):
         """groups: the envs are split into this many parts, each stepping on its own
         stream chain (see _Group), group g's act after group g - 1's (it overlaps that
         group's env.step); neither the env results nor the act's dropout masks (one stream
@@ -253,7 +253,9 @@ class VecTrainer:
         if self.fast is None:
             self.lagged = False  # the lagged schedule's two-phase learn needs the fused MLP path
         self._perm = None
-        if self.fast is not None and self.fast.x3 and layout_of is None:
+        if act_table is None:
+            act_table = True
+        if self.fast is not None and self.fast.x3 and layout_of is None and act_table:
             # act fast path: envs past the fire's last step start fc1 from a per-centre table of the
             # static features' contribution (rebuilt with every weight update) and add only the
             # occupancy columns; the act visits those envs first (VecEnv.act_perm) so its row tiles
