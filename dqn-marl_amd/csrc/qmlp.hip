@@ -183,6 +183,9 @@ struct Fwd {
     // grouped act (evx_qmlp_act_g): gn nets interleaved in the shared row buffers -- batch row i
     // of net g reads / writes row i * gn + g (0: not interleaved)
     int gn, g;
+    // fc1_tile<.., XIN>: the rows' x3 compact inputs [N][640] bf16 (X as x_expand_kernel writes it) in
+    // place of generating them from the observations (evx_qmlp_stat_x: the act table's static rows)
+    const __bf16* xin;
     // persistent x3 act (evx_qmlp_fwd_out.act_ws, or NULL): [0] tiles left to the 64-row kernel,
     // [1] qact3h_rest_kernel's finished workgroups, [2 ..] those tiles
     int* rest_ws;
@@ -279,9 +282,11 @@ __device__ __forceinline__ uint2 cell_feat(const evx_obs& ob, int c, uint32_t v)
 // Column tile nt of a wave starts at ncol0 + nt * nstride.
 // KU: K-loop unroll (0: the compiler's choice; the x3 act passes 2 -- fully unrolled, the
 // per-chunk feature offsets were hoisted into ~70 live VGPRs and spilled)
-template <int MT, int NTW, int NWV, bool X3 = false, int KU = 0>
+// XIN (x3): the A rows read from a.xin (16-B pieces of X at the positions the generator writes them)
+template <int MT, int NTW, int NWV, bool X3 = false, int KU = 0, bool XIN = false>
 __device__ __forceinline__ void fc1_tile(const Fwd& a, int m0, int ncol0, bool want_x, char* smem,
                                          f32x16 (&acc)[MT][NTW], int nstride = 32) {
+    static_assert(!XIN || X3, "X input: the x3 layout");
     constexpr int NT = 64 * NWV, RT = 32 * MT;
     constexpr int CPT = 8 * RT / NT, TPR = 8 / CPT;  // cells per thread and chunk, threads per row
     static_assert(CPT == 2 || CPT == 4, "generator: 16-B A stores");
@@ -293,10 +298,10 @@ __device__ __forceinline__ void fc1_tile(const Fwd& a, int m0, int ncol0, bool w
     const int gr = tid / TPR, gc = (tid % TPR) * CPT, gl = (tid % TPR) * LPT;
     const bool rowok = m0 + gr < a.N;
     evx_obs ob;
-    if (rowok) {
-        ob = a.obs[orow(a, m0 + gr)];
-    } else {
+    if (XIN || !rowok) {
         ob = evx_obs{{0u, 0u, 0u, 0u}, 0, 0, 0, 0};
+    } else {
+        ob = a.obs[orow(a, m0 + gr)];
     }
     const bool wx = a.x && rowok && want_x;
     const int fbase = feat_base(a, ob);
@@ -305,8 +310,16 @@ __device__ __forceinline__ void fc1_tile(const Fwd& a, int m0, int ncol0, bool w
     if constexpr (X3) flb = (a.feats_lo ? a.feats_lo[ob.layout] : a.feat_lo) + fbase;
     uint32_t fv[CPT];
     uint32_t lv[X3 ? LPT / 2 : 1];  // residual bf16 pairs
+    constexpr int XP = CPT / 2;  // XIN: 16-B pieces per thread and chunk (CPT / 2 compact = LPT / 8 residual)
+    static_assert(!XIN || LPT / 8 == XP, "XIN: the compact and residual pieces per thread agree");
+    uint4 xr[XP];
+    const __bf16* xrow = XIN ? a.xin + (size_t)(m0 + gr) * K1X : nullptr;
     auto reads = [&](int kc) {
-        if (!X3 || kc < NKC1) {
+        if constexpr (XIN) {
+            const int c0 = kc < NKC1 ? kc * KC1 + gc * 4 : kc * KC1 + gl;
+#pragma unroll
+            for (int t = 0; t < XP; t++) xr[t] = rowok ? *reinterpret_cast<const uint4*>(xrow + c0 + 8 * t) : make_uint4(0u, 0u, 0u, 0u);
+        } else if (!X3 || kc < NKC1) {
 #pragma unroll
             for (int t = 0; t < CPT; t++) fv[t] = fb[feat_off(a, kc * 8 + gc + t)];
         } else if constexpr (X3) {
@@ -320,7 +333,11 @@ __device__ __forceinline__ void fc1_tile(const Fwd& a, int m0, int ncol0, bool w
         }
     };
     auto stash = [&](int buf, int kc) {
-        if (!X3 || kc < NKC1) {
+        if constexpr (XIN) {
+            const int c0 = kc < NKC1 ? gc * 4 : gl;
+#pragma unroll
+            for (int t = 0; t < XP; t++) *reinterpret_cast<uint4*>(&As[buf][gr][c0 + 8 * t]) = xr[t];
+        } else if (!X3 || kc < NKC1) {
 #pragma unroll
             for (int t = 0; t < CPT; t += 2) {
                 const uint2 f0 = cell_feat(ob, kc * 8 + gc + t, fv[t]), f1 = cell_feat(ob, kc * 8 + gc + t + 1, fv[t + 1]);
@@ -500,7 +517,7 @@ __device__ __forceinline__ void fc1_slab(const Fwd& a, const f32x16 (&accm)[NTW]
 // <2, 1, 4> (64 x 128). H1 is staged per 32-row slab through LDS so it leaves in
 // 16-B row segments.
 // GR (grouped, blocked): blockIdx.z = net * np + problem, net g's view of the problem
-template <int MT, int NTW, int NWV, bool X3 = false, bool GR = false>
+template <int MT, int NTW, int NWV, bool X3 = false, bool GR = false, bool XIN = false>
 __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void qfc1_kernel(Fwd a0, Fwd a1, int np) {
     Fwd ag;
     if constexpr (GR) ag = fwd_net((int)blockIdx.z % np ? a1 : a0, (int)blockIdx.z / np);
@@ -515,7 +532,7 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void qfc1_kernel(Fwd a0
     const int m0 = blockIdx.x * RT;
     const int ncol0 = blockIdx.y * NW + w * (32 * NTW);
     f32x16 acc[MT][NTW];
-    fc1_tile<MT, NTW, NWV, X3>(a, m0, ncol0, blockIdx.y == 0, smem, acc);
+    fc1_tile<MT, NTW, NWV, X3, 0, XIN>(a, m0, ncol0, blockIdx.y == 0, smem, acc);
     float bias[NTW];
 #pragma unroll
     for (int nt = 0; nt < NTW; nt++) bias[nt] = a.b1[ncol0 + nt * 32 + (lane & 31)];
@@ -2752,6 +2769,7 @@ static int make_fwd(const evx_layout* lay, const evx_obs* obs, int32_t n, const 
         return mfail(-22, "qmlp: the table's centre range must lie in [0, L + 2)");
     a.raw = nullptr;
     a.rest_ws = nullptr;
+    a.xin = nullptr;
     a.drop_mask = drop ? drop->mask : nullptr;
     if (a.drop_mask && !(dp > 0.f)) return mfail(-22, "qmlp_forward: an explicit dropout mask needs p > 0 (its scale)");
     a.feat_lo = nullptr;
@@ -2930,6 +2948,50 @@ int evx_qmlp_act(const evx_layout* lay, const evx_obs* obs, int32_t n, const evx
 int evx_qmlp_act64(const evx_layout* lay, const evx_obs* obs, int32_t n, const evx_qmlp_params* p,
                    const evx_qmlp_dropout* drop, const evx_qmlp_fwd_out* out, void* stream) {
     return qmlp_act_impl(lay, obs, n, p, drop, out, stream, true);
+}
+
+int evx_qmlp_expand_x3(const evx_layout* lay, const evx_obs* obs, int32_t n, uint16_t* x, void* stream) {
+    if (n <= 0) return 0;
+    if (!lay || !obs || !x) return mfail(-22, "qmlp_expand_x3: NULL argument");
+    if (!lay->obs_feat || !lay->obs_feat_lo || (lay->layout_set && (!lay->obs_feats || !lay->obs_feats_lo)))
+        return mfail(-22, "qmlp_expand_x3: layout tables missing (obs_feat, obs_feat_lo)");
+    evxm::Fwd a{};
+    a.N = n;
+    a.obs = obs;
+    a.feat = lay->obs_feat;
+    a.feats = lay->layout_set ? lay->obs_feats : nullptr;
+    a.feat_lo = lay->obs_feat_lo;
+    a.feats_lo = lay->layout_set ? lay->obs_feats_lo : nullptr;
+    a.L = lay->L;
+    a.W = lay->W;
+    a.t_max = lay->t_max;
+    a.x = reinterpret_cast<__bf16*>(x);
+    const int64_t nx = (int64_t)n * 20;
+    hipLaunchKernelGGL(evxm::x_expand_kernel, dim3((unsigned)((nx + 255) / 256)), dim3(256), 0, (hipStream_t)stream, a);
+    return mlaunch("qmlp_expand_x3");
+}
+
+int evx_qmlp_stat_x(const evx_layout* lay, const evx_obs* obs, const uint16_t* x, int32_t n, const evx_qmlp_params* p,
+                    float* out, void* stream) {
+    if (!x) return evx_qmlp_stat(lay, obs, n, p, out, stream);
+    if (n <= 0) return 0;
+    if (!out || !p) return mfail(-22, "qmlp_stat_x: NULL argument");
+    if (!p->x3) return mfail(-22, "qmlp_stat_x: the X input is the x3 layout (p->x3)");
+    evx_qmlp_fwd_out o{};
+    o.h1 = reinterpret_cast<uint16_t*>(out);  // not written in raw mode
+    evxm::Fwd a;
+    int rc = make_fwd(lay, obs, n, p, nullptr, &o, a);
+    if (rc) return rc;
+    a.h1 = nullptr;
+    a.h1l = nullptr;
+    a.stat = nullptr;
+    a.perm = nullptr;
+    a.raw = out;
+    a.xin = reinterpret_cast<const __bf16*>(x);
+    const unsigned blocks = (unsigned)((n + evxm::RM - 1) / evxm::RM);
+    hipLaunchKernelGGL((evxm::qfc1_kernel<2, 1, 4, true, false, true>), dim3(blocks, 4, 1), dim3(256), 0,
+                       (hipStream_t)stream, a, a, 1);
+    return mlaunch("qmlp_stat_x");
 }
 
 int evx_qmlp_stat(const evx_layout* lay, const evx_obs* obs, int32_t n, const evx_qmlp_params* p, float* out,

@@ -62,6 +62,10 @@ def mlib():
         L.evx_qmlp_last_error.restype = C.c_char_p
         L.evx_qmlp_pack.argtypes = [C.c_void_p] * 9
         L.evx_qmlp_pack3.argtypes = [C.c_void_p] * 11
+        if hasattr(L, "evx_qmlp_stat_x"):  # (absent from older builds loaded through EVX_LIB for A/Bs)
+            L.evx_qmlp_stat_x.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(evx_qmlp_params),
+                                          C.c_void_p, C.c_void_p]
+            L.evx_qmlp_expand_x3.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
         L.evx_qmlp_stat.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(evx_qmlp_params), C.c_void_p,
                                     C.c_void_p]
         L.evx_qmlp_forward.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(evx_qmlp_params),
@@ -251,17 +255,30 @@ class MLPFast:
         ob[:, 4], ob[:, 5], ob[:, 6] = cx.ravel(), cy.ravel(), t_max
         self._static = (lay_c, torch.from_numpy(ob).to(self.device),
                         torch.empty(nx * (W + 2), HID, dtype=torch.float32, device=self.device))
+        # x3: the table rows' fc1 inputs are fixed (every centre at the last fire step, no occupancy):
+        # expanded once here, every rebuild reads them (evx_qmlp_stat_x) instead of regenerating them
+        self._static_x = None
+        if self.x3 and hasattr(mlib(), "evx_qmlp_stat_x"):
+            n = self._static[1].shape[0]
+            self._static_x = torch.empty(n * K1X, dtype=torch.int16, device=self.device)
+            mcheck(mlib().evx_qmlp_expand_x3(C.byref(lay_c), self._static[1].data_ptr(), n,
+                                             self._static_x.data_ptr(), _stream()), "qmlp_expand_x3")
         self._rebuild_static()
         self.c.w1o, self.c.stat, self.c.stat_fs = self.w1o.data_ptr(), self._static[2].data_ptr(), int(t_max)
         self.c.stat_x0, self.c.stat_nx = x0, nx
 
     def detach_static(self):
         self._static = None
+        self._static_x = None
         self.c.w1o = self.c.stat = None
         self.c.stat_x0 = self.c.stat_nx = 0
 
     def _rebuild_static(self):
         lay_c, ob, T = self._static
+        if getattr(self, "_static_x", None) is not None:
+            mcheck(mlib().evx_qmlp_stat_x(C.byref(lay_c), ob.data_ptr(), self._static_x.data_ptr(), ob.shape[0],
+                                          C.byref(self.c), T.data_ptr(), _stream()), "qmlp_stat_x")
+            return
         self.stat_table(lay_c, ob, ob.shape[0], T)
 
     def stat_table(self, lay_c, obs: torch.Tensor, n: int, out: torch.Tensor):

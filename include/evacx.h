@@ -478,6 +478,14 @@ int evx_qmlp_pack_occ3(const float *w1, uint16_t *w1o, uint16_t *w1ol, void *str
  * act fast path's table (evx_qmlp_params.stat; rebuild after every weight update) */
 int evx_qmlp_stat(const evx_layout *lay, const evx_obs *obs, int32_t n, const evx_qmlp_params *p, float *out,
                   void *stream);
+/* x3: the rows' compact fc1 inputs [n][640] bf16 (4 features per cell, then the cells' danger
+ * residuals: the X of evx_qmlp_fwd_out.x) of n observations */
+int evx_qmlp_expand_x3(const evx_layout *lay, const evx_obs *obs, int32_t n, uint16_t *x, void *stream);
+/* evx_qmlp_stat (x3) from the rows' X of evx_qmlp_expand_x3 instead of their observations: the same
+ * table bit for bit, with fc1's A operand read instead of generated (the act table's rows are fixed,
+ * so their X is expanded once; x NULL: evx_qmlp_stat) */
+int evx_qmlp_stat_x(const evx_layout *lay, const evx_obs *obs, const uint16_t *x, int32_t n, const evx_qmlp_params *p,
+                    float *out, void *stream);
 int evx_qmlp_forward(const evx_layout *lay, const evx_obs *obs, int32_t n, const evx_qmlp_params *p,
                      const evx_qmlp_dropout *drop, const evx_qmlp_fwd_out *out, void *stream);
 /* DQNAgent.act (agents/dqn_agent.py:101-124) in one launch: the forward of

@@ -290,7 +290,13 @@ def test_x3_static_table_vs_float64(grid, xr):
     lr.fast.attach_static(c, int(c.L), int(c.W), int(c.t_max), x_range=x_range)
     ob, T = lr.fast._static[1], lr.fast._static[2]
     n = ob.shape[0]
+    # the rebuild reads the rows' X expanded once (evx_qmlp_stat_x): the table generated from the
+    # observations (evx_qmlp_stat) is the same bit for bit
+    assert lr.fast._static_x is not None
+    T_gen = torch.empty_like(T)
+    lr.fast.stat_table(c, ob, n, T_gen)
     torch.cuda.synchronize()
+    assert torch.equal(T, T_gen)
     X = env.expand_obs(torch.float32, ob.reshape(-1)).reshape(n, K1).double()
     sd = lr.online.state_dict()
     W1, b1 = sd["fc1.weight"].double(), sd["fc1.bias"].double()
