@@ -186,6 +186,8 @@ struct Fwd {
     // fc1_tile<.., XIN>: the rows' x3 compact inputs [N][640] bf16 (X as x_expand_kernel writes it) in
     // place of generating them from the observations (evx_qmlp_stat_x: the act table's static rows)
     const __bf16* xin;
+    // x_expand_kernel: the act table rows' X (evx_qmlp_params.stat_xin, rows as a.stat's), or NULL
+    const __bf16* xtab;
     // persistent x3 act (evx_qmlp_fwd_out.act_ws, or NULL): [0] tiles left to the 64-row kernel,
     // [1] qact3h_rest_kernel's finished workgroups, [2 ..] those tiles
     int* rest_ws;
@@ -1631,6 +1633,27 @@ __global__ __launch_bounds__(256) void x_expand_kernel(Fwd a) {
     const int row = (int)(i / 20), t = (int)(i - (int64_t)row * 20);
     if (row >= a.N) return;
     const evx_obs ob = a.obs[orow(a, row)];
+    if (a.xtab && a.stat && min(max(ob.fire_step, 0), a.t_max) == a.stat_fs && ob.cx >= a.stat_x0 &&
+        ob.cx < a.stat_x0 + a.stat_nx && ob.cy >= 0 && ob.cy <= a.W + 1) {
+        // a table row: its static inputs are the table row's X (occupancy 0); the occupancy bits of
+        // cells 2q, 2q + 1 go into the low halves of words 0 and 2 of piece q < 64 (cell_feat's encoding)
+        const __bf16* src = a.xtab + (size_t)((ob.cx - a.stat_x0) * (a.W + 2) + ob.cy) * K1X;
+        uint4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) v[k] = *reinterpret_cast<const uint4*>(src + 8 * (t + 20 * k));
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int q = t + 20 * k;
+            if (q < 64) {
+                const int c0 = 2 * q, w = c0 >> 5;  // cells c0, c0 + 1 share an occupancy word
+                const uint32_t ow = w == 0 ? ob.occ[0] : w == 1 ? ob.occ[1] : w == 2 ? ob.occ[2] : ob.occ[3];
+                v[k].x |= c0 < NCELL ? ((ow >> (c0 & 31)) & 1u) * 0x3f80u : 0u;
+                v[k].z |= c0 + 1 < NCELL ? ((ow >> ((c0 + 1) & 31)) & 1u) * 0x3f80u : 0u;
+            }
+            *reinterpret_cast<uint4*>(a.x + (size_t)row * K1X + 8 * q) = v[k];
+        }
+        return;
+    }
     const int fbase = feat_base(a, ob);
     const uint32_t* fb = (a.feats ? a.feats[ob.layout] : a.feat) + fbase;
     const uint16_t* flb = (a.feats_lo ? a.feats_lo[ob.layout] : a.feat_lo) + fbase;
@@ -2770,6 +2793,7 @@ static int make_fwd(const evx_layout* lay, const evx_obs* obs, int32_t n, const 
     a.raw = nullptr;
     a.rest_ws = nullptr;
     a.xin = nullptr;
+    a.xtab = (p->x3 && a.stat) ? reinterpret_cast<const __bf16*>(p->stat_xin) : nullptr;
     a.drop_mask = drop ? drop->mask : nullptr;
     if (a.drop_mask && !(dp > 0.f)) return mfail(-22, "qmlp_forward: an explicit dropout mask needs p > 0 (its scale)");
     a.feat_lo = nullptr;

@@ -33,7 +33,7 @@ def compact_ref_cols() -> np.ndarray:
 class evx_qmlp_params(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in ["w1", "b1c", "w2", "w2t", "b2", "w3", "b3", "w1o", "stat"]] + \
         [("stat_fs", C.c_int32), ("x3", C.c_int32)] + [(n, C.c_void_p) for n in ["w1l", "w2l", "w2tl", "w1ol"]] + \
-        [("stat_x0", C.c_int32), ("stat_nx", C.c_int32)]
+        [("stat_x0", C.c_int32), ("stat_nx", C.c_int32), ("stat_xin", C.c_void_p)]
 
 
 class evx_qmlp_dropout(C.Structure):
@@ -266,11 +266,12 @@ class MLPFast:
         self._rebuild_static()
         self.c.w1o, self.c.stat, self.c.stat_fs = self.w1o.data_ptr(), self._static[2].data_ptr(), int(t_max)
         self.c.stat_x0, self.c.stat_nx = x0, nx
+        self.c.stat_xin = None if self._static_x is None else self._static_x.data_ptr()
 
     def detach_static(self):
         self._static = None
         self._static_x = None
-        self.c.w1o = self.c.stat = None
+        self.c.w1o = self.c.stat = self.c.stat_xin = None
         self.c.stat_x0 = self.c.stat_nx = 0
 
     def _rebuild_static(self):

@@ -423,6 +423,10 @@ typedef struct {
     /* the table's window centres: x in [stat_x0, stat_x0 + stat_nx) (Map.robot_range: robots never
      * leave it), every y in [0, W + 1], row (x - stat_x0) * (W + 2) + y; stat_nx = 0: all L + 2 */
     int32_t stat_x0, stat_nx;
+    /* x3, optional: the table rows' fc1 inputs (evx_qmlp_expand_x3 of the table's observations, the X of
+     * evx_qmlp_stat_x): the learner's X of a batch row on the table path is that row of it plus the
+     * row's occupancy bits (copied instead of regenerated; the same bits) */
+    const uint16_t *stat_xin;
 } evx_qmlp_params;
 
 typedef struct {
