@@ -1293,7 +1293,7 @@ __global__ __launch_bounds__(256, 1) void qact3h_rest_kernel(Fwd a) {
             }
         }
         __syncthreads();
-        nh = 2 * bad[0];
+        nh = 2 * min(max(bad[0], 0), (a.N + 127) / 128);  // (bounded by the list's length)
         h0 = (int)blockIdx.x;
         hs = (int)gridDim.x;
     } else {
@@ -1552,7 +1552,10 @@ __global__ __launch_bounds__(512, 2) void qact3p_kernel(Fwd a, int ntiles) {
                 setup_rows(tile, cur, ok, nullptr, 0);
                 fast = __syncthreads_and(ok);
                 if (fast) break;  // else qact3h_rest_kernel's: listed for it
-                if (tid == 0 && a.rest_ws) a.rest_ws[2 + atomicAdd(a.rest_ws, 1)] = tile;
+                if (tid == 0 && a.rest_ws) {  // (a count past ntiles: a workspace not zeroed -- nothing written)
+                    const int k = atomicAdd(a.rest_ws, 1);
+                    if (k >= 0 && k < ntiles) a.rest_ws[2 + k] = tile;
+                }
             }
             if (!fast) break;
             load_occ(tile * 128);
@@ -2092,9 +2095,10 @@ __global__ __launch_bounds__(256) void qbwd3_kernel(Bwd a0, int rb) {
 // every chunk waiting out a memory latency with one wave per SIMD: 120 us at B = 32768.)
 constexpr int QZ_P = HID2 + 8;  // LDS row pitch (bf16): 528 B, conflict-free ds_read_b128 rows
 constexpr int QZ_CP = 128 + 8;  // the dZ1 tile's row pitch (bf16)
+constexpr int QZ_RM = 32;        // rows per dZ1 tile
 static_assert(QZ_CP <= QZ_P, "each dZ1 plane overlays a dZ2 plane");
 template <bool X3>
-constexpr int qdz1_lds_bytes() { return (X3 ? 2 : 1) * RM * QZ_P * 2 + 2 * RM * 16; }  // + 2 tiles of [H1 > 0] bits
+constexpr int qdz1_lds_bytes() { return (X3 ? 2 : 1) * QZ_RM * QZ_P * 2 + 2 * QZ_RM * 16; }  // + 2 tiles of [H1 > 0] bits
 // Row tiles per qdz1 workgroup: the tiles' column sums (db1 and the centre column of dW1) leave
 // as one partial row pz1[bx] per workgroup row, which reduce2_kernel adds in bx order; fewer,
 // longer workgroups keep that reduction short. Up to QZ_RT tiles per workgroup while the grid
@@ -2104,56 +2108,58 @@ inline int qdz1_tiles_per_wg(int B) { return B / 4096 < 1 ? 1 : (B / 4096 > QZ_R
 template <bool X3 = false>
 __device__ __forceinline__ void qdz1_body(const Bwd& a, char* smem, int bx, int by, int ndzx) {
     constexpr int NPL = X3 ? 2 : 1;
-    auto As = reinterpret_cast<__bf16 (*)[RM][QZ_P]>(smem);  // [NPL][RM][QZ_P]
-    // [H1 > 0] of the tile's 64 rows x 128 columns as bits (byte b of a row: columns 8b .. 8b + 7),
+    auto As = reinterpret_cast<__bf16 (*)[QZ_RM][QZ_P]>(smem);  // [NPL][QZ_RM][QZ_P]
+    // [H1 > 0] of the tile's rows x 128 columns as bits (byte b of a row: columns 8b .. 8b + 7),
     // double-buffered by tile parity: H1 arrives with dZ2 in 16-B row pieces instead of the
     // 2-B loads of the accumulator layout (which cost 75 us at B = 32768)
-    auto Ms = reinterpret_cast<uint32_t (*)[RM][4]>(smem + NPL * RM * QZ_P * 2);  // [2][RM][4]
+    auto Ms = reinterpret_cast<uint32_t (*)[QZ_RM][4]>(smem + NPL * QZ_RM * QZ_P * 2);  // [2][QZ_RM][4]
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
     const int n0 = by * 128 + w * 32, col = n0 + (lane & 31);
-    const int nrt = (a.B + RM * ndzx - 1) / (RM * ndzx);  // row tiles per workgroup
-    const int t0 = bx * nrt, nt = min(nrt, (a.B + RM - 1) / RM - t0);
-    // staging: 16-B piece j of thread t = (row c >> 5, k 8 (c & 31)) for c = t + 256 j: a wave
-    // reads two whole 512-B rows per plane and piece
-    uint4 pre[NPL][8], hpre[4];
+    const int nrt = (a.B + QZ_RM * ndzx - 1) / (QZ_RM * ndzx);  // row tiles per workgroup
+    const int t0 = bx * nrt, nt = min(nrt, (a.B + QZ_RM - 1) / QZ_RM - t0);
+    constexpr int DP = QZ_RM * 32 / 256;  // dZ2 16-B pieces per thread and plane (a row: 32 pieces)
+    constexpr int HP = QZ_RM * 16 / 256;  // H1 (and dZ1) 16-B pieces per thread and plane (a row: 16)
+    // W2^T of the wave's 32 columns, every k-step, hi and lo: held in registers for all the workgroup's
+    // row tiles (weight-stationary: streamed from L2 per 64-row tile it moved 128 KB per tile)
+    bf16x8 bw[HID2 / 16][NPL];
+#pragma unroll
+    for (int ks = 0; ks < HID2 / 16; ks++) {
+        const size_t o = w2t_tile(n0 >> 5, ks >> 1, ks & 1) + lane * 8;
+        bw[ks][0] = *reinterpret_cast<const bf16x8*>(a.w2t + o);
+        if constexpr (X3) bw[ks][NPL - 1] = *reinterpret_cast<const bf16x8*>(a.w2tl + o);
+    }
+    // staging: 16-B piece j of thread t = (row c >> 5, k 8 (c & 31)) for c = t + 256 j
+    uint4 pre[NPL][DP], hpre[HP];
     auto fetch = [&](int m0) {
 #pragma unroll
-        for (int j = 0; j < 4; j++) {  // H1 piece j: row (c >> 4), columns 128 by + 8 (c & 15), c = t + 256 j
+        for (int j = 0; j < HP; j++) {  // H1 piece j: row (c >> 4), columns 128 by + 8 (c & 15), c = t + 256 j
             const int c = tid + 256 * j, row = m0 + (c >> 4);
             hpre[j] = make_uint4(0u, 0u, 0u, 0u);
-#ifndef QZ_NOH1
             if (row < a.B) hpre[j] = *reinterpret_cast<const uint4*>(a.h1 + (size_t)row * HID + by * 128 + (c & 15) * 8);
-#endif
         }
 #pragma unroll
         for (int p = 0; p < NPL; p++)
 #pragma unroll
-            for (int j = 0; j < 8; j++) {
+            for (int j = 0; j < DP; j++) {
                 const int c = tid + 256 * j, row = m0 + (c >> 5);
                 pre[p][j] = make_uint4(0u, 0u, 0u, 0u);
-#ifndef QZ_NOFETCH
                 if (row < a.B) pre[p][j] = *reinterpret_cast<const uint4*>((p ? a.dz2l : a.dz2) + (size_t)row * HID2 + (c & 31) * 8);
-#endif
             }
     };
-    auto loadB = [&](int ks, bf16x8 (&b)[NPL]) {  // k-step ks (16 k) of the wave's 32 columns
-        b[0] = *reinterpret_cast<const bf16x8*>(a.w2t + w2t_tile(n0 >> 5, ks >> 1, ks & 1) + lane * 8);
-        if constexpr (X3) b[NPL - 1] = *reinterpret_cast<const bf16x8*>(a.w2tl + w2t_tile(n0 >> 5, ks >> 1, ks & 1) + lane * 8);
-    };
-    constexpr int NKS = HID2 / 16, RING = 4;
+    constexpr int NKS = HID2 / 16;
     float cs = 0.f;
-    if (nt > 0) fetch(t0 * RM);
+    if (nt > 0) fetch(t0 * QZ_RM);
     for (int t = 0; t < nt; t++) {
-        const int m0 = (t0 + t) * RM;
+        const int m0 = (t0 + t) * QZ_RM;
 #pragma unroll
         for (int p = 0; p < NPL; p++)
 #pragma unroll
-            for (int j = 0; j < 8; j++) {
+            for (int j = 0; j < DP; j++) {
                 const int c = tid + 256 * j;
                 *reinterpret_cast<uint4*>(&As[p][c >> 5][(c & 31) * 8]) = pre[p][j];
             }
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
+        for (int j = 0; j < HP; j++) {
             const int c = tid + 256 * j;
             const uint32_t wv[4] = {hpre[j].x, hpre[j].y, hpre[j].z, hpre[j].w};
             uint32_t bits = 0u;
@@ -2164,56 +2170,42 @@ __device__ __forceinline__ void qdz1_body(const Bwd& a, char* smem, int bx, int 
             }
             reinterpret_cast<uint8_t*>(&Ms[t & 1][c >> 4][0])[c & 15] = (uint8_t)bits;
         }
-        bf16x8 bq[RING][NPL];
-#pragma unroll
-        for (int i = 0; i < RING; i++) loadB(i, bq[i]);
         __syncthreads();
-        if (t + 1 < nt) fetch(m0 + RM);
-        f32x16 acc[2];
+        if (t + 1 < nt) fetch(m0 + QZ_RM);
+        f32x16 acc;
 #pragma unroll
-        for (int i = 0; i < 2; i++)
-#pragma unroll
-            for (int r = 0; r < 16; r++) acc[i][r] = 0.f;
+        for (int r = 0; r < 16; r++) acc[r] = 0.f;
 #pragma unroll
         for (int ks = 0; ks < NKS; ks++) {
-            bf16x8 bc[NPL];
-#pragma unroll
-            for (int p = 0; p < NPL; p++) bc[p] = bq[ks % RING][p];
-            if (ks + RING < NKS) loadB(ks + RING, bq[ks % RING]);
-#pragma unroll
-            for (int mt = 0; mt < 2; mt++) {
-                const bf16x8 av = *reinterpret_cast<const bf16x8*>(&As[0][mt * 32 + (lane & 31)][ks * 16 + 8 * h]);
-                acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bc[0], acc[mt], 0, 0, 0);
-                if constexpr (X3) {
-                    const bf16x8 al = *reinterpret_cast<const bf16x8*>(&As[NPL - 1][mt * 32 + (lane & 31)][ks * 16 + 8 * h]);
-                    acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bc[NPL - 1], acc[mt], 0, 0, 0);
-                    acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bc[0], acc[mt], 0, 0, 0);
-                }
+            const bf16x8 av = *reinterpret_cast<const bf16x8*>(&As[0][lane & 31][ks * 16 + 8 * h]);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bw[ks][0], acc, 0, 0, 0);
+            if constexpr (X3) {
+                const bf16x8 al = *reinterpret_cast<const bf16x8*>(&As[NPL - 1][lane & 31][ks * 16 + 8 * h]);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bw[ks][NPL - 1], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bw[ks][0], acc, 0, 0, 0);
             }
         }
         __syncthreads();  // every wave is done with the tile's dZ2: its LDS takes the dZ1 tile
         // dZ1 (hi / lo planes) through LDS over the dZ2 image, so that it leaves in 16-B row
         // pieces rather than 2-B stores of the accumulator layout
-        auto Cs = reinterpret_cast<__bf16 (*)[RM][QZ_CP]>(smem);  // [NPL][RM][QZ_CP]
+        auto Cs = reinterpret_cast<__bf16 (*)[QZ_RM][QZ_CP]>(smem);  // [NPL][QZ_RM][QZ_CP]
 #pragma unroll
-        for (int mt = 0; mt < 2; mt++)
-#pragma unroll
-            for (int r = 0; r < 16; r++) {
-                const int rl = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                const bool pos = (Ms[t & 1][rl][w] >> (lane & 31)) & 1u;
-                const float v = pos && m0 + rl < a.B ? acc[mt][r] * a.scale : 0.f;
-                if constexpr (X3) {
-                    split2(v, Cs[0][rl][w * 32 + (lane & 31)], Cs[NPL - 1][rl][w * 32 + (lane & 31)]);
-                } else {
-                    Cs[0][rl][w * 32 + (lane & 31)] = (__bf16)v;
-                }
-                cs += v;
+        for (int r = 0; r < 16; r++) {
+            const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;
+            const bool pos = (Ms[t & 1][rl][w] >> (lane & 31)) & 1u;
+            const float v = pos && m0 + rl < a.B ? acc[r] * a.scale : 0.f;
+            if constexpr (X3) {
+                split2(v, Cs[0][rl][w * 32 + (lane & 31)], Cs[NPL - 1][rl][w * 32 + (lane & 31)]);
+            } else {
+                Cs[0][rl][w * 32 + (lane & 31)] = (__bf16)v;
             }
+            cs += v;
+        }
         __syncthreads();
 #pragma unroll
         for (int p = 0; p < NPL; p++)
 #pragma unroll
-            for (int j = 0; j < 4; j++) {  // piece j: row c >> 4, columns 8 (c & 15), c = t + 256 j
+            for (int j = 0; j < HP; j++) {  // piece j: row c >> 4, columns 8 (c & 15), c = t + 256 j
                 const int c = tid + 256 * j, row = m0 + (c >> 4);
                 if (row < a.B)
                     *reinterpret_cast<uint4*>((p ? a.dz1l : a.dz1) + (size_t)row * HID + by * 128 + (c & 15) * 8) =
