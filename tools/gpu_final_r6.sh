@@ -18,4 +18,5 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/t -o run --output-for
     --no-cpu --other-steps 0 --env-steps 0 --start-steps 0 > $OUT/trace_bench.json 2> $OUT/trace_bench.err || { tail -5 $OUT/trace_bench.err; exit 1; }
 find $OUT/t -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
 python3 $R/tools/step_gaps.py $OUT/t > $OUT/step_gaps.txt 2>&1 || true
+python3 $R/tools/step_kstats.py $OUT/t 20 > $OUT/kernel_stats_timed_steps.txt 2>&1 || true
 rm -rf $OUT/t
