@@ -140,7 +140,31 @@ __global__ __launch_bounds__(NT) void prio_sample_kernel(evx_replay rp, evx_prio
     double u = ((double)k + U) * (total / (double)B);
     int64_t node = 1;
     const int64_t C = t.capacity;
-    while (node < C) {
+    // two levels per round of loads: the children and the four grandchildren of node are read
+    // together (independent loads), then the same two decisions as one level at a time (the same
+    // comparisons and subtractions: the same leaf) -- half the dependent L2 round trips
+    while (2 * node < C) {
+        const double l = t.sum[2 * node], rr = t.sum[2 * node + 1];
+        const double g0 = t.sum[4 * node], g1 = t.sum[4 * node + 1], g2 = t.sum[4 * node + 2], g3 = t.sum[4 * node + 3];
+        double gl, gr;
+        if (u < l || rr <= 0.0) {
+            node = 2 * node;
+            gl = g0;
+            gr = g1;
+        } else {
+            u -= l;
+            node = 2 * node + 1;
+            gl = g2;
+            gr = g3;
+        }
+        if (u < gl || gr <= 0.0) {
+            node = 2 * node;
+        } else {
+            u -= gl;
+            node = 2 * node + 1;
+        }
+    }
+    if (node < C) {  // an odd number of levels: the last one alone
         const double l = t.sum[2 * node], rr = t.sum[2 * node + 1];
         if (u < l || rr <= 0.0) {
             node = 2 * node;

@@ -247,13 +247,6 @@ class VecTrainer:
         self.lstream = torch.cuda.Stream(device=self.device, priority=0)
         self.ev_learned = torch.cuda.Event()
         self.ev_learned.record(cur)
-        # prioritized replay, strict schedule: the priority update of learn t runs on its own stream
-        # beside clip+Adam, the act and env.step of t + 1 (nothing there reads the trees); the next
-        # expose / sample waits for it, so the trees see the same operations in the same order
-        self.pstream = torch.cuda.Stream(device=self.device, priority=0)
-        self.ev_td = torch.cuda.Event()
-        self.ev_prio = torch.cuda.Event()
-        self.ev_prio.record(cur)
         self.last_loss: Optional[torch.Tensor] = None
         # bf16 MLP: act and learn straight from compact observations (csrc/qmlp.hip)
         self.fast = self.learner.fast if self.learner is not None else None
@@ -358,7 +351,6 @@ class VecTrainer:
                 # the trees only hold exposed slots: the window is implicit (hidden slots have 0 mass)
                 beta = min(1.0, self.prio_beta0 + (1.0 - self.prio_beta0) * self.learn_steps / self.prio_beta_steps)
                 w, td = self.samp["w"], self.samp["td"]
-                torch.cuda.current_stream(self.device).wait_event(self.ev_prio)  # (free once it has run)
                 self.replay.sample_prio(self.batch, beta, self.seed + 1, self.learn_steps * self.batch, self.samp,
                                         self.samp["idx"], w)
             elif window is None:
@@ -368,26 +360,17 @@ class VecTrainer:
             else:
                 self.replay.sample_window(window[0], window[1], self.batch, self.seed + 1,
                                           self.learn_steps * self.batch, self.samp)
-            side_prio = self.prio and phase == "all" and self.fast is not None and not self.lagged
             if self.fast is not None:
                 loss = self.learner.learn_obs(self.lay.c, self.samp["s"], self.samp["a"], self.samp["r"],
-                                              self.samp["done"], self.samp["s2"], self.batch,
-                                              update=phase == "all" and not side_prio, weights=w, td_abs=td)
+                                              self.samp["done"], self.samp["s2"], self.batch, update=phase == "all",
+                                              weights=w, td_abs=td)
             else:
                 assert phase == "all", "a two-phase learn needs the fused MLP path"
                 s = self.env.expand_obs(torch.float32, self.samp["s"]).view(self.batch, 11, 11, 6)
                 s2 = self.env.expand_obs(torch.float32, self.samp["s2"]).view(self.batch, 11, 11, 6)
                 loss = self.learner.learn(s, self.samp["a"], self.samp["r"], self.samp["done"], s2, weights=w,
                                           td_abs=td)
-            if side_prio:  # |TD| is ready: the trees' update on the priority stream, then clip+Adam here
-                cur = torch.cuda.current_stream(self.device)
-                self.ev_td.record(cur)
-                with torch.cuda.stream(self.pstream):
-                    self.pstream.wait_event(self.ev_td)
-                    self.replay.update(self.samp["idx"], td, self.batch)
-                    self.ev_prio.record(self.pstream)
-                self.learner.step_optimizer()
-            elif self.prio:
+            if self.prio:
                 self.replay.update(self.samp["idx"], td, self.batch)
             if phase == "grads":
                 return loss
@@ -525,7 +508,6 @@ class VecTrainer:
                 for grp in G[1:]:
                     m.wait_event(grp.ev_push)
                 if self.prio:
-                    m.wait_event(self.ev_prio)  # the last learn's priority update (idx / td are rewritten next)
                     self.replay.expose()
                 if ev_learn is not None:
                     ev_learn[0].record(m)
@@ -548,7 +530,6 @@ class VecTrainer:
             cur.wait_event(grp.ev_order)
         cur.wait_event(self.ev_reset)
         cur.wait_event(self.ev_learned)
-        cur.wait_event(self.ev_prio)
         self.join_caller = True
 
 
