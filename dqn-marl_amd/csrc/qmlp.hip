@@ -2431,10 +2431,13 @@ struct Red2 {
     float* loss;         // qbwd3's TD step: loss[0] = the block partials' sum / B, or NULL
     int B;
 };
-// the small sums (dW3, db2, db3 from p3; db1 and W1's centre column from pz1): 64 columns per
-// workgroup, the partial rows in four contiguous quarters (one per wave), quarters added in order
+// the small sums (dW3, db2, db3 from p3; db1 and W1's centre column from pz1): 16 columns per
+// workgroup, the partial rows in 16 contiguous groups (16 lanes each), groups added in order (with
+// 64 columns x 4 groups each thread's 64-load chain of qbwd3's 256 block rows at B = 32768 was the
+// launch's tail)
 constexpr int P3L = NACT * HID2 + HID2 + NACT + 1;  // live columns of a p3 row (the gradients, the TD loss)
-constexpr int NRS3 = (P3L + 63) / 64, NRSZ = HID / 64, NRSMALL = NRS3 + NRSZ;
+constexpr int RSC = 16;                             // columns per small-sum workgroup
+constexpr int NRS3 = (P3L + RSC - 1) / RSC, NRSZ = HID / RSC, NRSMALL = NRS3 + NRSZ;
 __device__ __forceinline__ float red_sum256(float x, float* red) {
     red[threadIdx.x] = x;
     __syncthreads();
@@ -2466,8 +2469,8 @@ __global__ __launch_bounds__(256) void reduce2_kernel(Red2 r0) {
             const int m = q / nq, n = (q - m * nq) * 4;
             const float* src = r.part2 + (size_t)m * HID + n;
             float4 acc = *reinterpret_cast<const float4*>(src);
-#pragma unroll 8
-            for (int z = 1; z < r.S2; z++) {  // unrolled: 8 loads in flight, the adds still in z order
+#pragma unroll 16
+            for (int z = 1; z < r.S2; z++) {  // unrolled: 16 loads in flight, the adds still in z order
                 const float4 v = *reinterpret_cast<const float4*>(src + (size_t)z * HID2 * HID);
                 acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
             }
@@ -2484,18 +2487,26 @@ __global__ __launch_bounds__(256) void reduce2_kernel(Red2 r0) {
             const size_t zs = (size_t)HID * r.Np1;
             const float* src = r.part1 + (size_t)m * r.Np1 + n;
             float4 acc = *reinterpret_cast<const float4*>(src);
-#pragma unroll 8
-            for (int z = 1; z < r.S1; z++) {
-                const float4 v = *reinterpret_cast<const float4*>(src + (size_t)z * zs);
-                acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-            }
-            float a4[4] = {acc.x, acc.y, acc.z, acc.w};
-            if (r.remap1 == 3) {  // X3: cell n / 4's danger residual column (512 + n / 4) into its danger column
+            float a4[4];
+            if (r.remap1 == 3) {  // X3: cell n / 4's danger residual column (512 + n / 4) into its danger
+                                  // column, summed in the same loop (one chain of load rounds, not two)
                 const float* s2 = r.part1 + (size_t)m * r.Np1 + K1P + (n >> 2);
                 float d = s2[0];
-#pragma unroll 8
-                for (int z = 1; z < r.S1; z++) d += s2[(size_t)z * zs];
-                a4[1] += d;
+#pragma unroll 16
+                for (int z = 1; z < r.S1; z++) {
+                    const float4 v = *reinterpret_cast<const float4*>(src + (size_t)z * zs);
+                    const float dv = s2[(size_t)z * zs];
+                    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+                    d += dv;
+                }
+                a4[0] = acc.x; a4[1] = acc.y + d; a4[2] = acc.z; a4[3] = acc.w;
+            } else {
+#pragma unroll 16
+                for (int z = 1; z < r.S1; z++) {
+                    const float4 v = *reinterpret_cast<const float4*>(src + (size_t)z * zs);
+                    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+                }
+                a4[0] = acc.x; a4[1] = acc.y; a4[2] = acc.z; a4[3] = acc.w;
             }
 #pragma unroll
             for (int t = 0; t < 4; t++) {
@@ -2511,21 +2522,25 @@ __global__ __launch_bounds__(256) void reduce2_kernel(Red2 r0) {
             }
         }
     } else {  // the small gradients from qbwd3's / qdz1's partial rows
-        const int sb = b - r.nb2 - r.nb1, c = (int)threadIdx.x & 63, qw = (int)threadIdx.x >> 6;
+        const int sb = b - r.nb2 - r.nb1, c = (int)threadIdx.x & (RSC - 1), qw = (int)threadIdx.x / RSC;
+        constexpr int NG = 256 / RSC;  // row groups
         const bool z1 = sb >= NRS3;
-        const int col = (z1 ? sb - NRS3 : sb) * 64 + c;
+        const int col = (z1 ? sb - NRS3 : sb) * RSC + c;
         const int nrow = z1 ? r.nz1 : r.nb3, pitch = z1 ? HID : P3W, ncol = z1 ? HID : P3L;
         const float* src = (z1 ? r.pz1 : r.p3) + col;
         float acc = 0.f;
         if (col < ncol) {
-            const int r1 = (qw + 1) * nrow / 4;
+            const int r1 = (qw + 1) * nrow / NG;
 #pragma unroll 8
-            for (int i = qw * nrow / 4; i < r1; i++) acc += src[(size_t)i * pitch];
+            for (int i = qw * nrow / NG; i < r1; i++) acc += src[(size_t)i * pitch];
         }
         red[threadIdx.x] = acc;
         __syncthreads();
         if (qw == 0 && col < ncol) {
-            const float tot = (red[c] + red[64 + c]) + (red[128 + c] + red[192 + c]);
+            float tot = 0.f;  // groups in order, pairwise within each aligned quad
+#pragma unroll
+            for (int g = 0; g < NG; g += 4)
+                tot += (red[g * RSC + c] + red[(g + 1) * RSC + c]) + (red[(g + 2) * RSC + c] + red[(g + 3) * RSC + c]);
             if (z1) {
                 const float o = (r.acc ? r.gb1[col] : 0.f) + tot;
                 float* cc = r.gw1 + (size_t)col * K1 + CENTRE_COL;  // d/dW1 of the constant centre input
