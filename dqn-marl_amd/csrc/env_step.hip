@@ -3314,7 +3314,16 @@ static int heavy_cap(const evx_layout& l, int* hmin) {
     if (evx::big_grid(l.L, l.W)) return 0;  // BIGG kernels: no heavy workgroups
     const evx::WideLds wl = evx::wide_lds(l);
     if (step_launch_lds(l, evx::WNW) > 160 * 1024 || wl.end > wl.ctl) return 0;
-    return 176;
+    static const int cap_env = [] {
+        const char* v = getenv("EVX_HEAVY_CAP");
+        return v ? atoi(v) : -1;
+    }();
+    static const int min_env = [] {
+        const char* v = getenv("EVX_HEAVY_MIN");
+        return v ? atoi(v) : -1;
+    }();
+    if (min_env > 0) *hmin = min_env;
+    return cap_env >= 0 ? cap_env : 176;
 }
 
 namespace {
