@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 6 (session 2): the strict schedule's priority update on its own stream: prioritized parity /
-# (the "old" trainer: tools/ab/trainer_old.py = `git show 2c4571f:dqn-marl_amd/evacx/trainer.py`, written before the run)
 # determinism tests, cfg5 A/B (the previous commit's trainer vs this one, same library)
+# (the "old" trainer: tools/ab/trainer_old.py = `git show 2c4571f:dqn-marl_amd/evacx/trainer.py`, written before the run)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
