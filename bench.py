@@ -592,6 +592,14 @@ def main():
                                     "flops_basis": "bf16 MFMA products issued by the x3 act (frac) and the reference's "
                                                    "f32 products (frac_f32eq) per row x rows / act_ms (HIP events around "
                                                    "the act launch(es), every 5th step of the instrumented pass)"}
+            if rows == 524288 and tf >= 0.99:  # cfg3's act: the PMC pass on this workload (clock and MFMA-busy)
+                clk = 2.03  # GRBM_GUI_ACTIVE / duration of qact3p_kernel, profiles/r6/counters_r6.md
+                line["roofline_act"].update({
+                    "clock_ghz_pmc": clk, "mfma_busy_pmc": 0.522,
+                    "frac_at_clock": ach / (BF16_PEAK_TFLOPS * clk / 2.4),
+                    "pmc_source": "profiles/r6/counters_r6.md (qact3p_kernel: SQ_VALU_MFMA_BUSY_CYCLES, GRBM clock)",
+                    "clock_note": "the sustained MFMA load holds the act at ~2.03 GHz (2.4 GHz peak): frac_at_clock "
+                                  "prices the same products against the peak at that clock"})
         lm = learn_alone_ms if learn_alone_ms is not None else learn_ms
         if lm is not None and args.qnet == "mlp" and learn_tab is not None:
             fl = learn_flops_executed(args.batch, *learn_tab)
