@@ -19,7 +19,7 @@ ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--table-frac", type=float, default=0.0,
                 help="fraction of rows (the first ones) at the fire's last step, through the act table "
                      "(attach_static over Map.robot_range, as the trainer)")
-ap.add_argument("--order", choices=["env", "centre", "shuffle", "robot"], default="env",
+ap.add_argument("--order", choices=["env", "centre", "shuffle", "robot", "pair"], default="env",
                 help="row order: env (the envs' own), centre (sorted by window centre: rows sharing a table row "
                      "adjacent), shuffle (random), robot (robot-major: every env's robot 0, then robot 1, ...)")
 ap.add_argument("--drop-p", type=float, default=DROPOUT_P, help="dropout p of the act (0: no dropout epilogue)")
@@ -47,6 +47,9 @@ if args.order == "centre":
 elif args.order == "robot":
     assert args.rows % (E * R) == 0
     obs = obs.view(-1, E, R, 8).transpose(1, 2).contiguous().view(-1, 8)
+elif args.order == "pair":
+    assert args.rows % (E * R) == 0
+    obs = obs.view(-1, E, R // 2, 2, 8).transpose(1, 2).contiguous().view(-1, 8)
 elif args.order == "shuffle":
     obs = obs[torch.randperm(obs.shape[0], device="cuda")].contiguous()
 act = torch.empty(args.rows, dtype=torch.int32, device="cuda")
